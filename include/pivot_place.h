@@ -1,0 +1,137 @@
+/*
+ * pivot_place.h — C ABI of the MI355X placement engine for the PIVOT simulator.
+ *
+ * One call, pvt_place(), runs one scheduling round of one policy: every ready task x host
+ * candidate is scored on the GPU and a host is picked per task, with capacity commits applied
+ * in the reference's sequential order. It replaces the body of the reference policies'
+ * schedule() hook:
+ *
+ *   - scheduler/__init__.py:79-80   GlobalSchedulerBase.schedule(self, tasks)   (plugin hook)
+ *   - scheduler/__init__.py:103     the per-round call site in _dispatch
+ *   - scheduler/cost_aware.py:28-43, 60-127   PVT_CA_FF / PVT_CA_BF
+ *   - scheduler/opportunistic.py:11-20        PVT_OPP
+ *   - scheduler/vbp.py:13-29                  PVT_VBP_FF
+ *   - scheduler/vbp.py:39-50                  PVT_VBP_BF
+ *
+ * The reference binds nothing natively (it is pure Python); the binding a maintainer adds is
+ * a ctypes stub, shown in INTEGRATION.md and implemented in pivot_place/_lib.py.
+ *
+ * Conventions
+ *   - Plain C types only. Returns PVT_OK (0) or a negative PVT_E* code; never throws.
+ *   - Array pointers in pvt_round are DEVICE pointers (HBM, e.g. from torch-ROCm tensors),
+ *     except mt_state, which is host memory. The library never frees caller memory; scratch
+ *     lives in the context and grows on demand.
+ *   - Work is ordered on the context's stream; pvt_place() synchronises before it returns.
+ *   - A context is not thread-safe. Use one per thread and per GPU.
+ *   - Arithmetic is IEEE fp64 with no contraction, so results are bit-exact against the
+ *     reference (squared norms are the sequential FMA chain numpy/OpenBLAS ddot performs).
+ */
+#ifndef PIVOT_PLACE_H
+#define PIVOT_PLACE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PVT_ABI_VERSION 1
+
+/* Return codes. */
+#define PVT_OK            0
+#define PVT_EINVAL       -1   /* bad argument (null pointer, size, mode)          */
+#define PVT_ENODEV       -2   /* no usable gfx950 device                          */
+#define PVT_EHIP         -3   /* a HIP runtime call failed (see pvt_last_error)   */
+#define PVT_ENOMEM       -4   /* scratch allocation failed                        */
+#define PVT_EUNSUPPORTED -5   /* configuration the engine does not implement      */
+
+/* Policies (kernel modes). */
+enum pvt_mode {
+  PVT_CA_FF  = 0, /* cost_aware first-fit: strict fit, hosts ordered by frozen per-group key
+                     (sort_hosts) or by index; scheduler/cost_aware.py:99-127              */
+  PVT_CA_BF  = 1, /* cost_aware best-fit: fit >=, min egress-cost x residual / bw;
+                     scheduler/cost_aware.py:63-97                                         */
+  PVT_OPP    = 2, /* opportunistic: fit >=, uniform pick by MT19937 randint;
+                     scheduler/opportunistic.py:11-20                                      */
+  PVT_VBP_FF = 3, /* vbp first-fit: fit >=, lowest index; scheduler/vbp.py:13-29          */
+  PVT_VBP_BF = 4  /* vbp best-fit: strict fit, min residual norm, tie by host-id string;
+                     scheduler/vbp.py:39-50                                                */
+};
+
+/*
+ * One scheduling round. Sizes: H hosts, T ready tasks, Z zones, G groups.
+ *
+ * Host state is SoA: avail[r*H + h] for resource r in {0 cpus, 1 mem, 2 disk, 3 gpus}
+ * (the snapshot of scheduler/__init__.py:82-85, in cluster.hosts order). Task demands are
+ * SoA too: dem[r*T + t], in the order of the `tasks` list passed to schedule().
+ *
+ * Groups (cost_aware only, scheduler/cost_aware.py:45-58): task_group[t] in [0, G) and
+ * group_anchor[g] is the anchor storage zone. Groups run in id order; tasks of a group in
+ * caller order, stably sorted by descending ||d||2 when sort_tasks is set. For the other
+ * policies pass task_group = NULL (one group holding every task).
+ */
+typedef struct pvt_round {
+  int32_t mode;          /* enum pvt_mode                                                 */
+  int32_t n_hosts;       /* H >= 1                                                        */
+  int32_t n_tasks;       /* T >= 0                                                        */
+  int32_t n_zones;       /* Z >= 1 (cost/bw are Z x Z)                                    */
+  int32_t n_groups;      /* G (cost_aware); ignored when task_group is NULL               */
+  int32_t sort_tasks;    /* stable sort by descending ||d||2 within each group            */
+  int32_t sort_hosts;    /* PVT_CA_FF: order hosts by the frozen key (cost_aware.py:118)  */
+  int32_t reserved;      /* must be 0                                                     */
+  double* avail;         /* [4*H] in/out: commits are applied                             */
+  const int32_t* zone;   /* [H] zone index of each host (Host.locality)                   */
+  const uint32_t* tiebreak; /* [H] rank of the host-id string (PVT_VBP_BF), else NULL     */
+  const int32_t* decay;  /* [H] max(len(h.tasks),1) (PVT_CA_FF host_decay), else NULL     */
+  const double* cost;    /* [Z*Z] egress cost, cost[src*Z + dst] (ResourceMetadata.cost)  */
+  const double* bw;      /* [Z*Z] jittered bandwidth, bw[src*Z + dst]                     */
+  const double* dem;     /* [4*T] task demand (cpus, mem, disk, gpus)                     */
+  const int32_t* task_group;   /* [T] or NULL                                             */
+  const int32_t* group_anchor; /* [G] anchor zone per group, or NULL                      */
+  int32_t* order;        /* [T] out: processing order (task indices)                      */
+  int32_t* placement;    /* [T] out: host index, -1 = not placed (task stays waiting)     */
+  uint32_t* mt_state;    /* HOST [625] in/out: MT19937 key[624] then pos (PVT_OPP)        */
+} pvt_round;
+
+typedef struct pvt_ctx pvt_ctx;
+
+/* Per-kernel-class timing gathered while profiling is on (HIP events on the ctx stream). */
+typedef struct pvt_kstats {
+  int64_t launches;      /* kernel launches timed                                         */
+  double  ms;            /* summed device time, milliseconds                              */
+  double  candidates;    /* task x host candidates those launches evaluated               */
+  double  bytes;         /* algorithmic bytes: candidates x bytes/candidate (§8(d))       */
+} pvt_kstats;
+
+/* Kernel classes reported by pvt_get_kstats. */
+enum pvt_kclass {
+  PVT_K_SCORE = 0,   /* fused fit-mask + score + per-task top-K (the hot kernel)          */
+  PVT_K_MERGE = 1,   /* per-task merge of segment top-K lists                              */
+  PVT_K_COMMIT = 2,  /* sequential in-order commit walk                                    */
+  PVT_K_OTHER = 3,   /* keys, norms, sorts, counts                                         */
+  PVT_K_COUNT = 4
+};
+
+int  pvt_abi_version(void);
+int  pvt_ctx_create(int device, pvt_ctx** out);
+int  pvt_ctx_destroy(pvt_ctx* ctx);
+/* Use a caller stream (hipStream_t as void*), e.g. torch.cuda.current_stream().cuda_stream.
+ * NULL restores the context's own stream. */
+int  pvt_ctx_set_stream(pvt_ctx* ctx, void* stream);
+int  pvt_place(pvt_ctx* ctx, const pvt_round* r);
+/* Profiling: record HIP events around every kernel launch (adds a little host overhead). */
+int  pvt_set_profiling(pvt_ctx* ctx, int on);
+int  pvt_reset_kstats(pvt_ctx* ctx);
+int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
+/* Tuning knobs (0 = default): candidate-list window in tasks. */
+int  pvt_set_window(pvt_ctx* ctx, int tasks);
+/* Counters of the last pvt_place call: windows run and refills forced by exhausted lists. */
+int  pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills);
+/* Human-readable text of the last error on this context (static storage of the ctx). */
+const char* pvt_last_error(pvt_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PIVOT_PLACE_H */

@@ -1,0 +1,68 @@
+"""ctypes wrapper of the CPU restatement (oracle/pivot_oracle.c). TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+It checks the product; the product (pivot_place) never imports it.
+
+Parity is pinned: tests/test_oracle_golden.py runs it against the golden fixtures generated
+from the reference itself (tests/golden/make_golden.py).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libpivot_oracle.so")
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.oracle_place.restype = ctypes.c_int
+        _lib.oracle_place.argtypes = [ctypes.c_void_p]
+        _lib.oracle_norm4.restype = ctypes.c_double
+        _lib.oracle_norm4.argtypes = [ctypes.POINTER(ctypes.c_double)]
+        _lib.oracle_randint.restype = ctypes.c_uint32
+        _lib.oracle_randint.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def place(r):
+    """Run one round on the CPU restatement. ``r``: pivot_place._abi.RoundArrays."""
+    from pivot_place._abi import RoundResult, check_rc, fill_struct
+    avail = r.avail.copy()
+    T = r.n_tasks
+    placement = np.full(T, -1, dtype=np.int32)
+    order = np.zeros(T, dtype=np.int32)
+    mt = None if r.mt_state is None else r.mt_state.copy()
+    s = fill_struct(r)
+    s.avail, s.zone, s.tiebreak, s.decay = _ptr(avail), _ptr(r.zone), _ptr(r.tiebreak), _ptr(r.decay)
+    s.cost, s.bw, s.dem = _ptr(r.cost), _ptr(r.bw), _ptr(r.dem)
+    s.task_group, s.group_anchor = _ptr(r.task_group), _ptr(r.group_anchor)
+    s.order, s.placement, s.mt_state = _ptr(order), _ptr(placement), _ptr(mt)
+    check_rc(lib().oracle_place(ctypes.addressof(s)))
+    return RoundResult(placement=placement, order=order, avail=avail, mt_state=mt)
+
+
+def norm4(x):
+    a = (ctypes.c_double * 4)(*[float(v) for v in x])
+    return lib().oracle_norm4(a)
+
+
+def randint(state, n):
+    """numpy RandomState.randint(0, n) on a (625,) uint32 MT state, updated in place."""
+    assert state.dtype == np.uint32 and state.flags["C_CONTIGUOUS"]
+    return int(lib().oracle_randint(state.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n))

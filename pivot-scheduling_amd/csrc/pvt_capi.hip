@@ -1,0 +1,463 @@
+// pvt_capi.hip — the C ABI (include/pivot_place.h): context, scratch and the per-round driver.
+//
+// pvt_place() replaces the body of a reference policy's schedule() (scheduler/__init__.py:79-80,
+// called at :103). A round runs as:
+//   1. a2 order: tasks grouped (cost_aware groups, cost_aware.py:37) and stably sorted by
+//      descending ||d||2 (cost_aware.py:60-61, vbp.py:17,41) with two stable radix sorts.
+//   2. windows of up to W tasks: candidate lists for the window on the current state (score +
+//      merge kernels, or the ordered scan for index-order first-fit), then the commit walk. A
+//      walk that meets an exhausted list stops early; the next window starts at that task.
+//   3. cost_aware first-fit with sort_hosts recomputes the frozen host key at every group start
+//      (cost_aware.py:118-119), so its windows never cross a group boundary.
+// Opportunistic (PVT_OPP) runs its own count/select kernels (pvt_opp.hip).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pivot_place.h"
+#include "pvt_kernels.h"
+#include "pvt_opp.h"
+
+using namespace pvt;
+
+struct Buf {
+  void* p = nullptr;
+  size_t n = 0;
+};
+
+struct TimedLaunch {
+  int kclass;
+  double candidates, bytes;
+  hipEvent_t a, b;
+};
+
+struct pvt_ctx {
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  std::string err;
+  int window = MAX_WINDOW;
+  int64_t windows = 0, refills = 0;
+  bool profiling = false;
+  pvt_kstats ks[PVT_K_COUNT];
+  std::vector<hipEvent_t> evpool;
+  std::vector<TimedLaunch> pending;
+  // scratch
+  Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
+      seg, seg_feas, l_s, l_tb, l_id, l_zone, l_a, l_cnt, l_comp, next, opp;
+  int32_t* next_host = nullptr;   // pinned
+};
+
+static int fail(pvt_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return fail(ctx, PVT_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_));         \
+  } while (0)
+
+static int ensure(pvt_ctx* ctx, Buf& b, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (b.n >= bytes) return PVT_OK;
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.n = 0;
+  size_t want = std::max(bytes, b.n * 3 / 2);
+  if (hipMalloc(&b.p, want) != hipSuccess) {
+    b.p = nullptr;
+    return fail(ctx, PVT_ENOMEM, "hipMalloc(%zu) failed", want);
+  }
+  b.n = want;
+  return PVT_OK;
+}
+#define ENSURE(b, bytes)                              \
+  do {                                                \
+    int rc_ = ensure(ctx, (b), (bytes));              \
+    if (rc_) return rc_;                              \
+  } while (0)
+
+template <class T>
+static T* P(Buf& b) { return reinterpret_cast<T*>(b.p); }
+
+// ---------------------------------------------------------------- profiling
+static hipEvent_t take_event(pvt_ctx* ctx) {
+  if (!ctx->evpool.empty()) {
+    hipEvent_t e = ctx->evpool.back();
+    ctx->evpool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+struct Scope {
+  pvt_ctx* ctx;
+  TimedLaunch t;
+  Scope(pvt_ctx* c, int kclass, double cand, double bytes) : ctx(c) {
+    t.kclass = kclass; t.candidates = cand; t.bytes = bytes; t.a = t.b = nullptr;
+    if (ctx->profiling) { t.a = take_event(ctx); (void)hipEventRecord(t.a, ctx->stream); }
+  }
+  ~Scope() {
+    if (ctx->profiling) {
+      t.b = take_event(ctx);
+      (void)hipEventRecord(t.b, ctx->stream);
+      ctx->pending.push_back(t);
+    }
+  }
+};
+static void harvest(pvt_ctx* ctx) {
+  for (auto& t : ctx->pending) {
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, t.a, t.b);
+    pvt_kstats& k = ctx->ks[t.kclass];
+    k.launches += 1; k.ms += ms; k.candidates += t.candidates; k.bytes += t.bytes;
+    ctx->evpool.push_back(t.a);
+    ctx->evpool.push_back(t.b);
+  }
+  ctx->pending.clear();
+}
+
+// ---------------------------------------------------------------- ABI
+extern "C" int pvt_abi_version(void) { return PVT_ABI_VERSION; }
+
+extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
+  if (!out) return PVT_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return PVT_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return PVT_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return PVT_ENODEV;
+  pvt_ctx* ctx = new pvt_ctx();
+  ctx->device = device;
+  std::memset(ctx->ks, 0, sizeof(ctx->ks));
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
+      init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
+      hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess) {
+    delete ctx;
+    return PVT_EHIP;
+  }
+  ctx->stream = ctx->own;
+  *out = ctx;
+  return PVT_OK;
+}
+
+extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
+  if (!ctx) return PVT_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  harvest(ctx);
+  Buf* bufs[] = {&ctx->ord, &ctx->ord2, &ctx->keys64a, &ctx->keys64b, &ctx->keys32a, &ctx->keys32b,
+                 &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
+                 &ctx->seg, &ctx->seg_feas, &ctx->l_s, &ctx->l_tb, &ctx->l_id, &ctx->l_zone,
+                 &ctx->l_a, &ctx->l_cnt, &ctx->l_comp, &ctx->next, &ctx->opp};
+  for (Buf* b : bufs)
+    if (b->p) (void)hipFree(b->p);
+  for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
+  if (ctx->next_host) (void)hipHostFree(ctx->next_host);
+  if (ctx->own) (void)hipStreamDestroy(ctx->own);
+  delete ctx;
+  return PVT_OK;
+}
+
+extern "C" int pvt_ctx_set_stream(pvt_ctx* ctx, void* stream) {
+  if (!ctx) return PVT_EINVAL;
+  ctx->stream = stream ? (hipStream_t)stream : ctx->own;
+  return PVT_OK;
+}
+
+extern "C" int pvt_set_profiling(pvt_ctx* ctx, int on) {
+  if (!ctx) return PVT_EINVAL;
+  ctx->profiling = on != 0;
+  return PVT_OK;
+}
+extern "C" int pvt_reset_kstats(pvt_ctx* ctx) {
+  if (!ctx) return PVT_EINVAL;
+  (void)hipStreamSynchronize(ctx->stream);
+  harvest(ctx);
+  std::memset(ctx->ks, 0, sizeof(ctx->ks));
+  return PVT_OK;
+}
+extern "C" int pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out) {
+  if (!ctx || !out || kclass < 0 || kclass >= PVT_K_COUNT) return PVT_EINVAL;
+  (void)hipStreamSynchronize(ctx->stream);
+  harvest(ctx);
+  *out = ctx->ks[kclass];
+  return PVT_OK;
+}
+extern "C" int pvt_set_window(pvt_ctx* ctx, int tasks) {
+  if (!ctx || tasks < 0) return PVT_EINVAL;
+  ctx->window = tasks == 0 ? MAX_WINDOW : std::min(tasks, MAX_WINDOW);
+  return PVT_OK;
+}
+extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) {
+  if (!ctx) return PVT_EINVAL;
+  if (windows) *windows = ctx->windows;
+  if (refills) *refills = ctx->refills;
+  return PVT_OK;
+}
+extern "C" const char* pvt_last_error(pvt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+// ---------------------------------------------------------------- round driver
+static double bytes_per_candidate(int mode) {
+  // cost_aware 36 B (4 x fp64 avail + int32 zone); vbp best-fit 36 B
+  // (+ host-id rank); opportunistic / vbp first-fit 32 B.
+  return (mode == PVT_CA_FF || mode == PVT_CA_BF || mode == PVT_VBP_BF) ? 36.0 : 32.0;
+}
+
+// a2: processing order. Group-major (stable by group id), within a group caller order or, with
+// sort_tasks, stable descending ||d||2. Two LSD passes of a stable radix sort.
+static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
+  const int T = r->n_tasks;
+  hipStream_t st = ctx->stream;
+  ENSURE(ctx->ord, sizeof(int32_t) * T);
+  ENSURE(ctx->ord2, sizeof(int32_t) * T);
+  int32_t* cur = P<int32_t>(ctx->ord);
+  int32_t* alt = P<int32_t>(ctx->ord2);
+  launch_iota(cur, T, st);
+  const bool grouped = r->task_group != nullptr && r->n_groups > 1;
+  if (r->sort_tasks) {
+    ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
+    ENSURE(ctx->keys64b, sizeof(uint64_t) * T);
+    launch_norm_keys(r->dem, T, nullptr, P<uint64_t>(ctx->keys64a), st);
+    size_t tmp = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<uint64_t>(ctx->keys64a),
+                                              P<uint64_t>(ctx->keys64b), cur, alt, T, 0, 64, st));
+    ENSURE(ctx->sorttmp, tmp);
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->sorttmp.p, tmp, P<uint64_t>(ctx->keys64a),
+                                              P<uint64_t>(ctx->keys64b), cur, alt, T, 0, 64, st));
+    std::swap(cur, alt);
+  }
+  if (grouped) {
+    ENSURE(ctx->keys32a, sizeof(uint32_t) * T);
+    ENSURE(ctx->keys32b, sizeof(uint32_t) * T);
+    launch_group_keys(r->task_group, cur, T, P<uint32_t>(ctx->keys32a), st);
+    int bits = 1;
+    while ((1 << bits) < r->n_groups && bits < 31) bits++;
+    size_t tmp = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<uint32_t>(ctx->keys32a),
+                                              P<uint32_t>(ctx->keys32b), cur, alt, T, 0, bits, st));
+    ENSURE(ctx->sorttmp, tmp);
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->sorttmp.p, tmp, P<uint32_t>(ctx->keys32a),
+                                              P<uint32_t>(ctx->keys32b), cur, alt, T, 0, bits, st));
+    std::swap(cur, alt);
+  }
+  *ord_out = cur;
+  return PVT_OK;
+}
+
+static int check_round(pvt_ctx* ctx, const pvt_round* r) {
+  if (!r) return fail(ctx, PVT_EINVAL, "null round");
+  if (r->reserved != 0) return fail(ctx, PVT_EINVAL, "reserved must be 0");
+  if (r->n_hosts < 1 || r->n_tasks < 0 || r->n_zones < 1 || r->n_zones > ZMAX)
+    return fail(ctx, PVT_EINVAL, "bad sizes H=%d T=%d Z=%d", r->n_hosts, r->n_tasks, r->n_zones);
+  if (r->mode < PVT_CA_FF || r->mode > PVT_VBP_BF) return fail(ctx, PVT_EINVAL, "bad mode %d", r->mode);
+  if (!r->avail || !r->zone || !r->dem || !r->order || !r->placement)
+    return fail(ctx, PVT_EINVAL, "null array");
+  if ((r->mode == PVT_CA_FF || r->mode == PVT_CA_BF) && (!r->cost || !r->bw))
+    return fail(ctx, PVT_EINVAL, "cost_aware needs cost and bw");
+  if (r->task_group && (r->n_groups < 1 || !r->group_anchor))
+    return fail(ctx, PVT_EINVAL, "task_group needs n_groups >= 1 and group_anchor");
+  if (r->mode == PVT_VBP_BF && !r->tiebreak) return fail(ctx, PVT_EINVAL, "vbp best-fit needs tiebreak");
+  if (r->mode == PVT_OPP && !r->mt_state) return fail(ctx, PVT_EINVAL, "opportunistic needs mt_state");
+  if (r->mode == PVT_CA_BF && r->decay)
+    return fail(ctx, PVT_EUNSUPPORTED, "cost_aware best-fit with host_decay (reference crashes, cost_aware.py:26,81)");
+  return PVT_OK;
+}
+
+static void lists_from(pvt_ctx* ctx, Lists& L) {
+  L.s = P<double>(ctx->l_s); L.tb = P<uint32_t>(ctx->l_tb); L.id = P<int32_t>(ctx->l_id);
+  L.zone = P<int32_t>(ctx->l_zone); L.a = P<double>(ctx->l_a);
+  L.cnt = P<int32_t>(ctx->l_cnt); L.complete = P<int32_t>(ctx->l_comp);
+}
+
+// Opportunistic: windows of OPP_MAXW tasks in caller order; count pass then commit walk. The
+// MT19937 state travels host -> device -> host around the round.
+static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
+  const int T = r->n_tasks, H = r->n_hosts;
+  hipStream_t st = ctx->stream;
+  const int W = std::max(1, std::min(ctx->window, OPP_MAXW));
+  const int nq = (H + OPP_CH - 1) / OPP_CH, nsq = (nq + OPP_SUP - 1) / OPP_SUP;
+  int S = std::min(MAX_SEG, nsq);
+  const int seg_sup = (nsq + S - 1) / S;
+  S = (nsq + seg_sup - 1) / seg_sup;
+  ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
+  ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
+  launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord),
+                      P<int32_t>(ctx->anc_ord), st);
+  const size_t cc_bytes = ((sizeof(uint16_t) * (size_t)nq * W + 255) / 256) * 256;
+  ENSURE(ctx->opp, cc_bytes + sizeof(int32_t) * (size_t)nsq * W + sizeof(uint32_t) * 640);
+  uint16_t* cc = reinterpret_cast<uint16_t*>(ctx->opp.p);
+  int32_t* sc = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ctx->opp.p) + cc_bytes);
+  uint32_t* mt = reinterpret_cast<uint32_t*>(sc + (size_t)nsq * W);
+  HIPCHK(hipMemcpyAsync(mt, r->mt_state, sizeof(uint32_t) * 625, hipMemcpyHostToDevice, st));
+  const double bpc = bytes_per_candidate(r->mode);
+  for (int t0 = 0; t0 < T; t0 += W) {
+    const int nt = std::min(W, T - t0);
+    ctx->windows++;
+    OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, S, seg_sup, nq, nsq, W,
+                    cc, sc};
+    {
+      Scope s(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
+      launch_opp_count(ca, st);
+    }
+    OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, cc, sc, H, nt, nq, nsq, W,
+                     r->placement + t0, mt};
+    Scope s(ctx, PVT_K_COMMIT, 0, 0);
+    launch_opp_commit(oa, st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(r->mt_state, mt, sizeof(uint32_t) * 625, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  return PVT_OK;
+}
+
+extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
+  if (!ctx) return PVT_EINVAL;
+  int rc = check_round(ctx, r);
+  if (rc) return rc;
+  ctx->windows = ctx->refills = 0;
+  HIPCHK(hipSetDevice(ctx->device));
+  const int T = r->n_tasks, H = r->n_hosts, Z = r->n_zones;
+  if (T == 0) return PVT_OK;
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
+
+  if (r->mode == PVT_OPP) {
+    launch_iota(r->order, T, st);
+    return opp_round(ctx, r);
+  }
+
+  int32_t* ord = nullptr;
+  if ((rc = build_order(ctx, r, &ord))) return rc;
+  HIPCHK(hipMemcpyAsync(r->order, ord, sizeof(int32_t) * T, hipMemcpyDeviceToDevice, st));
+
+  ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
+  ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
+  launch_gather_tasks(r->dem, ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
+                      P<int32_t>(ctx->anc_ord), st);
+  const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
+  if (ca) {
+    ENSURE(ctx->csum, sizeof(double) * Z * Z);
+    ENSURE(ctx->bsum, sizeof(double) * Z * Z);
+    launch_zone_tables(r->cost, r->bw, Z, P<double>(ctx->csum), P<double>(ctx->bsum), st);
+  }
+
+  // group boundaries in processing order (only cost_aware first-fit with sort_hosts needs them)
+  const bool keyed = r->mode == PVT_CA_FF && r->sort_hosts;
+  const bool ordered = (r->mode == PVT_VBP_FF) || (r->mode == PVT_CA_FF && !r->sort_hosts);
+  std::vector<int> gstart{0}, ganchor;
+  if (keyed) {
+    std::vector<int32_t> tg(T), ga;
+    if (r->task_group) {
+      HIPCHK(hipMemcpyAsync(tg.data(), r->task_group, sizeof(int32_t) * T, hipMemcpyDeviceToHost, st));
+      ga.resize(r->n_groups);
+      HIPCHK(hipMemcpyAsync(ga.data(), r->group_anchor, sizeof(int32_t) * r->n_groups,
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      std::vector<int> cnt(r->n_groups, 0);
+      for (int t = 0; t < T; t++) {
+        if (tg[t] < 0 || tg[t] >= r->n_groups) return fail(ctx, PVT_EINVAL, "task_group out of range");
+        cnt[tg[t]]++;
+      }
+      int off = 0;
+      gstart.clear();
+      for (int g = 0; g < r->n_groups; g++) {
+        if (cnt[g] == 0) continue;
+        gstart.push_back(off);
+        ganchor.push_back(ga[g]);
+        off += cnt[g];
+      }
+    } else {
+      ganchor.push_back(0);
+    }
+  }
+  gstart.push_back(T);
+  if (keyed) ENSURE(ctx->key, sizeof(double) * H);
+
+  const int W = std::max(1, std::min(ctx->window, MAX_WINDOW));
+  int S = 1;
+  while (S < MAX_SEG && (int64_t)H >= (int64_t)S * 2 * 4096) S *= 2;
+  const int seg_len = ((H + S - 1) / S + WAVE - 1) / WAVE * WAVE;
+  ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)W * S * KL);
+  ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)W * S);
+  ENSURE(ctx->l_s, sizeof(double) * (size_t)W * KL);
+  ENSURE(ctx->l_tb, sizeof(uint32_t) * (size_t)W * KL);
+  ENSURE(ctx->l_id, sizeof(int32_t) * (size_t)W * KL);
+  ENSURE(ctx->l_zone, sizeof(int32_t) * (size_t)W * KL);
+  ENSURE(ctx->l_a, sizeof(double) * 4 * (size_t)W * KL);
+  ENSURE(ctx->l_cnt, sizeof(int32_t) * W);
+  ENSURE(ctx->l_comp, sizeof(int32_t) * W);
+  ENSURE(ctx->next, sizeof(int32_t) * 4);
+  Lists L;
+  lists_from(ctx, L);
+  const double bpc = bytes_per_candidate(r->mode);
+  const double* dem_ord = P<double>(ctx->dem_ord);
+  const int32_t* anc_ord = P<int32_t>(ctx->anc_ord);
+
+  const size_t ngroups = keyed ? ganchor.size() : 1;
+  for (size_t g = 0; g < ngroups; g++) {
+    const int gb = keyed ? gstart[g] : 0, ge = keyed ? gstart[g + 1] : T;
+    if (keyed) {
+      KeyArgs ka{r->avail, r->zone, r->decay, P<double>(ctx->csum), P<double>(ctx->bsum), H, Z,
+                 ganchor[g], P<double>(ctx->key)};
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_key(ka, st);
+    }
+    int t0 = gb;
+    while (t0 < ge) {
+      const int nt = std::min(W, ge - t0);
+      ctx->windows++;
+      if (ordered) {
+        OrderedArgs oa{r->avail, r->zone, dem_ord + (size_t)t0 * 4, H, nt,
+                       r->mode == PVT_CA_FF ? 1 : 0, L};
+        Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
+        launch_ordered(oa, st);
+      } else {
+        ScoreArgs sa{r->avail, r->zone, r->tiebreak, keyed ? P<double>(ctx->key) : nullptr,
+                     dem_ord + (size_t)t0 * 4, anc_ord + t0, P<double>(ctx->csum),
+                     P<double>(ctx->bsum), H, Z, nt, S, seg_len, P<SegEntry>(ctx->seg),
+                     P<int32_t>(ctx->seg_feas)};
+        {
+          Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
+          launch_score(r->mode, sa, st);
+        }
+        MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, H, nt, S, L};
+        Scope sc(ctx, PVT_K_MERGE, 0, 0);
+        launch_merge(ma, st);
+      }
+      CommitArgs ca_{r->avail, dem_ord + (size_t)t0 * 4, anc_ord + t0, ord + t0, P<double>(ctx->csum),
+                     P<double>(ctx->bsum), L, H, Z, nt, r->mode, r->placement, P<int32_t>(ctx->next)};
+      {
+        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+        launch_commit(ca_, st);
+      }
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t),
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const int adv = *ctx->next_host;
+      if (adv < 0 || adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", adv, nt);
+      if (adv == 0) return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
+      if (adv < nt) ctx->refills++;
+      t0 += adv;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return PVT_OK;
+}

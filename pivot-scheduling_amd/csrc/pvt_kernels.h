@@ -1,0 +1,117 @@
+// pvt_kernels.h — device data layout and kernel launch interface of the placement engine.
+//
+// Layout in HBM (all fp64 math is IEEE, no contraction):
+//   hosts   avail[4][H] SoA fp64 (cpus, mem, disk, gpus), zone[H] i32, tiebreak[H] u32
+//   tasks   processing order ord[T] i32; dem_ord[T][4] fp64 task-major (one 32-B row per
+//           task, so a wave reads a task's demand with one scalar load); anc_ord[T] i32
+//   zones   csum[Z][Z] = cost[a][z] + cost[z][a], bsum[Z][Z] = bw[a][z] + bw[z][a]
+//   lists   per window task: KL candidates, sorted by (score, tiebreak, host) ascending
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pvt {
+
+constexpr int WAVE = 64;
+constexpr int KL = 64;           // candidate list length per task (one entry per lane)
+constexpr int ZMAX = 64;         // zones supported (locality.yml has 31)
+constexpr int TW = 8;            // tasks per wave in the score kernel
+constexpr int WPB = 4;           // waves per score-kernel block
+constexpr int MAX_WINDOW = 2048; // tasks per window (bounded by the commit kernel's LDS)
+constexpr int HASH_BITS = 12;    // commit kernel touched-host hash: 4096 slots
+constexpr int MAX_SEG = 8;       // host segments per task (one per XCD)
+
+enum Mode { CA_FF = 0, CA_BF = 1, OPP = 2, VBP_FF = 3, VBP_BF = 4 };
+
+struct SegEntry {    // 16 B: one candidate in a per-segment list
+  double s;
+  uint32_t tb;
+  int32_t id;
+};
+
+// Merged (final) candidate lists of one window, SoA over [W][KL].
+struct Lists {
+  double* s;
+  uint32_t* tb;
+  int32_t* id;
+  int32_t* zone;
+  double* a;          // [4][W*KL] snapshot availability of the candidate host
+  int32_t* cnt;       // [W] valid entries
+  int32_t* complete;  // [W] 1 if every snapshot-feasible host is in the list
+};
+
+struct ScoreArgs {
+  const double* avail;
+  const int32_t* zone;
+  const uint32_t* tb;
+  const double* key;      // CA_FF: frozen per-group host key
+  const double* dem;      // window tasks [nt][4]
+  const int32_t* anc;     // window tasks [nt]
+  const double* csum;
+  const double* bsum;
+  int H, Z, nt, S, seg_len;
+  SegEntry* seg;          // [nt][S][KL]
+  int32_t* seg_feas;      // [nt][S]
+};
+
+struct MergeArgs {
+  const SegEntry* seg;
+  const int32_t* seg_feas;
+  const double* avail;
+  const int32_t* zone;
+  int H, nt, S;
+  Lists L;
+};
+
+struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible hosts
+  const double* avail;
+  const int32_t* zone;
+  const double* dem;
+  int H, nt, strict;
+  Lists L;
+};
+
+struct CommitArgs {
+  double* avail;          // global state, updated in place
+  const double* dem;      // window tasks [nt][4]
+  const int32_t* anc;
+  const int32_t* ord;     // window tasks' caller indices
+  const double* csum;
+  const double* bsum;
+  Lists L;
+  int H, Z, nt, mode;
+  int32_t* placement;     // [T] in caller order
+  int32_t* next;          // out: window-local index where the walk stopped (nt = done)
+};
+
+struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw)
+  const double* avail;
+  const int32_t* zone;
+  const int32_t* decay;
+  const double* csum;
+  const double* bsum;
+  int H, Z, anchor;
+  double* key;
+};
+
+void launch_score(int mode, const ScoreArgs& a, hipStream_t st);
+void launch_merge(const MergeArgs& a, hipStream_t st);
+void launch_ordered(const OrderedArgs& a, hipStream_t st);
+void launch_commit(const CommitArgs& a, hipStream_t st);
+void launch_key(const KeyArgs& a, hipStream_t st);
+void launch_zone_tables(const double* cost, const double* bw, int Z, double* csum, double* bsum,
+                        hipStream_t st);
+// a2: u64 sort key ~bits(||d||2) per task (descending norm == ascending key)
+void launch_norm_keys(const double* dem, int T, const int32_t* idx, uint64_t* keys,
+                      hipStream_t st);
+void launch_group_keys(const int32_t* task_group, const int32_t* idx, int T, uint32_t* keys,
+                       hipStream_t st);
+size_t commit_lds_bytes();
+hipError_t init_kernel_attrs();
+void launch_iota(int32_t* out, int n, hipStream_t st);
+// gather tasks into processing order: dem_ord[p][r] = dem[r*T + ord[p]], anc_ord[p]
+void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
+                         const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
+                         hipStream_t st);
+
+}  // namespace pvt

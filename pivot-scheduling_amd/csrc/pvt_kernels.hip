@@ -1,0 +1,564 @@
+// pvt_kernels.hip — gfx950 kernels of the placement engine.
+//
+// The hot path of every policy is one fused pass over the round's task x host candidates
+// (reference scheduler/cost_aware.py:63-127, scheduler/vbp.py:13-50): fit-mask, score, and a
+// per-task top-KL selection ordered by (score, tiebreak, host index). A single-wave kernel
+// then walks the tasks in the reference's order and commits capacity exactly as the
+// reference's sequential loops do (DESIGN.md §2 explains why the lists make this exact).
+//
+// Numerics: build with -ffp-contract=off. Squared norms are the explicit FMA chain that
+// numpy's la.norm -> OpenBLAS ddot computes for n = 4; sqrt and division are IEEE
+// correctly rounded (llvm.sqrt.f64 / fdiv lowering without afn/arcp).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pvt_device.h"
+#include "pvt_kernels.h"
+
+namespace pvt {
+
+// Conservative bound on the squared residual norm of a cost_aware best-fit candidate:
+// if fl(fl(c*sqrt(s2))/b) <= thr then s2 <= lim (rounding slack 2^-40 >> 2^-53).
+__device__ __forceinline__ double ca_lim(double thr, double c, double b) {
+  if (!(thr < DINF)) return DINF;
+  if (c == 0.0) return thr > 0.0 ? DINF : -1.0;   // score is exactly 0 in zero-cost zones
+  double r = thr * b / c;
+  r = r * (1.0 + 0x1p-40);
+  return r * r * (1.0 + 0x1p-40);
+}
+__device__ __forceinline__ double vbp_lim(double thr) {
+  if (!(thr < DINF)) return DINF;
+  double r = thr * (1.0 + 0x1p-40);
+  return r * r * (1.0 + 0x1p-40);
+}
+
+// Insert (cs, ct, ci) into the wave-held sorted list (lane j holds entry j). The caller has
+// checked it beats entry KL-1, which falls off.
+__device__ __forceinline__ void list_insert(double& s, uint32_t& t, int32_t& i, double cs,
+                                            uint32_t ct, int32_t ci) {
+  const int lane = lane_id();
+  const bool keep = lexless(s, t, i, cs, ct, ci);
+  const int pos = __popcll(__ballot(keep));
+  const double us = __shfl_up(s, 1);
+  const uint32_t ut = (uint32_t)__shfl_up((int)t, 1);
+  const int32_t ui = __shfl_up(i, 1);
+  if (lane == pos) {
+    s = cs; t = ct; i = ci;
+  } else if (lane > pos) {
+    s = us; t = ut; i = ui;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Score kernel: candidates (window tasks) x (one host segment). Block = 4 waves; each wave owns
+// TW tasks and streams the segment's hosts 64 at a time (lane = host), keeping a sorted top-KL
+// list per task in registers. blockIdx % S picks the segment, so with S = 8 the blocks of one
+// segment share an XCD (round-robin dispatch) and its L2 holds that slice of the host table.
+// ------------------------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
+  constexpr bool STRICT = (MODE != CA_BF);
+  constexpr int ZL = (MODE == CA_BF) ? ZMAX : 1;
+  __shared__ double s_lim[WPB][TW][ZL];
+  __shared__ double s_c[WPB][TW][ZL];
+  __shared__ double s_b[WPB][TW][ZL];
+
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int seg = blockIdx.x % A.S, tile = blockIdx.x / A.S;
+  const int t0 = (tile * WPB + wave) * TW;
+  if (t0 >= A.nt) return;
+  const int nt = min(TW, A.nt - t0);
+  const int hb0 = seg * A.seg_len, hb1 = min(A.H, hb0 + A.seg_len);
+
+  double d0[TW], d1[TW], d2[TW], d3[TW];
+  double ls[TW], ts[TW], lim[TW];
+  uint32_t lt[TW], tt[TW];
+  int32_t li[TW], ti[TW], feas[TW];
+#pragma unroll
+  for (int k = 0; k < TW; k++) {
+    if (k < nt) {
+      const double* dp = A.dem + (size_t)(t0 + k) * 4;
+      d0[k] = dp[0]; d1[k] = dp[1]; d2[k] = dp[2]; d3[k] = dp[3];
+    } else {
+      d0[k] = d1[k] = d2[k] = d3[k] = DINF;
+    }
+    ls[k] = DINF; lt[k] = 0xffffffffu; li[k] = 0x7fffffff;
+    ts[k] = DINF; tt[k] = 0xffffffffu; ti[k] = 0x7fffffff;
+    lim[k] = DINF;
+    feas[k] = 0;
+    if (MODE == CA_BF) {
+      const int a = (k < nt) ? A.anc[t0 + k] : 0;
+      if (lane < A.Z) {
+        s_c[wave][k][lane] = A.csum[a * A.Z + lane];
+        s_b[wave][k][lane] = A.bsum[a * A.Z + lane];
+        s_lim[wave][k][lane] = DINF;
+      }
+    }
+  }
+
+  for (int hb = hb0; hb < hb1; hb += WAVE) {
+    const int h = hb + lane;
+    const bool ok = h < hb1;
+    const double a0 = ok ? A.avail[h] : -DINF;
+    const double a1 = ok ? A.avail[(size_t)A.H + h] : -DINF;
+    const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : -DINF;
+    const double a3 = ok ? A.avail[3 * (size_t)A.H + h] : -DINF;
+    int z = 0;
+    if (MODE == CA_BF) z = ok ? A.zone[h] : 0;
+    double key = DINF;
+    if (MODE == CA_FF) key = ok ? A.key[h] : DINF;
+#pragma unroll
+    for (int k = 0; k < TW; k++) {
+      const bool fit = fits<STRICT>(a0, a1, a2, a3, d0[k], d1[k], d2[k], d3[k]);
+      feas[k] += __popcll(__ballot(fit));
+      double s2 = 0.0;
+      bool pass;
+      if (MODE == CA_FF) {
+        pass = fit && lexless(key, 0u, h, ts[k], tt[k], ti[k]);
+      } else {
+        s2 = norm2_seq(a0 - d0[k], a1 - d1[k], a2 - d2[k], a3 - d3[k]);
+        const double lm = (MODE == CA_BF) ? s_lim[wave][k][z] : lim[k];
+        pass = fit && (s2 <= lm);
+      }
+      uint64_t pm = __ballot(pass);
+      if (pm) {
+        double sc = DINF;
+        uint32_t tbv = 0;
+        if (pass) {
+          if (MODE == CA_FF) {
+            sc = key;
+          } else if (MODE == CA_BF) {
+            const double r = __builtin_sqrt(s2);
+            sc = (s_c[wave][k][z] * r) / s_b[wave][k][z];
+          } else {
+            sc = __builtin_sqrt(s2);
+            tbv = A.tb[h];
+          }
+        }
+        bool changed = false;
+        while (pm) {
+          const int L = __builtin_ctzll(pm);
+          pm &= pm - 1;
+          const double cs = readlane_d(sc, L);
+          const uint32_t ct = readlane_u(tbv, L);
+          const int32_t ci = hb + L;
+          if (lexless(cs, ct, ci, ts[k], tt[k], ti[k])) {
+            list_insert(ls[k], lt[k], li[k], cs, ct, ci);
+            ts[k] = readlane_d(ls[k], KL - 1);
+            tt[k] = readlane_u(lt[k], KL - 1);
+            ti[k] = readlane_i(li[k], KL - 1);
+            changed = true;
+          }
+        }
+        if (changed) {
+          if (MODE == CA_BF) {
+            if (lane < A.Z) s_lim[wave][k][lane] = ca_lim(ts[k], s_c[wave][k][lane], s_b[wave][k][lane]);
+          } else if (MODE == VBP_BF) {
+            lim[k] = vbp_lim(ts[k]);
+          }
+        }
+      }
+    }
+  }
+
+#pragma unroll
+  for (int k = 0; k < TW; k++) {
+    if (k < nt) {
+      const size_t row = (size_t)(t0 + k) * A.S + seg;
+      SegEntry e;
+      e.s = ls[k]; e.tb = lt[k]; e.id = li[k];
+      A.seg[row * KL + lane] = e;
+      if (lane == 0) A.seg_feas[row] = feas[k];
+    }
+  }
+}
+
+void launch_score(int mode, const ScoreArgs& a, hipStream_t st) {
+  const int tiles = (a.nt + WPB * TW - 1) / (WPB * TW);
+  dim3 grid(tiles * a.S), block(WPB * WAVE);
+  switch (mode) {
+    case CA_FF: hipLaunchKernelGGL(score_kernel<CA_FF>, grid, block, 0, st, a); break;
+    case CA_BF: hipLaunchKernelGGL(score_kernel<CA_BF>, grid, block, 0, st, a); break;
+    case VBP_BF: hipLaunchKernelGGL(score_kernel<VBP_BF>, grid, block, 0, st, a); break;
+    default: break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Merge: one wave per task folds the S segment lists into one sorted top-KL list (bitonic
+// merge of two sorted 64-lists), then gathers each candidate's zone and snapshot availability.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void cswap_lane(double& s, uint32_t& t, int32_t& i, int stride,
+                                           bool keep_min) {
+  const double os = __shfl_xor(s, stride);
+  const uint32_t ot = (uint32_t)__shfl_xor((int)t, stride);
+  const int32_t oi = __shfl_xor(i, stride);
+  const bool other_less = lexless(os, ot, oi, s, t, i);
+  if (other_less == keep_min) { s = os; t = ot; i = oi; }
+}
+
+__global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int task = blockIdx.x * 4 + wave;
+  if (task >= A.nt) return;
+  double s = DINF;
+  uint32_t t = 0xffffffffu;
+  int32_t id = 0x7fffffff;
+  int64_t tot = 0;
+  for (int g = 0; g < A.S; g++) {
+    const size_t row = (size_t)task * A.S + g;
+    const SegEntry e = A.seg[row * KL + lane];
+    tot += A.seg_feas[row];
+    if (g == 0) { s = e.s; t = e.tb; id = e.id; continue; }
+    // reversed second list, elementwise min -> bitonic sequence of the KL smallest
+    const double rs = __shfl(e.s, KL - 1 - lane);
+    const uint32_t rt = (uint32_t)__shfl((int)e.tb, KL - 1 - lane);
+    const int32_t ri = __shfl(e.id, KL - 1 - lane);
+    if (lexless(rs, rt, ri, s, t, id)) { s = rs; t = rt; id = ri; }
+#pragma unroll
+    for (int stride = KL / 2; stride > 0; stride >>= 1) cswap_lane(s, t, id, stride, !(lane & stride));
+  }
+  const int cnt = (int)(tot < KL ? tot : KL);
+  const size_t o = (size_t)task * KL + lane;
+  A.L.s[o] = s; A.L.tb[o] = t; A.L.id[o] = id;
+  const bool valid = lane < cnt;
+  const int h = valid ? id : 0;
+  A.L.zone[o] = valid ? A.zone[h] : 0;
+  const size_t WK = (size_t)A.nt * KL;
+  A.L.a[o] = valid ? A.avail[h] : 0.0;
+  A.L.a[WK + o] = valid ? A.avail[(size_t)A.H + h] : 0.0;
+  A.L.a[2 * WK + o] = valid ? A.avail[2 * (size_t)A.H + h] : 0.0;
+  A.L.a[3 * WK + o] = valid ? A.avail[3 * (size_t)A.H + h] : 0.0;
+  if (lane == 0) { A.L.cnt[task] = cnt; A.L.complete[task] = tot <= KL; }
+}
+
+void launch_merge(const MergeArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(merge_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// Ordered scan (vbp first-fit, cost_aware first-fit without sort_hosts): the first KL
+// snapshot-feasible hosts in index order, one wave per task, early exit.
+// ------------------------------------------------------------------------------------------
+template <bool STRICT>
+__global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int task = blockIdx.x * 4 + wave;
+  if (task >= A.nt) return;
+  const double* dp = A.dem + (size_t)task * 4;
+  const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+  const size_t WK = (size_t)A.nt * KL;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int cnt = 0;
+  int hb = 0;
+  for (; hb < A.H && cnt < KL; hb += WAVE) {
+    const int h = hb + lane;
+    const bool ok = h < A.H;
+    const double a0 = ok ? A.avail[h] : -DINF;
+    const double a1 = ok ? A.avail[(size_t)A.H + h] : -DINF;
+    const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : -DINF;
+    const double a3 = ok ? A.avail[3 * (size_t)A.H + h] : -DINF;
+    const bool fit = fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
+    const uint64_t m = __ballot(fit);
+    if (fit) {
+      const int pos = cnt + __popcll(m & below);
+      if (pos < KL) {
+        const size_t o = (size_t)task * KL + pos;
+        A.L.s[o] = 0.0; A.L.tb[o] = 0; A.L.id[o] = h; A.L.zone[o] = A.zone[h];
+        A.L.a[o] = a0; A.L.a[WK + o] = a1; A.L.a[2 * WK + o] = a2; A.L.a[3 * WK + o] = a3;
+      }
+    }
+    cnt += __popcll(m);
+  }
+  if (lane == 0) {
+    A.L.cnt[task] = cnt < KL ? cnt : KL;
+    A.L.complete[task] = (hb >= A.H) && cnt <= KL;
+  }
+}
+
+void launch_ordered(const OrderedArgs& a, hipStream_t st) {
+  dim3 grid((a.nt + 3) / 4), block(256);
+  if (a.strict) hipLaunchKernelGGL(ordered_kernel<true>, grid, block, 0, st, a);
+  else hipLaunchKernelGGL(ordered_kernel<false>, grid, block, 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// Commit walk: one wave visits the window's tasks in processing order and applies the
+// reference's sequential semantics. Hosts committed to in this window ("touched") live in LDS
+// with their current availability; every other host still has its snapshot state, so its list
+// entry (score, feasibility) is exact. Best-fit: winner = min(first untouched list entry,
+// rescored touched hosts). First-fit: first list entry that is still feasible. A list whose
+// entries are all touched and that may be missing hosts ("not complete") stops the walk; the
+// host side then starts a new window there (a refill).
+// ------------------------------------------------------------------------------------------
+constexpr int HASH_SLOTS = 1 << HASH_BITS;
+
+struct CommitLDS {
+  int32_t hkey[HASH_SLOTS];
+  int32_t hval[HASH_SLOTS];
+  int32_t tid[MAX_WINDOW];
+  int32_t tz[MAX_WINDOW];
+  uint32_t ttb[MAX_WINDOW];
+  double ta[4][MAX_WINDOW];
+};
+
+__device__ __forceinline__ uint32_t hslot(int32_t id) {
+  return ((uint32_t)id * 2654435761u) >> (32 - HASH_BITS);
+}
+__device__ __forceinline__ int hash_find(const CommitLDS& S, int32_t id) {
+  uint32_t p = hslot(id);
+  for (;;) {
+    const int32_t k = S.hkey[p];
+    if (k == id) return S.hval[p];
+    if (k < 0) return -1;
+    p = (p + 1) & (HASH_SLOTS - 1);
+  }
+}
+__device__ __forceinline__ void hash_put(CommitLDS& S, int32_t id, int32_t v) {
+  uint32_t p = hslot(id);
+  while (S.hkey[p] >= 0) p = (p + 1) & (HASH_SLOTS - 1);
+  S.hkey[p] = id;
+  S.hval[p] = v;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
+  constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
+  constexpr bool BEST = (MODE == CA_BF || MODE == VBP_BF);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  CommitLDS& S = *reinterpret_cast<CommitLDS*>(smem);
+  const int lane = lane_id();
+  for (int i = lane; i < HASH_SLOTS; i += WAVE) S.hkey[i] = -1;
+  int m = 0;               // touched hosts (uniform)
+  int next = A.nt;
+  const size_t WK = (size_t)A.nt * KL;
+
+  for (int i = 0; i < A.nt; i++) {
+    const double* dp = A.dem + (size_t)i * 4;
+    const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+    const int cnt = A.L.cnt[i];
+    const bool comp = A.L.complete[i] != 0;
+    const size_t o = (size_t)i * KL + lane;
+    const bool valid = lane < cnt;
+    const int32_t eid = A.L.id[o];
+    const int slot = valid ? hash_find(S, eid) : -1;
+
+    int w_id = -1, w_slot = -1, w_z = 0;
+    uint32_t w_tb = 0;
+    double w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+
+    if (BEST) {
+      const uint64_t mu = __ballot(valid && slot < 0);
+      if (mu == 0 && !comp) { next = i; break; }
+      double bs = DINF;
+      uint32_t bt = 0xffffffffu;
+      int32_t bi = 0x7fffffff;
+      int bl = -1;                       // lane of the untouched winner
+      if (mu) {
+        bl = __builtin_ctzll(mu);
+        bs = readlane_d(A.L.s[o], bl);
+        bt = readlane_u(A.L.tb[o], bl);
+        bi = readlane_i(eid, bl);
+      }
+      int bq = -1;                       // touched slot of the winner
+      const int anc = (MODE == CA_BF) ? A.anc[i] : 0;
+      for (int q0 = 0; q0 < m; q0 += WAVE) {
+        const int q = q0 + lane;
+        double cs = DINF;
+        uint32_t ct = 0xffffffffu;
+        int32_t ci = 0x7fffffff;
+        if (q < m) {
+          const double a0 = S.ta[0][q], a1 = S.ta[1][q], a2 = S.ta[2][q], a3 = S.ta[3][q];
+          if (fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3)) {
+            const double r = __builtin_sqrt(norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3));
+            if (MODE == CA_BF) {
+              const int z = S.tz[q];
+              cs = (A.csum[anc * A.Z + z] * r) / A.bsum[anc * A.Z + z];
+              ct = 0;
+            } else {
+              cs = r;
+              ct = S.ttb[q];
+            }
+            ci = S.tid[q];
+          }
+        }
+        int cq = q;
+        for (int off = 32; off > 0; off >>= 1) {
+          const double os = __shfl_xor(cs, off);
+          const uint32_t ot = (uint32_t)__shfl_xor((int)ct, off);
+          const int32_t oi = __shfl_xor(ci, off);
+          const int oq = __shfl_xor(cq, off);
+          if (lexless(os, ot, oi, cs, ct, ci)) { cs = os; ct = ot; ci = oi; cq = oq; }
+        }
+        if (lexless(cs, ct, ci, bs, bt, bi)) { bs = cs; bt = ct; bi = ci; bq = cq; bl = -1; }
+      }
+      if (bi == 0x7fffffff) continue;    // no feasible host: task waits
+      w_id = bi;
+      w_tb = bt;
+      if (bq >= 0) {
+        w_slot = bq;
+        w0 = S.ta[0][bq]; w1 = S.ta[1][bq]; w2 = S.ta[2][bq]; w3 = S.ta[3][bq];
+      } else {
+        w_z = readlane_i(A.L.zone[o], bl);
+        w0 = readlane_d(A.L.a[o], bl);
+        w1 = readlane_d(A.L.a[WK + o], bl);
+        w2 = readlane_d(A.L.a[2 * WK + o], bl);
+        w3 = readlane_d(A.L.a[3 * WK + o], bl);
+      }
+    } else {
+      bool ok = false;
+      if (valid) {
+        if (slot < 0) ok = true;
+        else ok = fits<STRICT>(S.ta[0][slot], S.ta[1][slot], S.ta[2][slot], S.ta[3][slot], d0, d1, d2, d3);
+      }
+      const uint64_t mf = __ballot(ok);
+      if (mf == 0) {
+        if (!comp) { next = i; break; }
+        continue;
+      }
+      const int L = __builtin_ctzll(mf);
+      w_id = readlane_i(eid, L);
+      w_slot = readlane_i(slot, L);
+      if (w_slot >= 0) {
+        w0 = S.ta[0][w_slot]; w1 = S.ta[1][w_slot]; w2 = S.ta[2][w_slot]; w3 = S.ta[3][w_slot];
+      } else {
+        w_z = readlane_i(A.L.zone[o], L);
+        w0 = readlane_d(A.L.a[o], L);
+        w1 = readlane_d(A.L.a[WK + o], L);
+        w2 = readlane_d(A.L.a[2 * WK + o], L);
+        w3 = readlane_d(A.L.a[3 * WK + o], L);
+      }
+    }
+    // commit: resc[h] -= t_demand (reference cost_aware.py:95,126; opportunistic.py:18; vbp.py:24,49)
+    const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
+    if (w_slot < 0) {
+      w_slot = m++;
+      if (lane == 0) {
+        hash_put(S, w_id, w_slot);
+        S.tid[w_slot] = w_id;
+        S.tz[w_slot] = w_z;
+        S.ttb[w_slot] = w_tb;
+      }
+    }
+    if (lane == 0) {
+      S.ta[0][w_slot] = n0; S.ta[1][w_slot] = n1; S.ta[2][w_slot] = n2; S.ta[3][w_slot] = n3;
+      A.avail[w_id] = n0;
+      A.avail[(size_t)A.H + w_id] = n1;
+      A.avail[2 * (size_t)A.H + w_id] = n2;
+      A.avail[3 * (size_t)A.H + w_id] = n3;
+      A.placement[A.ord[i]] = w_id;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes land before the next task reads
+  }
+  if (lane == 0) *A.next = next;
+}
+
+size_t commit_lds_bytes() { return sizeof(CommitLDS); }
+
+hipError_t init_kernel_attrs() {
+  const int lds = (int)sizeof(CommitLDS);
+  hipError_t e = hipSuccess, r;
+  r = hipFuncSetAttribute((const void*)commit_kernel<CA_FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (r != hipSuccess) e = r;
+  r = hipFuncSetAttribute((const void*)commit_kernel<CA_BF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (r != hipSuccess) e = r;
+  r = hipFuncSetAttribute((const void*)commit_kernel<VBP_FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (r != hipSuccess) e = r;
+  r = hipFuncSetAttribute((const void*)commit_kernel<VBP_BF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (r != hipSuccess) e = r;
+  return e;
+}
+
+void launch_commit(const CommitArgs& a, hipStream_t st) {
+  const size_t lds = sizeof(CommitLDS);
+  switch (a.mode) {
+    case CA_FF: hipLaunchKernelGGL(commit_kernel<CA_FF>, dim3(1), dim3(64), lds, st, a); break;
+    case CA_BF: hipLaunchKernelGGL(commit_kernel<CA_BF>, dim3(1), dim3(64), lds, st, a); break;
+    case VBP_FF: hipLaunchKernelGGL(commit_kernel<VBP_FF>, dim3(1), dim3(64), lds, st, a); break;
+    case VBP_BF: hipLaunchKernelGGL(commit_kernel<VBP_BF>, dim3(1), dim3(64), lds, st, a); break;
+    default: break;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Small kernels: zone tables, frozen first-fit keys, a2 sort keys, gathers.
+// ------------------------------------------------------------------------------------------
+__global__ void zone_tables_kernel(const double* cost, const double* bw, int Z, double* csum,
+                                   double* bsum) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= Z * Z) return;
+  const int a = i / Z, z = i % Z;
+  csum[i] = cost[a * Z + z] + cost[z * Z + a];   // cost_aware.py:82,113
+  bsum[i] = bw[a * Z + z] + bw[z * Z + a];       // in_route.bw + out_route.bw (:79,111)
+}
+void launch_zone_tables(const double* cost, const double* bw, int Z, double* csum, double* bsum,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(zone_tables_kernel, dim3((Z * Z + 255) / 256), dim3(256), 0, st, cost, bw, Z,
+                     csum, bsum);
+}
+
+// host_score_func of _first_fit (cost_aware.py:104-116): c * df / (r * bw), r = ||avail_h||.
+__global__ void key_kernel(KeyArgs A) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= A.H) return;
+  const double a0 = A.avail[h], a1 = A.avail[(size_t)A.H + h];
+  const double a2 = A.avail[2 * (size_t)A.H + h], a3 = A.avail[3 * (size_t)A.H + h];
+  const double r = __builtin_sqrt(norm2_seq(a0, a1, a2, a3));
+  const int z = A.zone[h];
+  const double c = A.csum[A.anchor * A.Z + z], bw = A.bsum[A.anchor * A.Z + z];
+  const double df = A.decay ? (double)A.decay[h] : 1.0;
+  A.key[h] = (c * df) / (r * bw);
+}
+void launch_key(const KeyArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(key_kernel, dim3((a.H + 255) / 256), dim3(256), 0, st, a);
+}
+
+__global__ void norm_keys_kernel(const double* dem, int T, const int32_t* idx, uint64_t* keys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T) return;
+  const int t = idx ? idx[i] : i;
+  const double n = __builtin_sqrt(norm2_seq(dem[t], dem[(size_t)T + t], dem[2 * (size_t)T + t],
+                                            dem[3 * (size_t)T + t]));
+  // n >= 0, so its bits order like the value; ~bits sorts descending norm ascending.
+  keys[i] = ~(uint64_t)__double_as_longlong(n);
+}
+void launch_norm_keys(const double* dem, int T, const int32_t* idx, uint64_t* keys, hipStream_t st) {
+  hipLaunchKernelGGL(norm_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, T, idx, keys);
+}
+
+__global__ void group_keys_kernel(const int32_t* tg, const int32_t* idx, int T, uint32_t* keys) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= T) return;
+  keys[i] = (uint32_t)tg[idx ? idx[i] : i];
+}
+void launch_group_keys(const int32_t* task_group, const int32_t* idx, int T, uint32_t* keys,
+                       hipStream_t st) {
+  hipLaunchKernelGGL(group_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, st, task_group, idx,
+                     T, keys);
+}
+
+__global__ void iota_kernel(int32_t* out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = i;
+}
+void launch_iota(int32_t* out, int n, hipStream_t st) {
+  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out, n);
+}
+
+__global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const int32_t* tg,
+                                    const int32_t* ga, int T, double* dem_ord, int32_t* anc_ord) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= T) return;
+  const int t = ord[p];
+  double* o = dem_ord + (size_t)p * 4;
+  o[0] = dem[t]; o[1] = dem[(size_t)T + t]; o[2] = dem[2 * (size_t)T + t]; o[3] = dem[3 * (size_t)T + t];
+  anc_ord[p] = (tg && ga) ? ga[tg[t]] : 0;
+}
+void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
+                         const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(gather_tasks_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, ord,
+                     task_group, group_anchor, T, dem_ord, anc_ord);
+}
+
+}  // namespace pvt

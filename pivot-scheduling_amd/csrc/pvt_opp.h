@@ -1,0 +1,43 @@
+// pvt_opp.h — opportunistic policy kernels (reference scheduler/opportunistic.py:11-20).
+//
+// Per task the reference lists every host with np.all(r >= d) in cluster order, draws
+// randomizer.choice(qualified) (= randint(0, n), no draw when n == 1) and commits. On the GPU:
+//   count kernel   per window task, the number of snapshot-feasible hosts in every chunk of
+//                  OPP_CH hosts and every super-chunk of OPP_SUP chunks (fused fit-mask pass)
+//   commit walk    one wave, tasks in order: n = snapshot count minus the touched hosts that
+//                  stopped fitting; MT19937 randint(n) in LDS; select the k-th currently
+//                  feasible host super-chunk -> chunk -> host; commit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pvt {
+
+constexpr int OPP_CH = 256;     // hosts per chunk
+constexpr int OPP_SUP = 64;     // chunks per super-chunk (16384 hosts)
+constexpr int OPP_TW = 8;       // tasks per wave in the count kernel
+constexpr int OPP_MAXW = 1024;  // tasks per window (commit-walk LDS: touched snapshot + current)
+
+struct OppCountArgs {
+  const double* avail;
+  const double* dem;      // window tasks [nt][4]
+  int H, nt, S, seg_sup, nq, nsq, ldc;
+  uint16_t* cc;           // [nq][ldc] chunk counts
+  int32_t* sc;            // [nsq][ldc] super-chunk counts
+};
+
+struct OppCommitArgs {
+  double* avail;
+  const double* dem;      // window tasks [nt][4]
+  const uint16_t* cc;
+  const int32_t* sc;
+  int H, nt, nq, nsq, ldc;
+  int32_t* placement;     // window tasks' placements (caller order == processing order)
+  uint32_t* mt;           // device MT19937 state: key[624], pos
+};
+
+void launch_opp_count(const OppCountArgs& a, hipStream_t st);
+void launch_opp_commit(const OppCommitArgs& a, hipStream_t st);
+hipError_t opp_init_attrs();
+
+}  // namespace pvt

@@ -1,0 +1,304 @@
+// pvt_opp.hip — opportunistic policy (reference scheduler/opportunistic.py:11-20) on gfx950.
+//
+// Exactness argument: within a window the snapshot feasibility of a host that
+// no task has committed to is unchanged, and a committed ("touched") host can only lose
+// feasibility. So the current feasible count of task t is its snapshot count minus the touched
+// hosts that fitted at the snapshot but no longer fit, and the k-th current feasible host is
+// found by walking snapshot counts corrected by those "lost" hosts.
+//
+// RandomState.choice(list) == randint(0, n) (numpy legacy): no draw when n == 1; otherwise
+// 32-bit MT19937 outputs masked to the next power of two minus one, rejected while > n - 1.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pvt_device.h"
+#include "pvt_kernels.h"
+#include "pvt_opp.h"
+
+namespace pvt {
+
+// ------------------------------------------------------------------------------------------
+// Count kernel: block = 4 waves, each wave OPP_TW tasks over one host segment (a run of
+// super-chunks); blockIdx % S picks the segment (XCD-affine, as in score_kernel).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int seg = blockIdx.x % A.S, tile = blockIdx.x / A.S;
+  const int t0 = (tile * 4 + wave) * OPP_TW;
+  if (t0 >= A.nt) return;
+  const int nt = min(OPP_TW, A.nt - t0);
+  double d0[OPP_TW], d1[OPP_TW], d2[OPP_TW], d3[OPP_TW];
+#pragma unroll
+  for (int k = 0; k < OPP_TW; k++) {
+    if (k < nt) {
+      const double* dp = A.dem + (size_t)(t0 + k) * 4;
+      d0[k] = dp[0]; d1[k] = dp[1]; d2[k] = dp[2]; d3[k] = dp[3];
+    } else {
+      d0[k] = d1[k] = d2[k] = d3[k] = DINF;
+    }
+  }
+  const int Q0 = seg * A.seg_sup, Q1 = min(A.nsq, Q0 + A.seg_sup);
+  for (int Q = Q0; Q < Q1; Q++) {
+    int sup[OPP_TW];
+#pragma unroll
+    for (int k = 0; k < OPP_TW; k++) sup[k] = 0;
+    const int q1 = min(A.nq, (Q + 1) * OPP_SUP);
+    for (int q = Q * OPP_SUP; q < q1; q++) {
+      int cnt[OPP_TW];
+#pragma unroll
+      for (int k = 0; k < OPP_TW; k++) cnt[k] = 0;
+#pragma unroll
+      for (int u = 0; u < OPP_CH / WAVE; u++) {
+        const int h = q * OPP_CH + u * WAVE + lane;
+        const bool ok = h < A.H;
+        const double a0 = ok ? A.avail[h] : -DINF;
+        const double a1 = ok ? A.avail[(size_t)A.H + h] : -DINF;
+        const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : -DINF;
+        const double a3 = ok ? A.avail[3 * (size_t)A.H + h] : -DINF;
+#pragma unroll
+        for (int k = 0; k < OPP_TW; k++)
+          cnt[k] += __popcll(__ballot(fits<false>(a0, a1, a2, a3, d0[k], d1[k], d2[k], d3[k])));
+      }
+      int v = 0;
+#pragma unroll
+      for (int k = 0; k < OPP_TW; k++) {
+        if (lane == k) v = cnt[k];
+        sup[k] += cnt[k];
+      }
+      if (lane < nt) A.cc[(size_t)q * A.ldc + t0 + lane] = (uint16_t)v;
+    }
+    int v = 0;
+#pragma unroll
+    for (int k = 0; k < OPP_TW; k++)
+      if (lane == k) v = sup[k];
+    if (lane < nt) A.sc[(size_t)Q * A.ldc + t0 + lane] = v;
+  }
+}
+
+void launch_opp_count(const OppCountArgs& a, hipStream_t st) {
+  const int tiles = (a.nt + 4 * OPP_TW - 1) / (4 * OPP_TW);
+  hipLaunchKernelGGL(opp_count_kernel, dim3(tiles * a.S), dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// Commit walk (one wave).
+// ------------------------------------------------------------------------------------------
+constexpr int OPP_HASH_BITS = 12;
+constexpr int OPP_HASH = 1 << OPP_HASH_BITS;
+
+struct OppLDS {
+  int32_t hkey[OPP_HASH];
+  int32_t hval[OPP_HASH];
+  int32_t tid[OPP_MAXW];
+  int32_t lost[OPP_MAXW];
+  double sa[4][OPP_MAXW];   // snapshot availability of touched hosts
+  double ta[4][OPP_MAXW];   // current availability of touched hosts
+  uint32_t mt[625];
+};
+
+__device__ __forceinline__ uint32_t ohslot(int32_t id) {
+  return ((uint32_t)id * 2654435761u) >> (32 - OPP_HASH_BITS);
+}
+__device__ __forceinline__ int ohash_find(const OppLDS& S, int32_t id) {
+  uint32_t p = ohslot(id);
+  for (;;) {
+    const int32_t k = S.hkey[p];
+    if (k == id) return S.hval[p];
+    if (k < 0) return -1;
+    p = (p + 1) & (OPP_HASH - 1);
+  }
+}
+__device__ __forceinline__ void ohash_put(OppLDS& S, int32_t id, int32_t v) {
+  uint32_t p = ohslot(id);
+  while (S.hkey[p] >= 0) p = (p + 1) & (OPP_HASH - 1);
+  S.hkey[p] = id;
+  S.hval[p] = v;
+}
+
+// numpy legacy MT19937 (mt19937_gen / mt19937_next), run by one lane.
+__device__ uint32_t mt_next(uint32_t* st) {
+  if (st[624] >= 624) {
+    for (int i = 0; i < 624; i++) {
+      const uint32_t y = (st[i] & 0x80000000u) | (st[(i + 1) % 624] & 0x7fffffffu);
+      uint32_t v = st[(i + 397) % 624] ^ (y >> 1);
+      if (y & 1u) v ^= 0x9908b0dfu;
+      st[i] = v;
+    }
+    st[624] = 0;
+  }
+  uint32_t y = st[st[624]++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  return y;
+}
+__device__ uint32_t mt_randint(uint32_t* st, uint32_t n) {
+  const uint32_t rng = n - 1;
+  if (rng == 0) return 0;
+  uint32_t mask = rng;
+  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
+  uint32_t v;
+  while ((v = (mt_next(st) & mask)) > rng) {}
+  return v;
+}
+
+// lost hosts among [lo, hi)
+__device__ __forceinline__ int lost_in(const OppLDS& S, int nl, int lo, int hi) {
+  int c = 0;
+  for (int j = 0; j < nl; j++) {
+    const int h = S.lost[j];
+    c += (h >= lo) & (h < hi);
+  }
+  return c;
+}
+
+__global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  OppLDS& S = *reinterpret_cast<OppLDS*>(smem);
+  const int lane = lane_id();
+  for (int i = lane; i < OPP_HASH; i += WAVE) S.hkey[i] = -1;
+  for (int i = lane; i < 625; i += WAVE) S.mt[i] = A.mt[i];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  constexpr int SUPH = OPP_SUP * OPP_CH;
+  int m = 0;
+
+  for (int i = 0; i < A.nt; i++) {
+    const double* dp = A.dem + (size_t)i * 4;
+    const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+    // touched hosts that fitted at the snapshot and no longer fit
+    int nl = 0;
+    for (int q0 = 0; q0 < m; q0 += WAVE) {
+      const int q = q0 + lane;
+      bool lf = false;
+      if (q < m)
+        lf = fits<false>(S.sa[0][q], S.sa[1][q], S.sa[2][q], S.sa[3][q], d0, d1, d2, d3) &&
+             !fits<false>(S.ta[0][q], S.ta[1][q], S.ta[2][q], S.ta[3][q], d0, d1, d2, d3);
+      const uint64_t b = __ballot(lf);
+      if (lf) S.lost[nl + __popcll(b & below)] = S.tid[q];
+      nl += __popcll(b);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    long long n = 0;
+    for (int Q0 = 0; Q0 < A.nsq; Q0 += WAVE) {
+      const int Q = Q0 + lane;
+      n += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)Q * A.ldc + i] : 0);
+    }
+    n -= nl;
+    if (n <= 0) continue;
+    uint32_t k = 0;
+    if (lane == 0) k = mt_randint(S.mt, (uint32_t)n);
+    k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+    // super-chunk
+    int Qs = -1;
+    long long acc = 0;
+    for (int Q0 = 0; Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
+      const int Q = Q0 + lane;
+      int v = 0;
+      if (Q < A.nsq) v = A.sc[(size_t)Q * A.ldc + i] - lost_in(S, nl, Q * SUPH, (Q + 1) * SUPH);
+      const int inc = wave_incl_scan(v);
+      const int tot = __builtin_amdgcn_readlane(inc, 63);
+      if ((long long)k < acc + tot) {
+        const uint64_t hit = __ballot(acc + inc > (long long)k);
+        const int L = __builtin_ctzll(hit);
+        Qs = Q0 + L;
+        acc += __builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(v, L);
+      } else {
+        acc += tot;
+      }
+    }
+    if (Qs < 0) continue;   // unreachable when counts are consistent
+    uint32_t k1 = k - (uint32_t)acc;
+    // chunk within the super-chunk
+    int qs;
+    {
+      const int q = Qs * OPP_SUP + lane;
+      int v = 0;
+      if (q < A.nq) v = (int)A.cc[(size_t)q * A.ldc + i] - lost_in(S, nl, q * OPP_CH, (q + 1) * OPP_CH);
+      const int inc = wave_incl_scan(v);
+      const uint64_t hit = __ballot(inc > (int)k1);
+      const int L = __builtin_ctzll(hit);
+      qs = Qs * OPP_SUP + L;
+      k1 -= (uint32_t)(__builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(v, L));
+    }
+    // host within the chunk: lane j covers hosts 4j .. 4j+3 of the chunk
+    double a[4][4];
+    int slot[4];
+    int f = 0, fm = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int h = qs * OPP_CH + lane * 4 + u;
+      slot[u] = -1;
+      if (h < A.H) {
+        slot[u] = ohash_find(S, h);
+        if (slot[u] >= 0) {
+          a[u][0] = S.ta[0][slot[u]]; a[u][1] = S.ta[1][slot[u]];
+          a[u][2] = S.ta[2][slot[u]]; a[u][3] = S.ta[3][slot[u]];
+        } else {
+          a[u][0] = A.avail[h]; a[u][1] = A.avail[(size_t)A.H + h];
+          a[u][2] = A.avail[2 * (size_t)A.H + h]; a[u][3] = A.avail[3 * (size_t)A.H + h];
+        }
+        const bool ok = fits<false>(a[u][0], a[u][1], a[u][2], a[u][3], d0, d1, d2, d3);
+        f += ok;
+        fm |= ok << u;
+      } else {
+        a[u][0] = a[u][1] = a[u][2] = a[u][3] = 0.0;
+      }
+    }
+    const int inc = wave_incl_scan(f);
+    const uint64_t hit = __ballot(inc > (int)k1);
+    if (hit == 0) continue;   // unreachable when counts are consistent
+    const int L = __builtin_ctzll(hit);
+    int r = (int)k1 - (__builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(f, L));
+    int pick = -1;
+    if (lane == L) {
+      for (int u = 0; u < 4; u++)
+        if ((fm >> u) & 1) {
+          if (r == 0) { pick = u; break; }
+          r--;
+        }
+    }
+    pick = __builtin_amdgcn_readlane(pick, L);
+    const int w = qs * OPP_CH + L * 4 + pick;
+    double w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    int ws = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (u == pick) {
+        w0 = readlane_d(a[u][0], L); w1 = readlane_d(a[u][1], L);
+        w2 = readlane_d(a[u][2], L); w3 = readlane_d(a[u][3], L);
+        ws = readlane_i(slot[u], L);
+      }
+    const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
+    if (ws < 0) {
+      ws = m++;
+      if (lane == 0) {
+        ohash_put(S, w, ws);
+        S.tid[ws] = w;
+        S.sa[0][ws] = w0; S.sa[1][ws] = w1; S.sa[2][ws] = w2; S.sa[3][ws] = w3;
+      }
+    }
+    if (lane == 0) {
+      S.ta[0][ws] = n0; S.ta[1][ws] = n1; S.ta[2][ws] = n2; S.ta[3][ws] = n3;
+      A.avail[w] = n0;
+      A.avail[(size_t)A.H + w] = n1;
+      A.avail[2 * (size_t)A.H + w] = n2;
+      A.avail[3 * (size_t)A.H + w] = n3;
+      A.placement[i] = w;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+  for (int i = lane; i < 625; i += WAVE) A.mt[i] = S.mt[i];
+}
+
+hipError_t opp_init_attrs() {
+  return hipFuncSetAttribute((const void*)opp_commit_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(OppLDS));
+}
+
+void launch_opp_commit(const OppCommitArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(opp_commit_kernel, dim3(1), dim3(64), sizeof(OppLDS), st, a);
+}
+
+}  // namespace pvt

@@ -1,0 +1,150 @@
+"""ctypes mirror of ``include/pivot_place.h`` (the engine's C ABI).
+
+The reference has no native code, so this module is the binding a maintainer would add next to
+its scheduler package. ``RoundArrays`` is the numpy-side description of one
+round; ``pvt_round`` is the C struct it is marshalled into.
+"""
+import ctypes
+import dataclasses
+from typing import Optional
+
+import numpy as np
+
+PVT_ABI_VERSION = 1
+
+PVT_OK = 0
+PVT_EINVAL = -1
+PVT_ENODEV = -2
+PVT_EHIP = -3
+PVT_ENOMEM = -4
+PVT_EUNSUPPORTED = -5
+ERRORS = {PVT_EINVAL: "EINVAL", PVT_ENODEV: "ENODEV", PVT_EHIP: "EHIP", PVT_ENOMEM: "ENOMEM",
+          PVT_EUNSUPPORTED: "EUNSUPPORTED"}
+
+PVT_CA_FF, PVT_CA_BF, PVT_OPP, PVT_VBP_FF, PVT_VBP_BF = range(5)
+MODE_NAMES = {PVT_CA_FF: "cost_aware_ff", PVT_CA_BF: "cost_aware_bf", PVT_OPP: "opportunistic",
+              PVT_VBP_FF: "vbp_ff", PVT_VBP_BF: "vbp_bf"}
+
+PVT_K_SCORE, PVT_K_MERGE, PVT_K_COMMIT, PVT_K_OTHER = range(4)
+
+# Algorithmic bytes per (task, host) candidate, SURVEY.md §8(d).
+BYTES_PER_CANDIDATE = {PVT_CA_FF: 36, PVT_CA_BF: 36, PVT_OPP: 32, PVT_VBP_FF: 32, PVT_VBP_BF: 36}
+
+
+class pvt_round(ctypes.Structure):
+    _fields_ = [
+        ("mode", ctypes.c_int32),
+        ("n_hosts", ctypes.c_int32),
+        ("n_tasks", ctypes.c_int32),
+        ("n_zones", ctypes.c_int32),
+        ("n_groups", ctypes.c_int32),
+        ("sort_tasks", ctypes.c_int32),
+        ("sort_hosts", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("avail", ctypes.c_void_p),
+        ("zone", ctypes.c_void_p),
+        ("tiebreak", ctypes.c_void_p),
+        ("decay", ctypes.c_void_p),
+        ("cost", ctypes.c_void_p),
+        ("bw", ctypes.c_void_p),
+        ("dem", ctypes.c_void_p),
+        ("task_group", ctypes.c_void_p),
+        ("group_anchor", ctypes.c_void_p),
+        ("order", ctypes.c_void_p),
+        ("placement", ctypes.c_void_p),
+        ("mt_state", ctypes.c_void_p),
+    ]
+
+
+class pvt_kstats(ctypes.Structure):
+    _fields_ = [("launches", ctypes.c_int64), ("ms", ctypes.c_double),
+                ("candidates", ctypes.c_double), ("bytes", ctypes.c_double)]
+
+
+@dataclasses.dataclass
+class RoundArrays:
+    """One scheduling round in the engine's SoA layout (host numpy arrays).
+
+    avail (4, H) f64 · zone (H,) i32 · dem (4, T) f64 · cost/bw (Z, Z) f64 · optional
+    tiebreak (H,) u32, decay (H,) i32, task_group (T,) i32 + group_anchor (G,) i32,
+    mt_state (625,) u32 (MT19937 key + pos).
+    """
+    mode: int
+    avail: np.ndarray
+    zone: np.ndarray
+    dem: np.ndarray
+    cost: Optional[np.ndarray] = None
+    bw: Optional[np.ndarray] = None
+    tiebreak: Optional[np.ndarray] = None
+    decay: Optional[np.ndarray] = None
+    task_group: Optional[np.ndarray] = None
+    group_anchor: Optional[np.ndarray] = None
+    sort_tasks: bool = False
+    sort_hosts: bool = False
+    mt_state: Optional[np.ndarray] = None
+
+    def __post_init__(self):
+        self.avail = np.ascontiguousarray(self.avail, dtype=np.float64).reshape(4, -1)
+        self.zone = np.ascontiguousarray(self.zone, dtype=np.int32)
+        self.dem = np.ascontiguousarray(self.dem, dtype=np.float64).reshape(4, -1)
+        if self.cost is None:
+            self.cost = np.zeros((1, 1))
+        if self.bw is None:
+            self.bw = np.ones((1, 1))
+        self.cost = np.ascontiguousarray(self.cost, dtype=np.float64)
+        self.bw = np.ascontiguousarray(self.bw, dtype=np.float64)
+        for name, dt in (("tiebreak", np.uint32), ("decay", np.int32), ("task_group", np.int32),
+                         ("group_anchor", np.int32), ("mt_state", np.uint32)):
+            v = getattr(self, name)
+            if v is not None:
+                setattr(self, name, np.ascontiguousarray(v, dtype=dt))
+
+    @property
+    def n_hosts(self):
+        return self.avail.shape[1]
+
+    @property
+    def n_tasks(self):
+        return self.dem.shape[1]
+
+    @property
+    def n_zones(self):
+        return self.cost.shape[0]
+
+    @property
+    def n_groups(self):
+        return 0 if self.group_anchor is None else len(self.group_anchor)
+
+    def copy(self):
+        return dataclasses.replace(self, **{f.name: (getattr(self, f.name).copy()
+                                                      if isinstance(getattr(self, f.name), np.ndarray)
+                                                      else getattr(self, f.name))
+                                             for f in dataclasses.fields(self)})
+
+
+@dataclasses.dataclass
+class RoundResult:
+    placement: np.ndarray      # (T,) i32 host index, -1 = not placed
+    order: np.ndarray          # (T,) i32 processing order
+    avail: np.ndarray          # (4, H) f64 after commits
+    mt_state: Optional[np.ndarray] = None
+
+
+def fill_struct(r: RoundArrays) -> pvt_round:
+    """A pvt_round with the scalar fields of ``r`` set; the caller fills the array pointers
+    (host pointers for the CPU oracle, device pointers for the engine)."""
+    s = pvt_round()
+    s.mode = r.mode
+    s.n_hosts = r.n_hosts
+    s.n_tasks = r.n_tasks
+    s.n_zones = r.n_zones
+    s.n_groups = r.n_groups
+    s.sort_tasks = int(bool(r.sort_tasks))
+    s.sort_hosts = int(bool(r.sort_hosts))
+    s.reserved = 0
+    return s
+
+
+def check_rc(rc, lib_error=""):
+    if rc != PVT_OK:
+        raise RuntimeError("pivot_place error %s (%d): %s" % (ERRORS.get(rc, "?"), rc, lib_error))

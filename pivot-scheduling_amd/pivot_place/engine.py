@@ -1,0 +1,191 @@
+"""PlacementEngine: the Python side of the C ABI (libpivot_place.so, gfx950 only).
+
+The engine owns one ``pvt_ctx`` per GPU. ``place()`` takes a round as host numpy arrays
+(``RoundArrays``), stages them in HBM as torch-ROCm tensors, calls ``pvt_place`` and returns
+host copies. ``DeviceRound`` keeps a round resident in HBM for repeated calls (bench, multi-GPU).
+
+There is no CPU fallback: if the HIP library is missing or no gfx950 device is visible, the
+constructor raises. The CPU restatement under oracle/ is test infrastructure and is never
+reached from here.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _abi
+from ._abi import RoundArrays, RoundResult
+
+LIB_NAME = "libpivot_place.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libpivot_place.so (raises OSError when it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError("pivot_place: %s not found; build it with `make -C pivot-scheduling_amd` "
+                      "(there is no CPU fallback)" % p)
+    lib = ctypes.CDLL(p)
+    c_int, c_void_p = ctypes.c_int, ctypes.c_void_p
+    sig = {
+        "pvt_abi_version": ([], c_int),
+        "pvt_ctx_create": ([c_int, ctypes.POINTER(c_void_p)], c_int),
+        "pvt_ctx_destroy": ([c_void_p], c_int),
+        "pvt_ctx_set_stream": ([c_void_p, c_void_p], c_int),
+        "pvt_place": ([c_void_p, c_void_p], c_int),
+        "pvt_set_profiling": ([c_void_p, c_int], c_int),
+        "pvt_reset_kstats": ([c_void_p], c_int),
+        "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
+        "pvt_set_window": ([c_void_p, c_int], c_int),
+        "pvt_last_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64),
+                            ctypes.POINTER(ctypes.c_int64)], c_int),
+        "pvt_last_error": ([c_void_p], ctypes.c_char_p),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes, f.restype = args, res
+    if lib.pvt_abi_version() != _abi.PVT_ABI_VERSION:
+        raise OSError("pivot_place ABI mismatch: library %d, binding %d"
+                      % (lib.pvt_abi_version(), _abi.PVT_ABI_VERSION))
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class DeviceRound:
+    """A round resident in HBM: torch tensors plus the pvt_round struct that points at them.
+
+    ``reset()`` restores the pristine availability (one D2D copy), so the same round can be
+    placed repeatedly (one bench step = reset + place)."""
+
+    def __init__(self, r: RoundArrays, device):
+        torch = _torch()
+        self.arrays = r
+        dev = torch.device(device)
+
+        def up(a):
+            return None if a is None else torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+        self.avail0 = up(r.avail)
+        self.avail = self.avail0.clone()
+        self.zone, self.tiebreak, self.decay = up(r.zone), up(r.tiebreak), up(r.decay)
+        self.cost, self.bw, self.dem = up(r.cost), up(r.bw), up(r.dem)
+        self.task_group, self.group_anchor = up(r.task_group), up(r.group_anchor)
+        T = r.n_tasks
+        self.order = torch.empty(max(T, 1), dtype=torch.int32, device=dev)
+        self.placement = torch.empty(max(T, 1), dtype=torch.int32, device=dev)
+        self.mt0 = None if r.mt_state is None else r.mt_state.copy()
+        self.mt = None if r.mt_state is None else r.mt_state.copy()
+        s = _abi.fill_struct(r)
+
+        def dp(t):
+            return None if t is None else t.data_ptr()
+
+        s.avail, s.zone, s.tiebreak, s.decay = dp(self.avail), dp(self.zone), dp(self.tiebreak), dp(self.decay)
+        s.cost, s.bw, s.dem = dp(self.cost), dp(self.bw), dp(self.dem)
+        s.task_group, s.group_anchor = dp(self.task_group), dp(self.group_anchor)
+        s.order, s.placement = dp(self.order), dp(self.placement)
+        s.mt_state = None if self.mt is None else self.mt.ctypes.data
+        self.struct = s
+
+    def reset(self):
+        self.avail.copy_(self.avail0)
+        if self.mt is not None:
+            self.mt[:] = self.mt0
+
+    def result(self) -> RoundResult:
+        T = self.arrays.n_tasks
+        return RoundResult(placement=self.placement[:T].cpu().numpy(),
+                           order=self.order[:T].cpu().numpy(),
+                           avail=self.avail.cpu().numpy(),
+                           mt_state=None if self.mt is None else self.mt.copy())
+
+
+class PlacementEngine:
+    """One pvt_ctx on one gfx950 device."""
+
+    def __init__(self, device=0, window=0):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError("pivot_place needs a ROCm GPU (gfx950); none is visible")
+        self.lib = load_library()
+        self.device_index = int(device)
+        self.device = torch.device("cuda", self.device_index)
+        ctx = ctypes.c_void_p()
+        rc = self.lib.pvt_ctx_create(self.device_index, ctypes.byref(ctx))
+        if rc != _abi.PVT_OK:
+            raise RuntimeError("pvt_ctx_create(%d) failed: %s" % (self.device_index,
+                                                                  _abi.ERRORS.get(rc, rc)))
+        self.ctx = ctx
+        if window:
+            self.lib.pvt_set_window(self.ctx, int(window))
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.pvt_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != _abi.PVT_OK:
+            msg = self.lib.pvt_last_error(self.ctx)
+            _abi.check_rc(rc, msg.decode() if msg else "")
+
+    def run(self, dr: DeviceRound):
+        """Place a resident round (its avail / placement / order / mt are updated in place)."""
+        torch = _torch()
+        stream = torch.cuda.current_stream(self.device)
+        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._check(self.lib.pvt_place(self.ctx, ctypes.addressof(dr.struct)))
+
+    def place(self, r: RoundArrays) -> RoundResult:
+        dr = DeviceRound(r, self.device)
+        self.run(dr)
+        return dr.result()
+
+    def set_window(self, tasks):
+        self._check(self.lib.pvt_set_window(self.ctx, int(tasks)))
+
+    def set_profiling(self, on=True):
+        self._check(self.lib.pvt_set_profiling(self.ctx, int(bool(on))))
+
+    def reset_kstats(self):
+        self._check(self.lib.pvt_reset_kstats(self.ctx))
+
+    def kstats(self, kclass):
+        k = _abi.pvt_kstats()
+        self._check(self.lib.pvt_get_kstats(self.ctx, int(kclass), ctypes.byref(k)))
+        return {"launches": k.launches, "ms": k.ms, "candidates": k.candidates, "bytes": k.bytes}
+
+    def last_stats(self):
+        w, r = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.pvt_last_stats(self.ctx, ctypes.byref(w), ctypes.byref(r)))
+        return {"windows": w.value, "refills": r.value}
+
+
+_engines = {}
+
+
+def default_engine(device=0) -> PlacementEngine:
+    """Process-wide engine per device (what the drop-in policies use)."""
+    eng = _engines.get(device)
+    if eng is None:
+        eng = PlacementEngine(device)
+        _engines[device] = eng
+    return eng

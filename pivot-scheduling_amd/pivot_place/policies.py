@@ -1,0 +1,298 @@
+"""Drop-in GPU policies with the reference's plugin contract.
+
+A reference policy subclasses ``GlobalSchedulerBase`` and overrides ``schedule(self, tasks)``
+(reference scheduler/__init__.py:79-80), called once per round at scheduler/__init__.py:103.
+The mixins below keep that contract and the reference's constructor kwargs. Their
+``schedule()`` marshals the round into the engine's SoA layout and calls ``pvt_place``:
+
+=============================  =======================================================
+reference class                drop-in here
+=============================  =======================================================
+CostAwareGlobalScheduler       ``CostAwarePlacement``    (scheduler/cost_aware.py:11-127)
+OpportunisticGlobalScheduler   ``OpportunisticPlacement`` (scheduler/opportunistic.py:8-20)
+FirstFitGlobalScheduler        ``FirstFitPlacement``     (scheduler/vbp.py:6-29)
+BestFitGlobalScheduler         ``BestFitPlacement``      (scheduler/vbp.py:32-50)
+=============================  =======================================================
+
+Each mixin needs only what the reference base provides: ``self.cluster`` (hosts, storage,
+get_host, get_storage_by_locality, meta), ``self.resource_info`` (the round snapshot, whose
+arrays it updates in place like the reference's ``resc[h.id] -= t_demand``) and
+``self.randomizer`` (numpy RandomState, advanced exactly as the reference advances it). So a
+maintainer combines a mixin with the reference base unchanged, or uses the
+ready-made classes at the bottom, built on ``GlobalSchedulerBase`` in this module (the
+attributes of reference scheduler/__init__.py:14-85, without the SimPy loop).
+
+What stays on the host, as in the reference: cost_aware grouping and anchor choice
+(cost_aware.py:45-58, the ``randomizer.choice(storage)`` at :38-39), because it reads the
+application DAG and advances the RNG.
+"""
+from collections import Counter, OrderedDict
+
+import numpy as np
+import numpy.random as rnd
+
+from . import _abi
+from ._abi import RoundArrays
+
+
+class GlobalSchedulerBase:
+    """The parts of reference scheduler/__init__.py:14-85 that ``schedule()`` relies on."""
+
+    def __init__(self, env, cluster, interval=5, seed=None, meter=None, *args, **kwargs):
+        assert isinstance(interval, int)
+        self.__env = env
+        self.__cluster = cluster
+        self.__interval = interval
+        self.__resource_info = {}
+        self.__randomizer = rnd.RandomState(seed)
+        self.__meter = meter
+
+    @property
+    def env(self):
+        return self.__env
+
+    @property
+    def cluster(self):
+        return self.__cluster
+
+    @property
+    def resource_info(self):
+        return dict(self.__resource_info)
+
+    @property
+    def randomizer(self):
+        return self.__randomizer
+
+    def schedule(self, tasks):
+        raise NotImplementedError
+
+    def _update_resource_info(self):
+        self.__resource_info = {h.id: np.array([h.resource.cpus_available, h.resource.mem_available,
+                                                h.resource.disk_available, h.resource.gpus_available])
+                                for h in self.cluster.hosts}
+
+
+class _ClusterTables:
+    """Per-cluster static arrays: zone index per host, host-id ranks, Z x Z cost / bw."""
+
+    def __init__(self, cluster):
+        meta = cluster.meta
+        hosts = cluster.hosts
+        self.n_hosts = len(hosts)
+        self.host_ids = [h.id for h in hosts]
+        self.zones = list(meta.zones) if meta is not None else []
+        self.zone_of = {z: i for i, z in enumerate(self.zones)}
+        self.zone = np.array([self.zone_of.get(h.locality, 0) for h in hosts], dtype=np.int32)
+        order = sorted(range(len(hosts)), key=lambda i: self.host_ids[i])
+        self.rank = np.empty(len(hosts), dtype=np.uint32)
+        self.rank[order] = np.arange(len(hosts), dtype=np.uint32)
+        if meta is not None and self.zones:
+            cost, bw = meta.cost, meta.bw
+            Z = len(self.zones)
+            self.cost = np.array([[cost[(a, b)] for b in self.zones] for a in self.zones],
+                                 dtype=np.float64).reshape(Z, Z)
+            self.bw = np.array([[bw[(a, b)] for b in self.zones] for a in self.zones],
+                               dtype=np.float64).reshape(Z, Z)
+        else:
+            self.cost = np.zeros((1, 1))
+            self.bw = np.ones((1, 1))
+
+    def matches(self, cluster):
+        hosts = cluster.hosts
+        return len(hosts) == self.n_hosts and all(h.id == i for h, i in zip(hosts, self.host_ids))
+
+
+class PlacementMixin:
+    """Shared marshalling: snapshot -> SoA, engine call, results -> tasks and resc."""
+
+    engine = None          # set to a PlacementEngine to pin a device; default: cuda:0
+
+    def _engine(self):
+        if self.engine is None:
+            from .engine import default_engine
+            return default_engine(0)
+        return self.engine
+
+    def _tables(self):
+        cl = self.cluster
+        tab = getattr(self, "_pvt_tables", None)
+        if tab is None or not tab.matches(cl):
+            tab = _ClusterTables(cl)
+            self._pvt_tables = tab
+        return tab
+
+    @staticmethod
+    def _snapshot(hosts, resc):
+        a = np.empty((4, len(hosts)), dtype=np.float64)
+        for j, h in enumerate(hosts):
+            a[:, j] = resc[h.id]
+        return a
+
+    @staticmethod
+    def _demand(tasks):
+        d = np.empty((4, len(tasks)), dtype=np.float64)
+        for j, t in enumerate(tasks):
+            d[0, j], d[1, j], d[2, j], d[3, j] = t.cpus, t.mem, t.disk, t.gpus
+        return d
+
+    def _apply(self, tasks, hosts, resc, res, before):
+        for t, p in zip(tasks, res.placement):
+            if p >= 0:
+                t.placement = hosts[p].id
+        changed = np.nonzero((res.avail != before).any(axis=0))[0]
+        for j in changed:
+            resc[hosts[j].id][:] = res.avail[:, j]
+
+
+class CostAwarePlacement(PlacementMixin):
+    """PIVOT's cost-aware policy (reference scheduler/cost_aware.py:11-127)."""
+
+    def __init__(self, *args, **kwargs):
+        bin_pack_algo = str(kwargs.pop('bin_pack_algo', 'first-fit'))
+        sort_tasks = bool(kwargs.pop('sort_tasks', False))
+        sort_hosts = bool(kwargs.pop('sort_hosts', False))
+        realtime_bw = kwargs.pop('realtime_bw', False)
+        host_decay = kwargs.pop('host_decay', False)
+        super().__init__(*args, **kwargs)
+        self._pvt_algo = bin_pack_algo
+        self._pvt_sort_tasks = sort_tasks
+        self._pvt_sort_hosts = sort_hosts
+        self._pvt_realtime_bw = realtime_bw
+        self._pvt_host_decay = host_decay
+
+    def _group_tasks(self, tasks):
+        """Groups keyed by anchor storage, or by application for source tasks, in first-seen
+        order (reference cost_aware.py:45-58). The anchor of a task with predecessors is the
+        zone of the MODE host of all predecessor task placements (first seen wins ties)."""
+        cluster = self.cluster
+        groups = OrderedDict()
+        memo = {}
+        for t in tasks:
+            c = t.container
+            key = memo.get(id(c))
+            if key is None:
+                app = c.application
+                placements = [p.placement for pc in app.get_predecessors(c.id) for p in pc.tasks]
+                if placements:
+                    host_id = max(Counter(placements).items(), key=lambda kv: kv[1])[0]
+                    key = ('storage', cluster.get_storage_by_locality(cluster.get_host(host_id).locality))
+                else:
+                    key = ('app', app)
+                memo[id(c)] = key
+            groups.setdefault(key, []).append(t)
+        return groups
+
+    def schedule(self, tasks):
+        algo = self._pvt_algo
+        if algo not in ('first-fit', 'best-fit'):
+            if tasks:   # the reference calls the str (cost_aware.py:42)
+                raise TypeError("'str' object is not callable")
+            return tasks
+        if self._pvt_realtime_bw:
+            raise NotImplementedError("realtime_bw=True is not supported by the GPU engine yet")
+        storage, hosts = self.cluster.storage, self.cluster.hosts
+        resc = self.resource_info
+        tab = self._tables()
+        groups = self._group_tasks(tasks)
+        task_pos = {id(t): i for i, t in enumerate(tasks)}
+        T = len(tasks)
+        task_group = np.zeros(T, dtype=np.int32)
+        anchors = []
+        avail = self._snapshot(hosts, resc)
+        dem = self._demand(tasks)
+        best_fit = algo == 'best-fit'
+        for g, ((kind, obj), members) in enumerate(groups.items()):
+            anchor = self.randomizer.choice(storage) if kind == 'app' else obj
+            if best_fit and self._pvt_host_decay:
+                # the reference reads None[h.id] on the first candidate (cost_aware.py:26,81)
+                idx = [task_pos[id(t)] for t in members]
+                if any(((avail >= dem[:, [i]]).all(axis=0)).any() for i in idx):
+                    raise TypeError("'NoneType' object is not subscriptable")
+            anchors.append(tab.zone_of[anchor.locality])
+            for t in members:
+                task_group[task_pos[id(t)]] = g
+        if best_fit and self._pvt_host_decay:
+            return tasks
+        decay = None
+        if self._pvt_host_decay:
+            decay = np.array([max(len(h.tasks), 1) for h in hosts], dtype=np.int32)
+        r = RoundArrays(mode=_abi.PVT_CA_BF if best_fit else _abi.PVT_CA_FF, avail=avail,
+                        zone=tab.zone, dem=dem, cost=tab.cost, bw=tab.bw, decay=decay,
+                        task_group=task_group, group_anchor=np.array(anchors, dtype=np.int32),
+                        sort_tasks=self._pvt_sort_tasks, sort_hosts=self._pvt_sort_hosts)
+        if T:
+            res = self._engine().place(r)
+            self._apply(tasks, hosts, resc, res, avail)
+        return tasks
+
+
+class OpportunisticPlacement(PlacementMixin):
+    """Uniform random feasible host (reference scheduler/opportunistic.py:11-20)."""
+
+    def schedule(self, tasks):
+        hosts = self.cluster.hosts
+        resc = self.resource_info
+        if not tasks:
+            return list(tasks)
+        tab = self._tables()
+        st = self.randomizer.get_state()
+        mt = np.empty(625, dtype=np.uint32)
+        mt[:624] = st[1]
+        mt[624] = st[2]
+        avail = self._snapshot(hosts, resc)
+        r = RoundArrays(mode=_abi.PVT_OPP, avail=avail, zone=tab.zone, dem=self._demand(tasks),
+                        mt_state=mt)
+        res = self._engine().place(r)
+        self.randomizer.set_state((st[0], res.mt_state[:624].copy(), int(res.mt_state[624]),
+                                   st[3], st[4]))
+        self._apply(tasks, hosts, resc, res, avail)
+        return list(tasks)
+
+
+class _VbpPlacement(PlacementMixin):
+    _mode = None
+
+    def __init__(self, *args, **kwargs):
+        # str(False) is truthy: the reference always sorts (scheduler/vbp.py:9,35)
+        decreasing = str(kwargs.pop('decreasing', False))
+        super().__init__(*args, **kwargs)
+        self._pvt_decreasing = decreasing
+
+    def schedule(self, tasks):
+        hosts = self.cluster.hosts
+        resc = self.resource_info
+        if not tasks:
+            return list(tasks) if self._pvt_decreasing else tasks
+        tab = self._tables()
+        avail = self._snapshot(hosts, resc)
+        r = RoundArrays(mode=self._mode, avail=avail, zone=tab.zone, dem=self._demand(tasks),
+                        tiebreak=tab.rank, sort_tasks=bool(self._pvt_decreasing))
+        res = self._engine().place(r)
+        self._apply(tasks, hosts, resc, res, avail)
+        return [tasks[i] for i in res.order]
+
+
+class FirstFitPlacement(_VbpPlacement):
+    """Vector bin packing, first fit (reference scheduler/vbp.py:6-29)."""
+    _mode = _abi.PVT_VBP_FF
+
+
+class BestFitPlacement(_VbpPlacement):
+    """Vector bin packing, best fit, ties by host-id string (reference scheduler/vbp.py:32-50)."""
+    _mode = _abi.PVT_VBP_BF
+
+
+class CostAwareGlobalScheduler(CostAwarePlacement, GlobalSchedulerBase):
+    pass
+
+
+class OpportunisticGlobalScheduler(OpportunisticPlacement, GlobalSchedulerBase):
+    pass
+
+
+class FirstFitGlobalScheduler(FirstFitPlacement, GlobalSchedulerBase):
+    pass
+
+
+class BestFitGlobalScheduler(BestFitPlacement, GlobalSchedulerBase):
+    pass
