@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Placement-candidate throughput of the MI355X engine (BASELINE.json metric).
+
+One step = one scheduling round of one policy over a synthetic round resident in HBM: reset
+the host availability to the round's snapshot (one D2D copy), then
+pvt_place (a2 ordering, fused score/top-K passes, merges, sequential commit walk).
+Candidates per step = T x H, the round's logical task x host space.
+
+Default workload (N=1): BASELINE config 5 shape on one GPU — 1M hosts x 10k ready tasks,
+20 zones, cost_aware best-fit (every candidate fit-masked and scored). For N > 1 every rank runs
+its own independent scenario (seed + rank), as in the scenario-batch config: weak scaling, no
+collective on the data path; only the final timing max is reduced.
+
+Run:  python bench.py [--gpus N --steps K --warmup W --mode ca_bf --hosts H --tasks T]
+      torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "pivot-scheduling_amd"), ROOT]
+
+import numpy as np  # noqa: E402
+
+MODES = {"ca_ff": 0, "ca_bf": 1, "opp": 2, "vbp_ff": 3, "vbp_bf": 4}
+POLICY = {"ca_ff": "cost_aware first-fit (sort_tasks, sort_hosts)", "ca_bf": "cost_aware best-fit",
+          "opp": "opportunistic", "vbp_ff": "vbp first-fit decreasing", "vbp_bf": "vbp best-fit"}
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--mode", default="ca_bf", choices=sorted(MODES))
+    p.add_argument("--hosts", type=int, default=1_000_000)
+    p.add_argument("--tasks", type=int, default=10_000)
+    p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--window", type=int, default=0)
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
+                   help="target CPU time of the oracle baseline sample (0 = skip)")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                   help="rocprofv3 PMC traffic summary (tools/pmc_traffic.py); absent = null")
+    return p.parse_args()
+
+
+def cpu_baseline(r, budget_s):
+    """The CPU restatement (oracle/, 1 thread) on the first n tasks of the same round, n sized
+    so the sample takes about ``budget_s`` seconds."""
+    from oracle import oracle
+    from pivot_place.synthetic import subset_tasks
+    n = min(r.n_tasks, 4)
+    t = time.perf_counter()
+    oracle.place(subset_tasks(r, n))
+    dt = max(time.perf_counter() - t, 1e-6)
+    n = int(max(1, min(r.n_tasks, n * budget_s / dt)))
+    sub = subset_tasks(r, n)
+    t = time.perf_counter()
+    oracle.place(sub)
+    dt = time.perf_counter() - t
+    cand = float(n) * r.n_hosts
+    return {"value": cand / dt, "unit": "candidates/s", "cores": 1, "kind": "port",
+            "sample": "oracle/pivot_oracle.c (C restatement, 1 thread, -O2) on the first %d tasks "
+                      "x %d hosts of the same round (%.1f s)" % (n, r.n_hosts, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from pivot_place import _abi, synthetic
+    from pivot_place.engine import DeviceRound, PlacementEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    mode = MODES[args.mode]
+    H, T = args.hosts, args.tasks
+    log("[rank %d] building synthetic round: %s, H=%d T=%d" % (rank, args.mode, H, T))
+    r = synthetic.make_round(mode, H, T, seed=args.seed + rank)
+    eng = PlacementEngine(local, window=args.window)
+    dr = DeviceRound(r, eng.device)
+    torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        dr.reset()
+        eng.run(dr)
+    torch.cuda.synchronize()
+    stats = eng.last_stats()
+    placed = int((dr.placement[:T] >= 0).sum().item())
+    log("[rank %d] warmup done: %d/%d placed, windows=%d refills=%d"
+        % (rank, placed, T, stats["windows"], stats["refills"]))
+
+    eng.reset_kstats()
+    eng.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        dr.reset()
+        eng.run(dr)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    eng.set_profiling(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    cand_per_step = float(T) * H * world
+    value = cand_per_step / (elapsed / args.steps)
+
+    ks = {name: eng.kstats(k) for name, k in (("score", _abi.PVT_K_SCORE), ("merge", _abi.PVT_K_MERGE),
+                                               ("commit", _abi.PVT_K_COMMIT), ("other", _abi.PVT_K_OTHER))}
+    score = ks["score"]
+    avg_ms = score["ms"] / max(score["launches"], 1)
+    bytes_per_launch = score["bytes"] / max(score["launches"], 1)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("mode") == args.mode and tj.get("hosts") == H and tj.get("tasks") == T:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    if rank == 0:
+        out = {
+            "metric": "task x host placement candidates scored/sec (HBM GB/s % peak) at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "candidates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8(d): trace demand rows, 20 locality.yml zones, seeded)",
+            "config": {
+                "workload": "synthetic %d hosts x %d ready tasks per round, 20 zones, %s, "
+                            "one independent scenario per GPU" % (H, T, POLICY[args.mode]),
+                "hosts": H, "tasks_per_round": T, "zones": 20, "policy": args.mode,
+                "parallelism": "scenario-sharded x%d (no data-path collective)" % world,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "score (fused fit-mask + score + top-K)",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "avg_launch_ms": avg_ms,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+                "bytes_per_candidate": _abi.BYTES_PER_CANDIDATE[mode],
+            },
+            "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items()},
+            "windows_per_step": stats["windows"], "refills_per_step": stats["refills"],
+        }
+        if world == 1 and args.cpu_baseline_seconds > 0:
+            log("[rank 0] cpu baseline (oracle, 1 thread) ...")
+            out["cpu_baseline"] = cpu_baseline(r, args.cpu_baseline_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -267,15 +267,16 @@ static int check_round(pvt_ctx* ctx, const pvt_round* r) {
   if (r->n_hosts < 1 || r->n_tasks < 0 || r->n_zones < 1 || r->n_zones > ZMAX)
     return fail(ctx, PVT_EINVAL, "bad sizes H=%d T=%d Z=%d", r->n_hosts, r->n_tasks, r->n_zones);
   if (r->mode < PVT_CA_FF || r->mode > PVT_VBP_BF) return fail(ctx, PVT_EINVAL, "bad mode %d", r->mode);
-  if (!r->avail || !r->zone || !r->dem || !r->order || !r->placement)
-    return fail(ctx, PVT_EINVAL, "null array");
+  if (!r->avail || !r->zone) return fail(ctx, PVT_EINVAL, "null host array");
+  if (r->n_tasks > 0 && (!r->dem || !r->order || !r->placement))
+    return fail(ctx, PVT_EINVAL, "null task array");
   if ((r->mode == PVT_CA_FF || r->mode == PVT_CA_BF) && (!r->cost || !r->bw))
     return fail(ctx, PVT_EINVAL, "cost_aware needs cost and bw");
-  if (r->task_group && (r->n_groups < 1 || !r->group_anchor))
+  if (r->n_tasks > 0 && r->task_group && (r->n_groups < 1 || !r->group_anchor))
     return fail(ctx, PVT_EINVAL, "task_group needs n_groups >= 1 and group_anchor");
   if (r->mode == PVT_VBP_BF && !r->tiebreak) return fail(ctx, PVT_EINVAL, "vbp best-fit needs tiebreak");
   if (r->mode == PVT_OPP && !r->mt_state) return fail(ctx, PVT_EINVAL, "opportunistic needs mt_state");
-  if (r->mode == PVT_CA_BF && r->decay)
+  if (r->mode == PVT_CA_BF && r->decay && r->n_tasks > 0)
     return fail(ctx, PVT_EUNSUPPORTED, "cost_aware best-fit with host_decay (reference crashes, cost_aware.py:26,81)");
   return PVT_OK;
 }

@@ -1,0 +1,81 @@
+"""GPU parity: the HIP engine (through the C ABI) against the reference's golden runs and the
+CPU restatement. Integer/index outputs and fp64 availability must match bit for bit."""
+import numpy as np
+import pytest
+
+import golden_io
+from oracle import oracle
+from pivot_place import _abi, synthetic
+
+pytestmark = pytest.mark.gpu
+
+ALL_MODES = [_abi.PVT_CA_FF, _abi.PVT_CA_BF, _abi.PVT_OPP, _abi.PVT_VBP_FF, _abi.PVT_VBP_BF]
+
+
+def _assert_same(res, placement, order, avail, mt=None):
+    np.testing.assert_array_equal(res.placement, placement)
+    np.testing.assert_array_equal(res.order, order)
+    bad = np.nonzero((res.avail != avail).any(axis=0))[0]
+    assert bad.size == 0, "availability differs on hosts %s" % bad[:10]
+    if mt is not None:
+        np.testing.assert_array_equal(res.mt_state, mt)
+
+
+@pytest.mark.parametrize("name,idx", golden_io.all_runs())
+def test_engine_matches_reference(engine, name, idx):
+    case = golden_io.load(name)
+    run = case["runs"][idx]
+    res = engine.place(golden_io.run_arrays(case, run))
+    _assert_same(res, *golden_io.expected(case, run))
+
+
+@pytest.mark.parametrize("window", [1, 7, 64])
+@pytest.mark.parametrize("name", ["saturate", "c1_sim_h100"])
+def test_small_windows_force_refills(engine, name, window):
+    """Tiny windows make every list-exhaustion / refill path run; results must not change."""
+    case = golden_io.load(name)
+    try:
+        engine.set_window(window)
+        for run in case["runs"]:
+            if run["error"]:
+                continue
+            res = engine.place(golden_io.run_arrays(case, run))
+            _assert_same(res, *golden_io.expected(case, run))
+    finally:
+        engine.set_window(0)
+
+
+@pytest.mark.parametrize("mode", ALL_MODES)
+@pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70000, 120, 2), (1, 5, 3), (64, 2000, 4)])
+def test_engine_matches_oracle_synthetic(engine, mode, H, T, seed):
+    r = synthetic.make_round(mode, H, T, seed=seed)
+    ref = oracle.place(r)
+    res = engine.place(r)
+    _assert_same(res, ref.placement, ref.order, ref.avail, ref.mt_state)
+
+
+@pytest.mark.parametrize("mode", ALL_MODES)
+def test_engine_crowded_hosts(engine, mode):
+    """Few, nearly full hosts with identical states: ties, exhaustion and unplaceable tasks."""
+    r = synthetic.make_round(mode, 300, 1500, seed=11)
+    r.avail[0, :] = 4.0
+    r.avail[1, :] = 40000.0
+    r.avail[0, ::7] = 0.5
+    ref = oracle.place(r)
+    res = engine.place(r)
+    _assert_same(res, ref.placement, ref.order, ref.avail, ref.mt_state)
+
+
+def test_sqrt_and_division_are_correctly_rounded(engine):
+    """Best-fit scores need IEEE sqrt and division: compare scores on many random residuals by
+    running vbp best-fit with one task against hosts whose residual norms nearly tie."""
+    rs = np.random.RandomState(9)
+    H = 4096
+    base = rs.uniform(1, 1e6, size=H)
+    r = synthetic.make_round(_abi.PVT_VBP_BF, H, 1, seed=9)
+    r.avail[1, :] = base
+    r.avail[1, 1::2] = np.nextafter(base[1::2], np.inf)
+    r.dem[:, 0] = [0.5, 1.0, 0.0, 0.0]
+    ref = oracle.place(r)
+    res = engine.place(r)
+    _assert_same(res, ref.placement, ref.order, ref.avail)
