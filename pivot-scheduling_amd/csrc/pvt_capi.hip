@@ -49,8 +49,9 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_s, l_tb, l_id, l_zone, l_a, l_cnt, l_comp, next, opp;
+      seg, seg_feas, l_e, l_t, next, opp;
   int32_t* next_host = nullptr;   // pinned
+  uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
 };
 
 static int fail(pvt_ctx* c, int code, const char* fmt, ...) {
@@ -164,8 +165,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   harvest(ctx);
   Buf* bufs[] = {&ctx->ord, &ctx->ord2, &ctx->keys64a, &ctx->keys64b, &ctx->keys32a, &ctx->keys32b,
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
-                 &ctx->seg, &ctx->seg_feas, &ctx->l_s, &ctx->l_tb, &ctx->l_id, &ctx->l_zone,
-                 &ctx->l_a, &ctx->l_cnt, &ctx->l_comp, &ctx->next, &ctx->opp};
+                 &ctx->seg, &ctx->seg_feas, &ctx->l_e, &ctx->l_t, &ctx->next, &ctx->opp};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -211,9 +211,40 @@ extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) 
   if (refills) *refills = ctx->refills;
   return PVT_OK;
 }
+// Diagnostic (not part of the public ABI): commit-walk phase cycle sums of a PVT_STAMPS build.
+extern "C" int pvt_debug_commit_stamps(pvt_ctx* ctx, uint64_t* out, int n) {
+  if (!ctx || !out || n < 6) return PVT_EINVAL;
+#ifdef PVT_STAMPS
+  if (!ctx->stamps) {
+    if (hipMalloc((void**)&ctx->stamps, 64) != hipSuccess) return PVT_ENOMEM;
+    (void)hipMemset(ctx->stamps, 0, 64);
+    std::memset(out, 0, sizeof(uint64_t) * 6);
+    return PVT_OK;
+  }
+  if (hipMemcpy(out, ctx->stamps, 48, hipMemcpyDeviceToHost) != hipSuccess) return PVT_EHIP;
+  return PVT_OK;
+#else
+  return PVT_EUNSUPPORTED;
+#endif
+}
+
 extern "C" const char* pvt_last_error(pvt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 // ---------------------------------------------------------------- round driver
+// Host segments per task for the score pass: enough waves to fill 256 CUs (~16 per CU) when
+// the window is short, at least 4096 hosts per segment, a multiple of 8 (one XCD per
+// blockIdx % 8), capped by the segment-list scratch.
+static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
+static void choose_segments(int H, int nt, int* S_out, int* len_out) {
+  const int task_waves = (nt + TW - 1) / TW;
+  int S = (4096 + task_waves - 1) / task_waves;
+  S = std::min(S, std::max(1, H / 4096));
+  S = std::min(S, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL)));
+  S = std::max(1, std::min(S, 256));
+  if (S >= 8) S = S / 8 * 8;
+  *S_out = S;
+  *len_out = ((H + S - 1) / S + WAVE - 1) / WAVE * WAVE;
+}
 static double bytes_per_candidate(int mode) {
   // cost_aware 36 B (4 x fp64 avail + int32 zone); vbp best-fit 36 B
   // (+ host-id rank); opportunistic / vbp first-fit 32 B.
@@ -282,9 +313,8 @@ static int check_round(pvt_ctx* ctx, const pvt_round* r) {
 }
 
 static void lists_from(pvt_ctx* ctx, Lists& L) {
-  L.s = P<double>(ctx->l_s); L.tb = P<uint32_t>(ctx->l_tb); L.id = P<int32_t>(ctx->l_id);
-  L.zone = P<int32_t>(ctx->l_zone); L.a = P<double>(ctx->l_a);
-  L.cnt = P<int32_t>(ctx->l_cnt); L.complete = P<int32_t>(ctx->l_comp);
+  L.e = P<ListEntry>(ctx->l_e);
+  L.t = P<TaskRec>(ctx->l_t);
 }
 
 // Opportunistic: windows of OPP_MAXW tasks in caller order; count pass then commit walk. The
@@ -391,25 +421,21 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
   gstart.push_back(T);
   if (keyed) ENSURE(ctx->key, sizeof(double) * H);
 
-  const int W = std::max(1, std::min(ctx->window, MAX_WINDOW));
-  int S = 1;
-  while (S < MAX_SEG && (int64_t)H >= (int64_t)S * 2 * 4096) S *= 2;
-  const int seg_len = ((H + S - 1) / S + WAVE - 1) / WAVE * WAVE;
-  ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)W * S * KL);
-  ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)W * S);
-  ENSURE(ctx->l_s, sizeof(double) * (size_t)W * KL);
-  ENSURE(ctx->l_tb, sizeof(uint32_t) * (size_t)W * KL);
-  ENSURE(ctx->l_id, sizeof(int32_t) * (size_t)W * KL);
-  ENSURE(ctx->l_zone, sizeof(int32_t) * (size_t)W * KL);
-  ENSURE(ctx->l_a, sizeof(double) * 4 * (size_t)W * KL);
-  ENSURE(ctx->l_cnt, sizeof(int32_t) * W);
-  ENSURE(ctx->l_comp, sizeof(int32_t) * W);
+  // Windows adapt to how far commit walks get before a list is exhausted: a walk that stops
+  // early means the next window only needs about that many tasks (the score pass costs the
+  // same per task either way, so short windows waste less on tasks that get re-scored).
+  const int Wmax = std::max(1, std::min(ctx->window, MAX_WINDOW));
+  ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)SEG_ENTRIES_MAX);
+  ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)SEG_ENTRIES_MAX / KL);
+  ENSURE(ctx->l_e, sizeof(ListEntry) * (size_t)Wmax * KL);
+  ENSURE(ctx->l_t, sizeof(TaskRec) * (size_t)Wmax);
   ENSURE(ctx->next, sizeof(int32_t) * 4);
   Lists L;
   lists_from(ctx, L);
   const double bpc = bytes_per_candidate(r->mode);
   const double* dem_ord = P<double>(ctx->dem_ord);
   const int32_t* anc_ord = P<int32_t>(ctx->anc_ord);
+  int W = Wmax;
 
   const size_t ngroups = keyed ? ganchor.size() : 1;
   for (size_t g = 0; g < ngroups; g++) {
@@ -424,26 +450,28 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
     while (t0 < ge) {
       const int nt = std::min(W, ge - t0);
       ctx->windows++;
+      const double* dem_w = dem_ord + (size_t)t0 * 4;
       if (ordered) {
-        OrderedArgs oa{r->avail, r->zone, dem_ord + (size_t)t0 * 4, H, nt,
-                       r->mode == PVT_CA_FF ? 1 : 0, L};
+        OrderedArgs oa{r->avail, r->zone, dem_w, anc_ord + t0, H, nt, r->mode == PVT_CA_FF ? 1 : 0, L};
         Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
         launch_ordered(oa, st);
       } else {
+        int S, seg_len;
+        choose_segments(H, nt, &S, &seg_len);
         ScoreArgs sa{r->avail, r->zone, r->tiebreak, keyed ? P<double>(ctx->key) : nullptr,
-                     dem_ord + (size_t)t0 * 4, anc_ord + t0, P<double>(ctx->csum),
-                     P<double>(ctx->bsum), H, Z, nt, S, seg_len, P<SegEntry>(ctx->seg),
-                     P<int32_t>(ctx->seg_feas)};
+                     dem_w, anc_ord + t0, P<double>(ctx->csum), P<double>(ctx->bsum), H, Z, nt, S,
+                     seg_len, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
         {
           Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
           launch_score(r->mode, sa, st);
         }
-        MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, H, nt, S, L};
+        MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
+                     anc_ord + t0, H, nt, S, L};
         Scope sc(ctx, PVT_K_MERGE, 0, 0);
         launch_merge(ma, st);
       }
-      CommitArgs ca_{r->avail, dem_ord + (size_t)t0 * 4, anc_ord + t0, ord + t0, P<double>(ctx->csum),
-                     P<double>(ctx->bsum), L, H, Z, nt, r->mode, r->placement, P<int32_t>(ctx->next)};
+      CommitArgs ca_{r->avail, dem_w, ord + t0, P<double>(ctx->csum), P<double>(ctx->bsum), L, H, Z,
+                     nt, r->mode, r->placement, P<int32_t>(ctx->next), ctx->stamps};
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0);
         launch_commit(ca_, st);
@@ -455,7 +483,12 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
       const int adv = *ctx->next_host;
       if (adv < 0 || adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", adv, nt);
       if (adv == 0) return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
-      if (adv < nt) ctx->refills++;
+      if (adv < nt) {
+        ctx->refills++;
+        W = std::max(std::min(64, Wmax), std::min(Wmax, adv + adv / 2));
+      } else if (nt == W) {
+        W = std::min(Wmax, 2 * W);
+      }
       t0 += adv;
     }
   }

@@ -14,8 +14,8 @@ namespace pvt {
 
 constexpr int WAVE = 64;
 constexpr int KL = 64;           // candidate list length per task (one entry per lane)
-constexpr int ZMAX = 64;         // zones supported (locality.yml has 31)
-constexpr int TW = 8;            // tasks per wave in the score kernel
+constexpr int ZMAX = 32;         // zones supported (locality.yml has 31)
+constexpr int TW = 4;            // tasks per wave in the score kernel
 constexpr int WPB = 4;           // waves per score-kernel block
 constexpr int MAX_WINDOW = 2048; // tasks per window (bounded by the commit kernel's LDS)
 constexpr int HASH_BITS = 12;    // commit kernel touched-host hash: 4096 slots
@@ -29,15 +29,29 @@ struct SegEntry {    // 16 B: one candidate in a per-segment list
   int32_t id;
 };
 
-// Merged (final) candidate lists of one window, SoA over [W][KL].
+// One candidate of a merged list: 64 B, so lane j of the commit walk reads entry j with
+// four 16-B loads.
+struct ListEntry {
+  double s;           // score (sort key)
+  uint32_t tb;        // tiebreak (host-id rank for vbp best-fit, else 0)
+  int32_t id;         // host index
+  int32_t zone;
+  int32_t pad;
+  double a[4];        // snapshot availability of the host
+  double pad2;
+};
+// Per window task: demand, list size, completeness, anchor (48 B, one scalar load burst).
+struct TaskRec {
+  double d[4];
+  int32_t cnt;        // valid entries
+  int32_t complete;   // 1 if every snapshot-feasible host is in the list
+  int32_t anc;
+  int32_t pad;
+};
+// Merged (final) candidate lists of one window.
 struct Lists {
-  double* s;
-  uint32_t* tb;
-  int32_t* id;
-  int32_t* zone;
-  double* a;          // [4][W*KL] snapshot availability of the candidate host
-  int32_t* cnt;       // [W] valid entries
-  int32_t* complete;  // [W] 1 if every snapshot-feasible host is in the list
+  ListEntry* e;       // [W][KL]
+  TaskRec* t;         // [W]
 };
 
 struct ScoreArgs {
@@ -59,6 +73,8 @@ struct MergeArgs {
   const int32_t* seg_feas;
   const double* avail;
   const int32_t* zone;
+  const double* dem;      // window tasks [nt][4]
+  const int32_t* anc;     // window tasks [nt]
   int H, nt, S;
   Lists L;
 };
@@ -67,14 +83,14 @@ struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible
   const double* avail;
   const int32_t* zone;
   const double* dem;
+  const int32_t* anc;
   int H, nt, strict;
   Lists L;
 };
 
 struct CommitArgs {
   double* avail;          // global state, updated in place
-  const double* dem;      // window tasks [nt][4]
-  const int32_t* anc;
+  const double* dem;      // window tasks [nt][4] (for the window's minimum demand)
   const int32_t* ord;     // window tasks' caller indices
   const double* csum;
   const double* bsum;
@@ -82,6 +98,7 @@ struct CommitArgs {
   int H, Z, nt, mode;
   int32_t* placement;     // [T] in caller order
   int32_t* next;          // out: window-local index where the walk stopped (nt = done)
+  uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
 };
 
 struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw)

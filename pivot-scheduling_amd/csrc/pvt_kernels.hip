@@ -96,17 +96,28 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
     }
   }
 
+  // Host data for block hb is loaded one iteration ahead (register double buffer), with the
+  // index clamped instead of branching, so the loads overlap the previous block's scoring.
+  double n0 = 0, n1 = 0, n2 = 0, n3 = 0, nkey = DINF;
+  int nz = 0;
+  auto fetch = [&](int hb) {
+    const int h = min(hb + lane, hb1 - 1);
+    n0 = A.avail[h];
+    n1 = A.avail[(size_t)A.H + h];
+    n2 = A.avail[2 * (size_t)A.H + h];
+    n3 = A.avail[3 * (size_t)A.H + h];
+    if (MODE == CA_BF) nz = A.zone[h];
+    if (MODE == CA_FF) nkey = A.key[h];
+  };
+  if (hb0 < hb1) fetch(hb0);
   for (int hb = hb0; hb < hb1; hb += WAVE) {
     const int h = hb + lane;
     const bool ok = h < hb1;
-    const double a0 = ok ? A.avail[h] : -DINF;
-    const double a1 = ok ? A.avail[(size_t)A.H + h] : -DINF;
-    const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : -DINF;
-    const double a3 = ok ? A.avail[3 * (size_t)A.H + h] : -DINF;
-    int z = 0;
-    if (MODE == CA_BF) z = ok ? A.zone[h] : 0;
-    double key = DINF;
-    if (MODE == CA_FF) key = ok ? A.key[h] : DINF;
+    const double a0 = ok ? n0 : -DINF;
+    const double a1 = n1, a2 = n2, a3 = n3;
+    const int z = nz;
+    const double key = nkey;
+    if (hb + WAVE < hb1) fetch(hb + WAVE);
 #pragma unroll
     for (int k = 0; k < TW; k++) {
       const bool fit = fits<STRICT>(a0, a1, a2, a3, d0[k], d1[k], d2[k], d3[k]);
@@ -219,17 +230,26 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
     for (int stride = KL / 2; stride > 0; stride >>= 1) cswap_lane(s, t, id, stride, !(lane & stride));
   }
   const int cnt = (int)(tot < KL ? tot : KL);
-  const size_t o = (size_t)task * KL + lane;
-  A.L.s[o] = s; A.L.tb[o] = t; A.L.id[o] = id;
   const bool valid = lane < cnt;
   const int h = valid ? id : 0;
-  A.L.zone[o] = valid ? A.zone[h] : 0;
-  const size_t WK = (size_t)A.nt * KL;
-  A.L.a[o] = valid ? A.avail[h] : 0.0;
-  A.L.a[WK + o] = valid ? A.avail[(size_t)A.H + h] : 0.0;
-  A.L.a[2 * WK + o] = valid ? A.avail[2 * (size_t)A.H + h] : 0.0;
-  A.L.a[3 * WK + o] = valid ? A.avail[3 * (size_t)A.H + h] : 0.0;
-  if (lane == 0) { A.L.cnt[task] = cnt; A.L.complete[task] = tot <= KL; }
+  ListEntry e;
+  e.s = s; e.tb = t; e.id = id; e.pad = 0; e.pad2 = 0.0;
+  e.zone = valid ? A.zone[h] : 0;
+  e.a[0] = valid ? A.avail[h] : 0.0;
+  e.a[1] = valid ? A.avail[(size_t)A.H + h] : 0.0;
+  e.a[2] = valid ? A.avail[2 * (size_t)A.H + h] : 0.0;
+  e.a[3] = valid ? A.avail[3 * (size_t)A.H + h] : 0.0;
+  A.L.e[(size_t)task * KL + lane] = e;
+  if (lane < 4) {
+    double* tr = reinterpret_cast<double*>(&A.L.t[task]);
+    tr[lane] = A.dem[(size_t)task * 4 + lane];
+  }
+  if (lane == 0) {
+    A.L.t[task].cnt = cnt;
+    A.L.t[task].complete = tot <= KL;
+    A.L.t[task].anc = A.anc[task];
+    A.L.t[task].pad = 0;
+  }
 }
 
 void launch_merge(const MergeArgs& a, hipStream_t st) {
@@ -247,7 +267,6 @@ __global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
   if (task >= A.nt) return;
   const double* dp = A.dem + (size_t)task * 4;
   const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
-  const size_t WK = (size_t)A.nt * KL;
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   int cnt = 0;
   int hb = 0;
@@ -263,16 +282,20 @@ __global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
     if (fit) {
       const int pos = cnt + __popcll(m & below);
       if (pos < KL) {
-        const size_t o = (size_t)task * KL + pos;
-        A.L.s[o] = 0.0; A.L.tb[o] = 0; A.L.id[o] = h; A.L.zone[o] = A.zone[h];
-        A.L.a[o] = a0; A.L.a[WK + o] = a1; A.L.a[2 * WK + o] = a2; A.L.a[3 * WK + o] = a3;
+        ListEntry e;
+        e.s = 0.0; e.tb = 0; e.id = h; e.zone = A.zone[h]; e.pad = 0; e.pad2 = 0.0;
+        e.a[0] = a0; e.a[1] = a1; e.a[2] = a2; e.a[3] = a3;
+        A.L.e[(size_t)task * KL + pos] = e;
       }
     }
     cnt += __popcll(m);
   }
+  if (lane < 4) reinterpret_cast<double*>(&A.L.t[task])[lane] = dp[lane];
   if (lane == 0) {
-    A.L.cnt[task] = cnt < KL ? cnt : KL;
-    A.L.complete[task] = (hb >= A.H) && cnt <= KL;
+    A.L.t[task].cnt = cnt < KL ? cnt : KL;
+    A.L.t[task].complete = (hb >= A.H) && cnt <= KL;
+    A.L.t[task].anc = A.anc ? A.anc[task] : 0;
+    A.L.t[task].pad = 0;
   }
 }
 
@@ -292,14 +315,20 @@ void launch_ordered(const OrderedArgs& a, hipStream_t st) {
 // host side then starts a new window there (a refill).
 // ------------------------------------------------------------------------------------------
 constexpr int HASH_SLOTS = 1 << HASH_BITS;
+constexpr int PREFETCH = 3;      // commit walk: task lists loaded this many tasks ahead
 
 struct CommitLDS {
   int32_t hkey[HASH_SLOTS];
   int32_t hval[HASH_SLOTS];
-  int32_t tid[MAX_WINDOW];
+  int32_t tid[MAX_WINDOW];       // touched slot -> host
   int32_t tz[MAX_WINDOW];
   uint32_t ttb[MAX_WINDOW];
-  double ta[4][MAX_WINDOW];
+  int32_t live[MAX_WINDOW];      // touched slots that can still fit some window task
+  int32_t lpos[MAX_WINDOW];      // slot -> position in live (-1: dead)
+  double ta[4][MAX_WINDOW];      // current availability of touched hosts
+  double csum[ZMAX * ZMAX];
+  double bsum[ZMAX * ZMAX];
+  double lim[ZMAX];
 };
 
 __device__ __forceinline__ uint32_t hslot(int32_t id) {
@@ -321,6 +350,37 @@ __device__ __forceinline__ void hash_put(CommitLDS& S, int32_t id, int32_t v) {
   S.hval[p] = v;
 }
 
+constexpr double ZERO_ZONE = -2.0;   // lim-table marker: score is exactly 0 in this zone
+
+// One task's candidate list: this lane's entry plus the task's (uniform) record.
+struct Cand {
+  ListEntry e;
+  TaskRec t;
+};
+__device__ __forceinline__ void load_cand(const CommitArgs& A, int i, int lane, Cand& c) {
+  c.e = A.L.e[(size_t)i * KL + lane];
+  c.t = A.L.t[i];
+}
+
+#ifdef PVT_STAMPS
+// Diagnostic build only (make stamps): per-phase cycle sums of the commit walk.
+__device__ __forceinline__ uint64_t stamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP(k)                          \
+  do {                                    \
+    const uint64_t t_ = stamp();          \
+    ph[k] += t_ - tl;                     \
+    tl = t_;                              \
+  } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#endif
+
 template <int MODE>
 __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
@@ -329,19 +389,47 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
   CommitLDS& S = *reinterpret_cast<CommitLDS*>(smem);
   const int lane = lane_id();
   for (int i = lane; i < HASH_SLOTS; i += WAVE) S.hkey[i] = -1;
+  if (MODE == CA_BF)
+    for (int i = lane; i < A.Z * A.Z; i += WAVE) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
+  // Componentwise minimum demand of the window: a touched host that cannot fit it can never
+  // win again in this window, so it leaves the rescoring list.
+  double m0 = DINF, m1 = DINF, m2 = DINF, m3 = DINF;
+  if (BEST) {
+    for (int i = lane; i < A.nt; i += WAVE) {
+      const double* dp = A.dem + (size_t)i * 4;
+      m0 = fmin(m0, dp[0]); m1 = fmin(m1, dp[1]); m2 = fmin(m2, dp[2]); m3 = fmin(m3, dp[3]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      m0 = fmin(m0, __shfl_xor(m0, off)); m1 = fmin(m1, __shfl_xor(m1, off));
+      m2 = fmin(m2, __shfl_xor(m2, off)); m3 = fmin(m3, __shfl_xor(m3, off));
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
   int m = 0;               // touched hosts (uniform)
+  int nl = 0;              // live touched hosts (uniform)
   int next = A.nt;
-  const size_t WK = (size_t)A.nt * KL;
 
+#ifdef PVT_STAMPS
+  uint64_t ph[5] = {0, 0, 0, 0, 0};
+  uint64_t tl = stamp();
+#endif
+  // Lists are loaded PREFETCH tasks ahead (register ring rotated by copies).
+  Cand c0, c1, c2, cur;
+  if (0 < A.nt) load_cand(A, 0, lane, c0);
+  if (1 < A.nt) load_cand(A, 1, lane, c1);
+  if (2 < A.nt) load_cand(A, 2, lane, c2);
   for (int i = 0; i < A.nt; i++) {
-    const double* dp = A.dem + (size_t)i * 4;
-    const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
-    const int cnt = A.L.cnt[i];
-    const bool comp = A.L.complete[i] != 0;
-    const size_t o = (size_t)i * KL + lane;
+    cur = c0;
+    c0 = c1;
+    c1 = c2;
+    if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, c2);
+    const double d0 = cur.t.d[0], d1 = cur.t.d[1], d2 = cur.t.d[2], d3 = cur.t.d[3];
+    const int cnt = __builtin_amdgcn_readfirstlane(cur.t.cnt);
+    const bool comp = __builtin_amdgcn_readfirstlane(cur.t.complete) != 0;
     const bool valid = lane < cnt;
-    const int32_t eid = A.L.id[o];
-    const int slot = valid ? hash_find(S, eid) : -1;
+    STAMP(0);
+    const int slot = valid ? hash_find(S, cur.e.id) : -1;
+    STAMP(1);
 
     int w_id = -1, w_slot = -1, w_z = 0;
     uint32_t w_tb = 0;
@@ -356,54 +444,78 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
       int bl = -1;                       // lane of the untouched winner
       if (mu) {
         bl = __builtin_ctzll(mu);
-        bs = readlane_d(A.L.s[o], bl);
-        bt = readlane_u(A.L.tb[o], bl);
-        bi = readlane_i(eid, bl);
+        bs = readlane_d(cur.e.s, bl);
+        bt = readlane_u(cur.e.tb, bl);
+        bi = readlane_i(cur.e.id, bl);
       }
       int bq = -1;                       // touched slot of the winner
-      const int anc = (MODE == CA_BF) ? A.anc[i] : 0;
-      for (int q0 = 0; q0 < m; q0 += WAVE) {
-        const int q = q0 + lane;
-        double cs = DINF;
-        uint32_t ct = 0xffffffffu;
-        int32_t ci = 0x7fffffff;
-        if (q < m) {
+      STAMP(2);
+      if (nl > 0) {
+        const int anc = __builtin_amdgcn_readfirstlane(cur.t.anc);
+        double vlim = DINF;
+        if (MODE == CA_BF) {
+          if (lane < A.Z) {
+            const double c = S.csum[anc * A.Z + lane];
+            S.lim[lane] = (c == 0.0) ? ZERO_ZONE : ca_lim(bs, c, S.bsum[anc * A.Z + lane]);
+          }
+          __builtin_amdgcn_s_waitcnt(0xc07f);
+        } else {
+          vlim = vbp_lim(bs);
+        }
+        for (int q0 = 0; q0 < nl; q0 += WAVE) {
+          const int j = q0 + lane;
+          const int q = S.live[min(j, nl - 1)];
           const double a0 = S.ta[0][q], a1 = S.ta[1][q], a2 = S.ta[2][q], a3 = S.ta[3][q];
-          if (fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3)) {
-            const double r = __builtin_sqrt(norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3));
+          const int32_t tid = S.tid[q];
+          const bool fit = (j < nl) && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
+          const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
+          bool pass;
+          int z = 0;
+          if (MODE == CA_BF) {
+            z = S.tz[q];
+            const double lm = S.lim[z];
+            pass = fit && ((lm == ZERO_ZONE) ? lexless(0.0, 0u, tid, bs, bt, bi) : (s2 <= lm));
+          } else {
+            pass = fit && (s2 <= vlim);
+          }
+          if (__ballot(pass) == 0) continue;
+          double cs = DINF;
+          uint32_t ct = 0xffffffffu;
+          int32_t ci = 0x7fffffff;
+          if (pass) {
             if (MODE == CA_BF) {
-              const int z = S.tz[q];
-              cs = (A.csum[anc * A.Z + z] * r) / A.bsum[anc * A.Z + z];
+              const double c = S.csum[anc * A.Z + z];
+              // (c * r) / b as the reference computes it; c == 0 gives exactly 0
+              cs = (c == 0.0) ? 0.0 : (c * __builtin_sqrt(s2)) / S.bsum[anc * A.Z + z];
               ct = 0;
             } else {
-              cs = r;
+              cs = __builtin_sqrt(s2);
               ct = S.ttb[q];
             }
-            ci = S.tid[q];
+            ci = tid;
           }
+          int cq = q;
+          for (int off = 32; off > 0; off >>= 1) {
+            const double os = __shfl_xor(cs, off);
+            const uint32_t ot = (uint32_t)__shfl_xor((int)ct, off);
+            const int32_t oi = __shfl_xor(ci, off);
+            const int oq = __shfl_xor(cq, off);
+            if (lexless(os, ot, oi, cs, ct, ci)) { cs = os; ct = ot; ci = oi; cq = oq; }
+          }
+          if (lexless(cs, ct, ci, bs, bt, bi)) { bs = cs; bt = ct; bi = ci; bq = cq; bl = -1; }
         }
-        int cq = q;
-        for (int off = 32; off > 0; off >>= 1) {
-          const double os = __shfl_xor(cs, off);
-          const uint32_t ot = (uint32_t)__shfl_xor((int)ct, off);
-          const int32_t oi = __shfl_xor(ci, off);
-          const int oq = __shfl_xor(cq, off);
-          if (lexless(os, ot, oi, cs, ct, ci)) { cs = os; ct = ot; ci = oi; cq = oq; }
-        }
-        if (lexless(cs, ct, ci, bs, bt, bi)) { bs = cs; bt = ct; bi = ci; bq = cq; bl = -1; }
       }
-      if (bi == 0x7fffffff) continue;    // no feasible host: task waits
+      STAMP(3);
+      if (bi == 0x7fffffff) continue;    // no feasible host: the task waits
       w_id = bi;
       w_tb = bt;
       if (bq >= 0) {
         w_slot = bq;
         w0 = S.ta[0][bq]; w1 = S.ta[1][bq]; w2 = S.ta[2][bq]; w3 = S.ta[3][bq];
       } else {
-        w_z = readlane_i(A.L.zone[o], bl);
-        w0 = readlane_d(A.L.a[o], bl);
-        w1 = readlane_d(A.L.a[WK + o], bl);
-        w2 = readlane_d(A.L.a[2 * WK + o], bl);
-        w3 = readlane_d(A.L.a[3 * WK + o], bl);
+        w_z = readlane_i(cur.e.zone, bl);
+        w0 = readlane_d(cur.e.a[0], bl); w1 = readlane_d(cur.e.a[1], bl);
+        w2 = readlane_d(cur.e.a[2], bl); w3 = readlane_d(cur.e.a[3], bl);
       }
     } else {
       bool ok = false;
@@ -417,20 +529,19 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
         continue;
       }
       const int L = __builtin_ctzll(mf);
-      w_id = readlane_i(eid, L);
+      w_id = readlane_i(cur.e.id, L);
       w_slot = readlane_i(slot, L);
       if (w_slot >= 0) {
         w0 = S.ta[0][w_slot]; w1 = S.ta[1][w_slot]; w2 = S.ta[2][w_slot]; w3 = S.ta[3][w_slot];
       } else {
-        w_z = readlane_i(A.L.zone[o], L);
-        w0 = readlane_d(A.L.a[o], L);
-        w1 = readlane_d(A.L.a[WK + o], L);
-        w2 = readlane_d(A.L.a[2 * WK + o], L);
-        w3 = readlane_d(A.L.a[3 * WK + o], L);
+        w_z = readlane_i(cur.e.zone, L);
+        w0 = readlane_d(cur.e.a[0], L); w1 = readlane_d(cur.e.a[1], L);
+        w2 = readlane_d(cur.e.a[2], L); w3 = readlane_d(cur.e.a[3], L);
       }
     }
-    // commit: resc[h] -= t_demand (reference cost_aware.py:95,126; opportunistic.py:18; vbp.py:24,49)
+    // commit: resc[h] -= t_demand (cost_aware.py:95,126; vbp.py:24,49)
     const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
+    const bool alive = BEST && fits<STRICT>(n0, n1, n2, n3, m0, m1, m2, m3);
     if (w_slot < 0) {
       w_slot = m++;
       if (lane == 0) {
@@ -438,6 +549,24 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
         S.tid[w_slot] = w_id;
         S.tz[w_slot] = w_z;
         S.ttb[w_slot] = w_tb;
+        S.lpos[w_slot] = -1;
+      }
+      if (alive) {
+        if (lane == 0) { S.live[nl] = w_slot; S.lpos[w_slot] = nl; }
+        nl++;
+      }
+    } else if (BEST && !alive) {
+      // swap-remove the slot from the live list
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      const int p = __builtin_amdgcn_readfirstlane(S.lpos[w_slot]);
+      if (p >= 0) {
+        nl--;
+        if (lane == 0) {
+          const int last = S.live[nl];
+          S.live[p] = last;
+          S.lpos[last] = p;
+          S.lpos[w_slot] = -1;
+        }
       }
     }
     if (lane == 0) {
@@ -449,8 +578,14 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
       A.placement[A.ord[i]] = w_id;
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes land before the next task reads
+    STAMP(4);
   }
   if (lane == 0) *A.next = next;
+#ifdef PVT_STAMPS
+  if (lane == 0 && A.stamps)
+    for (int k = 0; k < 5; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
+  if (lane == 0 && A.stamps) atomicAdd((unsigned long long*)&A.stamps[5], (unsigned long long)A.nt);
+#endif
 }
 
 size_t commit_lds_bytes() { return sizeof(CommitLDS); }

@@ -115,11 +115,11 @@ class DeviceRound:
 class PlacementEngine:
     """One pvt_ctx on one gfx950 device."""
 
-    def __init__(self, device=0, window=0):
+    def __init__(self, device=0, window=0, lib_path=None):
         torch = _torch()
         if not torch.cuda.is_available():
             raise RuntimeError("pivot_place needs a ROCm GPU (gfx950); none is visible")
-        self.lib = load_library()
+        self.lib = load_library(lib_path)
         self.device_index = int(device)
         self.device = torch.device("cuda", self.device_index)
         ctx = ctypes.c_void_p()

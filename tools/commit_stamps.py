@@ -1,0 +1,32 @@
+#!/usr/bin/env python3
+"""Diagnostic: per-phase cycle shares of the commit walk (PVT_STAMPS build, `make stamps`).
+Read the SHARES, not the absolute time: stamps serialise the walk."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "pivot-scheduling_amd"), ROOT]
+import torch  # noqa: E402
+from pivot_place import synthetic  # noqa: E402
+from pivot_place.engine import DeviceRound, PlacementEngine  # noqa: E402
+
+mode = int(sys.argv[1]) if len(sys.argv) > 1 else 1
+H = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
+T = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
+eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "build",
+                                               "libpivot_place_stamps.so"))
+f = eng.lib.pvt_debug_commit_stamps
+f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+buf = (ctypes.c_uint64 * 6)()
+assert f(eng.ctx, buf, 6) == 0          # allocates and zeroes the device counters
+r = synthetic.make_round(mode, H, T)
+dr = DeviceRound(r, eng.device)
+eng.run(dr)
+torch.cuda.synchronize()
+assert f(eng.ctx, buf, 6) == 0
+names = ["wait-prefetch", "hash-lookup", "untouched-pick", "touched-rescore", "commit"]
+tot = sum(buf[k] for k in range(5))
+print("mode %d H=%d T=%d tasks walked=%d stats=%s" % (mode, H, T, buf[5], eng.last_stats()))
+for k in range(5):
+    print("  %-16s %6.1f%%  %8.0f cycles/task" % (names[k], 100.0 * buf[k] / tot, buf[k] / max(buf[5], 1)))
