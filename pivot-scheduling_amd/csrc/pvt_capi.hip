@@ -452,7 +452,8 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
       ctx->windows++;
       const double* dem_w = dem_ord + (size_t)t0 * 4;
       if (ordered) {
-        OrderedArgs oa{r->avail, r->zone, dem_w, anc_ord + t0, H, nt, r->mode == PVT_CA_FF ? 1 : 0, L};
+        OrderedArgs oa{r->avail, r->zone, dem_w, anc_ord + t0, ord + t0, H, nt,
+                       r->mode == PVT_CA_FF ? 1 : 0, L};
         Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
         launch_ordered(oa, st);
       } else {
@@ -466,11 +467,11 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
           launch_score(r->mode, sa, st);
         }
         MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
-                     anc_ord + t0, H, nt, S, L};
+                     anc_ord + t0, ord + t0, H, nt, S, L};
         Scope sc(ctx, PVT_K_MERGE, 0, 0);
         launch_merge(ma, st);
       }
-      CommitArgs ca_{r->avail, dem_w, ord + t0, P<double>(ctx->csum), P<double>(ctx->bsum), L, H, Z,
+      CommitArgs ca_{r->avail, dem_w, P<double>(ctx->csum), P<double>(ctx->bsum), L, H, Z,
                      nt, r->mode, r->placement, P<int32_t>(ctx->next), ctx->stamps};
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0);

@@ -17,9 +17,9 @@ constexpr int KL = 64;           // candidate list length per task (one entry pe
 constexpr int ZMAX = 32;         // zones supported (locality.yml has 31)
 constexpr int TW = 4;            // tasks per wave in the score kernel
 constexpr int WPB = 4;           // waves per score-kernel block
-constexpr int MAX_WINDOW = 2048; // tasks per window (bounded by the commit kernel's LDS)
+constexpr int MAX_WINDOW = 1024; // tasks per window (bounded by the commit kernel's LDS)
 constexpr int HASH_BITS = 12;    // commit kernel touched-host hash: 4096 slots
-constexpr int MAX_SEG = 8;       // host segments per task (one per XCD)
+constexpr int MAX_SEG = 16;      // host segments per task at a full window
 
 enum Mode { CA_FF = 0, CA_BF = 1, OPP = 2, VBP_FF = 3, VBP_BF = 4 };
 
@@ -46,7 +46,7 @@ struct TaskRec {
   int32_t cnt;        // valid entries
   int32_t complete;   // 1 if every snapshot-feasible host is in the list
   int32_t anc;
-  int32_t pad;
+  int32_t ord;        // caller index of the task (where its placement is written)
 };
 // Merged (final) candidate lists of one window.
 struct Lists {
@@ -75,6 +75,7 @@ struct MergeArgs {
   const int32_t* zone;
   const double* dem;      // window tasks [nt][4]
   const int32_t* anc;     // window tasks [nt]
+  const int32_t* ord;     // window tasks' caller indices
   int H, nt, S;
   Lists L;
 };
@@ -84,6 +85,7 @@ struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible
   const int32_t* zone;
   const double* dem;
   const int32_t* anc;
+  const int32_t* ord;
   int H, nt, strict;
   Lists L;
 };
@@ -91,7 +93,6 @@ struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible
 struct CommitArgs {
   double* avail;          // global state, updated in place
   const double* dem;      // window tasks [nt][4] (for the window's minimum demand)
-  const int32_t* ord;     // window tasks' caller indices
   const double* csum;
   const double* bsum;
   Lists L;

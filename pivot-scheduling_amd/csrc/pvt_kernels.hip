@@ -248,7 +248,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
     A.L.t[task].cnt = cnt;
     A.L.t[task].complete = tot <= KL;
     A.L.t[task].anc = A.anc[task];
-    A.L.t[task].pad = 0;
+    A.L.t[task].ord = A.ord[task];
   }
 }
 
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
     A.L.t[task].cnt = cnt < KL ? cnt : KL;
     A.L.t[task].complete = (hb >= A.H) && cnt <= KL;
     A.L.t[task].anc = A.anc ? A.anc[task] : 0;
-    A.L.t[task].pad = 0;
+    A.L.t[task].ord = A.ord[task];
   }
 }
 
@@ -323,13 +323,20 @@ struct CommitLDS {
   int32_t tid[MAX_WINDOW];       // touched slot -> host
   int32_t tz[MAX_WINDOW];
   uint32_t ttb[MAX_WINDOW];
-  int32_t live[MAX_WINDOW];      // touched slots that can still fit some window task
-  int32_t lpos[MAX_WINDOW];      // slot -> position in live (-1: dead)
+  int32_t lpos[MAX_WINDOW];      // touched slot -> position in the live list (-1: dead)
   double ta[4][MAX_WINDOW];      // current availability of touched hosts
+  // live list: touched hosts that can still fit some task of the window, stored contiguously
+  double la[4][MAX_WINDOW];
+  int32_t lid[MAX_WINDOW];
+  int32_t lz[MAX_WINDOW];
+  uint32_t ltb[MAX_WINDOW];
+  int32_t lslot[MAX_WINDOW];
   double csum[ZMAX * ZMAX];
   double bsum[ZMAX * ZMAX];
   double lim[ZMAX];
 };
+
+static_assert(sizeof(CommitLDS) <= 160 * 1024, "commit walk LDS exceeds a CU's 160 KiB");
 
 __device__ __forceinline__ uint32_t hslot(int32_t id) {
   return ((uint32_t)id * 2654435761u) >> (32 - HASH_BITS);
@@ -351,15 +358,22 @@ __device__ __forceinline__ void hash_put(CommitLDS& S, int32_t id, int32_t v) {
 }
 
 constexpr double ZERO_ZONE = -2.0;   // lim-table marker: score is exactly 0 in this zone
+constexpr int SCAN_UNROLL = 4;       // live hosts rescored per lane per loop trip
 
-// One task's candidate list: this lane's entry plus the task's (uniform) record.
+// One task's candidate list: this lane's entry, plus the task record spread over lanes 0-11
+// (a vector load, so no scalar-memory wait is ever mixed with the LDS traffic of the walk).
 struct Cand {
   ListEntry e;
-  TaskRec t;
+  int32_t tv;
 };
 __device__ __forceinline__ void load_cand(const CommitArgs& A, int i, int lane, Cand& c) {
   c.e = A.L.e[(size_t)i * KL + lane];
-  c.t = A.L.t[i];
+  c.tv = reinterpret_cast<const int32_t*>(A.L.t + i)[lane < 12 ? lane : 0];
+}
+__device__ __forceinline__ double tv_d(int32_t tv, int k) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(tv, 2 * k);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(tv, 2 * k + 1);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 #ifdef PVT_STAMPS
@@ -392,7 +406,7 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
   if (MODE == CA_BF)
     for (int i = lane; i < A.Z * A.Z; i += WAVE) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
   // Componentwise minimum demand of the window: a touched host that cannot fit it can never
-  // win again in this window, so it leaves the rescoring list.
+  // win again in this window, so it leaves the live (rescoring) list.
   double m0 = DINF, m1 = DINF, m2 = DINF, m3 = DINF;
   if (BEST) {
     for (int i = lane; i < A.nt; i += WAVE) {
@@ -404,7 +418,6 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
       m2 = fmin(m2, __shfl_xor(m2, off)); m3 = fmin(m3, __shfl_xor(m3, off));
     }
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
   int m = 0;               // touched hosts (uniform)
   int nl = 0;              // live touched hosts (uniform)
   int next = A.nt;
@@ -413,19 +426,20 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
   uint64_t ph[5] = {0, 0, 0, 0, 0};
   uint64_t tl = stamp();
 #endif
-  // Lists are loaded PREFETCH tasks ahead (register ring rotated by copies).
-  Cand c0, c1, c2, cur;
+  // Lists are loaded PREFETCH tasks ahead into a ring of register sets that is never copied
+  // (a copy would wait for the youngest load): the walk is unrolled by PREFETCH and each step
+  // refills the set it just consumed.
+  Cand c0, c1, c2;
   if (0 < A.nt) load_cand(A, 0, lane, c0);
   if (1 < A.nt) load_cand(A, 1, lane, c1);
   if (2 < A.nt) load_cand(A, 2, lane, c2);
-  for (int i = 0; i < A.nt; i++) {
-    cur = c0;
-    c0 = c1;
-    c1 = c2;
-    if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, c2);
-    const double d0 = cur.t.d[0], d1 = cur.t.d[1], d2 = cur.t.d[2], d3 = cur.t.d[3];
-    const int cnt = __builtin_amdgcn_readfirstlane(cur.t.cnt);
-    const bool comp = __builtin_amdgcn_readfirstlane(cur.t.complete) != 0;
+  // step(cur, i): walk task i; returns true when the walk must stop (refill).
+  auto step = [&](Cand& cur, const int i) -> bool {
+    const double d0 = tv_d(cur.tv, 0), d1 = tv_d(cur.tv, 1), d2 = tv_d(cur.tv, 2), d3 = tv_d(cur.tv, 3);
+    const int cnt = __builtin_amdgcn_readlane(cur.tv, 8);
+    const bool comp = __builtin_amdgcn_readlane(cur.tv, 9) != 0;
+    const int anc = __builtin_amdgcn_readlane(cur.tv, 10);
+    const int caller = __builtin_amdgcn_readlane(cur.tv, 11);
     const bool valid = lane < cnt;
     STAMP(0);
     const int slot = valid ? hash_find(S, cur.e.id) : -1;
@@ -437,7 +451,10 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
 
     if (BEST) {
       const uint64_t mu = __ballot(valid && slot < 0);
-      if (mu == 0 && !comp) { next = i; break; }
+      // Every entry touched and hosts missing from the list: the untouched hosts outside the
+      // list all rank after the last entry, so a touched host that beats that entry still wins
+      // exactly; only if none does must the walk stop for a refill.
+      const bool exhausted = (mu == 0) && !comp;
       double bs = DINF;
       uint32_t bt = 0xffffffffu;
       int32_t bi = 0x7fffffff;
@@ -447,54 +464,68 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
         bs = readlane_d(cur.e.s, bl);
         bt = readlane_u(cur.e.tb, bl);
         bi = readlane_i(cur.e.id, bl);
+      } else if (exhausted) {
+        bs = readlane_d(cur.e.s, KL - 1);
+        bt = readlane_u(cur.e.tb, KL - 1);
+        bi = readlane_i(cur.e.id, KL - 1);
       }
-      int bq = -1;                       // touched slot of the winner
+      int bq = -1;                       // live position of the winner
       STAMP(2);
       if (nl > 0) {
-        const int anc = __builtin_amdgcn_readfirstlane(cur.t.anc);
         double vlim = DINF;
         if (MODE == CA_BF) {
           if (lane < A.Z) {
             const double c = S.csum[anc * A.Z + lane];
             S.lim[lane] = (c == 0.0) ? ZERO_ZONE : ca_lim(bs, c, S.bsum[anc * A.Z + lane]);
           }
-          __builtin_amdgcn_s_waitcnt(0xc07f);
         } else {
           vlim = vbp_lim(bs);
         }
-        for (int q0 = 0; q0 < nl; q0 += WAVE) {
-          const int j = q0 + lane;
-          const int q = S.live[min(j, nl - 1)];
-          const double a0 = S.ta[0][q], a1 = S.ta[1][q], a2 = S.ta[2][q], a3 = S.ta[3][q];
-          const int32_t tid = S.tid[q];
-          const bool fit = (j < nl) && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
-          const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
-          bool pass;
-          int z = 0;
-          if (MODE == CA_BF) {
-            z = S.tz[q];
-            const double lm = S.lim[z];
-            pass = fit && ((lm == ZERO_ZONE) ? lexless(0.0, 0u, tid, bs, bt, bi) : (s2 <= lm));
-          } else {
-            pass = fit && (s2 <= vlim);
+        for (int q0 = 0; q0 < nl; q0 += WAVE * SCAN_UNROLL) {
+          double s2[SCAN_UNROLL];
+          bool pass[SCAN_UNROLL];
+          int z[SCAN_UNROLL];
+          bool any = false;
+#pragma unroll
+          for (int u = 0; u < SCAN_UNROLL; u++) {
+            const int j = q0 + u * WAVE + lane;
+            const int jj = min(j, nl - 1);
+            const double a0 = S.la[0][jj], a1 = S.la[1][jj], a2 = S.la[2][jj], a3 = S.la[3][jj];
+            const bool fit = (j < nl) && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
+            s2[u] = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
+            if (MODE == CA_BF) {
+              z[u] = S.lz[jj];
+              const double lm = S.lim[z[u]];
+              pass[u] = fit && ((lm == ZERO_ZONE) ? lexless(0.0, 0u, S.lid[jj], bs, bt, bi) : (s2[u] <= lm));
+            } else {
+              z[u] = 0;
+              pass[u] = fit && (s2[u] <= vlim);
+            }
+            any |= pass[u];
           }
-          if (__ballot(pass) == 0) continue;
+          if (__ballot(any) == 0) continue;
           double cs = DINF;
           uint32_t ct = 0xffffffffu;
           int32_t ci = 0x7fffffff;
-          if (pass) {
+          int cq = -1;
+#pragma unroll
+          for (int u = 0; u < SCAN_UNROLL; u++) {
+            if (!pass[u]) continue;
+            const int j = q0 + u * WAVE + lane;
+            double sc;
+            uint32_t tb;
             if (MODE == CA_BF) {
-              const double c = S.csum[anc * A.Z + z];
+              const double c = S.csum[anc * A.Z + z[u]];
               // (c * r) / b as the reference computes it; c == 0 gives exactly 0
-              cs = (c == 0.0) ? 0.0 : (c * __builtin_sqrt(s2)) / S.bsum[anc * A.Z + z];
-              ct = 0;
+              sc = (c == 0.0) ? 0.0 : (c * __builtin_sqrt(s2[u])) / S.bsum[anc * A.Z + z[u]];
+              tb = 0;
             } else {
-              cs = __builtin_sqrt(s2);
-              ct = S.ttb[q];
+              sc = __builtin_sqrt(s2[u]);
+              tb = S.ltb[j];
             }
-            ci = tid;
+            const int32_t id = S.lid[j];
+            if (lexless(sc, tb, id, cs, ct, ci)) { cs = sc; ct = tb; ci = id; cq = j; }
           }
-          int cq = q;
           for (int off = 32; off > 0; off >>= 1) {
             const double os = __shfl_xor(cs, off);
             const uint32_t ot = (uint32_t)__shfl_xor((int)ct, off);
@@ -506,12 +537,16 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
         }
       }
       STAMP(3);
-      if (bi == 0x7fffffff) continue;    // no feasible host: the task waits
+      if (exhausted && bq < 0) { next = i; return true; }
+      if (bi == 0x7fffffff) {            // no feasible host: the task waits
+        if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
+        return false;
+      }
       w_id = bi;
       w_tb = bt;
       if (bq >= 0) {
-        w_slot = bq;
-        w0 = S.ta[0][bq]; w1 = S.ta[1][bq]; w2 = S.ta[2][bq]; w3 = S.ta[3][bq];
+        w_slot = S.lslot[bq];
+        w0 = S.la[0][bq]; w1 = S.la[1][bq]; w2 = S.la[2][bq]; w3 = S.la[3][bq];
       } else {
         w_z = readlane_i(cur.e.zone, bl);
         w0 = readlane_d(cur.e.a[0], bl); w1 = readlane_d(cur.e.a[1], bl);
@@ -525,8 +560,9 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
       }
       const uint64_t mf = __ballot(ok);
       if (mf == 0) {
-        if (!comp) { next = i; break; }
-        continue;
+        if (!comp) { next = i; return true; }
+        if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
+        return false;
       }
       const int L = __builtin_ctzll(mf);
       w_id = readlane_i(cur.e.id, L);
@@ -541,7 +577,6 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
     }
     // commit: resc[h] -= t_demand (cost_aware.py:95,126; vbp.py:24,49)
     const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
-    const bool alive = BEST && fits<STRICT>(n0, n1, n2, n3, m0, m1, m2, m3);
     if (w_slot < 0) {
       w_slot = m++;
       if (lane == 0) {
@@ -551,22 +586,29 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
         S.ttb[w_slot] = w_tb;
         S.lpos[w_slot] = -1;
       }
-      if (alive) {
-        if (lane == 0) { S.live[nl] = w_slot; S.lpos[w_slot] = nl; }
-        nl++;
-      }
-    } else if (BEST && !alive) {
-      // swap-remove the slot from the live list
-      __builtin_amdgcn_s_waitcnt(0xc07f);
+    }
+    if (BEST) {
+      const bool alive = fits<STRICT>(n0, n1, n2, n3, m0, m1, m2, m3);
       const int p = __builtin_amdgcn_readfirstlane(S.lpos[w_slot]);
-      if (p >= 0) {
-        nl--;
+      if (alive) {
+        const int q = (p >= 0) ? p : nl++;
         if (lane == 0) {
-          const int last = S.live[nl];
-          S.live[p] = last;
-          S.lpos[last] = p;
-          S.lpos[w_slot] = -1;
+          S.la[0][q] = n0; S.la[1][q] = n1; S.la[2][q] = n2; S.la[3][q] = n3;
+          if (p < 0) {
+            S.lid[q] = w_id; S.lz[q] = S.tz[w_slot]; S.ltb[q] = w_tb; S.lslot[q] = w_slot;
+            S.lpos[w_slot] = q;
+          }
         }
+      } else if (p >= 0) {               // swap-remove from the live list
+        nl--;
+        if (lane == 0 && p != nl) {
+          S.la[0][p] = S.la[0][nl]; S.la[1][p] = S.la[1][nl];
+          S.la[2][p] = S.la[2][nl]; S.la[3][p] = S.la[3][nl];
+          S.lid[p] = S.lid[nl]; S.lz[p] = S.lz[nl]; S.ltb[p] = S.ltb[nl];
+          S.lslot[p] = S.lslot[nl];
+          S.lpos[S.lslot[nl]] = p;
+        }
+        if (lane == 0) S.lpos[w_slot] = -1;
       }
     }
     if (lane == 0) {
@@ -575,10 +617,19 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
       A.avail[(size_t)A.H + w_id] = n1;
       A.avail[2 * (size_t)A.H + w_id] = n2;
       A.avail[3 * (size_t)A.H + w_id] = n3;
-      A.placement[A.ord[i]] = w_id;
+      A.placement[caller] = w_id;
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes land before the next task reads
     STAMP(4);
+    if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
+    return false;
+  };
+  for (int i = 0; i < A.nt;) {
+    if (step(c0, i)) break;
+    if (++i >= A.nt) break;
+    if (step(c1, i)) break;
+    if (++i >= A.nt) break;
+    if (step(c2, i)) break;
+    ++i;
   }
   if (lane == 0) *A.next = next;
 #ifdef PVT_STAMPS

@@ -96,6 +96,8 @@ struct OppLDS {
   uint32_t mt[625];
 };
 
+static_assert(sizeof(OppLDS) <= 160 * 1024, "opportunistic walk LDS exceeds a CU's 160 KiB");
+
 __device__ __forceinline__ uint32_t ohslot(int32_t id) {
   return ((uint32_t)id * 2654435761u) >> (32 - OPP_HASH_BITS);
 }

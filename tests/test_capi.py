@@ -1,0 +1,77 @@
+"""The C-ABI library loads and exports every symbol include/pivot_place.h declares (no GPU
+needed: nothing here launches a kernel), and the struct mirrors agree with the header."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from pivot_place import _abi, engine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pivot_place.h")
+
+
+def _declared_functions():
+    text = open(HEADER).read()
+    return re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(pvt_\w+)\s*\(", text, flags=re.M)
+
+
+def test_header_declares_the_abi():
+    names = set(_declared_functions())
+    assert {"pvt_ctx_create", "pvt_ctx_destroy", "pvt_place", "pvt_last_error"} <= names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = engine.load_library()
+    for name in _declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.pvt_abi_version() == _abi.PVT_ABI_VERSION
+
+
+def test_constants_match_header():
+    text = open(HEADER).read()
+    for name in ("PVT_OK", "PVT_EINVAL", "PVT_ENODEV", "PVT_EHIP", "PVT_ENOMEM", "PVT_EUNSUPPORTED",
+                 "PVT_ABI_VERSION"):
+        m = re.search(r"#define\s+%s\s+(-?\d+)" % name, text)
+        assert m and int(m.group(1)) == getattr(_abi, name), name
+    enum = re.search(r"enum pvt_mode \{(.*?)\};", text, flags=re.S).group(1)
+    for name in ("PVT_CA_FF", "PVT_CA_BF", "PVT_OPP", "PVT_VBP_FF", "PVT_VBP_BF"):
+        assert int(re.search(r"%s\s*=\s*(\d+)" % name, enum).group(1)) == getattr(_abi, name)
+
+
+def test_round_struct_layout_matches_header():
+    text = open(HEADER).read()
+    body = re.search(r"typedef struct pvt_round \{(.*?)\} pvt_round;", text, flags=re.S).group(1)
+    fields = re.findall(r"\b(\w+);", body)
+    assert fields == [f for f, _ in _abi.pvt_round._fields_]
+    assert ctypes.sizeof(_abi.pvt_round) == 8 * 4 + 12 * 8
+
+
+def test_null_arguments_are_rejected_without_a_device():
+    lib = engine.load_library()
+    assert lib.pvt_place(None, None) == _abi.PVT_EINVAL
+    assert lib.pvt_ctx_destroy(None) == _abi.PVT_EINVAL
+    assert lib.pvt_ctx_create(0, None) == _abi.PVT_EINVAL
+
+
+def test_no_device_means_enodev():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    lib = engine.load_library()
+    ctx = ctypes.c_void_p()
+    assert lib.pvt_ctx_create(0, ctypes.byref(ctx)) == _abi.PVT_ENODEV
+
+
+def test_engine_refuses_to_run_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    with pytest.raises(RuntimeError):
+        engine.PlacementEngine(0)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(OSError):
+        engine.load_library(str(tmp_path / "libpivot_place.so"))

@@ -1,0 +1,72 @@
+"""The drop-in policies (pivot_place.policies) against the reference's recorded schedule() runs.
+
+These tests exercise the Python side of the boundary exactly as the reference's round loop
+calls it (scheduler/__init__.py:100-103): _update_resource_info(), then schedule(ready_q).
+They check placements, the returned task order, the snapshot arrays mutated in place, the
+RandomState advanced by exactly the reference's draws, and the reference's error behaviour.
+
+The CPU variant swaps the engine for the CPU restatement (a test double with the same
+``place()`` contract) to check the host logic (grouping, anchors, RNG, marshalling) without a
+GPU; the gpu variant runs the real HIP engine.
+"""
+import numpy as np
+import pytest
+
+import fakes
+import golden_io
+from oracle import oracle
+from pivot_place import policies
+
+
+class OracleEngine:
+    """Test double: the CPU restatement behind PlacementEngine.place()'s contract."""
+
+    def place(self, r):
+        return oracle.place(r)
+
+
+CLASSES = {
+    "cost_aware": policies.CostAwareGlobalScheduler,
+    "opportunistic": policies.OpportunisticGlobalScheduler,
+    "vbp_ff": policies.FirstFitGlobalScheduler,
+    "vbp_bf": policies.BestFitGlobalScheduler,
+}
+
+
+def _run(name, idx, engine):
+    case = golden_io.load(name)
+    run = case["runs"][idx]
+    cluster, tasks = fakes.build(case)
+    sched = CLASSES[run["policy"]](None, cluster, seed=run["seed"], **run["kwargs"])
+    sched.engine = engine
+    sched._update_resource_info()
+    resc = sched.resource_info
+    err = None
+    try:
+        out = sched.schedule(list(tasks))
+    except Exception as e:   # the reference's own failure modes (cost_aware.py:26,81)
+        err = type(e).__name__
+        out = []
+    assert err == run["error"]
+    hidx = {h.id: i for i, h in enumerate(cluster.hosts)}
+    placement = np.array([-1 if t.placement is None else hidx[t.placement] for t in tasks])
+    np.testing.assert_array_equal(placement, np.array(run["placement"]))
+    pos = {id(t): i for i, t in enumerate(tasks)}
+    assert [pos[id(t)] for t in out] == run["order"]
+    after = np.array([resc[h.id] for h in cluster.hosts], dtype=np.float64).T
+    _, _, avail, _ = golden_io.expected(case, run)
+    assert np.array_equal(after, avail)
+    st = sched.randomizer.get_state()
+    ref = golden_io.mt_state(run["seed"], run["rng_draws"])
+    assert list(st[1]) == list(ref[:624]) and st[2] == ref[624]
+
+
+@pytest.mark.parametrize("name,idx", golden_io.all_runs(skip_errors=False))
+def test_policy_host_logic(name, idx):
+    _run(name, idx, OracleEngine())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,idx", golden_io.all_runs(skip_errors=False))
+def test_policy_on_engine(engine, name, idx):
+    _run(name, idx, engine)
