@@ -49,7 +49,7 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_e, l_t, next, opp;
+      seg, seg_feas, l_e, l_ids, l_t, next, opp;
   int32_t* next_host = nullptr;   // pinned
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
 };
@@ -165,7 +165,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   harvest(ctx);
   Buf* bufs[] = {&ctx->ord, &ctx->ord2, &ctx->keys64a, &ctx->keys64b, &ctx->keys32a, &ctx->keys32b,
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
-                 &ctx->seg, &ctx->seg_feas, &ctx->l_e, &ctx->l_t, &ctx->next, &ctx->opp};
+                 &ctx->seg, &ctx->seg_feas, &ctx->l_e, &ctx->l_ids, &ctx->l_t, &ctx->next, &ctx->opp};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -213,15 +213,15 @@ extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) 
 }
 // Diagnostic (not part of the public ABI): commit-walk phase cycle sums of a PVT_STAMPS build.
 extern "C" int pvt_debug_commit_stamps(pvt_ctx* ctx, uint64_t* out, int n) {
-  if (!ctx || !out || n < 6) return PVT_EINVAL;
+  if (!ctx || !out || n < 7) return PVT_EINVAL;
 #ifdef PVT_STAMPS
   if (!ctx->stamps) {
     if (hipMalloc((void**)&ctx->stamps, 64) != hipSuccess) return PVT_ENOMEM;
     (void)hipMemset(ctx->stamps, 0, 64);
-    std::memset(out, 0, sizeof(uint64_t) * 6);
+    std::memset(out, 0, sizeof(uint64_t) * 7);
     return PVT_OK;
   }
-  if (hipMemcpy(out, ctx->stamps, 48, hipMemcpyDeviceToHost) != hipSuccess) return PVT_EHIP;
+  if (hipMemcpy(out, ctx->stamps, 56, hipMemcpyDeviceToHost) != hipSuccess) return PVT_EHIP;
   return PVT_OK;
 #else
   return PVT_EUNSUPPORTED;
@@ -314,6 +314,7 @@ static int check_round(pvt_ctx* ctx, const pvt_round* r) {
 
 static void lists_from(pvt_ctx* ctx, Lists& L) {
   L.e = P<ListEntry>(ctx->l_e);
+  L.ids = P<int32_t>(ctx->l_ids);
   L.t = P<TaskRec>(ctx->l_t);
 }
 
@@ -331,10 +332,10 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord),
                       P<int32_t>(ctx->anc_ord), st);
-  const size_t cc_bytes = ((sizeof(uint16_t) * (size_t)nq * W + 255) / 256) * 256;
-  ENSURE(ctx->opp, cc_bytes + sizeof(int32_t) * (size_t)nsq * W + sizeof(uint32_t) * 640);
-  uint16_t* cc = reinterpret_cast<uint16_t*>(ctx->opp.p);
-  int32_t* sc = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ctx->opp.p) + cc_bytes);
+  const size_t bm_bytes = sizeof(uint64_t) * 4 * (size_t)nq * W;
+  ENSURE(ctx->opp, bm_bytes + sizeof(int32_t) * (size_t)nsq * W + sizeof(uint32_t) * 640);
+  uint64_t* bm = reinterpret_cast<uint64_t*>(ctx->opp.p);
+  int32_t* sc = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ctx->opp.p) + bm_bytes);
   uint32_t* mt = reinterpret_cast<uint32_t*>(sc + (size_t)nsq * W);
   HIPCHK(hipMemcpyAsync(mt, r->mt_state, sizeof(uint32_t) * 625, hipMemcpyHostToDevice, st));
   const double bpc = bytes_per_candidate(r->mode);
@@ -342,12 +343,12 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
     const int nt = std::min(W, T - t0);
     ctx->windows++;
     OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, S, seg_sup, nq, nsq, W,
-                    cc, sc};
+                    bm, sc};
     {
       Scope s(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
       launch_opp_count(ca, st);
     }
-    OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, cc, sc, H, nt, nq, nsq, W,
+    OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm, sc, H, nt, nq, nsq, W,
                      r->placement + t0, mt};
     Scope s(ctx, PVT_K_COMMIT, 0, 0);
     launch_opp_commit(oa, st);
@@ -427,7 +428,8 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
   const int Wmax = std::max(1, std::min(ctx->window, MAX_WINDOW));
   ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)SEG_ENTRIES_MAX);
   ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)SEG_ENTRIES_MAX / KL);
-  ENSURE(ctx->l_e, sizeof(ListEntry) * (size_t)Wmax * KL);
+  ENSURE(ctx->l_e, sizeof(ListEntry) * (size_t)Wmax * LMAX);
+  ENSURE(ctx->l_ids, sizeof(int32_t) * (size_t)Wmax * LMAX);
   ENSURE(ctx->l_t, sizeof(TaskRec) * (size_t)Wmax);
   ENSURE(ctx->next, sizeof(int32_t) * 4);
   Lists L;

@@ -40,17 +40,24 @@ struct ListEntry {
   double a[4];        // snapshot availability of the host
   double pad2;
 };
-// Per window task: demand, list size, completeness, anchor (48 B, one scalar load burst).
+// Per window task (64 B, read by lanes 0-15 of the commit walk with one vector load).
 struct TaskRec {
   double d[4];
-  int32_t cnt;        // valid entries
+  int32_t cnt;        // valid entries (<= LMAX)
   int32_t complete;   // 1 if every snapshot-feasible host is in the list
   int32_t anc;
   int32_t ord;        // caller index of the task (where its placement is written)
+  double bs;          // bound: every snapshot-feasible host NOT in the list has
+  uint32_t btb;       //   (score, tiebreak, host) >= (bs, btb, bid)
+  int32_t bid;
 };
-// Merged (final) candidate lists of one window.
+// Merged (final) candidate lists of one window: the exact top-cnt hosts of each task, up to
+// LMAX of them (the union of the segment lists is exact below the smallest last entry of an
+// incomplete segment list).
+constexpr int LMAX = 1024;
 struct Lists {
-  ListEntry* e;       // [W][KL]
+  ListEntry* e;       // [W][LMAX]
+  int32_t* ids;       // [W][LMAX] host index of each entry (compact copy for deep searches)
   TaskRec* t;         // [W]
 };
 

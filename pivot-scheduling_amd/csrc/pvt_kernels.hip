@@ -196,64 +196,128 @@ void launch_score(int mode, const ScoreArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Merge: one wave per task folds the S segment lists into one sorted top-KL list (bitonic
-// merge of two sorted 64-lists), then gathers each candidate's zone and snapshot availability.
+// Merge: one 256-thread block per task sorts the S segment lists (16 at a time, 1024 entries,
+// bitonic in LDS) into a running top-LMAX. Each segment list holds its segment's exact top-KL,
+// so the union is exact below B = the smallest last entry of a segment that has more than KL
+// feasible hosts: the merged list keeps the entries below B (at most LMAX) and records the
+// bound, so the commit walk knows which hosts can be missing. Zone and snapshot availability
+// of every kept host are gathered for the walk.
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ void cswap_lane(double& s, uint32_t& t, int32_t& i, int stride,
-                                           bool keep_min) {
-  const double os = __shfl_xor(s, stride);
-  const uint32_t ot = (uint32_t)__shfl_xor((int)t, stride);
-  const int32_t oi = __shfl_xor(i, stride);
-  const bool other_less = lexless(os, ot, oi, s, t, i);
-  if (other_less == keep_min) { s = os; t = ot; i = oi; }
+struct Key {
+  double s;
+  uint32_t tb;
+  int32_t id;
+};
+__device__ __forceinline__ bool kless(const Key& a, const Key& b) { return lexless(a.s, a.tb, a.id, b.s, b.tb, b.id); }
+
+__device__ __forceinline__ void bitonic_sort_lds(Key* v, int n, int tid, int nthreads) {
+  for (int size = 2; size <= n; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < n / 2; t += nthreads) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const Key a = v[lo], b = v[hi];
+        if (kless(b, a) == up) { v[lo] = b; v[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
 }
 
 __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
-  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int task = blockIdx.x * 4 + wave;
-  if (task >= A.nt) return;
-  double s = DINF;
-  uint32_t t = 0xffffffffu;
-  int32_t id = 0x7fffffff;
-  int64_t tot = 0;
-  for (int g = 0; g < A.S; g++) {
-    const size_t row = (size_t)task * A.S + g;
-    const SegEntry e = A.seg[row * KL + lane];
-    tot += A.seg_feas[row];
-    if (g == 0) { s = e.s; t = e.tb; id = e.id; continue; }
-    // reversed second list, elementwise min -> bitonic sequence of the KL smallest
-    const double rs = __shfl(e.s, KL - 1 - lane);
-    const uint32_t rt = (uint32_t)__shfl((int)e.tb, KL - 1 - lane);
-    const int32_t ri = __shfl(e.id, KL - 1 - lane);
-    if (lexless(rs, rt, ri, s, t, id)) { s = rs; t = rt; id = ri; }
-#pragma unroll
-    for (int stride = KL / 2; stride > 0; stride >>= 1) cswap_lane(s, t, id, stride, !(lane & stride));
+  constexpr int BATCH = LMAX / KL;     // segment lists per sort batch
+  __shared__ Key run[LMAX];
+  __shared__ Key buf[LMAX];
+  __shared__ Key bound;
+  __shared__ long long tot;
+  __shared__ int cnt_sh;
+  const int task = blockIdx.x, tid = threadIdx.x;
+  const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
+  for (int j = tid; j < LMAX; j += 256) run[j] = inv;
+  if (tid == 0) { bound = inv; tot = 0; cnt_sh = 0; }
+  __syncthreads();
+  for (int g0 = 0; g0 < A.S; g0 += BATCH) {
+    for (int e = tid; e < LMAX; e += 256) {
+      const int g = g0 + e / KL;
+      Key k = inv;
+      if (g < A.S) {
+        const SegEntry se = A.seg[((size_t)task * A.S + g) * KL + (e % KL)];
+        k = {se.s, se.tb, se.id};
+      }
+      buf[e] = k;
+    }
+    if (tid == 0) {
+      for (int g = g0; g < min(A.S, g0 + BATCH); g++) {
+        const int f = A.seg_feas[(size_t)task * A.S + g];
+        tot += f;
+        if (f > KL) {
+          const SegEntry se = A.seg[((size_t)task * A.S + g) * KL + KL - 1];
+          const Key k = {se.s, se.tb, se.id};
+          if (kless(k, bound)) bound = k;
+        }
+      }
+    }
+    __syncthreads();
+    bitonic_sort_lds(buf, LMAX, tid, 256);
+    // keep the LMAX smallest of run (ascending) and buf (ascending): elementwise min against the
+    // reversed buf gives a bitonic sequence, then a bitonic merge sorts it
+    for (int j = tid; j < LMAX; j += 256) {
+      const Key b = buf[LMAX - 1 - j];
+      if (kless(b, run[j])) run[j] = b;
+    }
+    __syncthreads();
+    for (int stride = LMAX / 2; stride > 0; stride >>= 1) {
+      for (int t = tid; t < LMAX / 2; t += 256) {
+        const int lo = 2 * t - (t & (stride - 1));
+        const int hi = lo + stride;
+        const Key a = run[lo], b = run[hi];
+        if (kless(b, a)) { run[lo] = b; run[hi] = a; }
+      }
+      __syncthreads();
+    }
   }
-  const int cnt = (int)(tot < KL ? tot : KL);
-  const bool valid = lane < cnt;
-  const int h = valid ? id : 0;
-  ListEntry e;
-  e.s = s; e.tb = t; e.id = id; e.pad = 0; e.pad2 = 0.0;
-  e.zone = valid ? A.zone[h] : 0;
-  e.a[0] = valid ? A.avail[h] : 0.0;
-  e.a[1] = valid ? A.avail[(size_t)A.H + h] : 0.0;
-  e.a[2] = valid ? A.avail[2 * (size_t)A.H + h] : 0.0;
-  e.a[3] = valid ? A.avail[3 * (size_t)A.H + h] : 0.0;
-  A.L.e[(size_t)task * KL + lane] = e;
-  if (lane < 4) {
+  // kept entries: valid and below the bound
+  int c = 0;
+  for (int j = tid; j < LMAX; j += 256) c += (run[j].id != 0x7fffffff) && kless(run[j], bound);
+  atomicAdd(&cnt_sh, c);
+  __syncthreads();
+  const int cnt = cnt_sh;
+  const bool complete = (bound.id == 0x7fffffff) && tot <= LMAX;
+  Key bnd = bound;
+  if (cnt == LMAX && kless(run[LMAX - 1], bnd)) bnd = run[LMAX - 1];
+  for (int j = tid; j < LMAX; j += 256) {
+    ListEntry e;
+    const Key k = run[j];
+    const bool valid = j < cnt;
+    const int h = valid ? k.id : 0;
+    e.s = k.s; e.tb = k.tb; e.id = k.id; e.pad = 0; e.pad2 = 0.0;
+    e.zone = valid ? A.zone[h] : 0;
+    e.a[0] = valid ? A.avail[h] : 0.0;
+    e.a[1] = valid ? A.avail[(size_t)A.H + h] : 0.0;
+    e.a[2] = valid ? A.avail[2 * (size_t)A.H + h] : 0.0;
+    e.a[3] = valid ? A.avail[3 * (size_t)A.H + h] : 0.0;
+    if (valid || j < KL) {
+      A.L.e[(size_t)task * LMAX + j] = e;
+      A.L.ids[(size_t)task * LMAX + j] = valid ? k.id : 0x7fffffff;
+    }
+  }
+  if (tid < 4) {
     double* tr = reinterpret_cast<double*>(&A.L.t[task]);
-    tr[lane] = A.dem[(size_t)task * 4 + lane];
+    tr[tid] = A.dem[(size_t)task * 4 + tid];
   }
-  if (lane == 0) {
-    A.L.t[task].cnt = cnt;
-    A.L.t[task].complete = tot <= KL;
-    A.L.t[task].anc = A.anc[task];
-    A.L.t[task].ord = A.ord[task];
+  if (tid == 0) {
+    TaskRec& r = A.L.t[task];
+    r.cnt = cnt;
+    r.complete = complete;
+    r.anc = A.anc[task];
+    r.ord = A.ord[task];
+    r.bs = bnd.s; r.btb = bnd.tb; r.bid = bnd.id;
   }
 }
 
 void launch_merge(const MergeArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(merge_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -285,17 +349,20 @@ __global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
         ListEntry e;
         e.s = 0.0; e.tb = 0; e.id = h; e.zone = A.zone[h]; e.pad = 0; e.pad2 = 0.0;
         e.a[0] = a0; e.a[1] = a1; e.a[2] = a2; e.a[3] = a3;
-        A.L.e[(size_t)task * KL + pos] = e;
+        A.L.e[(size_t)task * LMAX + pos] = e;
+        A.L.ids[(size_t)task * LMAX + pos] = h;
       }
     }
     cnt += __popcll(m);
   }
   if (lane < 4) reinterpret_cast<double*>(&A.L.t[task])[lane] = dp[lane];
   if (lane == 0) {
-    A.L.t[task].cnt = cnt < KL ? cnt : KL;
-    A.L.t[task].complete = (hb >= A.H) && cnt <= KL;
-    A.L.t[task].anc = A.anc ? A.anc[task] : 0;
-    A.L.t[task].ord = A.ord[task];
+    TaskRec& r = A.L.t[task];
+    r.cnt = cnt < KL ? cnt : KL;
+    r.complete = (hb >= A.H) && cnt <= KL;
+    r.anc = A.anc ? A.anc[task] : 0;
+    r.ord = A.ord[task];
+    r.bs = 0.0; r.btb = 0; r.bid = 0x7fffffff;   // first-fit walks never use the bound
   }
 }
 
@@ -363,12 +430,15 @@ constexpr int SCAN_UNROLL = 4;       // live hosts rescored per lane per loop tr
 // One task's candidate list: this lane's entry, plus the task record spread over lanes 0-11
 // (a vector load, so no scalar-memory wait is ever mixed with the LDS traffic of the walk).
 struct Cand {
-  ListEntry e;
-  int32_t tv;
+  ListEntry e;                 // entry `lane` of chunk 0
+  int32_t tv;                  // TaskRec dword `lane` (lanes 0-15)
+  int32_t ids[LMAX / KL - 1];  // host ids of entries 64*c + lane, c = 1..15
 };
 __device__ __forceinline__ void load_cand(const CommitArgs& A, int i, int lane, Cand& c) {
-  c.e = A.L.e[(size_t)i * KL + lane];
-  c.tv = reinterpret_cast<const int32_t*>(A.L.t + i)[lane < 12 ? lane : 0];
+  c.e = A.L.e[(size_t)i * LMAX + lane];
+  c.tv = reinterpret_cast<const int32_t*>(A.L.t + i)[lane < 16 ? lane : 0];
+#pragma unroll
+  for (int k = 0; k < LMAX / KL - 1; k++) c.ids[k] = A.L.ids[(size_t)i * LMAX + (k + 1) * KL + lane];
 }
 __device__ __forceinline__ double tv_d(int32_t tv, int k) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(tv, 2 * k);
@@ -424,6 +494,7 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
 
 #ifdef PVT_STAMPS
   uint64_t ph[5] = {0, 0, 0, 0, 0};
+  uint64_t nl_sum = 0;
   uint64_t tl = stamp();
 #endif
   // Lists are loaded PREFETCH tasks ahead into a ring of register sets that is never copied
@@ -448,30 +519,95 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
     int w_id = -1, w_slot = -1, w_z = 0;
     uint32_t w_tb = 0;
     double w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+    // The first usable list entry: chunk 0 is in registers; deeper chunks are searched by id
+    // (LDS hash probes) and only the winning entry is then read from memory.
+    int uc = -1, ul = -1;                // chunk and lane of the first usable entry
+    {
+      const bool ok0 = BEST ? (valid && slot < 0)
+                            : (valid && (slot < 0 || fits<STRICT>(S.ta[0][max(slot, 0)], S.ta[1][max(slot, 0)],
+                                                                  S.ta[2][max(slot, 0)], S.ta[3][max(slot, 0)],
+                                                                  d0, d1, d2, d3)));
+      const uint64_t m0 = __ballot(ok0);
+      if (m0) {
+        uc = 0;
+        ul = __builtin_ctzll(m0);
+      } else {
+#pragma unroll
+        for (int c = 1; c < LMAX / KL; c++) {
+          if (uc < 0 && c * KL < cnt) {
+            const bool v = c * KL + lane < cnt;
+            const int sl = v ? hash_find(S, cur.ids[c - 1]) : -1;
+            const bool ok = BEST ? (v && sl < 0)
+                                 : (v && (sl < 0 || fits<STRICT>(S.ta[0][max(sl, 0)], S.ta[1][max(sl, 0)],
+                                                                 S.ta[2][max(sl, 0)], S.ta[3][max(sl, 0)],
+                                                                 d0, d1, d2, d3)));
+            const uint64_t mc = __ballot(ok);
+            if (mc) { uc = c; ul = __builtin_ctzll(mc); }
+          }
+        }
+      }
+    }
+    // the usable entry's fields (uniform)
+    double us = DINF, ua0 = 0, ua1 = 0, ua2 = 0, ua3 = 0;
+    uint32_t utb = 0xffffffffu;
+    int32_t uid = 0x7fffffff, uz = 0, uslot = -1;
+    if (uc == 0) {
+      us = readlane_d(cur.e.s, ul); utb = readlane_u(cur.e.tb, ul); uid = readlane_i(cur.e.id, ul);
+      uz = readlane_i(cur.e.zone, ul); uslot = readlane_i(slot, ul);
+      ua0 = readlane_d(cur.e.a[0], ul); ua1 = readlane_d(cur.e.a[1], ul);
+      ua2 = readlane_d(cur.e.a[2], ul); ua3 = readlane_d(cur.e.a[3], ul);
+    } else if (uc > 0) {
+      const ListEntry& ue = A.L.e[(size_t)i * LMAX + uc * KL + ul];
+      us = ue.s; utb = ue.tb; uid = ue.id; uz = ue.zone;
+      ua0 = ue.a[0]; ua1 = ue.a[1]; ua2 = ue.a[2]; ua3 = ue.a[3];
+      uslot = BEST ? -1 : hash_find(S, uid);
+      uslot = __builtin_amdgcn_readfirstlane(uslot);
+    }
 
     if (BEST) {
-      const uint64_t mu = __ballot(valid && slot < 0);
-      // Every entry touched and hosts missing from the list: the untouched hosts outside the
-      // list all rank after the last entry, so a touched host that beats that entry still wins
-      // exactly; only if none does must the walk stop for a refill.
-      const bool exhausted = (mu == 0) && !comp;
-      double bs = DINF;
-      uint32_t bt = 0xffffffffu;
-      int32_t bi = 0x7fffffff;
-      int bl = -1;                       // lane of the untouched winner
-      if (mu) {
-        bl = __builtin_ctzll(mu);
-        bs = readlane_d(cur.e.s, bl);
-        bt = readlane_u(cur.e.tb, bl);
-        bi = readlane_i(cur.e.id, bl);
-      } else if (exhausted) {
-        bs = readlane_d(cur.e.s, KL - 1);
-        bt = readlane_u(cur.e.tb, KL - 1);
-        bi = readlane_i(cur.e.id, KL - 1);
+      // No untouched entry and hosts missing from the list: every untouched host outside the
+      // list ranks at or after the bound, so a touched host at or before it still wins exactly;
+      // only if none does must the walk stop for a refill. (bi = bid + 1 turns the strict
+      // comparisons below into <= bound; ids are unique, so equality means the same host.)
+      const bool exhausted = (uc < 0) && !comp;
+      double bs = us;
+      uint32_t bt = utb;
+      int32_t bi = uid;
+      if (exhausted) {
+        bs = tv_d(cur.tv, 6);
+        bt = (uint32_t)__builtin_amdgcn_readlane(cur.tv, 14);
+        bi = __builtin_amdgcn_readlane(cur.tv, 15) + 1;
       }
       int bq = -1;                       // live position of the winner
       STAMP(2);
-      if (nl > 0) {
+#ifdef PVT_STAMPS
+      nl_sum += nl;
+#endif
+      if (MODE == CA_BF && nl > 0 && bs == 0.0) {
+        // Best untouched score is exactly 0 (a zero-cost zone). A live host can only win with
+        // score 0 and a lower index: either it sits in a zero-cost zone, or its residual is
+        // exactly zero. Every such candidate scores 0, so the winner is the lowest index.
+        const uint32_t zz = (uint32_t)__ballot(lane < A.Z && S.csum[anc * A.Z + lane] == 0.0);
+        int best = 0x7fffffff, bestq = -1;
+        for (int q0 = 0; q0 < nl; q0 += WAVE * SCAN_UNROLL) {
+#pragma unroll
+          for (int u = 0; u < SCAN_UNROLL; u++) {
+            const int j = q0 + u * WAVE + lane;
+            const int jj = min(j, nl - 1);
+            const double a0 = S.la[0][jj], a1 = S.la[1][jj], a2 = S.la[2][jj], a3 = S.la[3][jj];
+            const int32_t id = S.lid[jj];
+            const bool zero_zone = (zz >> S.lz[jj]) & 1u;
+            const bool pass = (j < nl) && id < bi && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3) &&
+                              (zero_zone || (a0 == d0 && a1 == d1 && a2 == d2 && a3 == d3));
+            if (pass && id < best) { best = id; bestq = j; }
+          }
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+          const int ob = __shfl_xor(best, off), oq = __shfl_xor(bestq, off);
+          if (ob < best) { best = ob; bestq = oq; }
+        }
+        if (best < bi) { bs = 0.0; bt = 0; bi = best; bq = bestq; }
+      } else if (nl > 0) {
         double vlim = DINF;
         if (MODE == CA_BF) {
           if (lane < A.Z) {
@@ -533,12 +669,12 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
             const int oq = __shfl_xor(cq, off);
             if (lexless(os, ot, oi, cs, ct, ci)) { cs = os; ct = ot; ci = oi; cq = oq; }
           }
-          if (lexless(cs, ct, ci, bs, bt, bi)) { bs = cs; bt = ct; bi = ci; bq = cq; bl = -1; }
+          if (lexless(cs, ct, ci, bs, bt, bi)) { bs = cs; bt = ct; bi = ci; bq = cq; }
         }
       }
       STAMP(3);
       if (exhausted && bq < 0) { next = i; return true; }
-      if (bi == 0x7fffffff) {            // no feasible host: the task waits
+      if (bi == 0x7fffffff || (exhausted && bq < 0)) {   // no feasible host: the task waits
         if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
         return false;
       }
@@ -548,31 +684,22 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
         w_slot = S.lslot[bq];
         w0 = S.la[0][bq]; w1 = S.la[1][bq]; w2 = S.la[2][bq]; w3 = S.la[3][bq];
       } else {
-        w_z = readlane_i(cur.e.zone, bl);
-        w0 = readlane_d(cur.e.a[0], bl); w1 = readlane_d(cur.e.a[1], bl);
-        w2 = readlane_d(cur.e.a[2], bl); w3 = readlane_d(cur.e.a[3], bl);
+        w_z = uz;
+        w0 = ua0; w1 = ua1; w2 = ua2; w3 = ua3;
       }
     } else {
-      bool ok = false;
-      if (valid) {
-        if (slot < 0) ok = true;
-        else ok = fits<STRICT>(S.ta[0][slot], S.ta[1][slot], S.ta[2][slot], S.ta[3][slot], d0, d1, d2, d3);
-      }
-      const uint64_t mf = __ballot(ok);
-      if (mf == 0) {
+      if (uc < 0) {
         if (!comp) { next = i; return true; }
         if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
         return false;
       }
-      const int L = __builtin_ctzll(mf);
-      w_id = readlane_i(cur.e.id, L);
-      w_slot = readlane_i(slot, L);
+      w_id = uid;
+      w_slot = uslot;
       if (w_slot >= 0) {
         w0 = S.ta[0][w_slot]; w1 = S.ta[1][w_slot]; w2 = S.ta[2][w_slot]; w3 = S.ta[3][w_slot];
       } else {
-        w_z = readlane_i(cur.e.zone, L);
-        w0 = readlane_d(cur.e.a[0], L); w1 = readlane_d(cur.e.a[1], L);
-        w2 = readlane_d(cur.e.a[2], L); w3 = readlane_d(cur.e.a[3], L);
+        w_z = uz;
+        w0 = ua0; w1 = ua1; w2 = ua2; w3 = ua3;
       }
     }
     // commit: resc[h] -= t_demand (cost_aware.py:95,126; vbp.py:24,49)
@@ -636,6 +763,7 @@ __global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
   if (lane == 0 && A.stamps)
     for (int k = 0; k < 5; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
   if (lane == 0 && A.stamps) atomicAdd((unsigned long long*)&A.stamps[5], (unsigned long long)A.nt);
+  if (lane == 0 && A.stamps) atomicAdd((unsigned long long*)&A.stamps[6], (unsigned long long)nl_sum);
 #endif
 }
 

@@ -2,8 +2,8 @@
 //
 // Per task the reference lists every host with np.all(r >= d) in cluster order, draws
 // randomizer.choice(qualified) (= randint(0, n), no draw when n == 1) and commits. On the GPU:
-//   count kernel   per window task, the number of snapshot-feasible hosts in every chunk of
-//                  OPP_CH hosts and every super-chunk of OPP_SUP chunks (fused fit-mask pass)
+//   count kernel   per window task, the snapshot feasibility bitmap of every chunk of OPP_CH
+//                  hosts and the count of every super-chunk of OPP_SUP chunks (fit-mask pass)
 //   commit walk    one wave, tasks in order: n = snapshot count minus the touched hosts that
 //                  stopped fitting; MT19937 randint(n) in LDS; select the k-th currently
 //                  feasible host super-chunk -> chunk -> host; commit.
@@ -22,14 +22,14 @@ struct OppCountArgs {
   const double* avail;
   const double* dem;      // window tasks [nt][4]
   int H, nt, S, seg_sup, nq, nsq, ldc;
-  uint16_t* cc;           // [nq][ldc] chunk counts
+  uint64_t* bm;           // [nq][ldc][4] per-chunk feasibility bitmaps (bit = host)
   int32_t* sc;            // [nsq][ldc] super-chunk counts
 };
 
 struct OppCommitArgs {
   double* avail;
   const double* dem;      // window tasks [nt][4]
-  const uint16_t* cc;
+  const uint64_t* bm;
   const int32_t* sc;
   int H, nt, nq, nsq, ldc;
   int32_t* placement;     // window tasks' placements (caller order == processing order)

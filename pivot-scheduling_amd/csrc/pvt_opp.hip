@@ -19,9 +19,13 @@ namespace pvt {
 
 // ------------------------------------------------------------------------------------------
 // Count kernel: block = 4 waves, each wave OPP_TW tasks over one host segment (a run of
-// super-chunks); blockIdx % S picks the segment (XCD-affine, as in score_kernel).
+// super-chunks); blockIdx % S picks the segment (XCD-affine, as in score_kernel). For every
+// (task, 256-host chunk) it stores the chunk's feasibility bitmap (the four wave ballots,
+// 32 B) and, per super-chunk, the feasible count. A chunk's host loads are issued one chunk
+// ahead (register double buffer, clamped indices instead of branches).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
+  constexpr int U = OPP_CH / WAVE;
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int seg = blockIdx.x % A.S, tile = blockIdx.x / A.S;
   const int t0 = (tile * 4 + wave) * OPP_TW;
@@ -38,40 +42,55 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
     }
   }
   const int Q0 = seg * A.seg_sup, Q1 = min(A.nsq, Q0 + A.seg_sup);
-  for (int Q = Q0; Q < Q1; Q++) {
-    int sup[OPP_TW];
+  const int qa = Q0 * OPP_SUP, qb = min(A.nq, Q1 * OPP_SUP);
+  double n0[U], n1[U], n2[U], n3[U];
+  auto fetch = [&](int q) {
 #pragma unroll
-    for (int k = 0; k < OPP_TW; k++) sup[k] = 0;
-    const int q1 = min(A.nq, (Q + 1) * OPP_SUP);
-    for (int q = Q * OPP_SUP; q < q1; q++) {
-      int cnt[OPP_TW];
+    for (int u = 0; u < U; u++) {
+      const int h = min(q * OPP_CH + u * WAVE + lane, A.H - 1);
+      n0[u] = A.avail[h]; n1[u] = A.avail[(size_t)A.H + h];
+      n2[u] = A.avail[2 * (size_t)A.H + h]; n3[u] = A.avail[3 * (size_t)A.H + h];
+    }
+  };
+  if (qa < qb) fetch(qa);
+  int sup[OPP_TW];
 #pragma unroll
-      for (int k = 0; k < OPP_TW; k++) cnt[k] = 0;
+  for (int k = 0; k < OPP_TW; k++) sup[k] = 0;
+  for (int q = qa; q < qb; q++) {
+    double a0[U], a1[U], a2[U], a3[U];
 #pragma unroll
-      for (int u = 0; u < OPP_CH / WAVE; u++) {
-        const int h = q * OPP_CH + u * WAVE + lane;
-        const bool ok = h < A.H;
-        const double a0 = ok ? A.avail[h] : -DINF;
-        const double a1 = ok ? A.avail[(size_t)A.H + h] : -DINF;
-        const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : -DINF;
-        const double a3 = ok ? A.avail[3 * (size_t)A.H + h] : -DINF;
+    for (int u = 0; u < U; u++) {
+      const bool ok = q * OPP_CH + u * WAVE + lane < A.H;
+      a0[u] = ok ? n0[u] : -DINF; a1[u] = n1[u]; a2[u] = n2[u]; a3[u] = n3[u];
+    }
+    if (q + 1 < qb) fetch(q + 1);
+    uint64_t mine[U];
 #pragma unroll
-        for (int k = 0; k < OPP_TW; k++)
-          cnt[k] += __popcll(__ballot(fits<false>(a0, a1, a2, a3, d0[k], d1[k], d2[k], d3[k])));
+    for (int u = 0; u < U; u++) mine[u] = 0;
+#pragma unroll
+    for (int k = 0; k < OPP_TW; k++) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t b = __ballot(fits<false>(a0[u], a1[u], a2[u], a3[u], d0[k], d1[k], d2[k], d3[k]));
+        sup[k] += __popcll(b);
+        if (lane == k) mine[u] = b;
       }
+    }
+    if (lane < nt) {
+      uint64_t* o = A.bm + ((size_t)q * A.ldc + t0 + lane) * U;
+#pragma unroll
+      for (int u = 0; u < U; u++) o[u] = mine[u];
+    }
+    if ((q + 1) % OPP_SUP == 0 || q + 1 == qb) {   // super-chunk boundary
+      const int Q = q / OPP_SUP;
       int v = 0;
 #pragma unroll
       for (int k = 0; k < OPP_TW; k++) {
-        if (lane == k) v = cnt[k];
-        sup[k] += cnt[k];
+        if (lane == k) v = sup[k];
+        sup[k] = 0;
       }
-      if (lane < nt) A.cc[(size_t)q * A.ldc + t0 + lane] = (uint16_t)v;
+      if (lane < nt) A.sc[(size_t)Q * A.ldc + t0 + lane] = v;
     }
-    int v = 0;
-#pragma unroll
-    for (int k = 0; k < OPP_TW; k++)
-      if (lane == k) v = sup[k];
-    if (lane < nt) A.sc[(size_t)Q * A.ldc + t0 + lane] = v;
   }
 }
 
@@ -145,47 +164,58 @@ __device__ uint32_t mt_randint(uint32_t* st, uint32_t n) {
   return v;
 }
 
-// lost hosts among [lo, hi)
-__device__ __forceinline__ int lost_in(const OppLDS& S, int nl, int lo, int hi) {
-  int c = 0;
-  for (int j = 0; j < nl; j++) {
-    const int h = S.lost[j];
-    c += (h >= lo) & (h < hi);
+// Position of the r-th (0-based) set bit of x (r < popcount(x)).
+__device__ __forceinline__ int select_bit(uint64_t x, int r) {
+  int pos = 0;
+#pragma unroll
+  for (int w = 32; w > 0; w >>= 1) {
+    const uint64_t lo = x & ((w == 64 ? ~0ull : (1ull << w)) - 1);
+    const int c = __popcll(lo);
+    if (r >= c) { r -= c; x >>= w; pos += w; }
+    else x = lo;
   }
-  return c;
+  return pos;
 }
 
 __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
+  constexpr int U = OPP_CH / WAVE;
+  constexpr int SUPH = OPP_SUP * OPP_CH;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   OppLDS& S = *reinterpret_cast<OppLDS*>(smem);
   const int lane = lane_id();
   for (int i = lane; i < OPP_HASH; i += WAVE) S.hkey[i] = -1;
   for (int i = lane; i < 625; i += WAVE) S.mt[i] = A.mt[i];
-  __builtin_amdgcn_s_waitcnt(0xc07f);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  constexpr int SUPH = OPP_SUP * OPP_CH;
+  const bool fast = A.nsq <= WAVE;   // one super-chunk count per lane (H <= 1,048,576)
   int m = 0;
+  // super-chunk counts of the next task, prefetched (fast path)
+  int scn = (fast && A.nt > 0 && lane < A.nsq) ? A.sc[(size_t)lane * A.ldc] : 0;
 
   for (int i = 0; i < A.nt; i++) {
     const double* dp = A.dem + (size_t)i * 4;
     const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+    const int scv = scn;
+    if (fast && i + 1 < A.nt) scn = lane < A.nsq ? A.sc[(size_t)lane * A.ldc + i + 1] : 0;
     // touched hosts that fitted at the snapshot and no longer fit
     int nl = 0;
     for (int q0 = 0; q0 < m; q0 += WAVE) {
       const int q = q0 + lane;
-      bool lf = false;
-      if (q < m)
-        lf = fits<false>(S.sa[0][q], S.sa[1][q], S.sa[2][q], S.sa[3][q], d0, d1, d2, d3) &&
-             !fits<false>(S.ta[0][q], S.ta[1][q], S.ta[2][q], S.ta[3][q], d0, d1, d2, d3);
+      const int qq = min(q, m - 1);
+      const bool lf = (q < m) &&
+                      fits<false>(S.sa[0][qq], S.sa[1][qq], S.sa[2][qq], S.sa[3][qq], d0, d1, d2, d3) &&
+                      !fits<false>(S.ta[0][qq], S.ta[1][qq], S.ta[2][qq], S.ta[3][qq], d0, d1, d2, d3);
       const uint64_t b = __ballot(lf);
       if (lf) S.lost[nl + __popcll(b & below)] = S.tid[q];
       nl += __popcll(b);
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
     long long n = 0;
-    for (int Q0 = 0; Q0 < A.nsq; Q0 += WAVE) {
-      const int Q = Q0 + lane;
-      n += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)Q * A.ldc + i] : 0);
+    if (fast) {
+      n = wave_sum_ll(scv);
+    } else {
+      for (int Q0 = 0; Q0 < A.nsq; Q0 += WAVE) {
+        const int Q = Q0 + lane;
+        n += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)Q * A.ldc + i] : 0);
+      }
     }
     n -= nl;
     if (n <= 0) continue;
@@ -198,7 +228,10 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     for (int Q0 = 0; Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
       const int Q = Q0 + lane;
       int v = 0;
-      if (Q < A.nsq) v = A.sc[(size_t)Q * A.ldc + i] - lost_in(S, nl, Q * SUPH, (Q + 1) * SUPH);
+      if (Q < A.nsq) {
+        v = fast ? scv : A.sc[(size_t)Q * A.ldc + i];
+        for (int j = 0; j < nl; j++) v -= (S.lost[j] / SUPH) == Q;
+      }
       const int inc = wave_incl_scan(v);
       const int tot = __builtin_amdgcn_readlane(inc, 63);
       if ((long long)k < acc + tot) {
@@ -211,67 +244,57 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
       }
     }
     if (Qs < 0) continue;   // unreachable when counts are consistent
-    uint32_t k1 = k - (uint32_t)acc;
-    // chunk within the super-chunk
-    int qs;
-    {
-      const int q = Qs * OPP_SUP + lane;
-      int v = 0;
-      if (q < A.nq) v = (int)A.cc[(size_t)q * A.ldc + i] - lost_in(S, nl, q * OPP_CH, (q + 1) * OPP_CH);
-      const int inc = wave_incl_scan(v);
-      const uint64_t hit = __ballot(inc > (int)k1);
-      const int L = __builtin_ctzll(hit);
-      qs = Qs * OPP_SUP + L;
-      k1 -= (uint32_t)(__builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(v, L));
-    }
-    // host within the chunk: lane j covers hosts 4j .. 4j+3 of the chunk
-    double a[4][4];
-    int slot[4];
-    int f = 0, fm = 0;
+    int k1 = (int)(k - (uint32_t)acc);
+    // chunk within the super-chunk: lane = chunk, its current bitmap = snapshot bits minus lost
+    const int q = Qs * OPP_SUP + lane;
+    uint64_t bits[U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int h = qs * OPP_CH + lane * 4 + u;
-      slot[u] = -1;
-      if (h < A.H) {
-        slot[u] = ohash_find(S, h);
-        if (slot[u] >= 0) {
-          a[u][0] = S.ta[0][slot[u]]; a[u][1] = S.ta[1][slot[u]];
-          a[u][2] = S.ta[2][slot[u]]; a[u][3] = S.ta[3][slot[u]];
-        } else {
-          a[u][0] = A.avail[h]; a[u][1] = A.avail[(size_t)A.H + h];
-          a[u][2] = A.avail[2 * (size_t)A.H + h]; a[u][3] = A.avail[3 * (size_t)A.H + h];
+    for (int u = 0; u < U; u++) bits[u] = 0;
+    if (q < A.nq) {
+      const uint64_t* bp = A.bm + ((size_t)q * A.ldc + i) * U;
+#pragma unroll
+      for (int u = 0; u < U; u++) bits[u] = bp[u];
+      for (int j = 0; j < nl; j++) {
+        const int h = S.lost[j];
+        if (h / OPP_CH == q) {
+          const int o = h % OPP_CH;
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (o / WAVE == u) bits[u] &= ~(1ull << (o % WAVE));
         }
-        const bool ok = fits<false>(a[u][0], a[u][1], a[u][2], a[u][3], d0, d1, d2, d3);
-        f += ok;
-        fm |= ok << u;
-      } else {
-        a[u][0] = a[u][1] = a[u][2] = a[u][3] = 0.0;
       }
     }
-    const int inc = wave_incl_scan(f);
-    const uint64_t hit = __ballot(inc > (int)k1);
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < U; u++) c += __popcll(bits[u]);
+    const int inc = wave_incl_scan(c);
+    const uint64_t hit = __ballot(inc > k1);
     if (hit == 0) continue;   // unreachable when counts are consistent
     const int L = __builtin_ctzll(hit);
-    int r = (int)k1 - (__builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(f, L));
-    int pick = -1;
+    k1 -= __builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(c, L);
+    int off = -1;
     if (lane == L) {
-      for (int u = 0; u < 4; u++)
-        if ((fm >> u) & 1) {
-          if (r == 0) { pick = u; break; }
-          r--;
-        }
-    }
-    pick = __builtin_amdgcn_readlane(pick, L);
-    const int w = qs * OPP_CH + L * 4 + pick;
-    double w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-    int ws = 0;
+      int r = k1;
 #pragma unroll
-    for (int u = 0; u < 4; u++)
-      if (u == pick) {
-        w0 = readlane_d(a[u][0], L); w1 = readlane_d(a[u][1], L);
-        w2 = readlane_d(a[u][2], L); w3 = readlane_d(a[u][3], L);
-        ws = readlane_i(slot[u], L);
+      for (int u = 0; u < U; u++) {
+        const int cu = __popcll(bits[u]);
+        if (off < 0) {
+          if (r < cu) off = u * WAVE + select_bit(bits[u], r);
+          else r -= cu;
+        }
       }
+    }
+    off = __builtin_amdgcn_readlane(off, L);
+    const int w = (Qs * OPP_SUP + L) * OPP_CH + off;
+    int ws = ohash_find(S, w);
+    ws = __builtin_amdgcn_readfirstlane(ws);
+    double w0, w1, w2, w3;
+    if (ws >= 0) {
+      w0 = S.ta[0][ws]; w1 = S.ta[1][ws]; w2 = S.ta[2][ws]; w3 = S.ta[3][ws];
+    } else {
+      w0 = A.avail[w]; w1 = A.avail[(size_t)A.H + w];
+      w2 = A.avail[2 * (size_t)A.H + w]; w3 = A.avail[3 * (size_t)A.H + w];
+    }
     const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
     if (ws < 0) {
       ws = m++;
@@ -289,7 +312,6 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
       A.avail[3 * (size_t)A.H + w] = n3;
       A.placement[i] = w;
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
   }
   for (int i = lane; i < 625; i += WAVE) A.mt[i] = S.mt[i];
 }

@@ -18,15 +18,16 @@ eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "bu
                                                "libpivot_place_stamps.so"))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-buf = (ctypes.c_uint64 * 6)()
-assert f(eng.ctx, buf, 6) == 0          # allocates and zeroes the device counters
+buf = (ctypes.c_uint64 * 7)()
+assert f(eng.ctx, buf, 7) == 0          # allocates and zeroes the device counters
 r = synthetic.make_round(mode, H, T)
 dr = DeviceRound(r, eng.device)
 eng.run(dr)
 torch.cuda.synchronize()
-assert f(eng.ctx, buf, 6) == 0
+assert f(eng.ctx, buf, 7) == 0
 names = ["wait-prefetch", "hash-lookup", "untouched-pick", "touched-rescore", "commit"]
 tot = sum(buf[k] for k in range(5))
-print("mode %d H=%d T=%d tasks walked=%d stats=%s" % (mode, H, T, buf[5], eng.last_stats()))
+print("mode %d H=%d T=%d tasks walked=%d stats=%s mean live touched=%.1f"
+      % (mode, H, T, buf[5], eng.last_stats(), buf[6] / max(buf[5], 1)))
 for k in range(5):
     print("  %-16s %6.1f%%  %8.0f cycles/task" % (names[k], 100.0 * buf[k] / tot, buf[k] / max(buf[5], 1)))
