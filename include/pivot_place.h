@@ -14,7 +14,7 @@
  *   - scheduler/vbp.py:39-50                  PVT_VBP_BF
  *
  * The reference binds nothing natively (it is pure Python); the binding a maintainer adds is
- * a ctypes stub, shown in INTEGRATION.md and implemented in pivot_place/_lib.py.
+ * a ctypes stub, shown in INTEGRATION.md and implemented in pivot_place/engine.py + _abi.py.
  *
  * Conventions
  *   - Plain C types only. Returns PVT_OK (0) or a negative PVT_E* code; never throws.
@@ -123,7 +123,7 @@ int  pvt_place(pvt_ctx* ctx, const pvt_round* r);
 int  pvt_set_profiling(pvt_ctx* ctx, int on);
 int  pvt_reset_kstats(pvt_ctx* ctx);
 int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
-/* Tuning knobs (0 = default): candidate-list window in tasks. */
+/* Tuning knob: tasks per window (0 = the policy's default; capped at 1024). */
 int  pvt_set_window(pvt_ctx* ctx, int tasks);
 /* Counters of the last pvt_place call: windows run and refills forced by exhausted lists. */
 int  pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills);

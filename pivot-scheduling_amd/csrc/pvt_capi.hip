@@ -41,7 +41,7 @@ struct pvt_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   std::string err;
-  int window = MAX_WINDOW;
+  int window = 0;                 // 0: per-policy default
   int64_t windows = 0, refills = 0;
   bool profiling = false;
   pvt_kstats ks[PVT_K_COUNT];
@@ -202,7 +202,7 @@ extern "C" int pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out) {
 }
 extern "C" int pvt_set_window(pvt_ctx* ctx, int tasks) {
   if (!ctx || tasks < 0) return PVT_EINVAL;
-  ctx->window = tasks == 0 ? MAX_WINDOW : std::min(tasks, MAX_WINDOW);
+  ctx->window = std::min(tasks, MAX_WINDOW);
   return PVT_OK;
 }
 extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) {
@@ -213,15 +213,15 @@ extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) 
 }
 // Diagnostic (not part of the public ABI): commit-walk phase cycle sums of a PVT_STAMPS build.
 extern "C" int pvt_debug_commit_stamps(pvt_ctx* ctx, uint64_t* out, int n) {
-  if (!ctx || !out || n < 7) return PVT_EINVAL;
+  if (!ctx || !out || n < 8) return PVT_EINVAL;
 #ifdef PVT_STAMPS
   if (!ctx->stamps) {
     if (hipMalloc((void**)&ctx->stamps, 64) != hipSuccess) return PVT_ENOMEM;
     (void)hipMemset(ctx->stamps, 0, 64);
-    std::memset(out, 0, sizeof(uint64_t) * 7);
+    std::memset(out, 0, sizeof(uint64_t) * 8);
     return PVT_OK;
   }
-  if (hipMemcpy(out, ctx->stamps, 56, hipMemcpyDeviceToHost) != hipSuccess) return PVT_EHIP;
+  if (hipMemcpy(out, ctx->stamps, 64, hipMemcpyDeviceToHost) != hipSuccess) return PVT_EHIP;
   return PVT_OK;
 #else
   return PVT_EUNSUPPORTED;
@@ -323,9 +323,12 @@ static void lists_from(pvt_ctx* ctx, Lists& L) {
 static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   const int T = r->n_tasks, H = r->n_hosts;
   hipStream_t st = ctx->stream;
-  const int W = std::max(1, std::min(ctx->window, OPP_MAXW));
+  // Window: the walk rescans the window's touched hosts for every task, so short windows keep
+  // that scan short; the count pass then spreads each window over more host segments.
+  const int W = std::max(1, std::min(ctx->window > 0 ? ctx->window : OPP_WINDOW_DEFAULT, OPP_MAXW));
   const int nq = (H + OPP_CH - 1) / OPP_CH, nsq = (nq + OPP_SUP - 1) / OPP_SUP;
-  int S = std::min(MAX_SEG, nsq);
+  const int task_waves = (std::min(W, std::max(T, 1)) + OPP_TW - 1) / OPP_TW;
+  int S = std::max(1, std::min(nsq, (4096 + task_waves - 1) / task_waves));
   const int seg_sup = (nsq + S - 1) / S;
   S = (nsq + seg_sup - 1) / seg_sup;
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
@@ -349,7 +352,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
       launch_opp_count(ca, st);
     }
     OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm, sc, H, nt, nq, nsq, W,
-                     r->placement + t0, mt};
+                     r->placement + t0, mt, ctx->stamps};
     Scope s(ctx, PVT_K_COMMIT, 0, 0);
     launch_opp_commit(oa, st);
   }
@@ -425,7 +428,10 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
   // Windows adapt to how far commit walks get before a list is exhausted: a walk that stops
   // early means the next window only needs about that many tasks (the score pass costs the
   // same per task either way, so short windows waste less on tasks that get re-scored).
-  const int Wmax = std::max(1, std::min(ctx->window, MAX_WINDOW));
+  // default window: vbp best-fit walks search deeper lists as a window's touched hosts pile up
+  // at the top of every task's ranking, so its windows are shorter (bench sweep)
+  const int wdef = (r->mode == PVT_VBP_BF) ? 512 : MAX_WINDOW;
+  const int Wmax = std::max(1, std::min(ctx->window > 0 ? ctx->window : wdef, MAX_WINDOW));
   ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)SEG_ENTRIES_MAX);
   ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)SEG_ENTRIES_MAX / KL);
   ENSURE(ctx->l_e, sizeof(ListEntry) * (size_t)Wmax * LMAX);

@@ -17,6 +17,7 @@ constexpr int OPP_CH = 256;     // hosts per chunk
 constexpr int OPP_SUP = 64;     // chunks per super-chunk (16384 hosts)
 constexpr int OPP_TW = 8;       // tasks per wave in the count kernel
 constexpr int OPP_MAXW = 1024;  // tasks per window (commit-walk LDS: touched snapshot + current)
+constexpr int OPP_WINDOW_DEFAULT = 256;
 
 struct OppCountArgs {
   const double* avail;
@@ -34,6 +35,7 @@ struct OppCommitArgs {
   int H, nt, nq, nsq, ldc;
   int32_t* placement;     // window tasks' placements (caller order == processing order)
   uint32_t* mt;           // device MT19937 state: key[624], pos
+  uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
 };
 
 void launch_opp_count(const OppCountArgs& a, hipStream_t st);

@@ -103,6 +103,7 @@ void launch_opp_count(const OppCountArgs& a, hipStream_t st) {
 // Commit walk (one wave).
 // ------------------------------------------------------------------------------------------
 constexpr int OPP_HASH_BITS = 12;
+constexpr int OPP_NSQ_MAX = 1024;   // super-chunks supported: 16.7M hosts
 constexpr int OPP_HASH = 1 << OPP_HASH_BITS;
 
 struct OppLDS {
@@ -112,6 +113,8 @@ struct OppLDS {
   int32_t lost[OPP_MAXW];
   double sa[4][OPP_MAXW];   // snapshot availability of touched hosts
   double ta[4][OPP_MAXW];   // current availability of touched hosts
+  int32_t slost[OPP_NSQ_MAX];   // per task: lost hosts per super-chunk
+  uint64_t lmask[OPP_SUP][4];   // per task: lost hosts of the chosen super-chunk, as chunk bitmaps
   uint32_t mt[625];
 };
 
@@ -136,32 +139,73 @@ __device__ __forceinline__ void ohash_put(OppLDS& S, int32_t id, int32_t v) {
   S.hval[p] = v;
 }
 
-// numpy legacy MT19937 (mt19937_gen / mt19937_next), run by one lane.
-__device__ uint32_t mt_next(uint32_t* st) {
-  if (st[624] >= 624) {
-    for (int i = 0; i < 624; i++) {
-      const uint32_t y = (st[i] & 0x80000000u) | (st[(i + 1) % 624] & 0x7fffffffu);
-      uint32_t v = st[(i + 397) % 624] ^ (y >> 1);
-      if (y & 1u) v ^= 0x9908b0dfu;
-      st[i] = v;
-    }
-    st[624] = 0;
-  }
-  uint32_t y = st[st[624]++];
+// numpy legacy MT19937 (mt19937_gen / mt19937_next) for the whole wave: the 624-word key lives
+// in LDS, the twist runs 64 words per step (reads of a step precede its writes, and every
+// key[i + 397 - 624] it needs was written by an earlier step, so this is the sequential loop),
+// and 64 tempered outputs at a time sit in one VGPR (lane j = output j), consumed in order.
+struct MtWave {
+  uint32_t buf;   // tempered outputs (lane j)
+  int used;       // outputs of buf consumed (uniform)
+  int limit;      // outputs held by buf (uniform; a buffer never straddles a twist)
+};
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
   y ^= (y >> 11);
   y ^= (y << 7) & 0x9d2c5680u;
   y ^= (y << 15) & 0xefc60000u;
   y ^= (y >> 18);
   return y;
 }
-__device__ uint32_t mt_randint(uint32_t* st, uint32_t n) {
+__device__ void mt_twist_wave(uint32_t* key) {
+  const int lane = lane_id();
+  for (int base = 0; base < 624; base += WAVE) {
+    const int i = base + lane;
+    uint32_t v = 0;
+    if (i < 624) {
+      const uint32_t y = (key[i] & 0x80000000u) | (key[(i + 1) % 624] & 0x7fffffffu);
+      v = key[(i + 397) % 624] ^ (y >> 1);
+      if (y & 1u) v ^= 0x9908b0dfu;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // every lane's reads land before any write
+    if (i < 624) key[i] = v;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+}
+// Next outputs into the buffer; key[624] is numpy's pos, advanced past the buffered outputs.
+// As in numpy, the twist runs only when an output is needed at pos == 624.
+__device__ void mt_refill(uint32_t* key, MtWave& w) {
+  const int lane = lane_id();
+  int pos = __builtin_amdgcn_readfirstlane((int)key[624]);
+  if (pos >= 624) {
+    mt_twist_wave(key);
+    pos = 0;
+  }
+  const int n = min(WAVE, 624 - pos);
+  const uint32_t y = key[pos + min(lane, n - 1)];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  if (lane == 0) key[624] = (uint32_t)(pos + n);
+  w.buf = mt_temper(y);
+  w.used = 0;
+  w.limit = n;
+}
+__device__ __forceinline__ uint32_t mt_next(uint32_t* key, MtWave& w) {
+  if (w.used >= w.limit) mt_refill(key, w);
+  return (uint32_t)__builtin_amdgcn_readlane((int)w.buf, w.used++);
+}
+// RandomState.randint(0, n): masked rejection, no draw for n == 1.
+__device__ uint32_t mt_randint(uint32_t* key, MtWave& w, uint32_t n) {
   const uint32_t rng = n - 1;
   if (rng == 0) return 0;
   uint32_t mask = rng;
   mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
   uint32_t v;
-  while ((v = (mt_next(st) & mask)) > rng) {}
+  while ((v = (mt_next(key, w) & mask)) > rng) {}
   return v;
+}
+// Hand unconsumed buffered outputs back to the state (rewind pos).
+__device__ void mt_unbuffer(uint32_t* key, MtWave& w) {
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  if (lane_id() == 0) key[624] = key[624] - (uint32_t)(w.limit - w.used);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
 }
 
 // Position of the r-th (0-based) set bit of x (r < popcount(x)).
@@ -177,6 +221,24 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r) {
   return pos;
 }
 
+#ifdef PVT_STAMPS
+__device__ __forceinline__ uint64_t ostamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define OSTAMP(k)                         \
+  do {                                    \
+    const uint64_t t_ = ostamp();         \
+    ph[k] += t_ - tl;                     \
+    tl = t_;                              \
+  } while (0)
+#else
+#define OSTAMP(k) do {} while (0)
+#endif
+
 __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
   constexpr int U = OPP_CH / WAVE;
   constexpr int SUPH = OPP_SUP * OPP_CH;
@@ -185,29 +247,62 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
   const int lane = lane_id();
   for (int i = lane; i < OPP_HASH; i += WAVE) S.hkey[i] = -1;
   for (int i = lane; i < 625; i += WAVE) S.mt[i] = A.mt[i];
+  __builtin_amdgcn_s_waitcnt(0xc07f);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const bool fast = A.nsq <= WAVE;   // one super-chunk count per lane (H <= 1,048,576)
   int m = 0;
-  // super-chunk counts of the next task, prefetched (fast path)
+  MtWave mw;
+  mw.buf = 0; mw.used = 0; mw.limit = 0;
+  // next task's super-chunk counts and demand, prefetched with vector loads (lanes 0-3 hold
+  // the demand), so no scalar-memory wait is mixed with the walk's LDS traffic
   int scn = (fast && A.nt > 0 && lane < A.nsq) ? A.sc[(size_t)lane * A.ldc] : 0;
+  double dn = (A.nt > 0) ? A.dem[lane & 3] : 0.0;
 
+#ifdef PVT_STAMPS
+  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t tl = ostamp();
+#endif
   for (int i = 0; i < A.nt; i++) {
-    const double* dp = A.dem + (size_t)i * 4;
-    const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+    OSTAMP(6);
+    const double dv = dn;
+    const double d0 = readlane_d(dv, 0), d1 = readlane_d(dv, 1), d2 = readlane_d(dv, 2), d3 = readlane_d(dv, 3);
     const int scv = scn;
-    if (fast && i + 1 < A.nt) scn = lane < A.nsq ? A.sc[(size_t)lane * A.ldc + i + 1] : 0;
-    // touched hosts that fitted at the snapshot and no longer fit
-    int nl = 0;
-    for (int q0 = 0; q0 < m; q0 += WAVE) {
-      const int q = q0 + lane;
-      const int qq = min(q, m - 1);
-      const bool lf = (q < m) &&
-                      fits<false>(S.sa[0][qq], S.sa[1][qq], S.sa[2][qq], S.sa[3][qq], d0, d1, d2, d3) &&
-                      !fits<false>(S.ta[0][qq], S.ta[1][qq], S.ta[2][qq], S.ta[3][qq], d0, d1, d2, d3);
-      const uint64_t b = __ballot(lf);
-      if (lf) S.lost[nl + __popcll(b & below)] = S.tid[q];
-      nl += __popcll(b);
+    if (i + 1 < A.nt) {
+      dn = A.dem[(size_t)(i + 1) * 4 + (lane & 3)];
+      if (fast) scn = lane < A.nsq ? A.sc[(size_t)lane * A.ldc + i + 1] : 0;
     }
+    OSTAMP(0);
+    // Touched hosts that fitted at the snapshot and no longer fit ("lost"), listed and counted
+    // per super-chunk with LDS atomics (4 x 64 touched hosts per loop trip).
+    // (the barriers order the zeroing, the other lanes' atomics and the reads: without them the
+    // compiler may forward a lane's own zero store to its later read)
+    for (int Q = lane; Q < A.nsq; Q += WAVE) S.slost[Q] = 0;
+    __syncthreads();
+    int nl = 0;
+    for (int q0 = 0; q0 < m; q0 += 4 * WAVE) {
+      bool lf[4];
+      int32_t th[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int q = q0 + u * WAVE + lane;
+        const int qq = min(q, m - 1);
+        th[u] = S.tid[qq];
+        lf[u] = (q < m) &&
+                fits<false>(S.sa[0][qq], S.sa[1][qq], S.sa[2][qq], S.sa[3][qq], d0, d1, d2, d3) &&
+                !fits<false>(S.ta[0][qq], S.ta[1][qq], S.ta[2][qq], S.ta[3][qq], d0, d1, d2, d3);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint64_t b = __ballot(lf[u]);
+        if (lf[u]) {
+          S.lost[nl + __popcll(b & below)] = th[u];
+          atomicAdd(&S.slost[th[u] / SUPH], 1);
+        }
+        nl += __popcll(b);
+      }
+    }
+    __syncthreads();
+    OSTAMP(1);
     long long n = 0;
     if (fast) {
       n = wave_sum_ll(scv);
@@ -219,19 +314,15 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     }
     n -= nl;
     if (n <= 0) continue;
-    uint32_t k = 0;
-    if (lane == 0) k = mt_randint(S.mt, (uint32_t)n);
-    k = (uint32_t)__builtin_amdgcn_readfirstlane((int)k);
+    const uint32_t k = mt_randint(S.mt, mw, (uint32_t)n);
+    OSTAMP(2);
     // super-chunk
     int Qs = -1;
     long long acc = 0;
     for (int Q0 = 0; Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
       const int Q = Q0 + lane;
       int v = 0;
-      if (Q < A.nsq) {
-        v = fast ? scv : A.sc[(size_t)Q * A.ldc + i];
-        for (int j = 0; j < nl; j++) v -= (S.lost[j] / SUPH) == Q;
-      }
+      if (Q < A.nsq) v = (fast ? scv : A.sc[(size_t)Q * A.ldc + i]) - S.slost[Q];
       const int inc = wave_incl_scan(v);
       const int tot = __builtin_amdgcn_readlane(inc, 63);
       if ((long long)k < acc + tot) {
@@ -244,8 +335,10 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
       }
     }
     if (Qs < 0) continue;   // unreachable when counts are consistent
+    OSTAMP(3);
     int k1 = (int)(k - (uint32_t)acc);
-    // chunk within the super-chunk: lane = chunk, its current bitmap = snapshot bits minus lost
+    // chunk within the super-chunk: lane = chunk; its current bitmap is the snapshot bitmap
+    // minus the lost hosts, collected into per-chunk masks with LDS atomics
     const int q = Qs * OPP_SUP + lane;
     uint64_t bits[U];
 #pragma unroll
@@ -254,19 +347,24 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
       const uint64_t* bp = A.bm + ((size_t)q * A.ldc + i) * U;
 #pragma unroll
       for (int u = 0; u < U; u++) bits[u] = bp[u];
-      for (int j = 0; j < nl; j++) {
-        const int h = S.lost[j];
-        if (h / OPP_CH == q) {
-          const int o = h % OPP_CH;
+    }
 #pragma unroll
-          for (int u = 0; u < U; u++)
-            if (o / WAVE == u) bits[u] &= ~(1ull << (o % WAVE));
-        }
+    for (int u = 0; u < U; u++) S.lmask[lane][u] = 0;
+    __syncthreads();
+    for (int j = lane; j < nl; j += WAVE) {
+      const int h = S.lost[j];
+      if (h / SUPH == Qs) {
+        const int o = h % OPP_CH;
+        atomicOr((unsigned long long*)&S.lmask[(h / OPP_CH) % OPP_SUP][o / WAVE], 1ull << (o % WAVE));
       }
     }
+    __syncthreads();
     int c = 0;
 #pragma unroll
-    for (int u = 0; u < U; u++) c += __popcll(bits[u]);
+    for (int u = 0; u < U; u++) {
+      bits[u] &= ~S.lmask[lane][u];
+      c += __popcll(bits[u]);
+    }
     const int inc = wave_incl_scan(c);
     const uint64_t hit = __ballot(inc > k1);
     if (hit == 0) continue;   // unreachable when counts are consistent
@@ -286,15 +384,17 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     }
     off = __builtin_amdgcn_readlane(off, L);
     const int w = (Qs * OPP_SUP + L) * OPP_CH + off;
+    OSTAMP(4);
     int ws = ohash_find(S, w);
     ws = __builtin_amdgcn_readfirstlane(ws);
     double w0, w1, w2, w3;
     if (ws >= 0) {
       w0 = S.ta[0][ws]; w1 = S.ta[1][ws]; w2 = S.ta[2][ws]; w3 = S.ta[3][ws];
-    } else {
-      w0 = A.avail[w]; w1 = A.avail[(size_t)A.H + w];
-      w2 = A.avail[2 * (size_t)A.H + w]; w3 = A.avail[3 * (size_t)A.H + w];
+    } else {   // lanes 0-3 load the four resources (vector loads)
+      const double av = A.avail[(size_t)(lane & 3) * A.H + w];
+      w0 = readlane_d(av, 0); w1 = readlane_d(av, 1); w2 = readlane_d(av, 2); w3 = readlane_d(av, 3);
     }
+    OSTAMP(5);
     const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
     if (ws < 0) {
       ws = m++;
@@ -313,7 +413,14 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
       A.placement[i] = w;
     }
   }
+  mt_unbuffer(S.mt, mw);
   for (int i = lane; i < 625; i += WAVE) A.mt[i] = S.mt[i];
+#ifdef PVT_STAMPS
+  if (lane == 0 && A.stamps) {
+    for (int k = 0; k < 7; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
+    atomicAdd((unsigned long long*)&A.stamps[7], (unsigned long long)A.nt);
+  }
+#endif
 }
 
 hipError_t opp_init_attrs() {

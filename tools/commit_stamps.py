@@ -18,13 +18,21 @@ eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "bu
                                                "libpivot_place_stamps.so"))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-buf = (ctypes.c_uint64 * 7)()
-assert f(eng.ctx, buf, 7) == 0          # allocates and zeroes the device counters
+buf = (ctypes.c_uint64 * 8)()
+assert f(eng.ctx, buf, 8) == 0          # allocates and zeroes the device counters
 r = synthetic.make_round(mode, H, T)
 dr = DeviceRound(r, eng.device)
 eng.run(dr)
 torch.cuda.synchronize()
-assert f(eng.ctx, buf, 7) == 0
+assert f(eng.ctx, buf, 8) == 0
+if mode == 2:
+    names = ["prefetch/decode", "lost-scan", "count+draw", "super-select", "chunk-select",
+             "host-avail", "commit"]
+    tot = sum(buf[k] for k in range(7))
+    print("opportunistic H=%d T=%d tasks=%d stats=%s" % (H, T, buf[7], eng.last_stats()))
+    for k in range(7):
+        print("  %-16s %6.1f%%  %8.0f cycles/task" % (names[k], 100.0 * buf[k] / tot, buf[k] / max(buf[7], 1)))
+    sys.exit(0)
 names = ["wait-prefetch", "hash-lookup", "untouched-pick", "touched-rescore", "commit"]
 tot = sum(buf[k] for k in range(5))
 print("mode %d H=%d T=%d tasks walked=%d stats=%s mean live touched=%.1f"
