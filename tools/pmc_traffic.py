@@ -6,7 +6,7 @@ Two separate passes (FETCH_SIZE and WRITE_SIZE cannot share one: TCC slots), eac
 never touches the GPU itself). Per MI355X_MICROARCH.md §HBM, FETCH_SIZE on gfx950 reports half
 the bytes of a wide coalesced streaming read, so the read side is doubled; WRITE_SIZE is taken
 as is. Counters are summed per dispatch of `score_kernel` / `opp_count_kernel` and averaged.
-Writes profiles/traffic.json, which bench.py reports as roofline.traffic when its config
+Writes gpurun_out/traffic.json (copy it to profiles/traffic.json), which bench.py reports as roofline.traffic when its config
 matches.
 """
 import csv
@@ -71,7 +71,7 @@ def main():
                 "whose hits these counters include.",
     }
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
-    with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", "traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out))
 
