@@ -45,6 +45,9 @@ def parse():
     p.add_argument("--tasks", type=int, default=10_000)
     p.add_argument("--seed", type=int, default=20261015)
     p.add_argument("--window", type=int, default=0)
+    p.add_argument("--shard", default="scenarios", choices=["scenarios", "hosts"],
+                   help="N > 1: independent scenario per rank (weak scaling, config 4) or one "
+                        "round with its host dimension split over the ranks (strong, config 5)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                    help="target CPU time of the oracle baseline sample (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -88,14 +91,20 @@ def main():
     mode = MODES[args.mode]
     H, T = args.hosts, args.tasks
     log("[rank %d] building synthetic round: %s, H=%d T=%d" % (rank, args.mode, H, T))
-    r = synthetic.make_round(mode, H, T, seed=args.seed + rank)
+    hosts_sharded = args.shard == "hosts"
+    r = synthetic.make_round(mode, H, T, seed=args.seed + (0 if hosts_sharded else rank))
     eng = PlacementEngine(local, window=args.window)
     dr = DeviceRound(r, eng.device)
+    run = eng.run
+    if hosts_sharded:
+        from pivot_place.sharded import HostShardedPlacer, torch_exchange
+        placer = HostShardedPlacer(eng, rank, world, torch_exchange() if world > 1 else None)
+        run = placer.run
     torch.cuda.synchronize()
 
     for i in range(args.warmup):
         dr.reset()
-        eng.run(dr)
+        run(dr)
     torch.cuda.synchronize()
     stats = eng.last_stats()
     placed = int((dr.placement[:T] >= 0).sum().item())
@@ -110,7 +119,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         dr.reset()
-        eng.run(dr)
+        run(dr)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -121,7 +130,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    cand_per_step = float(T) * H * world
+    cand_per_step = float(T) * H * (1 if hosts_sharded else world)
     value = cand_per_step / (elapsed / args.steps)
 
     ks = {name: eng.kstats(k) for name, k in (("score", _abi.PVT_K_SCORE), ("merge", _abi.PVT_K_MERGE),
@@ -150,15 +159,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if hosts_sharded else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md §8(d): trace demand rows, 20 locality.yml zones, seeded)",
             "config": {
-                "workload": "synthetic %d hosts x %d ready tasks per round, 20 zones, %s, "
-                            "one independent scenario per GPU" % (H, T, POLICY[args.mode]),
+                "workload": "synthetic %d hosts x %d ready tasks per round, 20 zones, %s, %s"
+                            % (H, T, POLICY[args.mode],
+                               "host dimension split over the GPUs" if hosts_sharded
+                               else "one independent scenario per GPU"),
                 "hosts": H, "tasks_per_round": T, "zones": 20, "policy": args.mode,
-                "parallelism": "scenario-sharded x%d (no data-path collective)" % world,
+                "parallelism": ("host-sharded x%d (per-window candidate all-gather)" % world
+                                if hosts_sharded else
+                                "scenario-sharded x%d (no data-path collective)" % world),
             },
             "roofline": {
                 "bound": "hbm",

@@ -115,8 +115,9 @@ enum pvt_kclass {
 int  pvt_abi_version(void);
 int  pvt_ctx_create(int device, pvt_ctx** out);
 int  pvt_ctx_destroy(pvt_ctx* ctx);
-/* Use a caller stream (hipStream_t as void*), e.g. torch.cuda.current_stream().cuda_stream.
- * NULL restores the context's own stream. */
+/* Order the context's work on a caller stream (hipStream_t as void*), e.g.
+ * torch.cuda.current_stream().cuda_stream. NULL is the device's default (null) stream, which is
+ * what torch's default stream is. Until the first call the context uses a stream of its own. */
 int  pvt_ctx_set_stream(pvt_ctx* ctx, void* stream);
 int  pvt_place(pvt_ctx* ctx, const pvt_round* r);
 /* Profiling: record HIP events around every kernel launch (adds a little host overhead). */
@@ -127,6 +128,32 @@ int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
 int  pvt_set_window(pvt_ctx* ctx, int tasks);
 /* Counters of the last pvt_place call: windows run and refills forced by exhausted lists. */
 int  pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills);
+/*
+ * Host-dimension sharding (BASELINE config 5): `world` ranks (one per GPU)
+ * each score a contiguous host range [host_lo, host_hi) and exchange per-task candidate
+ * packages once per window; every rank then runs the same commit walk, so placements are
+ * identical on all ranks and equal to pvt_place(). Each rank keeps the FULL availability array
+ * (32 B per host, replicated and updated identically by the walk); only scoring is split.
+ * The exchange is the caller's (an all-gather, e.g. RCCL through torch.distributed):
+ *
+ *   pvt_shard_begin(ctx, r, lo, hi, world, &max_bytes)     allocate send [max_bytes] and
+ *                                                          recv [world * max_bytes] (device)
+ *   loop:
+ *     pvt_shard_score(ctx, send, &nt, &bytes)              nt == 0: the round is done
+ *     all-gather `bytes` from every rank into recv, rank order, contiguous (recv[k*bytes..])
+ *     pvt_shard_commit(ctx, recv)
+ *
+ * `r` and its arrays must stay valid until the round is done. nt and bytes are the same on
+ * every rank (window sizes depend only on walk results, which every rank shares).
+ * Opportunistic rounds return PVT_EUNSUPPORTED (their draw needs a per-task exchange; shard
+ * them by scenario instead). Replaces the per-task scan of scheduler/cost_aware.py:88-92,
+ * :118-122 and scheduler/vbp.py:19-22, :43-47 over a cluster too large for one GPU's pass.
+ */
+#define PVT_SHARD_MAX_WORLD 64
+int  pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo, int32_t host_hi,
+                     int32_t world, int64_t* max_package_bytes);
+int  pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks, int64_t* package_bytes);
+int  pvt_shard_commit(pvt_ctx* ctx, const void* packages);
 /* Human-readable text of the last error on this context (static storage of the ctx). */
 const char* pvt_last_error(pvt_ctx* ctx);
 

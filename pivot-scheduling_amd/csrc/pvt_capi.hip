@@ -37,6 +37,18 @@ struct TimedLaunch {
   hipEvent_t a, b;
 };
 
+struct RoundState {
+  pvt_round r;                    // the caller's round (arrays stay caller-owned)
+  bool active = false;
+  int T = 0, H = 0, Z = 0, lo = 0, hi = 0, world = 0;
+  bool keyed = false, ordered = false;
+  int32_t* ord = nullptr;         // processing order (ctx scratch)
+  std::vector<int> gstart, ganchor;
+  size_t g = 0, ngroups = 0;
+  int key_group = -1;             // group whose frozen first-fit key is computed
+  int t0 = 0, W = 0, Wmax = 0, nt = 0;
+};
+
 struct pvt_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
@@ -49,7 +61,8 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_e, l_ids, l_t, next, opp;
+      seg, seg_feas, l_e, l_ids, l_t, next, opp, pkg;
+  RoundState rs;
   int32_t* next_host = nullptr;   // pinned
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
 };
@@ -74,10 +87,10 @@ static int fail(pvt_ctx* c, int code, const char* fmt, ...) {
 static int ensure(pvt_ctx* ctx, Buf& b, size_t bytes) {
   if (bytes == 0) bytes = 16;
   if (b.n >= bytes) return PVT_OK;
+  const size_t want = std::max(bytes, b.n * 3 / 2);
   if (b.p) (void)hipFree(b.p);
   b.p = nullptr;
   b.n = 0;
-  size_t want = std::max(bytes, b.n * 3 / 2);
   if (hipMalloc(&b.p, want) != hipSuccess) {
     b.p = nullptr;
     return fail(ctx, PVT_ENOMEM, "hipMalloc(%zu) failed", want);
@@ -165,7 +178,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   harvest(ctx);
   Buf* bufs[] = {&ctx->ord, &ctx->ord2, &ctx->keys64a, &ctx->keys64b, &ctx->keys32a, &ctx->keys32b,
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
-                 &ctx->seg, &ctx->seg_feas, &ctx->l_e, &ctx->l_ids, &ctx->l_t, &ctx->next, &ctx->opp};
+                 &ctx->seg, &ctx->seg_feas, &ctx->l_e, &ctx->l_ids, &ctx->l_t, &ctx->next, &ctx->opp, &ctx->pkg};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -177,7 +190,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
 
 extern "C" int pvt_ctx_set_stream(pvt_ctx* ctx, void* stream) {
   if (!ctx) return PVT_EINVAL;
-  ctx->stream = stream ? (hipStream_t)stream : ctx->own;
+  ctx->stream = (hipStream_t)stream;   // NULL is the device's default (null) stream
   return PVT_OK;
 }
 
@@ -362,29 +375,34 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   return PVT_OK;
 }
 
-extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
-  if (!ctx) return PVT_EINVAL;
-  int rc = check_round(ctx, r);
+// ---------------------------------------------------------------- round state machine
+// pvt_place() and the sharded calls share one resumable round: begin (order, gathers, zone
+// tables, group boundaries), then per window: lists over this context's host range, optionally
+// exchanged between ranks, then the commit walk, which advances the window.
+static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int world) {
+  RoundState& R = ctx->rs;
+  R.active = false;
+  int rc = check_round(ctx, rin);
   if (rc) return rc;
+  R.r = *rin;
+  const pvt_round* r = &R.r;
   ctx->windows = ctx->refills = 0;
   HIPCHK(hipSetDevice(ctx->device));
   const int T = r->n_tasks, H = r->n_hosts, Z = r->n_zones;
-  if (T == 0) return PVT_OK;
+  R.T = T; R.H = H; R.Z = Z; R.lo = lo; R.hi = hi; R.world = world;
+  R.t0 = 0; R.g = 0; R.nt = 0;
+  R.gstart.assign(1, 0);
+  R.ganchor.clear();
+  if (T == 0) { R.ngroups = 0; R.active = true; return PVT_OK; }
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
 
-  if (r->mode == PVT_OPP) {
-    launch_iota(r->order, T, st);
-    return opp_round(ctx, r);
-  }
-
-  int32_t* ord = nullptr;
-  if ((rc = build_order(ctx, r, &ord))) return rc;
-  HIPCHK(hipMemcpyAsync(r->order, ord, sizeof(int32_t) * T, hipMemcpyDeviceToDevice, st));
+  if ((rc = build_order(ctx, r, &R.ord))) return rc;
+  HIPCHK(hipMemcpyAsync(r->order, R.ord, sizeof(int32_t) * T, hipMemcpyDeviceToDevice, st));
 
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
-  launch_gather_tasks(r->dem, ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
+  launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
                       P<int32_t>(ctx->anc_ord), st);
   const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
   if (ca) {
@@ -394,10 +412,9 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
   }
 
   // group boundaries in processing order (only cost_aware first-fit with sort_hosts needs them)
-  const bool keyed = r->mode == PVT_CA_FF && r->sort_hosts;
-  const bool ordered = (r->mode == PVT_VBP_FF) || (r->mode == PVT_CA_FF && !r->sort_hosts);
-  std::vector<int> gstart{0}, ganchor;
-  if (keyed) {
+  R.keyed = r->mode == PVT_CA_FF && r->sort_hosts;
+  R.ordered = (r->mode == PVT_VBP_FF) || (r->mode == PVT_CA_FF && !r->sort_hosts);
+  if (R.keyed) {
     std::vector<int32_t> tg(T), ga;
     if (r->task_group) {
       HIPCHK(hipMemcpyAsync(tg.data(), r->task_group, sizeof(int32_t) * T, hipMemcpyDeviceToHost, st));
@@ -411,19 +428,21 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
         cnt[tg[t]]++;
       }
       int off = 0;
-      gstart.clear();
+      R.gstart.clear();
       for (int g = 0; g < r->n_groups; g++) {
         if (cnt[g] == 0) continue;
-        gstart.push_back(off);
-        ganchor.push_back(ga[g]);
+        R.gstart.push_back(off);
+        R.ganchor.push_back(ga[g]);
         off += cnt[g];
       }
     } else {
-      ganchor.push_back(0);
+      R.ganchor.push_back(0);
     }
+    ENSURE(ctx->key, sizeof(double) * H);
   }
-  gstart.push_back(T);
-  if (keyed) ENSURE(ctx->key, sizeof(double) * H);
+  R.gstart.push_back(T);
+  R.ngroups = R.keyed ? R.ganchor.size() : 1;
+  R.key_group = -1;
 
   // Windows adapt to how far commit walks get before a list is exhausted: a walk that stops
   // early means the next window only needs about that many tasks (the score pass costs the
@@ -431,76 +450,197 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
   // default window: vbp best-fit walks search deeper lists as a window's touched hosts pile up
   // at the top of every task's ranking, so its windows are shorter (bench sweep)
   const int wdef = (r->mode == PVT_VBP_BF) ? 512 : MAX_WINDOW;
-  const int Wmax = std::max(1, std::min(ctx->window > 0 ? ctx->window : wdef, MAX_WINDOW));
+  R.Wmax = std::max(1, std::min(ctx->window > 0 ? ctx->window : wdef, MAX_WINDOW));
+  R.W = R.Wmax;
   ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)SEG_ENTRIES_MAX);
   ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)SEG_ENTRIES_MAX / KL);
-  ENSURE(ctx->l_e, sizeof(ListEntry) * (size_t)Wmax * LMAX);
-  ENSURE(ctx->l_ids, sizeof(int32_t) * (size_t)Wmax * LMAX);
-  ENSURE(ctx->l_t, sizeof(TaskRec) * (size_t)Wmax);
+  ENSURE(ctx->l_e, sizeof(ListEntry) * (size_t)R.Wmax * LMAX);
+  ENSURE(ctx->l_ids, sizeof(int32_t) * (size_t)R.Wmax * LMAX);
+  ENSURE(ctx->l_t, sizeof(TaskRec) * (size_t)R.Wmax);
   ENSURE(ctx->next, sizeof(int32_t) * 4);
+  R.active = true;
+  return PVT_OK;
+}
+
+// Size of the next window (0: the round is done). Computes the frozen first-fit key of this
+// context's hosts at a group start.
+static int round_next_window(pvt_ctx* ctx, int* nt_out) {
+  RoundState& R = ctx->rs;
+  *nt_out = 0;
+  if (!R.active) return fail(ctx, PVT_EINVAL, "no round in progress");
+  while (R.g < R.ngroups && R.t0 >= (R.keyed ? R.gstart[R.g + 1] : R.T)) R.g++;
+  if (R.g >= R.ngroups || R.T == 0) return PVT_OK;
+  const int ge = R.keyed ? R.gstart[R.g + 1] : R.T;
+  if (R.keyed && R.key_group != (int)R.g && R.hi > R.lo) {
+    KeyArgs ka{R.r.avail, R.r.zone, R.r.decay, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z,
+               R.ganchor[R.g], R.lo, R.hi, P<double>(ctx->key)};
+    Scope sc(ctx, PVT_K_OTHER, 0, 0);
+    launch_key(ka, ctx->stream);
+    R.key_group = (int)R.g;
+  }
+  R.nt = std::min(R.W, ge - R.t0);
+  *nt_out = R.nt;
+  return PVT_OK;
+}
+
+// The window's exact candidate lists over hosts [lo, hi) -> ctx lists.
+static int window_lists(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  const int nt = R.nt, t0 = R.t0, Hl = R.hi - R.lo;
+  ctx->windows++;
   Lists L;
   lists_from(ctx, L);
   const double bpc = bytes_per_candidate(r->mode);
-  const double* dem_ord = P<double>(ctx->dem_ord);
-  const int32_t* anc_ord = P<int32_t>(ctx->anc_ord);
-  int W = Wmax;
-
-  const size_t ngroups = keyed ? ganchor.size() : 1;
-  for (size_t g = 0; g < ngroups; g++) {
-    const int gb = keyed ? gstart[g] : 0, ge = keyed ? gstart[g + 1] : T;
-    if (keyed) {
-      KeyArgs ka{r->avail, r->zone, r->decay, P<double>(ctx->csum), P<double>(ctx->bsum), H, Z,
-                 ganchor[g], P<double>(ctx->key)};
-      Scope sc(ctx, PVT_K_OTHER, 0, 0);
-      launch_key(ka, st);
+  const double* dem_w = P<double>(ctx->dem_ord) + (size_t)t0 * 4;
+  const int32_t* anc_w = P<int32_t>(ctx->anc_ord) + t0;
+  if (R.ordered) {
+    OrderedArgs oa{r->avail, r->zone, dem_w, anc_w, R.ord + t0, R.H, nt,
+                   r->mode == PVT_CA_FF ? 1 : 0, R.lo, R.hi, L};
+    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc);
+    launch_ordered(oa, st);
+  } else {
+    int S, seg_len;
+    choose_segments(Hl, nt, &S, &seg_len);
+    ScoreArgs sa{r->avail, r->zone, r->tiebreak, R.keyed ? P<double>(ctx->key) : nullptr,
+                 dem_w, anc_w, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z, nt, S,
+                 seg_len, R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
+    {
+      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc);
+      launch_score(r->mode, sa, st);
     }
-    int t0 = gb;
-    while (t0 < ge) {
-      const int nt = std::min(W, ge - t0);
-      ctx->windows++;
-      const double* dem_w = dem_ord + (size_t)t0 * 4;
-      if (ordered) {
-        OrderedArgs oa{r->avail, r->zone, dem_w, anc_ord + t0, ord + t0, H, nt,
-                       r->mode == PVT_CA_FF ? 1 : 0, L};
-        Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
-        launch_ordered(oa, st);
-      } else {
-        int S, seg_len;
-        choose_segments(H, nt, &S, &seg_len);
-        ScoreArgs sa{r->avail, r->zone, r->tiebreak, keyed ? P<double>(ctx->key) : nullptr,
-                     dem_w, anc_ord + t0, P<double>(ctx->csum), P<double>(ctx->bsum), H, Z, nt, S,
-                     seg_len, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
-        {
-          Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
-          launch_score(r->mode, sa, st);
-        }
-        MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
-                     anc_ord + t0, ord + t0, H, nt, S, L};
-        Scope sc(ctx, PVT_K_MERGE, 0, 0);
-        launch_merge(ma, st);
-      }
-      CommitArgs ca_{r->avail, dem_w, P<double>(ctx->csum), P<double>(ctx->bsum), L, H, Z,
-                     nt, r->mode, r->placement, P<int32_t>(ctx->next), ctx->stamps};
-      {
-        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
-        launch_commit(ca_, st);
-      }
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t),
-                            hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      const int adv = *ctx->next_host;
-      if (adv < 0 || adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", adv, nt);
-      if (adv == 0) return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
-      if (adv < nt) {
-        ctx->refills++;
-        W = std::max(std::min(64, Wmax), std::min(Wmax, adv + adv / 2));
-      } else if (nt == W) {
-        W = std::min(Wmax, 2 * W);
-      }
-      t0 += adv;
-    }
+    MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
+                 anc_w, R.ord + t0, R.H, nt, S, KL, L};
+    Scope sc(ctx, PVT_K_MERGE, 0, 0);
+    launch_merge(ma, st);
   }
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(hipGetLastError());
   return PVT_OK;
+}
+
+// Commit walk over the window; advances the round.
+static int window_commit(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  const int nt = R.nt, t0 = R.t0;
+  Lists L;
+  lists_from(ctx, L);
+  CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
+                 P<double>(ctx->bsum), L, R.H, R.Z, nt, r->mode, r->placement,
+                 P<int32_t>(ctx->next), ctx->stamps};
+  {
+    Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+    launch_commit(ca_, st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t),
+                        hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const int adv = *ctx->next_host;
+  R.nt = 0;
+  if (adv < 0 || adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", adv, nt);
+  if (adv == 0) return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
+  if (adv < nt) {
+    ctx->refills++;
+    R.W = std::max(std::min(64, R.Wmax), std::min(R.Wmax, adv + adv / 2));
+  } else if (nt == R.W) {
+    R.W = std::min(R.Wmax, 2 * R.W);
+  }
+  R.t0 += adv;
+  return PVT_OK;
+}
+
+extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
+  if (!ctx) return PVT_EINVAL;
+  int rc = check_round(ctx, r);
+  if (rc) return rc;
+  if (r->mode == PVT_OPP) {
+    ctx->rs.active = false;
+    ctx->windows = ctx->refills = 0;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (r->n_tasks == 0) return PVT_OK;
+    HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * r->n_tasks, ctx->stream));
+    launch_iota(r->order, r->n_tasks, ctx->stream);
+    return opp_round(ctx, r);
+  }
+  if ((rc = round_begin(ctx, r, 0, r->n_hosts, 1))) return rc;
+  for (;;) {
+    int nt = 0;
+    if ((rc = round_next_window(ctx, &nt))) return rc;
+    if (nt == 0) break;
+    if ((rc = window_lists(ctx)) || (rc = window_commit(ctx))) return rc;
+  }
+  ctx->rs.active = false;
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  return PVT_OK;
+}
+
+// ---------------------------------------------------------------- host-dimension sharding
+static int shard_depth(int world) { return std::max(KL, LMAX / std::max(world, 1)); }
+
+extern "C" int pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo,
+                               int32_t host_hi, int32_t world, int64_t* max_package_bytes) {
+  if (!ctx || !r) return PVT_EINVAL;
+  ctx->rs.active = false;
+  if (world < 1 || world > PVT_SHARD_MAX_WORLD)
+    return fail(ctx, PVT_EINVAL, "world %d outside [1, %d]", world, PVT_SHARD_MAX_WORLD);
+  if (host_lo < 0 || host_hi < host_lo || host_hi > r->n_hosts)
+    return fail(ctx, PVT_EINVAL, "bad host range [%d, %d) of %d", host_lo, host_hi, r->n_hosts);
+  if (r->mode == PVT_OPP)
+    return fail(ctx, PVT_EUNSUPPORTED, "opportunistic rounds are not host-sharded (scenario-shard them)");
+  int rc = round_begin(ctx, r, host_lo, host_hi, world);
+  if (rc) return rc;
+  const int PK = shard_depth(world);
+  ENSURE(ctx->pkg, sizeof(SegEntry) * (size_t)(PK + 1) * ctx->rs.Wmax);
+  if (max_package_bytes) *max_package_bytes = (int64_t)sizeof(SegEntry) * (PK + 1) * ctx->rs.Wmax;
+  return PVT_OK;
+}
+
+extern "C" int pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out,
+                               int64_t* package_bytes) {
+  if (!ctx || !package || !n_tasks_out || !package_bytes) return PVT_EINVAL;
+  *n_tasks_out = 0;
+  *package_bytes = 0;
+  if (!ctx->rs.active || ctx->rs.world < 1) return fail(ctx, PVT_EINVAL, "no sharded round in progress");
+  if (ctx->rs.nt != 0) return fail(ctx, PVT_EINVAL, "pvt_shard_score called twice without pvt_shard_commit");
+  int nt = 0, rc;
+  if ((rc = round_next_window(ctx, &nt))) return rc;
+  if (nt == 0) {
+    ctx->rs.active = false;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return PVT_OK;
+  }
+  if ((rc = window_lists(ctx))) return rc;
+  const int PK = shard_depth(ctx->rs.world);
+  Lists L;
+  lists_from(ctx, L);
+  PackArgs pa{L, nt, PK, ctx->rs.ordered ? 1 : 0, reinterpret_cast<SegEntry*>(package)};
+  {
+    Scope sc(ctx, PVT_K_MERGE, 0, 0);
+    launch_pack(pa, ctx->stream);
+  }
+  HIPCHK(hipGetLastError());
+  *n_tasks_out = nt;
+  *package_bytes = (int64_t)sizeof(SegEntry) * (PK + 1) * nt;
+  return PVT_OK;
+}
+
+extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
+  if (!ctx || !packages) return PVT_EINVAL;
+  RoundState& R = ctx->rs;
+  if (!R.active || R.nt == 0) return fail(ctx, PVT_EINVAL, "pvt_shard_commit without a scored window");
+  const int PK = shard_depth(R.world);
+  Lists L;
+  lists_from(ctx, L);
+  MergeArgs ma{reinterpret_cast<const SegEntry*>(packages), nullptr, R.r.avail, R.r.zone,
+               P<double>(ctx->dem_ord) + (size_t)R.t0 * 4, P<int32_t>(ctx->anc_ord) + R.t0,
+               R.ord + R.t0, R.H, R.nt, R.world, PK, L};
+  {
+    Scope sc(ctx, PVT_K_MERGE, 0, 0);
+    launch_merge(ma, ctx->stream);
+  }
+  HIPCHK(hipGetLastError());
+  return window_commit(ctx);
 }

@@ -71,10 +71,17 @@ struct ScoreArgs {
   const double* csum;
   const double* bsum;
   int H, Z, nt, S, seg_len;
+  int h_lo, h_hi;         // host range scored (a rank's shard; [0, H) unsharded)
   SegEntry* seg;          // [nt][S][KL]
   int32_t* seg_feas;      // [nt][S]
 };
 
+// Merge of S sorted candidate lists per task into the task's exact top list. Two sources:
+//   score segments   seg[(task*S + g)*KL + e], SL = KL, seg_feas[task*S + g] = feasible hosts
+//                    of the segment (a list with more than KL of them is bounded by entry KL-1)
+//   rank packages    (host-dimension sharding) seg[(g*nt + task)*(SL+1) + e]: SL entries then
+//                    an explicit bound entry (id 0x7fffffff: the rank's list is complete);
+//                    seg_feas = NULL
 struct MergeArgs {
   const SegEntry* seg;
   const int32_t* seg_feas;
@@ -84,7 +91,16 @@ struct MergeArgs {
   const int32_t* anc;     // window tasks [nt]
   const int32_t* ord;     // window tasks' caller indices
   int H, nt, S;
+  int SL;                 // entries per source list (KL, or the package depth)
   Lists L;
+};
+
+// Host-dimension sharding: a rank's exact local lists -> its exchange package (see MergeArgs).
+struct PackArgs {
+  Lists L;                // local merged lists of the window
+  int nt, PK;
+  int ordered;            // index-order first-fit lists (score 0, bound = last id + 1)
+  SegEntry* out;          // [nt][PK + 1]
 };
 
 struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible hosts
@@ -94,6 +110,7 @@ struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible
   const int32_t* anc;
   const int32_t* ord;
   int H, nt, strict;
+  int h_lo, h_hi;         // host range scanned
   Lists L;
 };
 
@@ -116,11 +133,13 @@ struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw
   const double* csum;
   const double* bsum;
   int H, Z, anchor;
+  int h_lo, h_hi;         // hosts whose key is computed
   double* key;
 };
 
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st);
 void launch_merge(const MergeArgs& a, hipStream_t st);
+void launch_pack(const PackArgs& a, hipStream_t st);
 void launch_ordered(const OrderedArgs& a, hipStream_t st);
 void launch_commit(const CommitArgs& a, hipStream_t st);
 void launch_key(const KeyArgs& a, hipStream_t st);

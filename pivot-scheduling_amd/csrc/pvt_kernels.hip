@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   const int t0 = (tile * WPB + wave) * TW;
   if (t0 >= A.nt) return;
   const int nt = min(TW, A.nt - t0);
-  const int hb0 = seg * A.seg_len, hb1 = min(A.H, hb0 + A.seg_len);
+  const int hb0 = A.h_lo + seg * A.seg_len, hb1 = min(A.h_hi, hb0 + A.seg_len);
 
   double d0[TW], d1[TW], d2[TW], d3[TW];
   double ls[TW], ts[TW], lim[TW];
@@ -226,33 +226,50 @@ __device__ __forceinline__ void bitonic_sort_lds(Key* v, int n, int tid, int nth
 }
 
 __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
-  constexpr int BATCH = LMAX / KL;     // segment lists per sort batch
   __shared__ Key run[LMAX];
   __shared__ Key buf[LMAX];
   __shared__ Key bound;
   __shared__ long long tot;
   __shared__ int cnt_sh;
   const int task = blockIdx.x, tid = threadIdx.x;
+  const int SL = A.SL, batch = LMAX / SL;   // source lists per sort batch
+  const bool packed = A.seg_feas == nullptr;
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
+  // entry e of source list g
+  auto src = [&](int g, int e) -> const SegEntry& {
+    return packed ? A.seg[((size_t)g * A.nt + task) * (SL + 1) + e]
+                  : A.seg[((size_t)task * A.S + g) * SL + e];
+  };
   for (int j = tid; j < LMAX; j += 256) run[j] = inv;
   if (tid == 0) { bound = inv; tot = 0; cnt_sh = 0; }
   __syncthreads();
-  for (int g0 = 0; g0 < A.S; g0 += BATCH) {
+  for (int g0 = 0; g0 < A.S; g0 += batch) {
+    int nvalid = 0;
     for (int e = tid; e < LMAX; e += 256) {
-      const int g = g0 + e / KL;
+      const int g = g0 + e / SL;
       Key k = inv;
-      if (g < A.S) {
-        const SegEntry se = A.seg[((size_t)task * A.S + g) * KL + (e % KL)];
+      if (e < batch * SL && g < A.S) {
+        const SegEntry se = src(g, e % SL);
         k = {se.s, se.tb, se.id};
+        nvalid += se.id != 0x7fffffff;
       }
       buf[e] = k;
     }
-    if (tid == 0) {
-      for (int g = g0; g < min(A.S, g0 + BATCH); g++) {
+    if (packed) {
+      if (nvalid) atomicAdd((unsigned long long*)&tot, (unsigned long long)nvalid);
+      if (tid == 0) {
+        for (int g = g0; g < min(A.S, g0 + batch); g++) {
+          const SegEntry se = src(g, SL);        // the package's explicit bound
+          const Key k = {se.s, se.tb, se.id};
+          if (kless(k, bound)) bound = k;
+        }
+      }
+    } else if (tid == 0) {
+      for (int g = g0; g < min(A.S, g0 + batch); g++) {
         const int f = A.seg_feas[(size_t)task * A.S + g];
         tot += f;
-        if (f > KL) {
-          const SegEntry se = A.seg[((size_t)task * A.S + g) * KL + KL - 1];
+        if (f > SL) {
+          const SegEntry se = src(g, SL - 1);
           const Key k = {se.s, se.tb, se.id};
           if (kless(k, bound)) bound = k;
         }
@@ -321,6 +338,41 @@ void launch_merge(const MergeArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Pack (host-dimension sharding): one wave per task turns the rank's exact
+// local list into its exchange package: the first PK entries plus a bound every host of the
+// rank outside the package ranks at or after. The bound is entry PK when the list is longer,
+// else the list's own bound (none if complete). Index-order first-fit lists (score 0) are
+// bounded by (0, 0, last id + 1): the rank's unlisted feasible hosts come after its last one.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_kernel(PackArgs A) {
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int task = blockIdx.x * 4 + wave;
+  if (task >= A.nt) return;
+  const TaskRec& r = A.L.t[task];
+  const int cnt = r.cnt;
+  const ListEntry* e = A.L.e + (size_t)task * LMAX;
+  SegEntry* out = A.out + (size_t)task * (A.PK + 1);
+  for (int j = lane; j < A.PK; j += WAVE) {
+    SegEntry o = {DINF, 0xffffffffu, 0x7fffffff};
+    if (j < cnt) { o.s = e[j].s; o.tb = e[j].tb; o.id = e[j].id; }
+    out[j] = o;
+  }
+  if (lane == 0) {
+    SegEntry b = {DINF, 0xffffffffu, 0x7fffffff};
+    if (cnt > A.PK) {
+      b.s = e[A.PK].s; b.tb = e[A.PK].tb; b.id = e[A.PK].id;
+    } else if (!r.complete) {
+      if (A.ordered) { b.s = 0.0; b.tb = 0; b.id = e[cnt - 1].id + 1; }
+      else { b.s = r.bs; b.tb = r.btb; b.id = r.bid; }
+    }
+    out[A.PK] = b;
+  }
+}
+void launch_pack(const PackArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(pack_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
 // Ordered scan (vbp first-fit, cost_aware first-fit without sort_hosts): the first KL
 // snapshot-feasible hosts in index order, one wave per task, early exit.
 // ------------------------------------------------------------------------------------------
@@ -333,10 +385,10 @@ __global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
   const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   int cnt = 0;
-  int hb = 0;
-  for (; hb < A.H && cnt < KL; hb += WAVE) {
+  int hb = A.h_lo;
+  for (; hb < A.h_hi && cnt < KL; hb += WAVE) {
     const int h = hb + lane;
-    const bool ok = h < A.H;
+    const bool ok = h < A.h_hi;
     const double a0 = ok ? A.avail[h] : -DINF;
     const double a1 = ok ? A.avail[(size_t)A.H + h] : -DINF;
     const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : -DINF;
@@ -359,7 +411,7 @@ __global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
   if (lane == 0) {
     TaskRec& r = A.L.t[task];
     r.cnt = cnt < KL ? cnt : KL;
-    r.complete = (hb >= A.H) && cnt <= KL;
+    r.complete = (hb >= A.h_hi) && cnt <= KL;
     r.anc = A.anc ? A.anc[task] : 0;
     r.ord = A.ord[task];
     r.bs = 0.0; r.btb = 0; r.bid = 0x7fffffff;   // first-fit walks never use the bound
@@ -813,8 +865,8 @@ void launch_zone_tables(const double* cost, const double* bw, int Z, double* csu
 
 // host_score_func of _first_fit (cost_aware.py:104-116): c * df / (r * bw), r = ||avail_h||.
 __global__ void key_kernel(KeyArgs A) {
-  const int h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= A.H) return;
+  const int h = A.h_lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= A.h_hi) return;
   const double a0 = A.avail[h], a1 = A.avail[(size_t)A.H + h];
   const double a2 = A.avail[2 * (size_t)A.H + h], a3 = A.avail[3 * (size_t)A.H + h];
   const double r = __builtin_sqrt(norm2_seq(a0, a1, a2, a3));
@@ -824,7 +876,7 @@ __global__ void key_kernel(KeyArgs A) {
   A.key[h] = (c * df) / (r * bw);
 }
 void launch_key(const KeyArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(key_kernel, dim3((a.H + 255) / 256), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(key_kernel, dim3((a.h_hi - a.h_lo + 255) / 256), dim3(256), 0, st, a);
 }
 
 __global__ void norm_keys_kernel(const double* dem, int T, const int32_t* idx, uint64_t* keys) {

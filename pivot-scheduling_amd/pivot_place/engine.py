@@ -46,6 +46,11 @@ def load_library(path=None):
         "pvt_last_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64),
                             ctypes.POINTER(ctypes.c_int64)], c_int),
         "pvt_last_error": ([c_void_p], ctypes.c_char_p),
+        "pvt_shard_begin": ([c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                             ctypes.POINTER(ctypes.c_int64)], c_int),
+        "pvt_shard_score": ([c_void_p, c_void_p, ctypes.POINTER(ctypes.c_int32),
+                             ctypes.POINTER(ctypes.c_int64)], c_int),
+        "pvt_shard_commit": ([c_void_p, c_void_p], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -158,6 +163,30 @@ class PlacementEngine:
         dr = DeviceRound(r, self.device)
         self.run(dr)
         return dr.result()
+
+    # -- host-dimension sharding (include/pivot_place.h, pvt_shard_*); see pivot_place.sharded
+    def shard_begin(self, dr: DeviceRound, host_lo, host_hi, world):
+        """Start a sharded round on ``dr`` (full replicated availability); returns the largest
+        per-rank package in bytes."""
+        torch = _torch()
+        stream = torch.cuda.current_stream(self.device)
+        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        mx = ctypes.c_int64()
+        self._check(self.lib.pvt_shard_begin(self.ctx, ctypes.addressof(dr.struct), int(host_lo),
+                                             int(host_hi), int(world), ctypes.byref(mx)))
+        return mx.value
+
+    def shard_score(self, package):
+        """Score the next window over this rank's hosts into ``package`` (a device uint8
+        tensor). Returns (tasks in the window, package bytes); (0, 0) when the round is done."""
+        nt, nb = ctypes.c_int32(), ctypes.c_int64()
+        self._check(self.lib.pvt_shard_score(self.ctx, ctypes.c_void_p(package.data_ptr()),
+                                             ctypes.byref(nt), ctypes.byref(nb)))
+        return nt.value, nb.value
+
+    def shard_commit(self, packages):
+        """Merge every rank's package (rank order, contiguous) and run the commit walk."""
+        self._check(self.lib.pvt_shard_commit(self.ctx, ctypes.c_void_p(packages.data_ptr())))
 
     def set_window(self, tasks):
         self._check(self.lib.pvt_set_window(self.ctx, int(tasks)))

@@ -70,3 +70,81 @@ def test_shard_blocks_cover_everything():
             assert blocks[0][0] == 0 and blocks[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(blocks, blocks[1:]))
             assert max(b - a for a, b in blocks) - min(b - a for a, b in blocks) <= 1
+
+
+# ---------------------------------------------------------------- host-dimension sharding
+class _ProtocolEngine:
+    """Stands in for PlacementEngine's pvt_shard_* calls on CPU: rank k's package for window w
+    is bytes (k, w, ...); commit checks it received every rank's package in rank order."""
+
+    device = "cpu"
+
+    def __init__(self, rank, world, windows):
+        self.rank, self.world, self.windows, self.w = rank, world, windows, 0
+        self.seen = []
+
+    def shard_begin(self, dr, lo, hi, world):
+        assert world == self.world
+        self.range = (lo, hi)
+        return 64
+
+    def shard_score(self, send):
+        if self.w >= len(self.windows):
+            return 0, 0
+        nt = self.windows[self.w]
+        nb = 4 * nt
+        send[:nb] = torch_u8([self.rank, self.w] * (nb // 2))
+        return nt, nb
+
+    def shard_commit(self, recv):
+        nb = 4 * self.windows[self.w]
+        for k in range(self.world):
+            assert recv[k * nb:(k + 1) * nb].tolist() == [k, self.w] * (nb // 2)
+        self.seen.append(nb)
+        self.w += 1
+
+
+def torch_u8(vals):
+    import torch
+    return torch.tensor(vals, dtype=torch.uint8)
+
+
+class _FakeRound:
+    class arrays:
+        n_hosts = 1001
+
+
+def _shard_worker(rank, world, port, out_q):
+    sys.path[:0] = [os.path.join(os.path.dirname(HERE), "pivot-scheduling_amd"),
+                    os.path.dirname(HERE), HERE]
+    import torch.distributed as dist
+    from pivot_place.sharded import HostShardedPlacer
+    import test_distributed as td
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        eng = td._ProtocolEngine(rank, world, [5, 16, 3])
+        placer = HostShardedPlacer.from_process_group(eng)
+        placer.run(td._FakeRound())
+        out_q.put((rank, eng.range, eng.seen, placer.windows))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_host_sharded_exchange_two_ranks():
+    """The sharded driver's per-window all-gather (gloo path) delivers every rank's package in
+    rank order, and the ranks split the hosts into contiguous ranges."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, rest) for r, *rest in (q.get(timeout=120) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][0] == (0, 501) and got[1][0] == (501, 1001)
+    for r in range(2):
+        assert got[r][1] == [20, 64, 12] and got[r][2] == 3

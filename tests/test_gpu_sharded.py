@@ -1,0 +1,134 @@
+"""GPU parity of host-dimension sharding (include/pivot_place.h pvt_shard_*).
+
+A sharded round must return exactly what the unsharded engine and the CPU restatement return:
+placements, processing order, availability after commits. ``place_lockstep`` runs W contexts
+in one process (W shards of the host range, the exchange done by concatenation), so world sizes
+up to 8 are covered on a single GPU; the two-process test runs the torch.distributed exchange
+(gloo, staged through host memory) with both ranks on cuda:0.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+import golden_io
+from oracle import oracle
+from pivot_place import _abi, synthetic
+
+pytestmark = pytest.mark.gpu
+
+SHARDED_MODES = [_abi.PVT_CA_FF, _abi.PVT_CA_BF, _abi.PVT_VBP_FF, _abi.PVT_VBP_BF]
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from pivot_place.engine import PlacementEngine
+    return [PlacementEngine(0) for _ in range(8)]
+
+
+def _assert_same(res, ref):
+    np.testing.assert_array_equal(res.placement, ref.placement)
+    np.testing.assert_array_equal(res.order, ref.order)
+    bad = np.nonzero((res.avail != ref.avail).any(axis=0))[0]
+    assert bad.size == 0, "availability differs on hosts %s" % bad[:10]
+
+
+def _lockstep(engines, world, r):
+    from pivot_place.sharded import place_lockstep
+    outs = place_lockstep(engines[:world], r)
+    for o in outs[1:]:                      # every rank holds the same result
+        _assert_same(o, outs[0])
+    return outs[0]
+
+
+@pytest.mark.parametrize("mode", SHARDED_MODES)
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70000, 120, 2), (5, 40, 3)])
+def test_sharded_matches_oracle(engines, mode, world, H, T, seed):
+    r = synthetic.make_round(mode, H, T, seed=seed)
+    _assert_same(_lockstep(engines, world, r), oracle.place(r))
+
+
+@pytest.mark.parametrize("mode", SHARDED_MODES)
+def test_sharded_crowded_and_refills(engines, mode):
+    """Nearly full identical hosts + tiny windows: exhausted packages, bounds, refills."""
+    r = synthetic.make_round(mode, 3000, 1500, seed=11)
+    r.avail[0, :] = 4.0
+    r.avail[1, :] = 40000.0
+    r.avail[0, ::7] = 0.5
+    ref = oracle.place(r)
+    try:
+        for e in engines:
+            e.set_window(37)
+        _assert_same(_lockstep(engines, 4, r), ref)
+    finally:
+        for e in engines:
+            e.set_window(0)
+
+
+@pytest.mark.parametrize("name,idx", [x for x in golden_io.all_runs() if x[0] in ("c1_sim_h100", "c2_h1000", "decay", "saturate")])
+def test_sharded_matches_reference_golden(engines, name, idx):
+    case = golden_io.load(name)
+    run = case["runs"][idx]
+    r = golden_io.run_arrays(case, run)
+    if r.mode == _abi.PVT_OPP:
+        pytest.skip("opportunistic rounds are scenario-sharded, not host-sharded")
+    placement, order, avail = golden_io.expected(case, run)[:3]
+    res = _lockstep(engines, 3, r)
+    np.testing.assert_array_equal(res.placement, placement)
+    np.testing.assert_array_equal(res.order, order)
+    np.testing.assert_array_equal(res.avail, avail)
+
+
+def test_opportunistic_is_not_host_sharded(engines):
+    from pivot_place.engine import DeviceRound
+    r = synthetic.make_round(_abi.PVT_OPP, 100, 10, seed=1)
+    dr = DeviceRound(r, engines[0].device)
+    with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
+        engines[0].shard_begin(dr, 0, 50, 2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank, world, port, mode, out_q):
+    sys.path[:0] = [os.path.join(os.path.dirname(HERE), "pivot-scheduling_amd"), os.path.dirname(HERE)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from pivot_place.engine import PlacementEngine
+    from pivot_place.sharded import HostShardedPlacer
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        placer = HostShardedPlacer.from_process_group(PlacementEngine(0))
+        res = placer.place(synthetic.make_round(mode, 20000, 400, seed=5))
+        out_q.put((rank, res.placement.tolist(), res.avail.tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_VBP_FF])
+def test_two_process_group_on_one_gpu(mode):
+    import torch.multiprocessing as mp
+    ref = oracle.place(synthetic.make_round(mode, 20000, 400, seed=5))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(k, 2, port, mode, q)) for k in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((k, (pl, av)) for k, pl, av in (q.get(timeout=100) for _ in procs))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for k in range(2):
+        assert got[k][0] == ref.placement.tolist()
+        assert got[k][1] == ref.avail.tobytes()
