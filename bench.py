@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--tasks", type=int, default=10_000)
     p.add_argument("--seed", type=int, default=20261015)
     p.add_argument("--window", type=int, default=0)
+    p.add_argument("--pipeline", type=int, default=1,
+                   help="1: score window k+1 while window k is walked (default); 0: sequential")
     p.add_argument("--shard", default="scenarios", choices=["scenarios", "hosts"],
                    help="N > 1: independent scenario per rank (weak scaling, config 4) or one "
                         "round with its host dimension split over the ranks (strong, config 5)")
@@ -94,6 +96,7 @@ def main():
     hosts_sharded = args.shard == "hosts"
     r = synthetic.make_round(mode, H, T, seed=args.seed + (0 if hosts_sharded else rank))
     eng = PlacementEngine(local, window=args.window)
+    eng.set_pipeline(bool(args.pipeline))
     dr = DeviceRound(r, eng.device)
     run = eng.run
     if hosts_sharded:

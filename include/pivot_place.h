@@ -126,6 +126,9 @@ int  pvt_reset_kstats(pvt_ctx* ctx);
 int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
 /* Tuning knob: tasks per window (0 = the policy's default; capped at 1024). */
 int  pvt_set_window(pvt_ctx* ctx, int tasks);
+/* Window pipelining (default on): score window k+1 on a side stream while window k is walked.
+ * Results are identical either way; off runs windows strictly one after the other. */
+int  pvt_set_pipeline(pvt_ctx* ctx, int on);
 /* Counters of the last pvt_place call: windows run and refills forced by exhausted lists. */
 int  pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills);
 /*

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -47,11 +48,16 @@ struct RoundState {
   size_t g = 0, ngroups = 0;
   int key_group = -1;             // group whose frozen first-fit key is computed
   int t0 = 0, W = 0, Wmax = 0, nt = 0;
+  int lb = 0;                     // list buffer of the current window
 };
 
 struct pvt_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
+  hipStream_t side = nullptr;     // scores the next window while the current one is walked
+  hipEvent_t ev_lists = nullptr;
+  uint32_t* walk_flag = nullptr;  // device: sequence number of the last walk that started
+  uint32_t walk_seq = 0;
   std::string err;
   int window = 0;                 // 0: per-policy default
   int64_t windows = 0, refills = 0;
@@ -61,7 +67,8 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_e, l_ids, l_t, next, opp, pkg;
+      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2];
+  int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
   RoundState rs;
   int32_t* next_host = nullptr;   // pinned
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
@@ -120,15 +127,17 @@ static hipEvent_t take_event(pvt_ctx* ctx) {
 }
 struct Scope {
   pvt_ctx* ctx;
+  hipStream_t st;
   TimedLaunch t;
-  Scope(pvt_ctx* c, int kclass, double cand, double bytes) : ctx(c) {
+  Scope(pvt_ctx* c, int kclass, double cand, double bytes, hipStream_t s = nullptr)
+      : ctx(c), st(s ? s : c->stream) {
     t.kclass = kclass; t.candidates = cand; t.bytes = bytes; t.a = t.b = nullptr;
-    if (ctx->profiling) { t.a = take_event(ctx); (void)hipEventRecord(t.a, ctx->stream); }
+    if (ctx->profiling) { t.a = take_event(ctx); (void)hipEventRecord(t.a, st); }
   }
   ~Scope() {
     if (ctx->profiling) {
       t.b = take_event(ctx);
-      (void)hipEventRecord(t.b, ctx->stream);
+      (void)hipEventRecord(t.b, st);
       ctx->pending.push_back(t);
     }
   }
@@ -161,6 +170,10 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   std::memset(ctx->ks, 0, sizeof(ctx->ks));
   if (hipSetDevice(device) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void**)&ctx->walk_flag, 64) != hipSuccess ||
+      hipMemset(ctx->walk_flag, 0, 64) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_lists, hipEventDisableTiming) != hipSuccess ||
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
       hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess) {
     delete ctx;
@@ -175,14 +188,20 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   if (!ctx) return PVT_EINVAL;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   harvest(ctx);
   Buf* bufs[] = {&ctx->ord, &ctx->ord2, &ctx->keys64a, &ctx->keys64b, &ctx->keys32a, &ctx->keys32b,
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
-                 &ctx->seg, &ctx->seg_feas, &ctx->l_e, &ctx->l_ids, &ctx->l_t, &ctx->next, &ctx->opp, &ctx->pkg};
+                 &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
+                 &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
+                 &ctx->owned[0], &ctx->owned[1]};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->next_host) (void)hipHostFree(ctx->next_host);
+  if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->walk_flag) (void)hipFree(ctx->walk_flag);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return PVT_OK;
@@ -218,6 +237,11 @@ extern "C" int pvt_set_window(pvt_ctx* ctx, int tasks) {
   ctx->window = std::min(tasks, MAX_WINDOW);
   return PVT_OK;
 }
+extern "C" int pvt_set_pipeline(pvt_ctx* ctx, int on) {
+  if (!ctx) return PVT_EINVAL;
+  ctx->pipeline = on != 0;
+  return PVT_OK;
+}
 extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) {
   if (!ctx) return PVT_EINVAL;
   if (windows) *windows = ctx->windows;
@@ -248,15 +272,14 @@ extern "C" const char* pvt_last_error(pvt_ctx* ctx) { return ctx ? ctx->err.c_st
 // the window is short, at least 4096 hosts per segment, a multiple of 8 (one XCD per
 // blockIdx % 8), capped by the segment-list scratch.
 static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
-static void choose_segments(int H, int nt, int* S_out, int* len_out) {
+static int choose_segments(int H, int nt) {
   const int task_waves = (nt + TW - 1) / TW;
   int S = (4096 + task_waves - 1) / task_waves;
   S = std::min(S, std::max(1, H / 4096));
   S = std::min(S, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL)));
   S = std::max(1, std::min(S, 256));
   if (S >= 8) S = S / 8 * 8;
-  *S_out = S;
-  *len_out = ((H + S - 1) / S + WAVE - 1) / WAVE * WAVE;
+  return S;
 }
 static double bytes_per_candidate(int mode) {
   // cost_aware 36 B (4 x fp64 avail + int32 zone); vbp best-fit 36 B
@@ -325,10 +348,10 @@ static int check_round(pvt_ctx* ctx, const pvt_round* r) {
   return PVT_OK;
 }
 
-static void lists_from(pvt_ctx* ctx, Lists& L) {
-  L.e = P<ListEntry>(ctx->l_e);
-  L.ids = P<int32_t>(ctx->l_ids);
-  L.t = P<TaskRec>(ctx->l_t);
+static void lists_from(pvt_ctx* ctx, Lists& L, int b = 0) {
+  L.e = P<ListEntry>(ctx->l_e[b]);
+  L.ids = P<int32_t>(ctx->l_ids[b]);
+  L.t = P<TaskRec>(ctx->l_t[b]);
 }
 
 // Opportunistic: windows of OPP_MAXW tasks in caller order; count pass then commit walk. The
@@ -376,9 +399,9 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
 }
 
 // ---------------------------------------------------------------- round state machine
-// pvt_place() and the sharded calls share one resumable round: begin (order, gathers, zone
-// tables, group boundaries), then per window: lists over this context's host range, optionally
-// exchanged between ranks, then the commit walk, which advances the window.
+// pvt_place() and the sharded calls share one round: begin (order, gathers, zone tables, group
+// boundaries), then per window: candidate lists over this context's host range (optionally
+// exchanged between ranks), then the commit walk, which decides where the next window starts.
 static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int world) {
   RoundState& R = ctx->rs;
   R.active = false;
@@ -390,7 +413,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   HIPCHK(hipSetDevice(ctx->device));
   const int T = r->n_tasks, H = r->n_hosts, Z = r->n_zones;
   R.T = T; R.H = H; R.Z = Z; R.lo = lo; R.hi = hi; R.world = world;
-  R.t0 = 0; R.g = 0; R.nt = 0;
+  R.t0 = 0; R.g = 0; R.nt = 0; R.lb = 0;
   R.gstart.assign(1, 0);
   R.ganchor.clear();
   if (T == 0) { R.ngroups = 0; R.active = true; return PVT_OK; }
@@ -454,16 +477,27 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   R.W = R.Wmax;
   ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)SEG_ENTRIES_MAX);
   ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)SEG_ENTRIES_MAX / KL);
-  ENSURE(ctx->l_e, sizeof(ListEntry) * (size_t)R.Wmax * LMAX);
-  ENSURE(ctx->l_ids, sizeof(int32_t) * (size_t)R.Wmax * LMAX);
-  ENSURE(ctx->l_t, sizeof(TaskRec) * (size_t)R.Wmax);
+  for (int b = 0; b < 2; b++) {
+    ENSURE(ctx->l_e[b], sizeof(ListEntry) * (size_t)R.Wmax * LMAX);
+    ENSURE(ctx->l_ids[b], sizeof(int32_t) * (size_t)R.Wmax * LMAX);
+    ENSURE(ctx->l_t[b], sizeof(TaskRec) * (size_t)R.Wmax);
+    ENSURE(ctx->owned[b], sizeof(int32_t) * MAX_WINDOW);
+  }
   ENSURE(ctx->next, sizeof(int32_t) * 4);
   R.active = true;
   return PVT_OK;
 }
 
-// Size of the next window (0: the round is done). Computes the frozen first-fit key of this
-// context's hosts at a group start.
+// End of the group holding task t0 (keyed first-fit: windows never cross a group).
+static int group_end(const RoundState& R, int t0) {
+  if (!R.keyed) return R.T;
+  size_t g = 0;
+  while (g < R.ngroups && t0 >= R.gstart[g + 1]) g++;
+  return g < R.ngroups ? R.gstart[g + 1] : R.T;
+}
+
+// Size of the next window at R.t0 (0: the round is done). Computes the frozen first-fit key of
+// this context's hosts at a group start (cost_aware.py:118-119, on the current capacities).
 static int round_next_window(pvt_ctx* ctx, int* nt_out) {
   RoundState& R = ctx->rs;
   *nt_out = 0;
@@ -483,72 +517,142 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
   return PVT_OK;
 }
 
-// The window's exact candidate lists over hosts [lo, hi) -> ctx lists.
-static int window_lists(pvt_ctx* ctx) {
+// Exact candidate lists of tasks [t0, t0 + nt) over hosts [lo, hi) into list buffer `lb`, on
+// stream `st`.
+static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
   RoundState& R = ctx->rs;
   const pvt_round* r = &R.r;
-  hipStream_t st = ctx->stream;
-  const int nt = R.nt, t0 = R.t0, Hl = R.hi - R.lo;
+  const int Hl = R.hi - R.lo;
   ctx->windows++;
   Lists L;
-  lists_from(ctx, L);
+  lists_from(ctx, L, lb);
   const double bpc = bytes_per_candidate(r->mode);
   const double* dem_w = P<double>(ctx->dem_ord) + (size_t)t0 * 4;
   const int32_t* anc_w = P<int32_t>(ctx->anc_ord) + t0;
   if (R.ordered) {
     OrderedArgs oa{r->avail, r->zone, dem_w, anc_w, R.ord + t0, R.H, nt,
                    r->mode == PVT_CA_FF ? 1 : 0, R.lo, R.hi, L};
-    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc);
+    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
     launch_ordered(oa, st);
   } else {
-    int S, seg_len;
-    choose_segments(Hl, nt, &S, &seg_len);
+    const int S = choose_segments(Hl, nt);
     ScoreArgs sa{r->avail, r->zone, r->tiebreak, R.keyed ? P<double>(ctx->key) : nullptr,
                  dem_w, anc_w, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z, nt, S,
-                 seg_len, R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
+                 R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
     {
-      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc);
+      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
       launch_score(r->mode, sa, st);
     }
     MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
                  anc_w, R.ord + t0, R.H, nt, S, KL, L};
-    Scope sc(ctx, PVT_K_MERGE, 0, 0);
+    Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
     launch_merge(ma, st);
   }
   HIPCHK(hipGetLastError());
   return PVT_OK;
 }
 
-// Commit walk over the window; advances the round.
-static int window_commit(pvt_ctx* ctx) {
+// Launch the commit walk of tasks [t0, t0 + nt) on list buffer `lb` (inheriting n_prev hosts
+// from the other buffer's walk); status -> ctx->next_host after a sync.
+static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
   RoundState& R = ctx->rs;
   const pvt_round* r = &R.r;
   hipStream_t st = ctx->stream;
-  const int nt = R.nt, t0 = R.t0;
   Lists L;
-  lists_from(ctx, L);
+  lists_from(ctx, L, lb);
+  int32_t* status = P<int32_t>(ctx->next);
   CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
-                 P<double>(ctx->bsum), L, R.H, R.Z, nt, r->mode, r->placement,
-                 P<int32_t>(ctx->next), ctx->stamps};
+                 P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
+                 r->placement, P<int32_t>(ctx->owned[1 - lb]), n_prev, P<int32_t>(ctx->owned[lb]),
+                 status, ctx->walk_flag, ++ctx->walk_seq, ctx->stamps};
   {
     Scope sc(ctx, PVT_K_COMMIT, 0, 0);
     launch_commit(ca_, st);
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t),
-                        hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  const int adv = *ctx->next_host;
-  R.nt = 0;
-  if (adv < 0 || adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", adv, nt);
-  if (adv == 0) return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
+  HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
+  return PVT_OK;
+}
+
+// Window-size adaptation after a walk that advanced `adv` of `nt` tasks.
+static void adapt_window(pvt_ctx* ctx, int adv, int nt) {
+  RoundState& R = ctx->rs;
   if (adv < nt) {
     ctx->refills++;
     R.W = std::max(std::min(64, R.Wmax), std::min(R.Wmax, adv + adv / 2));
   } else if (nt == R.W) {
     R.W = std::min(R.Wmax, 2 * R.W);
   }
+}
+
+static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *adv = ctx->next_host[0];
+  if (*adv == -1) return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out at task %d", t0);
+  if (*adv < 0 || *adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", *adv, nt);
+  if (*adv == 0 && !inherited) return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
+  return PVT_OK;
+}
+
+// Sequential windows (sharded rounds): lists, [exchange], walk, repeat.
+static int window_commit(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  int rc, adv = 0;
+  const int nt = R.nt, t0 = R.t0;
+  if ((rc = walk_launch(ctx, t0, nt, 0, 0))) return rc;
+  R.nt = 0;
+  if ((rc = walk_status(ctx, t0, nt, false, &adv))) return rc;
+  adapt_window(ctx, adv, nt);
   R.t0 += adv;
+  return PVT_OK;
+}
+
+// pvt_place for the list policies. While window k is walked on the caller's stream, the side
+// stream scores window k+1 on the capacities as they stand (the walk of k-1 is complete; the
+// walk of k is in flight). The side stream is released by the walk kernel itself (it stores
+// its sequence number on entry; hipStreamWaitValue32): were both merely made ready by the end
+// of walk k-1, the score grid could fill every CU first and hold back the walk, which needs
+// almost all of one CU's LDS, until the grid drains. Hosts window k commits to are the only ones whose list entries can
+// be stale, so walk k+1 inherits them as touched (pvt_walk.hip) and stays exact. A walk that
+// stops early (refill) discards the speculative lists; keyed first-fit recomputes its frozen
+// key at a group start, so the pipeline drains at group boundaries.
+static int place_pipelined(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  int rc, nt = 0;
+  if ((rc = round_next_window(ctx, &nt))) return rc;
+  if (nt == 0) return PVT_OK;
+  int lb = 0, t0 = R.t0;
+  if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
+  int n_prev = 0;
+  bool inherited = false;
+  for (;;) {
+    // Walk k first; the side stream then waits until that walk has STARTED (its CU is taken,
+    // and walk k-1 is complete) before scoring window k+1 (same group) on the current state.
+    if ((rc = walk_launch(ctx, t0, nt, lb, n_prev))) return rc;
+    const int nt0 = t0 + nt, ge = group_end(R, t0);
+    const int nnt = (ctx->pipeline && nt0 < ge) ? std::min(R.W, ge - nt0) : 0;
+    if (nnt > 0) {
+      HIPCHK(hipStreamWaitValue32(ctx->side, ctx->walk_flag, ctx->walk_seq, hipStreamWaitValueGte,
+                                  0xffffffffu));
+      if ((rc = window_lists(ctx, nt0, nnt, 1 - lb, ctx->side))) return rc;
+      HIPCHK(hipEventRecord(ctx->ev_lists, ctx->side));
+    }
+    int adv = 0;
+    if ((rc = walk_status(ctx, t0, nt, inherited, &adv))) return rc;
+    const int n_own = ctx->next_host[1];
+    adapt_window(ctx, adv, nt);
+    if (adv == nt && nnt > 0) {                 // take the speculative window
+      HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_lists, 0));
+      t0 = nt0; nt = nnt; lb = 1 - lb; n_prev = n_own; inherited = true;
+      continue;
+    }
+    if (nnt > 0) HIPCHK(hipStreamSynchronize(ctx->side));   // discard the speculation
+    R.t0 = t0 + adv;
+    if ((rc = round_next_window(ctx, &nt))) return rc;
+    if (nt == 0) break;
+    t0 = R.t0; lb = 0; n_prev = 0; inherited = false;
+    if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
+  }
   return PVT_OK;
 }
 
@@ -566,13 +670,12 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
     return opp_round(ctx, r);
   }
   if ((rc = round_begin(ctx, r, 0, r->n_hosts, 1))) return rc;
-  for (;;) {
-    int nt = 0;
-    if ((rc = round_next_window(ctx, &nt))) return rc;
-    if (nt == 0) break;
-    if ((rc = window_lists(ctx)) || (rc = window_commit(ctx))) return rc;
-  }
+  rc = place_pipelined(ctx);
   ctx->rs.active = false;
+  if (rc) {
+    (void)hipStreamSynchronize(ctx->side);
+    return rc;
+  }
   HIPCHK(hipStreamSynchronize(ctx->stream));
   return PVT_OK;
 }
@@ -612,7 +715,7 @@ extern "C" int pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return PVT_OK;
   }
-  if ((rc = window_lists(ctx))) return rc;
+  if ((rc = window_lists(ctx, ctx->rs.t0, nt, 0, ctx->stream))) return rc;
   const int PK = shard_depth(ctx->rs.world);
   Lists L;
   lists_from(ctx, L);

@@ -33,6 +33,11 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   r.i[1] = __builtin_amdgcn_readlane(u.i[1], l);
   return r.d;
 }
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(v >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
 __device__ __forceinline__ int32_t readlane_i(int32_t v, int l) {
   return __builtin_amdgcn_readlane(v, l);
 }

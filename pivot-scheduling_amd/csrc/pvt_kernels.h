@@ -70,7 +70,7 @@ struct ScoreArgs {
   const int32_t* anc;     // window tasks [nt]
   const double* csum;
   const double* bsum;
-  int H, Z, nt, S, seg_len;
+  int H, Z, nt, S;        // S host segments: segment s = 64-host blocks s, s + S, ...
   int h_lo, h_hi;         // host range scored (a rank's shard; [0, H) unsharded)
   SegEntry* seg;          // [nt][S][KL]
   int32_t* seg_feas;      // [nt][S]
@@ -119,10 +119,20 @@ struct CommitArgs {
   const double* dem;      // window tasks [nt][4] (for the window's minimum demand)
   const double* csum;
   const double* bsum;
+  const int32_t* zone;    // host zones / tiebreak ranks (for inherited touched hosts)
+  const uint32_t* tb;     //   tb may be NULL (rank 0 for every host)
   Lists L;
   int H, Z, nt, mode;
   int32_t* placement;     // [T] in caller order
-  int32_t* next;          // out: window-local index where the walk stopped (nt = done)
+  // Hosts committed to by the previous window whose list entries in THIS window are stale
+  // (the lists were scored before that window's commits landed): treated as touched.
+  const int32_t* prev_ids;
+  int n_prev;
+  int32_t* own_ids;       // out: hosts this walk committed to (distinct), for the next window
+  int32_t* status;        // out: [0] window-local index where the walk stopped (nt = done,
+                          //      -1 = spin timeout), [1] number of own_ids
+  uint32_t* started;      // set to seq when the walk starts (releases the side stream)
+  uint32_t seq;
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
 };
 

@@ -68,7 +68,12 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   const int t0 = (tile * WPB + wave) * TW;
   if (t0 >= A.nt) return;
   const int nt = min(TW, A.nt - t0);
-  const int hb0 = A.h_lo + seg * A.seg_len, hb1 = min(A.h_hi, hb0 + A.seg_len);
+  // Segment `seg` owns the 64-host blocks seg, seg + S, seg + 2S, ... of [h_lo, h_hi): each
+  // block is one coalesced load per component, and interleaving keeps every segment's share of
+  // low host indices equal, so lists stay deep when many hosts tie (zero-cost zones, where the
+  // index breaks the tie) -- contiguous segments would bound the merged list at segment 0's
+  // 64th tied host.
+  const int hb0 = A.h_lo + seg * WAVE, hb1 = A.h_hi, hstep = A.S * WAVE;
 
   double d0[TW], d1[TW], d2[TW], d3[TW];
   double ls[TW], ts[TW], lim[TW];
@@ -110,14 +115,14 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
     if (MODE == CA_FF) nkey = A.key[h];
   };
   if (hb0 < hb1) fetch(hb0);
-  for (int hb = hb0; hb < hb1; hb += WAVE) {
+  for (int hb = hb0; hb < hb1; hb += hstep) {
     const int h = hb + lane;
     const bool ok = h < hb1;
     const double a0 = ok ? n0 : -DINF;
     const double a1 = n1, a2 = n2, a3 = n3;
     const int z = nz;
     const double key = nkey;
-    if (hb + WAVE < hb1) fetch(hb + WAVE);
+    if (hb + hstep < hb1) fetch(hb + hstep);
 #pragma unroll
     for (int k = 0; k < TW; k++) {
       const bool fit = fits<STRICT>(a0, a1, a2, a3, d0[k], d1[k], d2[k], d3[k]);
@@ -422,428 +427,6 @@ void launch_ordered(const OrderedArgs& a, hipStream_t st) {
   dim3 grid((a.nt + 3) / 4), block(256);
   if (a.strict) hipLaunchKernelGGL(ordered_kernel<true>, grid, block, 0, st, a);
   else hipLaunchKernelGGL(ordered_kernel<false>, grid, block, 0, st, a);
-}
-
-// ------------------------------------------------------------------------------------------
-// Commit walk: one wave visits the window's tasks in processing order and applies the
-// reference's sequential semantics. Hosts committed to in this window ("touched") live in LDS
-// with their current availability; every other host still has its snapshot state, so its list
-// entry (score, feasibility) is exact. Best-fit: winner = min(first untouched list entry,
-// rescored touched hosts). First-fit: first list entry that is still feasible. A list whose
-// entries are all touched and that may be missing hosts ("not complete") stops the walk; the
-// host side then starts a new window there (a refill).
-// ------------------------------------------------------------------------------------------
-constexpr int HASH_SLOTS = 1 << HASH_BITS;
-constexpr int PREFETCH = 3;      // commit walk: task lists loaded this many tasks ahead
-
-struct CommitLDS {
-  int32_t hkey[HASH_SLOTS];
-  int32_t hval[HASH_SLOTS];
-  int32_t tid[MAX_WINDOW];       // touched slot -> host
-  int32_t tz[MAX_WINDOW];
-  uint32_t ttb[MAX_WINDOW];
-  int32_t lpos[MAX_WINDOW];      // touched slot -> position in the live list (-1: dead)
-  double ta[4][MAX_WINDOW];      // current availability of touched hosts
-  // live list: touched hosts that can still fit some task of the window, stored contiguously
-  double la[4][MAX_WINDOW];
-  int32_t lid[MAX_WINDOW];
-  int32_t lz[MAX_WINDOW];
-  uint32_t ltb[MAX_WINDOW];
-  int32_t lslot[MAX_WINDOW];
-  double csum[ZMAX * ZMAX];
-  double bsum[ZMAX * ZMAX];
-  double lim[ZMAX];
-};
-
-static_assert(sizeof(CommitLDS) <= 160 * 1024, "commit walk LDS exceeds a CU's 160 KiB");
-
-__device__ __forceinline__ uint32_t hslot(int32_t id) {
-  return ((uint32_t)id * 2654435761u) >> (32 - HASH_BITS);
-}
-__device__ __forceinline__ int hash_find(const CommitLDS& S, int32_t id) {
-  uint32_t p = hslot(id);
-  for (;;) {
-    const int32_t k = S.hkey[p];
-    if (k == id) return S.hval[p];
-    if (k < 0) return -1;
-    p = (p + 1) & (HASH_SLOTS - 1);
-  }
-}
-__device__ __forceinline__ void hash_put(CommitLDS& S, int32_t id, int32_t v) {
-  uint32_t p = hslot(id);
-  while (S.hkey[p] >= 0) p = (p + 1) & (HASH_SLOTS - 1);
-  S.hkey[p] = id;
-  S.hval[p] = v;
-}
-
-constexpr double ZERO_ZONE = -2.0;   // lim-table marker: score is exactly 0 in this zone
-constexpr int SCAN_UNROLL = 4;       // live hosts rescored per lane per loop trip
-
-// One task's candidate list: this lane's entry, plus the task record spread over lanes 0-11
-// (a vector load, so no scalar-memory wait is ever mixed with the LDS traffic of the walk).
-struct Cand {
-  ListEntry e;                 // entry `lane` of chunk 0
-  int32_t tv;                  // TaskRec dword `lane` (lanes 0-15)
-  int32_t ids[LMAX / KL - 1];  // host ids of entries 64*c + lane, c = 1..15
-};
-__device__ __forceinline__ void load_cand(const CommitArgs& A, int i, int lane, Cand& c) {
-  c.e = A.L.e[(size_t)i * LMAX + lane];
-  c.tv = reinterpret_cast<const int32_t*>(A.L.t + i)[lane < 16 ? lane : 0];
-#pragma unroll
-  for (int k = 0; k < LMAX / KL - 1; k++) c.ids[k] = A.L.ids[(size_t)i * LMAX + (k + 1) * KL + lane];
-}
-__device__ __forceinline__ double tv_d(int32_t tv, int k) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane(tv, 2 * k);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane(tv, 2 * k + 1);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-#ifdef PVT_STAMPS
-// Diagnostic build only (make stamps): per-phase cycle sums of the commit walk.
-__device__ __forceinline__ uint64_t stamp() {
-  uint64_t t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define STAMP(k)                          \
-  do {                                    \
-    const uint64_t t_ = stamp();          \
-    ph[k] += t_ - tl;                     \
-    tl = t_;                              \
-  } while (0)
-#else
-#define STAMP(k) do {} while (0)
-#endif
-
-template <int MODE>
-__global__ __launch_bounds__(64) void commit_kernel(CommitArgs A) {
-  constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
-  constexpr bool BEST = (MODE == CA_BF || MODE == VBP_BF);
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  CommitLDS& S = *reinterpret_cast<CommitLDS*>(smem);
-  const int lane = lane_id();
-  for (int i = lane; i < HASH_SLOTS; i += WAVE) S.hkey[i] = -1;
-  if (MODE == CA_BF)
-    for (int i = lane; i < A.Z * A.Z; i += WAVE) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
-  // Componentwise minimum demand of the window: a touched host that cannot fit it can never
-  // win again in this window, so it leaves the live (rescoring) list.
-  double m0 = DINF, m1 = DINF, m2 = DINF, m3 = DINF;
-  if (BEST) {
-    for (int i = lane; i < A.nt; i += WAVE) {
-      const double* dp = A.dem + (size_t)i * 4;
-      m0 = fmin(m0, dp[0]); m1 = fmin(m1, dp[1]); m2 = fmin(m2, dp[2]); m3 = fmin(m3, dp[3]);
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-      m0 = fmin(m0, __shfl_xor(m0, off)); m1 = fmin(m1, __shfl_xor(m1, off));
-      m2 = fmin(m2, __shfl_xor(m2, off)); m3 = fmin(m3, __shfl_xor(m3, off));
-    }
-  }
-  int m = 0;               // touched hosts (uniform)
-  int nl = 0;              // live touched hosts (uniform)
-  int next = A.nt;
-
-#ifdef PVT_STAMPS
-  uint64_t ph[5] = {0, 0, 0, 0, 0};
-  uint64_t nl_sum = 0;
-  uint64_t tl = stamp();
-#endif
-  // Lists are loaded PREFETCH tasks ahead into a ring of register sets that is never copied
-  // (a copy would wait for the youngest load): the walk is unrolled by PREFETCH and each step
-  // refills the set it just consumed.
-  Cand c0, c1, c2;
-  if (0 < A.nt) load_cand(A, 0, lane, c0);
-  if (1 < A.nt) load_cand(A, 1, lane, c1);
-  if (2 < A.nt) load_cand(A, 2, lane, c2);
-  // step(cur, i): walk task i; returns true when the walk must stop (refill).
-  auto step = [&](Cand& cur, const int i) -> bool {
-    const double d0 = tv_d(cur.tv, 0), d1 = tv_d(cur.tv, 1), d2 = tv_d(cur.tv, 2), d3 = tv_d(cur.tv, 3);
-    const int cnt = __builtin_amdgcn_readlane(cur.tv, 8);
-    const bool comp = __builtin_amdgcn_readlane(cur.tv, 9) != 0;
-    const int anc = __builtin_amdgcn_readlane(cur.tv, 10);
-    const int caller = __builtin_amdgcn_readlane(cur.tv, 11);
-    const bool valid = lane < cnt;
-    STAMP(0);
-    const int slot = valid ? hash_find(S, cur.e.id) : -1;
-    STAMP(1);
-
-    int w_id = -1, w_slot = -1, w_z = 0;
-    uint32_t w_tb = 0;
-    double w0 = 0, w1 = 0, w2 = 0, w3 = 0;
-    // The first usable list entry: chunk 0 is in registers; deeper chunks are searched by id
-    // (LDS hash probes) and only the winning entry is then read from memory.
-    int uc = -1, ul = -1;                // chunk and lane of the first usable entry
-    {
-      const bool ok0 = BEST ? (valid && slot < 0)
-                            : (valid && (slot < 0 || fits<STRICT>(S.ta[0][max(slot, 0)], S.ta[1][max(slot, 0)],
-                                                                  S.ta[2][max(slot, 0)], S.ta[3][max(slot, 0)],
-                                                                  d0, d1, d2, d3)));
-      const uint64_t m0 = __ballot(ok0);
-      if (m0) {
-        uc = 0;
-        ul = __builtin_ctzll(m0);
-      } else {
-#pragma unroll
-        for (int c = 1; c < LMAX / KL; c++) {
-          if (uc < 0 && c * KL < cnt) {
-            const bool v = c * KL + lane < cnt;
-            const int sl = v ? hash_find(S, cur.ids[c - 1]) : -1;
-            const bool ok = BEST ? (v && sl < 0)
-                                 : (v && (sl < 0 || fits<STRICT>(S.ta[0][max(sl, 0)], S.ta[1][max(sl, 0)],
-                                                                 S.ta[2][max(sl, 0)], S.ta[3][max(sl, 0)],
-                                                                 d0, d1, d2, d3)));
-            const uint64_t mc = __ballot(ok);
-            if (mc) { uc = c; ul = __builtin_ctzll(mc); }
-          }
-        }
-      }
-    }
-    // the usable entry's fields (uniform)
-    double us = DINF, ua0 = 0, ua1 = 0, ua2 = 0, ua3 = 0;
-    uint32_t utb = 0xffffffffu;
-    int32_t uid = 0x7fffffff, uz = 0, uslot = -1;
-    if (uc == 0) {
-      us = readlane_d(cur.e.s, ul); utb = readlane_u(cur.e.tb, ul); uid = readlane_i(cur.e.id, ul);
-      uz = readlane_i(cur.e.zone, ul); uslot = readlane_i(slot, ul);
-      ua0 = readlane_d(cur.e.a[0], ul); ua1 = readlane_d(cur.e.a[1], ul);
-      ua2 = readlane_d(cur.e.a[2], ul); ua3 = readlane_d(cur.e.a[3], ul);
-    } else if (uc > 0) {
-      const ListEntry& ue = A.L.e[(size_t)i * LMAX + uc * KL + ul];
-      us = ue.s; utb = ue.tb; uid = ue.id; uz = ue.zone;
-      ua0 = ue.a[0]; ua1 = ue.a[1]; ua2 = ue.a[2]; ua3 = ue.a[3];
-      uslot = BEST ? -1 : hash_find(S, uid);
-      uslot = __builtin_amdgcn_readfirstlane(uslot);
-    }
-
-    if (BEST) {
-      // No untouched entry and hosts missing from the list: every untouched host outside the
-      // list ranks at or after the bound, so a touched host at or before it still wins exactly;
-      // only if none does must the walk stop for a refill. (bi = bid + 1 turns the strict
-      // comparisons below into <= bound; ids are unique, so equality means the same host.)
-      const bool exhausted = (uc < 0) && !comp;
-      double bs = us;
-      uint32_t bt = utb;
-      int32_t bi = uid;
-      if (exhausted) {
-        bs = tv_d(cur.tv, 6);
-        bt = (uint32_t)__builtin_amdgcn_readlane(cur.tv, 14);
-        bi = __builtin_amdgcn_readlane(cur.tv, 15) + 1;
-      }
-      int bq = -1;                       // live position of the winner
-      STAMP(2);
-#ifdef PVT_STAMPS
-      nl_sum += nl;
-#endif
-      if (MODE == CA_BF && nl > 0 && bs == 0.0) {
-        // Best untouched score is exactly 0 (a zero-cost zone). A live host can only win with
-        // score 0 and a lower index: either it sits in a zero-cost zone, or its residual is
-        // exactly zero. Every such candidate scores 0, so the winner is the lowest index.
-        const uint32_t zz = (uint32_t)__ballot(lane < A.Z && S.csum[anc * A.Z + lane] == 0.0);
-        int best = 0x7fffffff, bestq = -1;
-        for (int q0 = 0; q0 < nl; q0 += WAVE * SCAN_UNROLL) {
-#pragma unroll
-          for (int u = 0; u < SCAN_UNROLL; u++) {
-            const int j = q0 + u * WAVE + lane;
-            const int jj = min(j, nl - 1);
-            const double a0 = S.la[0][jj], a1 = S.la[1][jj], a2 = S.la[2][jj], a3 = S.la[3][jj];
-            const int32_t id = S.lid[jj];
-            const bool zero_zone = (zz >> S.lz[jj]) & 1u;
-            const bool pass = (j < nl) && id < bi && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3) &&
-                              (zero_zone || (a0 == d0 && a1 == d1 && a2 == d2 && a3 == d3));
-            if (pass && id < best) { best = id; bestq = j; }
-          }
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-          const int ob = __shfl_xor(best, off), oq = __shfl_xor(bestq, off);
-          if (ob < best) { best = ob; bestq = oq; }
-        }
-        if (best < bi) { bs = 0.0; bt = 0; bi = best; bq = bestq; }
-      } else if (nl > 0) {
-        double vlim = DINF;
-        if (MODE == CA_BF) {
-          if (lane < A.Z) {
-            const double c = S.csum[anc * A.Z + lane];
-            S.lim[lane] = (c == 0.0) ? ZERO_ZONE : ca_lim(bs, c, S.bsum[anc * A.Z + lane]);
-          }
-        } else {
-          vlim = vbp_lim(bs);
-        }
-        for (int q0 = 0; q0 < nl; q0 += WAVE * SCAN_UNROLL) {
-          double s2[SCAN_UNROLL];
-          bool pass[SCAN_UNROLL];
-          int z[SCAN_UNROLL];
-          bool any = false;
-#pragma unroll
-          for (int u = 0; u < SCAN_UNROLL; u++) {
-            const int j = q0 + u * WAVE + lane;
-            const int jj = min(j, nl - 1);
-            const double a0 = S.la[0][jj], a1 = S.la[1][jj], a2 = S.la[2][jj], a3 = S.la[3][jj];
-            const bool fit = (j < nl) && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
-            s2[u] = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
-            if (MODE == CA_BF) {
-              z[u] = S.lz[jj];
-              const double lm = S.lim[z[u]];
-              pass[u] = fit && ((lm == ZERO_ZONE) ? lexless(0.0, 0u, S.lid[jj], bs, bt, bi) : (s2[u] <= lm));
-            } else {
-              z[u] = 0;
-              pass[u] = fit && (s2[u] <= vlim);
-            }
-            any |= pass[u];
-          }
-          if (__ballot(any) == 0) continue;
-          double cs = DINF;
-          uint32_t ct = 0xffffffffu;
-          int32_t ci = 0x7fffffff;
-          int cq = -1;
-#pragma unroll
-          for (int u = 0; u < SCAN_UNROLL; u++) {
-            if (!pass[u]) continue;
-            const int j = q0 + u * WAVE + lane;
-            double sc;
-            uint32_t tb;
-            if (MODE == CA_BF) {
-              const double c = S.csum[anc * A.Z + z[u]];
-              // (c * r) / b as the reference computes it; c == 0 gives exactly 0
-              sc = (c == 0.0) ? 0.0 : (c * __builtin_sqrt(s2[u])) / S.bsum[anc * A.Z + z[u]];
-              tb = 0;
-            } else {
-              sc = __builtin_sqrt(s2[u]);
-              tb = S.ltb[j];
-            }
-            const int32_t id = S.lid[j];
-            if (lexless(sc, tb, id, cs, ct, ci)) { cs = sc; ct = tb; ci = id; cq = j; }
-          }
-          for (int off = 32; off > 0; off >>= 1) {
-            const double os = __shfl_xor(cs, off);
-            const uint32_t ot = (uint32_t)__shfl_xor((int)ct, off);
-            const int32_t oi = __shfl_xor(ci, off);
-            const int oq = __shfl_xor(cq, off);
-            if (lexless(os, ot, oi, cs, ct, ci)) { cs = os; ct = ot; ci = oi; cq = oq; }
-          }
-          if (lexless(cs, ct, ci, bs, bt, bi)) { bs = cs; bt = ct; bi = ci; bq = cq; }
-        }
-      }
-      STAMP(3);
-      if (exhausted && bq < 0) { next = i; return true; }
-      if (bi == 0x7fffffff || (exhausted && bq < 0)) {   // no feasible host: the task waits
-        if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
-        return false;
-      }
-      w_id = bi;
-      w_tb = bt;
-      if (bq >= 0) {
-        w_slot = S.lslot[bq];
-        w0 = S.la[0][bq]; w1 = S.la[1][bq]; w2 = S.la[2][bq]; w3 = S.la[3][bq];
-      } else {
-        w_z = uz;
-        w0 = ua0; w1 = ua1; w2 = ua2; w3 = ua3;
-      }
-    } else {
-      if (uc < 0) {
-        if (!comp) { next = i; return true; }
-        if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
-        return false;
-      }
-      w_id = uid;
-      w_slot = uslot;
-      if (w_slot >= 0) {
-        w0 = S.ta[0][w_slot]; w1 = S.ta[1][w_slot]; w2 = S.ta[2][w_slot]; w3 = S.ta[3][w_slot];
-      } else {
-        w_z = uz;
-        w0 = ua0; w1 = ua1; w2 = ua2; w3 = ua3;
-      }
-    }
-    // commit: resc[h] -= t_demand (cost_aware.py:95,126; vbp.py:24,49)
-    const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
-    if (w_slot < 0) {
-      w_slot = m++;
-      if (lane == 0) {
-        hash_put(S, w_id, w_slot);
-        S.tid[w_slot] = w_id;
-        S.tz[w_slot] = w_z;
-        S.ttb[w_slot] = w_tb;
-        S.lpos[w_slot] = -1;
-      }
-    }
-    if (BEST) {
-      const bool alive = fits<STRICT>(n0, n1, n2, n3, m0, m1, m2, m3);
-      const int p = __builtin_amdgcn_readfirstlane(S.lpos[w_slot]);
-      if (alive) {
-        const int q = (p >= 0) ? p : nl++;
-        if (lane == 0) {
-          S.la[0][q] = n0; S.la[1][q] = n1; S.la[2][q] = n2; S.la[3][q] = n3;
-          if (p < 0) {
-            S.lid[q] = w_id; S.lz[q] = S.tz[w_slot]; S.ltb[q] = w_tb; S.lslot[q] = w_slot;
-            S.lpos[w_slot] = q;
-          }
-        }
-      } else if (p >= 0) {               // swap-remove from the live list
-        nl--;
-        if (lane == 0 && p != nl) {
-          S.la[0][p] = S.la[0][nl]; S.la[1][p] = S.la[1][nl];
-          S.la[2][p] = S.la[2][nl]; S.la[3][p] = S.la[3][nl];
-          S.lid[p] = S.lid[nl]; S.lz[p] = S.lz[nl]; S.ltb[p] = S.ltb[nl];
-          S.lslot[p] = S.lslot[nl];
-          S.lpos[S.lslot[nl]] = p;
-        }
-        if (lane == 0) S.lpos[w_slot] = -1;
-      }
-    }
-    if (lane == 0) {
-      S.ta[0][w_slot] = n0; S.ta[1][w_slot] = n1; S.ta[2][w_slot] = n2; S.ta[3][w_slot] = n3;
-      A.avail[w_id] = n0;
-      A.avail[(size_t)A.H + w_id] = n1;
-      A.avail[2 * (size_t)A.H + w_id] = n2;
-      A.avail[3 * (size_t)A.H + w_id] = n3;
-      A.placement[caller] = w_id;
-    }
-    STAMP(4);
-    if (i + PREFETCH < A.nt) load_cand(A, i + PREFETCH, lane, cur);
-    return false;
-  };
-  for (int i = 0; i < A.nt;) {
-    if (step(c0, i)) break;
-    if (++i >= A.nt) break;
-    if (step(c1, i)) break;
-    if (++i >= A.nt) break;
-    if (step(c2, i)) break;
-    ++i;
-  }
-  if (lane == 0) *A.next = next;
-#ifdef PVT_STAMPS
-  if (lane == 0 && A.stamps)
-    for (int k = 0; k < 5; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
-  if (lane == 0 && A.stamps) atomicAdd((unsigned long long*)&A.stamps[5], (unsigned long long)A.nt);
-  if (lane == 0 && A.stamps) atomicAdd((unsigned long long*)&A.stamps[6], (unsigned long long)nl_sum);
-#endif
-}
-
-size_t commit_lds_bytes() { return sizeof(CommitLDS); }
-
-hipError_t init_kernel_attrs() {
-  const int lds = (int)sizeof(CommitLDS);
-  hipError_t e = hipSuccess, r;
-  r = hipFuncSetAttribute((const void*)commit_kernel<CA_FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (r != hipSuccess) e = r;
-  r = hipFuncSetAttribute((const void*)commit_kernel<CA_BF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (r != hipSuccess) e = r;
-  r = hipFuncSetAttribute((const void*)commit_kernel<VBP_FF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (r != hipSuccess) e = r;
-  r = hipFuncSetAttribute((const void*)commit_kernel<VBP_BF>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (r != hipSuccess) e = r;
-  return e;
-}
-
-void launch_commit(const CommitArgs& a, hipStream_t st) {
-  const size_t lds = sizeof(CommitLDS);
-  switch (a.mode) {
-    case CA_FF: hipLaunchKernelGGL(commit_kernel<CA_FF>, dim3(1), dim3(64), lds, st, a); break;
-    case CA_BF: hipLaunchKernelGGL(commit_kernel<CA_BF>, dim3(1), dim3(64), lds, st, a); break;
-    case VBP_FF: hipLaunchKernelGGL(commit_kernel<VBP_FF>, dim3(1), dim3(64), lds, st, a); break;
-    case VBP_BF: hipLaunchKernelGGL(commit_kernel<VBP_BF>, dim3(1), dim3(64), lds, st, a); break;
-    default: break;
-  }
 }
 
 // ------------------------------------------------------------------------------------------

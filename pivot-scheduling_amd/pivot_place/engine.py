@@ -43,6 +43,7 @@ def load_library(path=None):
         "pvt_reset_kstats": ([c_void_p], c_int),
         "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_set_window": ([c_void_p, c_int], c_int),
+        "pvt_set_pipeline": ([c_void_p, c_int], c_int),
         "pvt_last_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64),
                             ctypes.POINTER(ctypes.c_int64)], c_int),
         "pvt_last_error": ([c_void_p], ctypes.c_char_p),
@@ -190,6 +191,9 @@ class PlacementEngine:
 
     def set_window(self, tasks):
         self._check(self.lib.pvt_set_window(self.ctx, int(tasks)))
+
+    def set_pipeline(self, on=True):
+        self._check(self.lib.pvt_set_pipeline(self.ctx, int(bool(on))))
 
     def set_profiling(self, on=True):
         self._check(self.lib.pvt_set_profiling(self.ctx, int(bool(on))))

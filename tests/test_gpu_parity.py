@@ -79,3 +79,35 @@ def test_sqrt_and_division_are_correctly_rounded(engine):
     ref = oracle.place(r)
     res = engine.place(r)
     _assert_same(res, ref.placement, ref.order, ref.avail)
+
+
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_FF, _abi.PVT_CA_BF, _abi.PVT_VBP_FF, _abi.PVT_VBP_BF])
+def test_pipelined_windows_match_oracle(engine, mode):
+    """Several full windows, each scored while the previous one is walked (inherited touched
+    hosts), must equal the CPU restatement and the strictly sequential schedule."""
+    r = synthetic.make_round(mode, 100_000, 2600, seed=21)
+    ref = oracle.place(r)
+    res = engine.place(r)
+    _assert_same(res, ref.placement, ref.order, ref.avail)
+    try:
+        engine.set_pipeline(False)
+        seq = engine.place(r)
+    finally:
+        engine.set_pipeline(True)
+    _assert_same(seq, ref.placement, ref.order, ref.avail)
+
+
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_VBP_BF, _abi.PVT_CA_FF])
+@pytest.mark.parametrize("window", [96, 333])
+def test_pipelined_crowded_small_windows(engine, mode, window):
+    """Crowded hosts and short windows: many windows inherit many touched hosts."""
+    r = synthetic.make_round(mode, 2000, 4000, seed=13)
+    r.avail[0, :] = 6.0
+    r.avail[1, :] = 60000.0
+    ref = oracle.place(r)
+    try:
+        engine.set_window(window)
+        res = engine.place(r)
+    finally:
+        engine.set_window(0)
+    _assert_same(res, ref.placement, ref.order, ref.avail)
