@@ -275,6 +275,7 @@ static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
 static int choose_segments(int H, int nt) {
   const int task_waves = (nt + TW - 1) / TW;
   int S = (4096 + task_waves - 1) / task_waves;
+  if (const char* e = getenv("PVT_SEGMENTS")) S = std::max(1, atoi(e));   // tuning experiments
   S = std::min(S, std::max(1, H / 4096));
   S = std::min(S, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL)));
   S = std::max(1, std::min(S, 256));

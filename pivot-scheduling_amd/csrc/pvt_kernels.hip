@@ -55,11 +55,23 @@ __device__ __forceinline__ void list_insert(double& s, uint32_t& t, int32_t& i, 
 // list per task in registers. blockIdx % S picks the segment, so with S = 8 the blocks of one
 // segment share an XCD (round-robin dispatch) and its L2 holds that slice of the host table.
 // ------------------------------------------------------------------------------------------
+// Radius on the memory dimension implied by a squared-norm limit: an exact pass (fl(s2) <= lim,
+// s2 the FMA chain, every term >= 0, so fl(s2) >= fl(x1*x1)) implies |fl(a1 - d1)| <= rad(lim).
+// This one subtract-and-compare rejects nearly every candidate once a task's list has filled
+// (the best residuals are small next to the spread of host memory); only survivors pay for the
+// four-dimensional fit, the residual norm and the exact limit.
+__device__ __forceinline__ double rad(double lim) {
+  if (!(lim < DINF)) return DINF;
+  if (lim < 0.0) return -1.0;
+  return __builtin_sqrt(lim) * (1.0 + 0x1p-40);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   constexpr bool STRICT = (MODE != CA_BF);
   constexpr int ZL = (MODE == CA_BF) ? ZMAX : 1;
   __shared__ double s_lim[WPB][TW][ZL];
+  __shared__ double s_rad[WPB][TW][ZL];
   __shared__ double s_c[WPB][TW][ZL];
   __shared__ double s_b[WPB][TW][ZL];
 
@@ -76,9 +88,9 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   const int hb0 = A.h_lo + seg * WAVE, hb1 = A.h_hi, hstep = A.S * WAVE;
 
   double d0[TW], d1[TW], d2[TW], d3[TW];
-  double ls[TW], ts[TW], lim[TW];
+  double ls[TW], ts[TW], lim[TW], rd[TW];
   uint32_t lt[TW], tt[TW];
-  int32_t li[TW], ti[TW], feas[TW];
+  int32_t li[TW], ti[TW];
 #pragma unroll
   for (int k = 0; k < TW; k++) {
     if (k < nt) {
@@ -90,13 +102,14 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
     ls[k] = DINF; lt[k] = 0xffffffffu; li[k] = 0x7fffffff;
     ts[k] = DINF; tt[k] = 0xffffffffu; ti[k] = 0x7fffffff;
     lim[k] = DINF;
-    feas[k] = 0;
+    rd[k] = (k < nt) ? DINF : -1.0;        // a missing task never passes the prefilter
     if (MODE == CA_BF) {
       const int a = (k < nt) ? A.anc[t0 + k] : 0;
       if (lane < A.Z) {
         s_c[wave][k][lane] = A.csum[a * A.Z + lane];
         s_b[wave][k][lane] = A.bsum[a * A.Z + lane];
         s_lim[wave][k][lane] = DINF;
+        s_rad[wave][k][lane] = rd[k];
       }
     }
   }
@@ -105,6 +118,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   // index clamped instead of branching, so the loads overlap the previous block's scoring.
   double n0 = 0, n1 = 0, n2 = 0, n3 = 0, nkey = DINF;
   int nz = 0;
+  uint32_t ntb = 0;
   auto fetch = [&](int hb) {
     const int h = min(hb + lane, hb1 - 1);
     n0 = A.avail[h];
@@ -113,24 +127,38 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
     n3 = A.avail[3 * (size_t)A.H + h];
     if (MODE == CA_BF) nz = A.zone[h];
     if (MODE == CA_FF) nkey = A.key[h];
+    if (MODE == VBP_BF) ntb = A.tb[h];     // host-id rank: read with the block, not per hit
   };
   if (hb0 < hb1) fetch(hb0);
   for (int hb = hb0; hb < hb1; hb += hstep) {
+    const double a0 = n0, a1 = n1, a2 = n2, a3 = n3, key = nkey;
+    const int z = nz;
+    const uint32_t tbh = ntb;
+    if (hb + hstep < hb1) fetch(hb + hstep);
     const int h = hb + lane;
     const bool ok = h < hb1;
-    const double a0 = ok ? n0 : -DINF;
-    const double a1 = n1, a2 = n2, a3 = n3;
-    const int z = nz;
-    const double key = nkey;
-    if (hb + hstep < hb1) fetch(hb + hstep);
+    // prefilter, all tasks: frozen key (first-fit) or memory radius (best-fit)
+    bool pre[TW];
+    bool any = false;
 #pragma unroll
     for (int k = 0; k < TW; k++) {
-      const bool fit = fits<STRICT>(a0, a1, a2, a3, d0[k], d1[k], d2[k], d3[k]);
-      feas[k] += __popcll(__ballot(fit));
+      if (MODE == CA_FF) {
+        pre[k] = ok && lexless(key, 0u, h, ts[k], tt[k], ti[k]);
+      } else {
+        const double r = (MODE == CA_BF) ? s_rad[wave][k][z] : rd[k];
+        pre[k] = ok && (__builtin_fabs(a1 - d1[k]) <= r);
+      }
+      any |= pre[k];
+    }
+    if (__ballot(any) == 0) continue;
+#pragma unroll
+    for (int k = 0; k < TW; k++) {
+      if (__ballot(pre[k]) == 0) continue;
+      const bool fit = pre[k] && fits<STRICT>(a0, a1, a2, a3, d0[k], d1[k], d2[k], d3[k]);
       double s2 = 0.0;
       bool pass;
       if (MODE == CA_FF) {
-        pass = fit && lexless(key, 0u, h, ts[k], tt[k], ti[k]);
+        pass = fit;
       } else {
         s2 = norm2_seq(a0 - d0[k], a1 - d1[k], a2 - d2[k], a3 - d3[k]);
         const double lm = (MODE == CA_BF) ? s_lim[wave][k][z] : lim[k];
@@ -148,9 +176,16 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
             sc = (s_c[wave][k][z] * r) / s_b[wave][k][z];
           } else {
             sc = __builtin_sqrt(s2);
-            tbv = A.tb[h];
+            tbv = tbh;
           }
         }
+        // Candidates that beat the task's current last entry, as 128-bit keys (score bits,
+        // tiebreak:id): scores are >= +0, so their bits order like the values.
+        const uint64_t tk1 = (uint64_t)__double_as_longlong(ts[k]);
+        const uint64_t tk2 = ((uint64_t)tt[k] << 32) | (uint32_t)ti[k];
+        const uint64_t ck1 = (uint64_t)__double_as_longlong(sc);
+        const uint64_t ck2 = ((uint64_t)tbv << 32) | (uint32_t)h;
+        pm = __ballot(pass && (ck1 < tk1 || (ck1 == tk1 && ck2 < tk2)));
         bool changed = false;
         while (pm) {
           const int L = __builtin_ctzll(pm);
@@ -158,7 +193,11 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
           const double cs = readlane_d(sc, L);
           const uint32_t ct = readlane_u(tbv, L);
           const int32_t ci = hb + L;
-          if (lexless(cs, ct, ci, ts[k], tt[k], ti[k])) {
+          // insert unless an earlier insertion of this block raised the bar above it
+          const uint64_t c1 = (uint64_t)__double_as_longlong(cs), c2 = ((uint64_t)ct << 32) | (uint32_t)ci;
+          const uint64_t t1 = (uint64_t)__double_as_longlong(ts[k]), t2 = ((uint64_t)tt[k] << 32) | (uint32_t)ti[k];
+          const bool better = (c1 < t1) | ((c1 == t1) & (c2 < t2));
+          if (better) {
             list_insert(ls[k], lt[k], li[k], cs, ct, ci);
             ts[k] = readlane_d(ls[k], KL - 1);
             tt[k] = readlane_u(lt[k], KL - 1);
@@ -168,15 +207,23 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
         }
         if (changed) {
           if (MODE == CA_BF) {
-            if (lane < A.Z) s_lim[wave][k][lane] = ca_lim(ts[k], s_c[wave][k][lane], s_b[wave][k][lane]);
+            if (lane < A.Z) {
+              const double lm2 = ca_lim(ts[k], s_c[wave][k][lane], s_b[wave][k][lane]);
+              s_lim[wave][k][lane] = lm2;
+              s_rad[wave][k][lane] = rad(lm2);
+            }
           } else if (MODE == VBP_BF) {
             lim[k] = vbp_lim(ts[k]);
+            rd[k] = rad(lim[k]);
           }
         }
       }
     }
   }
 
+  // Feasible hosts per segment, as the merge needs it: a list that never filled holds every
+  // feasible host of the segment (its threshold stayed infinite); a full one reports KL + 1,
+  // i.e. "bounded by its last entry" (every host it rejected ranked at or after that entry).
 #pragma unroll
   for (int k = 0; k < TW; k++) {
     if (k < nt) {
@@ -184,7 +231,8 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
       SegEntry e;
       e.s = ls[k]; e.tb = lt[k]; e.id = li[k];
       A.seg[row * KL + lane] = e;
-      if (lane == 0) A.seg_feas[row] = feas[k];
+      const int filled = __popcll(__ballot(li[k] != 0x7fffffff));
+      if (lane == 0) A.seg_feas[row] = filled == KL ? KL + 1 : filled;
     }
   }
 }
