@@ -148,7 +148,12 @@ def main():
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             if tj.get("mode") == args.mode and tj.get("hosts") == H and tj.get("tasks") == T:
-                traffic = tj.get("hbm_bytes_per_launch")
+                # PMC bytes per candidate of the probe's launches (tools/pmc_traffic.py), scaled to
+                # this run's average candidates per score launch
+                per_cand = tj.get("hbm_bytes_per_candidate")
+                cand_per_launch = score["candidates"] / max(score["launches"], 1)
+                traffic = (per_cand * cand_per_launch if per_cand is not None
+                           else tj.get("hbm_bytes_per_launch"))
         except (OSError, ValueError):
             traffic = None
 
