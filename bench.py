@@ -50,6 +50,10 @@ def parse():
     p.add_argument("--shard", default="scenarios", choices=["scenarios", "hosts"],
                    help="N > 1: independent scenario per rank (weak scaling, config 4) or one "
                         "round with its host dimension split over the ranks (strong, config 5)")
+    p.add_argument("--batch", type=int, default=0,
+                   help="> 0: scenario-batch workload (BASELINE config 4): this many independent "
+                        "scenarios per GPU (seeds seed + rank*batch + s) of --hosts x --tasks, all "
+                        "placed by ONE pvt_place_batch launch per step (resident kernel)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0,
                    help="target CPU time of the oracle baseline sample (0 = skip)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -93,12 +97,20 @@ def main():
     mode = MODES[args.mode]
     H, T = args.hosts, args.tasks
     log("[rank %d] building synthetic round: %s, H=%d T=%d" % (rank, args.mode, H, T))
-    hosts_sharded = args.shard == "hosts"
-    r = synthetic.make_round(mode, H, T, seed=args.seed + (0 if hosts_sharded else rank))
+    hosts_sharded = args.shard == "hosts" and not args.batch
+    B = max(args.batch, 0)
     eng = PlacementEngine(local, window=args.window)
     eng.set_pipeline(bool(args.pipeline))
-    dr = DeviceRound(r, eng.device)
-    run = eng.run
+    if B:
+        from pivot_place.engine import DeviceBatch
+        rounds = [synthetic.make_round(mode, H, T, seed=args.seed + rank * B + s) for s in range(B)]
+        r = rounds[0]
+        dr = DeviceBatch(rounds, eng.device)
+        run = eng.run_batch
+    else:
+        r = synthetic.make_round(mode, H, T, seed=args.seed + (0 if hosts_sharded else rank))
+        dr = DeviceRound(r, eng.device)
+        run = eng.run
     if hosts_sharded:
         from pivot_place.sharded import HostShardedPlacer, torch_exchange
         placer = HostShardedPlacer(eng, rank, world, torch_exchange() if world > 1 else None)
@@ -110,7 +122,8 @@ def main():
         run(dr)
     torch.cuda.synchronize()
     stats = eng.last_stats()
-    placed = int((dr.placement[:T] >= 0).sum().item())
+    first = dr.rounds[0] if B else dr
+    placed = int((first.placement[:T] >= 0).sum().item())
     log("[rank %d] warmup done: %d/%d placed, windows=%d refills=%d"
         % (rank, placed, T, stats["windows"], stats["refills"]))
 
@@ -133,7 +146,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
-    cand_per_step = float(T) * H * (1 if hosts_sharded else world)
+    cand_per_step = float(T) * H * (1 if hosts_sharded else world) * (B if B else 1)
     value = cand_per_step / (elapsed / args.steps)
 
     ks = {name: eng.kstats(k) for name, k in (("score", _abi.PVT_K_SCORE), ("merge", _abi.PVT_K_MERGE),
@@ -174,8 +187,11 @@ def main():
             "config": {
                 "workload": "synthetic %d hosts x %d ready tasks per round, 20 zones, %s, %s"
                             % (H, T, POLICY[args.mode],
+                               "%d independent scenarios per GPU, one resident launch per step" % B
+                               if B else
                                "host dimension split over the GPUs" if hosts_sharded
                                else "one independent scenario per GPU"),
+                "scenarios_per_gpu": B if B else 1,
                 "hosts": H, "tasks_per_round": T, "zones": 20, "policy": args.mode,
                 "parallelism": ("host-sharded x%d (per-window candidate all-gather)" % world
                                 if hosts_sharded else
@@ -183,7 +199,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "score (fused fit-mask + score + top-K)",
+                "kernel": ("resident (registers-held hosts, full rescan per task)" if B
+                           else "score (fused fit-mask + score + top-K)"),
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

@@ -157,6 +157,25 @@ int  pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo, int32_t 
                      int32_t world, int64_t* max_package_bytes);
 int  pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks, int64_t* package_bytes);
 int  pvt_shard_commit(pvt_ctx* ctx, const void* packages);
+/*
+ * Resident rounds and scenario batches (BASELINE configs 1, 2 and 4; SURVEY.md §8(e), §8(f)
+ * rank 2). A round with n_hosts <= PVT_RESIDENT_MAX_HOSTS and n_tasks <= PVT_RESIDENT_MAX_TASKS
+ * fits one workgroup: its hosts stay in registers for the whole round and every task rescans
+ * them (the reference's loop, restated). pvt_place_batch() runs n such rounds of ONE policy
+ * (rounds[i].mode all equal) in a single launch, one workgroup per round, so independent
+ * scenarios' rounds run side by side on all CUs. `rounds` is a HOST array of descriptors whose
+ * array pointers are device pointers, exactly as for pvt_place() (mt_state in host memory);
+ * each round is placed exactly as pvt_place() would place it. Synchronises before returning.
+ * Returns PVT_EUNSUPPORTED if a round exceeds the limits (use pvt_place for it).
+ *
+ * pvt_set_resident(ctx, max_hosts): pvt_place() runs rounds with n_hosts <= max_hosts (and
+ * n_tasks within the limit) as a batch of one; 0 disables it (the windowed score/commit path
+ * runs every round). Default PVT_RESIDENT_MAX_HOSTS. Results are identical either way.
+ */
+#define PVT_RESIDENT_MAX_HOSTS 4096
+#define PVT_RESIDENT_MAX_TASKS 4096
+int  pvt_place_batch(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_rounds);
+int  pvt_set_resident(pvt_ctx* ctx, int32_t max_hosts);
 /* Human-readable text of the last error on this context (static storage of the ctx). */
 const char* pvt_last_error(pvt_ctx* ctx);
 

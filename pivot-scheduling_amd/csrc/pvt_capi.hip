@@ -67,8 +67,11 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2];
+      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
+  int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
+  std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
+  std::vector<uint32_t> rmt_host;
   RoundState rs;
   int32_t* next_host = nullptr;   // pinned
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
@@ -175,6 +178,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
       hipMemset(ctx->walk_flag, 0, 64) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_lists, hipEventDisableTiming) != hipSuccess ||
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
+      resident_init_attrs() != hipSuccess ||
       hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess) {
     delete ctx;
     return PVT_EHIP;
@@ -194,7 +198,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
-                 &ctx->owned[0], &ctx->owned[1]};
+                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -657,10 +661,92 @@ static int place_pipelined(pvt_ctx* ctx) {
   return PVT_OK;
 }
 
+// ---------------------------------------------------------------- resident rounds / batches
+static bool resident_fits(const pvt_round* r, int max_hosts) {
+  return r->n_hosts <= std::min(max_hosts, (int)PVT_RESIDENT_MAX_HOSTS) &&
+         r->n_tasks <= PVT_RESIDENT_MAX_TASKS;
+}
+
+static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n) {
+  const int mode = rounds[0].mode;
+  int maxH = 1, maxT = 1, maxZ = 1;
+  for (int i = 0; i < n; i++) {
+    const pvt_round* r = &rounds[i];
+    int rc = check_round(ctx, r);
+    if (rc) return rc;
+    if (r->mode != mode) return fail(ctx, PVT_EINVAL, "batch round %d: mode %d != %d", i, r->mode, mode);
+    if (!resident_fits(r, PVT_RESIDENT_MAX_HOSTS))
+      return fail(ctx, PVT_EUNSUPPORTED, "batch round %d: H=%d T=%d exceeds the resident limits (%d, %d)",
+                  i, r->n_hosts, r->n_tasks, PVT_RESIDENT_MAX_HOSTS, PVT_RESIDENT_MAX_TASKS);
+    maxH = std::max(maxH, r->n_hosts);
+    maxT = std::max(maxT, r->n_tasks);
+    maxZ = std::max(maxZ, r->n_zones);
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  int hpl = 1;
+  while (hpl * RES_THREADS < maxH) hpl <<= 1;
+  int tpad = 64;
+  while (tpad < maxT) tpad <<= 1;
+  ctx->rstage.assign(rounds, rounds + n);
+  ENSURE(ctx->rdesc, sizeof(pvt_round) * (size_t)n);
+  uint32_t* mt = nullptr;
+  if (mode == PVT_OPP) {
+    ENSURE(ctx->rmt, sizeof(uint32_t) * 625 * (size_t)n);
+    mt = P<uint32_t>(ctx->rmt);
+    ctx->rmt_host.resize((size_t)n * 625);
+    for (int i = 0; i < n; i++) {
+      std::memcpy(&ctx->rmt_host[(size_t)i * 625], rounds[i].mt_state, sizeof(uint32_t) * 625);
+      ctx->rstage[i].mt_state = mt + (size_t)i * 625;   // device copy (the kernel never reads the field)
+    }
+    HIPCHK(hipMemcpyAsync(mt, ctx->rmt_host.data(), sizeof(uint32_t) * 625 * n, hipMemcpyHostToDevice, st));
+  }
+  HIPCHK(hipMemcpyAsync(ctx->rdesc.p, ctx->rstage.data(), sizeof(pvt_round) * n, hipMemcpyHostToDevice, st));
+  ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad};
+  double cand = 0.0, bytes = 0.0;
+  for (int i = 0; i < n; i++) {
+    const double c = (double)rounds[i].n_tasks * rounds[i].n_hosts;
+    cand += c;
+    bytes += c * bytes_per_candidate(mode);
+  }
+  {
+    Scope sc(ctx, PVT_K_SCORE, cand, bytes);
+    launch_resident(mode, hpl, n, ra, st);
+  }
+  HIPCHK(hipGetLastError());
+  if (mode == PVT_OPP)
+    HIPCHK(hipMemcpyAsync(ctx->rmt_host.data(), mt, sizeof(uint32_t) * 625 * n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (mode == PVT_OPP)
+    for (int i = 0; i < n; i++)
+      std::memcpy(rounds[i].mt_state, &ctx->rmt_host[(size_t)i * 625], sizeof(uint32_t) * 625);
+  ctx->windows = n;
+  ctx->refills = 0;
+  return PVT_OK;
+}
+
+extern "C" int pvt_place_batch(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_rounds) {
+  if (!ctx) return PVT_EINVAL;
+  if (n_rounds < 0 || (n_rounds > 0 && !rounds)) return fail(ctx, PVT_EINVAL, "bad batch (%d rounds)", n_rounds);
+  ctx->rs.active = false;
+  if (n_rounds == 0) return PVT_OK;
+  return place_resident(ctx, rounds, n_rounds);
+}
+
+extern "C" int pvt_set_resident(pvt_ctx* ctx, int32_t max_hosts) {
+  if (!ctx || max_hosts < 0) return PVT_EINVAL;
+  ctx->resident_max = max_hosts;
+  return PVT_OK;
+}
+
 extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
   if (!ctx) return PVT_EINVAL;
   int rc = check_round(ctx, r);
   if (rc) return rc;
+  if (r->n_tasks > 0 && resident_fits(r, ctx->resident_max)) {
+    ctx->rs.active = false;
+    return place_resident(ctx, r, 1);
+  }
   if (r->mode == PVT_OPP) {
     ctx->rs.active = false;
     ctx->windows = ctx->refills = 0;

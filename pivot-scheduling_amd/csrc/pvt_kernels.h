@@ -160,6 +160,21 @@ void launch_norm_keys(const double* dem, int T, const int32_t* idx, uint64_t* ke
                       hipStream_t st);
 void launch_group_keys(const int32_t* task_group, const int32_t* idx, int T, uint32_t* keys,
                        hipStream_t st);
+// Resident rounds (pvt_batch.hip): one 256-thread block per round, hosts in registers
+// (HPL hosts per thread, HPL in {1, 2, 4, 8, 16}).
+constexpr int RES_THREADS = 256;
+constexpr int RES_MAX_HPL = 16;
+constexpr int RES_MAX_HOSTS = RES_THREADS * RES_MAX_HPL;   // 4096
+constexpr int RES_MAX_TASKS = 4096;
+struct ResidentArgs {
+  const void* rounds;     // device copy of pvt_round[n] (device array pointers)
+  uint32_t* mt;           // [n][625] MT19937 states (PVT_OPP), else unused
+  int Zb;                 // zone-table stride in LDS: max n_zones of the batch
+  int Tpad;               // power of two >= max n_tasks of the batch (sort network size)
+};
+size_t resident_lds_bytes(int Zb, int Tpad);
+void launch_resident(int mode, int hpl, int n, const ResidentArgs& a, hipStream_t st);
+hipError_t resident_init_attrs();
 size_t commit_lds_bytes();
 hipError_t init_kernel_attrs();
 void launch_iota(int32_t* out, int n, hipStream_t st);

@@ -13,6 +13,7 @@
 
 #include "pvt_device.h"
 #include "pvt_kernels.h"
+#include "pvt_mt.h"
 #include "pvt_opp.h"
 
 namespace pvt {
@@ -137,75 +138,6 @@ __device__ __forceinline__ void ohash_put(OppLDS& S, int32_t id, int32_t v) {
   while (S.hkey[p] >= 0) p = (p + 1) & (OPP_HASH - 1);
   S.hkey[p] = id;
   S.hval[p] = v;
-}
-
-// numpy legacy MT19937 (mt19937_gen / mt19937_next) for the whole wave: the 624-word key lives
-// in LDS, the twist runs 64 words per step (reads of a step precede its writes, and every
-// key[i + 397 - 624] it needs was written by an earlier step, so this is the sequential loop),
-// and 64 tempered outputs at a time sit in one VGPR (lane j = output j), consumed in order.
-struct MtWave {
-  uint32_t buf;   // tempered outputs (lane j)
-  int used;       // outputs of buf consumed (uniform)
-  int limit;      // outputs held by buf (uniform; a buffer never straddles a twist)
-};
-__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-  y ^= (y >> 11);
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
-  y ^= (y >> 18);
-  return y;
-}
-__device__ void mt_twist_wave(uint32_t* key) {
-  const int lane = lane_id();
-  for (int base = 0; base < 624; base += WAVE) {
-    const int i = base + lane;
-    uint32_t v = 0;
-    if (i < 624) {
-      const uint32_t y = (key[i] & 0x80000000u) | (key[(i + 1) % 624] & 0x7fffffffu);
-      v = key[(i + 397) % 624] ^ (y >> 1);
-      if (y & 1u) v ^= 0x9908b0dfu;
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // every lane's reads land before any write
-    if (i < 624) key[i] = v;
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-  }
-}
-// Next outputs into the buffer; key[624] is numpy's pos, advanced past the buffered outputs.
-// As in numpy, the twist runs only when an output is needed at pos == 624.
-__device__ void mt_refill(uint32_t* key, MtWave& w) {
-  const int lane = lane_id();
-  int pos = __builtin_amdgcn_readfirstlane((int)key[624]);
-  if (pos >= 624) {
-    mt_twist_wave(key);
-    pos = 0;
-  }
-  const int n = min(WAVE, 624 - pos);
-  const uint32_t y = key[pos + min(lane, n - 1)];
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  if (lane == 0) key[624] = (uint32_t)(pos + n);
-  w.buf = mt_temper(y);
-  w.used = 0;
-  w.limit = n;
-}
-__device__ __forceinline__ uint32_t mt_next(uint32_t* key, MtWave& w) {
-  if (w.used >= w.limit) mt_refill(key, w);
-  return (uint32_t)__builtin_amdgcn_readlane((int)w.buf, w.used++);
-}
-// RandomState.randint(0, n): masked rejection, no draw for n == 1.
-__device__ uint32_t mt_randint(uint32_t* key, MtWave& w, uint32_t n) {
-  const uint32_t rng = n - 1;
-  if (rng == 0) return 0;
-  uint32_t mask = rng;
-  mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4; mask |= mask >> 8; mask |= mask >> 16;
-  uint32_t v;
-  while ((v = (mt_next(key, w) & mask)) > rng) {}
-  return v;
-}
-// Hand unconsumed buffered outputs back to the state (rewind pos).
-__device__ void mt_unbuffer(uint32_t* key, MtWave& w) {
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  if (lane_id() == 0) key[624] = key[624] - (uint32_t)(w.limit - w.used);
-  __builtin_amdgcn_s_waitcnt(0xc07f);
 }
 
 // Position of the r-th (0-based) set bit of x (r < popcount(x)).

@@ -27,6 +27,10 @@ MODE_NAMES = {PVT_CA_FF: "cost_aware_ff", PVT_CA_BF: "cost_aware_bf", PVT_OPP: "
 
 PVT_K_SCORE, PVT_K_MERGE, PVT_K_COMMIT, PVT_K_OTHER = range(4)
 
+# Resident rounds / scenario batches (pvt_place_batch).
+PVT_RESIDENT_MAX_HOSTS = 4096
+PVT_RESIDENT_MAX_TASKS = 4096
+
 # Algorithmic bytes per (task, host) candidate, SURVEY.md §8(d).
 BYTES_PER_CANDIDATE = {PVT_CA_FF: 36, PVT_CA_BF: 36, PVT_OPP: 32, PVT_VBP_FF: 32, PVT_VBP_BF: 36}
 

@@ -52,6 +52,8 @@ def load_library(path=None):
         "pvt_shard_score": ([c_void_p, c_void_p, ctypes.POINTER(ctypes.c_int32),
                              ctypes.POINTER(ctypes.c_int64)], c_int),
         "pvt_shard_commit": ([c_void_p, c_void_p], c_int),
+        "pvt_place_batch": ([c_void_p, c_void_p, ctypes.c_int32], c_int),
+        "pvt_set_resident": ([c_void_p, ctypes.c_int32], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -118,6 +120,25 @@ class DeviceRound:
                            mt_state=None if self.mt is None else self.mt.copy())
 
 
+class DeviceBatch:
+    """Independent rounds resident in HBM for pvt_place_batch: one DeviceRound per round plus
+    the contiguous pvt_round[n] descriptor array the call takes."""
+
+    def __init__(self, rounds, device):
+        self.rounds = [r if isinstance(r, DeviceRound) else DeviceRound(r, device) for r in rounds]
+        self.structs = (_abi.pvt_round * max(len(self.rounds), 1))()
+        for i, dr in enumerate(self.rounds):
+            self.structs[i] = dr.struct
+
+    def reset(self):
+        for dr in self.rounds:
+            dr.reset()
+        # mt_state pointers are host arrays updated in place; nothing else to refresh
+
+    def results(self):
+        return [dr.result() for dr in self.rounds]
+
+
 class PlacementEngine:
     """One pvt_ctx on one gfx950 device."""
 
@@ -164,6 +185,26 @@ class PlacementEngine:
         dr = DeviceRound(r, self.device)
         self.run(dr)
         return dr.result()
+
+    # -- resident rounds and scenario batches (include/pivot_place.h, pvt_place_batch)
+    def run_batch(self, batch: "DeviceBatch"):
+        """Place every round of a resident batch in ONE launch (one workgroup per round)."""
+        torch = _torch()
+        stream = torch.cuda.current_stream(self.device)
+        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._check(self.lib.pvt_place_batch(self.ctx, ctypes.addressof(batch.structs),
+                                             len(batch.rounds)))
+
+    def place_batch(self, rounds) -> list:
+        """Place independent rounds of one policy (each <= PVT_RESIDENT_MAX_HOSTS hosts and
+        PVT_RESIDENT_MAX_TASKS tasks) together; returns one RoundResult per round."""
+        b = DeviceBatch(rounds, self.device)
+        self.run_batch(b)
+        return b.results()
+
+    def set_resident(self, max_hosts=_abi.PVT_RESIDENT_MAX_HOSTS):
+        """pvt_place runs rounds up to ``max_hosts`` hosts on the resident kernel (0: never)."""
+        self._check(self.lib.pvt_set_resident(self.ctx, int(max_hosts)))
 
     # -- host-dimension sharding (include/pivot_place.h, pvt_shard_*); see pivot_place.sharded
     def shard_begin(self, dr: DeviceRound, host_lo, host_hi, world):

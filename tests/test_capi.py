@@ -32,7 +32,7 @@ def test_library_exports_every_declared_symbol():
 def test_constants_match_header():
     text = open(HEADER).read()
     for name in ("PVT_OK", "PVT_EINVAL", "PVT_ENODEV", "PVT_EHIP", "PVT_ENOMEM", "PVT_EUNSUPPORTED",
-                 "PVT_ABI_VERSION"):
+                 "PVT_ABI_VERSION", "PVT_RESIDENT_MAX_HOSTS", "PVT_RESIDENT_MAX_TASKS"):
         m = re.search(r"#define\s+%s\s+(-?\d+)" % name, text)
         assert m and int(m.group(1)) == getattr(_abi, name), name
     enum = re.search(r"enum pvt_mode \{(.*?)\};", text, flags=re.S).group(1)

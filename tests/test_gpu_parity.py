@@ -1,5 +1,11 @@
 """GPU parity: the HIP engine (through the C ABI) against the reference's golden runs and the
-CPU restatement. Integer/index outputs and fp64 availability must match bit for bit."""
+CPU restatement. Integer/index outputs and fp64 availability must match bit for bit.
+
+Rounds small enough for the resident kernel (<= 4096 hosts and tasks) run there by default;
+``path`` runs each such test on both engines: "resident" (pvt_place -> resident kernel) and
+"windowed" (pvt_set_resident(0): score/merge/commit-walk windows)."""
+import contextlib
+
 import numpy as np
 import pytest
 
@@ -12,6 +18,18 @@ pytestmark = pytest.mark.gpu
 ALL_MODES = [_abi.PVT_CA_FF, _abi.PVT_CA_BF, _abi.PVT_OPP, _abi.PVT_VBP_FF, _abi.PVT_VBP_BF]
 
 
+@contextlib.contextmanager
+def on_path(engine, path):
+    engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS if path == "resident" else 0)
+    try:
+        yield
+    finally:
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+
+
+PATHS = ["resident", "windowed"]
+
+
 def _assert_same(res, placement, order, avail, mt=None):
     np.testing.assert_array_equal(res.placement, placement)
     np.testing.assert_array_equal(res.order, order)
@@ -21,11 +39,13 @@ def _assert_same(res, placement, order, avail, mt=None):
         np.testing.assert_array_equal(res.mt_state, mt)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("name,idx", golden_io.all_runs())
-def test_engine_matches_reference(engine, name, idx):
+def test_engine_matches_reference(engine, name, idx, path):
     case = golden_io.load(name)
     run = case["runs"][idx]
-    res = engine.place(golden_io.run_arrays(case, run))
+    with on_path(engine, path):
+        res = engine.place(golden_io.run_arrays(case, run))
     _assert_same(res, *golden_io.expected(case, run))
 
 
@@ -35,6 +55,7 @@ def test_small_windows_force_refills(engine, name, window):
     """Tiny windows make every list-exhaustion / refill path run; results must not change."""
     case = golden_io.load(name)
     try:
+        engine.set_resident(0)
         engine.set_window(window)
         for run in case["runs"]:
             if run["error"]:
@@ -43,30 +64,37 @@ def test_small_windows_force_refills(engine, name, window):
             _assert_same(res, *golden_io.expected(case, run))
     finally:
         engine.set_window(0)
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("mode", ALL_MODES)
-@pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70000, 120, 2), (1, 5, 3), (64, 2000, 4)])
-def test_engine_matches_oracle_synthetic(engine, mode, H, T, seed):
+@pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70000, 120, 2), (1, 5, 3), (64, 2000, 4),
+                                      (4096, 700, 5), (1000, 4096, 6)])
+def test_engine_matches_oracle_synthetic(engine, mode, H, T, seed, path):
     r = synthetic.make_round(mode, H, T, seed=seed)
     ref = oracle.place(r)
-    res = engine.place(r)
+    with on_path(engine, path):
+        res = engine.place(r)
     _assert_same(res, ref.placement, ref.order, ref.avail, ref.mt_state)
 
 
+@pytest.mark.parametrize("path", PATHS)
 @pytest.mark.parametrize("mode", ALL_MODES)
-def test_engine_crowded_hosts(engine, mode):
+def test_engine_crowded_hosts(engine, mode, path):
     """Few, nearly full hosts with identical states: ties, exhaustion and unplaceable tasks."""
     r = synthetic.make_round(mode, 300, 1500, seed=11)
     r.avail[0, :] = 4.0
     r.avail[1, :] = 40000.0
     r.avail[0, ::7] = 0.5
     ref = oracle.place(r)
-    res = engine.place(r)
+    with on_path(engine, path):
+        res = engine.place(r)
     _assert_same(res, ref.placement, ref.order, ref.avail, ref.mt_state)
 
 
-def test_sqrt_and_division_are_correctly_rounded(engine):
+@pytest.mark.parametrize("path", PATHS)
+def test_sqrt_and_division_are_correctly_rounded(engine, path):
     """Best-fit scores need IEEE sqrt and division: compare scores on many random residuals by
     running vbp best-fit with one task against hosts whose residual norms nearly tie."""
     rs = np.random.RandomState(9)
@@ -77,7 +105,8 @@ def test_sqrt_and_division_are_correctly_rounded(engine):
     r.avail[1, 1::2] = np.nextafter(base[1::2], np.inf)
     r.dem[:, 0] = [0.5, 1.0, 0.0, 0.0]
     ref = oracle.place(r)
-    res = engine.place(r)
+    with on_path(engine, path):
+        res = engine.place(r)
     _assert_same(res, ref.placement, ref.order, ref.avail)
 
 
@@ -106,8 +135,10 @@ def test_pipelined_crowded_small_windows(engine, mode, window):
     r.avail[1, :] = 60000.0
     ref = oracle.place(r)
     try:
+        engine.set_resident(0)
         engine.set_window(window)
         res = engine.place(r)
     finally:
         engine.set_window(0)
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
     _assert_same(res, ref.placement, ref.order, ref.avail)
