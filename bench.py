@@ -122,8 +122,7 @@ def main():
         run(dr)
     torch.cuda.synchronize()
     stats = eng.last_stats()
-    first = dr.rounds[0] if B else dr
-    placed = int((first.placement[:T] >= 0).sum().item())
+    placed = int(((dr.placement_of(0) if B else dr.placement[:T]) >= 0).sum().item())
     log("[rank %d] warmup done: %d/%d placed, windows=%d refills=%d"
         % (rank, placed, T, stats["windows"], stats["refills"]))
 

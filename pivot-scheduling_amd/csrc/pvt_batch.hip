@@ -13,13 +13,13 @@
 //     ONE launch, one block each, so the rounds' sequential walks run side by side on all CUs;
 //   - single rounds of the sim.py sizes (100-1000 hosts, configs 1-2) through pvt_place.
 //
-// Per task (4 waves): each lane reduces its HPL hosts to the best (score bits, tiebreak:host)
-// 128-bit key (scores are >= +0, so bit patterns order like values), the wave reduces to its
-// minimum, lane 0 posts it in LDS (double-buffered by task parity: ONE barrier per task), and
-// every wave picks the same winner from the four posts; the owning thread commits in its
-// registers. Opportunistic posts per-wave feasible counts instead; each wave draws the same
-// randint(0, n) from its own copy of the MT19937 state (no second barrier), and the wave that
-// holds the k-th feasible host commits it.
+// A round runs on 4 waves (HPL <= 16 hosts per lane: H <= 4096). Per task each lane reduces
+// its HPL hosts to the best (score bits, tiebreak:host) 128-bit key (scores are >= +0, so bit
+// patterns order like values) and the wave reduces to its minimum with DPP row steps
+// (first-fit: one ballot). Lane 0 posts the wave's minimum in LDS (double-buffered by task
+// parity: ONE barrier per task) and every wave picks the same winner from the four posts. The owning lane commits in its registers. Opportunistic reduces
+// feasible counts instead; every wave draws the same randint(0, n) from its own copy of the
+// MT19937 state (no second barrier), and the lane holding the k-th feasible host commits it.
 //
 // Numerics as everywhere in the engine: -ffp-contract=off, sequential-FMA squared norms,
 // correctly rounded sqrt/div, scores computed in the reference's operation order.
@@ -33,20 +33,21 @@
 
 namespace pvt {
 
-constexpr int RES_WAVES = RES_THREADS / WAVE;
+constexpr int RES_WAVES = RES_THREADS / WAVE;   // LDS is laid out for the 4-wave variant
 constexpr int RES_CHUNK = 256;           // tasks whose demand rows are staged in LDS at a time
 constexpr int RES_MT_STRIDE = 628;       // words per wave-private MT19937 copy (625 used)
 constexpr uint64_t NONE = ~0ull;
 
 // Dynamic LDS layout (bytes); the host sizes the launch with the same struct.
 struct ResLds {
-  int zt, ord, u, cd, ci, mt, slot, total;
+  int zt, ord, pl, u, cd, ci, mt, slot, total;
   __host__ __device__ ResLds(int Zb, int Tpad) {
     zt = 0;                                            // csum[Zb*Zb], bsum[Zb*Zb] f64
     ord = (16 * Zb * Zb + 15) & ~15;                   // processing order i32[Tpad]
-    u = (ord + 4 * Tpad + 15) & ~15;                   // union: sort keys | walk staging
+    pl = ord + 4 * Tpad;                               // placement by position i32[Tpad]
+    u = (pl + 4 * Tpad + 15) & ~15;                    // union: sort keys | walk staging
     cd = u;                                            // walk: demand rows f64[CHUNK][4]
-    ci = cd + 32 * RES_CHUNK;                          //       anchor, caller, group i32[3][CHUNK]
+    ci = cd + 32 * RES_CHUNK;                          //       anchor, group i32[2][CHUNK] (+pad)
     mt = ci + 12 * RES_CHUNK;                          //       MT copies u32[WAVES][628]
     slot = mt + 4 * RES_WAVES * RES_MT_STRIDE;         //       posts u64[2][WAVES][2]
     const int walk_end = slot + 32 * RES_WAVES;
@@ -57,19 +58,16 @@ struct ResLds {
 
 size_t resident_lds_bytes(int Zb, int Tpad) { return (size_t)ResLds(Zb, Tpad).total; }
 
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  const int lo = __shfl_xor((int)(uint32_t)v, m), hi = __shfl_xor((int)(uint32_t)(v >> 32), m);
-  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
-}
 __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
 
 // Stable processing order (a2): sort (group, ~bits(||d||2) or 0, caller index) ascending with a
 // bitonic network over Tpad entries; the caller index makes every key distinct, so the result
 // is the stable order cost_aware.py:37,60-61 / vbp.py:17,41 produce.
+template <int NT>
 __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_t* ka, uint64_t* kb,
                           int32_t* ord, int Tpad) {
   const int T = R.n_tasks, tid = threadIdx.x;
-  for (int i = tid; i < Tpad; i += RES_THREADS) {
+  for (int i = tid; i < Tpad; i += NT) {
     if (i < T) {
       const uint32_t g = grouped ? (uint32_t)R.task_group[i] : 0u;
       ka[i] = ((uint64_t)g << 32) | (uint32_t)i;
@@ -89,7 +87,7 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
   if (grouped || sorted) {
     for (int k = 2; k <= Tpad; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < Tpad; i += RES_THREADS) {
+        for (int i = tid; i < Tpad; i += NT) {
           const int l = i ^ j;
           if (l > i) {
             const uint64_t ai = ka[i], al = ka[l], bi = kb[i], bl = kb[l];
@@ -104,12 +102,13 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
       }
     }
   }
-  for (int i = tid; i < T; i += RES_THREADS) ord[i] = (int32_t)(uint32_t)ka[i];
+  for (int i = tid; i < T; i += NT) ord[i] = (int32_t)(uint32_t)ka[i];
   __syncthreads();
 }
 
-template <int MODE, int HPL>
-__global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
+template <int MODE, int WAVES, int HPL>
+__global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) {
+  constexpr int NT = WAVES * WAVE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool CA = (MODE == CA_FF || MODE == CA_BF);
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
@@ -126,12 +125,15 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
   const bool keyed = (MODE == CA_FF) && R.sort_hosts;
 
   if (CA)
-    for (int i = tid; i < Z * Z; i += RES_THREADS) {
+    for (int i = tid; i < Z * Z; i += NT) {
       const int a = i / Z, z = i - a * Z;
       csum[i] = R.cost[a * Z + z] + R.cost[z * Z + a];
       bsum[i] = R.bw[a * Z + z] + R.bw[z * Z + a];
     }
-  for (int t = tid; t < T; t += RES_THREADS) R.placement[t] = -1;
+  // Placements are kept in LDS by position and written out when the round ends: a global
+  // store inside the task loop would put its round trip (vmcnt) on every task's critical path.
+  int32_t* pl = reinterpret_cast<int32_t*>(smem + Lo.pl);
+  for (int i = tid; i < T; i += NT) pl[i] = -1;
 
   // hosts -> registers (padding slots never fit: -inf capacities)
   const int h0 = tid * HPL;
@@ -157,17 +159,16 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
   uint64_t* ka = reinterpret_cast<uint64_t*>(smem + Lo.u);
   uint64_t* kb = ka + A.Tpad;
   if (MODE == OPP) {
-    for (int i = tid; i < T; i += RES_THREADS) ord[i] = i;
+    for (int i = tid; i < T; i += NT) ord[i] = i;
     __syncthreads();
   } else {
-    res_order(R, grouped, R.sort_tasks != 0, ka, kb, ord, A.Tpad);
+    res_order<NT>(R, grouped, R.sort_tasks != 0, ka, kb, ord, A.Tpad);
   }
-  for (int i = tid; i < T; i += RES_THREADS) R.order[i] = ord[i];
+  for (int i = tid; i < T; i += NT) R.order[i] = ord[i];
 
   double* cd = reinterpret_cast<double*>(smem + Lo.cd);
   int32_t* c_anc = reinterpret_cast<int32_t*>(smem + Lo.ci);
-  int32_t* c_caller = c_anc + RES_CHUNK;
-  int32_t* c_grp = c_caller + RES_CHUNK;
+  int32_t* c_grp = c_anc + RES_CHUNK;
   uint32_t* mk = reinterpret_cast<uint32_t*>(smem + Lo.mt) + wave * RES_MT_STRIDE;
   uint64_t* posts = reinterpret_cast<uint64_t*>(smem + Lo.slot);   // [2][WAVES][2]
   int32_t* cposts = reinterpret_cast<int32_t*>(posts);              // opp: [2][WAVES]
@@ -183,24 +184,52 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
   for (int p0 = 0; p0 < T; p0 += RES_CHUNK) {
     const int n = min(RES_CHUNK, T - p0);
     __syncthreads();                      // the previous chunk (and the sort keys) are consumed
-    for (int i = tid; i < n; i += RES_THREADS) {
-      const int t = ord[p0 + i];
-      cd[i * 4 + 0] = R.dem[t];
-      cd[i * 4 + 1] = R.dem[(size_t)T + t];
-      cd[i * 4 + 2] = R.dem[2 * (size_t)T + t];
-      cd[i * 4 + 3] = R.dem[3 * (size_t)T + t];
-      const int g = has_groups ? R.task_group[t] : 0;
-      c_anc[i] = has_groups ? R.group_anchor[g] : 0;
-      c_caller[i] = t;
-      c_grp[i] = g;
+    {
+      // every load of the chunk is issued before the first one is waited for
+      constexpr int PER = RES_CHUNK / NT;
+      int tt[PER], gg[PER], aa[PER];
+      double dd[PER][4];
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        const int i = tid + k * NT;
+        tt[k] = i < n ? ord[p0 + i] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        const int t = tt[k];
+        dd[k][0] = R.dem[t];
+        dd[k][1] = R.dem[(size_t)T + t];
+        dd[k][2] = R.dem[2 * (size_t)T + t];
+        dd[k][3] = R.dem[3 * (size_t)T + t];
+        gg[k] = has_groups ? R.task_group[t] : 0;
+      }
+#pragma unroll
+      for (int k = 0; k < PER; k++) aa[k] = has_groups ? R.group_anchor[gg[k]] : 0;
+#pragma unroll
+      for (int k = 0; k < PER; k++) {
+        const int i = tid + k * NT;
+        if (i < n) {
+          cd[i * 4 + 0] = dd[k][0]; cd[i * 4 + 1] = dd[k][1];
+          cd[i * 4 + 2] = dd[k][2]; cd[i * 4 + 3] = dd[k][3];
+          c_anc[i] = aa[k];
+          c_grp[i] = gg[k];
+        }
+      }
     }
     __syncthreads();
+    // the next task's staged row is read while this task is scored (LDS latency off the chain)
+    double n0 = cd[0], n1 = cd[1], n2 = cd[2], n3 = cd[3];
+    int n_anc = c_anc[0], n_grp = c_grp[0];
     for (int q = 0; q < n; q++) {
       const int p = p0 + q;
-      const double d0 = cd[q * 4 + 0], d1 = cd[q * 4 + 1], d2 = cd[q * 4 + 2], d3 = cd[q * 4 + 3];
-      const int t = c_caller[q];
+      const double d0 = n0, d1 = n1, d2 = n2, d3 = n3;
+      const int anc_q = n_anc, grp_q = n_grp;
+      if (q + 1 < n) {
+        n0 = cd[(q + 1) * 4 + 0]; n1 = cd[(q + 1) * 4 + 1]; n2 = cd[(q + 1) * 4 + 2]; n3 = cd[(q + 1) * 4 + 3];
+        n_anc = c_anc[q + 1]; n_grp = c_grp[q + 1];
+      }
       if (CA) {
-        const int anc = c_anc[q];
+        const int anc = anc_q;
         if (anc != cur_anc) {             // anchor rows of the zone tables -> registers
           cur_anc = anc;
 #pragma unroll
@@ -208,7 +237,7 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
         }
       }
       if (MODE == CA_FF && keyed) {
-        const int g = c_grp[q];
+        const int g = grp_q;
         if (g != cur_grp) {               // frozen host key of the group (cost_aware.py:104-119)
           cur_grp = g;
 #pragma unroll
@@ -230,16 +259,21 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
           fm |= (f ? 1u : 0u) << j;
           cnt += f ? 1 : 0;
         }
-        const int inc = wave_incl_scan(cnt);
+        const int inc = wave_incl_scan_dpp(cnt);
         const int wt = __builtin_amdgcn_readlane(inc, 63);
-        if (lane == 0) cposts[par * RES_WAVES + wave] = wt;
-        __syncthreads();
-        int ntot = 0, off = 0;
+        int ntot = wt, off = 0;
+        if (WAVES > 1) {
+          if (lane == 0) cposts[par * RES_WAVES + wave] = wt;
+          __syncthreads();
+          int v[WAVES];
 #pragma unroll
-        for (int w = 0; w < RES_WAVES; w++) {
-          const int v = cposts[par * RES_WAVES + w];
-          off += (w < wave) ? v : 0;
-          ntot += v;
+          for (int w = 0; w < WAVES; w++) v[w] = cposts[par * RES_WAVES + w];
+          ntot = 0;
+#pragma unroll
+          for (int w = 0; w < WAVES; w++) {
+            off += (w < wave) ? v[w] : 0;
+            ntot += v[w];
+          }
         }
         if (ntot == 0) continue;
         const int k = (int)mt_randint(mk, mw, (uint32_t)ntot) - off;   // randomizer.choice (:16)
@@ -250,7 +284,7 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
             if ((fm >> j) & 1u) {
               if (rr == 0) {
                 a0[j] -= d0; a1[j] -= d1; a2[j] -= d2; a3[j] -= d3;   // commit (:18)
-                R.placement[t] = h0 + j;
+                pl[p] = h0 + j;
               }
               rr--;
             }
@@ -261,8 +295,30 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
 
       // lane best: (score bits, tiebreak:host), first minimum in host order
       uint64_t b1 = NONE, b2 = NONE;
+      bool full = true;
+      if (MODE == CA_BF) {
+        // Exact shortcut: 0 is the least score, and a feasible host scores exactly 0 when its
+        // zone pair is free (c == 0) or it fits exactly (s2 == 0). If the wave holds one, its
+        // best is the first such host and no sqrt/div is needed. A score that might underflow
+        // to 0 without c or s2 being 0 (c >= 2^-300, s2 >= 2^-600, b <= 2^300 keep
+        // c * sqrt(s2) / b >= 2^-900) sends the wave down the full path.
+        int32_t zh = 0x7fffffff;
+        bool risky = false;
 #pragma unroll
-      for (int j = 0; j < HPL; j++) {
+        for (int j = 0; j < HPL; j++) {
+          const bool f = fits<false>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+          const double s2 = norm2_seq(a0[j] - d0, a1[j] - d1, a2[j] - d2, a3[j] - d3);
+          if (f && (cc[j] == 0.0 || s2 == 0.0) && zh == 0x7fffffff) zh = h0 + j;
+          risky |= f && cc[j] != 0.0 && s2 != 0.0 &&
+                   (cc[j] < 0x1p-300 || s2 < 0x1p-600 || bb[j] > 0x1p+300);
+        }
+        if (__ballot(zh != 0x7fffffff) != 0 && __ballot(risky) == 0) {
+          full = false;
+          if (zh != 0x7fffffff) { b1 = 0; b2 = (uint32_t)zh; }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < HPL && full; j++) {
         const bool f = fits<STRICT>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
         uint64_t k1 = 0;
         if (MODE == CA_BF || MODE == VBP_BF) {
@@ -279,47 +335,54 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
       }
       // wave minimum: score bits first; among tied lanes the first holds the lowest host
       // (blocked host mapping), except vbp best-fit, whose tiebreak rank precedes the host
-      uint64_t m1 = b1;
-#pragma unroll
-      for (int off = 1; off < WAVE; off <<= 1) {
-        const uint64_t o = shfl_xor_u64(m1, off);
-        m1 = o < m1 ? o : m1;
+      uint64_t m1, m2;
+      if (MODE == VBP_FF || (MODE == CA_FF && !keyed)) {
+        // first fit by index: the first lane holding a feasible host (blocked host mapping)
+        const uint64_t any = __ballot(b1 != NONE);
+        m1 = any ? 0ull : NONE;
+        m2 = any ? readlane_u64(b2, __builtin_ctzll(any)) : NONE;
+      } else {
+        m1 = wave_min_u64(b1);
+        const uint64_t tied = __ballot(b1 == m1);
+        m2 = readlane_u64(b2, __builtin_ctzll(tied));
+        if (MODE == VBP_BF && __popcll(tied) > 1) m2 = wave_min_u64((b1 == m1) ? b2 : NONE);
       }
-      const uint64_t tied = __ballot(b1 == m1);
-      uint64_t m2 = readlane_u64(b2, __builtin_ctzll(tied));
-      if (MODE == VBP_BF && __popcll(tied) > 1) {
-        uint64_t c2 = (b1 == m1) ? b2 : NONE;
-#pragma unroll
-        for (int off = 1; off < WAVE; off <<= 1) {
-          const uint64_t o = shfl_xor_u64(c2, off);
-          c2 = o < c2 ? o : c2;
+      uint64_t g2 = m2;
+      if (WAVES > 1) {
+        if (lane == 0) {
+          posts[(par * RES_WAVES + wave) * 2 + 0] = m1;
+          posts[(par * RES_WAVES + wave) * 2 + 1] = m2;
         }
-        m2 = readlane_u64(c2, 0);
-      }
-      if (lane == 0) {
-        posts[(par * RES_WAVES + wave) * 2 + 0] = m1;
-        posts[(par * RES_WAVES + wave) * 2 + 1] = m2;
-      }
-      __syncthreads();
-      uint64_t g1 = NONE, g2 = NONE;
+        __syncthreads();
+        uint64_t v1[WAVES], v2[WAVES];         // all posts in flight at once, then compared
 #pragma unroll
-      for (int w = 0; w < RES_WAVES; w++) {
-        const uint64_t v1 = posts[(par * RES_WAVES + w) * 2 + 0];
-        const uint64_t v2 = posts[(par * RES_WAVES + w) * 2 + 1];
-        if (v1 < g1 || (v1 == g1 && v2 < g2)) { g1 = v1; g2 = v2; }
+        for (int w = 0; w < WAVES; w++) {
+          v1[w] = posts[(par * RES_WAVES + w) * 2 + 0];
+          v2[w] = posts[(par * RES_WAVES + w) * 2 + 1];
+        }
+        uint64_t g1 = v1[0];
+        g2 = v2[0];
+#pragma unroll
+        for (int w = 1; w < WAVES; w++) {
+          const bool lt = (v1[w] < g1) | ((v1[w] == g1) & (v2[w] < g2));
+          g1 = lt ? v1[w] : g1;
+          g2 = lt ? v2[w] : g2;
+        }
       }
       if (g2 == NONE) continue;          // no host fits: the task stays waiting
-      const int hw = (int)(uint32_t)g2;
+      const int hw = __builtin_amdgcn_readfirstlane((int)(uint32_t)g2);
+      const int jw = hw & (HPL - 1);     // uniform: the owning lane's register slot
       if (hw / HPL == tid) {
-        const int jw = hw - h0;
 #pragma unroll
         for (int j = 0; j < HPL; j++)
           if (j == jw) { a0[j] -= d0; a1[j] -= d1; a2[j] -= d2; a3[j] -= d3; }   // resc[h] -= d
-        R.placement[t] = hw;
+        pl[p] = hw;
       }
     }
   }
 
+  __syncthreads();
+  for (int i = tid; i < T; i += NT) R.placement[ord[i]] = pl[i];
 #pragma unroll
   for (int j = 0; j < HPL; j++) {
     const int h = h0 + j;
@@ -337,26 +400,38 @@ __global__ __launch_bounds__(RES_THREADS) void resident_kernel(ResidentArgs A) {
   }
 }
 
+// Four waves per round (one per SIMD of a CU). Measured on MI355X with 512 rounds of 1000 hosts
+// x 1000 tasks: one wave per round (16 hosts per lane, no barrier) is ~2x slower -- a single
+// wave's dependent per-task chain cannot hide its own latencies.
 template <int MODE>
-static void launch_mode(int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
-  const dim3 grid(n), block(RES_THREADS);
+static void launch_mode(int waves, int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
+  const dim3 grid(n), four(4 * WAVE);
+  (void)waves;
   switch (hpl) {
-    case 1: hipLaunchKernelGGL((resident_kernel<MODE, 1>), grid, block, lds, st, a); break;
-    case 2: hipLaunchKernelGGL((resident_kernel<MODE, 2>), grid, block, lds, st, a); break;
-    case 4: hipLaunchKernelGGL((resident_kernel<MODE, 4>), grid, block, lds, st, a); break;
-    case 8: hipLaunchKernelGGL((resident_kernel<MODE, 8>), grid, block, lds, st, a); break;
-    default: hipLaunchKernelGGL((resident_kernel<MODE, 16>), grid, block, lds, st, a); break;
+    case 1: hipLaunchKernelGGL((resident_kernel<MODE, 4, 1>), grid, four, lds, st, a); break;
+    case 2: hipLaunchKernelGGL((resident_kernel<MODE, 4, 2>), grid, four, lds, st, a); break;
+    case 4: hipLaunchKernelGGL((resident_kernel<MODE, 4, 4>), grid, four, lds, st, a); break;
+    case 8: hipLaunchKernelGGL((resident_kernel<MODE, 4, 8>), grid, four, lds, st, a); break;
+    default: hipLaunchKernelGGL((resident_kernel<MODE, 4, 16>), grid, four, lds, st, a); break;
   }
 }
 
-void launch_resident(int mode, int hpl, int n, const ResidentArgs& a, hipStream_t st) {
+// Hosts per lane for a batch whose largest round has maxH hosts (4 waves: 256 lanes).
+void resident_shape(int maxH, int* waves, int* hpl) {
+  int h = 1;
+  while (h * RES_THREADS < maxH) h <<= 1;
+  *waves = 4;
+  *hpl = h;
+}
+
+void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a, hipStream_t st) {
   const size_t lds = resident_lds_bytes(a.Zb, a.Tpad);
   switch (mode) {
-    case CA_FF: launch_mode<CA_FF>(hpl, n, lds, a, st); break;
-    case CA_BF: launch_mode<CA_BF>(hpl, n, lds, a, st); break;
-    case OPP: launch_mode<OPP>(hpl, n, lds, a, st); break;
-    case VBP_FF: launch_mode<VBP_FF>(hpl, n, lds, a, st); break;
-    case VBP_BF: launch_mode<VBP_BF>(hpl, n, lds, a, st); break;
+    case CA_FF: launch_mode<CA_FF>(waves, hpl, n, lds, a, st); break;
+    case CA_BF: launch_mode<CA_BF>(waves, hpl, n, lds, a, st); break;
+    case OPP: launch_mode<OPP>(waves, hpl, n, lds, a, st); break;
+    case VBP_FF: launch_mode<VBP_FF>(waves, hpl, n, lds, a, st); break;
+    case VBP_BF: launch_mode<VBP_BF>(waves, hpl, n, lds, a, st); break;
     default: break;
   }
 }
@@ -364,11 +439,11 @@ void launch_resident(int mode, int hpl, int n, const ResidentArgs& a, hipStream_
 template <int MODE>
 static hipError_t attrs_mode(int lds) {
   hipError_t e = hipSuccess, r;
-#define PVT_RES_ATTR(HPL)                                                                        \
-  r = hipFuncSetAttribute((const void*)resident_kernel<MODE, HPL>,                               \
+#define PVT_RES_ATTR(W, HPL)                                                                     \
+  r = hipFuncSetAttribute((const void*)resident_kernel<MODE, W, HPL>,                            \
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);                      \
   if (r != hipSuccess) e = r;
-  PVT_RES_ATTR(1) PVT_RES_ATTR(2) PVT_RES_ATTR(4) PVT_RES_ATTR(8) PVT_RES_ATTR(16)
+  PVT_RES_ATTR(4, 1) PVT_RES_ATTR(4, 2) PVT_RES_ATTR(4, 4) PVT_RES_ATTR(4, 8) PVT_RES_ATTR(4, 16)
 #undef PVT_RES_ATTR
   return e;
 }

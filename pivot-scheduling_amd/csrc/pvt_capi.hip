@@ -684,8 +684,8 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n) {
   }
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
-  int hpl = 1;
-  while (hpl * RES_THREADS < maxH) hpl <<= 1;
+  int waves = 1, hpl = 1;
+  resident_shape(maxH, &waves, &hpl);
   int tpad = 64;
   while (tpad < maxT) tpad <<= 1;
   ctx->rstage.assign(rounds, rounds + n);
@@ -711,7 +711,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n) {
   }
   {
     Scope sc(ctx, PVT_K_SCORE, cand, bytes);
-    launch_resident(mode, hpl, n, ra, st);
+    launch_resident(mode, waves, hpl, n, ra, st);
   }
   HIPCHK(hipGetLastError());
   if (mode == PVT_OPP)

@@ -63,4 +63,43 @@ __device__ __forceinline__ long long wave_sum_ll(long long v) {
   return v;
 }
 
+// DPP row shifts (gfx9 encodings): lane i of each 16-lane row reads lane i - n of the row; a
+// lane whose source falls outside the row keeps `old`.
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t src, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_min_step(uint64_t v) {
+  const uint32_t lo = dpp_u32<CTRL>((uint32_t)v, (uint32_t)v);
+  const uint32_t hi = dpp_u32<CTRL>((uint32_t)(v >> 32), (uint32_t)(v >> 32));
+  const uint64_t o = ((uint64_t)hi << 32) | lo;
+  return o < v ? o : v;
+}
+// Wave-wide unsigned 64-bit minimum, returned uniform: prefix-min over each row with four DPP
+// steps (lane 15 of a row then holds the row's minimum), then the four row minima via readlane.
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+  v = dpp_min_step<DPP_ROW_SHR1>(v);
+  v = dpp_min_step<DPP_ROW_SHR2>(v);
+  v = dpp_min_step<DPP_ROW_SHR4>(v);
+  v = dpp_min_step<DPP_ROW_SHR8>(v);
+  uint64_t m = readlane_u64(v, 15);
+  const uint64_t r1 = readlane_u64(v, 31), r2 = readlane_u64(v, 47), r3 = readlane_u64(v, 63);
+  m = r1 < m ? r1 : m;
+  m = r2 < m ? r2 : m;
+  return r3 < m ? r3 : m;
+}
+// Wave-wide inclusive prefix sum (lane order) with DPP row scans and row offsets.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+  v += (int)dpp_u32<DPP_ROW_SHR1>((uint32_t)v, 0u);
+  v += (int)dpp_u32<DPP_ROW_SHR2>((uint32_t)v, 0u);
+  v += (int)dpp_u32<DPP_ROW_SHR4>((uint32_t)v, 0u);
+  v += (int)dpp_u32<DPP_ROW_SHR8>((uint32_t)v, 0u);
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+  const int r2 = __builtin_amdgcn_readlane(v, 47);
+  const int row = lane_id() >> 4;
+  return v + (row > 0 ? r0 : 0) + (row > 1 ? r1 : 0) + (row > 2 ? r2 : 0);
+}
+
 }  // namespace pvt

@@ -160,8 +160,8 @@ void launch_norm_keys(const double* dem, int T, const int32_t* idx, uint64_t* ke
                       hipStream_t st);
 void launch_group_keys(const int32_t* task_group, const int32_t* idx, int T, uint32_t* keys,
                        hipStream_t st);
-// Resident rounds (pvt_batch.hip): one 256-thread block per round, hosts in registers
-// (HPL hosts per thread, HPL in {1, 2, 4, 8, 16}).
+// Resident rounds (pvt_batch.hip): one block per round (1 wave up to 1024 hosts, else 4), hosts
+// in registers (HPL hosts per lane, HPL in {1, 2, 4, 8, 16}).
 constexpr int RES_THREADS = 256;
 constexpr int RES_MAX_HPL = 16;
 constexpr int RES_MAX_HOSTS = RES_THREADS * RES_MAX_HPL;   // 4096
@@ -173,7 +173,8 @@ struct ResidentArgs {
   int Tpad;               // power of two >= max n_tasks of the batch (sort network size)
 };
 size_t resident_lds_bytes(int Zb, int Tpad);
-void launch_resident(int mode, int hpl, int n, const ResidentArgs& a, hipStream_t st);
+void resident_shape(int maxH, int* waves, int* hpl);
+void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a, hipStream_t st);
 hipError_t resident_init_attrs();
 size_t commit_lds_bytes();
 hipError_t init_kernel_attrs();

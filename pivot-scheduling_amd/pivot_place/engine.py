@@ -121,22 +121,81 @@ class DeviceRound:
 
 
 class DeviceBatch:
-    """Independent rounds resident in HBM for pvt_place_batch: one DeviceRound per round plus
-    the contiguous pvt_round[n] descriptor array the call takes."""
+    """Independent rounds resident in HBM for pvt_place_batch, packed field by field into flat
+    device buffers (round i's arrays are slices at fixed offsets), so ``reset()`` restores every
+    round's snapshot with one D2D copy; ``structs`` is the pvt_round[n] array the call takes."""
+
+    _FIELDS = (("avail", np.float64), ("zone", np.int32), ("tiebreak", np.uint32),
+               ("decay", np.int32), ("cost", np.float64), ("bw", np.float64),
+               ("dem", np.float64), ("task_group", np.int32), ("group_anchor", np.int32))
 
     def __init__(self, rounds, device):
-        self.rounds = [r if isinstance(r, DeviceRound) else DeviceRound(r, device) for r in rounds]
-        self.structs = (_abi.pvt_round * max(len(self.rounds), 1))()
-        for i, dr in enumerate(self.rounds):
-            self.structs[i] = dr.struct
+        torch = _torch()
+        dev = torch.device(device)
+        self.arrays = list(rounds)
+        n = len(self.arrays)
+        self.structs = (_abi.pvt_round * max(n, 1))()
+        self.bufs, offs = {}, {}
+        self.mt, self.mt0 = [], []
+        if n == 0:
+            return
+        for name, dt in self._FIELDS:
+            parts = [getattr(r, name) for r in self.arrays]
+            if all(p is None for p in parts):
+                continue
+            sizes = [0 if p is None else p.size for p in parts]
+            offs[name] = np.concatenate([[0], np.cumsum(sizes)])
+            flat = np.concatenate([np.ascontiguousarray(p, dtype=dt).ravel() for p in parts
+                                   if p is not None]) if any(sizes) else np.zeros(1, dtype=dt)
+            self.bufs[name] = torch.from_numpy(flat).to(dev)
+        self.avail0 = self.bufs["avail"].clone()
+        T = [r.n_tasks for r in self.arrays]
+        toff = np.concatenate([[0], np.cumsum(T)])
+        self.order = torch.empty(max(int(toff[-1]), 1), dtype=torch.int32, device=dev)
+        self.placement = torch.empty(max(int(toff[-1]), 1), dtype=torch.int32, device=dev)
+        self._toff = toff
+        self._hoff = offs["avail"]
+        self.mt0 = [None if r.mt_state is None else r.mt_state.copy() for r in self.arrays]
+        self.mt = [None if m is None else m.copy() for m in self.mt0]
+        for i, r in enumerate(self.arrays):
+            st = _abi.fill_struct(r)
+            for name, dt in self._FIELDS:
+                if name in self.bufs and getattr(r, name) is not None:
+                    buf = self.bufs[name]
+                    setattr(st, name, buf.data_ptr() + int(offs[name][i]) * buf.element_size())
+            st.order = self.order.data_ptr() + int(toff[i]) * 4
+            st.placement = self.placement.data_ptr() + int(toff[i]) * 4
+            st.mt_state = None if self.mt[i] is None else self.mt[i].ctypes.data
+            self.structs[i] = st
+
+    def __len__(self):
+        return len(self.arrays)
 
     def reset(self):
-        for dr in self.rounds:
-            dr.reset()
-        # mt_state pointers are host arrays updated in place; nothing else to refresh
+        if not self.arrays:
+            return
+        self.bufs["avail"].copy_(self.avail0)
+        for m, m0 in zip(self.mt, self.mt0):
+            if m is not None:
+                m[:] = m0
+
+    def placement_of(self, i):
+        return self.placement[int(self._toff[i]):int(self._toff[i + 1])]
 
     def results(self):
-        return [dr.result() for dr in self.rounds]
+        if not self.arrays:
+            return []
+        pl = self.placement.cpu().numpy()
+        od = self.order.cpu().numpy()
+        av = self.bufs["avail"].cpu().numpy()
+        out = []
+        for i, r in enumerate(self.arrays):
+            t0, t1 = int(self._toff[i]), int(self._toff[i + 1])
+            h0, h1 = int(self._hoff[i]), int(self._hoff[i + 1])
+            out.append(RoundResult(placement=pl[t0:t1].copy(), order=od[t0:t1].copy(),
+                                   avail=av[h0:h1].reshape(4, -1).copy(),
+                                   mt_state=None if self.mt[i] is None else self.mt[i].copy()))
+        return out
 
 
 class PlacementEngine:
@@ -192,8 +251,7 @@ class PlacementEngine:
         torch = _torch()
         stream = torch.cuda.current_stream(self.device)
         self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
-        self._check(self.lib.pvt_place_batch(self.ctx, ctypes.addressof(batch.structs),
-                                             len(batch.rounds)))
+        self._check(self.lib.pvt_place_batch(self.ctx, ctypes.addressof(batch.structs), len(batch)))
 
     def place_batch(self, rounds) -> list:
         """Place independent rounds of one policy (each <= PVT_RESIDENT_MAX_HOSTS hosts and

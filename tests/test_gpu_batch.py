@@ -58,6 +58,33 @@ def test_batch_crowded_and_tied(engine, mode):
         _assert_same(res, oracle.place(r), "scenario %d" % s)
 
 
+@pytest.mark.parametrize("resident", [True, False])
+def test_ca_bf_zero_scores_and_underflow(engine, resident):
+    """cost_aware best-fit scores of exactly 0 (free zone pairs, exact fits in costly zones) and
+    scores that underflow to 0 from a subnormal egress cost: ties at 0 go to the lowest host."""
+    rounds = []
+    for s in range(8):
+        r = synthetic.make_round(_abi.PVT_CA_BF, 600, 400, seed=70 + s)
+        r.cost = r.cost.copy()
+        r.cost[:, 1] = 5e-324 if s % 2 else 1e-300      # zone 1: (sub)normal tiny egress cost
+        r.cost[1, :] = 0.0 if s % 3 else r.cost[1, :]
+        # exact fits: some hosts hold exactly the demand of some tasks
+        for k in range(0, 600, 37):
+            t = (k * 7 + s) % r.n_tasks
+            r.avail[:, k] = r.dem[:, t]
+        rounds.append(r)
+    if resident:
+        got = engine.place_batch(rounds)
+    else:
+        engine.set_resident(0)
+        try:
+            got = [engine.place(r) for r in rounds]
+        finally:
+            engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+    for s, (r, res) in enumerate(zip(rounds, got)):
+        _assert_same(res, oracle.place(r), "scenario %d" % s)
+
+
 def test_batch_golden_runs(engine):
     """Every golden run (reference schedule() calls) batched per policy configuration."""
     by_mode = {}
