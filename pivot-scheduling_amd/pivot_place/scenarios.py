@@ -6,6 +6,9 @@ scenarios on its own GPU; a single gather of small per-scenario summaries at the
 rank the whole batch's results (the "final metrics gather" of §8(e)).
 
 ``engine`` is anything with ``place(RoundArrays) -> RoundResult`` (a PlacementEngine on a GPU).
+When it also has ``place_batch`` and the rounds fit the resident kernel (<= 4096 hosts and
+tasks), a rank's block is placed ``batch`` rounds per call: one launch, one workgroup per
+scenario (include/pivot_place.h, pvt_place_batch).
 """
 import hashlib
 
@@ -30,21 +33,33 @@ def summarize(seed, res):
             "digest": h.hexdigest()[:16]}
 
 
-def run_block(engine, mode, n_hosts, n_tasks, seeds):
+RESIDENT_MAX = 4096   # pvt_place_batch limits (PVT_RESIDENT_MAX_HOSTS / _TASKS)
+
+
+def run_block(engine, mode, n_hosts, n_tasks, seeds, batch=512):
+    """Place one synthetic round per seed; returns the per-scenario summaries in seed order."""
+    seeds = [int(s) for s in seeds]
+    batched = (hasattr(engine, "place_batch") and batch > 0 and n_hosts <= RESIDENT_MAX
+               and n_tasks <= RESIDENT_MAX)
     out = []
-    for s in seeds:
-        r = synthetic.make_round(mode, n_hosts, n_tasks, seed=int(s))
-        out.append(summarize(s, engine.place(r)))
+    if not batched:
+        for s in seeds:
+            out.append(summarize(s, engine.place(synthetic.make_round(mode, n_hosts, n_tasks, seed=s))))
+        return out
+    for i in range(0, len(seeds), batch):
+        block = seeds[i:i + batch]
+        rounds = [synthetic.make_round(mode, n_hosts, n_tasks, seed=s) for s in block]
+        out.extend(summarize(s, res) for s, res in zip(block, engine.place_batch(rounds)))
     return out
 
 
-def run_sharded(engine, mode, n_hosts, n_tasks, seeds, group=None):
+def run_sharded(engine, mode, n_hosts, n_tasks, seeds, group=None, batch=512):
     """Run this rank's block of ``seeds`` and gather every rank's summaries (in seed order)."""
     import torch.distributed as dist
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     lo, hi = shard(len(seeds), world, rank)
-    mine = run_block(engine, mode, n_hosts, n_tasks, seeds[lo:hi])
+    mine = run_block(engine, mode, n_hosts, n_tasks, seeds[lo:hi], batch=batch)
     if world == 1:
         return mine
     parts = [None] * world

@@ -29,6 +29,17 @@ class _OracleEngine:
         return oracle.place(r)
 
 
+class _OracleBatchEngine(_OracleEngine):
+    """Adds the batch entry point (PlacementEngine.place_batch's contract), counting calls."""
+
+    def __init__(self):
+        self.batches = []
+
+    def place_batch(self, rounds):
+        self.batches.append(len(rounds))
+        return [self.place(r) for r in rounds]
+
+
 def _worker(rank, world, port, mode, seeds, out_q):
     sys.path[:0] = [os.path.join(os.path.dirname(HERE), "pivot-scheduling_amd"),
                     os.path.dirname(HERE), HERE]
@@ -60,6 +71,20 @@ def test_scenario_batch_two_ranks(mode):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got[0] == ref and got[1] == ref
+
+
+def test_batched_block_equals_per_round_block():
+    """run_block through place_batch (blocks of `batch` rounds) == one place() per scenario."""
+    from pivot_place import scenarios
+    seeds = list(range(200, 211))
+    for mode in (1, 2, 4):
+        ref = scenarios.run_block(_OracleEngine(), mode, 200, 30, seeds)
+        eng = _OracleBatchEngine()
+        assert scenarios.run_block(eng, mode, 200, 30, seeds, batch=4) == ref
+        assert eng.batches == [4, 4, 3]
+    big = _OracleBatchEngine()
+    scenarios.run_block(big, 3, scenarios.RESIDENT_MAX + 1, 2, [1])
+    assert big.batches == []          # beyond the resident limits: one place() per round
 
 
 def test_shard_blocks_cover_everything():

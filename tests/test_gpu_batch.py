@@ -132,3 +132,18 @@ def test_batch_repeated_runs_are_identical(engine):
     engine.run_batch(b)
     for a, c in zip(first, b.results()):
         _assert_same(c, a)
+
+
+@pytest.mark.parametrize("mode", ALL_MODES)
+def test_scenario_driver_on_gpu(engine, mode):
+    """pivot_place.scenarios.run_block on the GPU engine (batched launches) equals the CPU
+    restatement run scenario by scenario (per-scenario digests of placements + availability)."""
+    from pivot_place import scenarios
+
+    class Cpu:
+        def place(self, r):
+            return oracle.place(r)
+
+    seeds = list(range(500, 540))
+    assert scenarios.run_block(engine, mode, 700, 250, seeds, batch=16) == \
+        scenarios.run_block(Cpu(), mode, 700, 250, seeds)
