@@ -14,6 +14,21 @@ __device__ __forceinline__ double norm2_seq(double x0, double x1, double x2, dou
   return __builtin_fma(x3, x3, s);
 }
 
+// Conservative bound on the squared residual norm of a cost_aware best-fit candidate:
+// if fl(fl(c*sqrt(s2))/b) <= thr then s2 <= lim (rounding slack 2^-40 >> 2^-53).
+__device__ __forceinline__ double ca_lim(double thr, double c, double b) {
+  if (!(thr < DINF)) return DINF;
+  if (c == 0.0) return thr > 0.0 ? DINF : -1.0;   // score is exactly 0 in zero-cost zones
+  double r = thr * b / c;
+  r = r * (1.0 + 0x1p-40);
+  return r * r * (1.0 + 0x1p-40);
+}
+__device__ __forceinline__ double vbp_lim(double thr) {
+  if (!(thr < DINF)) return DINF;
+  double r = thr * (1.0 + 0x1p-40);
+  return r * r * (1.0 + 0x1p-40);
+}
+
 __device__ __forceinline__ bool lexless(double s1, uint32_t t1, int32_t i1, double s2, uint32_t t2,
                                         int32_t i2) {
   return s1 < s2 || (s1 == s2 && (t1 < t2 || (t1 == t2 && i1 < i2)));

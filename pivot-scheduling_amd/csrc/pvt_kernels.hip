@@ -17,21 +17,6 @@
 
 namespace pvt {
 
-// Conservative bound on the squared residual norm of a cost_aware best-fit candidate:
-// if fl(fl(c*sqrt(s2))/b) <= thr then s2 <= lim (rounding slack 2^-40 >> 2^-53).
-__device__ __forceinline__ double ca_lim(double thr, double c, double b) {
-  if (!(thr < DINF)) return DINF;
-  if (c == 0.0) return thr > 0.0 ? DINF : -1.0;   // score is exactly 0 in zero-cost zones
-  double r = thr * b / c;
-  r = r * (1.0 + 0x1p-40);
-  return r * r * (1.0 + 0x1p-40);
-}
-__device__ __forceinline__ double vbp_lim(double thr) {
-  if (!(thr < DINF)) return DINF;
-  double r = thr * (1.0 + 0x1p-40);
-  return r * r * (1.0 + 0x1p-40);
-}
-
 // Insert (cs, ct, ci) into the wave-held sorted list (lane j holds entry j). The caller has
 // checked it beats entry KL-1, which falls off.
 __device__ __forceinline__ void list_insert(double& s, uint32_t& t, int32_t& i, double cs,

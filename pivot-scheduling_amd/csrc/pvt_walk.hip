@@ -53,7 +53,7 @@ struct RingSlot {
   int32_t rec[32];                        // TaskRec dwords 0-15, [16] ring entries,
 };                                        // [17] list position after the last one
 
-struct HK {
+struct alignas(8) HK {
   int32_t key;                            // host id or H_EMPTY
   int32_t val;                            // live index or H_DEAD
 };
@@ -84,9 +84,11 @@ __device__ __forceinline__ uint32_t wslot(int32_t id) {
 __device__ __forceinline__ int32_t wfind(const WalkLDS& S, int32_t id, int32_t& pos) {
   uint32_t p = wslot(id);
   for (;;) {
-    const HK e = S.hk[p];
-    if (e.key == id) { pos = (int32_t)p; return e.val; }
-    if (e.key == H_EMPTY) { pos = (int32_t)p; return H_MISS; }
+    // key and value in ONE 64-bit LDS read (two dependent reads would double a probe's latency)
+    const uint64_t kv = *reinterpret_cast<const uint64_t*>(&S.hk[p]);
+    const int32_t key = (int32_t)(uint32_t)kv, val = (int32_t)(uint32_t)(kv >> 32);
+    if (key == id) { pos = (int32_t)p; return val; }
+    if (key == H_EMPTY) { pos = (int32_t)p; return H_MISS; }
     p = (p + 1) & (WH_SLOTS - 1);
   }
 }
