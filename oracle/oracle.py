@@ -33,6 +33,8 @@ def lib():
         _lib.oracle_norm4.argtypes = [ctypes.POINTER(ctypes.c_double)]
         _lib.oracle_randint.restype = ctypes.c_uint32
         _lib.oracle_randint.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
+        _lib.oracle_place_mt.restype = ctypes.c_int
+        _lib.oracle_place_mt.argtypes = [ctypes.c_void_p, ctypes.c_int]
     return _lib
 
 
@@ -40,8 +42,10 @@ def _ptr(a):
     return None if a is None else a.ctypes.data
 
 
-def place(r):
-    """Run one round on the CPU restatement. ``r``: pivot_place._abi.RoundArrays."""
+def place(r, threads=0):
+    """Run one round on the CPU restatement. ``r``: pivot_place._abi.RoundArrays. ``threads``
+    > 0 runs the OpenMP variant (oracle_place_mt: same results, host scans split over threads;
+    the all-cores CPU baseline of bench.py)."""
     from pivot_place._abi import RoundResult, check_rc, fill_struct
     avail = r.avail.copy()
     T = r.n_tasks
@@ -53,7 +57,10 @@ def place(r):
     s.cost, s.bw, s.dem = _ptr(r.cost), _ptr(r.bw), _ptr(r.dem)
     s.task_group, s.group_anchor = _ptr(r.task_group), _ptr(r.group_anchor)
     s.order, s.placement, s.mt_state = _ptr(order), _ptr(placement), _ptr(mt)
-    check_rc(lib().oracle_place(ctypes.addressof(s)))
+    if threads > 0:
+        check_rc(lib().oracle_place_mt(ctypes.addressof(s), int(threads)))
+    else:
+        check_rc(lib().oracle_place(ctypes.addressof(s)))
     return RoundResult(placement=placement, order=order, avail=avail, mt_state=mt)
 
 

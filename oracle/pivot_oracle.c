@@ -269,3 +269,127 @@ int oracle_place(const pvt_round* r) {
   free(ks);
   return rc;
 }
+
+/* ---------------------------------------------------------------- multi-threaded baseline */
+/*
+ * oracle_place_mt: the same restatement with every per-task host scan split over `threads`
+ * OpenMP threads (static contiguous chunks), each chunk reduced to its first best host and the
+ * chunks combined in host order, then the commit applied serially -- so results are identical
+ * to oracle_place's (tests/test_oracle_golden.py checks it). bench.py times it as the all-cores
+ * CPU baseline; it is not a parity checker.
+ */
+#include <omp.h>
+
+typedef struct { double s; uint32_t tb; int32_t h; } cand;
+static inline int cand_less(cand a, cand b) {   /* (s, tb, h) lexicographic; h < 0 = none */
+  if (a.h < 0) return 0;
+  if (b.h < 0) return 1;
+  if (a.s != b.s) return a.s < b.s;
+  if (a.tb != b.tb) return a.tb < b.tb;
+  return a.h < b.h;
+}
+
+/* Best host of one task: mode CA_BF (>=, egress score), VBP_BF (>, norm, tiebreak), first-fit
+ * by index (strict or not), or first-fit over hosts in `hs` key order (CA_FF sort_hosts). */
+static int32_t mt_pick(const pvt_round* r, int mode, const double d[4], int anchor,
+                       const keyed* hs, int threads) {
+  const int H = r->n_hosts, Z = r->n_zones;
+  cand best = {0.0, 0u, -1};
+#pragma omp parallel num_threads(threads)
+  {
+    cand mine = {0.0, 0u, -1};
+#pragma omp for schedule(static) nowait
+    for (int q = 0; q < H; q++) {
+      const int h = hs ? hs[q].i : q;
+      double a[4]; host_vec(r->avail, H, h, a);
+      if (mode == PVT_CA_BF) {
+        if (!fits_ge(a, d)) continue;
+        double x[4] = {a[0] - d[0], a[1] - d[1], a[2] - d[2], a[3] - d[3]};
+        int z = r->zone[h];
+        double bw = r->bw[anchor * Z + z] + r->bw[z * Z + anchor];
+        double c = r->cost[anchor * Z + z] + r->cost[z * Z + anchor];
+        cand k = {c * oracle_norm4(x) * 1.0 / bw, 0u, h};
+        if (cand_less(k, mine)) mine = k;
+      } else if (mode == PVT_VBP_BF) {
+        if (!fits_gt(a, d)) continue;
+        double x[4] = {a[0] - d[0], a[1] - d[1], a[2] - d[2], a[3] - d[3]};
+        cand k = {oracle_norm4(x), r->tiebreak[h], h};
+        if (cand_less(k, mine)) mine = k;
+      } else {   /* first fit: the first position q in scan order */
+        const int strict = (mode == PVT_CA_FF);
+        if (mine.h >= 0) continue;
+        if (strict ? fits_gt(a, d) : fits_ge(a, d)) { mine.s = (double)q; mine.h = h; }
+      }
+    }
+#pragma omp critical
+    if (cand_less(mine, best)) best = mine;
+  }
+  return best.h;
+}
+
+int oracle_place_mt(const pvt_round* r, int threads) {
+  if (!r || r->n_hosts < 1 || r->n_tasks < 0 || r->n_zones < 1) return PVT_EINVAL;
+  if (threads < 1) threads = 1;
+  if (r->n_tasks == 0) return PVT_OK;
+  if (!r->avail || !r->zone || !r->dem || !r->placement || !r->order) return PVT_EINVAL;
+  const int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
+  if (r->mode == PVT_OPP) {
+    if (!r->mt_state) return PVT_EINVAL;
+    for (int t = 0; t < T; t++) {
+      r->order[t] = t;
+      r->placement[t] = -1;
+      double d[4]; task_vec(r->dem, T, t, d);
+      int64_t nq = 0;
+#pragma omp parallel for num_threads(threads) reduction(+ : nq) schedule(static)
+      for (int h = 0; h < H; h++) { double a[4]; host_vec(r->avail, H, h, a); nq += fits_ge(a, d); }
+      if (nq == 0) continue;
+      uint32_t k = oracle_randint(r->mt_state, (uint64_t)nq);
+      for (int h = 0; h < H; h++) {
+        double a[4]; host_vec(r->avail, H, h, a);
+        if (fits_ge(a, d)) {
+          if (k == 0) { r->placement[t] = h; commit(r->avail, H, h, d); break; }
+          k--;
+        }
+      }
+    }
+    return PVT_OK;
+  }
+  for (int t = 0; t < T; t++) r->placement[t] = -1;
+  keyed* ks = (keyed*)malloc(sizeof(keyed) * (size_t)(H > T ? H : T));
+  keyed* hs = (keyed*)malloc(sizeof(keyed) * (size_t)H);
+  if (!ks || !hs) { free(ks); free(hs); return PVT_ENOMEM; }
+  const int ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
+  if (ca && (!r->cost || !r->bw || (r->task_group && !r->group_anchor))) { free(ks); free(hs); return PVT_EINVAL; }
+  if (r->mode == PVT_VBP_BF && !r->tiebreak) { free(ks); free(hs); return PVT_EINVAL; }
+  const int G = (ca && r->task_group) ? r->n_groups : 1;
+  int off = 0;
+  for (int g = 0; g < G; g++) {
+    const int anchor = (ca && r->group_anchor) ? r->group_anchor[g] : 0;
+    const int n = group_tasks(r, ca ? g : 0, r->sort_tasks, ks, r->order + off);
+    const keyed* order = NULL;
+    if (r->mode == PVT_CA_FF && r->sort_hosts) {   /* frozen keys of the group (:104-119) */
+#pragma omp parallel for num_threads(threads) schedule(static)
+      for (int h = 0; h < H; h++) {
+        double a[4]; host_vec(r->avail, H, h, a);
+        int z = r->zone[h];
+        double bw = r->bw[anchor * Z + z] + r->bw[z * Z + anchor];
+        double c = r->cost[anchor * Z + z] + r->cost[z * Z + anchor];
+        double df = r->decay ? (double)r->decay[h] : 1.0;
+        hs[h].i = h;
+        hs[h].k = c * df / (oracle_norm4(a) * bw);
+      }
+      qsort(hs, (size_t)H, sizeof(keyed), cmp_keyed);
+      order = hs;
+    }
+    for (int j = 0; j < n; j++) {
+      const int t = r->order[off + j];
+      double d[4]; task_vec(r->dem, T, t, d);
+      const int32_t h = mt_pick(r, r->mode, d, anchor, order, threads);
+      if (h >= 0) { r->placement[t] = h; commit(r->avail, H, h, d); }
+    }
+    off += n;
+  }
+  free(ks);
+  free(hs);
+  return PVT_OK;
+}

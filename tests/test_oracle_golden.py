@@ -55,3 +55,27 @@ def test_choice_is_randint():
         a, b = np.random.RandomState(5), np.random.RandomState(5)
         for _ in range(100):
             assert a.choice(list(range(n))) == b.randint(0, n)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_multithreaded_baseline_equals_oracle(threads):
+    """oracle_place_mt (the all-cores CPU baseline bench.py times) returns exactly what the
+    single-threaded restatement returns: golden runs and synthetic rounds of every policy."""
+    from pivot_place import synthetic
+    rounds = []
+    for name, idx in golden_io.all_runs():
+        case = golden_io.load(name)
+        rounds.append(golden_io.run_arrays(case, case["runs"][idx]))
+    for mode in range(5):
+        rounds.append(synthetic.make_round(mode, 3000, 200, seed=40 + mode))
+        crowded = synthetic.make_round(mode, 300, 600, seed=50 + mode)
+        crowded.avail[0, :] = 4.0
+        crowded.avail[1, :] = 40000.0
+        rounds.append(crowded)
+    for r in rounds:
+        a, b = oracle.place(r), oracle.place(r, threads=threads)
+        np.testing.assert_array_equal(a.placement, b.placement)
+        np.testing.assert_array_equal(a.order, b.order)
+        assert np.array_equal(a.avail, b.avail)
+        if a.mt_state is not None:
+            np.testing.assert_array_equal(a.mt_state, b.mt_state)
