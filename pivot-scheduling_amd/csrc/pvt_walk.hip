@@ -17,12 +17,25 @@
 // capacities. Hosts committed to by the previous window, when that window's commits landed after
 // this window's lists were scored, enter the walk as touched hosts (inherited).
 //
-// Execution: ONE workgroup on one CU. Wave 0 is the walker; waves 1..PRODUCERS stream each
-// task's list head (64 entries + task record) from HBM into an LDS ring ahead of the walker, so
-// the walker's critical path is LDS, cross-lane and scalar work only: it never waits on HBM
-// except on the rare deep-list path. Ring hand-off: a producer fills slot i % RING, waits for
-// its LDS writes (lgkmcnt 0) and publishes flag[slot] = i; the walker publishes done = i + 1
-// when task i no longer needs its slot. Every spin is bounded; a timeout reports status -1.
+// Execution: ONE workgroup on one CU, pipelined. Waves 1..PRODUCERS ("scouts") each take every
+// PRODUCERS-th task: stream its list head (64 entries + task record) from HBM into an LDS ring
+// slot, wait until the walk has committed every task up to i - LOOK, and then evaluate task i
+// completely on that state -- touched-ness of the list entries, the deep list in HBM if needed,
+// exact rescoring of the live touched hosts -- keeping the LOOK best candidates of each kind.
+// Wave 0 (the walker) only patches that result with the hosts committed since (the tasks
+// i - LOOK + 1 .. i - 1: at most LOOK - 1 "dirty" hosts, whose exact state it holds in
+// registers), picks the winner and commits. A dirty host is dropped from the scout's lists by
+// id and rescored exactly; every other host's state is what the scout saw, so LOOK candidates
+// of each kind always leave a valid one.
+//
+// What a scout may see of a concurrent commit: the hash and the live table only grow (a host
+// that dies is marked in place, never moved), and a new live entry becomes visible only through
+// nl_pub, published after the entry is written. LDS operations of one wave execute in issue
+// order, so a scout that reads committed >= k (or nl_pub >= n) also reads everything the walker
+// wrote before. Anything torn belongs to a dirty host, which the walker re-evaluates.
+// Hand-offs: a scout publishes flag[slot] = i when task i's slot and result are complete; the
+// walker publishes done = i + 1 when it no longer reads slot i and committed = i + 1 after task
+// i's commit. Every spin is bounded; a timeout reports status -1.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -31,8 +44,16 @@
 
 namespace pvt {
 
-constexpr int RING = 16;                  // ring slots (task lists in LDS)
-constexpr int PRODUCERS = 8;              // loader waves
+constexpr int RING = 12;                  // ring slots (task lists in LDS)
+#ifndef PVT_LOOK
+#define PVT_LOOK 2
+#endif
+#ifndef PVT_PRODUCERS
+#define PVT_PRODUCERS 7
+#endif
+constexpr int LOOK = PVT_LOOK;            // a task is scouted on the state after task i - LOOK
+constexpr int NDIRTY = LOOK - 1;          // hosts committed since: re-evaluated by the walker
+constexpr int PRODUCERS = PVT_PRODUCERS;  // loader / scout waves
 constexpr int PRE_CHUNKS = 4;             // list chunks a loader fetches before filtering
 constexpr int WALK_THREADS = (1 + PRODUCERS) * WAVE;
 constexpr int WH_BITS = 12;               // touched-host hash: 4096 slots for <= 2048 hosts
@@ -44,6 +65,15 @@ constexpr int32_t H_DEAD = -2;            // hash value: touched, can no longer 
 constexpr int32_t H_PENDING = 0x7fffffff; // hash value before the walker writes it
 constexpr int SPIN_LIMIT = 1 << 24;       // bounded spins (x s_sleep 2 ~ seconds)
 
+// A scout's result: LOOK usable list entries in list order (untouched, or for first-fit
+// touched and fitting) and, for best-fit, the LOOK best live touched hosts; one 16-dword
+// record per candidate (the walker reads dword k from lane k / 2 of one 64-bit load).
+constexpr int RF_S = 0, RF_TB = 2, RF_ID = 3, RF_Z = 4, RF_Q = 5, RF_OWN = 6, RF_HP = 7, RF_A = 8;
+constexpr int RREC = 16;                  // dwords per candidate record
+constexpr int R_U = 0, R_T = LOOK * RREC, R_NU = 2 * LOOK * RREC, R_NT = R_NU + 1;
+constexpr int R_WORDS = 2 * WAVE;
+static_assert(R_NT < R_WORDS, "scout result exceeds 128 dwords");
+
 struct RingSlot {
   double s[WAVE];
   double a[4][WAVE];
@@ -51,7 +81,9 @@ struct RingSlot {
   int32_t zone[WAVE];
   uint32_t tb[WAVE];
   int32_t rec[32];                        // TaskRec dwords 0-15, [16] ring entries,
-};                                        // [17] list position after the last one
+                                          // [17] list position after the last one
+  int32_t res[R_WORDS];                   // the scout's result
+};
 
 struct alignas(8) HK {
   int32_t key;                            // host id or H_EMPTY
@@ -73,6 +105,8 @@ struct WalkLDS {
   int32_t done;
   int32_t stop;
   int32_t nl_init;
+  int32_t nl_pub;                         // live entries [0, nl_pub) are complete
+  int32_t committed;                      // tasks committed (-1 until the inherited hosts are in)
 };
 static_assert(sizeof(WalkLDS) <= 160 * 1024, "commit walk LDS exceeds a CU's 160 KiB");
 
@@ -142,13 +176,203 @@ __device__ __forceinline__ uint64_t stamp() {
 #define STAMP(k) do {} while (0)
 #endif
 
-// ---------------------------------------------------------------- loader waves
-// A loader copies task i's list into ring slot i % RING, skipping entries that can no longer
+// ---------------------------------------------------------------- scouts (loader waves)
+// Record r of a result block from lane `lane` (the lane holding the candidate): its score,
+// tiebreak, host, zone, live index (-1 untouched), own flag, hash position, capacities.
+__device__ __forceinline__ void put_rec(int32_t* res, int base, double s, uint32_t tb, int32_t id,
+                                        int32_t z, int32_t q, int32_t own, int32_t hp, double a0,
+                                        double a1, double a2, double a3) {
+  int32_t* r = res + base;
+  *reinterpret_cast<double*>(r + RF_S) = s;
+  r[RF_TB] = (int32_t)tb; r[RF_ID] = id; r[RF_Z] = z; r[RF_Q] = q; r[RF_OWN] = own; r[RF_HP] = hp;
+  double* a = reinterpret_cast<double*>(r + RF_A);
+  a[0] = a0; a[1] = a1; a[2] = a2; a[3] = a3;
+}
+
+// Exact best-fit key of a host for the task: (score bits, tiebreak:id); scores are >= +0, so
+// their bit patterns order like the values (cost_aware.py:83, vbp.py:45).
+template <int MODE>
+__device__ __forceinline__ void bf_key(const WalkLDS& S, int Z, int anc, double a0, double a1,
+                                       double a2, double a3, double d0, double d1, double d2,
+                                       double d3, int32_t z, uint32_t tb, int32_t id, uint64_t& k1,
+                                       uint64_t& k2) {
+  const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
+  double sc;
+  if (MODE == CA_BF) sc = (S.csum[anc * Z + z] * __builtin_sqrt(s2)) / S.bsum[anc * Z + z];
+  else sc = __builtin_sqrt(s2);
+  k1 = (uint64_t)__double_as_longlong(sc);
+  k2 = ((uint64_t)(MODE == VBP_BF ? tb : 0u) << 32) | (uint32_t)id;
+}
+__device__ __forceinline__ bool key_lt(uint64_t a1, uint64_t a2, uint64_t b1, uint64_t b2) {
+  return (a1 < b1) | ((a1 == b1) & (a2 < b2));
+}
+
+// Task i, after the walk has committed every task <= i - LOOK: the LOOK first usable entries of
+// its list (ring, then the deep list in HBM) and, for best-fit, the LOOK best live touched hosts
+// that could still win; written to R.res.
+template <int MODE>
+__device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int i, int k, int32_t rv) {
+  constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
+  constexpr bool BEST = (MODE == CA_BF || MODE == VBP_BF);
+  const int lane = lane_id();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const double d0 = rec_d(rv, 0), d1 = rec_d(rv, 1), d2 = rec_d(rv, 2), d3 = rec_d(rv, 3);
+  const int cnt = __builtin_amdgcn_readlane(rv, 8);
+  const bool comp = __builtin_amdgcn_readlane(rv, 9) != 0;
+  const int anc = __builtin_amdgcn_readlane(rv, 10);
+  const int npos = __builtin_amdgcn_readlane(R.rec[lane & 31], 17);   // own writes, in order
+
+  // usable ring entries (lane j: entry j)
+  int nU = 0;
+  uint64_t u1 = ~0ull, u2 = ~0ull;          // key of the last usable entry kept (best-fit)
+  {
+    const bool valid = lane < k;
+    const int32_t id = R.id[lane];
+    int32_t hp = 0;
+    const int32_t hv = valid ? wfind(S, id, hp) : H_MISS;
+    // H_PENDING: the walker is inserting this host right now, so it is dirty for this task and
+    // the walker re-evaluates it; first-fit keeps it (conservatively usable), best-fit does not
+    // list touched hosts at all
+    const bool live = hv >= 0 && hv != H_PENDING;
+    const int q = live ? hv : 0;
+    double c0 = R.a[0][lane], c1 = R.a[1][lane], c2 = R.a[2][lane], c3 = R.a[3][lane];
+    int32_t own = 0, hpos = hp;
+    bool usable;
+    if (BEST) {
+      usable = valid && hv == H_MISS;
+    } else {
+      if (live) {
+        c0 = S.la[0][q]; c1 = S.la[1][q]; c2 = S.la[2][q]; c3 = S.la[3][q];
+        own = S.lown[q]; hpos = S.lhp[q];
+      }
+      usable = valid && (hv == H_MISS || hv == H_PENDING ||
+                         (live && fits<STRICT>(c0, c1, c2, c3, d0, d1, d2, d3)));
+    }
+    const uint64_t m = __ballot(usable);
+    const int rank = __popcll(m & below);
+    const double s = R.s[lane];
+    const uint32_t tb = R.tb[lane];
+    if (usable && rank < LOOK)
+      put_rec(R.res, R_U + rank * RREC, s, tb, id, R.zone[lane], live ? hv : -1, own, hpos,
+              c0, c1, c2, c3);
+    nU = min(__popcll(m), LOOK);
+    if (BEST && nU == LOOK) {
+      const uint64_t lm = __ballot(usable && rank == LOOK - 1);
+      const int L = __builtin_ctzll(lm);
+      u1 = readlane_u64((uint64_t)__double_as_longlong(s), L);
+      u2 = ((uint64_t)(MODE == VBP_BF ? readlane_u(tb, L) : 0u) << 32) | (uint32_t)readlane_i(id, L);
+    }
+  }
+  // deep list (rare): entries after the ring's, by id, then their records from HBM
+  const int32_t* ids = A.L.ids + (size_t)i * LMAX;
+  const ListEntry* le = A.L.e + (size_t)i * LMAX;
+  for (int c0 = npos; c0 < cnt && nU < LOOK; c0 += WAVE) {
+    const bool v = c0 + lane < cnt;
+    const int32_t id = v ? ids[c0 + lane] : 0;
+    int32_t hp = 0;
+    const int32_t hv = v ? wfind(S, id, hp) : H_MISS;
+    const bool live = hv >= 0 && hv != H_PENDING;
+    const int q = live ? hv : 0;
+    bool usable;
+    if (BEST) {
+      usable = v && hv == H_MISS;
+    } else {
+      usable = v && (hv == H_MISS || hv == H_PENDING ||
+                     (live && fits<STRICT>(S.la[0][q], S.la[1][q], S.la[2][q], S.la[3][q], d0, d1, d2, d3)));
+    }
+    const uint64_t m = __ballot(usable);
+    const int rank = nU + __popcll(m & below);
+    if (usable && rank < LOOK) {
+      const ListEntry& x = le[c0 + lane];
+      double c0_ = x.a[0], c1 = x.a[1], c2 = x.a[2], c3 = x.a[3];
+      int32_t own = 0, hpos = hp;
+      if (!BEST && live) {
+        c0_ = S.la[0][q]; c1 = S.la[1][q]; c2 = S.la[2][q]; c3 = S.la[3][q];
+        own = S.lown[q]; hpos = S.lhp[q];
+      }
+      put_rec(R.res, R_U + rank * RREC, x.s, x.tb, id, x.zone, live ? hv : -1, own, hpos, c0_, c1, c2, c3);
+      if (BEST && rank == LOOK - 1) {
+        u1 = (uint64_t)__double_as_longlong(x.s);
+        u2 = ((uint64_t)(MODE == VBP_BF ? x.tb : 0u) << 32) | (uint32_t)id;
+      }
+    }
+    if (BEST && nU + __popcll(m) >= LOOK) {
+      const uint64_t lm = __ballot(usable && rank == LOOK - 1);
+      const int L = __builtin_ctzll(lm);
+      u1 = readlane_u64(u1, L);
+      u2 = readlane_u64(u2, L);
+    }
+    nU = min(nU + __popcll(m), LOOK);
+  }
+
+  // best-fit: the LOOK best live touched hosts that rank before the bound any winner respects:
+  // the LOOK-th usable entry, or with fewer the list bound (incomplete list) or nothing
+  int nT = 0;
+  if (BEST) {
+    uint64_t b1 = u1, b2 = u2;
+    if (nU < LOOK) {
+      if (comp) {
+        b1 = ~0ull; b2 = ~0ull;
+      } else {   // every untouched host outside the list ranks at or after the bound (bid + 1)
+        b1 = (uint64_t)__double_as_longlong(rec_d(rv, 6));
+        b2 = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane(rv, 14)) << 32) +
+             (uint32_t)__builtin_amdgcn_readlane(rv, 15) + 1;
+      }
+    }
+    uint64_t tk1[LOOK], tk2[LOOK];
+    int32_t tq[LOOK];
+#pragma unroll
+    for (int r = 0; r < LOOK; r++) { tk1[r] = ~0ull; tk2[r] = ~0ull; tq[r] = -1; }
+    const int nlp = __builtin_amdgcn_readfirstlane(vload(&S.nl_pub));
+    for (int q0 = 0; q0 < nlp; q0 += WAVE) {
+      const int q = q0 + lane;
+      const int qq = min(q, nlp - 1);
+      const double a0 = S.la[0][qq], a1 = S.la[1][qq], a2 = S.la[2][qq], a3 = S.la[3][qq];
+      const bool fit = (q < nlp) && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
+      if (__ballot(fit) == 0) continue;
+      uint64_t k1 = ~0ull, k2 = ~0ull;
+      bf_key<MODE>(S, A.Z, anc, a0, a1, a2, a3, d0, d1, d2, d3, S.lz[qq],
+                   MODE == VBP_BF ? S.ltb[qq] : 0u, S.lid[qq], k1, k2);
+      uint64_t pm = __ballot(fit && key_lt(k1, k2, b1, b2) && key_lt(k1, k2, tk1[LOOK - 1], tk2[LOOK - 1]));
+      while (pm) {
+        const int L = __builtin_ctzll(pm);
+        pm &= pm - 1;
+        uint64_t c1 = readlane_u64(k1, L), c2 = readlane_u64(k2, L);
+        int32_t cq = q0 + L;
+        // insertion into the sorted top-LOOK (scalar)
+#pragma unroll
+        for (int r = 0; r < LOOK; r++) {
+          if (key_lt(c1, c2, tk1[r], tk2[r])) {
+            const uint64_t x1 = tk1[r], x2 = tk2[r];
+            const int32_t xq = tq[r];
+            tk1[r] = c1; tk2[r] = c2; tq[r] = cq;
+            c1 = x1; c2 = x2; cq = xq;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < LOOK; r++) nT += tq[r] >= 0 ? 1 : 0;
+    // lane r writes record r of the touched block
+    int32_t myq = -1;
+    uint64_t my1 = 0;
+#pragma unroll
+    for (int r = 0; r < LOOK; r++)
+      if (lane == r) { myq = tq[r]; my1 = tk1[r]; }
+    if (lane < nT) {
+      put_rec(R.res, R_T + lane * RREC, __longlong_as_double((long long)my1), S.ltb[myq], S.lid[myq],
+              S.lz[myq], myq, S.lown[myq], S.lhp[myq], S.la[0][myq], S.la[1][myq], S.la[2][myq],
+              S.la[3][myq]);
+    }
+  }
+  if (lane == 0) { R.res[R_NU] = nU; R.res[R_NT] = nT; }
+}
+
+// A scout fills ring slot i % RING with task i's list head, skipping entries that can no longer
 // be picked: best-fit drops every touched host (touched hosts compete through the live table),
-// first-fit drops dead ones. Touched-ness only grows, so an entry skipped here is unusable for
-// the walker too; one the loader keeps is checked again by the walker. The ring holds the first
-// 64 kept entries and the list position after the last of them (the walker's deep search, if
-// needed, continues from there).
+// first-fit drops dead ones. Touched-ness only grows, so an entry skipped here is unusable later
+// too. The ring holds the first 64 kept entries and the list position after the last of them.
+// Then it waits for the walk to reach task i - LOOK and scouts task i.
 template <int MODE>
 __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
   constexpr bool BEST = (MODE == CA_BF || MODE == VBP_BF);
@@ -211,15 +435,29 @@ __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
     if (lane < 16) R.rec[lane] = rv;
     if (lane == 16) R.rec[16] = k;
     if (lane == 17) R.rec[17] = next_pos;
+    // the state this task is scouted on: every task <= i - LOOK committed
+    for (int spin = 0;; spin++) {
+      const int c = vload(&S.committed);
+      if (c >= 0 && c >= i - LOOK + 1) break;
+      if (vload(&S.stop) || spin > SPIN_LIMIT) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    cbarrier();
+    scout<MODE>(A, S, R, i, k, rv);
     lds_drain();
     if (lane == 0) publish(&S.flag[slot], i);
   }
 }
 
 // ---------------------------------------------------------------- the walker
-// Everything the walk decides is wave-uniform; values are moved to scalar registers
-// (readlane / readfirstlane) as soon as they are known, so branches stay scalar and no vector
-// register carries a pending HBM load across the per-task loop.
+// Reads dword k of a scout result (lane k / 2 holds dwords k & ~1, k | 1 of `rv`).
+__device__ __forceinline__ int32_t rdw(uint64_t rv, int k) {
+  return readlane_i((int32_t)(uint32_t)((k & 1) ? (rv >> 32) : rv), k >> 1);
+}
+__device__ __forceinline__ double rdd(uint64_t rv, int k) {
+  return __longlong_as_double((long long)readlane_u64(rv, k >> 1));
+}
+
 template <int MODE>
 __device__ void walk(const CommitArgs& A, WalkLDS& S) {
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
@@ -260,8 +498,19 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
   }
   lds_drain();
   int nl = __builtin_amdgcn_readfirstlane(vload(&S.nl_init));   // live touched hosts
+  if (lane == 0) { vstore(&S.nl_pub, nl); vstore(&S.committed, 0); }
   int n_own = 0;
   int status = A.nt;
+  // Dirty hosts (committed by the last NDIRTY tasks), newest first: exact state in registers.
+  int32_t x_id[NDIRTY], x_q[NDIRTY], x_z[NDIRTY], x_hp[NDIRTY];
+  uint32_t x_tb[NDIRTY];
+  bool x_alive[NDIRTY];
+  double x_a[NDIRTY][4];
+#pragma unroll
+  for (int r = 0; r < NDIRTY; r++) {
+    x_id[r] = -1; x_q[r] = -1; x_z[r] = 0; x_hp[r] = 0; x_tb[r] = 0; x_alive[r] = false;
+    x_a[r][0] = x_a[r][1] = x_a[r][2] = x_a[r][3] = 0.0;
+  }
 
 #ifdef PVT_STAMPS
   uint64_t ph[5] = {0, 0, 0, 0, 0};
@@ -278,198 +527,188 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     cbarrier();                               // no slot read may move above the flag poll
     const RingSlot& R = S.ring[slot];
     const int32_t tv = R.rec[lane & 31];
-    const int32_t e_id = R.id[lane];
-    const double e_s = R.s[lane];
-    const uint32_t e_tb = R.tb[lane];
-    const int32_t e_z = R.zone[lane];
-    const double e0 = R.a[0][lane], e1 = R.a[1][lane], e2 = R.a[2][lane], e3 = R.a[3][lane];
+    const uint64_t rs = reinterpret_cast<const uint64_t*>(R.res)[lane];
     const double d0 = rec_d(tv, 0), d1 = rec_d(tv, 1), d2 = rec_d(tv, 2), d3 = rec_d(tv, 3);
-    const int cnt = __builtin_amdgcn_readlane(tv, 8);
     const bool comp = __builtin_amdgcn_readlane(tv, 9) != 0;
     const int anc = __builtin_amdgcn_readlane(tv, 10);
     const int caller = __builtin_amdgcn_readlane(tv, 11);
-    const int rcnt = __builtin_amdgcn_readlane(tv, 16);
-    const int npos = __builtin_amdgcn_readlane(tv, 17);
+    const int nU = rdw(rs, R_NU);
     STAMP(0);
 
-    // touched-ness of the ring entries (lane j: entry j)
-    const bool valid = lane < rcnt;
-    int32_t hp = 0;
-    const int32_t hv = valid ? wfind(S, e_id, hp) : H_MISS;
-    bool usable;
+    // the winner: candidate record (block base, or -1) or a dirty host (index, or -1)
+    int wrec = -1, wx = -1;
+    bool none = false, refill = false;
     if (BEST) {
-      usable = valid && hv == H_MISS;
-    } else {
-      const int q = hv >= 0 ? hv : 0;
-      usable = valid && (hv == H_MISS ||
-                         (hv >= 0 && fits<STRICT>(S.la[0][q], S.la[1][q], S.la[2][q], S.la[3][q],
-                                                  d0, d1, d2, d3)));
-    }
-    const uint64_t um = __ballot(usable);
-    STAMP(1);
-
-    // the first usable entry: (us, utb, uid), zone, snapshot capacities, hash value/position
-    bool found = um != 0;
-    double us = DINF, ua0 = 0, ua1 = 0, ua2 = 0, ua3 = 0;
-    uint32_t utb = 0xffffffffu;
-    int32_t uid = 0x7fffffff, uz = 0, uhv = H_MISS, uhp = 0;
-    if (found) {
-      const int ul = __builtin_ctzll(um);
-      uid = readlane_i(e_id, ul); uhv = readlane_i(hv, ul); uhp = readlane_i(hp, ul);
-      us = readlane_d(e_s, ul); utb = readlane_u(e_tb, ul); uz = readlane_i(e_z, ul);
-      ua0 = readlane_d(e0, ul); ua1 = readlane_d(e1, ul);
-      ua2 = readlane_d(e2, ul); ua3 = readlane_d(e3, ul);
-    } else {
-      // Deep list (rare): search the entries after the ring's by id in HBM, then read the
-      // first usable one. Loaded values are consumed (moved to scalars) right here.
-      const int32_t* ids = A.L.ids + (size_t)i * LMAX;
-      for (int c0 = npos; c0 < cnt && !found; c0 += WAVE) {
-        const bool v = c0 + lane < cnt;
-        const int32_t id = v ? ids[c0 + lane] : 0;
-        int32_t p2 = 0;
-        const int32_t h2 = v ? wfind(S, id, p2) : H_MISS;
-        bool ok;
-        if (BEST) {
-          ok = v && h2 == H_MISS;
-        } else {
-          const int q = h2 >= 0 ? h2 : 0;
-          ok = v && (h2 == H_MISS ||
-                     (h2 >= 0 && fits<STRICT>(S.la[0][q], S.la[1][q], S.la[2][q], S.la[3][q],
-                                              d0, d1, d2, d3)));
+      const int nT = rdw(rs, R_NT);
+      int ui = -1, ti = -1;
+#pragma unroll
+      for (int r = 0; r < LOOK; r++) {
+        if (ui < 0 && r < nU) {
+          const int32_t id = rdw(rs, R_U + r * RREC + RF_ID);
+          bool dirty = false;
+#pragma unroll
+          for (int x = 0; x < NDIRTY; x++) dirty |= (id == x_id[x]);
+          if (!dirty) ui = r;
         }
-        const uint64_t mc = __ballot(ok);
-        if (mc) {
-          const int ul = __builtin_ctzll(mc);
-          found = true;
-          uhv = readlane_i(h2, ul);
-          uhp = readlane_i(p2, ul);
-          const ListEntry* ue = A.L.e + (size_t)i * LMAX + c0 + ul;
-          const double f = (lane < 4) ? ue->a[lane] : (lane == 4) ? ue->s : 0.0;
-          const int32_t g = (lane == 0) ? ue->id : (lane == 1) ? ue->zone : (int32_t)ue->tb;
-          ua0 = readlane_d(f, 0); ua1 = readlane_d(f, 1); ua2 = readlane_d(f, 2);
-          ua3 = readlane_d(f, 3); us = readlane_d(f, 4);
-          uid = readlane_i(g, 0); uz = readlane_i(g, 1); utb = readlane_u((uint32_t)g, 2);
+        if (ti < 0 && r < nT) {
+          const int32_t id = rdw(rs, R_T + r * RREC + RF_ID);
+          bool dirty = false;
+#pragma unroll
+          for (int x = 0; x < NDIRTY; x++) dirty |= (id == x_id[x]);
+          if (!dirty) ti = r;
         }
       }
-    }
-    STAMP(2);
-
-    // the winner: hash value (live index / H_MISS), hash position, capacities, zone, tiebreak,
-    // and whether this walk committed to it before
-    int32_t w_id, w_hv, w_hp, w_z, w_own = 0;
-    uint32_t w_tb;
-    double w0, w1, w2, w3;
-    if (BEST) {
-      // Best so far as a 128-bit key (score bits, tiebreak:id): scores are >= +0, so their bit
-      // patterns order like the values, and one unsigned compare pair replaces lexless.
+      const bool found = ui >= 0;
       const bool exhausted = !found && !comp;
-      uint64_t t1 = (uint64_t)__double_as_longlong(us);
-      uint64_t t2 = ((uint64_t)utb << 32) | (uint32_t)uid;
-      if (exhausted) {
+      uint64_t t1 = ~0ull, t2 = ~0ull;
+      if (found) {
+        const int b = R_U + ui * RREC;
+        t1 = (uint64_t)__double_as_longlong(rdd(rs, b + RF_S));
+        t2 = ((uint64_t)(MODE == VBP_BF ? (uint32_t)rdw(rs, b + RF_TB) : 0u) << 32) |
+             (uint32_t)rdw(rs, b + RF_ID);
+        wrec = b;
+      } else if (exhausted) {
         // every untouched host outside the list ranks at or after the bound; bid + 1 turns
-        // the strict comparison below into "at or before the bound" (ids are unique)
+        // the strict comparisons below into "at or before the bound" (ids are unique)
         t1 = (uint64_t)__double_as_longlong(rec_d(tv, 6));
         t2 = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane(tv, 14)) << 32) +
              (uint32_t)__builtin_amdgcn_readlane(tv, 15) + 1;
       }
-      int bq = -1;
-      double b0 = 0, b1 = 0, b2 = 0, b3 = 0;
-      int32_t bz = 0, bhp = 0, bown = 0;
-      uint32_t btb = 0;
-#ifdef PVT_STAMPS
-      nl_sum += nl;
-#endif
-      for (int q0 = 0; q0 < nl; q0 += WAVE) {
-        const int q = q0 + lane;
-        const int qq = min(q, nl - 1);
-        const double a0 = S.la[0][qq], a1 = S.la[1][qq], a2 = S.la[2][qq], a3 = S.la[3][qq];
-        const int32_t lidq = S.lid[qq], lzq = S.lz[qq], lhq = S.lhp[qq], loq = S.lown[qq];
-        const uint32_t ltq = (MODE == VBP_BF) ? S.ltb[qq] : 0u;
-        const bool fit = (q < nl) && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
-        if (__ballot(fit) == 0) continue;
-        const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
-        double sc;
-        if (MODE == CA_BF) {
-          sc = (S.csum[anc * A.Z + lzq] * __builtin_sqrt(s2)) / S.bsum[anc * A.Z + lzq];
-        } else {
-          sc = __builtin_sqrt(s2);
-        }
-        const uint64_t k1 = (uint64_t)__double_as_longlong(sc);
-        const uint64_t k2 = ((uint64_t)ltq << 32) | (uint32_t)lidq;
-        uint64_t pm = __ballot(fit && (k1 < t1 || (k1 == t1 && k2 < t2)));
-        while (pm) {
-          const int L = __builtin_ctzll(pm);
-          pm &= pm - 1;
-          const uint64_t c1 = readlane_u64(k1, L), c2 = readlane_u64(k2, L);
-          if ((c1 < t1) | ((c1 == t1) & (c2 < t2))) {
-            t1 = c1; t2 = c2; bq = q0 + L;
-            b0 = readlane_d(a0, L); b1 = readlane_d(a1, L); b2 = readlane_d(a2, L); b3 = readlane_d(a3, L);
-            bz = readlane_i(lzq, L); bhp = readlane_i(lhq, L); bown = readlane_i(loq, L);
-            btb = readlane_u(ltq, L);
+      if (ti >= 0) {
+        const int b = R_T + ti * RREC;
+        const uint64_t c1 = (uint64_t)__double_as_longlong(rdd(rs, b + RF_S));
+        const uint64_t c2 = ((uint64_t)(MODE == VBP_BF ? (uint32_t)rdw(rs, b + RF_TB) : 0u) << 32) |
+                            (uint32_t)rdw(rs, b + RF_ID);
+        if (key_lt(c1, c2, t1, t2)) { t1 = c1; t2 = c2; wrec = b; }
+      }
+      STAMP(1);
+      // dirty hosts, rescored exactly on their current capacities (lane x: dirty host x)
+      {
+        double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+        int32_t z = 0, id = -1;
+        uint32_t tb = 0;
+        bool al = false;
+#pragma unroll
+        for (int x = 0; x < NDIRTY; x++)
+          if (lane == x) { a0 = x_a[x][0]; a1 = x_a[x][1]; a2 = x_a[x][2]; a3 = x_a[x][3]; z = x_z[x]; tb = x_tb[x]; id = x_id[x]; al = x_alive[x]; }
+        const bool fit = lane < NDIRTY && id >= 0 && al && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
+        if (__ballot(fit) != 0) {
+          uint64_t k1 = ~0ull, k2 = ~0ull;
+          if (fit) bf_key<MODE>(S, A.Z, anc, a0, a1, a2, a3, d0, d1, d2, d3, z, tb, id, k1, k2);
+          uint64_t pm = __ballot(fit);
+          while (pm) {
+            const int L = __builtin_ctzll(pm);
+            pm &= pm - 1;
+            const uint64_t c1 = readlane_u64(k1, L), c2 = readlane_u64(k2, L);
+            if (key_lt(c1, c2, t1, t2)) { t1 = c1; t2 = c2; wx = L; wrec = -1; }
           }
         }
       }
-      STAMP(3);
-      if (exhausted && bq < 0) { status = i; break; }              // refill from here
-      if (!found && bq < 0) { release_slot(S, i + 1); continue; }  // no host fits: waits
-      if (bq >= 0) {
-        w_id = (int32_t)(uint32_t)t2; w_hv = bq; w_hp = bhp; w_z = bz; w_tb = btb; w_own = bown;
-        w0 = b0; w1 = b1; w2 = b2; w3 = b3;
-      } else {
-        w_id = uid; w_hv = H_MISS; w_hp = uhp; w_z = uz; w_tb = utb;
-        w0 = ua0; w1 = ua1; w2 = ua2; w3 = ua3;
+      STAMP(2);
+      if (wrec < 0 && wx < 0) {
+        if (exhausted) refill = true;           // refill from here
+        else none = true;                       // no host fits: the task waits
       }
     } else {
-      if (!found) {
-        if (!comp) { status = i; break; }
-        release_slot(S, i + 1);
-        continue;
+      // first fit: the first usable entry in list order; a dirty one is re-checked exactly
+#pragma unroll
+      for (int r = 0; r < LOOK; r++) {
+        if (wrec >= 0 || wx >= 0 || r >= nU) continue;
+        const int32_t id = rdw(rs, R_U + r * RREC + RF_ID);
+        int xi = -1;
+#pragma unroll
+        for (int x = 0; x < NDIRTY; x++) xi = (xi < 0 && id == x_id[x]) ? x : xi;
+        if (xi < 0) {
+          wrec = R_U + r * RREC;
+        } else {
+          bool ok = false;
+#pragma unroll
+          for (int x = 0; x < NDIRTY; x++)
+            if (x == xi) ok = x_alive[x] && fits<STRICT>(x_a[x][0], x_a[x][1], x_a[x][2], x_a[x][3], d0, d1, d2, d3);
+          if (ok) wx = xi;
+        }
       }
-      w_id = uid; w_hv = uhv; w_hp = uhp; w_z = uz; w_tb = utb;
-      if (uhv >= 0) {                         // a live touched host that still fits
-        const double f = (lane < 4) ? S.la[lane][uhv] : 0.0;
-        w0 = readlane_d(f, 0); w1 = readlane_d(f, 1); w2 = readlane_d(f, 2); w3 = readlane_d(f, 3);
-        w_own = __builtin_amdgcn_readfirstlane(S.lown[uhv]);
-      } else {
-        w0 = ua0; w1 = ua1; w2 = ua2; w3 = ua3;
+      STAMP(1);
+      STAMP(2);
+      if (wrec < 0 && wx < 0) {
+        if (!comp) refill = true;
+        else none = true;
       }
     }
+    if (refill) { status = i; break; }
     release_slot(S, i + 1);                   // the ring slot is no longer read
+    if (none) {
+      // nothing committed: the dirty window still slides by one task
+#pragma unroll
+      for (int x = NDIRTY - 1; x > 0; x--) {
+        x_id[x] = x_id[x - 1]; x_q[x] = x_q[x - 1]; x_z[x] = x_z[x - 1]; x_hp[x] = x_hp[x - 1];
+        x_tb[x] = x_tb[x - 1]; x_alive[x] = x_alive[x - 1];
+        x_a[x][0] = x_a[x - 1][0]; x_a[x][1] = x_a[x - 1][1]; x_a[x][2] = x_a[x - 1][2]; x_a[x][3] = x_a[x - 1][3];
+      }
+      x_id[0] = -1; x_alive[0] = false;
+      cbarrier();
+      if (lane == 0) vstore(&S.committed, i + 1);
+      STAMP(3);
+      STAMP(4);
+      continue;
+    }
+
+    // the winner's state
+    int32_t w_id, w_q, w_z, w_hp, w_own;
+    uint32_t w_tb;
+    double w0, w1, w2, w3;
+    if (wx >= 0) {
+      w_id = 0; w_q = -1; w_z = 0; w_hp = 0; w_tb = 0; w0 = w1 = w2 = w3 = 0.0;
+#pragma unroll
+      for (int x = 0; x < NDIRTY; x++)
+        if (x == wx) { w_id = x_id[x]; w_q = x_q[x]; w_z = x_z[x]; w_hp = x_hp[x]; w_tb = x_tb[x];
+                       w0 = x_a[x][0]; w1 = x_a[x][1]; w2 = x_a[x][2]; w3 = x_a[x][3]; }
+      w_own = 1;                              // committed to by this walk moments ago
+    } else {
+      w_id = rdw(rs, wrec + RF_ID); w_q = rdw(rs, wrec + RF_Q); w_z = rdw(rs, wrec + RF_Z);
+      w_hp = rdw(rs, wrec + RF_HP); w_own = rdw(rs, wrec + RF_OWN); w_tb = (uint32_t)rdw(rs, wrec + RF_TB);
+      w0 = rdd(rs, wrec + RF_A); w1 = rdd(rs, wrec + RF_A + 2); w2 = rdd(rs, wrec + RF_A + 4);
+      w3 = rdd(rs, wrec + RF_A + 6);
+      if (w_q < 0) {
+        // untouched: the scout's probe ended at w_hp (empty then); only a dirty host inserted
+        // since can have taken that slot -- then probe again
+        bool taken = false;
+#pragma unroll
+        for (int x = 0; x < NDIRTY; x++) taken |= (x_id[x] >= 0 && x_hp[x] == w_hp);
+        if (taken) { int32_t p; (void)wfind(S, w_id, p); w_hp = p; }
+      }
+    }
+    STAMP(3);
 
     // commit: resc[h] -= t_demand (cost_aware.py:95,126; vbp.py:24,49)
     const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
     const bool alive = fits<STRICT>(n0, n1, n2, n3, m0, m1, m2, m3);
-    if (w_hv == H_MISS && alive && nl >= LIVE_MAX) { status = i; break; }   // table full: refill
+    if (w_q < 0 && alive && nl >= LIVE_MAX) { status = i; break; }   // table full: refill
     const double nr = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
-    if (w_hv == H_MISS) {                     // first commit to this host in the window
+    int32_t q_after = w_q;
+    if (w_q < 0) {                            // first commit to this host in the window
       int32_t v = H_DEAD;
       if (alive) {
         v = nl++;
         if (lane < 4) S.la[lane][v] = nr;
         if (lane == 0) { S.lid[v] = w_id; S.lz[v] = w_z; S.ltb[v] = w_tb; S.lhp[v] = w_hp; S.lown[v] = 1; }
       }
+      cbarrier();                             // the entry before its hash value (scouts)
       if (lane == 0) {
         S.hk[w_hp].key = w_id;
+        cbarrier();
         S.hk[w_hp].val = v;
       }
+      cbarrier();
+      if (alive && lane == 0) vstore(&S.nl_pub, nl);   // after the entry's writes (in order)
+      q_after = alive ? v : -1;
     } else {                                  // a live touched host
-      const int q = w_hv;
       if (alive) {
-        if (lane < 4) S.la[lane][q] = nr;
-        if (lane == 0) S.lown[q] = 1;
-      } else {                                // swap-remove from the live table
-        const int last = --nl;
-        if (q != last) {
-          const double mv = S.la[lane & 3][last];
-          const int32_t mid = S.lid[last], mz = S.lz[last], mhp = S.lhp[last], mo = S.lown[last];
-          const uint32_t mtb = S.ltb[last];
-          if (lane < 4) S.la[lane][q] = mv;
-          if (lane == 0) {
-            S.lid[q] = mid; S.lz[q] = mz; S.ltb[q] = mtb; S.lhp[q] = mhp; S.lown[q] = mo;
-            S.hk[mhp].val = q;
-          }
-        }
-        if (lane == 0) S.hk[w_hp].val = H_DEAD;
+        if (lane < 4) S.la[lane][w_q] = nr;
+        if (lane == 0) S.lown[w_q] = 1;
+      } else {                                // dies: marked in place, never moved
+        if (lane == 0) { S.la[0][w_q] = -DINF; S.hk[w_hp].val = H_DEAD; }
+        q_after = -1;
       }
     }
     if (!w_own) {                             // first commit of this walk to the host
@@ -478,6 +717,25 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     }
     if (lane < 4) A.avail[(size_t)lane * A.H + w_id] = nr;
     if (lane == 0) A.placement[caller] = w_id;
+    // slide the dirty window: this host is the newest
+#pragma unroll
+    for (int x = NDIRTY - 1; x > 0; x--) {
+      x_id[x] = x_id[x - 1]; x_q[x] = x_q[x - 1]; x_z[x] = x_z[x - 1]; x_hp[x] = x_hp[x - 1];
+      x_tb[x] = x_tb[x - 1]; x_alive[x] = x_alive[x - 1];
+      x_a[x][0] = x_a[x - 1][0]; x_a[x][1] = x_a[x - 1][1]; x_a[x][2] = x_a[x - 1][2]; x_a[x][3] = x_a[x - 1][3];
+    }
+    x_id[0] = w_id; x_q[0] = q_after; x_z[0] = w_z; x_hp[0] = w_hp; x_tb[0] = w_tb; x_alive[0] = alive;
+    x_a[0][0] = n0; x_a[0][1] = n1; x_a[0][2] = n2; x_a[0][3] = n3;
+    // an older entry of the same host keeps excluding the scouts' view of it, but its state is
+    // stale: only the newest entry is rescored
+#pragma unroll
+    for (int x = 1; x < NDIRTY; x++)
+      if (x_id[x] == w_id) x_alive[x] = false;
+    cbarrier();
+    if (lane == 0) vstore(&S.committed, i + 1);   // after every LDS write of this commit
+#ifdef PVT_STAMPS
+    nl_sum += nl;
+#endif
     STAMP(4);
   }
   if (lane == 0) {
@@ -507,7 +765,7 @@ __global__ __launch_bounds__(WALK_THREADS) void commit_kernel(CommitArgs A) {
   if (MODE == CA_BF)
     for (int i = tid; i < A.Z * A.Z; i += WALK_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
   if (tid < RING) S.flag[tid] = -1;
-  if (tid == 0) { S.done = 0; S.stop = 0; S.nl_init = 0; }
+  if (tid == 0) { S.done = 0; S.stop = 0; S.nl_init = 0; S.nl_pub = 0; S.committed = -1; }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (wave == 0) walk<MODE>(A, S);

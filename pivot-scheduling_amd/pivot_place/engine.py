@@ -27,7 +27,7 @@ def load_library(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("PIVOT_PLACE_LIB") or LIB_PATH   # env: diagnostic builds
     if not os.path.exists(p):
         raise OSError("pivot_place: %s not found; build it with `make -C pivot-scheduling_amd` "
                       "(there is no CPU fallback)" % p)
