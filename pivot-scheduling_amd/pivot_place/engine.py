@@ -136,7 +136,7 @@ class DeviceBatch:
         n = len(self.arrays)
         self.structs = (_abi.pvt_round * max(n, 1))()
         self.bufs, offs = {}, {}
-        self.mt, self.mt0 = [], []
+        self.mt, self._mt, self._mt0 = [], None, None
         if n == 0:
             return
         for name, dt in self._FIELDS:
@@ -155,8 +155,12 @@ class DeviceBatch:
         self.placement = torch.empty(max(int(toff[-1]), 1), dtype=torch.int32, device=dev)
         self._toff = toff
         self._hoff = offs["avail"]
-        self.mt0 = [None if r.mt_state is None else r.mt_state.copy() for r in self.arrays]
-        self.mt = [None if m is None else m.copy() for m in self.mt0]
+        # MT19937 states (opportunistic) packed in one host array: reset is one copy
+        has_mt = [r.mt_state is not None for r in self.arrays]
+        self._mt0 = np.stack([r.mt_state if r.mt_state is not None else np.zeros(625, np.uint32)
+                              for r in self.arrays]).astype(np.uint32) if any(has_mt) else None
+        self._mt = None if self._mt0 is None else self._mt0.copy()
+        self.mt = [self._mt[i] if has_mt[i] else None for i in range(n)]
         for i, r in enumerate(self.arrays):
             st = _abi.fill_struct(r)
             for name, dt in self._FIELDS:
@@ -175,9 +179,8 @@ class DeviceBatch:
         if not self.arrays:
             return
         self.bufs["avail"].copy_(self.avail0)
-        for m, m0 in zip(self.mt, self.mt0):
-            if m is not None:
-                m[:] = m0
+        if self._mt is not None:
+            self._mt[:] = self._mt0
 
     def placement_of(self, i):
         return self.placement[int(self._toff[i]):int(self._toff[i + 1])]
