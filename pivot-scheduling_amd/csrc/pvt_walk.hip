@@ -52,7 +52,6 @@ constexpr int RING = 12;                  // ring slots (task lists in LDS)
 #define PVT_PRODUCERS 7
 #endif
 constexpr int LOOK = PVT_LOOK;            // a task is scouted on the state after task i - LOOK
-constexpr int NDIRTY = LOOK - 1;          // hosts committed since: re-evaluated by the walker
 constexpr int PRODUCERS = PVT_PRODUCERS;  // loader / scout waves
 constexpr int PRE_CHUNKS = 4;             // list chunks a loader fetches before filtering
 constexpr int WALK_THREADS = (1 + PRODUCERS) * WAVE;
@@ -458,6 +457,20 @@ __device__ __forceinline__ double rdd(uint64_t rv, int k) {
   return __longlong_as_double((long long)readlane_u64(rv, k >> 1));
 }
 
+// The walker's decisions are uniform: every value it branches on is a scalar (readlane of the
+// scout's result, scalar state of the patched hosts), so the compiler emits scalar branches and
+// the per-task chain is short. NP = LOOK - 1 patched hosts: the winners of the last NP tasks,
+// newest first (x[0]); an older entry of a host that won again is stale (not rescored).
+constexpr int NP = LOOK - 1;
+static_assert(NP >= 1 && NP <= 2, "walker patches one or two hosts");
+
+struct Patched {
+  int32_t id, q, z, hp, anc;                // anc: anchor its c / b were read for (-1: none)
+  uint32_t tb;
+  bool alive;
+  double a0, a1, a2, a3, c, b;
+};
+
 template <int MODE>
 __device__ void walk(const CommitArgs& A, WalkLDS& S) {
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
@@ -501,15 +514,11 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
   if (lane == 0) { vstore(&S.nl_pub, nl); vstore(&S.committed, 0); }
   int n_own = 0;
   int status = A.nt;
-  // Dirty hosts (committed by the last NDIRTY tasks), newest first: exact state in registers.
-  int32_t x_id[NDIRTY], x_q[NDIRTY], x_z[NDIRTY], x_hp[NDIRTY];
-  uint32_t x_tb[NDIRTY];
-  bool x_alive[NDIRTY];
-  double x_a[NDIRTY][4];
+  Patched X[NP];
 #pragma unroll
-  for (int r = 0; r < NDIRTY; r++) {
-    x_id[r] = -1; x_q[r] = -1; x_z[r] = 0; x_hp[r] = 0; x_tb[r] = 0; x_alive[r] = false;
-    x_a[r][0] = x_a[r][1] = x_a[r][2] = x_a[r][3] = 0.0;
+  for (int r = 0; r < NP; r++) {
+    X[r].id = -1; X[r].q = -1; X[r].z = 0; X[r].hp = 0; X[r].anc = -1; X[r].tb = 0;
+    X[r].alive = false; X[r].a0 = X[r].a1 = X[r].a2 = X[r].a3 = 0.0; X[r].c = 0.0; X[r].b = 1.0;
   }
 
 #ifdef PVT_STAMPS
@@ -535,38 +544,42 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     const int nU = rdw(rs, R_NU);
     STAMP(0);
 
-    // the winner: candidate record (block base, or -1) or a dirty host (index, or -1)
-    int wrec = -1, wx = -1;
+    auto patched = [&](int32_t id) {
+      bool p = false;
+#pragma unroll
+      for (int r = 0; r < NP; r++) p |= (id == X[r].id);
+      return p;
+    };
+    // the first candidate of each scout list that is not a patched host
+    int ub = -1;
+#pragma unroll
+    for (int r = 0; r < LOOK; r++)
+      if (ub < 0 && r < nU && !patched(rdw(rs, R_U + r * RREC + RF_ID))) ub = R_U + r * RREC;
+    // the patched hosts that can still take this task (the newest entry of a host only)
+    bool xf[NP];
+#pragma unroll
+    for (int r = 0; r < NP; r++) {
+      bool stale = false;
+#pragma unroll
+      for (int o = 0; o < r; o++) stale |= (X[o].id == X[r].id);
+      xf[r] = X[r].id >= 0 && X[r].alive && !stale &&
+              fits<STRICT>(X[r].a0, X[r].a1, X[r].a2, X[r].a3, d0, d1, d2, d3);
+    }
+    int wrec = -1, wx = -1;                   // winner: a scout record, or patched host wx
     bool none = false, refill = false;
     if (BEST) {
       const int nT = rdw(rs, R_NT);
-      int ui = -1, ti = -1;
+      int tb_ = -1;
 #pragma unroll
-      for (int r = 0; r < LOOK; r++) {
-        if (ui < 0 && r < nU) {
-          const int32_t id = rdw(rs, R_U + r * RREC + RF_ID);
-          bool dirty = false;
-#pragma unroll
-          for (int x = 0; x < NDIRTY; x++) dirty |= (id == x_id[x]);
-          if (!dirty) ui = r;
-        }
-        if (ti < 0 && r < nT) {
-          const int32_t id = rdw(rs, R_T + r * RREC + RF_ID);
-          bool dirty = false;
-#pragma unroll
-          for (int x = 0; x < NDIRTY; x++) dirty |= (id == x_id[x]);
-          if (!dirty) ti = r;
-        }
-      }
-      const bool found = ui >= 0;
-      const bool exhausted = !found && !comp;
+      for (int r = 0; r < LOOK; r++)
+        if (tb_ < 0 && r < nT && !patched(rdw(rs, R_T + r * RREC + RF_ID))) tb_ = R_T + r * RREC;
+      const bool exhausted = ub < 0 && !comp;
       uint64_t t1 = ~0ull, t2 = ~0ull;
-      if (found) {
-        const int b = R_U + ui * RREC;
-        t1 = (uint64_t)__double_as_longlong(rdd(rs, b + RF_S));
-        t2 = ((uint64_t)(MODE == VBP_BF ? (uint32_t)rdw(rs, b + RF_TB) : 0u) << 32) |
-             (uint32_t)rdw(rs, b + RF_ID);
-        wrec = b;
+      if (ub >= 0) {
+        t1 = (uint64_t)__double_as_longlong(rdd(rs, ub + RF_S));
+        t2 = ((uint64_t)(MODE == VBP_BF ? (uint32_t)rdw(rs, ub + RF_TB) : 0u) << 32) |
+             (uint32_t)rdw(rs, ub + RF_ID);
+        wrec = ub;
       } else if (exhausted) {
         // every untouched host outside the list ranks at or after the bound; bid + 1 turns
         // the strict comparisons below into "at or before the bound" (ids are unique)
@@ -574,58 +587,58 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
         t2 = (((uint64_t)(uint32_t)__builtin_amdgcn_readlane(tv, 14)) << 32) +
              (uint32_t)__builtin_amdgcn_readlane(tv, 15) + 1;
       }
-      if (ti >= 0) {
-        const int b = R_T + ti * RREC;
-        const uint64_t c1 = (uint64_t)__double_as_longlong(rdd(rs, b + RF_S));
-        const uint64_t c2 = ((uint64_t)(MODE == VBP_BF ? (uint32_t)rdw(rs, b + RF_TB) : 0u) << 32) |
-                            (uint32_t)rdw(rs, b + RF_ID);
-        if (key_lt(c1, c2, t1, t2)) { t1 = c1; t2 = c2; wrec = b; }
+      if (tb_ >= 0) {
+        const uint64_t c1 = (uint64_t)__double_as_longlong(rdd(rs, tb_ + RF_S));
+        const uint64_t c2 = ((uint64_t)(MODE == VBP_BF ? (uint32_t)rdw(rs, tb_ + RF_TB) : 0u) << 32) |
+                            (uint32_t)rdw(rs, tb_ + RF_ID);
+        if (key_lt(c1, c2, t1, t2)) { t1 = c1; t2 = c2; wrec = tb_; }
       }
       STAMP(1);
-      // dirty hosts, rescored exactly on their current capacities (lane x: dirty host x)
-      {
-        double a0 = 0, a1 = 0, a2 = 0, a3 = 0;
-        int32_t z = 0, id = -1;
-        uint32_t tb = 0;
-        bool al = false;
+      // the patched hosts, rescored exactly (independent chains: the compiler interleaves them)
+      uint64_t k1[NP], k2[NP];
 #pragma unroll
-        for (int x = 0; x < NDIRTY; x++)
-          if (lane == x) { a0 = x_a[x][0]; a1 = x_a[x][1]; a2 = x_a[x][2]; a3 = x_a[x][3]; z = x_z[x]; tb = x_tb[x]; id = x_id[x]; al = x_alive[x]; }
-        const bool fit = lane < NDIRTY && id >= 0 && al && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
-        if (__ballot(fit) != 0) {
-          uint64_t k1 = ~0ull, k2 = ~0ull;
-          if (fit) bf_key<MODE>(S, A.Z, anc, a0, a1, a2, a3, d0, d1, d2, d3, z, tb, id, k1, k2);
-          uint64_t pm = __ballot(fit);
-          while (pm) {
-            const int L = __builtin_ctzll(pm);
-            pm &= pm - 1;
-            const uint64_t c1 = readlane_u64(k1, L), c2 = readlane_u64(k2, L);
-            if (key_lt(c1, c2, t1, t2)) { t1 = c1; t2 = c2; wx = L; wrec = -1; }
+      for (int r = 0; r < NP; r++) {
+        k1[r] = ~0ull; k2[r] = ~0ull;
+        if (xf[r]) {
+          const double s2 = norm2_seq(X[r].a0 - d0, X[r].a1 - d1, X[r].a2 - d2, X[r].a3 - d3);
+          double sc;
+          if (MODE == CA_BF) {
+            if (anc != X[r].anc) {            // its zone-table entries for this anchor
+              X[r].anc = anc;
+              X[r].c = S.csum[anc * A.Z + X[r].z];
+              X[r].b = S.bsum[anc * A.Z + X[r].z];
+            }
+            sc = (X[r].c * __builtin_sqrt(s2)) / X[r].b;
+          } else {
+            sc = __builtin_sqrt(s2);
           }
+          k1[r] = (uint64_t)__double_as_longlong(sc);
+          k2[r] = ((uint64_t)(MODE == VBP_BF ? X[r].tb : 0u) << 32) | (uint32_t)X[r].id;
         }
       }
+#pragma unroll
+      for (int r = 0; r < NP; r++)
+        if (xf[r] && key_lt(k1[r], k2[r], t1, t2)) { t1 = k1[r]; t2 = k2[r]; wx = r; wrec = -1; }
       STAMP(2);
       if (wrec < 0 && wx < 0) {
-        if (exhausted) refill = true;           // refill from here
-        else none = true;                       // no host fits: the task waits
+        if (exhausted) refill = true;         // refill from here
+        else none = true;                     // no host fits: the task waits
       }
     } else {
-      // first fit: the first usable entry in list order; a dirty one is re-checked exactly
+      // first fit: the first usable entry in list order; a patched one is re-checked exactly
 #pragma unroll
       for (int r = 0; r < LOOK; r++) {
         if (wrec >= 0 || wx >= 0 || r >= nU) continue;
         const int32_t id = rdw(rs, R_U + r * RREC + RF_ID);
-        int xi = -1;
+        int pr = -1;
 #pragma unroll
-        for (int x = 0; x < NDIRTY; x++) xi = (xi < 0 && id == x_id[x]) ? x : xi;
-        if (xi < 0) {
+        for (int o = NP - 1; o >= 0; o--) pr = (id == X[o].id) ? o : pr;   // newest entry
+        if (pr < 0) {
           wrec = R_U + r * RREC;
         } else {
-          bool ok = false;
 #pragma unroll
-          for (int x = 0; x < NDIRTY; x++)
-            if (x == xi) ok = x_alive[x] && fits<STRICT>(x_a[x][0], x_a[x][1], x_a[x][2], x_a[x][3], d0, d1, d2, d3);
-          if (ok) wx = xi;
+          for (int o = 0; o < NP; o++)
+            if (o == pr && xf[o]) wx = o;
         }
       }
       STAMP(1);
@@ -637,15 +650,10 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     }
     if (refill) { status = i; break; }
     release_slot(S, i + 1);                   // the ring slot is no longer read
-    if (none) {
-      // nothing committed: the dirty window still slides by one task
+    if (none) {                               // nothing committed: the window slides
 #pragma unroll
-      for (int x = NDIRTY - 1; x > 0; x--) {
-        x_id[x] = x_id[x - 1]; x_q[x] = x_q[x - 1]; x_z[x] = x_z[x - 1]; x_hp[x] = x_hp[x - 1];
-        x_tb[x] = x_tb[x - 1]; x_alive[x] = x_alive[x - 1];
-        x_a[x][0] = x_a[x - 1][0]; x_a[x][1] = x_a[x - 1][1]; x_a[x][2] = x_a[x - 1][2]; x_a[x][3] = x_a[x - 1][3];
-      }
-      x_id[0] = -1; x_alive[0] = false;
+      for (int r = NP - 1; r > 0; r--) X[r] = X[r - 1];
+      X[0].id = -1; X[0].alive = false; X[0].anc = -1;
       cbarrier();
       if (lane == 0) vstore(&S.committed, i + 1);
       STAMP(3);
@@ -654,83 +662,75 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     }
 
     // the winner's state
-    int32_t w_id, w_q, w_z, w_hp, w_own;
-    uint32_t w_tb;
-    double w0, w1, w2, w3;
+    Patched W;
+    int32_t w_own;
     if (wx >= 0) {
-      w_id = 0; w_q = -1; w_z = 0; w_hp = 0; w_tb = 0; w0 = w1 = w2 = w3 = 0.0;
 #pragma unroll
-      for (int x = 0; x < NDIRTY; x++)
-        if (x == wx) { w_id = x_id[x]; w_q = x_q[x]; w_z = x_z[x]; w_hp = x_hp[x]; w_tb = x_tb[x];
-                       w0 = x_a[x][0]; w1 = x_a[x][1]; w2 = x_a[x][2]; w3 = x_a[x][3]; }
+      for (int r = 0; r < NP; r++)
+        if (r == wx) W = X[r];
       w_own = 1;                              // committed to by this walk moments ago
     } else {
-      w_id = rdw(rs, wrec + RF_ID); w_q = rdw(rs, wrec + RF_Q); w_z = rdw(rs, wrec + RF_Z);
-      w_hp = rdw(rs, wrec + RF_HP); w_own = rdw(rs, wrec + RF_OWN); w_tb = (uint32_t)rdw(rs, wrec + RF_TB);
-      w0 = rdd(rs, wrec + RF_A); w1 = rdd(rs, wrec + RF_A + 2); w2 = rdd(rs, wrec + RF_A + 4);
-      w3 = rdd(rs, wrec + RF_A + 6);
-      if (w_q < 0) {
-        // untouched: the scout's probe ended at w_hp (empty then); only a dirty host inserted
-        // since can have taken that slot -- then probe again
-        bool taken = false;
+      W.id = rdw(rs, wrec + RF_ID); W.q = rdw(rs, wrec + RF_Q); W.z = rdw(rs, wrec + RF_Z);
+      W.hp = rdw(rs, wrec + RF_HP); w_own = rdw(rs, wrec + RF_OWN); W.tb = (uint32_t)rdw(rs, wrec + RF_TB);
+      W.a0 = rdd(rs, wrec + RF_A); W.a1 = rdd(rs, wrec + RF_A + 2); W.a2 = rdd(rs, wrec + RF_A + 4);
+      W.a3 = rdd(rs, wrec + RF_A + 6);
+      W.anc = -1; W.c = 0.0; W.b = 1.0;
+      // untouched: the scout's probe ended at W.hp (empty then); only a patched host inserted
+      // since can have taken that slot -- then probe again
+      bool taken = false;
 #pragma unroll
-        for (int x = 0; x < NDIRTY; x++) taken |= (x_id[x] >= 0 && x_hp[x] == w_hp);
-        if (taken) { int32_t p; (void)wfind(S, w_id, p); w_hp = p; }
+      for (int r = 0; r < NP; r++) taken |= (X[r].id >= 0 && X[r].hp == W.hp);
+      if (W.q < 0 && taken) {
+        int32_t p;
+        (void)wfind(S, W.id, p);
+        W.hp = __builtin_amdgcn_readfirstlane(p);
       }
     }
     STAMP(3);
 
     // commit: resc[h] -= t_demand (cost_aware.py:95,126; vbp.py:24,49)
-    const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
+    const double n0 = W.a0 - d0, n1 = W.a1 - d1, n2 = W.a2 - d2, n3 = W.a3 - d3;
     const bool alive = fits<STRICT>(n0, n1, n2, n3, m0, m1, m2, m3);
-    if (w_q < 0 && alive && nl >= LIVE_MAX) { status = i; break; }   // table full: refill
+    if (W.q < 0 && alive && nl >= LIVE_MAX) { status = i; break; }   // table full: refill
     const double nr = lane == 0 ? n0 : lane == 1 ? n1 : lane == 2 ? n2 : n3;
-    int32_t q_after = w_q;
-    if (w_q < 0) {                            // first commit to this host in the window
+    int32_t q_after = W.q;
+    if (W.q < 0) {                            // first commit to this host in the window
       int32_t v = H_DEAD;
       if (alive) {
         v = nl++;
         if (lane < 4) S.la[lane][v] = nr;
-        if (lane == 0) { S.lid[v] = w_id; S.lz[v] = w_z; S.ltb[v] = w_tb; S.lhp[v] = w_hp; S.lown[v] = 1; }
+        if (lane == 0) { S.lid[v] = W.id; S.lz[v] = W.z; S.ltb[v] = W.tb; S.lhp[v] = W.hp; S.lown[v] = 1; }
       }
       cbarrier();                             // the entry before its hash value (scouts)
       if (lane == 0) {
-        S.hk[w_hp].key = w_id;
+        S.hk[W.hp].key = W.id;
         cbarrier();
-        S.hk[w_hp].val = v;
+        S.hk[W.hp].val = v;
       }
       cbarrier();
       if (alive && lane == 0) vstore(&S.nl_pub, nl);   // after the entry's writes (in order)
       q_after = alive ? v : -1;
     } else {                                  // a live touched host
       if (alive) {
-        if (lane < 4) S.la[lane][w_q] = nr;
-        if (lane == 0) S.lown[w_q] = 1;
+        if (lane < 4) S.la[lane][W.q] = nr;
+        if (lane == 0) S.lown[W.q] = 1;
       } else {                                // dies: marked in place, never moved
-        if (lane == 0) { S.la[0][w_q] = -DINF; S.hk[w_hp].val = H_DEAD; }
+        if (lane == 0) { S.la[0][W.q] = -DINF; S.hk[W.hp].val = H_DEAD; }
         q_after = -1;
       }
     }
     if (!w_own) {                             // first commit of this walk to the host
-      if (lane == 0) A.own_ids[n_own] = w_id;
+      if (lane == 0) A.own_ids[n_own] = W.id;
       n_own++;
     }
-    if (lane < 4) A.avail[(size_t)lane * A.H + w_id] = nr;
-    if (lane == 0) A.placement[caller] = w_id;
-    // slide the dirty window: this host is the newest
+    if (lane < 4) A.avail[(size_t)lane * A.H + W.id] = nr;
+    if (lane == 0) A.placement[caller] = W.id;
+    // the winner becomes the newest patched host (its c / b carry over when it was one)
 #pragma unroll
-    for (int x = NDIRTY - 1; x > 0; x--) {
-      x_id[x] = x_id[x - 1]; x_q[x] = x_q[x - 1]; x_z[x] = x_z[x - 1]; x_hp[x] = x_hp[x - 1];
-      x_tb[x] = x_tb[x - 1]; x_alive[x] = x_alive[x - 1];
-      x_a[x][0] = x_a[x - 1][0]; x_a[x][1] = x_a[x - 1][1]; x_a[x][2] = x_a[x - 1][2]; x_a[x][3] = x_a[x - 1][3];
-    }
-    x_id[0] = w_id; x_q[0] = q_after; x_z[0] = w_z; x_hp[0] = w_hp; x_tb[0] = w_tb; x_alive[0] = alive;
-    x_a[0][0] = n0; x_a[0][1] = n1; x_a[0][2] = n2; x_a[0][3] = n3;
-    // an older entry of the same host keeps excluding the scouts' view of it, but its state is
-    // stale: only the newest entry is rescored
-#pragma unroll
-    for (int x = 1; x < NDIRTY; x++)
-      if (x_id[x] == w_id) x_alive[x] = false;
+    for (int r = NP - 1; r > 0; r--) X[r] = X[r - 1];
+    X[0] = W;
+    X[0].q = q_after; X[0].alive = alive;
+    X[0].a0 = n0; X[0].a1 = n1; X[0].a2 = n2; X[0].a3 = n3;
     cbarrier();
     if (lane == 0) vstore(&S.committed, i + 1);   // after every LDS write of this commit
 #ifdef PVT_STAMPS
