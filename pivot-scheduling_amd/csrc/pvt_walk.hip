@@ -442,9 +442,13 @@ __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
       __builtin_amdgcn_s_sleep(1);
     }
     cbarrier();
+    // the scout is on the walk's critical path (the walker needs its result one task from now):
+    // it outranks the other scouts' list loading, not the walker
+    __builtin_amdgcn_s_setprio(2);
     scout<MODE>(A, S, R, i, k, rv);
     lds_drain();
     if (lane == 0) publish(&S.flag[slot], i);
+    __builtin_amdgcn_s_setprio(0);
   }
 }
 
