@@ -117,6 +117,7 @@ struct OppLDS {
   int32_t slost[OPP_NSQ_MAX];   // per task: lost hosts per super-chunk
   uint64_t lmask[OPP_SUP][4];   // per task: lost hosts of the chosen super-chunk, as chunk bitmaps
   uint32_t mt[625];
+  int32_t pl[OPP_MAXW];         // placements of the window, written out when the walk ends
 };
 
 static_assert(sizeof(OppLDS) <= 160 * 1024, "opportunistic walk LDS exceeds a CU's 160 KiB");
@@ -171,6 +172,14 @@ __device__ __forceinline__ uint64_t ostamp() {
 #define OSTAMP(k) do {} while (0)
 #endif
 
+// One wave orders its own LDS operations: a compiler fence plus lgkmcnt(0). (__syncthreads
+// would also wait vmcnt(0), i.e. for the next task's prefetched HBM loads.)
+__device__ __forceinline__ void wave_lds_fence() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
   constexpr int U = OPP_CH / WAVE;
   constexpr int SUPH = OPP_SUP * OPP_CH;
@@ -178,6 +187,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
   OppLDS& S = *reinterpret_cast<OppLDS*>(smem);
   const int lane = lane_id();
   for (int i = lane; i < OPP_HASH; i += WAVE) S.hkey[i] = -1;
+  for (int i = lane; i < A.nt; i += WAVE) S.pl[i] = -1;
   for (int i = lane; i < 625; i += WAVE) S.mt[i] = A.mt[i];
   __builtin_amdgcn_s_waitcnt(0xc07f);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -206,10 +216,10 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     OSTAMP(0);
     // Touched hosts that fitted at the snapshot and no longer fit ("lost"), listed and counted
     // per super-chunk with LDS atomics (4 x 64 touched hosts per loop trip).
-    // (the barriers order the zeroing, the other lanes' atomics and the reads: without them the
+    // (the fences order the zeroing, the other lanes' atomics and the reads: without them the
     // compiler may forward a lane's own zero store to its later read)
     for (int Q = lane; Q < A.nsq; Q += WAVE) S.slost[Q] = 0;
-    __syncthreads();
+    wave_lds_fence();
     int nl = 0;
     for (int q0 = 0; q0 < m; q0 += 4 * WAVE) {
       bool lf[4];
@@ -233,7 +243,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
         nl += __popcll(b);
       }
     }
-    __syncthreads();
+    wave_lds_fence();
     OSTAMP(1);
     long long n = 0;
     if (fast) {
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     }
 #pragma unroll
     for (int u = 0; u < U; u++) S.lmask[lane][u] = 0;
-    __syncthreads();
+    wave_lds_fence();
     for (int j = lane; j < nl; j += WAVE) {
       const int h = S.lost[j];
       if (h / SUPH == Qs) {
@@ -290,7 +300,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
         atomicOr((unsigned long long*)&S.lmask[(h / OPP_CH) % OPP_SUP][o / WAVE], 1ull << (o % WAVE));
       }
     }
-    __syncthreads();
+    wave_lds_fence();
     int c = 0;
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -336,15 +346,23 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
         S.sa[0][ws] = w0; S.sa[1][ws] = w1; S.sa[2][ws] = w2; S.sa[3][ws] = w3;
       }
     }
+    // commit in LDS only: a global store here would put its round trip on the next task (the
+    // next task's prefetched loads share the in-order vmcnt counter with it)
     if (lane == 0) {
       S.ta[0][ws] = n0; S.ta[1][ws] = n1; S.ta[2][ws] = n2; S.ta[3][ws] = n3;
-      A.avail[w] = n0;
-      A.avail[(size_t)A.H + w] = n1;
-      A.avail[2 * (size_t)A.H + w] = n2;
-      A.avail[3 * (size_t)A.H + w] = n3;
-      A.placement[i] = w;
+      S.pl[i] = w;
     }
   }
+  // the window's commits: current availability of every touched host, and the placements
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  for (int q = lane; q < m; q += WAVE) {
+    const int32_t h = S.tid[q];
+    A.avail[h] = S.ta[0][q];
+    A.avail[(size_t)A.H + h] = S.ta[1][q];
+    A.avail[2 * (size_t)A.H + h] = S.ta[2][q];
+    A.avail[3 * (size_t)A.H + h] = S.ta[3][q];
+  }
+  for (int i = lane; i < A.nt; i += WAVE) A.placement[i] = S.pl[i];
   mt_unbuffer(S.mt, mw);
   for (int i = lane; i < 625; i += WAVE) A.mt[i] = S.mt[i];
 #ifdef PVT_STAMPS
