@@ -218,6 +218,11 @@ def main():
                 "avg_launch_ms": avg_ms,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "bytes_per_candidate": _abi.BYTES_PER_CANDIDATE[mode],
+                "note": ("achieved = candidates per launch x bytes per candidate (SURVEY.md "
+                         "section 8(d)) / average launch time; a host row read once serves the "
+                         "tasks of a wave from registers/L1/L2, so the scan is not HBM-bound "
+                         "(frac > 1); traffic = DRAM bytes per launch from rocprofv3 PMC "
+                         "(tools/pmc_traffic.py)"),
             },
             "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items()},
             "windows_per_step": stats["windows"], "refills_per_step": stats["refills"],
