@@ -1,0 +1,267 @@
+#!/usr/bin/env python3
+"""Record every ``schedule()`` round of the REFERENCE's end-to-end Alibaba simulation (test-only).
+
+This extends ``make_golden.py`` from frozen states to whole simulations: the reference's
+``ExperimentRun.run`` (alibaba/runner.py:27-51) is restated inline (in-process instead of a
+``multiprocessing.Process``) and driven by ``pivot_place.des``, this repository's restatement
+of SimPy 3.0.11's event semantics, registered as ``simpy`` (SimPy is absent and not
+installable offline). Everything else — cluster generation
+(resources/gen.py), the trace loader (alibaba/runner.py:54-136), the round loop
+(scheduler/__init__.py:87-147,185-194), host execution, data pulls, network routes, the meter
+and the three policies — is the reference's own code, imported from /root/reference.
+
+Config 1 of BASELINE.json: ``sim.py --num-hosts 100 overall --num-apps 100`` on
+jobs-5000-200-172800-259200.yaml, hosts (16, 131072, 100, 1), output scale factor 1000, with
+sim.py's three policy configurations (alibaba/sim.py:179-186). Seeds are pinned where the
+reference leaves them to the OS: cluster generator ``seed=0`` (resources/gen.py:29),
+scheduler ``seed=0`` (scheduler/__init__.py:31), PYTHONHASHSEED=0, seeded uuid4,
+``np.random.seed(0)`` before the first ``ResourceMetadata`` (the bw jitter, shared with
+``zones_seed0.json``).
+
+Each non-empty round is written in the fixture schema of make_golden.py (a frozen state plus
+one run), with ``rng_draws`` counted from the scheduler's RandomState just before the round,
+so a replay carries one RandomState through the rounds exactly as the simulation does. The
+end-to-end outputs (simulated makespan, average application runtime by the reference's own
+formula, meter totals) are recorded beside the rounds. Because every round's placement is a
+function of that round's inputs, an engine that reproduces every round reproduces the whole
+trajectory and with it these end-to-end numbers.
+
+Only the JSON fixtures travel (tests/golden/sim_*.json.gz); nothing here runs on the GPU box.
+"""
+import gzip
+import json
+import os
+import subprocess
+import sys
+import time
+import zlib
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "pivot-scheduling_amd"))
+sys.path.insert(0, HERE)
+
+SIM_POLICIES = [   # alibaba/sim.py:179-186
+    ("opportunistic", "opportunistic", {}),
+    ("vbp_ff", "vbp_ff", {"decreasing": True}),
+    ("cost_aware", "cost_aware", {"bin_pack_algo": "first-fit", "sort_tasks": True,
+                                  "sort_hosts": True}),
+]
+EXTRA_POLICIES = [  # the other two bin-packing variants, same simulation
+    ("cost_aware_bf", "cost_aware", {"bin_pack_algo": "best-fit", "sort_tasks": True}),
+    ("vbp_bf", "vbp_bf", {"decreasing": True}),
+]
+
+CONFIGS = [
+    # config 1: sim.py --num-hosts 100 overall --num-apps 100, every policy variant
+    ("c1", 100, 100, "jobs-5000-200-172800-259200.yaml", SIM_POLICIES + EXTRA_POLICIES),
+    # contention: the same 100 apps on 12 hosts (wait queue, unplaceable tasks, LIFO retries)
+    ("h12", 12, 100, "jobs-5000-200-172800-259200.yaml", SIM_POLICIES + EXTRA_POLICIES),
+    # config 2 shape: 1000 hosts, sim.py's three policies, another trace file
+    ("c2", 1000, 300, "jobs-5000-200-86400-172800.yaml", SIM_POLICIES),
+]
+
+
+def _advance_to(shadow, target):
+    """Advance ``shadow`` (RandomState) by 32-bit draws until it equals ``target``; count them."""
+    import numpy as np
+    for n in range(1 << 22):
+        st = shadow.get_state()
+        if st[2] == target[2] and np.array_equal(st[1], target[1]):
+            return n
+        shadow.randint(0, 1 << 32, dtype=np.uint32)
+    raise RuntimeError("RNG advanced by more than 4M draws in one round")
+
+
+def dropin_class(policy, engine):
+    """One of this repository's drop-in policy mixins on the reference's own
+    GlobalSchedulerBase, with ``engine`` behind ``place()``."""
+    import scheduler
+    from pivot_place import policies
+    mixin = {"cost_aware": policies.CostAwarePlacement,
+             "opportunistic": policies.OpportunisticPlacement,
+             "vbp_ff": policies.FirstFitPlacement,
+             "vbp_bf": policies.BestFitPlacement}[policy]
+    return type("DropIn_" + policy, (mixin, scheduler.GlobalSchedulerBase), {"engine": engine})
+
+
+def simulate(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0, cls=None):
+    """Run one reference simulation; record its rounds unless ``cls`` (a scheduler class to
+    run instead of the reference policy) is given."""
+    import numpy as np
+    from resources.meter import Meter
+    from pivot_place import des
+
+    mg._seed_uuid(zlib.crc32(label.encode()))     # host ids: per trace, order-independent
+    recording = cls is None
+    if recording:
+        cls = mg.POLICIES[policy](world)
+    rounds, stats = [], {"rounds": 0, "empty_rounds": 0}
+    shadow = np.random.RandomState(seed)
+    zone_of = world.zone_index
+
+    class Recording(cls):
+        _record = recording
+
+        def _first_fit(self, hosts_, task_group, anchor, resc):
+            self._groups.append({"anchor_zone": zone_of(anchor.locality),
+                                 "tasks": [self._tpos[id(t)] for t in task_group]})
+            return super()._first_fit(hosts_, task_group, anchor, resc)
+
+        def _best_fit(self, hosts_, task_group, anchor, resc):
+            self._groups.append({"anchor_zone": zone_of(anchor.locality),
+                                 "tasks": [self._tpos[id(t)] for t in task_group]})
+            return super()._best_fit(hosts_, task_group, anchor, resc)
+
+        def schedule(self, tasks):
+            stats["rounds"] += 1
+            tasks = list(tasks)
+            if not self._record:
+                if not tasks:
+                    stats["empty_rounds"] += 1
+                out = list(super().schedule(tasks))
+                stats["placed_dropin"] = stats.get("placed_dropin", 0) + sum(
+                    t.placement is not None for t in tasks)
+                return out
+            if not tasks:
+                stats["empty_rounds"] += 1
+                return super().schedule(tasks)
+            cluster = self.cluster
+            hosts = cluster.hosts
+            hidx = {h.id: i for i, h in enumerate(hosts)}
+            state = mg.record_state(world, cluster, tasks, [len(h.tasks) for h in hosts])
+            snap = self.resource_info
+            # the recorded availability must be the snapshot the policy sees
+            assert all(np.array_equal(snap[h.id], np.array(a)) for h, a in zip(hosts, state["avail"]))
+            before = {hid: a.copy() for hid, a in snap.items()}
+            self._tpos = {id(t): i for i, t in enumerate(tasks)}
+            self._groups = []
+            out = list(super().schedule(tasks))
+            changed = []
+            for hid, a in snap.items():
+                if not np.array_equal(a, before[hid]):
+                    changed.append([hidx[hid]] + [float(x) for x in a])
+            changed.sort()
+            run = {"policy": policy, "kwargs": kwargs, "seed": seed, "error": None,
+                   "placement": [-1 if t.placement is None else hidx[t.placement] for t in tasks],
+                   "order": [self._tpos[id(t)] for t in out],
+                   "changed_avail": changed,
+                   "rng_draws": _advance_to(shadow, self.randomizer.get_state())}
+            if policy == "cost_aware":
+                run["groups"] = self._groups
+            state["time"] = self.env.now
+            state["runs"] = [run]
+            rounds.append(state)
+            return out
+
+    # alibaba/sim.py:203-205 (cluster built once) and alibaba/runner.py:27-44 (one run)
+    env0 = des.Environment()
+    gen = world.RandomClusterGenerator(env0, 16, 16, 131072, 131072, 100, 100, 1, 1,
+                                       meter=Meter(env0), seed=0)
+    base = gen.generate(n_hosts)
+    env = des.Environment()
+    meter = Meter(env)
+    cluster = base.clone(env, meter)
+    sched = Recording(env, cluster, meter=meter, seed=seed, **kwargs)
+    load_gen = world.TraceGen(env, os.path.join(mg.REF, "alibaba", "jobs", job_file), sched,
+                              1000, n_apps)
+    cluster.start()
+    sched.start()
+    load_gen.start()
+    t0 = time.time()
+    env.run()
+    wall = time.time() - t0
+    apps = load_gen.apps
+    submitted = [a for a in apps if a.start_time or a.end_time]
+    e2e = {
+        "makespan": env.now,
+        "avg_runtime_reference": float(np.mean([a.end_time - a.start_time for a in apps])),
+        "avg_runtime_submitted": float(np.mean([a.end_time - a.start_time for a in submitted])),
+        "n_apps_finished": sum(1 for a in submitted if a.is_finished),
+        "cumulative_instance_hours": meter.cumulative_instance_hours,
+        "total_network_traffic_cost": meter.total_network_traffic_cost,
+        "tasks_placed": (sum(sum(p >= 0 for p in r["runs"][0]["placement"]) for r in rounds)
+                         if recording else stats.get("placed_dropin", 0)),
+        "rounds": stats["rounds"], "empty_rounds": stats["empty_rounds"],
+        "reference_wall_s": wall,
+    }
+    return compact({"name": label, "policy": policy, "kwargs": kwargs, "seed": seed,
+                    "n_hosts": n_hosts, "n_apps": n_apps, "job_file": job_file, "e2e": e2e,
+                    "rounds": rounds})
+
+
+def compact(tr):
+    """Hoist what never changes (zone, id rank, storage order) to the trace and store each
+    round's availability and running-task counts as changes against the previous round
+    (``avail_delta``: [host, cpus, mem, disk, gpus]; ``n_running_delta``: [host, count]).
+    tests/golden_io.py ``sim_rounds`` expands it back to the per-state schema."""
+    rounds = tr["rounds"]
+    if not rounds:
+        return tr
+    for key in ("zone", "id_rank", "storage_zone"):
+        tr[key] = rounds[0][key]
+        assert all(r[key] == tr[key] for r in rounds)
+    prev_a, prev_n = None, None
+    for r in rounds:
+        for key in ("zone", "id_rank", "storage_zone", "n_hosts"):
+            del r[key]
+        a, n = r.pop("avail"), r.pop("n_running")
+        if prev_a is None:
+            r["avail_delta"] = [[h] + row for h, row in enumerate(a)]
+            r["n_running_delta"] = [[h, k] for h, k in enumerate(n)]
+        else:
+            r["avail_delta"] = [[h] + row for h, row in enumerate(a) if row != prev_a[h]]
+            r["n_running_delta"] = [[h, k] for h, k in enumerate(n) if k != prev_n[h]]
+        prev_a, prev_n = a, n
+    return tr
+
+
+def main():
+    if os.environ.get("PYTHONHASHSEED") != "0":
+        env = dict(os.environ, PYTHONHASHSEED="0")
+        sys.exit(subprocess.call([sys.executable] + sys.argv, env=env))
+    from pivot_place import des
+    des.install(force=True)
+    import make_golden as mg
+    mg._install_compat()
+    import logging
+    logging.disable(logging.CRITICAL)
+    world = mg.World()
+    if sys.argv[1:2] == ["--dropin"]:
+        # e2e check of the drop-in policies inside the reference simulator (tests/
+        # test_sim_replay.py): the CPU restatement stands behind the engine contract here
+        sys.path.insert(0, ROOT)
+        from oracle import oracle
+
+        class OracleEngine:
+            def place(self, r):
+                return oracle.place(r)
+
+        name = sys.argv[2]
+        for cfg, n_hosts, n_apps, job_file, pols in CONFIGS:
+            for label, policy, kwargs in pols:
+                if "sim_%s_%s" % (cfg, label) == name:
+                    tr = simulate(mg, world, name, policy, kwargs, n_hosts, n_apps, job_file,
+                                  cls=dropin_class(policy, OracleEngine()))
+                    print(json.dumps(tr["e2e"]))
+                    return
+        raise SystemExit("unknown trace %s" % name)
+    which = sys.argv[1:]
+    for cfg, n_hosts, n_apps, job_file, pols in CONFIGS:
+        for label, policy, kwargs in pols:
+            name = "sim_%s_%s" % (cfg, label)
+            if which and name not in which:
+                continue
+            tr = simulate(mg, world, name, policy, kwargs, n_hosts, n_apps, job_file)
+            fn = os.path.join(HERE, tr["name"] + ".json.gz")
+            with gzip.open(fn, "wt") as f:
+                json.dump(tr, f, separators=(",", ":"))
+            e = tr["e2e"]
+            print("%-26s rounds=%d (empty %d) recorded=%d placed=%d makespan=%.3f wall=%.1fs %d KB"
+                  % (tr["name"], e["rounds"], e["empty_rounds"], len(tr["rounds"]),
+                     e["tasks_placed"], e["makespan"], e["reference_wall_s"],
+                     os.path.getsize(fn) // 1024), flush=True)
+
+
+if __name__ == "__main__":
+    main()

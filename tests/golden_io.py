@@ -111,3 +111,33 @@ def all_runs(skip_errors=True):
                 continue
             out.append((name, i))
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# Whole-simulation traces (tests/golden/sim_*.json.gz, made by make_golden_sim.py)
+# ---------------------------------------------------------------------------------------
+def sim_traces():
+    """Names of the recorded reference simulations, e.g. ``sim_c1_cost_aware``."""
+    return sorted(f[:-len(".json.gz")] for f in os.listdir(GOLDEN)
+                  if f.startswith("sim_") and f.endswith(".json.gz"))
+
+
+def sim_rounds(name):
+    """(trace, [case, ...]): every recorded non-empty round expanded to the per-state schema of
+    ``load()`` (one run per case), so ``fakes.build`` and ``expected`` apply unchanged."""
+    tr = load(name)
+    cases, avail, nrun = [], None, None
+    for r in tr["rounds"]:
+        if avail is None:
+            avail = [None] * tr["n_hosts"]
+            nrun = [0] * tr["n_hosts"]
+        for row in r["avail_delta"]:
+            avail[row[0]] = row[1:]
+        for h, k in r["n_running_delta"]:
+            nrun[h] = k
+        case = {"n_hosts": tr["n_hosts"], "avail": [list(a) for a in avail], "zone": tr["zone"],
+                "id_rank": tr["id_rank"], "n_running": list(nrun),
+                "storage_zone": tr["storage_zone"], "tasks": r["tasks"],
+                "containers": r["containers"], "runs": r["runs"], "time": r["time"]}
+        cases.append(case)
+    return tr, cases
