@@ -176,6 +176,38 @@ int  pvt_shard_commit(pvt_ctx* ctx, const void* packages);
 #define PVT_RESIDENT_MAX_TASKS 4096
 int  pvt_place_batch(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_rounds);
 int  pvt_set_resident(pvt_ctx* ctx, int32_t max_hosts);
+/*
+ * Anchor resolution for cost_aware groups (replaces the Counter/max of
+ * CostAwareGlobalScheduler._group_tasks, scheduler/cost_aware.py:45-58).
+ *
+ * Item c (a container of ready tasks) has the predecessor list list[off[c] .. off[c+1]): the
+ * placement of every task of every predecessor container, in the reference's iteration order
+ * (app.get_predecessors(c.id) order = the container's `dependencies` order, application/
+ * __init__.py:87-92,137-139; then p.tasks order). An entry is a host index (-1 = a predecessor
+ * task without placement), or, when inst_host is set, an index into inst_host (a per-instance
+ * host table kept resident in HBM, e.g. pivot_place.trace.DeviceTrace).
+ * Outputs per item: mode_host = the host with the highest count, the first seen among equal
+ * counts (Counter insertion order + max's first maximum); anchor_zone = zone[mode_host], or
+ *   -1  empty list (the task groups by its application, cost_aware.py:56-57),
+ *   -2  the mode entry is -1 (the reference raises AttributeError on get_host(None).locality),
+ *   -3  invalid offsets or an index out of range (the call then returns PVT_EINVAL).
+ * All pointers are device pointers. n_pred = off[C]; lists may hold up to 2^30 entries.
+ * Synchronises before returning.
+ */
+typedef struct pvt_anchor_args {
+  int32_t n_items;            /* C                                                        */
+  int32_t n_hosts;            /* H                                                        */
+  int64_t n_pred;             /* length of list (= off[C])                                */
+  int64_t n_inst;             /* length of inst_host (0 when inst_host is NULL)           */
+  const int64_t* off;         /* [C+1]                                                    */
+  const int32_t* list;        /* [n_pred]                                                 */
+  const int32_t* inst_host;   /* [n_inst] or NULL                                         */
+  const int32_t* zone;        /* [H]                                                      */
+  int32_t* mode_host;         /* [C] out                                                  */
+  int32_t* anchor_zone;       /* [C] out                                                  */
+} pvt_anchor_args;
+int  pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a);
+
 /* Human-readable text of the last error on this context (static storage of the ctx). */
 const char* pvt_last_error(pvt_ctx* ctx);
 

@@ -35,6 +35,9 @@ def lib():
         _lib.oracle_randint.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
         _lib.oracle_place_mt.restype = ctypes.c_int
         _lib.oracle_place_mt.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _lib.oracle_anchor.restype = ctypes.c_int
+        _lib.oracle_anchor.argtypes = [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 3 + [
+            ctypes.c_int64] + [ctypes.c_void_p] * 3
     return _lib
 
 
@@ -73,3 +76,18 @@ def randint(state, n):
     """numpy RandomState.randint(0, n) on a (625,) uint32 MT state, updated in place."""
     assert state.dtype == np.uint32 and state.flags["C_CONTIGUOUS"]
     return int(lib().oracle_randint(state.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n))
+
+
+def anchor(off, lst, zone, n_hosts, inst_host=None):
+    """Mode-host anchors (scheduler/cost_aware.py:45-58) of the items off[c]..off[c+1] of
+    ``lst``. Returns (mode_host, anchor_zone, rc); rc = PVT_EINVAL (-1) on an invalid item."""
+    off = np.ascontiguousarray(off, dtype=np.int64)
+    lst = np.ascontiguousarray(lst, dtype=np.int32)
+    zone = np.ascontiguousarray(zone, dtype=np.int32)
+    ih = None if inst_host is None else np.ascontiguousarray(inst_host, dtype=np.int32)
+    C = len(off) - 1
+    mode = np.zeros(C, dtype=np.int32)
+    az = np.zeros(C, dtype=np.int32)
+    rc = lib().oracle_anchor(C, int(n_hosts), _ptr(off), _ptr(lst), _ptr(ih),
+                             0 if ih is None else len(ih), _ptr(zone), _ptr(mode), _ptr(az))
+    return mode, az, rc

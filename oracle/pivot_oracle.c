@@ -393,3 +393,46 @@ int oracle_place_mt(const pvt_round* r, int threads) {
   free(hs);
   return PVT_OK;
 }
+
+/* ---------------------------------------------------------------- anchor resolution (a3)
+ * CostAwareGlobalScheduler._group_tasks (scheduler/cost_aware.py:45-58), per item:
+ *   placement, _ = max(Counter(list).items(), key=lambda x: x[1])
+ * Counter's items() follow first insertion and max() keeps the first maximum. Entries are host
+ * indices (-1 = no placement) or, with inst_host, indices into it. Outputs as pvt_anchor():
+ * anchor_zone -1 empty list, -2 mode entry -1, -3 invalid item (returns PVT_EINVAL). */
+int oracle_anchor(int32_t C, int32_t H, const int64_t* off, const int32_t* list,
+                  const int32_t* inst_host, int64_t n_inst, const int32_t* zone,
+                  int32_t* mode_host, int32_t* anchor_zone) {
+  int64_t* count = (int64_t*)calloc((size_t)H + 1, sizeof(int64_t));
+  int bad = 0;
+  if (!count) return PVT_ENOMEM;
+  for (int32_t c = 0; c < C; ++c) {
+    const int64_t lo = off[c], hi = off[c + 1];
+    int ok = lo >= 0 && hi >= lo;
+    for (int64_t j = lo; ok && j < hi; ++j) {
+      int32_t h = list[j];
+      if (inst_host) { if (h < 0 || h >= n_inst) { ok = 0; break; } h = inst_host[h]; }
+      if (h < -1 || h >= H) ok = 0;
+    }
+    if (!ok) { mode_host[c] = -1; anchor_zone[c] = -3; ++bad; continue; }
+    if (hi == lo) { mode_host[c] = -1; anchor_zone[c] = -1; continue; }
+    int32_t best = 0; int64_t best_n = -1;
+    for (int64_t j = lo; j < hi; ++j) {                 /* Counter(list) */
+      int32_t h = inst_host ? inst_host[list[j]] : list[j];
+      count[h + 1] += 1;
+    }
+    for (int64_t j = lo; j < hi; ++j) {                 /* max over items() in insertion order */
+      int32_t h = inst_host ? inst_host[list[j]] : list[j];
+      if (count[h + 1] > best_n) { best_n = count[h + 1]; best = h; }
+      if (count[h + 1] > 0) count[h + 1] = -count[h + 1];   /* visit each key once */
+    }
+    for (int64_t j = lo; j < hi; ++j) {
+      int32_t h = inst_host ? inst_host[list[j]] : list[j];
+      count[h + 1] = 0;
+    }
+    mode_host[c] = best;
+    anchor_zone[c] = best >= 0 ? zone[best] : -2;
+  }
+  free(count);
+  return bad ? PVT_EINVAL : PVT_OK;
+}

@@ -1,0 +1,37 @@
+// pvt_anchor.h — anchor resolution for cost_aware groups.
+//
+// The reference groups each ready task by the storage of the zone of its predecessors' MODE
+// host (scheduler/cost_aware.py:45-58):
+//     preds = [t for p in app.get_predecessors(c.id) for t in p.tasks]
+//     placement, _ = max(Counter([t.placement for t in preds]).items(), key=lambda x: x[1])
+// Counter keeps first-insertion order and max() returns the first maximum, so the mode is the
+// host with the highest count and, among equal counts, the earliest first occurrence in the
+// predecessor list. On the GPU: one workgroup per item (a container of ready tasks) sorts its
+// list as 64-bit keys (host + 1) << 32 | position (LDS for lists up to ANC_LDS entries, a
+// global scratch region beyond), finds each run's length with a binary search for its first
+// key, and reduces (count, ~first position) with a block max.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pvt {
+
+constexpr int ANC_THREADS = 256;
+constexpr int ANC_LDS = 4096;    // 32 KiB of keys per workgroup; longer lists sort in scratch
+
+struct AnchorArgs {
+  int C, H;
+  int64_t n_pred, n_inst;
+  const int64_t* off;       // [C+1]
+  const int32_t* list;      // [n_pred] host index (or instance index when inst_host is set)
+  const int32_t* inst_host; // optional [n_inst]: host per instance, -1 = not placed
+  const int32_t* zone;      // [H]
+  int32_t* mode_host;       // [C] out
+  int32_t* anchor_zone;     // [C] out
+  uint64_t* scratch;        // [2 * n_pred] keys for lists longer than ANC_LDS
+  int32_t* bad;             // [1] count of items with an invalid range or host index
+};
+
+void launch_anchor(const AnchorArgs& a, hipStream_t st);
+
+}  // namespace pvt

@@ -24,6 +24,7 @@
 #include "pivot_place.h"
 #include "pvt_kernels.h"
 #include "pvt_opp.h"
+#include "pvt_anchor.h"
 
 using namespace pvt;
 
@@ -67,7 +68,7 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt;
+      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
   int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
   std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
@@ -198,7 +199,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
-                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt};
+                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -731,6 +732,34 @@ extern "C" int pvt_place_batch(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_
   ctx->rs.active = false;
   if (n_rounds == 0) return PVT_OK;
   return place_resident(ctx, rounds, n_rounds);
+}
+
+// ---------------------------------------------------------------- anchor resolution (a3)
+extern "C" int pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a) {
+  if (!ctx || !a) return PVT_EINVAL;
+  if (a->n_items < 0 || a->n_hosts < 0 || a->n_pred < 0 || a->n_inst < 0)
+    return fail(ctx, PVT_EINVAL, "negative size in pvt_anchor_args");
+  if (a->n_items == 0) return PVT_OK;
+  if (!a->off || !a->mode_host || !a->anchor_zone || (a->n_pred > 0 && (!a->list || !a->zone)) ||
+      (a->inst_host == nullptr) != (a->n_inst == 0))
+    return fail(ctx, PVT_EINVAL, "null pointer in pvt_anchor_args");
+  (void)hipSetDevice(ctx->device);
+  ENSURE(ctx->anc_scr, 16 + sizeof(uint64_t) * 2 * (size_t)a->n_pred);
+  int32_t* bad = P<int32_t>(ctx->anc_scr);
+  HIPCHK(hipMemsetAsync(bad, 0, sizeof(int32_t), ctx->stream));
+  AnchorArgs k{a->n_items, a->n_hosts, a->n_pred, a->n_inst, a->off, a->list, a->inst_host,
+               a->zone, a->mode_host, a->anchor_zone,
+               reinterpret_cast<uint64_t*>(P<char>(ctx->anc_scr) + 16), bad};
+  {
+    Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * (double)a->n_pred);
+    launch_anchor(k, ctx->stream);
+  }
+  HIPCHK(hipGetLastError());
+  int32_t nbad = 0;
+  HIPCHK(hipMemcpyAsync(&nbad, bad, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (nbad) return fail(ctx, PVT_EINVAL, "%d anchor item(s) with invalid offsets or indices", nbad);
+  return PVT_OK;
 }
 
 extern "C" int pvt_set_resident(pvt_ctx* ctx, int32_t max_hosts) {

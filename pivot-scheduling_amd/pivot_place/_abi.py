@@ -60,6 +60,25 @@ class pvt_round(ctypes.Structure):
     ]
 
 
+class pvt_anchor_args(ctypes.Structure):
+    _fields_ = [
+        ("n_items", ctypes.c_int32),
+        ("n_hosts", ctypes.c_int32),
+        ("n_pred", ctypes.c_int64),
+        ("n_inst", ctypes.c_int64),
+        ("off", ctypes.c_void_p),
+        ("list", ctypes.c_void_p),
+        ("inst_host", ctypes.c_void_p),
+        ("zone", ctypes.c_void_p),
+        ("mode_host", ctypes.c_void_p),
+        ("anchor_zone", ctypes.c_void_p),
+    ]
+
+
+# pvt_anchor anchor_zone codes (include/pivot_place.h)
+ANCHOR_NO_PREDS, ANCHOR_UNPLACED, ANCHOR_INVALID = -1, -2, -3
+
+
 class pvt_kstats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_int64), ("ms", ctypes.c_double),
                 ("candidates", ctypes.c_double), ("bytes", ctypes.c_double)]

@@ -54,6 +54,7 @@ def load_library(path=None):
         "pvt_shard_commit": ([c_void_p, c_void_p], c_int),
         "pvt_place_batch": ([c_void_p, c_void_p, ctypes.c_int32], c_int),
         "pvt_set_resident": ([c_void_p, ctypes.c_int32], c_int),
+        "pvt_anchor": ([c_void_p, c_void_p], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -266,6 +267,39 @@ class PlacementEngine:
     def set_resident(self, max_hosts=_abi.PVT_RESIDENT_MAX_HOSTS):
         """pvt_place runs rounds up to ``max_hosts`` hosts on the resident kernel (0: never)."""
         self._check(self.lib.pvt_set_resident(self.ctx, int(max_hosts)))
+
+    # -- anchor resolution (include/pivot_place.h, pvt_anchor; reference cost_aware.py:45-58)
+    def anchor_device(self, off, lst, zone, mode_host, anchor_zone, inst_host=None):
+        """Mode-host anchors of the items off[c]..off[c+1] of ``lst`` (device int64 / int32
+        tensors); writes ``mode_host`` and ``anchor_zone`` (device int32 tensors, one per item).
+        ``inst_host``: optional device int32 table that ``lst`` indexes."""
+        torch = _torch()
+        stream = torch.cuda.current_stream(self.device)
+        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        a = _abi.pvt_anchor_args()
+        a.n_items = off.numel() - 1
+        a.n_hosts = zone.numel()
+        a.n_pred = lst.numel()
+        a.n_inst = 0 if inst_host is None else inst_host.numel()
+        a.off, a.list, a.zone = off.data_ptr(), lst.data_ptr(), zone.data_ptr()
+        a.inst_host = None if inst_host is None else inst_host.data_ptr()
+        a.mode_host, a.anchor_zone = mode_host.data_ptr(), anchor_zone.data_ptr()
+        self._check(self.lib.pvt_anchor(self.ctx, ctypes.addressof(a)))
+
+    def anchor(self, off, lst, zone, inst_host=None):
+        """Host-array form of anchor_device: returns (mode_host, anchor_zone) numpy arrays."""
+        torch = _torch()
+        dev = self.device
+        off_d = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
+        C = off_d.numel() - 1
+        lst_d = torch.from_numpy(np.ascontiguousarray(lst, dtype=np.int32)).to(dev)
+        zone_d = torch.from_numpy(np.ascontiguousarray(zone, dtype=np.int32)).to(dev)
+        ih = None if inst_host is None else torch.from_numpy(
+            np.ascontiguousarray(inst_host, dtype=np.int32)).to(dev)
+        mode = torch.empty(max(C, 0), dtype=torch.int32, device=dev)
+        az = torch.empty(max(C, 0), dtype=torch.int32, device=dev)
+        self.anchor_device(off_d, lst_d, zone_d, mode, az, ih)
+        return mode.cpu().numpy(), az.cpu().numpy()
 
     # -- host-dimension sharding (include/pivot_place.h, pvt_shard_*); see pivot_place.sharded
     def shard_begin(self, dr: DeviceRound, host_lo, host_hi, world):

@@ -26,7 +26,7 @@ What stays on the host, as in the reference: cost_aware grouping and anchor choi
 (cost_aware.py:45-58, the ``randomizer.choice(storage)`` at :38-39), because it reads the
 application DAG and advances the RNG.
 """
-from collections import Counter, OrderedDict
+from collections import OrderedDict
 
 import numpy as np
 import numpy.random as rnd
@@ -80,6 +80,7 @@ class _ClusterTables:
         hosts = cluster.hosts
         self.n_hosts = len(hosts)
         self.host_ids = [h.id for h in hosts]
+        self.host_index = {hid: i for i, hid in enumerate(self.host_ids)}
         self.zones = list(meta.zones) if meta is not None else []
         self.zone_of = {z: i for i, z in enumerate(self.zones)}
         self.zone = np.array([self.zone_of.get(h.locality, 0) for h in hosts], dtype=np.int32)
@@ -163,22 +164,36 @@ class CostAwarePlacement(PlacementMixin):
     def _group_tasks(self, tasks):
         """Groups keyed by anchor storage, or by application for source tasks, in first-seen
         order (reference cost_aware.py:45-58). The anchor of a task with predecessors is the
-        zone of the MODE host of all predecessor task placements (first seen wins ties)."""
+        zone of the MODE host of all predecessor task placements (first seen wins ties); the
+        mode is computed on the GPU (pvt_anchor), one item per distinct container."""
         cluster = self.cluster
-        groups = OrderedDict()
+        tab = self._tables()
+        items, item_of, off, lst = [], [], [0], []
         memo = {}
         for t in tasks:
             c = t.container
-            key = memo.get(id(c))
-            if key is None:
-                app = c.application
-                placements = [p.placement for pc in app.get_predecessors(c.id) for p in pc.tasks]
-                if placements:
-                    host_id = max(Counter(placements).items(), key=lambda kv: kv[1])[0]
-                    key = ('storage', cluster.get_storage_by_locality(cluster.get_host(host_id).locality))
-                else:
-                    key = ('app', app)
-                memo[id(c)] = key
+            i = memo.get(id(c))
+            if i is None:
+                i = memo[id(c)] = len(items)
+                items.append(c)
+                idx = tab.host_index
+                for pc in c.application.get_predecessors(c.id):
+                    lst.extend(idx.get(p.placement, -1) for p in pc.tasks)
+                off.append(len(lst))
+            item_of.append(i)
+        zones = None
+        if lst:
+            _, zones = self._engine().anchor(np.array(off, dtype=np.int64),
+                                             np.array(lst, dtype=np.int32), tab.zone)
+        groups = OrderedDict()
+        for t, i in zip(tasks, item_of):
+            z = -1 if zones is None else int(zones[i])
+            if z == _abi.ANCHOR_NO_PREDS:
+                key = ('app', items[i].application)
+            elif z >= 0:
+                key = ('storage', cluster.get_storage_by_locality(tab.zones[z]))
+            else:   # the mode placement is not a host of the cluster (get_host -> None)
+                raise AttributeError("'NoneType' object has no attribute 'locality'")
             groups.setdefault(key, []).append(t)
         return groups
 

@@ -237,6 +237,11 @@ def main():
             def place(self, r):
                 return oracle.place(r)
 
+            def anchor(self, off, lst, zone, inst_host=None):
+                mode, az, rc = oracle.anchor(off, lst, zone, len(zone), inst_host)
+                assert rc == 0
+                return mode, az
+
         name = sys.argv[2]
         for cfg, n_hosts, n_apps, job_file, pols in CONFIGS:
             for label, policy, kwargs in pols:

@@ -48,8 +48,18 @@ def test_round_struct_layout_matches_header():
     assert ctypes.sizeof(_abi.pvt_round) == 8 * 4 + 12 * 8
 
 
+def test_anchor_struct_layout_matches_header():
+    text = open(HEADER).read()
+    body = re.search(r"typedef struct pvt_anchor_args \{(.*?)\} pvt_anchor_args;", text,
+                     flags=re.S).group(1)
+    fields = re.findall(r"\b(\w+);", body)
+    assert fields == [f for f, _ in _abi.pvt_anchor_args._fields_]
+    assert ctypes.sizeof(_abi.pvt_anchor_args) == 4 * 2 + 8 * 2 + 6 * 8
+
+
 def test_null_arguments_are_rejected_without_a_device():
     lib = engine.load_library()
+    assert lib.pvt_anchor(None, None) == _abi.PVT_EINVAL
     assert lib.pvt_place(None, None) == _abi.PVT_EINVAL
     assert lib.pvt_ctx_destroy(None) == _abi.PVT_EINVAL
     assert lib.pvt_ctx_create(0, None) == _abi.PVT_EINVAL

@@ -24,6 +24,11 @@ class OracleEngine:
     def place(self, r):
         return oracle.place(r)
 
+    def anchor(self, off, lst, zone, inst_host=None):
+        mode, az, rc = oracle.anchor(off, lst, zone, len(zone), inst_host)
+        assert rc == 0
+        return mode, az
+
 
 CLASSES = {
     "cost_aware": policies.CostAwareGlobalScheduler,
