@@ -190,21 +190,26 @@ int  pvt_set_resident(pvt_ctx* ctx, int32_t max_hosts);
  * counts (Counter insertion order + max's first maximum); anchor_zone = zone[mode_host], or
  *   -1  empty list (the task groups by its application, cost_aware.py:56-57),
  *   -2  the mode entry is -1 (the reference raises AttributeError on get_host(None).locality),
- *   -3  invalid offsets or an index out of range (the call then returns PVT_EINVAL).
- * All pointers are device pointers. n_pred = off[C]; lists may hold up to 2^30 entries.
- * Synchronises before returning.
+ *   -3  invalid row, offsets or index out of range (the call then returns PVT_EINVAL).
+ * With `item` set, item c uses row item[c] of a resident list table instead: its list is
+ * list[off[item[c]] .. off[item[c]+1]) (off then has n_rows + 1 entries), so a trace kept in
+ * HBM uploads only the ready containers' row numbers per round.
+ * All pointers are device pointers. Lists may hold up to 2^30 entries. Synchronises before
+ * returning.
  */
 typedef struct pvt_anchor_args {
   int32_t n_items;            /* C                                                        */
   int32_t n_hosts;            /* H                                                        */
-  int64_t n_pred;             /* length of list (= off[C])                                */
+  int64_t n_pred;             /* length of list                                           */
   int64_t n_inst;             /* length of inst_host (0 when inst_host is NULL)           */
-  const int64_t* off;         /* [C+1]                                                    */
+  const int64_t* off;         /* [C+1], or [n_rows+1] when item is set                    */
   const int32_t* list;        /* [n_pred]                                                 */
   const int32_t* inst_host;   /* [n_inst] or NULL                                         */
   const int32_t* zone;        /* [H]                                                      */
   int32_t* mode_host;         /* [C] out                                                  */
   int32_t* anchor_zone;       /* [C] out                                                  */
+  const int32_t* item;        /* [C] row of off per item, or NULL (item c = row c)        */
+  int64_t n_rows;             /* rows of off when item is set (0 when item is NULL)       */
 } pvt_anchor_args;
 int  pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a);
 

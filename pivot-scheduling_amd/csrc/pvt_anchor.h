@@ -6,10 +6,12 @@
 //     placement, _ = max(Counter([t.placement for t in preds]).items(), key=lambda x: x[1])
 // Counter keeps first-insertion order and max() returns the first maximum, so the mode is the
 // host with the highest count and, among equal counts, the earliest first occurrence in the
-// predecessor list. On the GPU: one workgroup per item (a container of ready tasks) sorts its
-// list as 64-bit keys (host + 1) << 32 | position (LDS for lists up to ANC_LDS entries, a
-// global scratch region beyond), finds each run's length with a binary search for its first
-// key, and reduces (count, ~first position) with a block max.
+// predecessor list. On the GPU: one workgroup per item (a container of ready tasks). A list of
+// up to ANC_LDS entries is sorted in LDS as 64-bit keys (host + 1) << 32 | position; each run
+// end finds its run start by binary search, and the block keeps the max of (count, ~first
+// position). A longer list is counted instead: passes over host ranges of ANC_LDS hosts
+// (between the list's min and max host) build LDS histograms of (count, first position) with
+// LDS atomics. No global scratch, so items may share rows of a resident list table.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -17,18 +19,18 @@
 namespace pvt {
 
 constexpr int ANC_THREADS = 256;
-constexpr int ANC_LDS = 4096;    // 32 KiB of keys per workgroup; longer lists sort in scratch
+constexpr int ANC_LDS = 8192;    // 64 KiB of LDS per workgroup; longer lists are counted
 
 struct AnchorArgs {
   int C, H;
-  int64_t n_pred, n_inst;
-  const int64_t* off;       // [C+1]
+  int64_t n_pred, n_inst, n_rows;
+  const int64_t* off;       // [C+1], or [n_rows+1] when item is set
+  const int32_t* item;      // optional [C]: the row of off for each item
   const int32_t* list;      // [n_pred] host index (or instance index when inst_host is set)
   const int32_t* inst_host; // optional [n_inst]: host per instance, -1 = not placed
   const int32_t* zone;      // [H]
   int32_t* mode_host;       // [C] out
   int32_t* anchor_zone;     // [C] out
-  uint64_t* scratch;        // [2 * n_pred] keys for lists longer than ANC_LDS
   int32_t* bad;             // [1] count of items with an invalid range or host index
 };
 

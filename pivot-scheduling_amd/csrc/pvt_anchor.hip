@@ -1,7 +1,8 @@
 // pvt_anchor.hip — mode-host anchor resolution (reference scheduler/cost_aware.py:45-58).
 // See pvt_anchor.h for the rule. One 256-thread workgroup per item; the item's predecessor
-// list is sorted as (host + 1) << 32 | position keys (bitonic, LDS or scratch), every run end
-// binary-searches its run start, and the block keeps the max of (count << 32 | ~first).
+// list is sorted in LDS as (host + 1) << 32 | position keys (bitonic), every run end
+// binary-searches its run start, and the block keeps the max of (count << 32 | ~first); lists
+// longer than the LDS tile are counted in LDS histograms over host ranges instead.
 // Integer-only, gather-bound: 4 B (8 B through inst_host) read per list entry.
 #include "pvt_anchor.h"
 
@@ -28,20 +29,40 @@ __device__ __forceinline__ int entry_host(const AnchorArgs& a, int64_t j, bool* 
   return h;
 }
 
+__device__ __forceinline__ void item_fail(const AnchorArgs& a, int c) {
+  a.mode_host[c] = -1;
+  a.anchor_zone[c] = -3;
+  atomicAdd(a.bad, 1);
+}
+
+// Block max of a 64-bit value; every thread gets the result. `red` holds one slot per wave.
+__device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t* red) {
+  v = wave_max_u64(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  uint64_t b = red[0];
+#pragma unroll
+  for (int w = 1; w < ANC_THREADS / 64; ++w) b = red[w] > b ? red[w] : b;
+  return b;
+}
+
 __global__ void __launch_bounds__(ANC_THREADS) anchor_kernel(AnchorArgs a) {
   __shared__ uint64_t lds[ANC_LDS];
   __shared__ uint64_t red[ANC_THREADS / 64];
-  __shared__ int flag;
   const int c = blockIdx.x;
   const int tid = threadIdx.x;
-  const int64_t lo = a.off[c], hi = a.off[c + 1];
-  const bool range_ok = lo >= 0 && hi >= lo && hi <= a.n_pred && hi - lo <= (1LL << 30);
-  if (!range_ok) {
-    if (tid == 0) {
-      a.mode_host[c] = -1;
-      a.anchor_zone[c] = -3;
-      atomicAdd(a.bad, 1);
+  int64_t row = c;
+  if (a.item) {
+    row = a.item[c];
+    if (row < 0 || row >= a.n_rows) {
+      if (tid == 0) item_fail(a, c);
+      return;
     }
+  }
+  const int64_t lo = a.off[row], hi = a.off[row + 1];
+  if (!(lo >= 0 && hi >= lo && hi <= a.n_pred && hi - lo <= (1LL << 30))) {
+    if (tid == 0) item_fail(a, c);
     return;
   }
   const int n = (int)(hi - lo);
@@ -49,67 +70,93 @@ __global__ void __launch_bounds__(ANC_THREADS) anchor_kernel(AnchorArgs a) {
     if (tid == 0) { a.mode_host[c] = -1; a.anchor_zone[c] = -1; }
     return;
   }
-  int m = 1;
-  while (m < n) m <<= 1;
-  uint64_t* buf = m <= ANC_LDS ? lds : a.scratch + 2 * lo;
-  if (tid == 0) flag = 0;
-  __syncthreads();
-  bool ok = true;
-  for (int i = tid; i < m; i += ANC_THREADS) {
-    uint64_t k = ~0ull;
-    if (i < n) {
-      const int h = entry_host(a, lo + i, &ok);
-      k = ((uint64_t)(uint32_t)(h + 1) << 32) | (uint32_t)i;
+  uint64_t best = 0;
+  if (n <= ANC_LDS) {
+    int m = 1;
+    while (m < n) m <<= 1;
+    bool ok = true;
+    for (int i = tid; i < m; i += ANC_THREADS) {
+      uint64_t k = ~0ull;
+      if (i < n) {
+        const int h = entry_host(a, lo + i, &ok);
+        k = ((uint64_t)(uint32_t)(h + 1) << 32) | (uint32_t)i;
+      }
+      lds[i] = k;
     }
-    buf[i] = k;
-  }
-  if (!ok) atomicOr(&flag, 1);
-  __syncthreads();
-  if (flag) {
-    if (tid == 0) {
-      a.mode_host[c] = -1;
-      a.anchor_zone[c] = -3;
-      atomicAdd(a.bad, 1);
+    if (__syncthreads_or(!ok)) {
+      if (tid == 0) item_fail(a, c);
+      return;
     }
-    return;
-  }
-  // bitonic sort, ascending
-  for (int k = 2; k <= m; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < m; i += ANC_THREADS) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint64_t x = buf[i], y = buf[l];
-          const bool up = (i & k) == 0;
-          if (up ? x > y : x < y) { buf[i] = y; buf[l] = x; }
+    // bitonic sort, ascending
+    for (int k = 2; k <= m; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < m; i += ANC_THREADS) {
+          const int l = i ^ j;
+          if (l > i) {
+            const uint64_t x = lds[i], y = lds[l];
+            const bool up = (i & k) == 0;
+            if (up ? x > y : x < y) { lds[i] = y; lds[l] = x; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // run ends: count = end - start + 1, first position = low word of the run's first key
+    for (int i = tid; i < n; i += ANC_THREADS) {
+      const uint32_t key_hi = (uint32_t)(lds[i] >> 32);
+      if (i + 1 < n && (uint32_t)(lds[i + 1] >> 32) == key_hi) continue;
+      const uint64_t target = (uint64_t)key_hi << 32;
+      int s = 0, e = i;         // first index in [0, i] with lds[idx] >= target
+      while (s < e) {
+        const int mid = (s + e) >> 1;
+        if (lds[mid] < target) s = mid + 1; else e = mid;
+      }
+      const uint32_t first = (uint32_t)lds[s];
+      const uint64_t v = ((uint64_t)(uint32_t)(i - s + 1) << 32) | (uint64_t)(0xffffffffu - first);
+      best = v > best ? v : best;
+    }
+    best = block_max_u64(best, red);
+  } else {
+    // long list: histogram passes over ranges of ANC_LDS keys (key = host + 1)
+    bool ok = true;
+    uint32_t kmin = 0xffffffffu, kmax = 0;
+    for (int i = tid; i < n; i += ANC_THREADS) {
+      const uint32_t k = (uint32_t)(entry_host(a, lo + i, &ok) + 1);
+      kmin = k < kmin ? k : kmin;
+      kmax = k > kmax ? k : kmax;
+    }
+    if (__syncthreads_or(!ok)) {
+      if (tid == 0) item_fail(a, c);
+      return;
+    }
+    const uint32_t khi = (uint32_t)block_max_u64(kmax, red);
+    const uint32_t klo = 0xffffffffu - (uint32_t)block_max_u64(0xffffffffu - kmin, red);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(lds);
+    uint32_t* fst = cnt + ANC_LDS;
+    for (uint32_t base = klo; base <= khi; base += ANC_LDS) {
+      for (int j = tid; j < ANC_LDS; j += ANC_THREADS) { cnt[j] = 0; fst[j] = 0xffffffffu; }
+      __syncthreads();
+      for (int i = tid; i < n; i += ANC_THREADS) {
+        bool ok2 = true;
+        const uint32_t k = (uint32_t)(entry_host(a, lo + i, &ok2) + 1) - base;
+        if (k < (uint32_t)ANC_LDS) {
+          atomicAdd(&cnt[k], 1u);
+          atomicMin(&fst[k], (uint32_t)i);
         }
       }
       __syncthreads();
+      for (int j = tid; j < ANC_LDS; j += ANC_THREADS)
+        if (cnt[j]) {
+          const uint64_t v = ((uint64_t)cnt[j] << 32) | (uint64_t)(0xffffffffu - fst[j]);
+          best = v > best ? v : best;
+        }
+      __syncthreads();
+      if (khi - base < (uint32_t)ANC_LDS) break;    // (also stops base from wrapping)
     }
+    best = block_max_u64(best, red);
   }
-  // run ends: count = end - start + 1, first position = low word of the run's first key
-  uint64_t best = 0;
-  for (int i = tid; i < n; i += ANC_THREADS) {
-    const uint64_t k = buf[i];
-    const uint32_t key_hi = (uint32_t)(k >> 32);
-    if (i + 1 < n && (uint32_t)(buf[i + 1] >> 32) == key_hi) continue;
-    const uint64_t target = (uint64_t)key_hi << 32;
-    int s = 0, e = i;           // first index in [0, i] with buf[idx] >= target
-    while (s < e) {
-      const int mid = (s + e) >> 1;
-      if (buf[mid] < target) s = mid + 1; else e = mid;
-    }
-    const uint32_t first = (uint32_t)buf[s];
-    const uint64_t v = ((uint64_t)(uint32_t)(i - s + 1) << 32) | (uint64_t)(0xffffffffu - first);
-    best = v > best ? v : best;
-  }
-  best = wave_max_u64(best);
-  if ((tid & 63) == 0) red[tid >> 6] = best;
-  __syncthreads();
   if (tid == 0) {
-    uint64_t b = red[0];
-    for (int w = 1; w < ANC_THREADS / 64; ++w) b = red[w] > b ? red[w] : b;
-    const uint32_t first = 0xffffffffu - (uint32_t)b;
+    const uint32_t first = 0xffffffffu - (uint32_t)best;
     bool ok2 = true;
     const int h = entry_host(a, lo + first, &ok2);
     a.mode_host[c] = h;

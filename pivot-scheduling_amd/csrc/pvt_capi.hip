@@ -741,15 +741,14 @@ extern "C" int pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a) {
     return fail(ctx, PVT_EINVAL, "negative size in pvt_anchor_args");
   if (a->n_items == 0) return PVT_OK;
   if (!a->off || !a->mode_host || !a->anchor_zone || (a->n_pred > 0 && (!a->list || !a->zone)) ||
-      (a->inst_host == nullptr) != (a->n_inst == 0))
+      (a->inst_host == nullptr) != (a->n_inst == 0) || (a->item == nullptr) != (a->n_rows == 0))
     return fail(ctx, PVT_EINVAL, "null pointer in pvt_anchor_args");
   (void)hipSetDevice(ctx->device);
-  ENSURE(ctx->anc_scr, 16 + sizeof(uint64_t) * 2 * (size_t)a->n_pred);
+  ENSURE(ctx->anc_scr, 16);
   int32_t* bad = P<int32_t>(ctx->anc_scr);
   HIPCHK(hipMemsetAsync(bad, 0, sizeof(int32_t), ctx->stream));
-  AnchorArgs k{a->n_items, a->n_hosts, a->n_pred, a->n_inst, a->off, a->list, a->inst_host,
-               a->zone, a->mode_host, a->anchor_zone,
-               reinterpret_cast<uint64_t*>(P<char>(ctx->anc_scr) + 16), bad};
+  AnchorArgs k{a->n_items, a->n_hosts, a->n_pred, a->n_inst, a->n_rows, a->off, a->item,
+               a->list, a->inst_host, a->zone, a->mode_host, a->anchor_zone, bad};
   {
     Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * (double)a->n_pred);
     launch_anchor(k, ctx->stream);

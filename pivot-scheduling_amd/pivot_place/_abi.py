@@ -72,6 +72,8 @@ class pvt_anchor_args(ctypes.Structure):
         ("zone", ctypes.c_void_p),
         ("mode_host", ctypes.c_void_p),
         ("anchor_zone", ctypes.c_void_p),
+        ("item", ctypes.c_void_p),
+        ("n_rows", ctypes.c_int64),
     ]
 
 

@@ -269,15 +269,18 @@ class PlacementEngine:
         self._check(self.lib.pvt_set_resident(self.ctx, int(max_hosts)))
 
     # -- anchor resolution (include/pivot_place.h, pvt_anchor; reference cost_aware.py:45-58)
-    def anchor_device(self, off, lst, zone, mode_host, anchor_zone, inst_host=None):
+    def anchor_device(self, off, lst, zone, mode_host, anchor_zone, inst_host=None, item=None):
         """Mode-host anchors of the items off[c]..off[c+1] of ``lst`` (device int64 / int32
         tensors); writes ``mode_host`` and ``anchor_zone`` (device int32 tensors, one per item).
-        ``inst_host``: optional device int32 table that ``lst`` indexes."""
+        ``inst_host``: optional device int32 table that ``lst`` indexes. ``item``: optional
+        device int32 row numbers (item c uses row item[c] of ``off``)."""
         torch = _torch()
         stream = torch.cuda.current_stream(self.device)
         self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
         a = _abi.pvt_anchor_args()
-        a.n_items = off.numel() - 1
+        a.n_items = off.numel() - 1 if item is None else item.numel()
+        a.n_rows = 0 if item is None else off.numel() - 1
+        a.item = None if item is None else item.data_ptr()
         a.n_hosts = zone.numel()
         a.n_pred = lst.numel()
         a.n_inst = 0 if inst_host is None else inst_host.numel()

@@ -54,7 +54,7 @@ def test_anchor_struct_layout_matches_header():
                      flags=re.S).group(1)
     fields = re.findall(r"\b(\w+);", body)
     assert fields == [f for f, _ in _abi.pvt_anchor_args._fields_]
-    assert ctypes.sizeof(_abi.pvt_anchor_args) == 4 * 2 + 8 * 2 + 6 * 8
+    assert ctypes.sizeof(_abi.pvt_anchor_args) == 4 * 2 + 8 * 2 + 7 * 8 + 8
 
 
 def test_null_arguments_are_rejected_without_a_device():
