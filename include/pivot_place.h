@@ -213,6 +213,46 @@ typedef struct pvt_anchor_args {
 } pvt_anchor_args;
 int  pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a);
 
+/*
+ * Meter aggregates of a batch of S scenarios (replaces the properties
+ * Meter.cumulative_instance_hours, .total_network_traffic_cost and .average_congestion_delay,
+ * resources/meter.py:31-53, read by alibaba/runner.py:45-51 via Meter.save).
+ *
+ * The logs are nested CSR arrays in the meter's own dict orders:
+ *   scenario s -> hosts  host_off[s] .. host_off[s+1]          (Meter.__hosts)
+ *   host h     -> intervals iv_off[h] .. iv_off[h+1]: [iv_start, iv_end] (check-in/out)
+ *   scenario s -> routes route_off[s] .. route_off[s+1]        (Meter.__routes)
+ *   route r    -> packets pkt_off[r] .. pkt_off[r+1]; route_cost[r] = cost[src.loc, dst.loc]
+ *   packet p   -> transfers tr_off[p] .. tr_off[p+1]: [tr_start, tr_end, tr_size]
+ * Per scenario: instance_hours = sum_h sum_v (end - start) / 3600; egress_cost = sum_r
+ * route_cost * (sum_p sum_t size) / 8000 (ResourceMetadata.calc_network_traffic_cost,
+ * resources/__init__.py:565-569); congestion_delay = sum over consecutive transfers of a packet
+ * of (start_i - end_{i-1}) / #packets, 0 without packets. Per host and per route the sums run
+ * in the reference's order; across hosts / routes a fixed tree (fp64, within 1e-9 relative of
+ * the reference's left-to-right sum). All pointers are device pointers. Returns PVT_EINVAL if an
+ * offset is out of range. Synchronises before returning.
+ */
+typedef struct pvt_meter_log {
+  int32_t n_scen;             /* S                                                        */
+  int32_t reserved;           /* must be 0                                                */
+  int64_t n_host_rows, n_iv, n_routes, n_pkts, n_tr;   /* lengths of the level arrays    */
+  const int64_t* host_off;    /* [S+1]                                                    */
+  const int64_t* iv_off;      /* [n_host_rows+1]                                          */
+  const double* iv_start;     /* [n_iv]                                                   */
+  const double* iv_end;       /* [n_iv]                                                   */
+  const int64_t* route_off;   /* [S+1]                                                    */
+  const double* route_cost;   /* [n_routes]                                               */
+  const int64_t* pkt_off;     /* [n_routes+1]                                             */
+  const int64_t* tr_off;      /* [n_pkts+1]                                               */
+  const double* tr_start;     /* [n_tr]                                                   */
+  const double* tr_end;       /* [n_tr]                                                   */
+  const double* tr_size;      /* [n_tr]                                                   */
+  double* instance_hours;     /* [S] out                                                  */
+  double* egress_cost;        /* [S] out                                                  */
+  double* congestion_delay;   /* [S] out                                                  */
+} pvt_meter_log;
+int  pvt_meter(pvt_ctx* ctx, const pvt_meter_log* m);
+
 /* Human-readable text of the last error on this context (static storage of the ctx). */
 const char* pvt_last_error(pvt_ctx* ctx);
 

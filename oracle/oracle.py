@@ -35,6 +35,8 @@ def lib():
         _lib.oracle_randint.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint64]
         _lib.oracle_place_mt.restype = ctypes.c_int
         _lib.oracle_place_mt.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        _lib.oracle_meter.restype = ctypes.c_int
+        _lib.oracle_meter.argtypes = [ctypes.c_void_p]
         _lib.oracle_anchor.restype = ctypes.c_int
         _lib.oracle_anchor.argtypes = [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_void_p] * 3 + [
             ctypes.c_int64] + [ctypes.c_void_p] * 3
@@ -91,3 +93,14 @@ def anchor(off, lst, zone, n_hosts, inst_host=None):
     rc = lib().oracle_anchor(C, int(n_hosts), _ptr(off), _ptr(lst), _ptr(ih),
                              0 if ih is None else len(ih), _ptr(zone), _ptr(mode), _ptr(az))
     return mode, az, rc
+
+
+def meter(log):
+    """Reference-order aggregates of a pivot_place.meter.MeterLog: (dict of arrays, rc)."""
+    S = log.n_scen
+    out = {k: np.zeros(max(S, 1)) for k in ("instance_hours", "egress_cost", "congestion_delay")}
+    arrs = [np.ascontiguousarray(a) for _, a in log.arrays()]
+    m = log.fill(lambda a: a.ctypes.data if a.size else None, [o.ctypes.data for o in out.values()])
+    rc = lib().oracle_meter(ctypes.addressof(m))
+    del arrs
+    return {k: v[:S] for k, v in out.items()}, rc

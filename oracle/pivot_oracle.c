@@ -436,3 +436,54 @@ int oracle_anchor(int32_t C, int32_t H, const int64_t* off, const int32_t* list,
   free(count);
   return bad ? PVT_EINVAL : PVT_OK;
 }
+
+/* ---------------------------------------------------------------- meter aggregates (f4)
+ * resources/meter.py:31-53, left to right exactly as the reference's Python sums run:
+ *   cumulative_instance_hours = sum([sum([v[1]-v[0] for v in vals]) for h, vals in hosts])/3600
+ *   total_network_traffic_cost: cost += meta.cost[src, dst] * data_size / 8000 per route, with
+ *     data_size = sum([sum(size for transfers) for packets])
+ *   average_congestion_delay: delay += start_i - end_{i-1} over every packet's transfers,
+ *     n_pkts and delay / n_pkts
+ * Host pointers, layout of pvt_meter_log. Returns PVT_EINVAL on an out-of-range offset. */
+int oracle_meter(const pvt_meter_log* m) {
+  for (int32_t s = 0; s < m->n_scen; ++s) {
+    const int64_t h0 = m->host_off[s], h1 = m->host_off[s + 1];
+    const int64_t r0 = m->route_off[s], r1 = m->route_off[s + 1];
+    if (h0 < 0 || h1 < h0 || h1 > m->n_host_rows || r0 < 0 || r1 < r0 || r1 > m->n_routes)
+      return PVT_EINVAL;
+    double hours = 0.0;
+    for (int64_t h = h0; h < h1; ++h) {
+      const int64_t v0 = m->iv_off[h], v1 = m->iv_off[h + 1];
+      if (v0 < 0 || v1 < v0 || v1 > m->n_iv) return PVT_EINVAL;
+      double acc = 0.0;
+      for (int64_t v = v0; v < v1; ++v) acc += m->iv_end[v] - m->iv_start[v];
+      hours += acc;
+    }
+    double cost = 0.0, delay = 0.0;
+    int64_t npk = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+      const int64_t p0 = m->pkt_off[r], p1 = m->pkt_off[r + 1];
+      if (p0 < 0 || p1 < p0 || p1 > m->n_pkts) return PVT_EINVAL;
+      double size = 0.0;
+      for (int64_t p = p0; p < p1; ++p) {
+        const int64_t t0 = m->tr_off[p], t1 = m->tr_off[p + 1];
+        if (t0 < 0 || t1 < t0 || t1 > m->n_tr) return PVT_EINVAL;
+        double ps = 0.0;
+        for (int64_t t = t0; t < t1; ++t) ps += m->tr_size[t];
+        size += ps;
+      }
+      cost += m->route_cost[r] * size / 8000.0;
+    }
+    for (int64_t r = r0; r < r1; ++r) {           /* average_congestion_delay's own loop */
+      const int64_t p0 = m->pkt_off[r], p1 = m->pkt_off[r + 1];
+      npk += p1 - p0;
+      for (int64_t p = p0; p < p1; ++p)
+        for (int64_t t = m->tr_off[p] + 1; t < m->tr_off[p + 1]; ++t)
+          delay += m->tr_start[t] - m->tr_end[t - 1];
+    }
+    m->instance_hours[s] = hours / 3600.0;
+    m->egress_cost[s] = cost;
+    m->congestion_delay[s] = npk ? delay / (double)npk : 0.0;
+  }
+  return PVT_OK;
+}

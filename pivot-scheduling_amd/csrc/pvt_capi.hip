@@ -25,6 +25,7 @@
 #include "pvt_kernels.h"
 #include "pvt_opp.h"
 #include "pvt_anchor.h"
+#include "pvt_meter.h"
 
 using namespace pvt;
 
@@ -758,6 +759,38 @@ extern "C" int pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a) {
   HIPCHK(hipMemcpyAsync(&nbad, bad, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPCHK(hipStreamSynchronize(ctx->stream));
   if (nbad) return fail(ctx, PVT_EINVAL, "%d anchor item(s) with invalid offsets or indices", nbad);
+  return PVT_OK;
+}
+
+// ---------------------------------------------------------------- meter aggregates (f4)
+extern "C" int pvt_meter(pvt_ctx* ctx, const pvt_meter_log* m) {
+  if (!ctx || !m) return PVT_EINVAL;
+  if (m->n_scen < 0 || m->reserved != 0 || m->n_host_rows < 0 || m->n_iv < 0 ||
+      m->n_routes < 0 || m->n_pkts < 0 || m->n_tr < 0)
+    return fail(ctx, PVT_EINVAL, "bad size in pvt_meter_log");
+  if (m->n_scen == 0) return PVT_OK;
+  if (!m->host_off || !m->iv_off || !m->route_off || !m->pkt_off || !m->tr_off ||
+      !m->instance_hours || !m->egress_cost || !m->congestion_delay ||
+      (m->n_iv && (!m->iv_start || !m->iv_end)) || (m->n_routes && !m->route_cost) ||
+      (m->n_tr && (!m->tr_start || !m->tr_end || !m->tr_size)))
+    return fail(ctx, PVT_EINVAL, "null pointer in pvt_meter_log");
+  (void)hipSetDevice(ctx->device);
+  ENSURE(ctx->anc_scr, 16);
+  int32_t* bad = P<int32_t>(ctx->anc_scr);
+  HIPCHK(hipMemsetAsync(bad, 0, sizeof(int32_t), ctx->stream));
+  MeterArgs k{m->n_scen, m->n_host_rows, m->n_iv, m->n_routes, m->n_pkts, m->n_tr,
+              m->host_off, m->iv_off, m->route_off, m->pkt_off, m->tr_off,
+              m->iv_start, m->iv_end, m->route_cost, m->tr_start, m->tr_end, m->tr_size,
+              m->instance_hours, m->egress_cost, m->congestion_delay, bad};
+  {
+    Scope sc(ctx, PVT_K_OTHER, 0, 16.0 * (double)m->n_iv + 24.0 * (double)m->n_tr);
+    launch_meter(k, ctx->stream);
+  }
+  HIPCHK(hipGetLastError());
+  int32_t nbad = 0;
+  HIPCHK(hipMemcpyAsync(&nbad, bad, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (nbad) return fail(ctx, PVT_EINVAL, "%d scenario(s) with out-of-range meter offsets", nbad);
   return PVT_OK;
 }
 

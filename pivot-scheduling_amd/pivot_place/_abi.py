@@ -77,6 +77,15 @@ class pvt_anchor_args(ctypes.Structure):
     ]
 
 
+class pvt_meter_log(ctypes.Structure):
+    _fields_ = [("n_scen", ctypes.c_int32), ("reserved", ctypes.c_int32)] + [
+        (n, ctypes.c_int64) for n in ("n_host_rows", "n_iv", "n_routes", "n_pkts", "n_tr")] + [
+        (n, ctypes.c_void_p) for n in ("host_off", "iv_off", "iv_start", "iv_end", "route_off",
+                                       "route_cost", "pkt_off", "tr_off", "tr_start", "tr_end",
+                                       "tr_size", "instance_hours", "egress_cost",
+                                       "congestion_delay")]
+
+
 # pvt_anchor anchor_zone codes (include/pivot_place.h)
 ANCHOR_NO_PREDS, ANCHOR_UNPLACED, ANCHOR_INVALID = -1, -2, -3
 

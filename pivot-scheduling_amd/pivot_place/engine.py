@@ -55,6 +55,7 @@ def load_library(path=None):
         "pvt_place_batch": ([c_void_p, c_void_p, ctypes.c_int32], c_int),
         "pvt_set_resident": ([c_void_p, ctypes.c_int32], c_int),
         "pvt_anchor": ([c_void_p, c_void_p], c_int),
+        "pvt_meter": ([c_void_p, c_void_p], c_int),
     }
     for name, (args, res) in sig.items():
         f = getattr(lib, name)
@@ -303,6 +304,25 @@ class PlacementEngine:
         az = torch.empty(max(C, 0), dtype=torch.int32, device=dev)
         self.anchor_device(off_d, lst_d, zone_d, mode, az, ih)
         return mode.cpu().numpy(), az.cpu().numpy()
+
+    # -- meter aggregates (include/pivot_place.h, pvt_meter; reference resources/meter.py:31-53)
+    def meter(self, log):
+        """Aggregates of every scenario of a ``pivot_place.meter.MeterLog`` in one launch:
+        dict of [S] float64 numpy arrays instance_hours / egress_cost / congestion_delay."""
+        torch = _torch()
+        dev = self.device
+        keep = {name: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                for name, a in log.arrays()}
+        S = log.n_scen
+        out = {k: torch.empty(max(S, 1), dtype=torch.float64, device=dev)
+               for k in ("instance_hours", "egress_cost", "congestion_delay")}
+        m = log.fill(lambda a: None, [o.data_ptr() for o in out.values()])
+        for name, t in keep.items():
+            setattr(m, name, t.data_ptr() if t.numel() else None)
+        stream = torch.cuda.current_stream(dev)
+        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._check(self.lib.pvt_meter(self.ctx, ctypes.addressof(m)))
+        return {k: v[:S].cpu().numpy() for k, v in out.items()}
 
     # -- host-dimension sharding (include/pivot_place.h, pvt_shard_*); see pivot_place.sharded
     def shard_begin(self, dr: DeviceRound, host_lo, host_hi, world):

@@ -85,9 +85,11 @@ def dropin_class(policy, engine):
     return type("DropIn_" + policy, (mixin, scheduler.GlobalSchedulerBase), {"engine": engine})
 
 
-def simulate(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0, cls=None):
+def simulate(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0, cls=None,
+             meter_out=None):
     """Run one reference simulation; record its rounds unless ``cls`` (a scheduler class to
-    run instead of the reference policy) is given."""
+    run instead of the reference policy) is given. ``meter_out``: a list that receives
+    (meter, cluster) after the run (make_meter_logs.py)."""
     import numpy as np
     from resources.meter import Meter
     from pivot_place import des
@@ -171,6 +173,8 @@ def simulate(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0
     t0 = time.time()
     env.run()
     wall = time.time() - t0
+    if meter_out is not None:
+        meter_out.append((meter, cluster))
     apps = load_gen.apps
     submitted = [a for a in apps if a.start_time or a.end_time]
     e2e = {
