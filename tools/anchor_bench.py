@@ -47,12 +47,24 @@ def main():
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / args.steps
     P = len(tr.pinst)
+    # CPU baseline: the C restatement (oracle_anchor, 1 thread) on the same items
+    import time
+    sys.path.insert(0, ROOT)
+    from oracle import oracle
+    ih = dt.inst_host[:tr.n_instances].cpu().numpy()
+    t0 = time.perf_counter()
+    cref = oracle.anchor(tr.pinst_off, tr.pinst, zone, args.hosts, inst_host=ih)
+    cpu_s = time.perf_counter() - t0
+    mode, az = dt.anchors(items)
+    assert np.array_equal(mode.cpu().numpy(), cref[0]), "GPU anchors differ from the oracle"
     print(json.dumps({"metric": "anchor resolution (pvt_anchor, item form)", "apps": tr.n_apps,
                       "containers": tr.n_containers, "instances": tr.n_instances,
                       "list_entries": P, "hosts": args.hosts, "ms_per_launch": ms,
                       "items_per_s": tr.n_containers / ms * 1e3,
                       "entries_per_s": P / ms * 1e3,
                       "algorithmic_GBps": 8.0 * P / ms * 1e-6,
+                      "cpu_baseline": {"items_per_s": tr.n_containers / cpu_s, "cores": 1,
+                                       "kind": "port", "sample": "oracle_anchor on all items"},
                       "note": "ms includes the host-side argument checks and the 4-byte "
                               "error-count read-back of each synchronous pvt_anchor call"}))
 

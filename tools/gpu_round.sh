@@ -16,3 +16,5 @@ run bench 600 python bench.py --traffic-json gpurun_out/traffic.json
 for m in ca_bf ca_ff opp vbp_ff vbp_bf; do
   run batch_$m 200 python -u bench.py --mode $m --batch 512 --hosts 1000 --tasks 1000 --steps 5 --warmup 2 --cpu-baseline-seconds 0
 done
+run anchor_prof 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_anchor -o anchor -- python tools/anchor_bench.py
+f=$(find gpurun_out/prof_${TAG}_anchor -name "anchor_kernel_stats.csv" | head -1); cp "$f" gpurun_out/${TAG}_anchor_kernel_stats.csv
