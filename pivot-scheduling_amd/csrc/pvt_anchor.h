@@ -6,12 +6,13 @@
 //     placement, _ = max(Counter([t.placement for t in preds]).items(), key=lambda x: x[1])
 // Counter keeps first-insertion order and max() returns the first maximum, so the mode is the
 // host with the highest count and, among equal counts, the earliest first occurrence in the
-// predecessor list. On the GPU: one workgroup per item (a container of ready tasks). A list of
-// up to ANC_LDS entries is sorted in LDS as 64-bit keys (host + 1) << 32 | position; each run
-// end finds its run start by binary search, and the block keeps the max of (count, ~first
-// position). A longer list is counted instead: passes over host ranges of ANC_LDS hosts
-// (between the list's min and max host) build LDS histograms of (count, first position) with
-// LDS atomics. No global scratch, so items may share rows of a resident list table.
+// predecessor list. On the GPU: one wave per item (a container of ready tasks). Up to 64
+// entries are counted in registers; up to ANC_WLDS are sorted in the wave's LDS slice as
+// 64-bit keys (host + 1) << 32 | position, each run end finding its run start by binary search,
+// and the wave keeps the max of (count, ~first position). Longer lists are deferred to a block
+// kernel: a block-wide LDS sort up to ANC_LDS entries, beyond that passes over host ranges of
+// ANC_LDS hosts (between the list's min and max host) building LDS histograms of (count, first
+// position). No global scratch, so items may share rows of a resident list table.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -19,7 +20,8 @@
 namespace pvt {
 
 constexpr int ANC_THREADS = 256;
-constexpr int ANC_LDS = 8192;    // 64 KiB of LDS per workgroup; longer lists are counted
+constexpr int ANC_WLDS = 1024;   // keys a wave sorts alone (8 KiB of LDS per wave)
+constexpr int ANC_LDS = 8192;    // block kernel: 64 KiB of LDS per workgroup; longer are counted
 
 struct AnchorArgs {
   int C, H;
@@ -32,6 +34,8 @@ struct AnchorArgs {
   int32_t* mode_host;       // [C] out
   int32_t* anchor_zone;     // [C] out
   int32_t* bad;             // [1] count of items with an invalid range or host index
+  int32_t* deferred;        // [C] items whose lists exceed ANC_WLDS (block kernel)
+  int32_t* n_deferred;      // [1]
 };
 
 void launch_anchor(const AnchorArgs& a, hipStream_t st);

@@ -1,8 +1,9 @@
 // pvt_anchor.hip — mode-host anchor resolution (reference scheduler/cost_aware.py:45-58).
-// See pvt_anchor.h for the rule. One 256-thread workgroup per item; the item's predecessor
-// list is sorted in LDS as (host + 1) << 32 | position keys (bitonic), every run end
-// binary-searches its run start, and the block keeps the max of (count << 32 | ~first); lists
-// longer than the LDS tile are counted in LDS histograms over host ranges instead.
+// See pvt_anchor.h for the rule. One wave per item: short lists counted in registers, longer
+// ones sorted in the wave's LDS slice as (host + 1) << 32 | position keys (bitonic), every run
+// end binary-searching its run start, and the wave keeps the max of (count << 32 | ~first).
+// Lists beyond the wave's slice go to a block kernel (block-wide LDS sort, or LDS histograms
+// over host ranges for lists longer than the block's tile).
 // Integer-only, gather-bound: 4 B (8 B through inst_host) read per list entry.
 #include "pvt_anchor.h"
 
@@ -47,29 +48,12 @@ __device__ __forceinline__ uint64_t block_max_u64(uint64_t v, uint64_t* red) {
   return b;
 }
 
-__global__ void __launch_bounds__(ANC_THREADS) anchor_kernel(AnchorArgs a) {
-  __shared__ uint64_t lds[ANC_LDS];
-  __shared__ uint64_t red[ANC_THREADS / 64];
-  const int c = blockIdx.x;
+// One long list (deferred by the wave kernel: its range is already validated), whole block.
+__device__ void block_item(const AnchorArgs& a, int c, uint64_t* lds, uint64_t* red) {
   const int tid = threadIdx.x;
-  int64_t row = c;
-  if (a.item) {
-    row = a.item[c];
-    if (row < 0 || row >= a.n_rows) {
-      if (tid == 0) item_fail(a, c);
-      return;
-    }
-  }
-  const int64_t lo = a.off[row], hi = a.off[row + 1];
-  if (!(lo >= 0 && hi >= lo && hi <= a.n_pred && hi - lo <= (1LL << 30))) {
-    if (tid == 0) item_fail(a, c);
-    return;
-  }
-  const int n = (int)(hi - lo);
-  if (n == 0) {            // no predecessors: the task's group is its application
-    if (tid == 0) { a.mode_host[c] = -1; a.anchor_zone[c] = -1; }
-    return;
-  }
+  const int64_t row = a.item ? a.item[c] : c;
+  const int64_t lo = a.off[row];
+  const int n = (int)(a.off[row + 1] - lo);
   uint64_t best = 0;
   if (n <= ANC_LDS) {
     int m = 1;
@@ -164,9 +148,126 @@ __global__ void __launch_bounds__(ANC_THREADS) anchor_kernel(AnchorArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(ANC_THREADS) anchor_block_kernel(AnchorArgs a) {
+  __shared__ uint64_t lds[ANC_LDS];
+  __shared__ uint64_t red[ANC_THREADS / 64];
+  const int nd = *a.n_deferred;
+  for (int q = blockIdx.x; q < nd; q += gridDim.x) {
+    block_item(a, a.deferred[q], lds, red);
+    __syncthreads();
+  }
+}
+
+// Wave-level LDS ordering between the stages of a single wave's sort.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// One item per wave. Lists of up to 64 entries are counted in registers (lane j holds entry
+// j; a pass over the lanes gives each its host's count and first position); up to ANC_WLDS
+// entries are sorted in the wave's LDS slice; longer lists are deferred to the block kernel.
+__global__ void __launch_bounds__(ANC_THREADS) anchor_wave_kernel(AnchorArgs a) {
+  __shared__ uint64_t lds[ANC_THREADS / 64][ANC_WLDS];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int c = blockIdx.x * (ANC_THREADS / 64) + wave;
+  if (c >= a.C) return;
+  int64_t row = c;
+  if (a.item) {
+    row = a.item[c];
+    if (row < 0 || row >= a.n_rows) {
+      if (lane == 0) item_fail(a, c);
+      return;
+    }
+  }
+  const int64_t lo = a.off[row], hi = a.off[row + 1];
+  if (!(lo >= 0 && hi >= lo && hi <= a.n_pred && hi - lo <= (1LL << 30))) {
+    if (lane == 0) item_fail(a, c);
+    return;
+  }
+  const int n = (int)(hi - lo);
+  if (n == 0) {            // no predecessors: the task's group is its application
+    if (lane == 0) { a.mode_host[c] = -1; a.anchor_zone[c] = -1; }
+    return;
+  }
+  if (n > ANC_WLDS) {
+    if (lane == 0) a.deferred[atomicAdd(a.n_deferred, 1)] = c;
+    return;
+  }
+  bool ok = true;
+  uint64_t best = 0;
+  if (n <= 64) {
+    const uint32_t k = lane < n ? (uint32_t)(entry_host(a, lo + lane, &ok) + 1) : 0xffffffffu;
+    if (__ballot(!ok)) {
+      if (lane == 0) item_fail(a, c);
+      return;
+    }
+    uint32_t cnt = 0, first = 0xffffffffu;
+    for (int j = 0; j < n; ++j) {
+      const uint32_t kj = (uint32_t)__shfl((int)k, j, 64);
+      if (kj == k) {
+        ++cnt;
+        first = first < (uint32_t)j ? first : (uint32_t)j;
+      }
+    }
+    if (lane < n) best = ((uint64_t)cnt << 32) | (uint64_t)(0xffffffffu - first);
+  } else {
+    uint64_t* buf = lds[wave];
+    int m = 64;
+    while (m < n) m <<= 1;
+    for (int i = lane; i < m; i += 64) {
+      uint64_t k = ~0ull;
+      if (i < n) k = ((uint64_t)(uint32_t)(entry_host(a, lo + i, &ok) + 1) << 32) | (uint32_t)i;
+      buf[i] = k;
+    }
+    if (__ballot(!ok)) {
+      if (lane == 0) item_fail(a, c);
+      return;
+    }
+    wave_sync();
+    for (int k = 2; k <= m; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = lane; i < m; i += 64) {
+          const int l = i ^ j;
+          if (l > i) {
+            const uint64_t x = buf[i], y = buf[l];
+            const bool up = (i & k) == 0;
+            if (up ? x > y : x < y) { buf[i] = y; buf[l] = x; }
+          }
+        }
+        wave_sync();
+      }
+    }
+    for (int i = lane; i < n; i += 64) {
+      const uint32_t key_hi = (uint32_t)(buf[i] >> 32);
+      if (i + 1 < n && (uint32_t)(buf[i + 1] >> 32) == key_hi) continue;
+      const uint64_t target = (uint64_t)key_hi << 32;
+      int s = 0, e = i;
+      while (s < e) {
+        const int mid = (s + e) >> 1;
+        if (buf[mid] < target) s = mid + 1; else e = mid;
+      }
+      const uint32_t first = (uint32_t)buf[s];
+      const uint64_t v = ((uint64_t)(uint32_t)(i - s + 1) << 32) | (uint64_t)(0xffffffffu - first);
+      best = v > best ? v : best;
+    }
+  }
+  best = wave_max_u64(best);
+  if (lane == 0) {
+    const uint32_t first = 0xffffffffu - (uint32_t)best;
+    bool ok2 = true;
+    const int h = entry_host(a, lo + first, &ok2);
+    a.mode_host[c] = h;
+    a.anchor_zone[c] = h >= 0 ? a.zone[h] : -2;
+  }
+}
+
 void launch_anchor(const AnchorArgs& a, hipStream_t st) {
   if (a.C <= 0) return;
-  anchor_kernel<<<a.C, ANC_THREADS, 0, st>>>(a);
+  constexpr int IPB = ANC_THREADS / 64;
+  anchor_wave_kernel<<<(a.C + IPB - 1) / IPB, ANC_THREADS, 0, st>>>(a);
+  anchor_block_kernel<<<a.C < 256 ? a.C : 256, ANC_THREADS, 0, st>>>(a);
 }
 
 }  // namespace pvt

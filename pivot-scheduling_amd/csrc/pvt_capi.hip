@@ -745,11 +745,11 @@ extern "C" int pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a) {
       (a->inst_host == nullptr) != (a->n_inst == 0) || (a->item == nullptr) != (a->n_rows == 0))
     return fail(ctx, PVT_EINVAL, "null pointer in pvt_anchor_args");
   (void)hipSetDevice(ctx->device);
-  ENSURE(ctx->anc_scr, 16);
-  int32_t* bad = P<int32_t>(ctx->anc_scr);
-  HIPCHK(hipMemsetAsync(bad, 0, sizeof(int32_t), ctx->stream));
+  ENSURE(ctx->anc_scr, 16 + sizeof(int32_t) * (size_t)a->n_items);
+  int32_t* bad = P<int32_t>(ctx->anc_scr);   // [0] bad items, [1] deferred count, [4..] list
+  HIPCHK(hipMemsetAsync(bad, 0, 16, ctx->stream));
   AnchorArgs k{a->n_items, a->n_hosts, a->n_pred, a->n_inst, a->n_rows, a->off, a->item,
-               a->list, a->inst_host, a->zone, a->mode_host, a->anchor_zone, bad};
+               a->list, a->inst_host, a->zone, a->mode_host, a->anchor_zone, bad, bad + 4, bad + 1};
   {
     Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * (double)a->n_pred);
     launch_anchor(k, ctx->stream);

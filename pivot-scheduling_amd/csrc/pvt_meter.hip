@@ -1,12 +1,13 @@
 // pvt_meter.hip — Meter aggregates of a batch of scenarios (SURVEY.md §8(f) rank 4;
 // reference resources/meter.py:31-53, resources/__init__.py:565-569).
 //
-// One 256-thread workgroup per scenario. Each thread folds whole hosts / routes sequentially,
-// in the reference's nesting (per host: the sum of its intervals; per route: the sum over its
-// packets of the sum of their transfer sizes, then cost * size / 8000), and the block sums the
-// per-thread partials in a fixed tree. Only the cross-host / cross-route order differs from
-// the reference's left-to-right sum (fp64; the north star's 1e-9 relative bound holds by a wide
-// margin: all terms are non-negative). HBM-bound streaming reduction, no MFMA.
+// One 256-thread workgroup per scenario, in the reference's nesting: per host the sum of its
+// intervals (a thread per host, intervals in order); per route (a wave per route, lanes over
+// its packets so the packet / transfer arrays stream coalesced) the sum of its packets' transfer
+// sizes, then cost * size / 8000; the block sums the partials in a fixed tree. Only the order
+// across hosts, across a route's packets and across routes differs from the reference's
+// left-to-right sums (fp64; the north star's 1e-9 relative bound holds by a wide margin: all
+// terms are non-negative). HBM-bound streaming reduction, no MFMA.
 #include <hip/hip_runtime.h>
 
 #include "pvt_meter.h"
@@ -51,26 +52,36 @@ __global__ void __launch_bounds__(MET_THREADS) meter_kernel(MeterArgs a) {
   } else {
     ok = false;
   }
-  // total_network_traffic_cost and average_congestion_delay
+  // total_network_traffic_cost and average_congestion_delay: one wave per route, lanes over
+  // its packets (coalesced), each lane folding its packet's transfers in order
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   double cost = 0.0, delay = 0.0, npk = 0.0;
   int64_t r0, r1;
   if (range_ok(a.route_off, s, a.n_scen, a.n_routes, &r0, &r1)) {
-    for (int64_t r = r0 + threadIdx.x; r < r1; r += MET_THREADS) {
+    for (int64_t r = r0 + wave; r < r1; r += MET_THREADS / 64) {
       int64_t p0, p1;
       if (!range_ok(a.pkt_off, r, a.n_routes, a.n_pkts, &p0, &p1)) { ok = false; continue; }
-      double size = 0.0;
-      for (int64_t p = p0; p < p1; ++p) {
+      double size = 0.0, dl = 0.0;
+      for (int64_t p = p0 + lane; p < p1; p += 64) {
         int64_t t0, t1;
-        if (!range_ok(a.tr_off, p, a.n_pkts, a.n_tr, &t0, &t1)) { ok = false; break; }
+        if (!range_ok(a.tr_off, p, a.n_pkts, a.n_tr, &t0, &t1)) { ok = false; continue; }
         double ps = 0.0;
         for (int64_t t = t0; t < t1; ++t) {
           ps += a.tr_size[t];
-          if (t > t0) delay += a.tr_start[t] - a.tr_end[t - 1];
+          if (t > t0) dl += a.tr_start[t] - a.tr_end[t - 1];
         }
         size += ps;
       }
-      cost += a.route_cost[r] * size / 8000.0;
-      npk += (double)(p1 - p0);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        size += __shfl_xor(size, o, 64);
+        dl += __shfl_xor(dl, o, 64);
+      }
+      if (lane == 0) {
+        cost += a.route_cost[r] * size / 8000.0;
+        delay += dl;
+        npk += (double)(p1 - p0);
+      }
     }
   } else {
     ok = false;

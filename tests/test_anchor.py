@@ -125,17 +125,36 @@ def test_gpu_anchor_random(engine, max_len, n_items, H):
 
 @pytest.mark.gpu
 def test_gpu_anchor_distinct_hosts_long_list(engine):
-    """All-distinct lists (every count 1: the first entry wins) across the LDS/scratch edge."""
+    """All-distinct lists (every count 1: the first entry wins) across every path edge:
+    registers (<= 64), wave LDS sort (<= 1024), block LDS sort (<= 8192), LDS histograms."""
     H = 1 << 20
     zone = (np.arange(H) % 20).astype(np.int32)
     rng = np.random.default_rng(11)
-    lens = [1, 2, 4095, 4096, 4097, 9000, 70000]
+    lens = [1, 2, 63, 64, 65, 1023, 1024, 1025, 4095, 4096, 4097, 8192, 8193, 9000, 70000]
     off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
     lst = np.concatenate([rng.permutation(H)[:n] for n in lens]).astype(np.int32)
     want = oracle.anchor(off, lst, zone, H)
     got = engine.anchor(off, lst, zone)
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[0], lst[off[:-1]])
     assert np.array_equal(got[1], want[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [64, 65, 700, 1024, 1025, 3000, 8192, 8193, 20000])
+def test_gpu_anchor_tied_lists(engine, n):
+    """Every path with heavy ties: two hosts with equal counts, the later-seen one sorted first
+    by host index (the first-seen one must win), plus unplaced entries."""
+    H = 5000
+    zone = (np.arange(H) % 31).astype(np.int32)
+    rng = np.random.default_rng(n)
+    base = np.where(np.arange(n) % 2 == 0, 4000, 7).astype(np.int32)   # 4000 seen first
+    base[rng.random(n) < 0.1] = -1
+    rng.shuffle(base[1:])
+    off = np.array([0, n, 2 * n], dtype=np.int64)
+    lst = np.concatenate([base, base[::-1]]).astype(np.int32)
+    want = oracle.anchor(off, lst, zone, H)
+    got = engine.anchor(off, lst, zone)
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
 
 
 @pytest.mark.gpu
