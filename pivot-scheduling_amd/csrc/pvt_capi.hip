@@ -45,6 +45,7 @@ struct RoundState {
   bool active = false;
   int T = 0, H = 0, Z = 0, lo = 0, hi = 0, world = 0;
   bool keyed = false, ordered = false;
+  bool kscan = false;             // keyed first-fit lists from the per-group sorted order
   int32_t* ord = nullptr;         // processing order (ctx scratch)
   std::vector<int> gstart, ganchor;
   size_t g = 0, ngroups = 0;
@@ -69,8 +70,9 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr;
+      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, kskey, kperm, kiota, ksorttmp;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
+  int keyed_scan = 1;             // keyed first-fit: sorted host order + early-exit scan
   int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
   std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
   std::vector<uint32_t> rmt_host;
@@ -200,7 +202,8 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
-                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr};
+                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
+                 &ctx->ksorttmp};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -288,6 +291,8 @@ static int choose_segments(int H, int nt) {
   if (S >= 8) S = S / 8 * 8;
   return S;
 }
+// keyed first-fit scan depth: entries per task list (deeper lists, fewer refills)
+static constexpr int KSCAN_DEPTH = 256;
 static double bytes_per_candidate(int mode) {
   // cost_aware 36 B (4 x fp64 avail + int32 zone); vbp best-fit 36 B
   // (+ host-id rank); opportunistic / vbp first-fit 32 B.
@@ -443,6 +448,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
 
   // group boundaries in processing order (only cost_aware first-fit with sort_hosts needs them)
   R.keyed = r->mode == PVT_CA_FF && r->sort_hosts;
+  R.kscan = false;
   R.ordered = (r->mode == PVT_VBP_FF) || (r->mode == PVT_CA_FF && !r->sort_hosts);
   if (R.keyed) {
     std::vector<int32_t> tg(T), ga;
@@ -469,6 +475,20 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
       R.ganchor.push_back(0);
     }
     ENSURE(ctx->key, sizeof(double) * H);
+    R.kscan = ctx->keyed_scan != 0;
+    if (const char* e = getenv("PVT_KEYED_SCAN")) R.kscan = atoi(e) != 0;   // A/B experiments
+    if (R.kscan && hi > lo) {
+      const int n = hi - lo;
+      ENSURE(ctx->kskey, sizeof(uint64_t) * 2 * (size_t)std::max(n, 1));
+      ENSURE(ctx->kperm, sizeof(int32_t) * (size_t)std::max(n, 1));
+      ENSURE(ctx->kiota, sizeof(int32_t) * (size_t)std::max(n, 1));
+      size_t tmp = 0;
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<uint64_t>(ctx->kskey),
+                                                P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kiota),
+                                                P<int32_t>(ctx->kperm), n, 0, 64, st));
+      ENSURE(ctx->ksorttmp, tmp);
+      launch_iota(P<int32_t>(ctx->kiota), n, st);
+    }
   }
   R.gstart.push_back(T);
   R.ngroups = R.keyed ? R.ganchor.size() : 1;
@@ -517,6 +537,14 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
                R.ganchor[R.g], R.lo, R.hi, P<double>(ctx->key)};
     Scope sc(ctx, PVT_K_OTHER, 0, 0);
     launch_key(ka, ctx->stream);
+    if (R.kscan) {   // the group's host order (cost_aware.py:118-119), stable radix sort
+      const int n = R.hi - R.lo;
+      size_t tmp = ctx->ksorttmp.n;
+      const uint64_t* kin = reinterpret_cast<const uint64_t*>(P<double>(ctx->key) + R.lo);
+      HIPCHK(hipcub::DeviceRadixSort::SortPairs(P<void>(ctx->ksorttmp), tmp, kin,
+                                                P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kiota),
+                                                P<int32_t>(ctx->kperm), n, 0, 64, ctx->stream));
+    }
     R.key_group = (int)R.g;
   }
   R.nt = std::min(R.W, ge - R.t0);
@@ -536,7 +564,13 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
   const double bpc = bytes_per_candidate(r->mode);
   const double* dem_w = P<double>(ctx->dem_ord) + (size_t)t0 * 4;
   const int32_t* anc_w = P<int32_t>(ctx->anc_ord) + t0;
-  if (R.ordered) {
+  if (R.kscan) {
+    const int n = R.hi - R.lo;
+    PermArgs pa{r->avail, r->zone, P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kperm), dem_w,
+                anc_w, R.ord + t0, R.H, nt, n, KSCAN_DEPTH, R.lo, L};
+    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
+    launch_perm_scan(pa, st);
+  } else if (R.ordered) {
     OrderedArgs oa{r->avail, r->zone, dem_w, anc_w, R.ord + t0, R.H, nt,
                    r->mode == PVT_CA_FF ? 1 : 0, R.lo, R.hi, L};
     Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);

@@ -136,6 +136,24 @@ struct CommitArgs {
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
 };
 
+// cost_aware first-fit with sort_hosts, as the reference runs it (cost_aware.py:118-124): the
+// hosts sorted once per group by the frozen key (perm, skey = sorted key bits; the radix sort
+// is stable, so equal keys keep host order), then per task the first `depth` snapshot-feasible
+// hosts in that order. Lists come out exactly as merge_kernel would build them: sorted by
+// (key, 0, host), cnt, complete, and a bound every unlisted host ranks at or after.
+struct PermArgs {
+  const double* avail;
+  const int32_t* zone;
+  const uint64_t* skey;   // [n] sorted key bits
+  const int32_t* perm;    // [n] host at each sorted position, minus h_lo
+  const double* dem;      // window tasks [nt][4]
+  const int32_t* anc;
+  const int32_t* ord;
+  int H, nt, n, depth;    // depth <= LMAX
+  int h_lo;               // first host of the sorted range (a rank's shard; 0 unsharded)
+  Lists L;
+};
+
 struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw)
   const double* avail;
   const int32_t* zone;
@@ -151,6 +169,7 @@ void launch_score(int mode, const ScoreArgs& a, hipStream_t st);
 void launch_merge(const MergeArgs& a, hipStream_t st);
 void launch_pack(const PackArgs& a, hipStream_t st);
 void launch_ordered(const OrderedArgs& a, hipStream_t st);
+void launch_perm_scan(const PermArgs& a, hipStream_t st);
 void launch_commit(const CommitArgs& a, hipStream_t st);
 void launch_key(const KeyArgs& a, hipStream_t st);
 void launch_zone_tables(const double* cost, const double* bw, int Z, double* csum, double* bsum,

@@ -462,6 +462,61 @@ void launch_ordered(const OrderedArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL(ordered_kernel<false>, grid, block, 0, st, a);
 }
 
+// One wave per task: walk the group's sorted host order 64 positions at a time (perm and key
+// loads coalesced, host state gathered), keep the first `depth` strictly feasible hosts.
+__global__ __launch_bounds__(256) void perm_scan_kernel(PermArgs A) {
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int task = blockIdx.x * 4 + wave;
+  if (task >= A.nt) return;
+  const double* dp = A.dem + (size_t)task * 4;
+  const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int cnt = 0, p_next = A.n;      // p_next: first sorted position after the last listed host
+  int pb = 0;
+  for (; pb < A.n && cnt < A.depth; pb += WAVE) {
+    const int p = pb + lane;
+    const bool ok = p < A.n;
+    const int h = ok ? A.h_lo + A.perm[p] : 0;
+    const double a0 = ok ? A.avail[h] : -DINF;
+    const double a1 = ok ? A.avail[(size_t)A.H + h] : -DINF;
+    const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : -DINF;
+    const double a3 = ok ? A.avail[3 * (size_t)A.H + h] : -DINF;
+    const bool fit = ok && fits<true>(a0, a1, a2, a3, d0, d1, d2, d3);
+    const uint64_t m = __ballot(fit);
+    const int pos = cnt + __popcll(m & below);
+    if (fit && pos < A.depth) {
+      ListEntry e;
+      e.s = __longlong_as_double((long long)A.skey[p]); e.tb = 0; e.id = h;
+      e.zone = A.zone[h]; e.pad = 0; e.pad2 = 0.0;
+      e.a[0] = a0; e.a[1] = a1; e.a[2] = a2; e.a[3] = a3;
+      A.L.e[(size_t)task * LMAX + pos] = e;
+      A.L.ids[(size_t)task * LMAX + pos] = h;
+      if (pos == A.depth - 1) p_next = p + 1;      // one lane at most
+    }
+    cnt += __popcll(m);
+  }
+  p_next = (int)wave_min_u64((uint64_t)(uint32_t)p_next);
+  if (lane < 4) reinterpret_cast<double*>(&A.L.t[task])[lane] = dp[lane];
+  if (lane == 0) {
+    TaskRec& r = A.L.t[task];
+    const bool complete = pb >= A.n && cnt <= A.depth;   // every feasible host is listed
+    r.cnt = complete ? cnt : A.depth;
+    r.complete = complete;
+    r.anc = A.anc ? A.anc[task] : 0;
+    r.ord = A.ord[task];
+    if (complete || p_next >= A.n) {
+      r.bs = DINF; r.btb = 0xffffffffu; r.bid = 0x7fffffff;
+    } else {
+      r.bs = __longlong_as_double((long long)A.skey[p_next]); r.btb = 0;
+      r.bid = A.h_lo + A.perm[p_next];
+    }
+  }
+}
+
+void launch_perm_scan(const PermArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(perm_scan_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+}
+
 // ------------------------------------------------------------------------------------------
 // Small kernels: zone tables, frozen first-fit keys, a2 sort keys, gathers.
 // ------------------------------------------------------------------------------------------
