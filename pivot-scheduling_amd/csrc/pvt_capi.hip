@@ -14,6 +14,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <limits>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -46,6 +47,9 @@ struct RoundState {
   int T = 0, H = 0, Z = 0, lo = 0, hi = 0, world = 0;
   bool keyed = false, ordered = false;
   bool kscan = false;             // keyed first-fit lists from the per-group sorted order
+  int kmode = 0;                  // 1: zero-key prefix in host order, 2: full sort
+  int kn = 0;                     // hosts in the current order (prefix length in mode 1)
+  bool kstall = false;            // a walk found a prefix list exhausted: sort the rest
   int32_t* ord = nullptr;         // processing order (ctx scratch)
   std::vector<int> gstart, ganchor;
   size_t g = 0, ngroups = 0;
@@ -70,7 +74,7 @@ struct pvt_ctx {
   std::vector<TimedLaunch> pending;
   // scratch
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
-      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, kskey, kperm, kiota, ksorttmp;
+      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, kskey, kperm, kiota, ksorttmp, kflag;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
   int keyed_scan = 1;             // keyed first-fit: sorted host order + early-exit scan
   int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
@@ -203,7 +207,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
-                 &ctx->ksorttmp};
+                 &ctx->ksorttmp, &ctx->kflag};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -293,6 +297,8 @@ static int choose_segments(int H, int nt) {
 }
 // keyed first-fit scan depth: entries per task list (deeper lists, fewer refills)
 static constexpr int KSCAN_DEPTH = 256;
+// zero-key prefix used alone (no sort) when it holds at least this many hosts
+static constexpr int KPREFIX_MIN = 1024;
 static double bytes_per_candidate(int mode) {
   // cost_aware 36 B (4 x fp64 avail + int32 zone); vbp best-fit 36 B
   // (+ host-id rank); opportunistic / vbp first-fit 32 B.
@@ -449,6 +455,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   // group boundaries in processing order (only cost_aware first-fit with sort_hosts needs them)
   R.keyed = r->mode == PVT_CA_FF && r->sort_hosts;
   R.kscan = false;
+  R.kmode = 0; R.kn = 0; R.kstall = false;
   R.ordered = (r->mode == PVT_VBP_FF) || (r->mode == PVT_CA_FF && !r->sort_hosts);
   if (R.keyed) {
     std::vector<int32_t> tg(T), ga;
@@ -475,6 +482,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
       R.ganchor.push_back(0);
     }
     ENSURE(ctx->key, sizeof(double) * H);
+    ENSURE(ctx->next, sizeof(int32_t) * 4);
     R.kscan = ctx->keyed_scan != 0;
     if (const char* e = getenv("PVT_KEYED_SCAN")) R.kscan = atoi(e) != 0;   // A/B experiments
     if (R.kscan && hi > lo) {
@@ -486,7 +494,12 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
       HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, P<uint64_t>(ctx->kskey),
                                                 P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kiota),
                                                 P<int32_t>(ctx->kperm), n, 0, 64, st));
-      ENSURE(ctx->ksorttmp, tmp);
+      size_t tmp2 = 0;
+      HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, tmp2, P<int32_t>(ctx->kiota),
+                                           P<uint8_t>(ctx->kflag), P<int32_t>(ctx->kperm),
+                                           P<int32_t>(ctx->next) + 2, n, st));
+      ENSURE(ctx->ksorttmp, std::max(tmp, tmp2));
+      ENSURE(ctx->kflag, (size_t)n);
       launch_iota(P<int32_t>(ctx->kiota), n, st);
     }
   }
@@ -523,6 +536,20 @@ static int group_end(const RoundState& R, int t0) {
   return g < R.ngroups ? R.gstart[g + 1] : R.T;
 }
 
+// Full stable radix sort of the frozen keys of this context's hosts (cost_aware.py:118-119).
+static int keyed_full_sort(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const int n = R.hi - R.lo;
+  size_t tmp = ctx->ksorttmp.n;
+  const uint64_t* kin = reinterpret_cast<const uint64_t*>(P<double>(ctx->key) + R.lo);
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(P<void>(ctx->ksorttmp), tmp, kin,
+                                            P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kiota),
+                                            P<int32_t>(ctx->kperm), n, 0, 64, ctx->stream));
+  R.kmode = 2;
+  R.kn = n;
+  return PVT_OK;
+}
+
 // Size of the next window at R.t0 (0: the round is done). Computes the frozen first-fit key of
 // this context's hosts at a group start (cost_aware.py:118-119, on the current capacities).
 static int round_next_window(pvt_ctx* ctx, int* nt_out) {
@@ -532,18 +559,38 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
   while (R.g < R.ngroups && R.t0 >= (R.keyed ? R.gstart[R.g + 1] : R.T)) R.g++;
   if (R.g >= R.ngroups || R.T == 0) return PVT_OK;
   const int ge = R.keyed ? R.gstart[R.g + 1] : R.T;
+  int rc = 0;
+  if (R.kstall) {                 // same group, frozen keys: complete the order
+    R.kstall = false;
+    if (R.key_group == (int)R.g && R.kmode == 1 && (rc = keyed_full_sort(ctx))) return rc;
+  }
   if (R.keyed && R.key_group != (int)R.g && R.hi > R.lo) {
     KeyArgs ka{R.r.avail, R.r.zone, R.r.decay, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z,
                R.ganchor[R.g], R.lo, R.hi, P<double>(ctx->key)};
     Scope sc(ctx, PVT_K_OTHER, 0, 0);
     launch_key(ka, ctx->stream);
-    if (R.kscan) {   // the group's host order (cost_aware.py:118-119), stable radix sort
+    if (R.kscan) {
+      // The group's host order (cost_aware.py:118-119). Hosts of zero key (the anchor zone's:
+      // no egress cost) come first, in host order; when there are enough of them the rest is
+      // sorted only if a walk ever exhausts that prefix (kstall).
       const int n = R.hi - R.lo;
+      const double* kin = P<double>(ctx->key) + R.lo;
+      launch_zero_key_flags(kin, n, P<uint8_t>(ctx->kflag), ctx->stream);
       size_t tmp = ctx->ksorttmp.n;
-      const uint64_t* kin = reinterpret_cast<const uint64_t*>(P<double>(ctx->key) + R.lo);
-      HIPCHK(hipcub::DeviceRadixSort::SortPairs(P<void>(ctx->ksorttmp), tmp, kin,
-                                                P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kiota),
-                                                P<int32_t>(ctx->kperm), n, 0, 64, ctx->stream));
+      HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(ctx->ksorttmp), tmp, P<int32_t>(ctx->kiota),
+                                           P<uint8_t>(ctx->kflag), P<int32_t>(ctx->kperm),
+                                           P<int32_t>(ctx->next) + 2, n, ctx->stream));
+      HIPCHK(hipMemcpyAsync(ctx->next_host + 2, P<int32_t>(ctx->next) + 2, sizeof(int32_t),
+                            hipMemcpyDeviceToHost, ctx->stream));
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      const int nz = ctx->next_host[2];
+      if (nz >= KPREFIX_MIN && nz < n) {
+        R.kmode = 1;
+        R.kn = nz;
+        HIPCHK(hipMemsetAsync(P<uint64_t>(ctx->kskey) + n, 0, sizeof(uint64_t) * nz, ctx->stream));
+      } else {
+        if ((rc = keyed_full_sort(ctx))) return rc;
+      }
     }
     R.key_group = (int)R.g;
   }
@@ -567,7 +614,8 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
   if (R.kscan) {
     const int n = R.hi - R.lo;
     PermArgs pa{r->avail, r->zone, P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kperm), dem_w,
-                anc_w, R.ord + t0, R.H, nt, n, KSCAN_DEPTH, R.lo, L};
+                anc_w, R.ord + t0, R.H, nt, n > 0 ? R.kn : 0, KSCAN_DEPTH, R.lo,
+                R.kmode == 1 ? 1 : 0, std::numeric_limits<double>::denorm_min(), L};
     Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
     launch_perm_scan(pa, st);
   } else if (R.ordered) {
@@ -631,7 +679,13 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
   *adv = ctx->next_host[0];
   if (*adv == -1) return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out at task %d", t0);
   if (*adv < 0 || *adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", *adv, nt);
-  if (*adv == 0 && !inherited) return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
+  if (*adv == 0 && !inherited) {
+    if (ctx->rs.kscan && ctx->rs.kmode == 1) {   // a zero-key prefix ran dry: sort the rest
+      ctx->rs.kstall = true;
+      return PVT_OK;
+    }
+    return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", t0);
+  }
   return PVT_OK;
 }
 

@@ -151,6 +151,8 @@ struct PermArgs {
   const int32_t* ord;
   int H, nt, n, depth;    // depth <= LMAX
   int h_lo;               // first host of the sorted range (a rank's shard; 0 unsharded)
+  int partial;            // perm is a prefix of the order: every other host's key >= rest_s
+  double rest_s;
   Lists L;
 };
 
@@ -170,6 +172,7 @@ void launch_merge(const MergeArgs& a, hipStream_t st);
 void launch_pack(const PackArgs& a, hipStream_t st);
 void launch_ordered(const OrderedArgs& a, hipStream_t st);
 void launch_perm_scan(const PermArgs& a, hipStream_t st);
+void launch_zero_key_flags(const double* key, int n, uint8_t* flags, hipStream_t st);
 void launch_commit(const CommitArgs& a, hipStream_t st);
 void launch_key(const KeyArgs& a, hipStream_t st);
 void launch_zone_tables(const double* cost, const double* bw, int Z, double* csum, double* bsum,

@@ -499,18 +499,31 @@ __global__ __launch_bounds__(256) void perm_scan_kernel(PermArgs A) {
   if (lane < 4) reinterpret_cast<double*>(&A.L.t[task])[lane] = dp[lane];
   if (lane == 0) {
     TaskRec& r = A.L.t[task];
-    const bool complete = pb >= A.n && cnt <= A.depth;   // every feasible host is listed
-    r.cnt = complete ? cnt : A.depth;
+    const bool complete = pb >= A.n && cnt <= A.depth && !A.partial;   // all feasible listed
+    r.cnt = cnt < A.depth ? cnt : A.depth;
     r.complete = complete;
     r.anc = A.anc ? A.anc[task] : 0;
     r.ord = A.ord[task];
-    if (complete || p_next >= A.n) {
+    if (complete) {
       r.bs = DINF; r.btb = 0xffffffffu; r.bid = 0x7fffffff;
+    } else if (p_next >= A.n) {     // the whole prefix is listed: the rest rank after it
+      r.bs = A.partial ? A.rest_s : DINF; r.btb = A.partial ? 0u : 0xffffffffu;
+      r.bid = A.partial ? 0 : 0x7fffffff;
     } else {
       r.bs = __longlong_as_double((long long)A.skey[p_next]); r.btb = 0;
       r.bid = A.h_lo + A.perm[p_next];
     }
   }
+}
+
+__global__ void zero_key_flags_kernel(const uint64_t* key, int n, uint8_t* flags) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = key[i] == 0ull;
+}
+void launch_zero_key_flags(const double* key, int n, uint8_t* flags, hipStream_t st) {
+  if (n > 0)
+    hipLaunchKernelGGL(zero_key_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, st,
+                       reinterpret_cast<const uint64_t*>(key), n, flags);
 }
 
 void launch_perm_scan(const PermArgs& a, hipStream_t st) {

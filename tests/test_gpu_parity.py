@@ -142,3 +142,25 @@ def test_pipelined_crowded_small_windows(engine, mode, window):
         engine.set_window(0)
         engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
     _assert_same(res, ref.placement, ref.order, ref.avail)
+
+
+@pytest.mark.parametrize("pipeline", [True, False])
+@pytest.mark.parametrize("H,cpus", [(30000, 1.0), (25000, 1.5), (1500, 2.0)])
+def test_keyed_first_fit_zero_key_prefix_runs_dry(engine, pipeline, H, cpus):
+    """cost_aware first-fit with sort_hosts, one group: the anchor zone's hosts (key 0, listed
+    first in host order without a sort) fill up, walks stop on empty prefix lists, and the
+    engine completes the order with the full sort mid-group; placements equal the oracle's."""
+    r = synthetic.make_round(_abi.PVT_CA_FF, H, 5000, seed=17)
+    r.task_group = np.zeros(r.n_tasks, dtype=np.int32)
+    r.group_anchor = np.array([3], dtype=np.int32)
+    r.avail[0, :] = cpus
+    ref = oracle.place(r)
+    try:
+        engine.set_resident(0)
+        engine.set_pipeline(pipeline)
+        res = engine.place(r)
+    finally:
+        engine.set_pipeline(True)
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+    assert (ref.placement >= 0).sum() > 0
+    _assert_same(res, ref.placement, ref.order, ref.avail)
