@@ -132,3 +132,17 @@ def test_two_process_group_on_one_gpu(mode):
     for k in range(2):
         assert got[k][0] == ref.placement.tolist()
         assert got[k][1] == ref.avail.tobytes()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+def test_sharded_keyed_prefix_runs_dry(engines, world):
+    """Keyed first-fit, one group: every rank's zero-key prefix (the anchor zone's hosts of its
+    range, listed without a sort) fills up, the replicated walk stops on empty lists, and every
+    rank completes its order with the full sort; all ranks equal the oracle."""
+    r = synthetic.make_round(_abi.PVT_CA_FF, 60000, 4000, seed=19)
+    r.task_group = np.zeros(r.n_tasks, dtype=np.int32)
+    r.group_anchor = np.array([5], dtype=np.int32)
+    r.avail[0, :] = 1.0
+    ref = oracle.place(r)
+    assert (ref.placement >= 0).sum() > 0
+    _assert_same(_lockstep(engines, world, r), ref)
