@@ -379,7 +379,10 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   hipStream_t st = ctx->stream;
   // Window: the walk rescans the window's touched hosts for every task, so short windows keep
   // that scan short; the count pass then spreads each window over more host segments.
-  const int W = std::max(1, std::min(ctx->window > 0 ? ctx->window : OPP_WINDOW_DEFAULT, OPP_MAXW));
+  // (bench sweep at 1M hosts x 10k tasks, DESIGN.md §5: pipelined 64 -> 34.6 ms, 128 -> 35.6,
+  // 192 -> 39.7, 256 -> 42.8; sequential 256 -> 39.2)
+  const int wdef = ctx->pipeline ? OPP_WINDOW_PIPE : OPP_WINDOW_DEFAULT;
+  const int W = std::max(1, std::min(ctx->window > 0 ? ctx->window : wdef, OPP_MAXW));
   const int nq = (H + OPP_CH - 1) / OPP_CH, nsq = (nq + OPP_SUP - 1) / OPP_SUP;
   const int task_waves = (std::min(W, std::max(T, 1)) + OPP_TW - 1) / OPP_TW;
   int S = std::max(1, std::min(nsq, (4096 + task_waves - 1) / task_waves));
@@ -389,26 +392,54 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord),
                       P<int32_t>(ctx->anc_ord), st);
+  // Pipelined windows (W <= OPP_MAXW / 2, so a walk's inherited + own touched hosts fit its
+  // LDS): window k+1's count pass runs on the side stream while window k is walked. Walk k
+  // leaves global availability untouched and hands its hosts to walk k+1, which applies them
+  // on entry and then releases count k+2; so every count pass reads the capacities its walk's
+  // predecessor started from, and the hosts that walk touched are touched for the next walk.
+  const int nwin = (T + W - 1) / W;
+  const bool pipe = ctx->pipeline && nwin > 1 && W <= OPP_MAXW / 2;
+  const int nbuf = pipe ? 2 : 1;
   const size_t bm_bytes = sizeof(uint64_t) * 4 * (size_t)nq * W;
-  ENSURE(ctx->opp, bm_bytes + sizeof(int32_t) * (size_t)nsq * W + sizeof(uint32_t) * 640);
-  uint64_t* bm = reinterpret_cast<uint64_t*>(ctx->opp.p);
-  int32_t* sc = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(ctx->opp.p) + bm_bytes);
-  uint32_t* mt = reinterpret_cast<uint32_t*>(sc + (size_t)nsq * W);
+  const size_t sc_bytes = sizeof(int32_t) * (size_t)nsq * W;
+  const size_t tl_bytes = pipe ? sizeof(OppTouched) : 0;
+  const size_t slot = (bm_bytes + sc_bytes + tl_bytes + 255) / 256 * 256;
+  ENSURE(ctx->opp, slot * nbuf + sizeof(uint32_t) * 640);
+  char* base = reinterpret_cast<char*>(ctx->opp.p);
+  auto bm_of = [&](int b) { return reinterpret_cast<uint64_t*>(base + slot * b); };
+  auto sc_of = [&](int b) { return reinterpret_cast<int32_t*>(base + slot * b + bm_bytes); };
+  auto tl_of = [&](int b) { return reinterpret_cast<OppTouched*>(base + slot * b + bm_bytes + sc_bytes); };
+  uint32_t* mt = reinterpret_cast<uint32_t*>(base + slot * nbuf);
   HIPCHK(hipMemcpyAsync(mt, r->mt_state, sizeof(uint32_t) * 625, hipMemcpyHostToDevice, st));
   const double bpc = bytes_per_candidate(r->mode);
-  for (int t0 = 0; t0 < T; t0 += W) {
-    const int nt = std::min(W, T - t0);
+  auto count = [&](int k, hipStream_t s) {
+    const int t0 = k * W, nt = std::min(W, T - t0);
+    OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, S, seg_sup, nq, nsq,
+                    W, bm_of(k % nbuf), sc_of(k % nbuf)};
+    Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc, s);
+    launch_opp_count(ca, s);
+  };
+  if (nwin > 0) count(0, st);
+  for (int k = 0; k < nwin; k++) {
+    const int t0 = k * W, nt = std::min(W, T - t0);
+    const bool next = pipe && k + 1 < nwin;
     ctx->windows++;
-    OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, S, seg_sup, nq, nsq, W,
-                    bm, sc};
-    {
-      Scope s(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc);
-      launch_opp_count(ca, st);
+    const uint32_t seq = ++ctx->walk_seq;
+    if (next) {
+      HIPCHK(hipStreamWaitValue32(ctx->side, ctx->walk_flag, seq, hipStreamWaitValueGte, 0xffffffffu));
+      count(k + 1, ctx->side);
+      HIPCHK(hipEventRecord(ctx->ev_lists, ctx->side));
     }
-    OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm, sc, H, nt, nq, nsq, W,
-                     r->placement + t0, mt, ctx->stamps};
-    Scope s(ctx, PVT_K_COMMIT, 0, 0);
-    launch_opp_commit(oa, st);
+    OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm_of(k % nbuf),
+                     sc_of(k % nbuf), H, nt, nq, nsq, W, r->placement + t0, mt, ctx->stamps,
+                     (pipe && k > 0) ? tl_of((k - 1) % nbuf) : nullptr,
+                     next ? tl_of(k % nbuf) : nullptr, next ? 0 : 1,
+                     next ? ctx->walk_flag : nullptr, seq};
+    {
+      Scope s(ctx, PVT_K_COMMIT, 0, 0);
+      launch_opp_commit(oa, st);
+    }
+    if (next) HIPCHK(hipStreamWaitEvent(st, ctx->ev_lists, 0));
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(r->mt_state, mt, sizeof(uint32_t) * 625, hipMemcpyDeviceToHost, st));

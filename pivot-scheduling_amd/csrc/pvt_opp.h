@@ -17,14 +17,25 @@ constexpr int OPP_CH = 256;     // hosts per chunk
 constexpr int OPP_SUP = 64;     // chunks per super-chunk (16384 hosts)
 constexpr int OPP_TW = 8;       // tasks per wave in the count kernel
 constexpr int OPP_MAXW = 1024;  // tasks per window (commit-walk LDS: touched snapshot + current)
-constexpr int OPP_WINDOW_DEFAULT = 256;
+constexpr int OPP_WINDOW_DEFAULT = 256;   // sequential count / walk
+constexpr int OPP_WINDOW_PIPE = 64;       // pipelined: the walk (touched scan) is the bound
 
 struct OppCountArgs {
   const double* avail;
   const double* dem;      // window tasks [nt][4]
   int H, nt, S, seg_sup, nq, nsq, ldc;
-  uint64_t* bm;           // [nq][ldc][4] per-chunk feasibility bitmaps (bit = host)
-  int32_t* sc;            // [nsq][ldc] super-chunk counts
+  uint64_t* bm;           // [ldc][nq][4] per-chunk feasibility bitmaps (bit = host), task-major
+  int32_t* sc;            // [ldc][nsq] super-chunk counts, task-major
+};
+
+// A walk's touched hosts handed to the next window's walk (pipelined windows): the next
+// window's count pass ran on the capacities the walk started from, so these hosts are touched
+// relative to it. sb = capacity when this walk started (the next count's snapshot), ta = after.
+struct OppTouched {
+  int32_t n, pad[3];
+  int32_t tid[OPP_MAXW];
+  double sb[4][OPP_MAXW];
+  double ta[4][OPP_MAXW];
 };
 
 struct OppCommitArgs {
@@ -36,6 +47,11 @@ struct OppCommitArgs {
   int32_t* placement;     // window tasks' placements (caller order == processing order)
   uint32_t* mt;           // device MT19937 state: key[624], pos
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
+  const OppTouched* in;   // previous walk's hosts: applied to avail on entry, then touched
+  OppTouched* out;        // this walk's own hosts for the next walk (NULL: none)
+  int writeback;          // write this walk's own hosts to avail at the end
+  uint32_t* started;      // set to seq once `in` is applied (releases the next count pass)
+  uint32_t seq;
 };
 
 void launch_opp_count(const OppCountArgs& a, hipStream_t st);

@@ -22,7 +22,8 @@ namespace pvt {
 // Count kernel: block = 4 waves, each wave OPP_TW tasks over one host segment (a run of
 // super-chunks); blockIdx % S picks the segment (XCD-affine, as in score_kernel). For every
 // (task, 256-host chunk) it stores the chunk's feasibility bitmap (the four wave ballots,
-// 32 B) and, per super-chunk, the feasible count. A chunk's host loads are issued one chunk
+// 32 B) and, per super-chunk, the feasible count, task-major: the walk's dependent read of one
+// super-chunk's 64 chunk bitmaps for one task is then 2 KiB contiguous. A chunk's host loads are issued one chunk
 // ahead (register double buffer, clamped indices instead of branches).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
       }
     }
     if (lane < nt) {
-      uint64_t* o = A.bm + ((size_t)q * A.ldc + t0 + lane) * U;
+      uint64_t* o = A.bm + ((size_t)(t0 + lane) * A.nq + q) * U;
 #pragma unroll
       for (int u = 0; u < U; u++) o[u] = mine[u];
     }
@@ -90,7 +91,7 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
         if (lane == k) v = sup[k];
         sup[k] = 0;
       }
-      if (lane < nt) A.sc[(size_t)Q * A.ldc + t0 + lane] = v;
+      if (lane < nt) A.sc[(size_t)(t0 + lane) * A.nsq + Q] = v;
     }
   }
 }
@@ -112,8 +113,10 @@ struct OppLDS {
   int32_t hval[OPP_HASH];
   int32_t tid[OPP_MAXW];
   int32_t lost[OPP_MAXW];
-  double sa[4][OPP_MAXW];   // snapshot availability of touched hosts
+  double sa[4][OPP_MAXW];   // snapshot availability of touched hosts (the count pass's view)
   double ta[4][OPP_MAXW];   // current availability of touched hosts
+  double sb[4][OPP_MAXW];   // availability when this walk started (pipelined hand-off)
+  int32_t own[OPP_MAXW];    // touched by this walk
   int32_t slost[OPP_NSQ_MAX];   // per task: lost hosts per super-chunk
   uint64_t lmask[OPP_SUP][4];   // per task: lost hosts of the chosen super-chunk, as chunk bitmaps
   uint32_t mt[625];
@@ -190,14 +193,38 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
   for (int i = lane; i < A.nt; i += WAVE) S.pl[i] = -1;
   for (int i = lane; i < 625; i += WAVE) S.mt[i] = A.mt[i];
   __builtin_amdgcn_s_waitcnt(0xc07f);
+  int m = 0;
+  if (A.in) {
+    // the previous walk's commits: applied to global availability (the next count pass may
+    // then start), and listed as touched with the count pass's snapshot as sa
+    m = __builtin_amdgcn_readfirstlane(A.in->n);
+    for (int q = lane; q < m; q += WAVE) {
+      const int32_t h = A.in->tid[q];
+      for (int r = 0; r < 4; r++) {
+        const double t = A.in->ta[r][q];
+        A.avail[(size_t)r * A.H + h] = t;
+        S.sa[r][q] = A.in->sb[r][q];
+        S.ta[r][q] = t;
+        S.sb[r][q] = t;
+      }
+      S.tid[q] = h;
+      S.own[q] = 0;
+      uint32_t p = ohslot(h);
+      while (atomicCAS(&S.hkey[p], -1, h) != -1) p = (p + 1) & (OPP_HASH - 1);
+      S.hval[p] = q;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  }
+  if (A.started && lane == 0)
+    __hip_atomic_store(A.started, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const bool fast = A.nsq <= WAVE;   // one super-chunk count per lane (H <= 1,048,576)
-  int m = 0;
   MtWave mw;
   mw.buf = 0; mw.used = 0; mw.limit = 0;
   // next task's super-chunk counts and demand, prefetched with vector loads (lanes 0-3 hold
   // the demand), so no scalar-memory wait is mixed with the walk's LDS traffic
-  int scn = (fast && A.nt > 0 && lane < A.nsq) ? A.sc[(size_t)lane * A.ldc] : 0;
+  int scn = (fast && A.nt > 0 && lane < A.nsq) ? A.sc[lane] : 0;
   double dn = (A.nt > 0) ? A.dem[lane & 3] : 0.0;
 
 #ifdef PVT_STAMPS
@@ -211,7 +238,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     const int scv = scn;
     if (i + 1 < A.nt) {
       dn = A.dem[(size_t)(i + 1) * 4 + (lane & 3)];
-      if (fast) scn = lane < A.nsq ? A.sc[(size_t)lane * A.ldc + i + 1] : 0;
+      if (fast) scn = lane < A.nsq ? A.sc[(size_t)(i + 1) * A.nsq + lane] : 0;
     }
     OSTAMP(0);
     // Touched hosts that fitted at the snapshot and no longer fit ("lost"), listed and counted
@@ -251,7 +278,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     } else {
       for (int Q0 = 0; Q0 < A.nsq; Q0 += WAVE) {
         const int Q = Q0 + lane;
-        n += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)Q * A.ldc + i] : 0);
+        n += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)i * A.nsq + Q] : 0);
       }
     }
     n -= nl;
@@ -264,7 +291,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
     for (int Q0 = 0; Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
       const int Q = Q0 + lane;
       int v = 0;
-      if (Q < A.nsq) v = (fast ? scv : A.sc[(size_t)Q * A.ldc + i]) - S.slost[Q];
+      if (Q < A.nsq) v = (fast ? scv : A.sc[(size_t)i * A.nsq + Q]) - S.slost[Q];
       const int inc = wave_incl_scan(v);
       const int tot = __builtin_amdgcn_readlane(inc, 63);
       if ((long long)k < acc + tot) {
@@ -286,7 +313,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
 #pragma unroll
     for (int u = 0; u < U; u++) bits[u] = 0;
     if (q < A.nq) {
-      const uint64_t* bp = A.bm + ((size_t)q * A.ldc + i) * U;
+      const uint64_t* bp = A.bm + ((size_t)i * A.nq + q) * U;
 #pragma unroll
       for (int u = 0; u < U; u++) bits[u] = bp[u];
     }
@@ -344,24 +371,38 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
         ohash_put(S, w, ws);
         S.tid[ws] = w;
         S.sa[0][ws] = w0; S.sa[1][ws] = w1; S.sa[2][ws] = w2; S.sa[3][ws] = w3;
+        S.sb[0][ws] = w0; S.sb[1][ws] = w1; S.sb[2][ws] = w2; S.sb[3][ws] = w3;
       }
     }
     // commit in LDS only: a global store here would put its round trip on the next task (the
     // next task's prefetched loads share the in-order vmcnt counter with it)
     if (lane == 0) {
       S.ta[0][ws] = n0; S.ta[1][ws] = n1; S.ta[2][ws] = n2; S.ta[3][ws] = n3;
+      S.own[ws] = 1;
       S.pl[i] = w;
     }
   }
-  // the window's commits: current availability of every touched host, and the placements
+  // the window's commits (hosts this walk touched): to global availability, or handed to the
+  // next walk, which applies them once the next count pass (running now) has read the old state
   __builtin_amdgcn_s_waitcnt(0xc07f);
-  for (int q = lane; q < m; q += WAVE) {
-    const int32_t h = S.tid[q];
-    A.avail[h] = S.ta[0][q];
-    A.avail[(size_t)A.H + h] = S.ta[1][q];
-    A.avail[2 * (size_t)A.H + h] = S.ta[2][q];
-    A.avail[3 * (size_t)A.H + h] = S.ta[3][q];
+  int no = 0;
+  for (int q0 = 0; q0 < m; q0 += WAVE) {
+    const int q = q0 + lane;
+    const bool own = q < m && S.own[q];
+    const uint64_t b = __ballot(own);
+    if (own) {
+      const int32_t h = S.tid[q];
+      if (A.writeback)
+        for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + h] = S.ta[r][q];
+      if (A.out) {
+        const int o = no + __popcll(b & below);
+        A.out->tid[o] = h;
+        for (int r = 0; r < 4; r++) { A.out->sb[r][o] = S.sb[r][q]; A.out->ta[r][o] = S.ta[r][q]; }
+      }
+    }
+    no += __popcll(b);
   }
+  if (A.out && lane == 0) A.out->n = no;
   for (int i = lane; i < A.nt; i += WAVE) A.placement[i] = S.pl[i];
   mt_unbuffer(S.mt, mw);
   for (int i = lane; i < 625; i += WAVE) A.mt[i] = S.mt[i];
