@@ -285,9 +285,14 @@ extern "C" const char* pvt_last_error(pvt_ctx* ctx) { return ctx ? ctx->err.c_st
 // the window is short, at least 4096 hosts per segment, a multiple of 8 (one XCD per
 // blockIdx % 8), capped by the segment-list scratch.
 static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
-static int choose_segments(int H, int nt) {
+// vbp best-fit scores are continuous, so a segment's list keeps improving while it streams:
+// about KL * (1 + ln(H / (S * KL))) serial insertions per segment, S times per task. Fewer,
+// longer segments halve those insertions at 16 (measured: 29.7 -> 26.2 ms of score per
+// 1M x 10k round); cost_aware's zero-cost zone fills its lists at once and wants the waves.
+static int choose_segments(int H, int nt, int mode) {
   const int task_waves = (nt + TW - 1) / TW;
   int S = (4096 + task_waves - 1) / task_waves;
+  if (mode == PVT_VBP_BF) S = std::min(S, 16);
   if (const char* e = getenv("PVT_SEGMENTS")) S = std::max(1, atoi(e));   // tuning experiments
   S = std::min(S, std::max(1, H / 4096));
   S = std::min(S, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL)));
@@ -655,7 +660,7 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
     Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
     launch_ordered(oa, st);
   } else {
-    const int S = choose_segments(Hl, nt);
+    const int S = choose_segments(Hl, nt, r->mode);
     ScoreArgs sa{r->avail, r->zone, r->tiebreak, R.keyed ? P<double>(ctx->key) : nullptr,
                  dem_w, anc_w, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z, nt, S,
                  R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};

@@ -24,9 +24,11 @@ __device__ __forceinline__ void list_insert(double& s, uint32_t& t, int32_t& i, 
   const int lane = lane_id();
   const bool keep = lexless(s, t, i, cs, ct, ci);
   const int pos = __popcll(__ballot(keep));
-  const double us = __shfl_up(s, 1);
-  const uint32_t ut = (uint32_t)__shfl_up((int)t, 1);
-  const int32_t ui = __shfl_up(i, 1);
+  // shift by one lane with DPP wave_shr:1 (a VALU op) instead of ds_bpermute (an LDS round
+  // trip per dword): this shift is on every insertion's dependent chain
+  const double us = wave_shr1_d(s);
+  const uint32_t ut = (uint32_t)wave_shr1_i((int)t);
+  const int32_t ui = wave_shr1_i(i);
   if (lane == pos) {
     s = cs; t = ct; i = ci;
   } else if (lane > pos) {
@@ -49,6 +51,14 @@ __device__ __forceinline__ double rad(double lim) {
   if (!(lim < DINF)) return DINF;
   if (lim < 0.0) return -1.0;
   return __builtin_sqrt(lim) * (1.0 + 0x1p-40);
+}
+
+// The same radius straight from a vbp threshold, without the square root: with
+// r = fl(thr (1 + 2^-40)), sqrt(vbp_lim(thr)) <= r (1 + 2^-41 + 2^-52), and fl(r (1 + 2^-38))
+// exceeds that with room for the rounding of fl(x1 * x1).
+__device__ __forceinline__ double vbp_rad(double thr) {
+  if (!(thr < DINF)) return DINF;
+  return (thr * (1.0 + 0x1p-40)) * (1.0 + 0x1p-38);
 }
 
 template <int MODE>
@@ -199,7 +209,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
             }
           } else if (MODE == VBP_BF) {
             lim[k] = vbp_lim(ts[k]);
-            rd[k] = rad(lim[k]);
+            rd[k] = vbp_rad(ts[k]);
           }
         }
       }
