@@ -56,20 +56,18 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int l) {
 __device__ __forceinline__ int32_t readlane_i(int32_t v, int l) {
   return __builtin_amdgcn_readlane(v, l);
 }
-// Lane i receives lane i-1's value (DPP wave_shr:1, GFX9 whole-wave shift); lane 0 keeps its own.
-__device__ __forceinline__ int32_t wave_shr1_i(int32_t v) {
-  return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false);
-}
-__device__ __forceinline__ double wave_shr1_d(double v) {
-  const int64_t b = __double_as_longlong(v);
-  const int32_t lo = wave_shr1_i((int32_t)(uint32_t)b);
-  const int32_t hi = wave_shr1_i((int32_t)(uint32_t)((uint64_t)b >> 32));
-  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
-}
 __device__ __forceinline__ uint32_t readlane_u(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l);
 }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+// Orders one wave's LDS accesses across its lanes: the LDS unit executes a wave's DS operations
+// in issue order, so only the compiler's reordering needs fencing.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 
 // Wave-wide inclusive prefix sum of an int (lane order).

@@ -17,23 +17,38 @@
 
 namespace pvt {
 
-// Insert (cs, ct, ci) into the wave-held sorted list (lane j holds entry j). The caller has
-// checked it beats entry KL-1, which falls off.
-__device__ __forceinline__ void list_insert(double& s, uint32_t& t, int32_t& i, double cs,
-                                            uint32_t ct, int32_t ci) {
+// Merge a block's candidates (the lanes of pm: each beats entry KL-1, ids distinct from the
+// list's) into the wave-held sorted list in one step. Every entry moves down by the number of
+// candidates ahead of it; a candidate lands at (entries ahead) + (candidates ahead); whatever
+// lands at KL or beyond falls off. Keys are (score bits, tiebreak:id), all distinct, and the
+// loop over candidates carries no dependence from one candidate to the next (one insertion
+// after another did: each waited for the previous shift and the new last entry).
+__device__ __forceinline__ void list_merge(double& s, uint32_t& t, int32_t& i, double cs,
+                                           uint32_t ct, int32_t ci, uint64_t pm, uint64_t* m1,
+                                           uint64_t* m2) {
   const int lane = lane_id();
-  const bool keep = lexless(s, t, i, cs, ct, ci);
-  const int pos = __popcll(__ballot(keep));
-  // shift by one lane with DPP wave_shr:1 (a VALU op) instead of ds_bpermute (an LDS round
-  // trip per dword): this shift is on every insertion's dependent chain
-  const double us = wave_shr1_d(s);
-  const uint32_t ut = (uint32_t)wave_shr1_i((int)t);
-  const int32_t ui = wave_shr1_i(i);
-  if (lane == pos) {
-    s = cs; t = ct; i = ci;
-  } else if (lane > pos) {
-    s = us; t = ut; i = ui;
+  const uint64_t e1 = (uint64_t)__double_as_longlong(s), e2 = ((uint64_t)t << 32) | (uint32_t)i;
+  const uint64_t c1 = (uint64_t)__double_as_longlong(cs), c2 = ((uint64_t)ct << 32) | (uint32_t)ci;
+  const bool cand = (pm >> lane) & 1ull;
+  int below = 0, mypos = KL;
+  for (uint64_t q = pm; q; q &= q - 1) {
+    const int L = __builtin_ctzll(q);
+    const uint64_t x1 = readlane_u64(c1, L), x2 = readlane_u64(c2, L);
+    const bool elt = (e1 < x1) | ((e1 == x1) & (e2 < x2));     // entry ahead of candidate L
+    const bool clt = cand & ((c1 < x1) | ((c1 == x1) & (c2 < x2)));
+    below += elt ? 0 : 1;
+    const int pos = __popcll(__ballot(elt)) + __popcll(__ballot(clt));
+    mypos = (lane == L) ? pos : mypos;
   }
+  const int np = lane + below;
+  if (np < KL) { m1[np] = e1; m2[np] = e2; }
+  if (mypos < KL) { m1[mypos] = c1; m2[mypos] = c2; }
+  wave_sync();
+  const uint64_t r1 = m1[lane], r2 = m2[lane];
+  wave_sync();   // read before the next merge writes
+  s = __longlong_as_double((long long)r1);
+  t = (uint32_t)(r2 >> 32);
+  i = (int32_t)(uint32_t)r2;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -69,6 +84,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   __shared__ double s_rad[WPB][TW][ZL];
   __shared__ double s_c[WPB][TW][ZL];
   __shared__ double s_b[WPB][TW][ZL];
+  __shared__ uint64_t s_m1[WPB][KL], s_m2[WPB][KL];   // list_merge staging, per wave
 
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int seg = blockIdx.x % A.S, tile = blockIdx.x / A.S;
@@ -181,26 +197,12 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
         const uint64_t ck1 = (uint64_t)__double_as_longlong(sc);
         const uint64_t ck2 = ((uint64_t)tbv << 32) | (uint32_t)h;
         pm = __ballot(pass && (ck1 < tk1 || (ck1 == tk1 && ck2 < tk2)));
-        bool changed = false;
-        while (pm) {
-          const int L = __builtin_ctzll(pm);
-          pm &= pm - 1;
-          const double cs = readlane_d(sc, L);
-          const uint32_t ct = readlane_u(tbv, L);
-          const int32_t ci = hb + L;
-          // insert unless an earlier insertion of this block raised the bar above it
-          const uint64_t c1 = (uint64_t)__double_as_longlong(cs), c2 = ((uint64_t)ct << 32) | (uint32_t)ci;
-          const uint64_t t1 = (uint64_t)__double_as_longlong(ts[k]), t2 = ((uint64_t)tt[k] << 32) | (uint32_t)ti[k];
-          const bool better = (c1 < t1) | ((c1 == t1) & (c2 < t2));
-          if (better) {
-            list_insert(ls[k], lt[k], li[k], cs, ct, ci);
-            ts[k] = readlane_d(ls[k], KL - 1);
-            tt[k] = readlane_u(lt[k], KL - 1);
-            ti[k] = readlane_i(li[k], KL - 1);
-            changed = true;
-          }
-        }
-        if (changed) {
+        if (pm) {
+          list_merge(ls[k], lt[k], li[k], sc, tbv, h, pm, s_m1[wave], s_m2[wave]);
+          ts[k] = readlane_d(ls[k], KL - 1);
+          tt[k] = readlane_u(lt[k], KL - 1);
+          ti[k] = readlane_i(li[k], KL - 1);
+
           if (MODE == CA_BF) {
             if (lane < A.Z) {
               const double lm2 = ca_lim(ts[k], s_c[wave][k][lane], s_b[wave][k][lane]);
