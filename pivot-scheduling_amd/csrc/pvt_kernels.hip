@@ -53,7 +53,7 @@ __device__ __forceinline__ void list_merge(double& s, uint32_t& t, int32_t& i, d
 
 // ------------------------------------------------------------------------------------------
 // Score kernel: candidates (window tasks) x (one host segment). Block = 4 waves; each wave owns
-// TW tasks and streams the segment's hosts 64 at a time (lane = host), keeping a sorted top-KL
+// TW tasks (2 for vbp best-fit, 4 otherwise) and streams the segment's hosts 64 at a time (lane = host), keeping a sorted top-KL
 // list per task in registers. blockIdx % S picks the segment, so with S = 8 the blocks of one
 // segment share an XCD (round-robin dispatch) and its L2 holds that slice of the host table.
 // ------------------------------------------------------------------------------------------
@@ -76,7 +76,7 @@ __device__ __forceinline__ double vbp_rad(double thr) {
   return (thr * (1.0 + 0x1p-40)) * (1.0 + 0x1p-38);
 }
 
-template <int MODE>
+template <int MODE, int TW>
 __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   constexpr bool STRICT = (MODE != CA_BF);
   constexpr int ZL = (MODE == CA_BF) ? ZMAX : 1;
@@ -234,13 +234,19 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   }
 }
 
+// Tasks per wave: vbp best-fit lists keep improving while a segment streams, so each block costs
+// a few list merges; 2 tasks per wave doubles the waves that hide them (4.2e11 -> 4.9e11 cand/s
+// at 1M x 10k). cost_aware's lists fill at once: 4 tasks share each host block's loads.
+int score_tasks_per_wave(int mode) { return mode == VBP_BF ? 2 : TW; }
+
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st) {
-  const int tiles = (a.nt + WPB * TW - 1) / (WPB * TW);
+  const int tw = score_tasks_per_wave(mode);
+  const int tiles = (a.nt + WPB * tw - 1) / (WPB * tw);
   dim3 grid(tiles * a.S), block(WPB * WAVE);
   switch (mode) {
-    case CA_FF: hipLaunchKernelGGL(score_kernel<CA_FF>, grid, block, 0, st, a); break;
-    case CA_BF: hipLaunchKernelGGL(score_kernel<CA_BF>, grid, block, 0, st, a); break;
-    case VBP_BF: hipLaunchKernelGGL(score_kernel<VBP_BF>, grid, block, 0, st, a); break;
+    case CA_FF: hipLaunchKernelGGL((score_kernel<CA_FF, TW>), grid, block, 0, st, a); break;
+    case CA_BF: hipLaunchKernelGGL((score_kernel<CA_BF, TW>), grid, block, 0, st, a); break;
+    case VBP_BF: hipLaunchKernelGGL((score_kernel<VBP_BF, 2>), grid, block, 0, st, a); break;
     default: break;
   }
 }
