@@ -290,7 +290,7 @@ static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
 // longer segments halve those insertions at 16 (measured: 29.7 -> 26.2 ms of score per
 // 1M x 10k round); cost_aware's zero-cost zone fills its lists at once and wants the waves.
 static int choose_segments(int H, int nt, int mode) {
-  const int tw = score_tasks_per_wave(mode);
+  const int tw = score_tasks_per_wave(mode, H);
   const int task_waves = (nt + tw - 1) / tw;
   int S = (4096 + task_waves - 1) / task_waves;
   if (mode == PVT_VBP_BF) S = std::min(S, 16);

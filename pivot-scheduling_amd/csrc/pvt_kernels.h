@@ -167,7 +167,7 @@ struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw
   double* key;
 };
 
-int score_tasks_per_wave(int mode);
+int score_tasks_per_wave(int mode, int hosts);
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st);
 void launch_merge(const MergeArgs& a, hipStream_t st);
 void launch_pack(const PackArgs& a, hipStream_t st);

@@ -236,16 +236,25 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
 
 // Tasks per wave: vbp best-fit lists keep improving while a segment streams, so each block costs
 // a few list merges; 2 tasks per wave doubles the waves that hide them (4.2e11 -> 4.9e11 cand/s
-// at 1M x 10k). cost_aware's lists fill at once: 4 tasks share each host block's loads.
-int score_tasks_per_wave(int mode) { return mode == VBP_BF ? 2 : TW; }
+// at 1M x 10k). cost_aware's lists fill at once from the zero-cost zone, so 4 tasks share each
+// host block's loads -- unless the segments are short enough (100k hosts) that filling the lists
+// is most of the pass (config 3 ca_bf: 5.6e10 -> 6.1e10 with 2; 1M hosts: 7.4e11 -> 6.8e11).
+int score_tasks_per_wave(int mode, int hosts) {
+  if (mode == VBP_BF) return 2;
+  if (mode == CA_BF && hosts < (1 << 18)) return 2;
+  return TW;
+}
 
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st) {
-  const int tw = score_tasks_per_wave(mode);
+  const int tw = score_tasks_per_wave(mode, a.h_hi - a.h_lo);
   const int tiles = (a.nt + WPB * tw - 1) / (WPB * tw);
   dim3 grid(tiles * a.S), block(WPB * WAVE);
   switch (mode) {
     case CA_FF: hipLaunchKernelGGL((score_kernel<CA_FF, TW>), grid, block, 0, st, a); break;
-    case CA_BF: hipLaunchKernelGGL((score_kernel<CA_BF, TW>), grid, block, 0, st, a); break;
+    case CA_BF:
+      if (tw == 2) hipLaunchKernelGGL((score_kernel<CA_BF, 2>), grid, block, 0, st, a);
+      else hipLaunchKernelGGL((score_kernel<CA_BF, TW>), grid, block, 0, st, a);
+      break;
     case VBP_BF: hipLaunchKernelGGL((score_kernel<VBP_BF, 2>), grid, block, 0, st, a); break;
     default: break;
   }
