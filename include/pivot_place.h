@@ -126,6 +126,9 @@ int  pvt_reset_kstats(pvt_ctx* ctx);
 int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
 /* Tuning knob: tasks per window (0 = the policy's default; capped at 1024). */
 int  pvt_set_window(pvt_ctx* ctx, int tasks);
+/* Tuning knob: tasks per wave of the best-fit score kernel, 0 (the policy's default: 2 for vbp
+ * best-fit and for cost_aware below 262144 hosts, else 4), 2 or 4. Results are identical. */
+int  pvt_set_score_tw(pvt_ctx* ctx, int tw);
 /* Window pipelining (default on): score window k+1 on a side stream while window k is walked.
  * Results are identical either way; off runs windows strictly one after the other. */
 int  pvt_set_pipeline(pvt_ctx* ctx, int on);

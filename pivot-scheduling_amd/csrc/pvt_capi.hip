@@ -77,6 +77,7 @@ struct pvt_ctx {
       seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, kskey, kperm, kiota, ksorttmp, kflag;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
   int keyed_scan = 1;             // keyed first-fit: sorted host order + early-exit scan
+  int score_tw = 0;               // score kernel tasks per wave (0: policy default; 2 or 4)
   int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
   std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
   std::vector<uint32_t> rmt_host;
@@ -250,6 +251,11 @@ extern "C" int pvt_set_window(pvt_ctx* ctx, int tasks) {
   ctx->window = std::min(tasks, MAX_WINDOW);
   return PVT_OK;
 }
+extern "C" int pvt_set_score_tw(pvt_ctx* ctx, int tw) {
+  if (!ctx || (tw != 0 && tw != 2 && tw != 4)) return PVT_EINVAL;
+  ctx->score_tw = tw;
+  return PVT_OK;
+}
 extern "C" int pvt_set_pipeline(pvt_ctx* ctx, int on) {
   if (!ctx) return PVT_EINVAL;
   ctx->pipeline = on != 0;
@@ -278,6 +284,13 @@ extern "C" int pvt_debug_commit_stamps(pvt_ctx* ctx, uint64_t* out, int n) {
 #endif
 }
 
+// Diagnostic (not part of the public ABI): score-pass candidate counters of a PVT_DIAG build.
+extern "C" int pvt_debug_score_counts(pvt_ctx* ctx, uint64_t* out, int n, int reset) {
+  if (!ctx || !out || n < 5) return PVT_EINVAL;
+  (void)hipSetDevice(ctx->device);
+  return pvt::score_diag(out, n, reset);
+}
+
 extern "C" const char* pvt_last_error(pvt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
 // ---------------------------------------------------------------- round driver
@@ -289,8 +302,8 @@ static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
 // about KL * (1 + ln(H / (S * KL))) serial insertions per segment, S times per task. Fewer,
 // longer segments halve those insertions at 16 (measured: 29.7 -> 26.2 ms of score per
 // 1M x 10k round); cost_aware's zero-cost zone fills its lists at once and wants the waves.
-static int choose_segments(int H, int nt, int mode) {
-  const int tw = score_tasks_per_wave(mode, H);
+static int choose_segments(int H, int nt, int mode, int force_tw) {
+  const int tw = score_tasks_per_wave(mode, H, force_tw);
   const int task_waves = (nt + tw - 1) / tw;
   int S = (4096 + task_waves - 1) / task_waves;
   if (mode == PVT_VBP_BF) S = std::min(S, 16);
@@ -661,10 +674,10 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
     Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
     launch_ordered(oa, st);
   } else {
-    const int S = choose_segments(Hl, nt, r->mode);
+    const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw);
     ScoreArgs sa{r->avail, r->zone, r->tiebreak, R.keyed ? P<double>(ctx->key) : nullptr,
                  dem_w, anc_w, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z, nt, S,
-                 R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
+                 R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), ctx->score_tw};
     {
       Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
       launch_score(r->mode, sa, st);

@@ -74,6 +74,7 @@ struct ScoreArgs {
   int h_lo, h_hi;         // host range scored (a rank's shard; [0, H) unsharded)
   SegEntry* seg;          // [nt][S][KL]
   int32_t* seg_feas;      // [nt][S]
+  int tw;                 // tasks per wave: 0 = the policy's default, else 2 or 4 (tuning/tests)
 };
 
 // Merge of S sorted candidate lists per task into the task's exact top list. Two sources:
@@ -167,7 +168,8 @@ struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw
   double* key;
 };
 
-int score_tasks_per_wave(int mode, int hosts);
+int score_tasks_per_wave(int mode, int hosts, int force = 0);
+int score_diag(uint64_t* out, int n, int reset);   // PVT_DIAG builds; else PVT_EUNSUPPORTED
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st);
 void launch_merge(const MergeArgs& a, hipStream_t st);
 void launch_pack(const PackArgs& a, hipStream_t st);

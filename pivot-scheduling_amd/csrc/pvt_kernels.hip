@@ -17,6 +17,13 @@
 
 namespace pvt {
 
+#ifdef PVT_DIAG
+// Diagnostic build only (make diag): score-pass candidate counts, summed over launches:
+// [0] candidates streamed (task x host), [1] prefilter survivors, [2] exact survivors (fit and
+// within the list's limit), [3] list merges, [4] host blocks streamed per wave.
+__device__ unsigned long long g_score_diag[8];
+#endif
+
 // Merge a block's candidates (the lanes of pm: each beats entry KL-1, ids distinct from the
 // list's) into the wave-held sorted list in one step. Every entry moves down by the number of
 // candidates ahead of it; a candidate lands at (entries ahead) + (candidates ahead); whatever
@@ -140,8 +147,21 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
     if (MODE == CA_FF) nkey = A.key[h];
     if (MODE == VBP_BF) ntb = A.tb[h];     // host-id rank: read with the block, not per hit
   };
+#ifdef PVT_DIAG
+  unsigned long long dg[5] = {0, 0, 0, 0, 0};
+#endif
   if (hb0 < hb1) fetch(hb0);
   for (int hb = hb0; hb < hb1; hb += hstep) {
+    // Exact early exit (cost_aware): scores are >= +0 and the tiebreak is 0, so once every task's
+    // last entry is (0, 0, id) no later host of the segment -- all of larger index -- can enter
+    // any list: the lists are final. The anchor zone's free-egress hosts fill the lists this way.
+    if (MODE == CA_BF || MODE == CA_FF) {
+      bool final_ = true;
+#pragma unroll
+      for (int k = 0; k < TW; k++)
+        if (k < nt) final_ &= (__double_as_longlong(ts[k]) == 0) & (tt[k] == 0u);
+      if (final_) break;
+    }
     const double a0 = n0, a1 = n1, a2 = n2, a3 = n3, key = nkey;
     const int z = nz;
     const uint32_t tbh = ntb;
@@ -161,6 +181,14 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
       }
       any |= pre[k];
     }
+#ifdef PVT_DIAG
+    dg[4] += 1;
+#pragma unroll
+    for (int k = 0; k < TW; k++) {
+      dg[0] += (k < nt) ? __popcll(__ballot(ok)) : 0;
+      dg[1] += __popcll(__ballot(pre[k]));
+    }
+#endif
     if (__ballot(any) == 0) continue;
 #pragma unroll
     for (int k = 0; k < TW; k++) {
@@ -176,6 +204,9 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
         pass = fit && (s2 <= lm);
       }
       uint64_t pm = __ballot(pass);
+#ifdef PVT_DIAG
+      dg[2] += __popcll(pm);
+#endif
       if (pm) {
         double sc = DINF;
         uint32_t tbv = 0;
@@ -198,6 +229,9 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
         const uint64_t ck2 = ((uint64_t)tbv << 32) | (uint32_t)h;
         pm = __ballot(pass && (ck1 < tk1 || (ck1 == tk1 && ck2 < tk2)));
         if (pm) {
+#ifdef PVT_DIAG
+          dg[3] += 1;
+#endif
           list_merge(ls[k], lt[k], li[k], sc, tbv, h, pm, s_m1[wave], s_m2[wave]);
           ts[k] = readlane_d(ls[k], KL - 1);
           tt[k] = readlane_u(lt[k], KL - 1);
@@ -218,6 +252,10 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
     }
   }
 
+#ifdef PVT_DIAG
+  if (lane == 0)
+    for (int c = 0; c < 5; c++) atomicAdd(&g_score_diag[c], dg[c]);
+#endif
   // Feasible hosts per segment, as the merge needs it: a list that never filled holds every
   // feasible host of the segment (its threshold stayed infinite); a full one reports KL + 1,
   // i.e. "bounded by its last entry" (every host it rejected ranked at or after that entry).
@@ -239,23 +277,45 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
 // at 1M x 10k). cost_aware's lists fill at once from the zero-cost zone, so 4 tasks share each
 // host block's loads -- unless the segments are short enough (100k hosts) that filling the lists
 // is most of the pass (config 3 ca_bf: 5.6e10 -> 6.1e10 with 2; 1M hosts: 7.4e11 -> 6.8e11).
-int score_tasks_per_wave(int mode, int hosts) {
+// Diagnostic build: read (and with reset != 0 clear) the score-pass counters.
+int score_diag(uint64_t* out, int n, int reset) {
+#ifdef PVT_DIAG
+  unsigned long long h[8];
+  if (hipDeviceSynchronize() != hipSuccess) return -3;
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_score_diag), sizeof(h)) != hipSuccess) return -3;
+  for (int i = 0; i < n && i < 8; i++) out[i] = h[i];
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_score_diag), z, sizeof(z)) != hipSuccess) return -3;
+  }
+  return 0;
+#else
+  (void)out; (void)n; (void)reset;
+  return -5;
+#endif
+}
+
+int score_tasks_per_wave(int mode, int hosts, int force) {
+  if (force == 2 || force == 4) return force;   // pvt_set_score_tw: both instances stay tested
   if (mode == VBP_BF) return 2;
   if (mode == CA_BF && hosts < (1 << 18)) return 2;
   return TW;
 }
 
+template <int MODE>
+static void launch_score_tw(int tw, dim3 grid, dim3 block, const ScoreArgs& a, hipStream_t st) {
+  if (tw == 2) hipLaunchKernelGGL((score_kernel<MODE, 2>), grid, block, 0, st, a);
+  else hipLaunchKernelGGL((score_kernel<MODE, 4>), grid, block, 0, st, a);
+}
+
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st) {
-  const int tw = score_tasks_per_wave(mode, a.h_hi - a.h_lo);
+  const int tw = score_tasks_per_wave(mode, a.h_hi - a.h_lo, a.tw);
   const int tiles = (a.nt + WPB * tw - 1) / (WPB * tw);
   dim3 grid(tiles * a.S), block(WPB * WAVE);
   switch (mode) {
-    case CA_FF: hipLaunchKernelGGL((score_kernel<CA_FF, TW>), grid, block, 0, st, a); break;
-    case CA_BF:
-      if (tw == 2) hipLaunchKernelGGL((score_kernel<CA_BF, 2>), grid, block, 0, st, a);
-      else hipLaunchKernelGGL((score_kernel<CA_BF, TW>), grid, block, 0, st, a);
-      break;
-    case VBP_BF: hipLaunchKernelGGL((score_kernel<VBP_BF, 2>), grid, block, 0, st, a); break;
+    case CA_FF: launch_score_tw<CA_FF>(tw, grid, block, a, st); break;
+    case CA_BF: launch_score_tw<CA_BF>(tw, grid, block, a, st); break;
+    case VBP_BF: launch_score_tw<VBP_BF>(tw, grid, block, a, st); break;
     default: break;
   }
 }

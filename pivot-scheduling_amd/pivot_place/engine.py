@@ -44,6 +44,7 @@ def load_library(path=None):
         "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_set_window": ([c_void_p, c_int], c_int),
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
+        "pvt_set_score_tw": ([c_void_p, c_int], c_int),
         "pvt_last_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64),
                             ctypes.POINTER(ctypes.c_int64)], c_int),
         "pvt_last_error": ([c_void_p], ctypes.c_char_p),
@@ -350,6 +351,10 @@ class PlacementEngine:
 
     def set_window(self, tasks):
         self._check(self.lib.pvt_set_window(self.ctx, int(tasks)))
+
+    def set_score_tw(self, tw=0):
+        """Score-kernel tasks per wave: 0 = the policy default, 2 or 4 (identical results)."""
+        self._check(self.lib.pvt_set_score_tw(self.ctx, int(tw)))
 
     def set_pipeline(self, on=True):
         self._check(self.lib.pvt_set_pipeline(self.ctx, int(bool(on))))

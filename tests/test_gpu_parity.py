@@ -164,3 +164,25 @@ def test_keyed_first_fit_zero_key_prefix_runs_dry(engine, pipeline, H, cpus):
         engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
     assert (ref.placement >= 0).sum() > 0
     _assert_same(res, ref.placement, ref.order, ref.avail)
+
+
+@pytest.mark.parametrize("tw", [2, 4])
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_VBP_BF])
+@pytest.mark.parametrize("H,T,window", [(100_000, 2600, 0), (20_000, 900, 96), (2000, 3000, 333)])
+def test_score_instances_both_tasks_per_wave(engine, mode, tw, H, T, window):
+    """pvt_set_score_tw forces the score kernel's 2- or 4-tasks-per-wave instance, so both stay
+    under parity at every host count (the default picks by policy and host count)."""
+    r = synthetic.make_round(mode, H, T, seed=31 + tw)
+    if H <= 2000:
+        r.avail[0, :] = 6.0
+    ref = oracle.place(r)
+    try:
+        engine.set_resident(0)
+        engine.set_score_tw(tw)
+        engine.set_window(window)
+        res = engine.place(r)
+    finally:
+        engine.set_window(0)
+        engine.set_score_tw(0)
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+    _assert_same(res, ref.placement, ref.order, ref.avail)

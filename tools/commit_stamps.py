@@ -14,7 +14,7 @@ from pivot_place.engine import DeviceRound, PlacementEngine  # noqa: E402
 mode = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 T = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
-eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "build",
+eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "diag",
                                                "libpivot_place_stamps.so"))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]

@@ -28,12 +28,17 @@ def main():
     p.add_argument("--tasks", type=int, default=10_000)
     p.add_argument("--seed", type=int, default=20261015)
     p.add_argument("--reps", type=int, default=3)
+    p.add_argument("--diag", action="store_true",
+                   help="load the PVT_DIAG build (make -C pivot-scheduling_amd diag) and print the "
+                        "score pass's candidate counters (prefilter survivors) as JSON")
     a = p.parse_args()
     import torch
     from pivot_place import _abi, synthetic
     from pivot_place.engine import DeviceRound, PlacementEngine
     r = synthetic.make_round(MODES[a.mode], a.hosts, a.tasks, seed=a.seed)
-    eng = PlacementEngine(0)
+    lib = (os.path.join(ROOT, "pivot-scheduling_amd", "diag", "libpivot_place_diag.so")
+           if a.diag else None)
+    eng = PlacementEngine(0, lib_path=lib)
     dr = DeviceRound(r, eng.device)
     eng.reset_kstats()
     eng.set_profiling(True)
@@ -50,6 +55,21 @@ def main():
     print("score probe: mode %s H=%d window=%d tasks reps=%d  score launches=%d avg %.3f ms  (%.2f s)"
           % (a.mode, a.hosts, nt, a.reps, k["launches"], k["ms"] / max(k["launches"], 1), dt),
           flush=True)
+    if a.diag:
+        import ctypes
+        import json
+        f = eng.lib.pvt_debug_score_counts
+        f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int, ctypes.c_int]
+        buf = (ctypes.c_uint64 * 8)()
+        assert f(eng.ctx, buf, 8, 1) == 0
+        c = [int(buf[i]) for i in range(5)]
+        print("DIAG " + json.dumps({
+            "mode": a.mode, "hosts": a.hosts, "window_tasks": nt, "reps": a.reps,
+            "candidates_streamed": c[0], "prefilter_survivors": c[1], "exact_survivors": c[2],
+            "list_merges": c[3], "wave_host_blocks": c[4],
+            "logical_candidates": nt * a.hosts * a.reps,
+            "prefilter_survivor_frac": c[1] / max(c[0], 1),
+            "streamed_frac_of_logical": c[0] / max(nt * a.hosts * a.reps, 1)}), flush=True)
 
 
 if __name__ == "__main__":

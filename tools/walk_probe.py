@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Whole-round probe for PMC counter runs and hang diagnosis: pvt_place on one synthetic round,
+`--reps` times, with the window pipeline on or off, printing a line per rep (so a run that
+stalls shows where). Exits non-zero if the engine reports an error (e.g. a hand-off timeout).
+
+    python tools/walk_probe.py --mode ca_bf --hosts 100000 --tasks 2000 --pipeline 0 --reps 2
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "pivot-scheduling_amd"), ROOT]
+
+MODES = {"ca_ff": 0, "ca_bf": 1, "opp": 2, "vbp_ff": 3, "vbp_bf": 4}
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mode", default="ca_bf", choices=sorted(MODES))
+    p.add_argument("--hosts", type=int, default=100_000)
+    p.add_argument("--tasks", type=int, default=2000)
+    p.add_argument("--seed", type=int, default=20261015)
+    p.add_argument("--pipeline", type=int, default=1)
+    p.add_argument("--window", type=int, default=0)
+    p.add_argument("--reps", type=int, default=2)
+    a = p.parse_args()
+    import torch
+    from pivot_place import _abi, synthetic
+    from pivot_place.engine import DeviceRound, PlacementEngine
+    r = synthetic.make_round(MODES[a.mode], a.hosts, a.tasks, seed=a.seed)
+    eng = PlacementEngine(0, window=a.window)
+    eng.set_resident(0)
+    eng.set_pipeline(bool(a.pipeline))
+    dr = DeviceRound(r, eng.device)
+    eng.reset_kstats()
+    eng.set_profiling(True)
+    for rep in range(a.reps):
+        t = time.perf_counter()
+        dr.reset()
+        eng.run(dr)
+        torch.cuda.synchronize()
+        st = eng.last_stats()
+        print("walk probe rep %d: mode %s H=%d T=%d pipeline=%d  %.2f ms  windows=%d refills=%d"
+              % (rep, a.mode, a.hosts, a.tasks, a.pipeline, (time.perf_counter() - t) * 1e3,
+                 st["windows"], st["refills"]), flush=True)
+    eng.set_profiling(False)
+    k = eng.kstats(_abi.PVT_K_COMMIT)
+    print("commit launches=%d avg %.3f ms" % (k["launches"], k["ms"] / max(k["launches"], 1)),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
