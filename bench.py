@@ -58,6 +58,9 @@ def parse():
     p.add_argument("--window", type=int, default=0)
     p.add_argument("--pipeline", type=int, default=1,
                    help="1: score window k+1 while window k is walked (default); 0: sequential")
+    p.add_argument("--epochs", type=int, default=1,
+                   help="cost_aware best-fit: 1 walks groups side by side in speculative epochs "
+                        "(default), 0: one group after the other")
     p.add_argument("--shard", default="scenarios", choices=["scenarios", "hosts"],
                    help="N > 1: independent scenario per rank (weak scaling, config 4) or one "
                         "round with its host dimension split over the ranks (strong, config 5)")
@@ -267,6 +270,7 @@ def main():
     B = max(args.batch, 0)
     eng = PlacementEngine(local, window=args.window)
     eng.set_pipeline(bool(args.pipeline))
+    eng.set_epochs(bool(args.epochs))
     if B:
         from pivot_place.engine import DeviceBatch
         rounds = [synthetic.make_round(mode, H, T, seed=args.seed + rank * B + s) for s in range(B)]
@@ -288,6 +292,7 @@ def main():
         run(dr)
     torch.cuda.synchronize()
     stats = eng.last_stats()
+    ep = eng.epoch_stats()
     placed = int(((dr.placement_of(0) if B else dr.placement[:T]) >= 0).sum().item())
     log("[rank %d] warmup done: %d/%d placed, windows=%d refills=%d"
         % (rank, placed, T, stats["windows"], stats["refills"]))
@@ -348,6 +353,8 @@ def main():
             "walk_us_per_task": (ks["commit"]["ms"] * 1e3 / args.steps / max(T * (B or 1), 1)
                                  if not B else None),
             "windows_per_step": stats["windows"], "refills_per_step": stats["refills"],
+            "epochs_per_step": ep["epochs"], "segments_per_step": ep["segments"],
+            "rejected_segments_per_step": ep["rejected"],
         }
         ref = None
         if world == 1 and args.cpu_baseline_seconds > 0:
@@ -362,7 +369,7 @@ def main():
             else:
                 out["parity"] = check_parity(dr.result(), r, ref)
         default = (not B and not hosts_sharded and world == 1 and H == DEFAULT_H
-                   and T == DEFAULT_T and args.window == 0 and args.pipeline == 1)
+                   and T == DEFAULT_T and args.window == 0 and args.pipeline == 1 and args.epochs == 1)
         if args.extra == 1 or (args.extra < 0 and default):
             out["extra"] = extra_workloads(eng, args, args.mode)
         print(json.dumps(out), flush=True)

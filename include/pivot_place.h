@@ -132,6 +132,17 @@ int  pvt_set_score_tw(pvt_ctx* ctx, int tw);
 /* Window pipelining (default on): score window k+1 on a side stream while window k is walked.
  * Results are identical either way; off runs windows strictly one after the other. */
 int  pvt_set_pipeline(pvt_ctx* ctx, int on);
+/*
+ * Group-parallel epochs (default on): a cost_aware best-fit round of several groups walks
+ * consecutive groups of distinct anchor zones side by side, each on the epoch's start state,
+ * and keeps exactly the prefix the sequential order would have produced (a group is rejected,
+ * and walked again in the next epoch, if a host an earlier group committed to is its winner or
+ * beats it); results are identical either way. Replaces the group loop of
+ * scheduler/cost_aware.py:37-42 around _best_fit (:63-97).
+ * pvt_epoch_stats: epochs run, segments walked and segments rejected in the last pvt_place.
+ */
+int  pvt_set_epochs(pvt_ctx* ctx, int on);
+int  pvt_epoch_stats(pvt_ctx* ctx, int64_t* epochs, int64_t* segments, int64_t* rejected);
 /* Counters of the last pvt_place call: windows run and refills forced by exhausted lists. */
 int  pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills);
 /*

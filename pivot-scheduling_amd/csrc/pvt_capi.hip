@@ -30,6 +30,14 @@
 
 using namespace pvt;
 
+// Group-parallel epochs (cost_aware best-fit): at most EPOCH_SEGS segments (one walk workgroup
+// each, <= MAX_WINDOW tasks) and EPOCH_MAX tasks per epoch (its lists: 64 B x LMAX per task).
+static constexpr int EPOCH_SEGS = 64;
+static constexpr int EPOCH_MAX = 16384;
+// ep_dev / ep_host words: seg_off [EPOCH_SEGS + 1], status [2 x EPOCH_SEGS], bad [EPOCH_SEGS]
+static constexpr int EP_OFF = 0, EP_STATUS = EPOCH_SEGS + 1, EP_BAD = EP_STATUS + 2 * EPOCH_SEGS;
+static constexpr int EP_WORDS = EP_BAD + EPOCH_SEGS;
+
 struct Buf {
   void* p = nullptr;
   size_t n = 0;
@@ -56,15 +64,17 @@ struct RoundState {
   int key_group = -1;             // group whose frozen first-fit key is computed
   int t0 = 0, W = 0, Wmax = 0, nt = 0;
   int lb = 0;                     // list buffer of the current window
+  std::vector<int> egs, ega;      // cost_aware best-fit epochs: group starts (+ T) and anchors
+  std::vector<int> ecomp;         // zone -> its component of zones joined by zero egress cost
 };
 
 struct pvt_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   hipStream_t side = nullptr;     // scores the next window while the current one is walked
-  hipEvent_t ev_lists = nullptr;
-  uint32_t* walk_flag = nullptr;  // device: sequence number of the last walk that started
-  uint32_t walk_seq = 0;
+  hipEvent_t ev_lists = nullptr;   // side stream: the next window's lists are ready
+  hipEvent_t ev_walk = nullptr;    // caller stream: everything before the current walk is done
+  int walk_cus = 0;                // CUs the side stream leaves to the walks
   std::string err;
   int window = 0;                 // 0: per-policy default
   int64_t windows = 0, refills = 0;
@@ -79,6 +89,10 @@ struct pvt_ctx {
   int keyed_scan = 1;             // keyed first-fit: sorted host order + early-exit scan
   int score_tw = 0;               // score kernel tasks per wave (0: policy default; 2 or 4)
   int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
+  int epochs = 1;                 // cost_aware best-fit: group-parallel speculative epochs
+  int64_t n_epochs = 0, n_segs = 0, n_rejected = 0;
+  Buf ep_dev, own_a, wres;        // epoch descriptors / status / flags, own-host logs, winners
+  int32_t* ep_host = nullptr;     // pinned staging of ep_dev
   std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
   std::vector<uint32_t> rmt_host;
   RoundState rs;
@@ -169,6 +183,40 @@ static void harvest(pvt_ctx* ctx) {
 // ---------------------------------------------------------------- ABI
 extern "C" int pvt_abi_version(void) { return PVT_ABI_VERSION; }
 
+// The side stream (the next window's score / count pass while a walk runs) is ordered against
+// the walks by events only -- no in-kernel flag polled by the command processor, which never
+// completes under serialising tools (rocprofv3 counter collection) -- and runs at the lowest
+// queue priority (the context's own stream at the highest), so when walk k and the side pass k+1 become ready together (walk k-1 done)
+// the walk, one workgroup that needs a whole CU's LDS, is dispatched first. PVT_WALK_CUS=n keeps
+// the side stream off n CUs instead (measured: it serialises the two streams).
+static hipError_t create_streams(pvt_ctx* ctx, int ncu) {
+  int prio = 1;
+  if (const char* e = getenv("PVT_SIDE_PRIO")) prio = atoi(e);
+  int least = 0, greatest = 0;
+  if (prio && (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest))
+    prio = 0;
+  hipError_t e = prio ? hipStreamCreateWithPriority(&ctx->own, hipStreamNonBlocking, greatest)
+                      : hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
+  int cus = 0;
+  if (const char* e = getenv("PVT_WALK_CUS")) cus = atoi(e);   // tuning experiments
+  if (cus > 0 && ncu > 2 * cus) {
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    const int stride = ncu / cus;
+    int kept = 0;
+    for (int i = 0; i < ncu; i++)
+      if (i % stride != stride - 1 || i / stride >= cus) { mask[i / 32] |= 1u << (i % 32); kept++; }
+    if (hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mask.size(), mask.data()) == hipSuccess) {
+      ctx->walk_cus = ncu - kept;
+      return hipSuccess;
+    }
+    (void)hipGetLastError();
+  }
+  ctx->walk_cus = 0;
+  if (prio) return hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, least);
+  return hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
+}
+
 extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (!out) return PVT_EINVAL;
   *out = nullptr;
@@ -181,14 +229,13 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   ctx->device = device;
   std::memset(ctx->ks, 0, sizeof(ctx->ks));
   if (hipSetDevice(device) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->own, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc((void**)&ctx->walk_flag, 64) != hipSuccess ||
-      hipMemset(ctx->walk_flag, 0, 64) != hipSuccess ||
+      create_streams(ctx, prop.multiProcessorCount) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_lists, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_walk, hipEventDisableTiming) != hipSuccess ||
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
       resident_init_attrs() != hipSuccess ||
-      hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess) {
+      hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->ep_host, sizeof(int32_t) * EP_WORDS) != hipSuccess) {
     delete ctx;
     return PVT_EHIP;
   }
@@ -208,14 +255,15 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
-                 &ctx->ksorttmp, &ctx->kflag};
+                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->own_a, &ctx->wres};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->next_host) (void)hipHostFree(ctx->next_host);
+  if (ctx->ep_host) (void)hipHostFree(ctx->ep_host);
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
+  if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
-  if (ctx->walk_flag) (void)hipFree(ctx->walk_flag);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
   return PVT_OK;
@@ -259,6 +307,18 @@ extern "C" int pvt_set_score_tw(pvt_ctx* ctx, int tw) {
 extern "C" int pvt_set_pipeline(pvt_ctx* ctx, int on) {
   if (!ctx) return PVT_EINVAL;
   ctx->pipeline = on != 0;
+  return PVT_OK;
+}
+extern "C" int pvt_set_epochs(pvt_ctx* ctx, int on) {
+  if (!ctx) return PVT_EINVAL;
+  ctx->epochs = on != 0;
+  return PVT_OK;
+}
+extern "C" int pvt_epoch_stats(pvt_ctx* ctx, int64_t* epochs, int64_t* segments, int64_t* rejected) {
+  if (!ctx) return PVT_EINVAL;
+  if (epochs) *epochs = ctx->n_epochs;
+  if (segments) *segments = ctx->n_segs;
+  if (rejected) *rejected = ctx->n_rejected;
   return PVT_OK;
 }
 extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) {
@@ -309,7 +369,7 @@ static int choose_segments(int H, int nt, int mode, int force_tw) {
   if (mode == PVT_VBP_BF) S = std::min(S, 16);
   if (const char* e = getenv("PVT_SEGMENTS")) S = std::max(1, atoi(e));   // tuning experiments
   S = std::min(S, std::max(1, H / 4096));
-  S = std::min(S, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL)));
+  S = std::min(S, std::max(MAX_SEG, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL))));
   S = std::max(1, std::min(S, 256));
   if (S >= 8) S = S / 8 * 8;
   return S;
@@ -443,17 +503,17 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
     const int t0 = k * W, nt = std::min(W, T - t0);
     const bool next = pipe && k + 1 < nwin;
     ctx->windows++;
-    const uint32_t seq = ++ctx->walk_seq;
+    const OppTouched* in = (pipe && k > 0) ? tl_of((k - 1) % nbuf) : nullptr;
+    if (in) launch_opp_apply(in, r->avail, H, st);   // walk k-1's commits, before count k+1
     if (next) {
-      HIPCHK(hipStreamWaitValue32(ctx->side, ctx->walk_flag, seq, hipStreamWaitValueGte, 0xffffffffu));
+      HIPCHK(hipEventRecord(ctx->ev_walk, st));
+      HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_walk, 0));
       count(k + 1, ctx->side);
       HIPCHK(hipEventRecord(ctx->ev_lists, ctx->side));
     }
     OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm_of(k % nbuf),
                      sc_of(k % nbuf), H, nt, nq, nsq, W, r->placement + t0, mt, ctx->stamps,
-                     (pipe && k > 0) ? tl_of((k - 1) % nbuf) : nullptr,
-                     next ? tl_of(k % nbuf) : nullptr, next ? 0 : 1,
-                     next ? ctx->walk_flag : nullptr, seq};
+                     in, next ? tl_of(k % nbuf) : nullptr, next ? 0 : 1};
     {
       Scope s(ctx, PVT_K_COMMIT, 0, 0);
       launch_opp_commit(oa, st);
@@ -675,6 +735,8 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
     launch_ordered(oa, st);
   } else {
     const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw);
+    ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)nt * S * KL);
+    ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)nt * S);
     ScoreArgs sa{r->avail, r->zone, r->tiebreak, R.keyed ? P<double>(ctx->key) : nullptr,
                  dem_w, anc_w, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z, nt, S,
                  R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), ctx->score_tw};
@@ -703,7 +765,7 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
   CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
                  P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
                  r->placement, P<int32_t>(ctx->owned[1 - lb]), n_prev, P<int32_t>(ctx->owned[lb]),
-                 status, ctx->walk_flag, ++ctx->walk_seq, ctx->stamps};
+                 status, ctx->stamps};
   {
     Scope sc(ctx, PVT_K_COMMIT, 0, 0);
     launch_commit(ca_, st);
@@ -754,11 +816,10 @@ static int window_commit(pvt_ctx* ctx) {
 
 // pvt_place for the list policies. While window k is walked on the caller's stream, the side
 // stream scores window k+1 on the capacities as they stand (the walk of k-1 is complete; the
-// walk of k is in flight). The side stream is released by the walk kernel itself (it stores
-// its sequence number on entry; hipStreamWaitValue32): were both merely made ready by the end
-// of walk k-1, the score grid could fill every CU first and hold back the walk, which needs
-// almost all of one CU's LDS, until the grid drains. Hosts window k commits to are the only ones whose list entries can
-// be stale, so walk k+1 inherits them as touched (pvt_walk.hip) and stays exact. A walk that
+// walk of k is in flight): an event recorded just before walk k releases it. The side stream
+// runs on all but a few CUs (create_side_stream), so the score grid never holds back the walk,
+// which needs a whole CU's LDS. Hosts window k commits to are the only ones whose list entries
+// can be stale, so walk k+1 inherits them as touched (pvt_walk.hip) and stays exact. A walk that
 // stops early (refill) discards the speculative lists; keyed first-fit recomputes its frozen
 // key at a group start, so the pipeline drains at group boundaries.
 static int place_pipelined(pvt_ctx* ctx) {
@@ -771,14 +832,13 @@ static int place_pipelined(pvt_ctx* ctx) {
   int n_prev = 0;
   bool inherited = false;
   for (;;) {
-    // Walk k first; the side stream then waits until that walk has STARTED (its CU is taken,
-    // and walk k-1 is complete) before scoring window k+1 (same group) on the current state.
-    if ((rc = walk_launch(ctx, t0, nt, lb, n_prev))) return rc;
+    // Walk k, and beside it window k+1 (same group) scored on the state walk k-1 left.
     const int nt0 = t0 + nt, ge = group_end(R, t0);
     const int nnt = (ctx->pipeline && nt0 < ge) ? std::min(R.W, ge - nt0) : 0;
+    if (nnt > 0) HIPCHK(hipEventRecord(ctx->ev_walk, ctx->stream));
+    if ((rc = walk_launch(ctx, t0, nt, lb, n_prev))) return rc;
     if (nnt > 0) {
-      HIPCHK(hipStreamWaitValue32(ctx->side, ctx->walk_flag, ctx->walk_seq, hipStreamWaitValueGte,
-                                  0xffffffffu));
+      HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_walk, 0));
       if ((rc = window_lists(ctx, nt0, nnt, 1 - lb, ctx->side))) return rc;
       HIPCHK(hipEventRecord(ctx->ev_lists, ctx->side));
     }
@@ -797,6 +857,161 @@ static int place_pipelined(pvt_ctx* ctx) {
     if (nt == 0) break;
     t0 = R.t0; lb = 0; n_prev = 0; inherited = false;
     if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
+  }
+  return PVT_OK;
+}
+
+// ---------------------------------------------------------------- group-parallel epochs
+// cost_aware best-fit rounds of several groups (pvt_epoch.hip). The groups in processing
+// order, from the caller's task_group / group_anchor (a group's tasks are contiguous).
+static int epoch_groups(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  R.egs.clear();
+  R.ega.clear();
+  const int T = R.T;
+  if (!ctx->epochs || r->mode != PVT_CA_BF || !r->task_group || r->n_groups < 2 || T < 2) return PVT_OK;
+  std::vector<int32_t> tg(T), ga(r->n_groups);
+  hipStream_t st = ctx->stream;
+  HIPCHK(hipMemcpyAsync(tg.data(), r->task_group, sizeof(int32_t) * T, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ga.data(), r->group_anchor, sizeof(int32_t) * r->n_groups,
+                        hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  std::vector<int> cnt(r->n_groups, 0);
+  for (int t = 0; t < T; t++) {
+    if (tg[t] < 0 || tg[t] >= r->n_groups) return fail(ctx, PVT_EINVAL, "task_group out of range");
+    cnt[tg[t]]++;
+  }
+  int off = 0, ng = 0;
+  for (int g = 0; g < r->n_groups; g++) {
+    if (cnt[g] == 0) continue;
+    R.egs.push_back(off);
+    R.ega.push_back(ga[g]);
+    off += cnt[g];
+    ng++;
+  }
+  R.egs.push_back(T);
+  // Zones joined by zero egress cost (csum = 0) form one component: a group's winners are the
+  // lowest-index fitting hosts of its anchor's component (score 0), so two groups anchored in
+  // one component compete for the same hosts and an epoch never holds both.
+  const int Z = R.Z;
+  std::vector<double> cost((size_t)Z * Z);
+  HIPCHK(hipMemcpyAsync(cost.data(), r->cost, sizeof(double) * Z * Z, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  R.ecomp.resize(Z);
+  for (int z = 0; z < Z; z++) R.ecomp[z] = z;
+  auto root = [&](int z) { while (R.ecomp[z] != z) z = R.ecomp[z] = R.ecomp[R.ecomp[z]]; return z; };
+  int plan = 1;
+  if (const char* e = getenv("PVT_EPOCH_PLAN")) plan = atoi(e);   // 0: distinct zones only
+  for (int a = 0; a < Z && plan; a++)
+    for (int z = 0; z < Z; z++)
+      if (cost[(size_t)a * Z + z] + cost[(size_t)z * Z + a] == 0.0) R.ecomp[root(a)] = root(z);
+  for (int z = 0; z < Z; z++) R.ecomp[z] = root(z);
+  // worth it when groups are many and short (a group longer than a walk's window is walked in
+  // sequential epochs of one segment, without the score / walk pipeline of place_pipelined)
+  if (ng < 2 || T > ng * MAX_WINDOW) { R.egs.clear(); R.ega.clear(); }
+  return PVT_OK;
+}
+
+// The next epoch from task t0: consecutive group segments whose anchors lie in distinct
+// zero-cost components (two groups of one component compete for the same hosts: the second
+// would be rejected), each at most
+// MAX_WINDOW tasks; a segment that ends inside its group ends the epoch (the rest of the group
+// depends on it). Returns the segment offsets relative to t0 in off (off[0] = 0).
+static void epoch_plan(const RoundState& R, int t0, std::vector<int>& off) {
+  off.assign(1, 0);
+  size_t g = 0;
+  while (g + 1 < R.egs.size() && R.egs[g + 1] <= t0) g++;
+  std::vector<int> zones;
+  int t = t0;
+  while (t < R.T && (int)off.size() <= EPOCH_SEGS) {
+    const int ge = R.egs[g + 1];
+    const int a = (R.ega[g] >= 0 && R.ega[g] < (int)R.ecomp.size()) ? R.ecomp[R.ega[g]] : R.ega[g];
+    if (off.size() > 1 && std::find(zones.begin(), zones.end(), a) != zones.end()) break;
+    const int e = std::min({ge, t + MAX_WINDOW, t0 + EPOCH_MAX});
+    if (e <= t) break;
+    off.push_back(e - t0);
+    zones.push_back(a);
+    t = e;
+    if (e < ge) break;
+    g++;
+  }
+}
+
+static int place_epochs(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  ENSURE(ctx->ep_dev, sizeof(int32_t) * EP_WORDS);
+  ENSURE(ctx->own_a, sizeof(double) * 4 * (size_t)MAX_WINDOW * EPOCH_SEGS);
+  ENSURE(ctx->wres, sizeof(WinRec) * (size_t)EPOCH_MAX);
+  ENSURE(ctx->owned[0], sizeof(int32_t) * (size_t)MAX_WINDOW * EPOCH_SEGS);
+  ENSURE(ctx->l_e[0], sizeof(ListEntry) * (size_t)EPOCH_MAX * LMAX);
+  ENSURE(ctx->l_ids[0], sizeof(int32_t) * (size_t)EPOCH_MAX * LMAX);
+  ENSURE(ctx->l_t[0], sizeof(TaskRec) * (size_t)EPOCH_MAX);
+  int32_t* dev = P<int32_t>(ctx->ep_dev);
+  int32_t* host = ctx->ep_host;
+  std::vector<int> off;
+  int t0 = 0, rc;
+  while (t0 < R.T) {
+    epoch_plan(R, t0, off);
+    const int nseg = (int)off.size() - 1, nt = off.back();
+    ctx->n_epochs++;
+    ctx->n_segs += nseg;
+    if ((rc = window_lists(ctx, t0, nt, 0, st))) return rc;
+    Lists L;
+    lists_from(ctx, L, 0);
+    if (nseg == 1) {                          // one segment: the plain walk (writes avail)
+      if ((rc = walk_launch(ctx, t0, nt, 0, 0))) return rc;
+      int adv = 0;
+      if ((rc = walk_status(ctx, t0, nt, false, &adv))) return rc;
+      if (adv < nt) ctx->refills++;
+      t0 += adv;
+      continue;
+    }
+    for (int k = 0; k <= nseg; k++) host[EP_OFF + k] = off[k];
+    HIPCHK(hipMemcpyAsync(dev + EP_OFF, host + EP_OFF, sizeof(int32_t) * (nseg + 1),
+                          hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(dev + EP_BAD, 0, sizeof(int32_t) * nseg, st));
+    CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
+                   P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
+                   r->placement, nullptr, 0, P<int32_t>(ctx->owned[0]), dev + EP_STATUS,
+                   ctx->stamps, dev + EP_OFF, P<double>(ctx->own_a), P<WinRec>(ctx->wres)};
+    {
+      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+      launch_commit_segments(ca_, nseg, st);
+    }
+    EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
+                 P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_OFF,
+                 P<int32_t>(ctx->owned[0]), P<double>(ctx->own_a), dev + EP_STATUS,
+                 P<WinRec>(ctx->wres), r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD};
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_epoch_validate(ea, st);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    // the exact prefix: segments before the first rejected one, up to and including the first
+    // that stopped early (its walked tasks are exact; the next epoch starts where it stopped)
+    int acc = 0, next = t0;
+    for (int j = 0; j < nseg; j++) {
+      const int adv = host[EP_STATUS + 2 * j], len = off[j + 1] - off[j];
+      if (adv == -1) return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out at task %d", t0 + off[j]);
+      if (adv < 0 || adv > len) return fail(ctx, PVT_EHIP, "epoch walk returned %d of %d", adv, len);
+      if (j > 0 && host[EP_BAD + j]) { ctx->n_rejected += nseg - j; break; }
+      acc = j + 1;
+      next = t0 + off[j] + adv;
+      if (adv < len) { ctx->refills++; ctx->n_rejected += nseg - j - 1; break; }
+    }
+    if (next == t0) return fail(ctx, PVT_EHIP, "epoch made no progress at task %d", t0);
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_epoch_apply(ea, acc, st);
+    }
+    HIPCHK(hipGetLastError());
+    t0 = next;
   }
   return PVT_OK;
 }
@@ -956,7 +1171,9 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
     return opp_round(ctx, r);
   }
   if ((rc = round_begin(ctx, r, 0, r->n_hosts, 1))) return rc;
-  rc = place_pipelined(ctx);
+  ctx->n_epochs = ctx->n_segs = ctx->n_rejected = 0;
+  if ((rc = epoch_groups(ctx))) return rc;
+  rc = ctx->rs.egs.empty() ? place_pipelined(ctx) : place_epochs(ctx);
   ctx->rs.active = false;
   if (rc) {
     (void)hipStreamSynchronize(ctx->side);

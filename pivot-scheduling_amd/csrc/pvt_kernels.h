@@ -115,6 +115,13 @@ struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible
   Lists L;
 };
 
+// Winner of a walked task in an epoch walk (log mode): its key (score, host); id -1 = no host.
+struct WinRec {
+  double s;
+  int32_t id;
+  int32_t pad;
+};
+
 struct CommitArgs {
   double* avail;          // global state, updated in place
   const double* dem;      // window tasks [nt][4] (for the window's minimum demand)
@@ -132,10 +139,37 @@ struct CommitArgs {
   int32_t* own_ids;       // out: hosts this walk committed to (distinct), for the next window
   int32_t* status;        // out: [0] window-local index where the walk stopped (nt = done,
                           //      -1 = spin timeout), [1] number of own_ids
-  uint32_t* started;      // set to seq when the walk starts (releases the side stream)
-  uint32_t seq;
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
+  // Group-parallel epochs (pvt_capi.hip place_epochs): with seg_off set, workgroup b walks the
+  // window tasks [seg_off[b], seg_off[b+1]) on its own (own_ids, status at b * MAX_WINDOW and
+  // 2 * b) and LOGS its commits instead of writing avail: own_a[b][4][MAX_WINDOW] = capacities
+  // of its own hosts after the walk, wres[i] = the winner of task i.
+  const int32_t* seg_off;
+  double* own_a;
+  WinRec* wres;
 };
+
+// Speculative epochs, cost_aware best-fit: segment j > 0 of an epoch was walked on the epoch's
+// start state; it is exact iff no host an earlier segment committed to (at its state after that
+// segment) is the winner of, or fits and beats the winner of, one of j's walked tasks.
+struct EpochArgs {
+  const double* dem;      // window tasks [nt][4]
+  const int32_t* anc;     // window tasks [nt]
+  const double* csum;
+  const double* bsum;
+  const int32_t* zone;
+  const int32_t* seg_off; // [nseg + 1] window-local task offsets
+  const int32_t* own_ids; // [nseg][MAX_WINDOW]
+  const double* own_a;    // [nseg][4][MAX_WINDOW]
+  const int32_t* status;  // [nseg][2]: tasks walked, own hosts
+  const WinRec* wres;     // [nt]
+  double* avail;          // apply: accepted segments' own hosts written here
+  int H, Z, nt, nseg;
+  int32_t* bad;           // [nseg] out: 1 = segment j is not exact (zeroed by the caller)
+};
+void launch_epoch_validate(const EpochArgs& a, hipStream_t st);
+void launch_epoch_apply(const EpochArgs& a, int n_accept, hipStream_t st);
+void launch_commit_segments(const CommitArgs& a, int nseg, hipStream_t st);
 
 // cost_aware first-fit with sort_hosts, as the reference runs it (cost_aware.py:118-124): the
 // hosts sorted once per group by the frozen key (perm, skey = sorted key bits; the radix sort

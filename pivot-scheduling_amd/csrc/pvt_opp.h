@@ -47,15 +47,17 @@ struct OppCommitArgs {
   int32_t* placement;     // window tasks' placements (caller order == processing order)
   uint32_t* mt;           // device MT19937 state: key[624], pos
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
-  const OppTouched* in;   // previous walk's hosts: applied to avail on entry, then touched
+  const OppTouched* in;   // previous walk's hosts (already applied to avail by
+                          // launch_opp_apply): touched for this walk
   OppTouched* out;        // this walk's own hosts for the next walk (NULL: none)
   int writeback;          // write this walk's own hosts to avail at the end
-  uint32_t* started;      // set to seq once `in` is applied (releases the next count pass)
-  uint32_t seq;
 };
 
 void launch_opp_count(const OppCountArgs& a, hipStream_t st);
 void launch_opp_commit(const OppCommitArgs& a, hipStream_t st);
+// Pipelined windows: the previous walk's commits (t->ta) written to global availability before
+// the next walk starts; an event after it releases the count pass of the window after.
+void launch_opp_apply(const OppTouched* t, double* avail, int H, hipStream_t st);
 hipError_t opp_init_attrs();
 
 }  // namespace pvt

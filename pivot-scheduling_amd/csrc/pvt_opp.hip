@@ -195,14 +195,13 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
   __builtin_amdgcn_s_waitcnt(0xc07f);
   int m = 0;
   if (A.in) {
-    // the previous walk's commits: applied to global availability (the next count pass may
-    // then start), and listed as touched with the count pass's snapshot as sa
+    // the previous walk's commits (already in global availability, launch_opp_apply): touched,
+    // with the count pass's snapshot as sa
     m = __builtin_amdgcn_readfirstlane(A.in->n);
     for (int q = lane; q < m; q += WAVE) {
       const int32_t h = A.in->tid[q];
       for (int r = 0; r < 4; r++) {
         const double t = A.in->ta[r][q];
-        A.avail[(size_t)r * A.H + h] = t;
         S.sa[r][q] = A.in->sb[r][q];
         S.ta[r][q] = t;
         S.sb[r][q] = t;
@@ -213,10 +212,7 @@ __global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
       while (atomicCAS(&S.hkey[p], -1, h) != -1) p = (p + 1) & (OPP_HASH - 1);
       S.hval[p] = q;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
   }
-  if (A.started && lane == 0)
-    __hip_atomic_store(A.started, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const bool fast = A.nsq <= WAVE;   // one super-chunk count per lane (H <= 1,048,576)
@@ -421,6 +417,19 @@ hipError_t opp_init_attrs() {
 
 void launch_opp_commit(const OppCommitArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(opp_commit_kernel, dim3(1), dim3(64), sizeof(OppLDS), st, a);
+}
+
+__global__ __launch_bounds__(256) void opp_apply_kernel(const OppTouched* t, double* avail, int H) {
+  const int n = t->n;
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int32_t h = t->tid[q];
+#pragma unroll
+    for (int r = 0; r < 4; r++) avail[(size_t)r * H + h] = t->ta[r][q];
+  }
+}
+
+void launch_opp_apply(const OppTouched* t, double* avail, int H, hipStream_t st) {
+  hipLaunchKernelGGL(opp_apply_kernel, dim3(OPP_MAXW / 256), dim3(256), 0, st, t, avail, H);
 }
 
 }  // namespace pvt

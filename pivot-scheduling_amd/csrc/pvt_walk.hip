@@ -98,6 +98,7 @@ struct WalkLDS {
   int32_t lhp[LIVE_MAX];                  // hash position of the live host
   uint32_t ltb[LIVE_MAX];
   int32_t lown[LIVE_MAX];                 // 1: committed to by this walk (in own_ids)
+  int32_t lo[LIVE_MAX];                   // its index in own_ids, once lown
   double csum[ZMAX * ZMAX];
   double bsum[ZMAX * ZMAX];
   int32_t flag[RING];
@@ -571,6 +572,7 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     }
     int wrec = -1, wx = -1;                   // winner: a scout record, or patched host wx
     bool none = false, refill = false;
+    uint64_t wk = 0;                          // best-fit: the winner's score bits
     if (BEST) {
       const int nT = rdw(rs, R_NT);
       int tb_ = -1;
@@ -628,6 +630,7 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
         if (exhausted) refill = true;         // refill from here
         else none = true;                     // no host fits: the task waits
       }
+      wk = t1;
     } else {
       // first fit: the first usable entry in list order; a patched one is re-checked exactly
 #pragma unroll
@@ -655,6 +658,10 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     if (refill) { status = i; break; }
     release_slot(S, i + 1);                   // the ring slot is no longer read
     if (none) {                               // nothing committed: the window slides
+      if (lane == 0) {
+        A.placement[caller] = -1;             // (an earlier speculative walk may have set it)
+        if (A.wres) { A.wres[i].s = DINF; A.wres[i].id = -1; }
+      }
 #pragma unroll
       for (int r = NP - 1; r > 0; r--) X[r] = X[r - 1];
       X[0].id = -1; X[0].alive = false; X[0].anc = -1;
@@ -723,11 +730,22 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
         q_after = -1;
       }
     }
+    int32_t o;                                // the host's index in own_ids
     if (!w_own) {                             // first commit of this walk to the host
-      if (lane == 0) A.own_ids[n_own] = W.id;
-      n_own++;
+      o = n_own++;
+      if (lane == 0) {
+        A.own_ids[o] = W.id;
+        if (q_after >= 0) S.lo[q_after] = o;
+      }
+    } else {
+      o = __builtin_amdgcn_readfirstlane(S.lo[W.q]);
     }
-    if (lane < 4) A.avail[(size_t)lane * A.H + W.id] = nr;
+    if (A.own_a) {                            // epoch walk: logged, applied once validated
+      if (lane < 4) A.own_a[(size_t)lane * MAX_WINDOW + o] = nr;
+      if (lane == 0) { A.wres[i].s = __longlong_as_double((long long)wk); A.wres[i].id = W.id; }
+    } else {
+      if (lane < 4) A.avail[(size_t)lane * A.H + W.id] = nr;
+    }
     if (lane == 0) A.placement[caller] = W.id;
     // the winner becomes the newest patched host (its c / b carry over when it was one)
 #pragma unroll
@@ -758,11 +776,22 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
 
 template <int MODE>
 __global__ __launch_bounds__(WALK_THREADS) void commit_kernel(CommitArgs A) {
+  if (A.seg_off) {                            // epoch walk: this workgroup's segment
+    const int b = blockIdx.x;
+    const int base = A.seg_off[b];
+    A.nt = A.seg_off[b + 1] - base;
+    A.dem += (size_t)base * 4;
+    A.L.e += (size_t)base * LMAX;
+    A.L.ids += (size_t)base * LMAX;
+    A.L.t += base;
+    A.own_ids += (size_t)b * MAX_WINDOW;
+    A.own_a += (size_t)b * 4 * MAX_WINDOW;
+    A.status += 2 * b;
+    A.wres += base;
+  }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WalkLDS& S = *reinterpret_cast<WalkLDS*>(smem);
   const int tid = threadIdx.x;
-  if (tid == 0 && A.started)    // this CU is ours: the next window's scoring may start
-    __hip_atomic_store(A.started, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   // val starts as "not dead": a loader can see a key the walker is inserting before its value
   // (loaders only act on H_DEAD, which is final, so a stale live value is merely conservative)
   for (int i = tid; i < WH_SLOTS; i += WALK_THREADS) { S.hk[i].key = H_EMPTY; S.hk[i].val = H_PENDING; }
@@ -796,9 +825,11 @@ hipError_t init_kernel_attrs() {
   return e;
 }
 
-void launch_commit(const CommitArgs& a, hipStream_t st) {
+void launch_commit(const CommitArgs& a, hipStream_t st) { launch_commit_segments(a, 1, st); }
+
+void launch_commit_segments(const CommitArgs& a, int nseg, hipStream_t st) {
   const size_t lds = WALK_LDS_BYTES;
-  const dim3 grid(1), block(WALK_THREADS);
+  const dim3 grid(nseg), block(WALK_THREADS);
   switch (a.mode) {
     case CA_FF: hipLaunchKernelGGL(commit_kernel<CA_FF>, grid, block, lds, st, a); break;
     case CA_BF: hipLaunchKernelGGL(commit_kernel<CA_BF>, grid, block, lds, st, a); break;

@@ -45,6 +45,9 @@ def load_library(path=None):
         "pvt_set_window": ([c_void_p, c_int], c_int),
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
         "pvt_set_score_tw": ([c_void_p, c_int], c_int),
+        "pvt_set_epochs": ([c_void_p, c_int], c_int),
+        "pvt_epoch_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
+                             ctypes.POINTER(ctypes.c_int64)], c_int),
         "pvt_last_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64),
                             ctypes.POINTER(ctypes.c_int64)], c_int),
         "pvt_last_error": ([c_void_p], ctypes.c_char_p),
@@ -358,6 +361,15 @@ class PlacementEngine:
 
     def set_pipeline(self, on=True):
         self._check(self.lib.pvt_set_pipeline(self.ctx, int(bool(on))))
+
+    def set_epochs(self, on=True):
+        """cost_aware best-fit: group-parallel speculative epochs (default on; identical results)."""
+        self._check(self.lib.pvt_set_epochs(self.ctx, int(bool(on))))
+
+    def epoch_stats(self):
+        e, s, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.pvt_epoch_stats(self.ctx, ctypes.byref(e), ctypes.byref(s), ctypes.byref(r)))
+        return {"epochs": e.value, "segments": s.value, "rejected": r.value}
 
     def set_profiling(self, on=True):
         self._check(self.lib.pvt_set_profiling(self.ctx, int(bool(on))))

@@ -1,0 +1,109 @@
+"""GPU parity of the group-parallel speculative epochs (cost_aware best-fit, pvt_epoch.hip):
+groups of distinct anchor zones are walked side by side on the epoch's start state and only the
+exact prefix is kept. Placements, order and availability must equal the CPU restatement and the
+sequential engine (pvt_set_epochs(0)) -- including rounds built so that groups DO collide
+(spill into other zones, exact fits, repeated anchors), which exercises rejection."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from pivot_place import _abi, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(res, ref):
+    np.testing.assert_array_equal(res.placement, ref.placement)
+    np.testing.assert_array_equal(res.order, ref.order)
+    bad = np.nonzero((res.avail != ref.avail).any(axis=0))[0]
+    assert bad.size == 0, "availability differs on hosts %s" % bad[:10]
+
+
+def _place(engine, r, epochs=True):
+    try:
+        engine.set_resident(0)
+        engine.set_epochs(epochs)
+        res = engine.place(r)
+        st = engine.epoch_stats()
+    finally:
+        engine.set_epochs(True)
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+    return res, st
+
+
+def _regroup(r, anchors):
+    """Tasks grouped by the given per-task anchors (first-seen group order)."""
+    first = {}
+    for a in anchors:
+        first.setdefault(int(a), len(first))
+    r.task_group = np.array([first[int(a)] for a in anchors], dtype=np.int32)
+    r.group_anchor = np.array(list(first.keys()), dtype=np.int32)
+    return r
+
+
+@pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70_000, 2600, 2), (200_000, 12_000, 3),
+                                      (9000, 4000, 4)])
+def test_epochs_match_oracle(engine, H, T, seed):
+    r = synthetic.make_round(_abi.PVT_CA_BF, H, T, seed=seed)
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    assert st["epochs"] >= 1 and st["segments"] >= 2
+    seq, st0 = _place(engine, r, epochs=False)
+    _same(seq, ref)
+    assert st0["epochs"] == 0
+
+
+@pytest.mark.parametrize("cpus,seed", [(1.0, 5), (2.0, 6), (4.0, 7)])
+def test_epochs_crowded_groups(engine, cpus, seed):
+    """Few small hosts: zones fill up, many tasks find no host; placements stay exact."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 8000, 6000, seed=seed)
+    r.avail[0, :] = cpus
+    r.avail[1, :] = 50000.0
+    ref = oracle.place(r, threads=8)
+    res, _ = _place(engine, r)
+    _same(res, ref)
+
+
+@pytest.mark.parametrize("seed", [10, 11])
+def test_epochs_groups_spill_and_collide(engine, seed):
+    """Zones 0-9 have no capacity: groups anchored there spill into zones 10-19, onto hosts the
+    groups anchored there want too -- speculation must be rejected and redone."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 20_000, 6000, seed=seed)
+    r.avail[:2, r.zone < 10] = 0.0
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    assert st["rejected"] > 0, st
+
+
+def test_epochs_repeated_anchor_zones(engine):
+    """40 groups over 20 zones (each zone anchors two groups): epochs split where an anchor
+    repeats."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 60_000, 8000, seed=8)
+    rs = np.random.RandomState(8)
+    groups = rs.randint(0, 40, size=r.n_tasks)
+    first = {}
+    for g in groups:
+        first.setdefault(int(g), len(first))
+    r.task_group = np.array([first[int(g)] for g in groups], dtype=np.int32)
+    r.group_anchor = np.array([g % 20 for g in first.keys()], dtype=np.int32)
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    assert st["epochs"] >= 2
+
+
+def test_epochs_exact_fits_tie_at_zero(engine):
+    """Hosts of other zones that fit a task exactly score 0 and win ties by index: the
+    validation must see a foreign host that an earlier group filled to an exact fit."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 6000, 3000, seed=9)
+    r.avail[0, :] = 1.0
+    r.avail[1, :] = 7864.32
+    r.avail[2, :] = 0.0
+    r.avail[3, :] = 0.0
+    r.dem[0, :] = 0.5
+    r.dem[1, :] = 3932.16
+    ref = oracle.place(r, threads=8)
+    res, _ = _place(engine, r)
+    _same(res, ref)
