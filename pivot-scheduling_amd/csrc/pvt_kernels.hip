@@ -11,6 +11,7 @@
 // correctly rounded (llvm.sqrt.f64 / fdiv lowering without afn/arcp).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "pvt_device.h"
 #include "pvt_kernels.h"
@@ -458,8 +459,103 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
   }
 }
 
+// Merge of a few segment lists (S <= MERGE_SMALL_S, score-pass lists): one wave per task. Keys
+// are distinct (a host is in one segment), so an entry's place in the merged order is its index
+// in its own sorted list plus, in every other list, the number of entries below it (a binary
+// search in LDS); entries land at their places directly -- no sorting network.
+constexpr int MERGE_SMALL_S = 8;
+__global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
+  __shared__ Key lk[4][MERGE_SMALL_S * KL];
+  __shared__ Key out[4][MERGE_SMALL_S * KL];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int task = blockIdx.x * 4 + wave;
+  if (task >= A.nt) return;
+  const int S = A.S, n = S * KL;
+  Key* L = lk[wave];
+  Key* O = out[wave];
+  const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
+  for (int j = lane; j < n; j += WAVE) {
+    const SegEntry se = A.seg[((size_t)task * S) * KL + j];
+    L[j] = {se.s, se.tb, se.id};
+    O[j] = inv;
+  }
+  // bound: the smallest last entry of a segment with more than KL feasible hosts
+  Key bound = inv;
+  long long tot = 0;
+  for (int g = 0; g < S; g++) {
+    const int f = A.seg_feas[(size_t)task * S + g];
+    tot += f;
+    if (f > KL) {
+      const SegEntry se = A.seg[((size_t)task * S + g) * KL + KL - 1];
+      const Key k = {se.s, se.tb, se.id};
+      if (kless(k, bound)) bound = k;
+    }
+  }
+  wave_sync();
+  int c = 0;
+  for (int j = lane; j < n; j += WAVE) {
+    const Key x = L[j];
+    if (x.id == 0x7fffffff || !kless(x, bound)) continue;   // invalid, or at/after the bound
+    const int g = j / KL;
+    int pos = j - g * KL;
+    for (int h = 0; h < S; h++) {
+      if (h == g) continue;
+      const Key* Lh = L + h * KL;
+      int lo = 0, hi = KL;                                   // entries of list h below x
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (kless(Lh[mid], x)) lo = mid + 1;
+        else hi = mid;
+      }
+      pos += lo;
+    }
+    O[pos] = x;
+    c++;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  wave_sync();
+  const int cnt = c;
+  const bool complete = (bound.id == 0x7fffffff) && tot <= LMAX;
+  Key bnd = bound;
+  if (cnt == LMAX && kless(O[LMAX - 1], bnd)) bnd = O[LMAX - 1];
+  const int nw = max(cnt, KL);
+  for (int j = lane; j < nw; j += WAVE) {
+    ListEntry e;
+    const bool valid = j < cnt;
+    const Key k = valid ? O[j] : inv;
+    const int h = valid ? k.id : 0;
+    e.s = k.s; e.tb = k.tb; e.id = k.id; e.pad = 0; e.pad2 = 0.0;
+    e.zone = valid ? A.zone[h] : 0;
+    e.a[0] = valid ? A.avail[h] : 0.0;
+    e.a[1] = valid ? A.avail[(size_t)A.H + h] : 0.0;
+    e.a[2] = valid ? A.avail[2 * (size_t)A.H + h] : 0.0;
+    e.a[3] = valid ? A.avail[3 * (size_t)A.H + h] : 0.0;
+    A.L.e[(size_t)task * LMAX + j] = e;
+    A.L.ids[(size_t)task * LMAX + j] = valid ? k.id : 0x7fffffff;
+  }
+  if (lane < 4) {
+    double* tr = reinterpret_cast<double*>(&A.L.t[task]);
+    tr[lane] = A.dem[(size_t)task * 4 + lane];
+  }
+  if (lane == 0) {
+    TaskRec& r = A.L.t[task];
+    r.cnt = cnt;
+    r.complete = complete;
+    r.anc = A.anc[task];
+    r.ord = A.ord[task];
+    r.bs = bnd.s; r.btb = bnd.tb; r.bid = bnd.id;
+  }
+}
+
 void launch_merge(const MergeArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
+  static const int small = [] {
+    const char* e = getenv("PVT_MERGE_SMALL");   // A/B experiments: 0 = bitonic merge always
+    return e ? atoi(e) : 1;
+  }();
+  if (small && a.seg_feas != nullptr && a.SL == KL && a.S <= MERGE_SMALL_S)
+    hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -90,6 +90,14 @@ def simulate(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0
     """Run one reference simulation; record its rounds unless ``cls`` (a scheduler class to
     run instead of the reference policy) is given. ``meter_out``: a list that receives
     (meter, cluster) after the run (make_meter_logs.py)."""
+    return setup(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed, cls,
+                 meter_out)()
+
+
+def setup(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0, cls=None,
+          meter_out=None):
+    """Build one reference simulation (cluster, scheduler, trace generator: everything up to
+    ``env.run()``) and return a callable that runs it and returns the trace dict."""
     import numpy as np
     from resources.meter import Meter
     from pivot_place import des
@@ -170,6 +178,13 @@ def simulate(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0
     cluster.start()
     sched.start()
     load_gen.start()
+    return lambda: _run(env, meter, cluster, load_gen, rounds, stats, recording, meter_out,
+                        label, policy, kwargs, seed, n_hosts, n_apps, job_file)
+
+
+def _run(env, meter, cluster, load_gen, rounds, stats, recording, meter_out, label, policy,
+         kwargs, seed, n_hosts, n_apps, job_file):
+    import numpy as np
     t0 = time.time()
     env.run()
     wall = time.time() - t0
@@ -192,6 +207,86 @@ def simulate(mg, world, label, policy, kwargs, n_hosts, n_apps, job_file, seed=0
     return compact({"name": label, "policy": policy, "kwargs": kwargs, "seed": seed,
                     "n_hosts": n_hosts, "n_apps": n_apps, "job_file": job_file, "e2e": e2e,
                     "rounds": rounds})
+
+
+def lockstep_main(mg, world, names):
+    """Run the named simulations SIDE BY SIDE through pivot_place.lockstep.LockstepDriver (one
+    thread each; every engine call batched across them), with the drop-in policies and the CPU
+    restatement behind the batched engine contract; print one JSON line: each simulation's
+    end-to-end results and the driver's batching counters. Each simulation keeps its own
+    uuid4 stream and its own global numpy RNG stream (the reference draws from np.random while
+    hosts pull predecessor data, resources/__init__.py:266), exactly as when it runs alone."""
+    import random
+    import threading
+    import uuid
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from oracle import oracle
+    from pivot_place.lockstep import LockstepDriver
+
+    class BatchOracle:
+        def place(self, r):
+            return oracle.place(r)
+
+        def place_batch(self, rounds):
+            return [oracle.place(r) for r in rounds]
+
+        def anchor(self, off, lst, zone, inst_host=None):
+            mode, az, rc = oracle.anchor(off, lst, zone, len(zone), inst_host)
+            assert rc == 0
+            return mode, az
+
+    local = threading.local()
+    main = {"rng": None}
+
+    def uuid4():
+        rng = getattr(local, "uuid_rng", None) or main["rng"]
+        return uuid.UUID(int=rng.getrandbits(128), version=4)
+
+    class ThreadRnd:
+        """numpy.random as the reference's modules see it: the running thread's own stream."""
+        def __getattr__(self, name):
+            rs = getattr(local, "np_rs", None)
+            return getattr(rs if rs is not None else np.random, name)
+
+    import resources
+    uuid.uuid4 = uuid4
+    specs = {}
+    for cfg, n_hosts, n_apps, job_file, pols in CONFIGS:
+        for label, policy, kwargs in pols:
+            specs["sim_%s_%s" % (cfg, label)] = (policy, kwargs, n_hosts, n_apps, job_file)
+    runs = []
+    for name in names:
+        policy, kwargs, n_hosts, n_apps, job_file = specs[name]
+        rng = random.Random(zlib.crc32(name.encode()))
+        main["rng"] = rng
+        mg._seed_uuid = lambda seed: None          # setup() would re-seed the global stream
+        go = setup(mg, world, name, policy, kwargs, n_hosts, n_apps, job_file,
+                   cls=dropin_class(policy, None))
+        rs = np.random.RandomState()
+        rs.set_state(np.random.get_state())        # this simulation's stream after its setup
+        runs.append((name, go, rng, rs))
+    saved_rnd = resources.rnd
+    resources.rnd = ThreadRnd()
+
+    def sim(name, go, rng, rs):
+        def f(engine):
+            local.uuid_rng, local.np_rs, local.engine = rng, rs, engine
+            return go()["e2e"]
+        return f
+
+    # the drop-in classes take their engine from the running thread: each simulation's
+    # policy sees its own SimEngine proxy
+    from pivot_place import policies
+    saved = policies.PlacementMixin._engine
+    policies.PlacementMixin._engine = lambda self: local.engine
+    try:
+        driver = LockstepDriver(BatchOracle())
+        out = driver.run([sim(*x) for x in runs])
+    finally:
+        resources.rnd = saved_rnd
+        policies.PlacementMixin._engine = saved
+    print(json.dumps({"names": names, "e2e": out, "stats": driver.stats}))
 
 
 def compact(tr):
@@ -255,6 +350,9 @@ def main():
                     print(json.dumps(tr["e2e"]))
                     return
         raise SystemExit("unknown trace %s" % name)
+    if sys.argv[1:2] == ["--lockstep"]:
+        lockstep_main(mg, world, sys.argv[2:])
+        return
     which = sys.argv[1:]
     for cfg, n_hosts, n_apps, job_file, pols in CONFIGS:
         for label, policy, kwargs in pols:
