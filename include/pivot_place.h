@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PVT_ABI_VERSION 1
+#define PVT_ABI_VERSION 2
 
 /* Return codes. */
 #define PVT_OK            0
@@ -69,6 +69,12 @@ enum pvt_mode {
  * group_anchor[g] is the anchor storage zone. Groups run in id order; tasks of a group in
  * caller order, stably sorted by descending ||d||2 when sort_tasks is set. For the other
  * policies pass task_group = NULL (one group holding every task).
+ *
+ * realtime_bw (cost_aware, scheduler/cost_aware.py:17,79,112): rt_bw[g*H + h] is the bandwidth
+ * the reference uses instead of the static one for group g (0 without task_group) and host h,
+ * in_route.realtime_bw + out_route.realtime_bw of the routes between g's anchor storage and h
+ * (resources/network.py:70-73: 1 / ((queued MB + 1) / bw) per route, summed in that order). NULL:
+ * the static bw[a][z] + bw[z][a].
  */
 typedef struct pvt_round {
   int32_t mode;          /* enum pvt_mode                                                 */
@@ -91,6 +97,7 @@ typedef struct pvt_round {
   int32_t* order;        /* [T] out: processing order (task indices)                      */
   int32_t* placement;    /* [T] out: host index, -1 = not placed (task stays waiting)     */
   uint32_t* mt_state;    /* HOST [625] in/out: MT19937 key[624] then pos (PVT_OPP)        */
+  const double* rt_bw;   /* [G*H] realtime bandwidth per (group, host), or NULL (cost_aware) */
 } pvt_round;
 
 typedef struct pvt_ctx pvt_ctx;

@@ -62,6 +62,7 @@ def place(r, threads=0):
     s.cost, s.bw, s.dem = _ptr(r.cost), _ptr(r.bw), _ptr(r.dem)
     s.task_group, s.group_anchor = _ptr(r.task_group), _ptr(r.group_anchor)
     s.order, s.placement, s.mt_state = _ptr(order), _ptr(placement), _ptr(mt)
+    s.rt_bw = _ptr(r.rt_bw)
     if threads > 0:
         check_rc(lib().oracle_place_mt(ctypes.addressof(s), int(threads)))
     else:

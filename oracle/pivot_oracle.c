@@ -115,9 +115,18 @@ static int group_tasks(const pvt_round* r, int g, int sort, keyed* scratch, int3
   return n;
 }
 
+/* The bandwidth of cost_aware's host_score_func (cost_aware.py:73-79, :106-112): the static
+ * in_route.bw + out_route.bw = bw[a][z] + bw[z][a], or with realtime_bw the caller's
+ * in_route.realtime_bw + out_route.realtime_bw of group g and host h. */
+static inline double ca_bw(const pvt_round* r, int g, int anchor, int h) {
+  const int Z = r->n_zones, z = r->zone[h];
+  if (r->rt_bw) return r->rt_bw[(size_t)g * r->n_hosts + h];
+  return r->bw[anchor * Z + z] + r->bw[z * Z + anchor];
+}
+
 /* ---------------------------------------------------------------- policies */
 /* cost_aware _first_fit (cost_aware.py:99-127). */
-static void ca_first_fit(const pvt_round* r, const int32_t* tasks, int n, int anchor,
+static void ca_first_fit(const pvt_round* r, const int32_t* tasks, int n, int g, int anchor,
                          keyed* hs) {
   int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
   for (int h = 0; h < H; h++) { hs[h].i = h; hs[h].k = 0.0; }
@@ -127,7 +136,7 @@ static void ca_first_fit(const pvt_round* r, const int32_t* tasks, int n, int an
       double a[4]; host_vec(r->avail, H, h, a);
       double rn = oracle_norm4(a);
       int z = r->zone[h];
-      double bw = r->bw[anchor * Z + z] + r->bw[z * Z + anchor];
+      double bw = ca_bw(r, g, anchor, h);
       double c = r->cost[anchor * Z + z] + r->cost[z * Z + anchor];
       double df = r->decay ? (double)r->decay[h] : 1.0;
       hs[h].k = c * df / (rn * bw);
@@ -150,7 +159,7 @@ static void ca_first_fit(const pvt_round* r, const int32_t* tasks, int n, int an
 }
 
 /* cost_aware _best_fit (cost_aware.py:63-97); host_decay is rejected by the caller. */
-static void ca_best_fit(const pvt_round* r, const int32_t* tasks, int n, int anchor) {
+static void ca_best_fit(const pvt_round* r, const int32_t* tasks, int n, int g, int anchor) {
   int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
   for (int j = 0; j < n; j++) {
     int t = tasks[j];
@@ -162,7 +171,7 @@ static void ca_best_fit(const pvt_round* r, const int32_t* tasks, int n, int anc
       double x[4] = {a[0] - d[0], a[1] - d[1], a[2] - d[2], a[3] - d[3]};
       double rn = oracle_norm4(x);
       int z = r->zone[h];
-      double bw = r->bw[anchor * Z + z] + r->bw[z * Z + anchor];
+      double bw = ca_bw(r, g, anchor, h);
       double c = r->cost[anchor * Z + z] + r->cost[z * Z + anchor];
       double s = c * rn * 1.0 / bw;              /* t * r * decay / bw (:83), decay == 1 */
       if (best < 0 || s < bs) { best = h; bs = s; }   /* min(): first minimum (:92) */
@@ -244,8 +253,8 @@ int oracle_place(const pvt_round* r) {
         int n = group_tasks(r, g, r->sort_tasks, ks, r->order + off);
         keyed* hs = (keyed*)malloc(sizeof(keyed) * (size_t)H);
         if (!hs) { rc = PVT_ENOMEM; break; }
-        if (r->mode == PVT_CA_FF) ca_first_fit(r, r->order + off, n, anchor, hs);
-        else ca_best_fit(r, r->order + off, n, anchor);
+        if (r->mode == PVT_CA_FF) ca_first_fit(r, r->order + off, n, g, anchor, hs);
+        else ca_best_fit(r, r->order + off, n, g, anchor);
         free(hs);
         off += n;
       }
@@ -291,7 +300,7 @@ static inline int cand_less(cand a, cand b) {   /* (s, tb, h) lexicographic; h <
 
 /* Best host of one task: mode CA_BF (>=, egress score), VBP_BF (>, norm, tiebreak), first-fit
  * by index (strict or not), or first-fit over hosts in `hs` key order (CA_FF sort_hosts). */
-static int32_t mt_pick(const pvt_round* r, int mode, const double d[4], int anchor,
+static int32_t mt_pick(const pvt_round* r, int mode, const double d[4], int g, int anchor,
                        const keyed* hs, int threads) {
   const int H = r->n_hosts, Z = r->n_zones;
   cand best = {0.0, 0u, -1};
@@ -306,7 +315,7 @@ static int32_t mt_pick(const pvt_round* r, int mode, const double d[4], int anch
         if (!fits_ge(a, d)) continue;
         double x[4] = {a[0] - d[0], a[1] - d[1], a[2] - d[2], a[3] - d[3]};
         int z = r->zone[h];
-        double bw = r->bw[anchor * Z + z] + r->bw[z * Z + anchor];
+        double bw = ca_bw(r, g, anchor, h);
         double c = r->cost[anchor * Z + z] + r->cost[z * Z + anchor];
         cand k = {c * oracle_norm4(x) * 1.0 / bw, 0u, h};
         if (cand_less(k, mine)) mine = k;
@@ -372,7 +381,7 @@ int oracle_place_mt(const pvt_round* r, int threads) {
       for (int h = 0; h < H; h++) {
         double a[4]; host_vec(r->avail, H, h, a);
         int z = r->zone[h];
-        double bw = r->bw[anchor * Z + z] + r->bw[z * Z + anchor];
+        double bw = ca_bw(r, g, anchor, h);
         double c = r->cost[anchor * Z + z] + r->cost[z * Z + anchor];
         double df = r->decay ? (double)r->decay[h] : 1.0;
         hs[h].i = h;
@@ -384,7 +393,7 @@ int oracle_place_mt(const pvt_round* r, int threads) {
     for (int j = 0; j < n; j++) {
       const int t = r->order[off + j];
       double d[4]; task_vec(r->dem, T, t, d);
-      const int32_t h = mt_pick(r, r->mode, d, anchor, order, threads);
+      const int32_t h = mt_pick(r, r->mode, d, g, anchor, order, threads);
       if (h >= 0) { r->placement[t] = h; commit(r->avail, H, h, d); }
     }
     off += n;

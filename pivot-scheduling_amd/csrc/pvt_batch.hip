@@ -180,7 +180,8 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
     __builtin_amdgcn_s_waitcnt(0xc07f);
   }
 
-  int cur_anc = -1, cur_grp = -1;
+  int cur_anc = -1, cur_grp = -1, cur_bgrp = -1;
+  const bool rt = (MODE == CA_FF || MODE == CA_BF) && R.rt_bw != nullptr;
   for (int p0 = 0; p0 < T; p0 += RES_CHUNK) {
     const int n = min(RES_CHUNK, T - p0);
     __syncthreads();                      // the previous chunk (and the sort keys) are consumed
@@ -230,10 +231,16 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
       }
       if (CA) {
         const int anc = anc_q;
-        if (anc != cur_anc) {             // anchor rows of the zone tables -> registers
+        // anchor rows of the zone tables -> registers; realtime_bw (cost_aware.py:79,112): the
+        // bandwidth is the group's per-host row instead
+        if (anc != cur_anc || (rt && grp_q != cur_bgrp)) {
           cur_anc = anc;
+          cur_bgrp = grp_q;
 #pragma unroll
-          for (int j = 0; j < HPL; j++) { cc[j] = csum[anc * Z + zz[j]]; bb[j] = bsum[anc * Z + zz[j]]; }
+          for (int j = 0; j < HPL; j++) {
+            cc[j] = csum[anc * Z + zz[j]];
+            bb[j] = rt ? (h0 + j < H ? R.rt_bw[(size_t)grp_q * H + h0 + j] : 1.0) : bsum[anc * Z + zz[j]];
+          }
         }
       }
       if (MODE == CA_FF && keyed) {

@@ -30,12 +30,18 @@
 
 using namespace pvt;
 
-// Group-parallel epochs (cost_aware best-fit): at most EPOCH_SEGS segments (one walk workgroup
-// each, <= MAX_WINDOW tasks) and EPOCH_MAX tasks per epoch (its lists: 64 B x LMAX per task).
+// Group-parallel epochs (cost_aware best-fit): at most EPOCH_SEGS group segments, walked in at
+// most EPOCH_SEGS chains of <= CHAIN_MAX tasks, and EPOCH_MAX tasks per epoch (its lists: 64 B
+// x LMAX per task).
 static constexpr int EPOCH_SEGS = 64;
 static constexpr int EPOCH_MAX = 16384;
-// ep_dev / ep_host words: seg_off [EPOCH_SEGS + 1], status [2 x EPOCH_SEGS], bad [EPOCH_SEGS]
-static constexpr int EP_OFF = 0, EP_STATUS = EPOCH_SEGS + 1, EP_BAD = EP_STATUS + 2 * EPOCH_SEGS;
+// ep_dev / ep_host words: uploaded [seg_off | seg_chain | seg_cstart | coff | csoff | cseg |
+// cmap], then read back [status (2 per chain) | bad (per segment)]
+static constexpr int EP_SEG_OFF = 0, EP_SEG_CHAIN = EP_SEG_OFF + EPOCH_SEGS + 1,
+                     EP_SEG_CSTART = EP_SEG_CHAIN + EPOCH_SEGS, EP_COFF = EP_SEG_CSTART + EPOCH_SEGS,
+                     EP_CSOFF = EP_COFF + EPOCH_SEGS + 1, EP_CSEG = EP_CSOFF + EPOCH_SEGS + 1,
+                     EP_CMAP = EP_CSEG + EPOCH_SEGS, EP_STATUS = EP_CMAP + EPOCH_MAX,
+                     EP_BAD = EP_STATUS + 2 * EPOCH_SEGS;
 static constexpr int EP_WORDS = EP_BAD + EPOCH_SEGS;
 
 struct Buf {
@@ -59,13 +65,14 @@ struct RoundState {
   int kn = 0;                     // hosts in the current order (prefix length in mode 1)
   bool kstall = false;            // a walk found a prefix list exhausted: sort the rest
   int32_t* ord = nullptr;         // processing order (ctx scratch)
-  std::vector<int> gstart, ganchor;
+  std::vector<int> gstart, ganchor, gid;   // keyed groups: starts, anchors, caller's group ids
   size_t g = 0, ngroups = 0;
   int key_group = -1;             // group whose frozen first-fit key is computed
   int t0 = 0, W = 0, Wmax = 0, nt = 0;
   int lb = 0;                     // list buffer of the current window
   std::vector<int> egs, ega;      // cost_aware best-fit epochs: group starts (+ T) and anchors
   std::vector<int> ecomp;         // zone -> its component of zones joined by zero egress cost
+  bool in_epoch = false;          // lists scored for an epoch (place_epochs)
 };
 
 struct pvt_ctx {
@@ -83,7 +90,7 @@ struct pvt_ctx {
   std::vector<hipEvent_t> evpool;
   std::vector<TimedLaunch> pending;
   // scratch
-  Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, csum, bsum, key,
+  Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, grp_ord, csum, bsum, key,
       seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, kskey, kperm, kiota, ksorttmp, kflag;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
   int keyed_scan = 1;             // keyed first-fit: sorted host order + early-exit scan
@@ -91,7 +98,7 @@ struct pvt_ctx {
   int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
   int epochs = 1;                 // cost_aware best-fit: group-parallel speculative epochs
   int64_t n_epochs = 0, n_segs = 0, n_rejected = 0;
-  Buf ep_dev, own_a, wres;        // epoch descriptors / status / flags, own-host logs, winners
+  Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
   std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
   std::vector<uint32_t> rmt_host;
@@ -251,11 +258,11 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   if (ctx->side) (void)hipStreamSynchronize(ctx->side);
   harvest(ctx);
   Buf* bufs[] = {&ctx->ord, &ctx->ord2, &ctx->keys64a, &ctx->keys64b, &ctx->keys32a, &ctx->keys32b,
-                 &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->csum, &ctx->bsum, &ctx->key,
+                 &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->grp_ord, &ctx->csum, &ctx->bsum, &ctx->key,
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
-                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->own_a, &ctx->wres};
+                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -362,11 +369,17 @@ static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
 // about KL * (1 + ln(H / (S * KL))) serial insertions per segment, S times per task. Fewer,
 // longer segments halve those insertions at 16 (measured: 29.7 -> 26.2 ms of score per
 // 1M x 10k round); cost_aware's zero-cost zone fills its lists at once and wants the waves.
-static int choose_segments(int H, int nt, int mode, int force_tw) {
+static int choose_segments(int H, int nt, int mode, int force_tw, bool epoch) {
   const int tw = score_tasks_per_wave(mode, H, force_tw);
   const int task_waves = (nt + tw - 1) / tw;
   int S = (4096 + task_waves - 1) / task_waves;
   if (mode == PVT_VBP_BF) S = std::min(S, 16);
+  // cost_aware best-fit over many tasks (epochs): each segment fills its list from the zero-cost
+  // zones' lowest-index hosts and exits early, so fewer, longer segments stream fewer hosts per
+  // task -- but a merged list of S x 64 entries must stay deep enough for a whole group's walk
+  // (config 5 ca_bf epoch of 10k tasks: S = 2 -> 5.6 ms, 4 -> 4.1, 8 -> 4.8; S = 2 refills;
+  // config 3, 1k tasks: 8 -> 0.82 ms, 4 -> 0.73)
+  if (mode == PVT_CA_BF && epoch) S = 4;
   if (const char* e = getenv("PVT_SEGMENTS")) S = std::max(1, atoi(e));   // tuning experiments
   S = std::min(S, std::max(1, H / 4096));
   S = std::min(S, std::max(MAX_SEG, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL))));
@@ -469,7 +482,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   S = (nsq + seg_sup - 1) / seg_sup;
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
-  launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord),
+  launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord), nullptr,
                       P<int32_t>(ctx->anc_ord), st);
   // Pipelined windows (W <= OPP_MAXW / 2, so a walk's inherited + own touched hosts fit its
   // LDS): window k+1's count pass runs on the side stream while window k is walked. Walk k
@@ -544,6 +557,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   R.t0 = 0; R.g = 0; R.nt = 0; R.lb = 0;
   R.gstart.assign(1, 0);
   R.ganchor.clear();
+  R.gid.clear();
   if (T == 0) { R.ngroups = 0; R.active = true; return PVT_OK; }
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
@@ -553,7 +567,8 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
 
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
-  launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
+  ENSURE(ctx->grp_ord, sizeof(int32_t) * T);
+  launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord), P<int32_t>(ctx->grp_ord),
                       P<int32_t>(ctx->anc_ord), st);
   const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
   if (ca) {
@@ -586,10 +601,12 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
         if (cnt[g] == 0) continue;
         R.gstart.push_back(off);
         R.ganchor.push_back(ga[g]);
+        R.gid.push_back(g);
         off += cnt[g];
       }
     } else {
       R.ganchor.push_back(0);
+      R.gid.push_back(0);
     }
     ENSURE(ctx->key, sizeof(double) * H);
     ENSURE(ctx->next, sizeof(int32_t) * 4);
@@ -676,7 +693,8 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
   }
   if (R.keyed && R.key_group != (int)R.g && R.hi > R.lo) {
     KeyArgs ka{R.r.avail, R.r.zone, R.r.decay, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z,
-               R.ganchor[R.g], R.lo, R.hi, P<double>(ctx->key)};
+               R.ganchor[R.g], R.lo, R.hi, P<double>(ctx->key),
+               R.r.rt_bw ? R.r.rt_bw + (size_t)R.gid[R.g] * R.H : nullptr};
     Scope sc(ctx, PVT_K_OTHER, 0, 0);
     launch_key(ka, ctx->stream);
     if (R.kscan) {
@@ -734,12 +752,13 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
     Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
     launch_ordered(oa, st);
   } else {
-    const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw);
+    const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw, R.in_epoch);
     ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)nt * S * KL);
     ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)nt * S);
     ScoreArgs sa{r->avail, r->zone, r->tiebreak, R.keyed ? P<double>(ctx->key) : nullptr,
                  dem_w, anc_w, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z, nt, S,
-                 R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), ctx->score_tw};
+                 R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), ctx->score_tw,
+                 r->mode == PVT_CA_BF ? r->rt_bw : nullptr, P<int32_t>(ctx->grp_ord) + t0};
     {
       Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
       launch_score(r->mode, sa, st);
@@ -765,7 +784,8 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
   CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
                  P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
                  r->placement, P<int32_t>(ctx->owned[1 - lb]), n_prev, P<int32_t>(ctx->owned[lb]),
-                 status, ctx->stamps};
+                 status, r->mode == PVT_CA_BF ? r->rt_bw : nullptr, P<int32_t>(ctx->grp_ord) + t0,
+                 ctx->stamps};
   {
     Scope sc(ctx, PVT_K_COMMIT, 0, 0);
     launch_commit(ca_, st);
@@ -913,27 +933,42 @@ static int epoch_groups(pvt_ctx* ctx) {
   return PVT_OK;
 }
 
-// The next epoch from task t0: consecutive group segments whose anchors lie in distinct
-// zero-cost components (two groups of one component compete for the same hosts: the second
-// would be rejected), each at most
-// MAX_WINDOW tasks; a segment that ends inside its group ends the epoch (the rest of the group
-// depends on it). Returns the segment offsets relative to t0 in off (off[0] = 0).
-static void epoch_plan(const RoundState& R, int t0, std::vector<int>& off) {
-  off.assign(1, 0);
+// The next epoch from task t0: consecutive group segments (processing order), each assigned to
+// the chain of its anchor's zero-cost component (two groups of one component compete for the
+// same hosts: one walk takes them in order). A chain holds at most CHAIN_MAX tasks; a segment
+// that ends inside its group ends the epoch (the rest of the group depends on it).
+struct EpochPlan {
+  std::vector<int> off, chain, cstart;     // segments: window offsets (+ end), chain, start in it
+  std::vector<std::vector<int>> segs;      // chains: their segments
+  std::vector<int> len;                    // chains: tasks
+};
+
+static void epoch_plan(const RoundState& R, int t0, EpochPlan& P) {
+  P.off.assign(1, 0);
+  P.chain.clear(); P.cstart.clear(); P.segs.clear(); P.len.clear();
   size_t g = 0;
   while (g + 1 < R.egs.size() && R.egs[g + 1] <= t0) g++;
-  std::vector<int> zones;
+  std::vector<int> chain_of(R.ecomp.size() + 1, -1);
   int t = t0;
-  while (t < R.T && (int)off.size() <= EPOCH_SEGS) {
+  while (t < R.T && (int)P.chain.size() < EPOCH_SEGS) {
     const int ge = R.egs[g + 1];
-    const int a = (R.ega[g] >= 0 && R.ega[g] < (int)R.ecomp.size()) ? R.ecomp[R.ega[g]] : R.ega[g];
-    if (off.size() > 1 && std::find(zones.begin(), zones.end(), a) != zones.end()) break;
-    const int e = std::min({ge, t + MAX_WINDOW, t0 + EPOCH_MAX});
-    if (e <= t) break;
-    off.push_back(e - t0);
-    zones.push_back(a);
-    t = e;
-    if (e < ge) break;
+    const int z = R.ega[g];
+    const int comp = (z >= 0 && z < (int)R.ecomp.size()) ? R.ecomp[z] : (int)R.ecomp.size();
+    int c = chain_of[comp];
+    if (c < 0) {
+      c = chain_of[comp] = (int)P.segs.size();
+      P.segs.emplace_back();
+      P.len.push_back(0);
+    }
+    const int take = std::min({ge - t, CHAIN_MAX - P.len[c], t0 + EPOCH_MAX - t});
+    if (take <= 0) break;
+    P.segs[c].push_back((int)P.chain.size());
+    P.chain.push_back(c);
+    P.cstart.push_back(P.len[c]);
+    P.len[c] += take;
+    t += take;
+    P.off.push_back(t - t0);
+    if (t < ge) break;
     g++;
   }
 }
@@ -943,25 +978,26 @@ static int place_epochs(pvt_ctx* ctx) {
   const pvt_round* r = &R.r;
   hipStream_t st = ctx->stream;
   ENSURE(ctx->ep_dev, sizeof(int32_t) * EP_WORDS);
-  ENSURE(ctx->own_a, sizeof(double) * 4 * (size_t)MAX_WINDOW * EPOCH_SEGS);
   ENSURE(ctx->wres, sizeof(WinRec) * (size_t)EPOCH_MAX);
-  ENSURE(ctx->owned[0], sizeof(int32_t) * (size_t)MAX_WINDOW * EPOCH_SEGS);
+  ENSURE(ctx->owned[0], sizeof(int32_t) * (size_t)CHAIN_MAX);
   ENSURE(ctx->l_e[0], sizeof(ListEntry) * (size_t)EPOCH_MAX * LMAX);
   ENSURE(ctx->l_ids[0], sizeof(int32_t) * (size_t)EPOCH_MAX * LMAX);
   ENSURE(ctx->l_t[0], sizeof(TaskRec) * (size_t)EPOCH_MAX);
   int32_t* dev = P<int32_t>(ctx->ep_dev);
   int32_t* host = ctx->ep_host;
-  std::vector<int> off;
+  EpochPlan E;
   int t0 = 0, rc;
+  R.in_epoch = true;
+  struct Reset { bool& f; ~Reset() { f = false; } } reset_{R.in_epoch};
   while (t0 < R.T) {
-    epoch_plan(R, t0, off);
-    const int nseg = (int)off.size() - 1, nt = off.back();
+    epoch_plan(R, t0, E);
+    const int nseg = (int)E.chain.size(), nch = (int)E.segs.size(), nt = E.off.back();
     ctx->n_epochs++;
     ctx->n_segs += nseg;
     if ((rc = window_lists(ctx, t0, nt, 0, st))) return rc;
     Lists L;
     lists_from(ctx, L, 0);
-    if (nseg == 1) {                          // one segment: the plain walk (writes avail)
+    if (nch == 1) {                           // one chain: the plain walk (writes avail)
       if ((rc = walk_launch(ctx, t0, nt, 0, 0))) return rc;
       int adv = 0;
       if ((rc = walk_status(ctx, t0, nt, false, &adv))) return rc;
@@ -969,22 +1005,35 @@ static int place_epochs(pvt_ctx* ctx) {
       t0 += adv;
       continue;
     }
-    for (int k = 0; k <= nseg; k++) host[EP_OFF + k] = off[k];
-    HIPCHK(hipMemcpyAsync(dev + EP_OFF, host + EP_OFF, sizeof(int32_t) * (nseg + 1),
-                          hipMemcpyHostToDevice, st));
+    // chain tables, in one upload
+    for (int k = 0; k <= nseg; k++) host[EP_SEG_OFF + k] = E.off[k];
+    for (int k = 0; k < nseg; k++) { host[EP_SEG_CHAIN + k] = E.chain[k]; host[EP_SEG_CSTART + k] = E.cstart[k]; }
+    int nm = 0, ns = 0;
+    for (int c = 0; c < nch; c++) {
+      host[EP_COFF + c] = nm;
+      host[EP_CSOFF + c] = ns;
+      for (int sg : E.segs[c]) {
+        host[EP_CSEG + ns++] = E.cstart[sg];
+        for (int w = E.off[sg]; w < E.off[sg + 1]; w++) host[EP_CMAP + nm++] = w;
+      }
+    }
+    host[EP_COFF + nch] = nm;
+    host[EP_CSOFF + nch] = ns;
+    HIPCHK(hipMemcpyAsync(dev, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(dev + EP_BAD, 0, sizeof(int32_t) * nseg, st));
     CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
                    P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
                    r->placement, nullptr, 0, P<int32_t>(ctx->owned[0]), dev + EP_STATUS,
-                   ctx->stamps, dev + EP_OFF, P<double>(ctx->own_a), P<WinRec>(ctx->wres)};
+                   r->rt_bw, P<int32_t>(ctx->grp_ord) + t0, ctx->stamps, dev + EP_COFF, dev + EP_CMAP, dev + EP_CSOFF, dev + EP_CSEG,
+                   P<WinRec>(ctx->wres)};
     {
       Scope sc(ctx, PVT_K_COMMIT, 0, 0);
-      launch_commit_segments(ca_, nseg, st);
+      launch_commit_chains(ca_, nch, st);
     }
     EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
-                 P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_OFF,
-                 P<int32_t>(ctx->owned[0]), P<double>(ctx->own_a), dev + EP_STATUS,
-                 P<WinRec>(ctx->wres), r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD};
+                 P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_SEG_OFF,
+                 dev + EP_SEG_CHAIN, dev + EP_SEG_CSTART, dev + EP_STATUS, P<WinRec>(ctx->wres),
+                 r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD, r->rt_bw, P<int32_t>(ctx->grp_ord) + t0};
     {
       Scope sc(ctx, PVT_K_OTHER, 0, 0);
       launch_epoch_validate(ea, st);
@@ -994,21 +1043,23 @@ static int place_epochs(pvt_ctx* ctx) {
                           hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     // the exact prefix: segments before the first rejected one, up to and including the first
-    // that stopped early (its walked tasks are exact; the next epoch starts where it stopped)
+    // that its chain did not finish (its walked tasks are exact; the next epoch starts there)
+    for (int c = 0; c < nch; c++)
+      if (host[EP_STATUS + 2 * c] == -1)
+        return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out (epoch at task %d)", t0);
     int acc = 0, next = t0;
     for (int j = 0; j < nseg; j++) {
-      const int adv = host[EP_STATUS + 2 * j], len = off[j + 1] - off[j];
-      if (adv == -1) return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out at task %d", t0 + off[j]);
-      if (adv < 0 || adv > len) return fail(ctx, PVT_EHIP, "epoch walk returned %d of %d", adv, len);
+      const int len = E.off[j + 1] - E.off[j];
+      const int adv = std::max(0, std::min(len, host[EP_STATUS + 2 * E.chain[j]] - E.cstart[j]));
       if (j > 0 && host[EP_BAD + j]) { ctx->n_rejected += nseg - j; break; }
       acc = j + 1;
-      next = t0 + off[j] + adv;
+      next = t0 + E.off[j] + adv;
       if (adv < len) { ctx->refills++; ctx->n_rejected += nseg - j - 1; break; }
     }
     if (next == t0) return fail(ctx, PVT_EHIP, "epoch made no progress at task %d", t0);
     {
       Scope sc(ctx, PVT_K_OTHER, 0, 0);
-      launch_epoch_apply(ea, acc, st);
+      launch_epoch_apply(ea, acc, nch, st);
     }
     HIPCHK(hipGetLastError());
     t0 = next;

@@ -2,23 +2,26 @@
 //
 // The reference runs its groups one after the other (scheduler/cost_aware.py:37-42), each task
 // taking the minimum of (c * ||avail - d||) / bw over every feasible host and committing before
-// the next (:85-97). The groups of a round usually anchor to different zones, and a group's
-// winners are its own zone's free-egress hosts, so consecutive groups rarely touch the same
-// hosts. An epoch therefore walks up to EPOCH_SEGMENTS groups side by side, each on the
-// epoch's start state (one commit-walk workgroup per group, logging its commits), and then
-// proves, exactly, which of them the sequential order would have produced:
+// the next (:85-97). A group's winners are the lowest-index fitting hosts of the zones its
+// anchor reaches at zero egress cost (score 0), so groups anchored in different zero-cost
+// components rarely touch the same hosts. An epoch splits its groups (segments, processing
+// order) into chains, one per component: one commit-walk workgroup walks a chain's segments in
+// order, all chains side by side on the epoch's start state, logging every commit (WinRec).
+// Then it proves, exactly, which prefix the sequential order would have produced:
 //
 //   segment 0 started from the true state, so it is exact;
 //   segment j > 0 is exact iff segments 0..j-1 are exact and complete, and for every task t
-//   it walked and every host h that an earlier segment committed to (at its capacities after
-//   that segment, which are its capacities throughout j): h is not t's winner, and h does not
-//   fit t with a key (score, index) below the winner's.
+//   it walked and every final log entry (host h, capacities after that segment) of an earlier
+//   segment of ANOTHER chain: h is not t's winner, and h does not fit t with a key (score,
+//   index) below the winner's. (Earlier segments of j's own chain were walked before j on the
+//   same state, so the walk already saw their commits.)
 //
-// By induction over j's tasks, every host outside those earlier segments' hosts has the same
-// state in the speculative and the sequential run, so the argmin over them is the same host,
-// and no earlier-touched host beats it (capacities only decrease, so a task that found no host
-// still finds none). validate_kernel checks exactly that; the host accepts the exact prefix,
-// applies its logged capacities (apply_kernel) and starts the next epoch where it ended.
+// By induction over j's tasks, every host the other chains' earlier segments did not touch has
+// the same state in the speculative and the sequential run, so the argmin over them is the same
+// host, and no touched host beats it (capacities only decrease, so a task that found no host
+// still finds none; a stale entry of a host committed again later only adds checks). The
+// validate kernel checks exactly that; the host accepts the exact prefix, the apply kernel
+// writes its final entries chain by chain, and the next epoch starts where the prefix ended.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,70 +30,117 @@
 
 namespace pvt {
 
-// One wave per walked task of segments j >= 1: scan the own hosts of segments 0..j-1.
-__global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
-  const int lane = lane_id();
-  const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
-  if (i >= A.nt) return;
-  int j = 0;
-  while (j + 1 < A.nseg && A.seg_off[j + 1] <= i) j++;   // segment of task i (nseg is small)
-  if (j == 0) return;
-  if (i - A.seg_off[j] >= A.status[2 * j]) return;        // not walked (the walk stopped early)
-  const WinRec w = A.wres[i];
-  if (w.id < 0) return;                                    // no host fits: stays so
-  if (__hip_atomic_load(&A.bad[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  const double d0 = A.dem[(size_t)i * 4], d1 = A.dem[(size_t)i * 4 + 1];
-  const double d2 = A.dem[(size_t)i * 4 + 2], d3 = A.dem[(size_t)i * 4 + 3];
-  const int a = A.anc[i];
-  const uint64_t w1 = (uint64_t)__double_as_longlong(w.s);
-  for (int s = 0; s < j; s++) {
-    const int n = A.status[2 * s + 1];
-    const int32_t* ids = A.own_ids + (size_t)s * MAX_WINDOW;
-    const double* oa = A.own_a + (size_t)s * 4 * MAX_WINDOW;
-    for (int o0 = 0; o0 < n; o0 += WAVE) {
-      const int o = o0 + lane;
-      bool beats = false;
-      if (o < n) {
-        const int32_t h = ids[o];
-        const double f0 = oa[o], f1 = oa[MAX_WINDOW + o], f2 = oa[2 * MAX_WINDOW + o];
-        const double f3 = oa[3 * MAX_WINDOW + o];
-        beats = (h == w.id);
-        if (!beats && fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) {
-          const int z = A.zone[h];
-          const double s2 = norm2_seq(f0 - d0, f1 - d1, f2 - d2, f3 - d3);
-          const double sc = (A.csum[a * A.Z + z] * __builtin_sqrt(s2)) / A.bsum[a * A.Z + z];
-          const uint64_t k1 = (uint64_t)__double_as_longlong(sc);
-          beats = (k1 < w1) | ((k1 == w1) & (h < w.id));
-        }
-      }
-      if (__ballot(beats)) {
-        if (lane == 0) __hip_atomic_store(&A.bad[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-      }
-    }
-  }
+// Tasks of segment j its chain's walk got through.
+__device__ __forceinline__ int seg_adv(const EpochArgs& A, int j) {
+  const int len = A.seg_off[j + 1] - A.seg_off[j];
+  const int done = A.status[2 * A.seg_chain[j]] - A.seg_cstart[j];
+  return max(0, min(len, done));
 }
 
-// The accepted segments' logged capacities -> global availability (their hosts are disjoint).
-__global__ __launch_bounds__(256) void epoch_apply_kernel(EpochArgs A) {
-  const int s = blockIdx.y;
-  const int n = A.status[2 * s + 1];
-  const int32_t* ids = A.own_ids + (size_t)s * MAX_WINDOW;
-  const double* oa = A.own_a + (size_t)s * 4 * MAX_WINDOW;
-  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < n; o += gridDim.x * blockDim.x) {
-    const int32_t h = ids[o];
+// Block (segment j, 256-task tile of j): every thread holds one walked task of j and checks it
+// against the final log entries of every earlier segment of another chain, staged 256 at a time
+// in LDS (each entry is read once per tile and broadcast to the tile's tasks).
+__global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
+  __shared__ int32_t e_id[256];
+  __shared__ double e_a[4][256];
+  __shared__ int32_t stop;
+  const int j = blockIdx.y, tid = threadIdx.x;
+  if (j == 0 || j >= A.nseg) return;
+  const int s0 = A.seg_off[j], adv = seg_adv(A, j);
+  const int t = s0 + blockIdx.x * 256 + tid;
+  if (blockIdx.x * 256 >= adv) return;
+  const bool mine = t < s0 + adv;
+  const int cj = A.seg_chain[j];
+  WinRec w{};
+  double d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+  int a = 0, g = 0;
+  bool active = false;
+  if (mine) {
+    w = A.wlog[t];
+    active = w.id >= 0;                      // no host fits: stays so (capacities only drop)
+    d0 = A.dem[(size_t)t * 4]; d1 = A.dem[(size_t)t * 4 + 1];
+    d2 = A.dem[(size_t)t * 4 + 2]; d3 = A.dem[(size_t)t * 4 + 3];
+    a = A.anc[t];
+    g = A.rtb ? A.grp[t] : 0;
+  }
+  const uint64_t w1 = (uint64_t)__double_as_longlong(w.s);
+  if (tid == 0) stop = 0;
+  __syncthreads();
+  bool beaten = false;
+  for (int s = 0; s < j && !stop; s++) {
+    if (A.seg_chain[s] == cj) continue;     // same chain: walked in order, exact
+    const int e0 = A.seg_off[s], ne = seg_adv(A, s);
+    for (int c0 = 0; c0 < ne; c0 += 256) {
+      __syncthreads();
+      if (c0 + tid < ne) {
+        const WinRec& e = A.wlog[e0 + c0 + tid];
+        const bool fin = e.id >= 0 && !e.sup;
+        e_id[tid] = fin ? e.id : -1;
+        e_a[0][tid] = e.a[0]; e_a[1][tid] = e.a[1]; e_a[2][tid] = e.a[2]; e_a[3][tid] = e.a[3];
+      } else {
+        e_id[tid] = -1;
+      }
+      __syncthreads();
+      if (active && !beaten) {
+        const int n = min(256, ne - c0);
+        for (int k = 0; k < n; k++) {
+          const int32_t h = e_id[k];
+          if (h < 0) continue;
+          const double f0 = e_a[0][k], f1 = e_a[1][k], f2 = e_a[2][k], f3 = e_a[3][k];
+          bool hit = (h == w.id);
+          if (!hit && fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) {
+            const int z = A.zone[h];
+            const double s2 = norm2_seq(f0 - d0, f1 - d1, f2 - d2, f3 - d3);
+            const double c = A.csum[a * A.Z + z];
+            const double bw = A.rtb ? A.rtb[(size_t)g * A.H + h] : A.bsum[a * A.Z + z];
+            if (c == 0.0) {
+              // zero egress cost: the score is exactly +0 (finite s2, bw > 0)
+              hit = (0ull < w1) | ((0ull == w1) & (h < w.id));
+            } else if (w1 == 0ull && s2 >= 0x1p-600 && c >= 0x1p-300 && bw <= 0x1p300) {
+              hit = false;   // c * sqrt(s2) >= 2^-600 and / bw >= 2^-900: the score is > 0
+            } else {
+              const double sc = (c * __builtin_sqrt(s2)) / bw;
+              const uint64_t k1 = (uint64_t)__double_as_longlong(sc);
+              hit = (k1 < w1) | ((k1 == w1) & (h < w.id));
+            }
+          }
+          if (hit) { beaten = true; break; }
+        }
+      }
+      if (beaten) stop = 1;                  // benign race: every writer stores 1
+      __syncthreads();
+      if (stop) break;
+    }
+  }
+  if (tid == 0 && stop) __hip_atomic_store(&A.bad[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One block per chain: its accepted segments in order, each segment's final entries written to
+// global availability (a later segment of the chain overwrites an earlier one's entry for the
+// same host; different chains' accepted segments touch disjoint hosts).
+__global__ __launch_bounds__(256) void epoch_apply_kernel(EpochArgs A, int n_accept) {
+  const int c = blockIdx.x;
+  for (int s = 0; s < n_accept; s++) {
+    if (A.seg_chain[s] != c) continue;
+    const int e0 = A.seg_off[s], ne = seg_adv(A, s);
+    for (int k = threadIdx.x; k < ne; k += blockDim.x) {
+      const WinRec& e = A.wlog[e0 + k];
+      if (e.id < 0 || e.sup) continue;
 #pragma unroll
-    for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + h] = oa[(size_t)r * MAX_WINDOW + o];
+      for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + e.id] = e.a[r];
+    }
+    __syncthreads();
   }
 }
 
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(epoch_validate_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+  const int tiles = (CHAIN_MAX + 255) / 256;   // a segment never exceeds its chain's cap
+  hipLaunchKernelGGL(epoch_validate_kernel, dim3(tiles, a.nseg), dim3(256), 0, st, a);
 }
 
-void launch_epoch_apply(const EpochArgs& a, int n_accept, hipStream_t st) {
-  if (n_accept <= 0) return;
-  hipLaunchKernelGGL(epoch_apply_kernel, dim3(MAX_WINDOW / 256, n_accept), dim3(256), 0, st, a);
+void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st) {
+  if (n_accept <= 0 || nchains <= 0) return;
+  hipLaunchKernelGGL(epoch_apply_kernel, dim3(nchains), dim3(256), 0, st, a, n_accept);
 }
 
 }  // namespace pvt

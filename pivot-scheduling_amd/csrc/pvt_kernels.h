@@ -20,6 +20,7 @@ constexpr int WPB = 4;           // waves per score-kernel block
 constexpr int MAX_WINDOW = 1024; // tasks per window (bounded by the commit kernel's LDS)
 constexpr int HASH_BITS = 12;    // commit kernel touched-host hash: 4096 slots
 constexpr int MAX_SEG = 16;      // host segments per task at a full window
+constexpr int CHAIN_MAX = 2048;  // tasks per epoch chain walk (touched-host hash: 4096 slots)
 
 enum Mode { CA_FF = 0, CA_BF = 1, OPP = 2, VBP_FF = 3, VBP_BF = 4 };
 
@@ -75,6 +76,8 @@ struct ScoreArgs {
   SegEntry* seg;          // [nt][S][KL]
   int32_t* seg_feas;      // [nt][S]
   int tw;                 // tasks per wave: 0 = the policy's default, else 2 or 4 (tuning/tests)
+  const double* rtb;      // CA_BF realtime_bw: bandwidth per (group, host) [G][H], or NULL
+  const int32_t* grp;     // window tasks' groups [nt] (rows of rtb)
 };
 
 // Merge of S sorted candidate lists per task into the task's exact top list. Two sources:
@@ -115,11 +118,14 @@ struct OrderedArgs {      // first-fit by host index: first KL snapshot-feasible
   Lists L;
 };
 
-// Winner of a walked task in an epoch walk (log mode): its key (score, host); id -1 = no host.
+// One walked task of an epoch walk (chain mode): its winner's key (score, host; id -1 = no
+// host) and the host's capacities after the commit; sup = 1 once a later task of the same
+// group segment committed to the same host (the entry is then not the segment's final state).
 struct WinRec {
   double s;
   int32_t id;
-  int32_t pad;
+  int32_t sup;
+  double a[4];
 };
 
 struct CommitArgs {
@@ -139,37 +145,48 @@ struct CommitArgs {
   int32_t* own_ids;       // out: hosts this walk committed to (distinct), for the next window
   int32_t* status;        // out: [0] window-local index where the walk stopped (nt = done,
                           //      -1 = spin timeout), [1] number of own_ids
+  const double* rtb;      // CA_BF realtime_bw: bandwidth per (group, host) [G][H], or NULL
+  const int32_t* grp;     // window tasks' groups [nt] (rows of rtb)
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): per-phase cycle sums
-  // Group-parallel epochs (pvt_capi.hip place_epochs): with seg_off set, workgroup b walks the
-  // window tasks [seg_off[b], seg_off[b+1]) on its own (own_ids, status at b * MAX_WINDOW and
-  // 2 * b) and LOGS its commits instead of writing avail: own_a[b][4][MAX_WINDOW] = capacities
-  // of its own hosts after the walk, wres[i] = the winner of task i.
-  const int32_t* seg_off;
-  double* own_a;
-  WinRec* wres;
+  // Speculative epochs (pvt_capi.hip place_epochs), chain mode when cmap is set: workgroup b
+  // walks the window tasks cmap[coff[b] .. coff[b+1]) (processing order), a chain of group
+  // segments whose chain-local starts are cseg[csoff[b] .. csoff[b+1]); it writes wlog[w] for
+  // every walked window task w instead of avail, and status[2b] = tasks walked.
+  const int32_t* coff;
+  const int32_t* cmap;
+  const int32_t* csoff;
+  const int32_t* cseg;
+  WinRec* wlog;
 };
 
-// Speculative epochs, cost_aware best-fit: segment j > 0 of an epoch was walked on the epoch's
-// start state; it is exact iff no host an earlier segment committed to (at its state after that
-// segment) is the winner of, or fits and beats the winner of, one of j's walked tasks.
+// Speculative epochs, cost_aware best-fit. The epoch's group segments (processing order,
+// contiguous window ranges seg_off) are walked in chains -- the segments whose anchors share a
+// zero-cost zone component, in order, by one workgroup -- all chains side by side on the epoch's
+// start state. Segment j is exact iff every earlier segment is exact and complete, and for
+// every task t it walked and every final log entry (host h, capacities after that segment) of
+// an earlier segment of ANOTHER chain: h is not t's winner and h does not fit t with a key
+// (score, index) below the winner's.
 struct EpochArgs {
   const double* dem;      // window tasks [nt][4]
   const int32_t* anc;     // window tasks [nt]
   const double* csum;
   const double* bsum;
   const int32_t* zone;
-  const int32_t* seg_off; // [nseg + 1] window-local task offsets
-  const int32_t* own_ids; // [nseg][MAX_WINDOW]
-  const double* own_a;    // [nseg][4][MAX_WINDOW]
-  const int32_t* status;  // [nseg][2]: tasks walked, own hosts
-  const WinRec* wres;     // [nt]
-  double* avail;          // apply: accepted segments' own hosts written here
+  const int32_t* seg_off; // [nseg + 1] window offsets of the segments (processing order)
+  const int32_t* seg_chain;   // [nseg] chain of each segment
+  const int32_t* seg_cstart;  // [nseg] index of the segment's first task in its chain's walk
+  const int32_t* status;  // [nchains][2]: tasks the chain's walk got through (-1: timeout)
+  const WinRec* wlog;     // [nt]
+  double* avail;          // apply: accepted segments' final entries written here
   int H, Z, nt, nseg;
   int32_t* bad;           // [nseg] out: 1 = segment j is not exact (zeroed by the caller)
+  const double* rtb;      // realtime_bw: bandwidth per (group, host) [G][H], or NULL
+  const int32_t* grp;     // window tasks' groups [nt]
 };
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st);
-void launch_epoch_apply(const EpochArgs& a, int n_accept, hipStream_t st);
-void launch_commit_segments(const CommitArgs& a, int nseg, hipStream_t st);
+// apply: the accepted segments [0, n_accept) of each chain, chain by chain in segment order
+void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st);
+void launch_commit_chains(const CommitArgs& a, int nchains, hipStream_t st);
 
 // cost_aware first-fit with sort_hosts, as the reference runs it (cost_aware.py:118-124): the
 // hosts sorted once per group by the frozen key (perm, skey = sorted key bits; the radix sort
@@ -200,6 +217,7 @@ struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw
   int H, Z, anchor;
   int h_lo, h_hi;         // hosts whose key is computed
   double* key;
+  const double* rtb;      // realtime_bw: the group's bandwidth row [H], or NULL
 };
 
 int score_tasks_per_wave(int mode, int hosts, int force = 0);
@@ -241,6 +259,6 @@ void launch_iota(int32_t* out, int n, hipStream_t st);
 // gather tasks into processing order: dem_ord[p][r] = dem[r*T + ord[p]], anc_ord[p]
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
                          const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
-                         hipStream_t st);
+                         int32_t* grp_ord, hipStream_t st);
 
 }  // namespace pvt

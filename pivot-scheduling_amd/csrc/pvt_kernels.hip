@@ -99,6 +99,9 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
   const int t0 = (tile * WPB + wave) * TW;
   if (t0 >= A.nt) return;
   const int nt = min(TW, A.nt - t0);
+  // realtime_bw (cost_aware.py:79): the bandwidth is per (group, host), so no per-zone radius
+  // bounds the score -- every fitting candidate is scored exactly
+  const bool rt = (MODE == CA_BF) && A.rtb != nullptr;
   // Segment `seg` owns the 64-host blocks seg, seg + S, seg + 2S, ... of [h_lo, h_hi): each
   // block is one coalesced load per component, and interleaving keeps every segment's share of
   // low host indices equal, so lists stay deep when many hosts tie (zero-cost zones, where the
@@ -108,6 +111,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
 
   double d0[TW], d1[TW], d2[TW], d3[TW];
   double ls[TW], ts[TW], lim[TW], rd[TW];
+  const double* rb[TW];
   uint32_t lt[TW], tt[TW];
   int32_t li[TW], ti[TW];
 #pragma unroll
@@ -122,6 +126,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
     ts[k] = DINF; tt[k] = 0xffffffffu; ti[k] = 0x7fffffff;
     lim[k] = DINF;
     rd[k] = (k < nt) ? DINF : -1.0;        // a missing task never passes the prefilter
+    rb[k] = (rt && k < nt) ? A.rtb + (size_t)A.grp[t0 + k] * A.H : A.rtb;
     if (MODE == CA_BF) {
       const int a = (k < nt) ? A.anc[t0 + k] : 0;
       if (lane < A.Z) {
@@ -216,7 +221,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
             sc = key;
           } else if (MODE == CA_BF) {
             const double r = __builtin_sqrt(s2);
-            sc = (s_c[wave][k][z] * r) / s_b[wave][k][z];
+            sc = (s_c[wave][k][z] * r) / (rt ? rb[k][h] : s_b[wave][k][z]);
           } else {
             sc = __builtin_sqrt(s2);
             tbv = tbh;
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
           tt[k] = readlane_u(lt[k], KL - 1);
           ti[k] = readlane_i(li[k], KL - 1);
 
-          if (MODE == CA_BF) {
+          if (MODE == CA_BF && !rt) {
             if (lane < A.Z) {
               const double lm2 = ca_lim(ts[k], s_c[wave][k][lane], s_b[wave][k][lane]);
               s_lim[wave][k][lane] = lm2;
@@ -738,7 +743,8 @@ __global__ void key_kernel(KeyArgs A) {
   const double a2 = A.avail[2 * (size_t)A.H + h], a3 = A.avail[3 * (size_t)A.H + h];
   const double r = __builtin_sqrt(norm2_seq(a0, a1, a2, a3));
   const int z = A.zone[h];
-  const double c = A.csum[A.anchor * A.Z + z], bw = A.bsum[A.anchor * A.Z + z];
+  const double c = A.csum[A.anchor * A.Z + z];
+  const double bw = A.rtb ? A.rtb[h] : A.bsum[A.anchor * A.Z + z];
   const double df = A.decay ? (double)A.decay[h] : 1.0;
   A.key[h] = (c * df) / (r * bw);
 }
@@ -779,19 +785,21 @@ void launch_iota(int32_t* out, int n, hipStream_t st) {
 }
 
 __global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const int32_t* tg,
-                                    const int32_t* ga, int T, double* dem_ord, int32_t* anc_ord) {
+                                    const int32_t* ga, int T, double* dem_ord, int32_t* anc_ord,
+                                    int32_t* grp_ord) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= T) return;
   const int t = ord[p];
   double* o = dem_ord + (size_t)p * 4;
   o[0] = dem[t]; o[1] = dem[(size_t)T + t]; o[2] = dem[2 * (size_t)T + t]; o[3] = dem[3 * (size_t)T + t];
   anc_ord[p] = (tg && ga) ? ga[tg[t]] : 0;
+  if (grp_ord) grp_ord[p] = tg ? tg[t] : 0;
 }
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
                          const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
-                         hipStream_t st) {
+                         int32_t* grp_ord, hipStream_t st) {
   hipLaunchKernelGGL(gather_tasks_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, ord,
-                     task_group, group_anchor, T, dem_ord, anc_ord);
+                     task_group, group_anchor, T, dem_ord, anc_ord, grp_ord);
 }
 
 }  // namespace pvt

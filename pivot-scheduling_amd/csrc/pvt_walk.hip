@@ -63,6 +63,7 @@ constexpr int32_t H_MISS = -1;            // lookup result: host not touched
 constexpr int32_t H_DEAD = -2;            // hash value: touched, can no longer fit the window
 constexpr int32_t H_PENDING = 0x7fffffff; // hash value before the walker writes it
 constexpr int SPIN_LIMIT = 1 << 24;       // bounded spins (x s_sleep 2 ~ seconds)
+constexpr int MAX_CHAIN_SEGS = 64;        // group segments per epoch chain
 
 // A scout's result: LOOK usable list entries in list order (untouched, or for first-fit
 // touched and fitting) and, for best-fit, the LOOK best live touched hosts; one 16-dword
@@ -98,7 +99,10 @@ struct WalkLDS {
   int32_t lhp[LIVE_MAX];                  // hash position of the live host
   uint32_t ltb[LIVE_MAX];
   int32_t lown[LIVE_MAX];                 // 1: committed to by this walk (in own_ids)
-  int32_t lo[LIVE_MAX];                   // its index in own_ids, once lown
+  int32_t lpw[LIVE_MAX];                  // epoch walks: window task of its last commit,
+  int32_t lpi[LIVE_MAX];                  //   and that task's index in this walk
+  int32_t cseg[MAX_CHAIN_SEGS + 1];       // epoch walks: segment starts in this walk (+ nt)
+  int32_t cwin[MAX_CHAIN_SEGS + 1];       //   and their first tasks' window indices
   double csum[ZMAX * ZMAX];
   double bsum[ZMAX * ZMAX];
   int32_t flag[RING];
@@ -176,6 +180,9 @@ __device__ __forceinline__ uint64_t stamp() {
 #define STAMP(k) do {} while (0)
 #endif
 
+// Window index of the walk's i-th task (epoch chains walk a subsequence of the window).
+__device__ __forceinline__ int widx(const CommitArgs& A, int i) { return A.cmap ? A.cmap[i] : i; }
+
 // ---------------------------------------------------------------- scouts (loader waves)
 // Record r of a result block from lane `lane` (the lane holding the candidate): its score,
 // tiebreak, host, zone, live index (-1 untouched), own flag, hash position, capacities.
@@ -191,14 +198,16 @@ __device__ __forceinline__ void put_rec(int32_t* res, int base, double s, uint32
 
 // Exact best-fit key of a host for the task: (score bits, tiebreak:id); scores are >= +0, so
 // their bit patterns order like the values (cost_aware.py:83, vbp.py:45).
+// rtrow: the task's group row of the realtime bandwidth (cost_aware.py:79), or NULL.
 template <int MODE>
-__device__ __forceinline__ void bf_key(const WalkLDS& S, int Z, int anc, double a0, double a1,
-                                       double a2, double a3, double d0, double d1, double d2,
-                                       double d3, int32_t z, uint32_t tb, int32_t id, uint64_t& k1,
-                                       uint64_t& k2) {
+__device__ __forceinline__ void bf_key(const WalkLDS& S, int Z, int anc, const double* rtrow,
+                                       double a0, double a1, double a2, double a3, double d0,
+                                       double d1, double d2, double d3, int32_t z, uint32_t tb,
+                                       int32_t id, uint64_t& k1, uint64_t& k2) {
   const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
   double sc;
-  if (MODE == CA_BF) sc = (S.csum[anc * Z + z] * __builtin_sqrt(s2)) / S.bsum[anc * Z + z];
+  if (MODE == CA_BF)
+    sc = (S.csum[anc * Z + z] * __builtin_sqrt(s2)) / (rtrow ? rtrow[id] : S.bsum[anc * Z + z]);
   else sc = __builtin_sqrt(s2);
   k1 = (uint64_t)__double_as_longlong(sc);
   k2 = ((uint64_t)(MODE == VBP_BF ? tb : 0u) << 32) | (uint32_t)id;
@@ -211,7 +220,8 @@ __device__ __forceinline__ bool key_lt(uint64_t a1, uint64_t a2, uint64_t b1, ui
 // its list (ring, then the deep list in HBM) and, for best-fit, the LOOK best live touched hosts
 // that could still win; written to R.res.
 template <int MODE>
-__device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int i, int k, int32_t rv) {
+__device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k, int32_t rv,
+                      const double* rtrow) {
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
   constexpr bool BEST = (MODE == CA_BF || MODE == VBP_BF);
   const int lane = lane_id();
@@ -264,8 +274,8 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int i, int k
     }
   }
   // deep list (rare): entries after the ring's, by id, then their records from HBM
-  const int32_t* ids = A.L.ids + (size_t)i * LMAX;
-  const ListEntry* le = A.L.e + (size_t)i * LMAX;
+  const int32_t* ids = A.L.ids + (size_t)w * LMAX;
+  const ListEntry* le = A.L.e + (size_t)w * LMAX;
   for (int c0 = npos; c0 < cnt && nU < LOOK; c0 += WAVE) {
     const bool v = c0 + lane < cnt;
     const int32_t id = v ? ids[c0 + lane] : 0;
@@ -331,7 +341,7 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int i, int k
       const bool fit = (q < nlp) && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
       if (__ballot(fit) == 0) continue;
       uint64_t k1 = ~0ull, k2 = ~0ull;
-      bf_key<MODE>(S, A.Z, anc, a0, a1, a2, a3, d0, d1, d2, d3, S.lz[qq],
+      bf_key<MODE>(S, A.Z, anc, rtrow, a0, a1, a2, a3, d0, d1, d2, d3, S.lz[qq],
                    MODE == VBP_BF ? S.ltb[qq] : 0u, S.lid[qq], k1, k2);
       uint64_t pm = __ballot(fit && key_lt(k1, k2, b1, b2) && key_lt(k1, k2, tk1[LOOK - 1], tk2[LOOK - 1]));
       while (pm) {
@@ -379,8 +389,9 @@ __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
   const int lane = lane_id();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int i = pw; i < A.nt; i += PRODUCERS) {
-    const ListEntry* le = A.L.e + (size_t)i * LMAX;
-    const int32_t rv = reinterpret_cast<const int32_t*>(A.L.t + i)[lane & 15];
+    const int w = widx(A, i);
+    const ListEntry* le = A.L.e + (size_t)w * LMAX;
+    const int32_t rv = reinterpret_cast<const int32_t*>(A.L.t + w)[lane & 15];
     const int cnt = __builtin_amdgcn_readlane(rv, 8);
     // The first PRE_CHUNKS chunks of the list are in flight while the slot is busy (deep lists
     // full of touched hosts would otherwise cost one HBM round trip per chunk).
@@ -432,9 +443,12 @@ __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
       }
       k += got;
     }
+    // realtime_bw: the task's group (the walker's patched-host rescoring reads it from rec[18])
+    const int grp = (MODE == CA_BF && A.rtb) ? __builtin_amdgcn_readfirstlane(A.grp[w]) : 0;
     if (lane < 16) R.rec[lane] = rv;
     if (lane == 16) R.rec[16] = k;
     if (lane == 17) R.rec[17] = next_pos;
+    if (lane == 18) R.rec[18] = grp;
     // the state this task is scouted on: every task <= i - LOOK committed
     for (int spin = 0;; spin++) {
       const int c = vload(&S.committed);
@@ -446,7 +460,7 @@ __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
     // the scout is on the walk's critical path (the walker needs its result one task from now):
     // it outranks the other scouts' list loading, not the walker
     __builtin_amdgcn_s_setprio(2);
-    scout<MODE>(A, S, R, i, k, rv);
+    scout<MODE>(A, S, R, w, k, rv, (MODE == CA_BF && A.rtb) ? A.rtb + (size_t)grp * A.H : nullptr);
     lds_drain();
     if (lane == 0) publish(&S.flag[slot], i);
     __builtin_amdgcn_s_setprio(0);
@@ -486,7 +500,7 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
   // Componentwise minimum demand of the window: a touched host that cannot fit it is dead.
   double m0 = DINF, m1 = DINF, m2 = DINF, m3 = DINF;
   for (int i = lane; i < A.nt; i += WAVE) {
-    const double* dp = A.dem + (size_t)i * 4;
+    const double* dp = A.dem + (size_t)widx(A, i) * 4;
     m0 = fmin(m0, dp[0]); m1 = fmin(m1, dp[1]); m2 = fmin(m2, dp[2]); m3 = fmin(m3, dp[3]);
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -519,6 +533,8 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
   if (lane == 0) { vstore(&S.nl_pub, nl); vstore(&S.committed, 0); }
   int n_own = 0;
   int status = A.nt;
+  int sstart = 0, sk = 1, wbase = 0;        // epoch chains: the current segment's start in
+  if (A.wlog) wbase = S.cwin[0];            //   this walk and in the window
   Patched X[NP];
 #pragma unroll
   for (int r = 0; r < NP; r++) {
@@ -546,6 +562,7 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     const bool comp = __builtin_amdgcn_readlane(tv, 9) != 0;
     const int anc = __builtin_amdgcn_readlane(tv, 10);
     const int caller = __builtin_amdgcn_readlane(tv, 11);
+    const int grp = __builtin_amdgcn_readlane(tv, 18);   // realtime_bw: the task's group
     const int nU = rdw(rs, R_NU);
     STAMP(0);
 
@@ -609,10 +626,12 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
           const double s2 = norm2_seq(X[r].a0 - d0, X[r].a1 - d1, X[r].a2 - d2, X[r].a3 - d3);
           double sc;
           if (MODE == CA_BF) {
-            if (anc != X[r].anc) {            // its zone-table entries for this anchor
-              X[r].anc = anc;
+            // its zone-table entries for this anchor (realtime_bw: its bandwidth for this group)
+            const int ck = A.rtb ? grp : anc;
+            if (ck != X[r].anc) {
+              X[r].anc = ck;
               X[r].c = S.csum[anc * A.Z + X[r].z];
-              X[r].b = S.bsum[anc * A.Z + X[r].z];
+              X[r].b = A.rtb ? A.rtb[(size_t)grp * A.H + X[r].id] : S.bsum[anc * A.Z + X[r].z];
             }
             sc = (X[r].c * __builtin_sqrt(s2)) / X[r].b;
           } else {
@@ -657,10 +676,13 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     }
     if (refill) { status = i; break; }
     release_slot(S, i + 1);                   // the ring slot is no longer read
+    if (A.wlog) {                             // entering the chain's next segment
+      while (i >= S.cseg[sk]) { sstart = S.cseg[sk]; wbase = S.cwin[sk]; sk++; }
+    }
     if (none) {                               // nothing committed: the window slides
       if (lane == 0) {
         A.placement[caller] = -1;             // (an earlier speculative walk may have set it)
-        if (A.wres) { A.wres[i].s = DINF; A.wres[i].id = -1; }
+        if (A.wlog) { const int w = wbase + i - sstart; A.wlog[w].s = DINF; A.wlog[w].id = -1; A.wlog[w].sup = 0; }
       }
 #pragma unroll
       for (int r = NP - 1; r > 0; r--) X[r] = X[r - 1];
@@ -730,20 +752,22 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
         q_after = -1;
       }
     }
-    int32_t o;                                // the host's index in own_ids
-    if (!w_own) {                             // first commit of this walk to the host
-      o = n_own++;
+    if (A.wlog) {                             // epoch walk: logged, applied once validated
+      const int w = wbase + i - sstart;
+      if (lane < 4) A.wlog[w].a[lane] = nr;
       if (lane == 0) {
-        A.own_ids[o] = W.id;
-        if (q_after >= 0) S.lo[q_after] = o;
+        A.wlog[w].s = __longlong_as_double((long long)wk);
+        A.wlog[w].id = W.id;
+        A.wlog[w].sup = 0;
+        // this walk's previous commit to the host, if in the same segment, is not final
+        if (W.q >= 0 && S.lpi[W.q] >= sstart) A.wlog[S.lpw[W.q]].sup = 1;
+        if (q_after >= 0) { S.lpw[q_after] = w; S.lpi[q_after] = i; }
       }
     } else {
-      o = __builtin_amdgcn_readfirstlane(S.lo[W.q]);
-    }
-    if (A.own_a) {                            // epoch walk: logged, applied once validated
-      if (lane < 4) A.own_a[(size_t)lane * MAX_WINDOW + o] = nr;
-      if (lane == 0) { A.wres[i].s = __longlong_as_double((long long)wk); A.wres[i].id = W.id; }
-    } else {
+      if (!w_own) {                           // first commit of this walk to the host
+        if (lane == 0) A.own_ids[n_own] = W.id;
+        n_own++;
+      }
       if (lane < 4) A.avail[(size_t)lane * A.H + W.id] = nr;
     }
     if (lane == 0) A.placement[caller] = W.id;
@@ -776,18 +800,12 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
 
 template <int MODE>
 __global__ __launch_bounds__(WALK_THREADS) void commit_kernel(CommitArgs A) {
-  if (A.seg_off) {                            // epoch walk: this workgroup's segment
+  if (A.cmap) {                               // epoch walk: this workgroup's chain
     const int b = blockIdx.x;
-    const int base = A.seg_off[b];
-    A.nt = A.seg_off[b + 1] - base;
-    A.dem += (size_t)base * 4;
-    A.L.e += (size_t)base * LMAX;
-    A.L.ids += (size_t)base * LMAX;
-    A.L.t += base;
-    A.own_ids += (size_t)b * MAX_WINDOW;
-    A.own_a += (size_t)b * 4 * MAX_WINDOW;
+    const int base = A.coff[b];
+    A.nt = A.coff[b + 1] - base;
+    A.cmap += base;
     A.status += 2 * b;
-    A.wres += base;
   }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WalkLDS& S = *reinterpret_cast<WalkLDS*>(smem);
@@ -798,6 +816,13 @@ __global__ __launch_bounds__(WALK_THREADS) void commit_kernel(CommitArgs A) {
   if (MODE == CA_BF)
     for (int i = tid; i < A.Z * A.Z; i += WALK_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
   if (tid < RING) S.flag[tid] = -1;
+  if (A.cmap) {                               // the chain's segment starts (chain-local), then nt
+    const int s0 = A.csoff[blockIdx.x], ns = min(A.csoff[blockIdx.x + 1] - s0, MAX_CHAIN_SEGS);
+    for (int k = tid; k <= MAX_CHAIN_SEGS; k += WALK_THREADS) {
+      S.cseg[k] = k < ns ? A.cseg[s0 + k] : A.nt;
+      S.cwin[k] = k < ns ? A.cmap[A.cseg[s0 + k]] : 0;
+    }
+  }
   if (tid == 0) { S.done = 0; S.stop = 0; S.nl_init = 0; S.nl_pub = 0; S.committed = -1; }
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -825,11 +850,11 @@ hipError_t init_kernel_attrs() {
   return e;
 }
 
-void launch_commit(const CommitArgs& a, hipStream_t st) { launch_commit_segments(a, 1, st); }
+void launch_commit(const CommitArgs& a, hipStream_t st) { launch_commit_chains(a, 1, st); }
 
-void launch_commit_segments(const CommitArgs& a, int nseg, hipStream_t st) {
+void launch_commit_chains(const CommitArgs& a, int nchains, hipStream_t st) {
   const size_t lds = WALK_LDS_BYTES;
-  const dim3 grid(nseg), block(WALK_THREADS);
+  const dim3 grid(nchains), block(WALK_THREADS);
   switch (a.mode) {
     case CA_FF: hipLaunchKernelGGL(commit_kernel<CA_FF>, grid, block, lds, st, a); break;
     case CA_BF: hipLaunchKernelGGL(commit_kernel<CA_BF>, grid, block, lds, st, a); break;

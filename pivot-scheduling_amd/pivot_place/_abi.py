@@ -10,7 +10,7 @@ from typing import Optional
 
 import numpy as np
 
-PVT_ABI_VERSION = 1
+PVT_ABI_VERSION = 2
 
 PVT_OK = 0
 PVT_EINVAL = -1
@@ -57,6 +57,7 @@ class pvt_round(ctypes.Structure):
         ("order", ctypes.c_void_p),
         ("placement", ctypes.c_void_p),
         ("mt_state", ctypes.c_void_p),
+        ("rt_bw", ctypes.c_void_p),
     ]
 
 
@@ -101,7 +102,8 @@ class RoundArrays:
 
     avail (4, H) f64 · zone (H,) i32 · dem (4, T) f64 · cost/bw (Z, Z) f64 · optional
     tiebreak (H,) u32, decay (H,) i32, task_group (T,) i32 + group_anchor (G,) i32,
-    mt_state (625,) u32 (MT19937 key + pos).
+    mt_state (625,) u32 (MT19937 key + pos), rt_bw (G, H) f64 (cost_aware realtime_bw: in +
+    out realtime bandwidth per group and host; row 0 without task_group).
     """
     mode: int
     avail: np.ndarray
@@ -116,6 +118,7 @@ class RoundArrays:
     sort_tasks: bool = False
     sort_hosts: bool = False
     mt_state: Optional[np.ndarray] = None
+    rt_bw: Optional[np.ndarray] = None
 
     def __post_init__(self):
         self.avail = np.ascontiguousarray(self.avail, dtype=np.float64).reshape(4, -1)
@@ -128,7 +131,8 @@ class RoundArrays:
         self.cost = np.ascontiguousarray(self.cost, dtype=np.float64)
         self.bw = np.ascontiguousarray(self.bw, dtype=np.float64)
         for name, dt in (("tiebreak", np.uint32), ("decay", np.int32), ("task_group", np.int32),
-                         ("group_anchor", np.int32), ("mt_state", np.uint32)):
+                         ("group_anchor", np.int32), ("mt_state", np.uint32),
+                         ("rt_bw", np.float64)):
             v = getattr(self, name)
             if v is not None:
                 setattr(self, name, np.ascontiguousarray(v, dtype=dt))

@@ -96,6 +96,7 @@ class DeviceRound:
         self.zone, self.tiebreak, self.decay = up(r.zone), up(r.tiebreak), up(r.decay)
         self.cost, self.bw, self.dem = up(r.cost), up(r.bw), up(r.dem)
         self.task_group, self.group_anchor = up(r.task_group), up(r.group_anchor)
+        self.rt_bw = up(r.rt_bw)
         T = r.n_tasks
         self.order = torch.empty(max(T, 1), dtype=torch.int32, device=dev)
         self.placement = torch.empty(max(T, 1), dtype=torch.int32, device=dev)
@@ -110,6 +111,7 @@ class DeviceRound:
         s.cost, s.bw, s.dem = dp(self.cost), dp(self.bw), dp(self.dem)
         s.task_group, s.group_anchor = dp(self.task_group), dp(self.group_anchor)
         s.order, s.placement = dp(self.order), dp(self.placement)
+        s.rt_bw = dp(self.rt_bw)
         s.mt_state = None if self.mt is None else self.mt.ctypes.data
         self.struct = s
 
@@ -133,7 +135,8 @@ class DeviceBatch:
 
     _FIELDS = (("avail", np.float64), ("zone", np.int32), ("tiebreak", np.uint32),
                ("decay", np.int32), ("cost", np.float64), ("bw", np.float64),
-               ("dem", np.float64), ("task_group", np.int32), ("group_anchor", np.int32))
+               ("dem", np.float64), ("task_group", np.int32), ("group_anchor", np.int32),
+               ("rt_bw", np.float64))
 
     def __init__(self, rounds, device):
         torch = _torch()

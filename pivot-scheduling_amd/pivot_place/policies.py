@@ -197,14 +197,21 @@ class CostAwarePlacement(PlacementMixin):
             groups.setdefault(key, []).append(t)
         return groups
 
+    def _realtime_row(self, anchor, hosts):
+        """realtime_bw=True (cost_aware.py:73-79, :106-112): per host, the bandwidth the
+        reference's host_score_func uses, in_route.realtime_bw + out_route.realtime_bw of the
+        routes between the anchor storage and the host (resources/network.py:70-73), read from
+        the cluster's own route objects and summed in the reference's order."""
+        get_route = self.cluster.get_route
+        return [get_route(anchor.id, h.id).realtime_bw + get_route(h.id, anchor.id).realtime_bw
+                for h in hosts]
+
     def schedule(self, tasks):
         algo = self._pvt_algo
         if algo not in ('first-fit', 'best-fit'):
             if tasks:   # the reference calls the str (cost_aware.py:42)
                 raise TypeError("'str' object is not callable")
             return tasks
-        if self._pvt_realtime_bw:
-            raise NotImplementedError("realtime_bw=True is not supported by the GPU engine yet")
         storage, hosts = self.cluster.storage, self.cluster.hosts
         resc = self.resource_info
         tab = self._tables()
@@ -212,7 +219,7 @@ class CostAwarePlacement(PlacementMixin):
         task_pos = {id(t): i for i, t in enumerate(tasks)}
         T = len(tasks)
         task_group = np.zeros(T, dtype=np.int32)
-        anchors = []
+        anchors, rt_rows = [], []
         avail = self._snapshot(hosts, resc)
         dem = self._demand(tasks)
         best_fit = algo == 'best-fit'
@@ -226,6 +233,8 @@ class CostAwarePlacement(PlacementMixin):
             anchors.append(tab.zone_of[anchor.locality])
             for t in members:
                 task_group[task_pos[id(t)]] = g
+            if self._pvt_realtime_bw:
+                rt_rows.append(self._realtime_row(anchor, hosts))
         if best_fit and self._pvt_host_decay:
             return tasks
         decay = None
@@ -234,7 +243,9 @@ class CostAwarePlacement(PlacementMixin):
         r = RoundArrays(mode=_abi.PVT_CA_BF if best_fit else _abi.PVT_CA_FF, avail=avail,
                         zone=tab.zone, dem=dem, cost=tab.cost, bw=tab.bw, decay=decay,
                         task_group=task_group, group_anchor=np.array(anchors, dtype=np.int32),
-                        sort_tasks=self._pvt_sort_tasks, sort_hosts=self._pvt_sort_hosts)
+                        sort_tasks=self._pvt_sort_tasks, sort_hosts=self._pvt_sort_hosts,
+                        rt_bw=np.array(rt_rows, dtype=np.float64).reshape(len(rt_rows), -1)
+                        if rt_rows else None)
         if T:
             res = self._engine().place(r)
             self._apply(tasks, hosts, resc, res, avail)

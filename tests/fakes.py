@@ -52,13 +52,23 @@ class Meta:
         self.bw = {(a, b): float(bw[i][j]) for i, a in enumerate(zones) for j, b in enumerate(zones)}
 
 
+class Route:
+    def __init__(self, bw, realtime_bw):
+        self.bw = bw
+        self.realtime_bw = realtime_bw
+
+
 class Cluster:
-    def __init__(self, hosts, storage, meta):
+    def __init__(self, hosts, storage, meta, routes=None):
         self.hosts = hosts
         self.storage = storage
         self.meta = meta
         self._by_id = {h.id: h for h in hosts}
         self._storage_by_loc = {s.locality: s for s in storage}
+        self._routes = routes or {}
+
+    def get_route(self, src_id, dst_id):
+        return self._routes.get((src_id, dst_id))
 
     def get_host(self, hid):
         return self._by_id.get(hid)
@@ -100,7 +110,14 @@ def build(case):
     hosts = [Host(ids[i], zones[z], a, nr) for i, (z, a, nr) in
              enumerate(zip(case["zone"], case["avail"], case["n_running"]))]
     storage = [Storage("s%02d" % k, zones[z]) for k, z in enumerate(case["storage_zone"])]
-    cluster = Cluster(hosts, storage, Meta(zones, cost, bw))
+    routes = {}
+    if "rt_in" in case:     # storage <-> host routes with the recorded realtime bandwidths
+        for k, s in enumerate(storage):
+            for j, h in enumerate(hosts):
+                zs, zh = names.index(s.locality.name), names.index(h.locality.name)
+                routes[(s.id, h.id)] = Route(float(bw[zs][zh]), case["rt_in"][k][j])
+                routes[(h.id, s.id)] = Route(float(bw[zh][zs]), case["rt_out"][k][j])
+    cluster = Cluster(hosts, storage, Meta(zones, cost, bw), routes)
     apps, conts = {}, []
     for k, c in enumerate(case["containers"]):
         app = apps.setdefault(c["app"], Application("app%d" % c["app"]))

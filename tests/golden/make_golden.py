@@ -435,6 +435,60 @@ def case_trace(world, name, n_hosts, n_apps, job_file, max_tasks, seed, full_rou
     return state
 
 
+# realtime_bw=True (cost_aware.py:17,79,112): the bandwidth of a storage<->host pair is each
+# route's realtime_bw (resources/network.py:70-73), 1 / ((queued MB + 1) / bw) -- so routes get
+# queued packets here, and the fixture records every route's realtime_bw as the policy read it.
+RT_RUNS = [
+    ("cost_aware", {"bin_pack_algo": "first-fit", "sort_tasks": True, "sort_hosts": True,
+                    "realtime_bw": True}, 0),
+    ("cost_aware", {"bin_pack_algo": "first-fit", "sort_tasks": False, "sort_hosts": True,
+                    "realtime_bw": True}, 1),
+    ("cost_aware", {"bin_pack_algo": "first-fit", "sort_tasks": True, "sort_hosts": True,
+                    "realtime_bw": True, "host_decay": True}, 3),
+    ("cost_aware", {"bin_pack_algo": "best-fit", "sort_tasks": True, "realtime_bw": True}, 4),
+    ("cost_aware", {"bin_pack_algo": "best-fit", "sort_tasks": False, "realtime_bw": True}, 5),
+    ("cost_aware", {"bin_pack_algo": "best-fit", "sort_tasks": True}, 4),
+]
+
+
+def queue_packets(world, cluster, rs, frac=0.4, max_pkts=3):
+    """Queue packets (1..max_pkts, uniform sizes up to 4000 MB) on a fraction of the
+    storage<->host routes, as in-flight data pulls would (resources/network.py:82-100)."""
+    from resources.network import Packet
+    env = world.simpy.Environment()
+    for s in cluster.storage:
+        for h in cluster.hosts:
+            for r in (cluster.get_route(s.id, h.id), cluster.get_route(h.id, s.id)):
+                if rs.random_sample() < frac:
+                    for _ in range(rs.randint(1, max_pkts + 1)):
+                        r._NetworkRoute__pkts.items.append(Packet(float(rs.uniform(1, 4000)), env.event()))
+
+
+def record_realtime(cluster):
+    """Every storage<->host route's realtime_bw, as the policy reads it: rt_in[k][h] for
+    storage k -> host h, rt_out[k][h] for host h -> storage k."""
+    rt_in = [[cluster.get_route(s.id, h.id).realtime_bw for h in cluster.hosts] for s in cluster.storage]
+    rt_out = [[cluster.get_route(h.id, s.id).realtime_bw for h in cluster.hosts] for s in cluster.storage]
+    return rt_in, rt_out
+
+
+def case_realtime(world, name, n_hosts, n_apps, job_file, max_tasks, seed, runs):
+    """A config-1-shaped state (storage<->host routes only) with queued packets on its routes."""
+    env = world.simpy.Environment()
+    cluster = world.cluster(env, n_hosts, False)
+    rs = world.np.random.RandomState(seed)
+    fill_hosts(world, cluster, rs)
+    running = add_running(cluster, rs)
+    apps = world.apps(env, job_file, n_apps)
+    tasks = make_ready(world, apps, cluster, rs, max_tasks)
+    queue_packets(world, cluster, rs)
+    state = record_state(world, cluster, tasks, running)
+    state["name"] = name
+    state["rt_in"], state["rt_out"] = record_realtime(cluster)
+    state["runs"] = [run_policy(world, env, cluster, tasks, p, dict(k), s) for p, k, s in runs]
+    return state
+
+
 class _Cont:
     """A ready task's container for hand-built edge cases (no predecessors)."""
 
@@ -539,15 +593,32 @@ def main():
     import logging
     logging.disable(logging.CRITICAL)
     world = World()
+    only = sys.argv[1:]
+    if only:      # e.g. `make_golden.py rt_c1_h100`: the realtime_bw fixtures alone
+        cases = [c for c in realtime_cases(world) if c["name"] in only]
+        write_cases(cases)
+        return
     cases = []
     cases += edge_cases(world)
     cases.append(case_trace(world, "c1_sim_h100", 100, 100, "jobs-5000-200-172800-259200.yaml",
                             800, 42, True, SIM_RUNS))
     cases.append(case_trace(world, "c2_h1000", 1000, 200, "jobs-5000-200-86400-172800.yaml",
                             1500, 43, False, SIM_RUNS))
+    cases += realtime_cases(world)
     cost, bw = world.tables()
     with open(os.path.join(HERE, "zones_seed0.json"), "w") as f:
         json.dump({"zones": [repr(z) for z in world.zones], "cost": cost, "bw": bw}, f)
+    write_cases(cases)
+
+
+def realtime_cases(world):
+    return [case_realtime(world, "rt_c1_h100", 100, 100, "jobs-5000-200-172800-259200.yaml", 800,
+                          44, RT_RUNS),
+            case_realtime(world, "rt_h12", 12, 100, "jobs-5000-200-172800-259200.yaml", 300, 45,
+                          RT_RUNS)]
+
+
+def write_cases(cases):
     for c in cases:
         fn = os.path.join(HERE, "%s.json.gz" % c["name"])
         with gzip.open(fn, "wt") as f:

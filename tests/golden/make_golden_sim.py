@@ -59,6 +59,8 @@ CONFIGS = [
     ("h12", 12, 100, "jobs-5000-200-172800-259200.yaml", SIM_POLICIES + EXTRA_POLICIES),
     # config 2 shape: 1000 hosts, sim.py's three policies, another trace file
     ("c2", 1000, 300, "jobs-5000-200-86400-172800.yaml", SIM_POLICIES),
+    # config 2 at the top of its sweep (alibaba/sim.py:199+ n_apps up to 1000)
+    ("c2a1000", 1000, 1000, "jobs-5000-200-86400-172800.yaml", SIM_POLICIES),
 ]
 
 

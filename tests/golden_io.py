@@ -16,7 +16,7 @@ from pivot_place._abi import RoundArrays
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 CASES = ["empty", "one_host", "ties", "exact_fit", "opp_single", "saturate", "pred_ties", "decay",
-         "c1_sim_h100", "c2_h1000"]
+         "c1_sim_h100", "c2_h1000", "rt_c1_h100", "rt_h12"]
 
 
 @functools.lru_cache(maxsize=None)
@@ -78,12 +78,26 @@ def run_arrays(case, run):
         kw["sort_hosts"] = bool(k.get("sort_hosts", False))
         if k.get("host_decay"):
             kw["decay"] = np.maximum(np.array(case["n_running"], dtype=np.int32), 1)
+        if k.get("realtime_bw"):
+            kw["rt_bw"] = realtime_rows(case, ga if ga else [0])
     elif mode in (_abi.PVT_VBP_FF, _abi.PVT_VBP_BF):
         kw["sort_tasks"] = bool(str(k.get("decreasing", False)))
         kw["tiebreak"] = np.array(case["id_rank"], dtype=np.uint32)
     else:
         kw["mt_state"] = mt_state(run["seed"])
     return RoundArrays(**kw)
+
+
+def realtime_rows(case, anchor_zones):
+    """(G, H) realtime bandwidth per group: in_route.realtime_bw + out_route.realtime_bw of the
+    group's anchor storage (the storage of its anchor zone; cost_aware.py:73-79) and each host."""
+    sz = case["storage_zone"]
+    rt_in, rt_out = case["rt_in"], case["rt_out"]
+    rows = []
+    for z in anchor_zones:
+        k = sz.index(z)
+        rows.append([a + b for a, b in zip(rt_in[k], rt_out[k])])
+    return np.array(rows, dtype=np.float64).reshape(len(anchor_zones), -1)
 
 
 def expected(case, run):

@@ -45,7 +45,7 @@ def test_round_struct_layout_matches_header():
     body = re.search(r"typedef struct pvt_round \{(.*?)\} pvt_round;", text, flags=re.S).group(1)
     fields = re.findall(r"\b(\w+);", body)
     assert fields == [f for f, _ in _abi.pvt_round._fields_]
-    assert ctypes.sizeof(_abi.pvt_round) == 8 * 4 + 12 * 8
+    assert ctypes.sizeof(_abi.pvt_round) == 8 * 4 + 13 * 8
 
 
 def test_anchor_struct_layout_matches_header():

@@ -107,3 +107,20 @@ def test_epochs_exact_fits_tie_at_zero(engine):
     ref = oracle.place(r, threads=8)
     res, _ = _place(engine, r)
     _same(res, ref)
+
+
+def test_epochs_long_chains_split(engine):
+    """40 groups anchored alternately in two zero-cost components (zones 0-2 and 3-5): each
+    component's chain exceeds a walk's cap, so epochs split inside the chain sequence."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 30_000, 8000, seed=12)
+    rs = np.random.RandomState(12)
+    groups = np.sort(rs.randint(0, 40, size=r.n_tasks))
+    first = {}
+    for g in groups:
+        first.setdefault(int(g), len(first))
+    r.task_group = np.array([first[int(g)] for g in groups], dtype=np.int32)
+    r.group_anchor = np.array([(g % 2) * 3 + (g // 2) % 3 for g in first.keys()], dtype=np.int32)
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    assert st["epochs"] >= 2

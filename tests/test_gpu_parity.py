@@ -186,3 +186,27 @@ def test_score_instances_both_tasks_per_wave(engine, mode, tw, H, T, window):
         engine.set_score_tw(0)
         engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
     _assert_same(res, ref.placement, ref.order, ref.avail)
+
+
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_FF, _abi.PVT_CA_BF])
+@pytest.mark.parametrize("H,T,epochs", [(3000, 400, True), (20_000, 1500, True), (20_000, 1500, False),
+                                         (70_000, 3000, True)])
+def test_realtime_bw_synthetic(engine, mode, H, T, epochs):
+    """cost_aware with realtime_bw (cost_aware.py:79,112): a bandwidth per (group, host) -- here
+    the static one scaled by random queue factors -- through the resident kernel (3000 hosts),
+    the windowed engine and the epochs; equal to the CPU restatement."""
+    r = synthetic.make_round(mode, H, T, seed=41)
+    r.cost = r.cost + 0.001            # no free-egress zone: every score depends on the bandwidth
+    rs = np.random.RandomState(41)
+    bsum = r.bw + r.bw.T
+    a = r.group_anchor
+    r.rt_bw = (bsum[a][:, r.zone] / rs.randint(1, 4, size=(len(a), H))).astype(np.float64)
+    ref = oracle.place(r)
+    try:
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS if H <= 4096 else 0)
+        engine.set_epochs(epochs)
+        res = engine.place(r)
+    finally:
+        engine.set_epochs(True)
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+    _assert_same(res, ref.placement, ref.order, ref.avail)
