@@ -74,7 +74,7 @@ def parse():
     p.add_argument("--extra", type=int, default=-1,
                    help="1: also time (and parity-check) the other policies at config 5 and all "
                         "policies at config 3; -1 (default): only for the default workload at N=1")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02_score_pmc.json"),
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02c_score_pmc.json"),
                    help="rocprofv3 PMC summary of the score kernel of this binary "
                         "(tools/pmc_profile.py); absent or another config = counters null")
     return p.parse_args()

@@ -482,8 +482,8 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   S = (nsq + seg_sup - 1) / seg_sup;
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
-  launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord), nullptr,
-                      P<int32_t>(ctx->anc_ord), st);
+  launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord),
+                      P<int32_t>(ctx->anc_ord), nullptr, st);
   // Pipelined windows (W <= OPP_MAXW / 2, so a walk's inherited + own touched hosts fit its
   // LDS): window k+1's count pass runs on the side stream while window k is walked. Walk k
   // leaves global availability untouched and hands its hosts to walk k+1, which applies them
@@ -568,8 +568,8 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   ENSURE(ctx->grp_ord, sizeof(int32_t) * T);
-  launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord), P<int32_t>(ctx->grp_ord),
-                      P<int32_t>(ctx->anc_ord), st);
+  launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
+                      P<int32_t>(ctx->anc_ord), P<int32_t>(ctx->grp_ord), st);
   const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
   if (ca) {
     ENSURE(ctx->csum, sizeof(double) * Z * Z);

@@ -37,80 +37,97 @@ __device__ __forceinline__ int seg_adv(const EpochArgs& A, int j) {
   return max(0, min(len, done));
 }
 
-// Block (segment j, 256-task tile of j): every thread holds one walked task of j and checks it
-// against the final log entries of every earlier segment of another chain, staged 256 at a time
-// in LDS (each entry is read once per tile and broadcast to the tile's tasks).
+// Block (task tile x of segment j, entry slice z): every thread holds one walked task of j; the
+// block stages the final log entries of slice z of the window's earlier tasks (those of other
+// chains' segments) 256 at a time in LDS -- host, capacities, and the zone-table (or realtime)
+// c and bw for j's anchor, which every task of j shares -- so the pair checks are LDS broadcasts
+// only. Slices split each segment's checks over VAL_SPLIT blocks.
+constexpr int VAL_SPLIT = 8;
+__device__ __forceinline__ int seg_of(const EpochArgs& A, int e) {
+  int lo = 0, hi = A.nseg - 1;                // the segment holding window task e
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (A.seg_off[mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
   __shared__ int32_t e_id[256];
   __shared__ double e_a[4][256];
+  __shared__ double e_c[256], e_b[256];
   __shared__ int32_t stop;
   const int j = blockIdx.y, tid = threadIdx.x;
   if (j == 0 || j >= A.nseg) return;
   const int s0 = A.seg_off[j], adv = seg_adv(A, j);
+  if ((int)blockIdx.x * 256 >= adv) return;
+  const int L = s0;                           // earlier window tasks: [0, s0)
+  const int lo = (int)((long long)L * blockIdx.z / VAL_SPLIT);
+  const int hi = (int)((long long)L * (blockIdx.z + 1) / VAL_SPLIT);
+  if (lo >= hi) return;
   const int t = s0 + blockIdx.x * 256 + tid;
-  if (blockIdx.x * 256 >= adv) return;
   const bool mine = t < s0 + adv;
   const int cj = A.seg_chain[j];
+  const int a = A.anc[s0];                    // a segment is one group: one anchor, one row
+  const double* rtrow = A.rtb ? A.rtb + (size_t)A.grp[s0] * A.H : nullptr;
   WinRec w{};
   double d0 = 0, d1 = 0, d2 = 0, d3 = 0;
-  int a = 0, g = 0;
   bool active = false;
   if (mine) {
     w = A.wlog[t];
     active = w.id >= 0;                      // no host fits: stays so (capacities only drop)
     d0 = A.dem[(size_t)t * 4]; d1 = A.dem[(size_t)t * 4 + 1];
     d2 = A.dem[(size_t)t * 4 + 2]; d3 = A.dem[(size_t)t * 4 + 3];
-    a = A.anc[t];
-    g = A.rtb ? A.grp[t] : 0;
   }
   const uint64_t w1 = (uint64_t)__double_as_longlong(w.s);
-  if (tid == 0) stop = 0;
+  if (tid == 0) stop = __hip_atomic_load(&A.bad[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   bool beaten = false;
-  for (int s = 0; s < j && !stop; s++) {
-    if (A.seg_chain[s] == cj) continue;     // same chain: walked in order, exact
-    const int e0 = A.seg_off[s], ne = seg_adv(A, s);
-    for (int c0 = 0; c0 < ne; c0 += 256) {
-      __syncthreads();
-      if (c0 + tid < ne) {
-        const WinRec& e = A.wlog[e0 + c0 + tid];
-        const bool fin = e.id >= 0 && !e.sup;
-        e_id[tid] = fin ? e.id : -1;
-        e_a[0][tid] = e.a[0]; e_a[1][tid] = e.a[1]; e_a[2][tid] = e.a[2]; e_a[3][tid] = e.a[3];
-      } else {
-        e_id[tid] = -1;
-      }
-      __syncthreads();
-      if (active && !beaten) {
-        const int n = min(256, ne - c0);
-        for (int k = 0; k < n; k++) {
-          const int32_t h = e_id[k];
-          if (h < 0) continue;
-          const double f0 = e_a[0][k], f1 = e_a[1][k], f2 = e_a[2][k], f3 = e_a[3][k];
-          bool hit = (h == w.id);
-          if (!hit && fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) {
-            const int z = A.zone[h];
-            const double s2 = norm2_seq(f0 - d0, f1 - d1, f2 - d2, f3 - d3);
-            const double c = A.csum[a * A.Z + z];
-            const double bw = A.rtb ? A.rtb[(size_t)g * A.H + h] : A.bsum[a * A.Z + z];
-            if (c == 0.0) {
-              // zero egress cost: the score is exactly +0 (finite s2, bw > 0)
-              hit = (0ull < w1) | ((0ull == w1) & (h < w.id));
-            } else if (w1 == 0ull && s2 >= 0x1p-600 && c >= 0x1p-300 && bw <= 0x1p300) {
-              hit = false;   // c * sqrt(s2) >= 2^-600 and / bw >= 2^-900: the score is > 0
-            } else {
-              const double sc = (c * __builtin_sqrt(s2)) / bw;
-              const uint64_t k1 = (uint64_t)__double_as_longlong(sc);
-              hit = (k1 < w1) | ((k1 == w1) & (h < w.id));
-            }
-          }
-          if (hit) { beaten = true; break; }
+  for (int c0 = lo; c0 < hi && !stop; c0 += 256) {
+    const int e = c0 + tid;
+    int32_t id = -1;
+    if (e < hi) {
+      const int s = seg_of(A, e);
+      if (A.seg_chain[s] != cj && e - A.seg_off[s] < seg_adv(A, s)) {
+        const WinRec& x = A.wlog[e];
+        if (x.id >= 0 && !x.sup) {
+          id = x.id;
+          e_a[0][tid] = x.a[0]; e_a[1][tid] = x.a[1]; e_a[2][tid] = x.a[2]; e_a[3][tid] = x.a[3];
+          const int z = A.zone[id];
+          e_c[tid] = A.csum[a * A.Z + z];
+          e_b[tid] = rtrow ? rtrow[id] : A.bsum[a * A.Z + z];
         }
       }
-      if (beaten) stop = 1;                  // benign race: every writer stores 1
-      __syncthreads();
-      if (stop) break;
     }
+    e_id[tid] = id;
+    __syncthreads();
+    if (active && !beaten) {
+      const int n = min(256, hi - c0);
+      for (int k = 0; k < n; k++) {
+        const int32_t h = e_id[k];
+        if (h < 0) continue;
+        const double f0 = e_a[0][k], f1 = e_a[1][k], f2 = e_a[2][k], f3 = e_a[3][k];
+        bool hit = (h == w.id);
+        if (!hit && fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) {
+          const double s2 = norm2_seq(f0 - d0, f1 - d1, f2 - d2, f3 - d3);
+          const double c = e_c[k], bw = e_b[k];
+          if (c == 0.0) {
+            // zero egress cost: the score is exactly +0 (finite s2, bw > 0)
+            hit = (0ull < w1) | ((0ull == w1) & (h < w.id));
+          } else if (w1 == 0ull && s2 >= 0x1p-600 && c >= 0x1p-300 && bw <= 0x1p300) {
+            hit = false;   // c * sqrt(s2) >= 2^-600 and / bw >= 2^-900: the score is > 0
+          } else {
+            const double sc = (c * __builtin_sqrt(s2)) / bw;
+            const uint64_t k1 = (uint64_t)__double_as_longlong(sc);
+            hit = (k1 < w1) | ((k1 == w1) & (h < w.id));
+          }
+        }
+        if (hit) { beaten = true; break; }
+      }
+    }
+    if (beaten) stop = 1;                    // benign race: every writer stores 1
+    __syncthreads();
   }
   if (tid == 0 && stop) __hip_atomic_store(&A.bad[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -135,7 +152,7 @@ __global__ __launch_bounds__(256) void epoch_apply_kernel(EpochArgs A, int n_acc
 
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {
   const int tiles = (CHAIN_MAX + 255) / 256;   // a segment never exceeds its chain's cap
-  hipLaunchKernelGGL(epoch_validate_kernel, dim3(tiles, a.nseg), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(epoch_validate_kernel, dim3(tiles, a.nseg, VAL_SPLIT), dim3(256), 0, st, a);
 }
 
 void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st) {

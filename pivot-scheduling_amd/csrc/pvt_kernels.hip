@@ -792,7 +792,7 @@ __global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const
   const int t = ord[p];
   double* o = dem_ord + (size_t)p * 4;
   o[0] = dem[t]; o[1] = dem[(size_t)T + t]; o[2] = dem[2 * (size_t)T + t]; o[3] = dem[3 * (size_t)T + t];
-  anc_ord[p] = (tg && ga) ? ga[tg[t]] : 0;
+  if (anc_ord) anc_ord[p] = (tg && ga) ? ga[tg[t]] : 0;
   if (grp_ord) grp_ord[p] = tg ? tg[t] : 0;
 }
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,

@@ -198,18 +198,28 @@ __device__ __forceinline__ void put_rec(int32_t* res, int base, double s, uint32
 
 // Exact best-fit key of a host for the task: (score bits, tiebreak:id); scores are >= +0, so
 // their bit patterns order like the values (cost_aware.py:83, vbp.py:45).
-// rtrow: the task's group row of the realtime bandwidth (cost_aware.py:79), or NULL.
+// The cost_aware score (c * sqrt(s2)) / bw without its square root and division where they
+// cannot matter: c == 0 (a zero-cost zone pair) gives exactly +0 (finite s2, bw > 0); and when
+// only a score of 0 can win (lim1 == 0, the bits of +0), c >= 2^-300, bw <= 2^300 and
+// s2 >= 2^-600 prove the score positive (>= 2^-900): the key is then "beats nothing" (~0).
+__device__ __forceinline__ uint64_t ca_score_bits(double c, double s2, double bw, uint64_t lim1) {
+  if (c == 0.0) return 0ull;
+  if (lim1 == 0ull && c >= 0x1p-300 && bw <= 0x1p300 && s2 >= 0x1p-600) return ~0ull;
+  return (uint64_t)__double_as_longlong((c * __builtin_sqrt(s2)) / bw);
+}
+
+// rtrow: the task's group row of the realtime bandwidth (cost_aware.py:79), or NULL. lim1: the
+// score bits a candidate must reach to matter (see ca_score_bits; ~0 = any).
 template <int MODE>
 __device__ __forceinline__ void bf_key(const WalkLDS& S, int Z, int anc, const double* rtrow,
                                        double a0, double a1, double a2, double a3, double d0,
                                        double d1, double d2, double d3, int32_t z, uint32_t tb,
-                                       int32_t id, uint64_t& k1, uint64_t& k2) {
+                                       int32_t id, uint64_t lim1, uint64_t& k1, uint64_t& k2) {
   const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
-  double sc;
   if (MODE == CA_BF)
-    sc = (S.csum[anc * Z + z] * __builtin_sqrt(s2)) / (rtrow ? rtrow[id] : S.bsum[anc * Z + z]);
-  else sc = __builtin_sqrt(s2);
-  k1 = (uint64_t)__double_as_longlong(sc);
+    k1 = ca_score_bits(S.csum[anc * Z + z], s2, rtrow ? rtrow[id] : S.bsum[anc * Z + z], lim1);
+  else
+    k1 = (uint64_t)__double_as_longlong(__builtin_sqrt(s2));
   k2 = ((uint64_t)(MODE == VBP_BF ? tb : 0u) << 32) | (uint32_t)id;
 }
 __device__ __forceinline__ bool key_lt(uint64_t a1, uint64_t a2, uint64_t b1, uint64_t b2) {
@@ -342,7 +352,8 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k
       if (__ballot(fit) == 0) continue;
       uint64_t k1 = ~0ull, k2 = ~0ull;
       bf_key<MODE>(S, A.Z, anc, rtrow, a0, a1, a2, a3, d0, d1, d2, d3, S.lz[qq],
-                   MODE == VBP_BF ? S.ltb[qq] : 0u, S.lid[qq], k1, k2);
+                   MODE == VBP_BF ? S.ltb[qq] : 0u, S.lid[qq], b1 < tk1[LOOK - 1] ? b1 : tk1[LOOK - 1],
+                   k1, k2);
       uint64_t pm = __ballot(fit && key_lt(k1, k2, b1, b2) && key_lt(k1, k2, tk1[LOOK - 1], tk2[LOOK - 1]));
       while (pm) {
         const int L = __builtin_ctzll(pm);
@@ -624,7 +635,6 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
         k1[r] = ~0ull; k2[r] = ~0ull;
         if (xf[r]) {
           const double s2 = norm2_seq(X[r].a0 - d0, X[r].a1 - d1, X[r].a2 - d2, X[r].a3 - d3);
-          double sc;
           if (MODE == CA_BF) {
             // its zone-table entries for this anchor (realtime_bw: its bandwidth for this group)
             const int ck = A.rtb ? grp : anc;
@@ -633,11 +643,10 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
               X[r].c = S.csum[anc * A.Z + X[r].z];
               X[r].b = A.rtb ? A.rtb[(size_t)grp * A.H + X[r].id] : S.bsum[anc * A.Z + X[r].z];
             }
-            sc = (X[r].c * __builtin_sqrt(s2)) / X[r].b;
+            k1[r] = ca_score_bits(X[r].c, s2, X[r].b, t1);   // must beat the best so far
           } else {
-            sc = __builtin_sqrt(s2);
+            k1[r] = (uint64_t)__double_as_longlong(__builtin_sqrt(s2));
           }
-          k1[r] = (uint64_t)__double_as_longlong(sc);
           k2[r] = ((uint64_t)(MODE == VBP_BF ? X[r].tb : 0u) << 32) | (uint32_t)X[r].id;
         }
       }

@@ -78,8 +78,8 @@ def test_epochs_groups_spill_and_collide(engine, seed):
 
 
 def test_epochs_repeated_anchor_zones(engine):
-    """40 groups over 20 zones (each zone anchors two groups): epochs split where an anchor
-    repeats."""
+    """40 groups over 20 zones (each zone anchors two groups): groups of one zero-cost
+    component share a chain walk, in order."""
     r = synthetic.make_round(_abi.PVT_CA_BF, 60_000, 8000, seed=8)
     rs = np.random.RandomState(8)
     groups = rs.randint(0, 40, size=r.n_tasks)
@@ -91,7 +91,7 @@ def test_epochs_repeated_anchor_zones(engine):
     ref = oracle.place(r, threads=8)
     res, st = _place(engine, r)
     _same(res, ref)
-    assert st["epochs"] >= 2
+    assert st["segments"] >= 40
 
 
 def test_epochs_exact_fits_tie_at_zero(engine):
