@@ -70,6 +70,10 @@ struct RoundState {
   int key_group = -1;             // group whose frozen first-fit key is computed
   int t0 = 0, W = 0, Wmax = 0, nt = 0;
   int lb = 0;                     // list buffer of the current window
+  // host-sharded opportunistic rounds: windows of opp_W tasks; this rank counts super-chunks
+  // [opp_sq_lo, opp_sq_hi); packages hold opp_Psq super-chunks per task (the largest share)
+  bool opp = false;
+  int opp_W = 0, opp_nq = 0, opp_nsq = 0, opp_Psq = 0, opp_sq_lo = 0, opp_sq_hi = 0;
   std::vector<int> egs, ega;      // cost_aware best-fit epochs: group starts (+ T) and anchors
   std::vector<int> ecomp;         // zone -> its component of zones joined by zero egress cost
   bool in_epoch = false;          // lists scored for an epoch (place_epochs)
@@ -507,7 +511,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   auto count = [&](int k, hipStream_t s) {
     const int t0 = k * W, nt = std::min(W, T - t0);
     OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, S, seg_sup, nq, nsq,
-                    W, bm_of(k % nbuf), sc_of(k % nbuf)};
+                    W, bm_of(k % nbuf), sc_of(k % nbuf), 0, nsq, nq, nsq};
     Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc, s);
     launch_opp_count(ca, s);
   };
@@ -1237,6 +1241,121 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
 // ---------------------------------------------------------------- host-dimension sharding
 static int shard_depth(int world) { return std::max(KL, LMAX / std::max(world, 1)); }
 
+// ---- host-sharded opportunistic rounds (per-rank feasible counts, exchanged;
+// the draw and the k-th selection replicated). Each rank counts its super-chunks of a window
+// (bitmaps + counts, task-major) into its package; after the all-gather every rank unpacks the
+// full tables and runs the same commit walk, so placements, availability and the MT19937 state
+// are identical on all ranks and equal to pvt_place()'s.
+static constexpr int OPP_SHARD_WINDOW = OPP_WINDOW_DEFAULT;
+static constexpr int OPP_SUP_HOSTS = OPP_SUP * OPP_CH;
+
+static size_t opp_pkg_bytes(const RoundState& R, int nt) {
+  return (size_t)nt * R.opp_Psq * OPP_SUP * 4 * sizeof(uint64_t) + (size_t)nt * R.opp_Psq * sizeof(int32_t);
+}
+static size_t opp_table_bytes(const RoundState& R) {   // full bitmaps + counts of one window
+  return (((size_t)R.opp_W * R.opp_nq * 4 * sizeof(uint64_t) + (size_t)R.opp_W * R.opp_nsq * sizeof(int32_t)) + 255) / 256 * 256;
+}
+
+static int opp_shard_begin(pvt_ctx* ctx, const pvt_round* r, int lo, int hi, int world,
+                           int64_t* max_package_bytes) {
+  RoundState& R = ctx->rs;
+  const int H = r->n_hosts, T = r->n_tasks;
+  if (!r->mt_state) return fail(ctx, PVT_EINVAL, "opportunistic needs mt_state");
+  R.r = *r;
+  R.T = T; R.H = H; R.Z = r->n_zones; R.lo = lo; R.hi = hi; R.world = world;
+  R.t0 = 0; R.nt = 0; R.opp = true;
+  R.opp_W = OPP_SHARD_WINDOW;
+  R.opp_nq = (H + OPP_CH - 1) / OPP_CH;
+  R.opp_nsq = (R.opp_nq + OPP_SUP - 1) / OPP_SUP;
+  R.opp_Psq = (R.opp_nsq + world - 1) / world;
+  if ((lo % OPP_SUP_HOSTS != 0 && lo != H) || (hi != H && hi % OPP_SUP_HOSTS != 0) ||
+      hi - lo > R.opp_Psq * OPP_SUP_HOSTS)
+    return fail(ctx, PVT_EINVAL, "opportunistic shard [%d, %d) must span whole super-chunks of %d hosts, "
+                "at most %d of them (rank r: [r*%d, (r+1)*%d) clamped to H)", lo, hi, OPP_SUP_HOSTS,
+                R.opp_Psq, R.opp_Psq * OPP_SUP_HOSTS, R.opp_Psq * OPP_SUP_HOSTS);
+  R.opp_sq_lo = lo < hi ? lo / OPP_SUP_HOSTS : 0;    // an empty shard counts nothing
+  R.opp_sq_hi = lo < hi ? (hi + OPP_SUP_HOSTS - 1) / OPP_SUP_HOSTS : 0;
+  if (max_package_bytes) *max_package_bytes = (int64_t)opp_pkg_bytes(R, R.opp_W);
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  if (T > 0) {
+    HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
+    launch_iota(r->order, T, st);
+    ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
+    launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord), nullptr,
+                        nullptr, st);
+    ENSURE(ctx->opp, opp_table_bytes(R) + sizeof(uint32_t) * 640);
+    uint32_t* mt = reinterpret_cast<uint32_t*>(P<char>(ctx->opp) + opp_table_bytes(R));
+    HIPCHK(hipMemcpyAsync(mt, r->mt_state, sizeof(uint32_t) * 625, hipMemcpyHostToDevice, st));
+  }
+  R.active = true;
+  return PVT_OK;
+}
+
+static int opp_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out, int64_t* package_bytes) {
+  RoundState& R = ctx->rs;
+  hipStream_t st = ctx->stream;
+  if (R.t0 >= R.T) {                          // done: the MT19937 state back to the caller
+    if (R.T > 0) {
+      uint32_t* mt = reinterpret_cast<uint32_t*>(P<char>(ctx->opp) + opp_table_bytes(R));
+      HIPCHK(hipMemcpyAsync(R.r.mt_state, mt, sizeof(uint32_t) * 625, hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    R.active = false;
+    return PVT_OK;
+  }
+  const int nt = std::min(R.opp_W, R.T - R.t0);
+  const int nsr = std::max(0, R.opp_sq_hi - R.opp_sq_lo);
+  const int task_waves = (nt + OPP_TW - 1) / OPP_TW;
+  int S = std::max(1, std::min(std::max(nsr, 1), (4096 + task_waves - 1) / task_waves));
+  const int seg_sup = (std::max(nsr, 1) + S - 1) / S;
+  S = (std::max(nsr, 1) + seg_sup - 1) / seg_sup;
+  uint64_t* bm = reinterpret_cast<uint64_t*>(package);
+  int32_t* sc = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(package) +
+                                           (size_t)nt * R.opp_Psq * OPP_SUP * 4 * sizeof(uint64_t));
+  if (nsr > 0) {
+    OppCountArgs ca{R.r.avail, P<double>(ctx->dem_ord) + (size_t)R.t0 * 4, R.H, nt, S, seg_sup,
+                    R.opp_nq, R.opp_nsq, nt, bm, sc, R.opp_sq_lo, R.opp_sq_hi,
+                    R.opp_Psq * OPP_SUP, R.opp_Psq};
+    Scope s(ctx, PVT_K_SCORE, (double)nt * (R.hi - R.lo), (double)nt * (R.hi - R.lo) * 32.0);
+    launch_opp_count(ca, st);
+  }
+  HIPCHK(hipGetLastError());
+  R.nt = nt;
+  ctx->windows++;
+  *n_tasks_out = nt;
+  *package_bytes = (int64_t)opp_pkg_bytes(R, nt);
+  HIPCHK(hipStreamSynchronize(st));           // the package is complete when this returns
+  return PVT_OK;
+}
+
+static int opp_shard_commit(pvt_ctx* ctx, const void* packages) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  const int nt = R.nt, t0 = R.t0;
+  char* base = P<char>(ctx->opp);
+  uint64_t* bm = reinterpret_cast<uint64_t*>(base);
+  int32_t* sc = reinterpret_cast<int32_t*>(base + (size_t)R.opp_W * R.opp_nq * 4 * sizeof(uint64_t));
+  uint32_t* mt = reinterpret_cast<uint32_t*>(base + opp_table_bytes(R));
+  OppUnpackArgs ua{reinterpret_cast<const uint8_t*>(packages), (int64_t)opp_pkg_bytes(R, nt),
+                   R.world, nt, R.opp_nq, R.opp_nsq, R.opp_Psq, R.opp_W, bm, sc};
+  {
+    Scope s(ctx, PVT_K_MERGE, 0, 0);
+    launch_opp_unpack(ua, st);
+  }
+  OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm, sc, R.H, nt, R.opp_nq,
+                   R.opp_nsq, R.opp_W, r->placement + t0, mt, ctx->stamps, nullptr, nullptr, 1};
+  {
+    Scope s(ctx, PVT_K_COMMIT, 0, 0);
+    launch_opp_commit(oa, st);
+  }
+  HIPCHK(hipGetLastError());
+  R.t0 += nt;
+  R.nt = 0;
+  return PVT_OK;
+}
+
 extern "C" int pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo,
                                int32_t host_hi, int32_t world, int64_t* max_package_bytes) {
   if (!ctx || !r) return PVT_EINVAL;
@@ -1245,8 +1364,13 @@ extern "C" int pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo
     return fail(ctx, PVT_EINVAL, "world %d outside [1, %d]", world, PVT_SHARD_MAX_WORLD);
   if (host_lo < 0 || host_hi < host_lo || host_hi > r->n_hosts)
     return fail(ctx, PVT_EINVAL, "bad host range [%d, %d) of %d", host_lo, host_hi, r->n_hosts);
-  if (r->mode == PVT_OPP)
-    return fail(ctx, PVT_EUNSUPPORTED, "opportunistic rounds are not host-sharded (scenario-shard them)");
+  ctx->rs.opp = false;
+  if (r->mode == PVT_OPP) {
+    int rc = check_round(ctx, r);
+    if (rc) return rc;
+    ctx->windows = ctx->refills = 0;
+    return opp_shard_begin(ctx, r, host_lo, host_hi, world, max_package_bytes);
+  }
   int rc = round_begin(ctx, r, host_lo, host_hi, world);
   if (rc) return rc;
   const int PK = shard_depth(world);
@@ -1262,6 +1386,7 @@ extern "C" int pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out
   *package_bytes = 0;
   if (!ctx->rs.active || ctx->rs.world < 1) return fail(ctx, PVT_EINVAL, "no sharded round in progress");
   if (ctx->rs.nt != 0) return fail(ctx, PVT_EINVAL, "pvt_shard_score called twice without pvt_shard_commit");
+  if (ctx->rs.opp) return opp_shard_score(ctx, package, n_tasks_out, package_bytes);
   int nt = 0, rc;
   if ((rc = round_next_window(ctx, &nt))) return rc;
   if (nt == 0) {
@@ -1288,6 +1413,7 @@ extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
   if (!ctx || !packages) return PVT_EINVAL;
   RoundState& R = ctx->rs;
   if (!R.active || R.nt == 0) return fail(ctx, PVT_EINVAL, "pvt_shard_commit without a scored window");
+  if (R.opp) return opp_shard_commit(ctx, packages);
   const int PK = shard_depth(R.world);
   Lists L;
   lists_from(ctx, L);

@@ -24,9 +24,24 @@ struct OppCountArgs {
   const double* avail;
   const double* dem;      // window tasks [nt][4]
   int H, nt, S, seg_sup, nq, nsq, ldc;
-  uint64_t* bm;           // [ldc][nq][4] per-chunk feasibility bitmaps (bit = host), task-major
-  int32_t* sc;            // [ldc][nsq] super-chunk counts, task-major
+  uint64_t* bm;           // [ldc][ldq][4] per-chunk feasibility bitmaps (bit = host), task-major
+  int32_t* sc;            // [ldc][lds] super-chunk counts, task-major
+  // super-chunks [sq_lo, sq_hi) are counted (a rank's share under host sharding; [0, nsq)
+  // unsharded); chunk q lands at row position q - sq_lo * OPP_SUP of ldq, super-chunk Q at
+  // Q - sq_lo of lds
+  int sq_lo, sq_hi, ldq, lds;
 };
+
+// Host sharding: rank r's package (ldq = P_sq * OPP_SUP chunks and lds = P_sq super-chunks per
+// task, super-chunks [r * P_sq, ...)) -> the full task-major tables of a window.
+struct OppUnpackArgs {
+  const uint8_t* recv;    // world packages, pkg_bytes each
+  int64_t pkg_bytes;
+  int world, nt, nq, nsq, P_sq, ldc;
+  uint64_t* bm;           // [ldc][nq][4]
+  int32_t* sc;            // [ldc][nsq]
+};
+void launch_opp_unpack(const OppUnpackArgs& a, hipStream_t st);
 
 // A walk's touched hosts handed to the next window's walk (pipelined windows): the next
 // window's count pass ran on the capacities the walk started from, so these hosts are touched

@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
       d0[k] = d1[k] = d2[k] = d3[k] = DINF;
     }
   }
-  const int Q0 = seg * A.seg_sup, Q1 = min(A.nsq, Q0 + A.seg_sup);
+  const int Q0 = A.sq_lo + seg * A.seg_sup, Q1 = min(A.sq_hi, Q0 + A.seg_sup);
   const int qa = Q0 * OPP_SUP, qb = min(A.nq, Q1 * OPP_SUP);
   double n0[U], n1[U], n2[U], n3[U];
   auto fetch = [&](int q) {
@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
       }
     }
     if (lane < nt) {
-      uint64_t* o = A.bm + ((size_t)(t0 + lane) * A.nq + q) * U;
+      uint64_t* o = A.bm + ((size_t)(t0 + lane) * A.ldq + (q - A.sq_lo * OPP_SUP)) * U;
 #pragma unroll
       for (int u = 0; u < U; u++) o[u] = mine[u];
     }
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
         if (lane == k) v = sup[k];
         sup[k] = 0;
       }
-      if (lane < nt) A.sc[(size_t)(t0 + lane) * A.nsq + Q] = v;
+      if (lane < nt) A.sc[(size_t)(t0 + lane) * A.lds + (Q - A.sq_lo)] = v;
     }
   }
 }
@@ -417,6 +417,34 @@ hipError_t opp_init_attrs() {
 
 void launch_opp_commit(const OppCommitArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(opp_commit_kernel, dim3(1), dim3(64), sizeof(OppLDS), st, a);
+}
+
+// Rank packages -> full tables: package r holds, task-major, the chunk bitmaps ([nt][ldq][4]
+// u64) then the super-chunk counts ([nt][lds] i32) of super-chunks [r * P_sq, ...).
+__global__ __launch_bounds__(256) void opp_unpack_kernel(OppUnpackArgs A) {
+  constexpr int U = OPP_CH / WAVE;
+  const int r = blockIdx.y;
+  const int s0 = r * A.P_sq, ns = min(A.P_sq, A.nsq - s0);
+  if (ns <= 0) return;
+  const int ldq = A.P_sq * OPP_SUP, lds = A.P_sq;
+  const int q0 = s0 * OPP_SUP, nqr = min(ns * OPP_SUP, A.nq - q0);
+  const uint8_t* base = A.recv + (size_t)r * A.pkg_bytes;
+  const uint64_t* bm = reinterpret_cast<const uint64_t*>(base);
+  const int32_t* sc = reinterpret_cast<const int32_t*>(base + sizeof(uint64_t) * U * (size_t)A.nt * ldq);
+  const size_t nb = (size_t)A.nt * nqr * U;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < nb; k += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = k / ((size_t)nqr * U), rem = k % ((size_t)nqr * U);
+    A.bm[(t * A.nq + q0) * U + rem] = bm[t * ldq * U + rem];
+  }
+  const size_t ns_all = (size_t)A.nt * ns;
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < ns_all; k += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = k / ns, j = k % ns;
+    A.sc[t * A.nsq + s0 + j] = sc[t * lds + j];
+  }
+}
+
+void launch_opp_unpack(const OppUnpackArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(opp_unpack_kernel, dim3(256, a.world), dim3(256), 0, st, a);
 }
 
 __global__ __launch_bounds__(256) void opp_apply_kernel(const OppTouched* t, double* avail, int H) {

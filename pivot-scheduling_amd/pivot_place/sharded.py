@@ -8,11 +8,30 @@ over xGMI with RCCL (``torch.distributed`` backend "nccl"), staged through host 
 gloo. The reference scans every host of the cluster per task (scheduler/cost_aware.py:88-92,
 scheduler/vbp.py:19-22, 43-47); a sharded round returns exactly what pvt_place() returns.
 
+Opportunistic rounds shard by whole super-chunks of 16384 hosts (the count pass's unit): each
+rank counts the feasible hosts of its super-chunks per task (bitmaps + counts), the window's
+packages are all-gathered, and every rank runs the same draw / k-th-host walk on the full
+tables (per-rank feasible counts -> all-gather -> draw -> select), so the
+MT19937 state and placements agree everywhere (reference scheduler/opportunistic.py:11-20).
+
 ``place_lockstep`` drives several contexts in one process (one per shard, same or different
 GPUs) with the exchange done by concatenation: the same protocol without a process group.
 """
+from . import _abi
 from .engine import DeviceRound
 from .scenarios import shard
+
+OPP_SUPER_CHUNK = 64 * 256     # hosts per super-chunk of the opportunistic count pass
+
+
+def shard_range(n_hosts, world, rank, mode):
+    """Host range of ``rank``: an even split, or for opportunistic rounds whole super-chunks
+    (rank r takes super-chunks [r * P, (r + 1) * P), P = ceil(super-chunks / world))."""
+    if mode != _abi.PVT_OPP:
+        return shard(n_hosts, world, rank)
+    nsq = (n_hosts + OPP_SUPER_CHUNK - 1) // OPP_SUPER_CHUNK
+    per = (nsq + world - 1) // world
+    return (min(n_hosts, rank * per * OPP_SUPER_CHUNK), min(n_hosts, (rank + 1) * per * OPP_SUPER_CHUNK))
 
 
 def torch_exchange(group=None):
@@ -47,14 +66,14 @@ class HostShardedPlacer:
         import torch.distributed as dist
         return cls(engine, dist.get_rank(group), dist.get_world_size(group), torch_exchange(group))
 
-    def host_range(self, n_hosts):
-        return shard(n_hosts, self.world, self.rank)
+    def host_range(self, n_hosts, mode=None):
+        return shard_range(n_hosts, self.world, self.rank, mode)
 
     def run(self, dr: DeviceRound):
         """Place a resident round in place (``dr.placement``/``order``/``avail`` as pvt_place)."""
         import torch
         eng = self.engine
-        lo, hi = self.host_range(dr.arrays.n_hosts)
+        lo, hi = self.host_range(dr.arrays.n_hosts, dr.arrays.mode)
         mx = eng.shard_begin(dr, lo, hi, self.world)
         send = torch.empty(max(mx, 1), dtype=torch.uint8, device=eng.device)
         recv = torch.empty(max(mx, 1) * self.world, dtype=torch.uint8, device=eng.device)
@@ -82,7 +101,7 @@ def place_lockstep(engines, r):
     import torch
     world = len(engines)
     drs = [DeviceRound(r, e.device) for e in engines]
-    mx = [e.shard_begin(dr, *shard(r.n_hosts, world, k), world)
+    mx = [e.shard_begin(dr, *shard_range(r.n_hosts, world, k, r.mode), world)
           for k, (e, dr) in enumerate(zip(engines, drs))]
     sends = [torch.empty(max(m, 1), dtype=torch.uint8, device=e.device) for m, e in zip(mx, engines)]
     recvs = [torch.empty(max(m, 1) * world, dtype=torch.uint8, device=e.device)

@@ -137,6 +137,7 @@ def torch_u8(vals):
 class _FakeRound:
     class arrays:
         n_hosts = 1001
+        mode = 1      # PVT_CA_BF: an even split
 
 
 def _shard_worker(rank, world, port, out_q):
@@ -173,3 +174,17 @@ def test_host_sharded_exchange_two_ranks():
     assert got[0][0] == (0, 501) and got[1][0] == (501, 1001)
     for r in range(2):
         assert got[r][1] == [20, 64, 12] and got[r][2] == 3
+
+
+def test_opportunistic_shard_ranges_are_whole_super_chunks():
+    """Opportunistic host shards: whole 16384-host super-chunks, contiguous, covering [0, H);
+    ranks past the last super-chunk get an empty range."""
+    from pivot_place import _abi
+    from pivot_place.sharded import OPP_SUPER_CHUNK, shard_range
+    for H, world in ((1_000_000, 8), (5000, 3), (200_000, 8), (40000, 2)):
+        rs = [shard_range(H, world, k, _abi.PVT_OPP) for k in range(world)]
+        assert rs[0][0] == 0 and rs[-1][1] == H
+        for (a, b), (c, d) in zip(rs, rs[1:]):
+            assert b == c
+        for a, b in rs:
+            assert a <= b and (a % OPP_SUPER_CHUNK == 0 or a == H) and (b == H or b % OPP_SUPER_CHUNK == 0)

@@ -34,6 +34,8 @@ def _assert_same(res, ref):
     np.testing.assert_array_equal(res.order, ref.order)
     bad = np.nonzero((res.avail != ref.avail).any(axis=0))[0]
     assert bad.size == 0, "availability differs on hosts %s" % bad[:10]
+    if ref.mt_state is not None:
+        np.testing.assert_array_equal(res.mt_state, ref.mt_state)
 
 
 def _lockstep(engines, world, r):
@@ -74,21 +76,31 @@ def test_sharded_matches_reference_golden(engines, name, idx):
     case = golden_io.load(name)
     run = case["runs"][idx]
     r = golden_io.run_arrays(case, run)
-    if r.mode == _abi.PVT_OPP:
-        pytest.skip("opportunistic rounds are scenario-sharded, not host-sharded")
-    placement, order, avail = golden_io.expected(case, run)[:3]
+    placement, order, avail, mt = golden_io.expected(case, run)
     res = _lockstep(engines, 3, r)
     np.testing.assert_array_equal(res.placement, placement)
     np.testing.assert_array_equal(res.order, order)
     np.testing.assert_array_equal(res.avail, avail)
+    if mt is not None:
+        np.testing.assert_array_equal(res.mt_state, mt)
 
 
-def test_opportunistic_is_not_host_sharded(engines):
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70000, 600, 2), (200_000, 700, 4), (5, 40, 3)])
+def test_opportunistic_host_sharded(engines, world, H, T, seed):
+    """Per-rank feasible counts of whole 16384-host super-chunks, all-gathered per window;
+    every rank draws and selects on the full tables: placements, availability and the MT19937
+    state equal the oracle's on every rank (ranks past the last super-chunk count nothing)."""
+    r = synthetic.make_round(_abi.PVT_OPP, H, T, seed=seed)
+    _assert_same(_lockstep(engines, world, r), oracle.place(r))
+
+
+def test_opportunistic_shard_must_be_super_chunk_aligned(engines):
     from pivot_place.engine import DeviceRound
-    r = synthetic.make_round(_abi.PVT_OPP, 100, 10, seed=1)
+    r = synthetic.make_round(_abi.PVT_OPP, 40000, 10, seed=1)
     dr = DeviceRound(r, engines[0].device)
-    with pytest.raises(RuntimeError, match="EUNSUPPORTED"):
-        engines[0].shard_begin(dr, 0, 50, 2)
+    with pytest.raises(RuntimeError, match="EINVAL"):
+        engines[0].shard_begin(dr, 0, 20000, 2)
 
 
 def _free_port():
@@ -115,7 +127,7 @@ def _rank_main(rank, world, port, mode, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_VBP_FF])
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_VBP_FF, _abi.PVT_OPP])
 def test_two_process_group_on_one_gpu(mode):
     import torch.multiprocessing as mp
     ref = oracle.place(synthetic.make_round(mode, 20000, 400, seed=5))
