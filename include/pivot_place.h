@@ -44,6 +44,9 @@ extern "C" {
 #define PVT_EHIP         -3   /* a HIP runtime call failed (see pvt_last_error)   */
 #define PVT_ENOMEM       -4   /* scratch allocation failed                        */
 #define PVT_EUNSUPPORTED -5   /* configuration the engine does not implement      */
+#define PVT_ESTALE       -6   /* pvt_shard_commit: the exchanged window was scored while the
+                                 previous walk ran, and that walk stopped early -- call
+                                 pvt_shard_score again (every rank gets it together)     */
 
 /* Policies (kernel modes). */
 enum pvt_mode {
@@ -165,12 +168,23 @@ int  pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills);
  *   loop:
  *     pvt_shard_score(ctx, send, &nt, &bytes)              nt == 0: the round is done
  *     all-gather `bytes` from every rank into recv, rank order, contiguous (recv[k*bytes..])
- *     pvt_shard_commit(ctx, recv)
+ *     pvt_shard_commit(ctx, recv)                          PVT_ESTALE: score again
+ *
+ * pvt_shard_commit launches the window's commit walk and returns without waiting for it
+ * (pvt_set_pipeline on, the default): the next pvt_shard_score scores the following window on
+ * a side stream while the walk runs and returns its package (complete on return), so the
+ * caller's exchange -- issued on a stream that does not wait for the context's stream -- also
+ * overlaps the walk. If that walk stops early the speculative package is stale: the next
+ * pvt_shard_commit returns PVT_ESTALE on every rank and the caller scores again. With the
+ * pipeline off every call completes its window before returning.
+ * Opportunistic rounds shard by whole super-chunks of 16384 hosts: rank r of world W must take
+ * hosts [r * P * 16384, (r + 1) * P * 16384) clamped to H, P = ceil(ceil(H / 16384) / W); the
+ * packages carry its per-task feasibility bitmaps and super-chunk counts and every rank runs the
+ * same draw / selection walk (windows of 256 tasks, not pipelined).
  *
  * `r` and its arrays must stay valid until the round is done. nt and bytes are the same on
  * every rank (window sizes depend only on walk results, which every rank shares).
- * Opportunistic rounds return PVT_EUNSUPPORTED (their draw needs a per-task exchange; shard
- * them by scenario instead). Replaces the per-task scan of scheduler/cost_aware.py:88-92,
+ * Replaces the per-task scan of scheduler/cost_aware.py:88-92,
  * :118-122 and scheduler/vbp.py:19-22, :43-47 over a cluster too large for one GPU's pass.
  */
 #define PVT_SHARD_MAX_WORLD 64

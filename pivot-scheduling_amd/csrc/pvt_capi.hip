@@ -74,6 +74,11 @@ struct RoundState {
   // [opp_sq_lo, opp_sq_hi); packages hold opp_Psq super-chunks per task (the largest share)
   bool opp = false;
   int opp_W = 0, opp_nq = 0, opp_nsq = 0, opp_Psq = 0, opp_sq_lo = 0, opp_sq_hi = 0;
+  // host-sharded list rounds, pipelined: the walk in flight (window if_t0 + [0, if_nt) on list
+  // buffer if_lb) and the scored window awaiting its exchange (pt0, nt, plb; spec = scored
+  // while a walk was in flight, so it inherits that walk's hosts)
+  bool inflight = false, spec = false;
+  int if_t0 = 0, if_nt = 0, if_lb = 0, pt0 = 0, plb = 0;
   std::vector<int> egs, ega;      // cost_aware best-fit epochs: group starts (+ T) and anchors
   std::vector<int> ecomp;         // zone -> its component of zones joined by zero egress cost
   bool in_epoch = false;          // lists scored for an epoch (place_epochs)
@@ -825,19 +830,6 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
   return PVT_OK;
 }
 
-// Sequential windows (sharded rounds): lists, [exchange], walk, repeat.
-static int window_commit(pvt_ctx* ctx) {
-  RoundState& R = ctx->rs;
-  int rc, adv = 0;
-  const int nt = R.nt, t0 = R.t0;
-  if ((rc = walk_launch(ctx, t0, nt, 0, 0))) return rc;
-  R.nt = 0;
-  if ((rc = walk_status(ctx, t0, nt, false, &adv))) return rc;
-  adapt_window(ctx, adv, nt);
-  R.t0 += adv;
-  return PVT_OK;
-}
-
 // pvt_place for the list policies. While window k is walked on the caller's stream, the side
 // stream scores window k+1 on the capacities as they stand (the walk of k-1 is complete; the
 // walk of k is in flight): an event recorded just before walk k releases it. The side stream
@@ -1365,6 +1357,7 @@ extern "C" int pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo
   if (host_lo < 0 || host_hi < host_lo || host_hi > r->n_hosts)
     return fail(ctx, PVT_EINVAL, "bad host range [%d, %d) of %d", host_lo, host_hi, r->n_hosts);
   ctx->rs.opp = false;
+  ctx->rs.inflight = ctx->rs.spec = false;
   if (r->mode == PVT_OPP) {
     int rc = check_round(ctx, r);
     if (rc) return rc;
@@ -1379,31 +1372,70 @@ extern "C" int pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo
   return PVT_OK;
 }
 
+// The walk in flight, waited for: the round continues where it stopped.
+static int shard_finish_walk(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  if (!R.inflight) return PVT_OK;
+  R.inflight = false;
+  int adv = 0, rc;
+  if ((rc = walk_status(ctx, R.if_t0, R.if_nt, R.spec, &adv))) return rc;
+  adapt_window(ctx, adv, R.if_nt);
+  R.t0 = R.if_t0 + adv;
+  return PVT_OK;
+}
+
+// Pipelined (pvt_set_pipeline, default on): while walk k runs, window k+1 of the same group is
+// scored on the side stream -- on the state walk k-1 left -- and its package returned for the
+// exchange, which the caller overlaps with walk k; pvt_shard_commit then waits for walk k and
+// returns PVT_ESTALE if it stopped early (every rank sees the same walk, so all ranks agree).
 extern "C" int pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out,
                                int64_t* package_bytes) {
   if (!ctx || !package || !n_tasks_out || !package_bytes) return PVT_EINVAL;
   *n_tasks_out = 0;
   *package_bytes = 0;
-  if (!ctx->rs.active || ctx->rs.world < 1) return fail(ctx, PVT_EINVAL, "no sharded round in progress");
-  if (ctx->rs.nt != 0) return fail(ctx, PVT_EINVAL, "pvt_shard_score called twice without pvt_shard_commit");
-  if (ctx->rs.opp) return opp_shard_score(ctx, package, n_tasks_out, package_bytes);
-  int nt = 0, rc;
-  if ((rc = round_next_window(ctx, &nt))) return rc;
-  if (nt == 0) {
-    ctx->rs.active = false;
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    return PVT_OK;
+  RoundState& R = ctx->rs;
+  if (!R.active || R.world < 1) return fail(ctx, PVT_EINVAL, "no sharded round in progress");
+  if (R.nt != 0) return fail(ctx, PVT_EINVAL, "pvt_shard_score called twice without pvt_shard_commit");
+  if (R.opp) return opp_shard_score(ctx, package, n_tasks_out, package_bytes);
+  const int PK = shard_depth(R.world);
+  int nt = 0, rc, lb = 0;
+  hipStream_t st = ctx->stream;
+  R.spec = false;
+  if (R.inflight) {
+    const int t1 = R.if_t0 + R.if_nt, ge = group_end(R, R.if_t0);
+    if (ctx->pipeline && t1 < ge) {           // speculative: the window after the walk in flight
+      nt = std::min(R.W, ge - t1);
+      lb = 1 - R.if_lb;
+      st = ctx->side;
+      HIPCHK(hipStreamWaitEvent(st, ctx->ev_walk, 0));
+      if ((rc = window_lists(ctx, t1, nt, lb, st))) return rc;
+      R.spec = true;
+      R.pt0 = t1;
+    } else if ((rc = shard_finish_walk(ctx))) {
+      return rc;
+    }
   }
-  if ((rc = window_lists(ctx, ctx->rs.t0, nt, 0, ctx->stream))) return rc;
-  const int PK = shard_depth(ctx->rs.world);
+  if (!R.spec) {
+    if ((rc = round_next_window(ctx, &nt))) return rc;
+    if (nt == 0) {
+      R.active = false;
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      return PVT_OK;
+    }
+    if ((rc = window_lists(ctx, R.t0, nt, lb, st))) return rc;
+    R.pt0 = R.t0;
+  }
   Lists L;
-  lists_from(ctx, L);
-  PackArgs pa{L, nt, PK, ctx->rs.ordered ? 1 : 0, reinterpret_cast<SegEntry*>(package)};
+  lists_from(ctx, L, lb);
+  PackArgs pa{L, nt, PK, R.ordered ? 1 : 0, reinterpret_cast<SegEntry*>(package)};
   {
-    Scope sc(ctx, PVT_K_MERGE, 0, 0);
-    launch_pack(pa, ctx->stream);
+    Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
+    launch_pack(pa, st);
   }
   HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));           // the package is complete when this returns
+  R.nt = nt;
+  R.plb = lb;
   *n_tasks_out = nt;
   *package_bytes = (int64_t)sizeof(SegEntry) * (PK + 1) * nt;
   return PVT_OK;
@@ -1414,16 +1446,32 @@ extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
   RoundState& R = ctx->rs;
   if (!R.active || R.nt == 0) return fail(ctx, PVT_EINVAL, "pvt_shard_commit without a scored window");
   if (R.opp) return opp_shard_commit(ctx, packages);
-  const int PK = shard_depth(R.world);
+  int rc, n_prev = 0;
+  if (R.spec) {                               // wait for the walk the package speculated past
+    if ((rc = shard_finish_walk(ctx))) return rc;
+    if (R.t0 != R.pt0) {                      // it stopped early: the package is stale
+      R.nt = 0;
+      R.spec = false;
+      return PVT_ESTALE;
+    }
+    n_prev = ctx->next_host[1];               // its hosts: stale in these lists, so touched
+  }
+  const int PK = shard_depth(R.world), t0 = R.pt0, nt = R.nt, lb = R.plb;
   Lists L;
-  lists_from(ctx, L);
+  lists_from(ctx, L, lb);
   MergeArgs ma{reinterpret_cast<const SegEntry*>(packages), nullptr, R.r.avail, R.r.zone,
-               P<double>(ctx->dem_ord) + (size_t)R.t0 * 4, P<int32_t>(ctx->anc_ord) + R.t0,
-               R.ord + R.t0, R.H, R.nt, R.world, PK, L};
+               P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
+               R.ord + t0, R.H, nt, R.world, PK, L};
   {
     Scope sc(ctx, PVT_K_MERGE, 0, 0);
     launch_merge(ma, ctx->stream);
   }
   HIPCHK(hipGetLastError());
-  return window_commit(ctx);
+  HIPCHK(hipEventRecord(ctx->ev_walk, ctx->stream));   // releases the next speculative score
+  if ((rc = walk_launch(ctx, t0, nt, lb, n_prev))) return rc;
+  R.inflight = true;
+  R.if_t0 = t0; R.if_nt = nt; R.if_lb = lb;
+  R.nt = 0;
+  if (!ctx->pipeline) return shard_finish_walk(ctx);
+  return PVT_OK;
 }

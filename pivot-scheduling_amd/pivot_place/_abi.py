@@ -18,8 +18,9 @@ PVT_ENODEV = -2
 PVT_EHIP = -3
 PVT_ENOMEM = -4
 PVT_EUNSUPPORTED = -5
+PVT_ESTALE = -6
 ERRORS = {PVT_EINVAL: "EINVAL", PVT_ENODEV: "ENODEV", PVT_EHIP: "EHIP", PVT_ENOMEM: "ENOMEM",
-          PVT_EUNSUPPORTED: "EUNSUPPORTED"}
+          PVT_EUNSUPPORTED: "EUNSUPPORTED", PVT_ESTALE: "ESTALE"}
 
 PVT_CA_FF, PVT_CA_BF, PVT_OPP, PVT_VBP_FF, PVT_VBP_BF = range(5)
 MODE_NAMES = {PVT_CA_FF: "cost_aware_ff", PVT_CA_BF: "cost_aware_bf", PVT_OPP: "opportunistic",

@@ -352,8 +352,14 @@ class PlacementEngine:
         return nt.value, nb.value
 
     def shard_commit(self, packages):
-        """Merge every rank's package (rank order, contiguous) and run the commit walk."""
-        self._check(self.lib.pvt_shard_commit(self.ctx, ctypes.c_void_p(packages.data_ptr())))
+        """Merge every rank's package (rank order, contiguous) and launch the commit walk.
+        Returns False when the package was scored past a walk that stopped early (PVT_ESTALE:
+        every rank gets it together; score again), True otherwise."""
+        rc = self.lib.pvt_shard_commit(self.ctx, ctypes.c_void_p(packages.data_ptr()))
+        if rc == _abi.PVT_ESTALE:
+            return False
+        self._check(rc)
+        return True
 
     def set_window(self, tasks):
         self._check(self.lib.pvt_set_window(self.ctx, int(tasks)))

@@ -70,24 +70,37 @@ class HostShardedPlacer:
         return shard_range(n_hosts, self.world, self.rank, mode)
 
     def run(self, dr: DeviceRound):
-        """Place a resident round in place (``dr.placement``/``order``/``avail`` as pvt_place)."""
+        """Place a resident round in place (``dr.placement``/``order``/``avail`` as pvt_place).
+
+        The exchange runs on its own stream, so it overlaps the commit walk the engine left in
+        flight (pvt_shard_commit returns at once; the next pvt_shard_score scores the following
+        window beside it); the context's stream waits for the exchange before the merge."""
         import torch
         eng = self.engine
         lo, hi = self.host_range(dr.arrays.n_hosts, dr.arrays.mode)
         mx = eng.shard_begin(dr, lo, hi, self.world)
         send = torch.empty(max(mx, 1), dtype=torch.uint8, device=eng.device)
         recv = torch.empty(max(mx, 1) * self.world, dtype=torch.uint8, device=eng.device)
-        self.windows = 0
+        gpu = torch.device(eng.device).type == "cuda"
+        cur = torch.cuda.current_stream(eng.device) if gpu else None
+        side = torch.cuda.Stream(eng.device) if gpu else None
+        self.windows = self.stale = 0
         while True:
             nt, nbytes = eng.shard_score(send)
             if nt == 0:
                 return
             if self.exchange is None:          # a single shard: its package is the whole set
-                eng.shard_commit(send)
-            else:
+                ok = eng.shard_commit(send)
+            elif gpu:
+                with torch.cuda.stream(side):
+                    self.exchange(send, nbytes, recv)
+                cur.wait_stream(side)
+                ok = eng.shard_commit(recv)
+            else:                              # host-side stand-ins (tests)
                 self.exchange(send, nbytes, recv)
-                eng.shard_commit(recv)
+                ok = eng.shard_commit(recv)
             self.windows += 1
+            self.stale += 0 if ok else 1
 
     def place(self, r):
         dr = DeviceRound(r, self.engine.device)
@@ -116,6 +129,7 @@ def place_lockstep(engines, r):
         for recv in recvs:
             for k, s in enumerate(sends):
                 recv[k * nb:(k + 1) * nb].copy_(s[:nb])
-        for e, recv in zip(engines, recvs):
-            e.shard_commit(recv)
+        ok = [e.shard_commit(recv) for e, recv in zip(engines, recvs)]
+        if len(set(ok)) != 1:
+            raise RuntimeError("shards disagree on a stale window: %s" % (ok,))
     return [dr.result() for dr in drs]

@@ -127,6 +127,7 @@ class _ProtocolEngine:
             assert recv[k * nb:(k + 1) * nb].tolist() == [k, self.w] * (nb // 2)
         self.seen.append(nb)
         self.w += 1
+        return True
 
 
 def torch_u8(vals):

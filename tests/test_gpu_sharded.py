@@ -54,9 +54,11 @@ def test_sharded_matches_oracle(engines, mode, world, H, T, seed):
     _assert_same(_lockstep(engines, world, r), oracle.place(r))
 
 
+@pytest.mark.parametrize("pipeline", [True, False])
 @pytest.mark.parametrize("mode", SHARDED_MODES)
-def test_sharded_crowded_and_refills(engines, mode):
-    """Nearly full identical hosts + tiny windows: exhausted packages, bounds, refills."""
+def test_sharded_crowded_and_refills(engines, mode, pipeline):
+    """Nearly full identical hosts + tiny windows: exhausted packages, bounds, refills; with the
+    pipeline on, windows scored past a walk that then stops early come back PVT_ESTALE."""
     r = synthetic.make_round(mode, 3000, 1500, seed=11)
     r.avail[0, :] = 4.0
     r.avail[1, :] = 40000.0
@@ -65,10 +67,31 @@ def test_sharded_crowded_and_refills(engines, mode):
     try:
         for e in engines:
             e.set_window(37)
+            e.set_pipeline(pipeline)
         _assert_same(_lockstep(engines, 4, r), ref)
     finally:
         for e in engines:
             e.set_window(0)
+            e.set_pipeline(True)
+
+
+def test_sharded_pipelined_placer_counts_stale_windows(engines):
+    """HostShardedPlacer at world 1 (no exchange): crowded hosts make walks stop early, so some
+    speculative windows are stale and re-scored; the result equals the oracle."""
+    from pivot_place.engine import DeviceRound
+    from pivot_place.sharded import HostShardedPlacer
+    r = synthetic.make_round(_abi.PVT_CA_BF, 3000, 1500, seed=11)
+    r.avail[0, :] = 4.0
+    r.avail[1, :] = 40000.0
+    try:
+        engines[0].set_window(37)
+        placer = HostShardedPlacer(engines[0], 0, 1)
+        dr = DeviceRound(r, engines[0].device)
+        placer.run(dr)
+    finally:
+        engines[0].set_window(0)
+    _assert_same(dr.result(), oracle.place(r))
+    assert placer.stale > 0 and placer.windows > placer.stale
 
 
 @pytest.mark.parametrize("name,idx", [x for x in golden_io.all_runs() if x[0] in ("c1_sim_h100", "c2_h1000", "decay", "saturate")])
