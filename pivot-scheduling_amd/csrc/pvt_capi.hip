@@ -77,8 +77,8 @@ struct RoundState {
   // host-sharded list rounds, pipelined: the walk in flight (window if_t0 + [0, if_nt) on list
   // buffer if_lb) and the scored window awaiting its exchange (pt0, nt, plb; spec = scored
   // while a walk was in flight, so it inherits that walk's hosts)
-  bool inflight = false, spec = false;
-  int if_t0 = 0, if_nt = 0, if_lb = 0, pt0 = 0, plb = 0;
+  bool inflight = false, spec = false, if_inh = false;   // if_inh: the walk in flight
+  int if_t0 = 0, if_nt = 0, if_lb = 0, pt0 = 0, plb = 0;   //   inherited touched hosts
   std::vector<int> egs, ega;      // cost_aware best-fit epochs: group starts (+ T) and anchors
   std::vector<int> ecomp;         // zone -> its component of zones joined by zero egress cost
   bool in_epoch = false;          // lists scored for an epoch (place_epochs)
@@ -1378,7 +1378,7 @@ static int shard_finish_walk(pvt_ctx* ctx) {
   if (!R.inflight) return PVT_OK;
   R.inflight = false;
   int adv = 0, rc;
-  if ((rc = walk_status(ctx, R.if_t0, R.if_nt, R.spec, &adv))) return rc;
+  if ((rc = walk_status(ctx, R.if_t0, R.if_nt, R.if_inh, &adv))) return rc;
   adapt_window(ctx, adv, R.if_nt);
   R.t0 = R.if_t0 + adv;
   return PVT_OK;
@@ -1470,7 +1470,7 @@ extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
   HIPCHK(hipEventRecord(ctx->ev_walk, ctx->stream));   // releases the next speculative score
   if ((rc = walk_launch(ctx, t0, nt, lb, n_prev))) return rc;
   R.inflight = true;
-  R.if_t0 = t0; R.if_nt = nt; R.if_lb = lb;
+  R.if_t0 = t0; R.if_nt = nt; R.if_lb = lb; R.if_inh = R.spec;
   R.nt = 0;
   if (!ctx->pipeline) return shard_finish_walk(ctx);
   return PVT_OK;

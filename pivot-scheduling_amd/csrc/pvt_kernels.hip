@@ -552,6 +552,95 @@ __global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
   }
 }
 
+// Merge of the ranks' packages (host-dimension sharding): one block per task, the same
+// rank-by-counting as merge_small_kernel over world sorted lists of SL entries (world * SL <=
+// LMAX), bounded by the smallest of the packages' explicit bound entries.
+__device__ __forceinline__ int lower_bound_key(const Key* L, int n, const Key& x) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (kless(L[mid], x)) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
+  __shared__ Key lk[LMAX];
+  __shared__ Key out[LMAX];
+  __shared__ Key bound;
+  __shared__ int cnt_sh, tot_sh;
+  const int task = blockIdx.x, tid = threadIdx.x;
+  const int W = A.S, SL = A.SL, n = W * SL;
+  const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
+  if (tid == 0) { bound = inv; cnt_sh = 0; tot_sh = 0; }
+  int valid = 0;
+  for (int j = tid; j < n; j += 256) {
+    const int g = j / SL, e = j - g * SL;
+    const SegEntry se = A.seg[((size_t)g * A.nt + task) * (SL + 1) + e];
+    lk[j] = {se.s, se.tb, se.id};
+    out[j] = inv;
+    valid += se.id != 0x7fffffff;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    Key b = inv;
+    for (int g = 0; g < W; g++) {
+      const SegEntry se = A.seg[((size_t)g * A.nt + task) * (SL + 1) + SL];
+      const Key k = {se.s, se.tb, se.id};
+      if (kless(k, b)) b = k;
+    }
+    bound = b;
+  }
+  if (valid) atomicAdd(&tot_sh, valid);
+  __syncthreads();
+  const Key bnd0 = bound;
+  int c = 0;
+  for (int j = tid; j < n; j += 256) {
+    const Key x = lk[j];
+    if (x.id == 0x7fffffff || !kless(x, bnd0)) continue;
+    const int g = j / SL;
+    int pos = j - g * SL;
+    for (int h = 0; h < W; h++)
+      if (h != g) pos += lower_bound_key(lk + h * SL, SL, x);
+    out[pos] = x;
+    c++;
+  }
+  if (c) atomicAdd(&cnt_sh, c);
+  __syncthreads();
+  const int cnt = cnt_sh;
+  const bool complete = (bnd0.id == 0x7fffffff) && tot_sh <= LMAX;
+  Key bnd = bnd0;
+  if (cnt == LMAX && kless(out[LMAX - 1], bnd)) bnd = out[LMAX - 1];
+  const int nw = max(cnt, KL);
+  for (int j = tid; j < nw; j += 256) {
+    ListEntry e;
+    const bool ok = j < cnt;
+    const Key k = ok ? out[j] : inv;
+    const int h = ok ? k.id : 0;
+    e.s = k.s; e.tb = k.tb; e.id = k.id; e.pad = 0; e.pad2 = 0.0;
+    e.zone = ok ? A.zone[h] : 0;
+    e.a[0] = ok ? A.avail[h] : 0.0;
+    e.a[1] = ok ? A.avail[(size_t)A.H + h] : 0.0;
+    e.a[2] = ok ? A.avail[2 * (size_t)A.H + h] : 0.0;
+    e.a[3] = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
+    A.L.e[(size_t)task * LMAX + j] = e;
+    A.L.ids[(size_t)task * LMAX + j] = ok ? k.id : 0x7fffffff;
+  }
+  if (tid < 4) {
+    double* tr = reinterpret_cast<double*>(&A.L.t[task]);
+    tr[tid] = A.dem[(size_t)task * 4 + tid];
+  }
+  if (tid == 0) {
+    TaskRec& r = A.L.t[task];
+    r.cnt = cnt;
+    r.complete = complete;
+    r.anc = A.anc[task];
+    r.ord = A.ord[task];
+    r.bs = bnd.s; r.btb = bnd.tb; r.bid = bnd.id;
+  }
+}
+
 void launch_merge(const MergeArgs& a, hipStream_t st) {
   static const int small = [] {
     const char* e = getenv("PVT_MERGE_SMALL");   // A/B experiments: 0 = bitonic merge always
@@ -559,6 +648,8 @@ void launch_merge(const MergeArgs& a, hipStream_t st) {
   }();
   if (small && a.seg_feas != nullptr && a.SL == KL && a.S <= MERGE_SMALL_S)
     hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+  else if (small && a.seg_feas == nullptr && (size_t)a.S * a.SL <= LMAX)
+    hipLaunchKernelGGL(merge_pkg_kernel, dim3(a.nt), dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
 }

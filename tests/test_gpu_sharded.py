@@ -76,20 +76,17 @@ def test_sharded_crowded_and_refills(engines, mode, pipeline):
 
 
 def test_sharded_pipelined_placer_counts_stale_windows(engines):
-    """HostShardedPlacer at world 1 (no exchange): crowded hosts make walks stop early, so some
-    speculative windows are stale and re-scored; the result equals the oracle."""
+    """HostShardedPlacer at world 1 (no exchange): every host fits exactly one task, so a
+    window's late tasks find every listed host taken and the walk stops early; the window
+    scored past it is stale and re-scored. The result equals the oracle."""
     from pivot_place.engine import DeviceRound
     from pivot_place.sharded import HostShardedPlacer
-    r = synthetic.make_round(_abi.PVT_CA_BF, 3000, 1500, seed=11)
-    r.avail[0, :] = 4.0
-    r.avail[1, :] = 40000.0
-    try:
-        engines[0].set_window(37)
-        placer = HostShardedPlacer(engines[0], 0, 1)
-        dr = DeviceRound(r, engines[0].device)
-        placer.run(dr)
-    finally:
-        engines[0].set_window(0)
+    r = synthetic.make_round(_abi.PVT_VBP_BF, 3000, 2800, seed=11)
+    r.avail[0, :] = 1.5
+    r.dem[0, :] = 1.0
+    placer = HostShardedPlacer(engines[0], 0, 1)
+    dr = DeviceRound(r, engines[0].device)
+    placer.run(dr)
     _assert_same(dr.result(), oracle.place(r))
     assert placer.stale > 0 and placer.windows > placer.stale
 
