@@ -132,6 +132,25 @@ __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
   if (tid == 0 && stop) __hip_atomic_store(&A.bad[j], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Finality of the log entries: per segment, an entry is its host's final state unless a later
+// walked task of the same segment committed to the same host (sup = 1). One block per segment,
+// its walked hosts staged in LDS (a segment never exceeds CHAIN_MAX tasks).
+__global__ __launch_bounds__(256) void epoch_final_kernel(EpochArgs A) {
+  __shared__ int32_t ids[CHAIN_MAX];
+  const int j = blockIdx.x, tid = threadIdx.x;
+  const int s0 = A.seg_off[j], n = seg_adv(A, j);
+  for (int k = tid; k < n; k += 256) ids[k] = A.wlog[s0 + k].id;
+  __syncthreads();
+  for (int k = tid; k < n; k += 256) {
+    const int32_t h = ids[k];
+    int sup = 0;
+    if (h >= 0)
+      for (int m = k + 1; m < n; m++)
+        if (ids[m] == h) { sup = 1; break; }
+    A.wlog[s0 + k].sup = sup;
+  }
+}
+
 // One block per chain: its accepted segments in order, each segment's final entries written to
 // global availability (a later segment of the chain overwrites an earlier one's entry for the
 // same host; different chains' accepted segments touch disjoint hosts).
@@ -151,6 +170,7 @@ __global__ __launch_bounds__(256) void epoch_apply_kernel(EpochArgs A, int n_acc
 }
 
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(256), 0, st, a);
   const int tiles = (CHAIN_MAX + 255) / 256;   // a segment never exceeds its chain's cap
   hipLaunchKernelGGL(epoch_validate_kernel, dim3(tiles, a.nseg, VAL_SPLIT), dim3(256), 0, st, a);
 }

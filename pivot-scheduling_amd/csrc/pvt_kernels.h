@@ -176,7 +176,7 @@ struct EpochArgs {
   const int32_t* seg_chain;   // [nseg] chain of each segment
   const int32_t* seg_cstart;  // [nseg] index of the segment's first task in its chain's walk
   const int32_t* status;  // [nchains][2]: tasks the chain's walk got through (-1: timeout)
-  const WinRec* wlog;     // [nt]
+  WinRec* wlog;           // [nt] (sup set by the finality pass)
   double* avail;          // apply: accepted segments' final entries written here
   int H, Z, nt, nseg;
   int32_t* bad;           // [nseg] out: 1 = segment j is not exact (zeroed by the caller)

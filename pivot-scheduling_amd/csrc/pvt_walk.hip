@@ -99,8 +99,6 @@ struct WalkLDS {
   int32_t lhp[LIVE_MAX];                  // hash position of the live host
   uint32_t ltb[LIVE_MAX];
   int32_t lown[LIVE_MAX];                 // 1: committed to by this walk (in own_ids)
-  int32_t lpw[LIVE_MAX];                  // epoch walks: window task of its last commit,
-  int32_t lpi[LIVE_MAX];                  //   and that task's index in this walk
   int32_t cseg[MAX_CHAIN_SEGS + 1];       // epoch walks: segment starts in this walk (+ nt)
   int32_t cwin[MAX_CHAIN_SEGS + 1];       //   and their first tasks' window indices
   double csum[ZMAX * ZMAX];
@@ -355,6 +353,23 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k
                    MODE == VBP_BF ? S.ltb[qq] : 0u, S.lid[qq], b1 < tk1[LOOK - 1] ? b1 : tk1[LOOK - 1],
                    k1, k2);
       uint64_t pm = __ballot(fit && key_lt(k1, k2, b1, b2) && key_lt(k1, k2, tk1[LOOK - 1], tk2[LOOK - 1]));
+      // Many candidates (a zero-cost component's touched hosts all score 0): take the chunk's
+      // LOOK smallest keys by wave-wide minima (DPP) instead of inserting them one by one.
+      if (__popcll(pm) > LOOK + 1) {
+        bool cand = (pm >> lane) & 1ull;
+        uint64_t sel = 0;
+#pragma unroll
+        for (int r = 0; r < LOOK; r++) {
+          const uint64_t m1 = wave_min_u64(cand ? k1 : ~0ull);
+          const uint64_t m2 = wave_min_u64((cand && k1 == m1) ? k2 : ~0ull);
+          const uint64_t lm = __ballot(cand && k1 == m1 && k2 == m2);
+          if (lm == 0) break;
+          const int L = __builtin_ctzll(lm);
+          sel |= 1ull << L;
+          cand = cand && lane != L;
+        }
+        pm = sel;
+      }
       while (pm) {
         const int L = __builtin_ctzll(pm);
         pm &= pm - 1;
@@ -544,8 +559,9 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
   if (lane == 0) { vstore(&S.nl_pub, nl); vstore(&S.committed, 0); }
   int n_own = 0;
   int status = A.nt;
-  int sstart = 0, sk = 1, wbase = 0;        // epoch chains: the current segment's start in
-  if (A.wlog) wbase = S.cwin[0];            //   this walk and in the window
+  // epoch chains: the current segment's start in this walk and in the window, the next start
+  int sstart = 0, sk = 1, wbase = 0, snext = A.nt;
+  if (A.wlog) { wbase = S.cwin[0]; snext = S.cseg[1]; }
   Patched X[NP];
 #pragma unroll
   for (int r = 0; r < NP; r++) {
@@ -685,8 +701,9 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     }
     if (refill) { status = i; break; }
     release_slot(S, i + 1);                   // the ring slot is no longer read
-    if (A.wlog) {                             // entering the chain's next segment
+    if (i >= snext) {                         // entering the chain's next segment
       while (i >= S.cseg[sk]) { sstart = S.cseg[sk]; wbase = S.cwin[sk]; sk++; }
+      snext = S.cseg[sk];
     }
     if (none) {                               // nothing committed: the window slides
       if (lane == 0) {
@@ -764,13 +781,9 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
     if (A.wlog) {                             // epoch walk: logged, applied once validated
       const int w = wbase + i - sstart;
       if (lane < 4) A.wlog[w].a[lane] = nr;
-      if (lane == 0) {
+      if (lane == 0) {                        // (sup: set by epoch_final_kernel)
         A.wlog[w].s = __longlong_as_double((long long)wk);
         A.wlog[w].id = W.id;
-        A.wlog[w].sup = 0;
-        // this walk's previous commit to the host, if in the same segment, is not final
-        if (W.q >= 0 && S.lpi[W.q] >= sstart) A.wlog[S.lpw[W.q]].sup = 1;
-        if (q_after >= 0) { S.lpw[q_after] = w; S.lpi[q_after] = i; }
       }
     } else {
       if (!w_own) {                           // first commit of this walk to the host
