@@ -104,6 +104,7 @@ struct WalkLDS {
   double csum[ZMAX * ZMAX];
   double bsum[ZMAX * ZMAX];
   int32_t flag[RING];
+  int32_t flagB[RING];                    // best-fit: the touched-host part of slot's task
   int32_t done;
   int32_t stop;
   int32_t nl_init;
@@ -226,8 +227,9 @@ __device__ __forceinline__ bool key_lt(uint64_t a1, uint64_t a2, uint64_t b1, ui
 
 // Task i, after the walk has committed every task <= i - LOOK: the LOOK first usable entries of
 // its list (ring, then the deep list in HBM) and, for best-fit, the LOOK best live touched hosts
-// that could still win; written to R.res.
-template <int MODE>
+// that could still win; written to R.res. PART: 0 both, 1 the list entries only, 2 the touched
+// hosts only (best-fit tasks are scouted by two waves at once, one per part).
+template <int MODE, int PART>
 __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k, int32_t rv,
                       const double* rtrow) {
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
@@ -238,11 +240,11 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k
   const int cnt = __builtin_amdgcn_readlane(rv, 8);
   const bool comp = __builtin_amdgcn_readlane(rv, 9) != 0;
   const int anc = __builtin_amdgcn_readlane(rv, 10);
-  const int npos = __builtin_amdgcn_readlane(R.rec[lane & 31], 17);   // own writes, in order
-
   // usable ring entries (lane j: entry j)
   int nU = 0;
   uint64_t u1 = ~0ull, u2 = ~0ull;          // key of the last usable entry kept (best-fit)
+  if (PART != 2) {
+  const int npos = __builtin_amdgcn_readlane(R.rec[lane & 31], 17);   // own writes, in order
   {
     const bool valid = lane < k;
     const int32_t id = R.id[lane];
@@ -322,13 +324,15 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k
     }
     nU = min(nU + __popcll(m), LOOK);
   }
+  }   // PART != 2
 
   // best-fit: the LOOK best live touched hosts that rank before the bound any winner respects:
-  // the LOOK-th usable entry, or with fewer the list bound (incomplete list) or nothing
+  // the LOOK-th usable entry, or with fewer the list bound (incomplete list) or nothing (the
+  // touched-only part does not know the entries: the list bound, or nothing)
   int nT = 0;
-  if (BEST) {
+  if (BEST && PART != 1) {
     uint64_t b1 = u1, b2 = u2;
-    if (nU < LOOK) {
+    if (PART == 2 || nU < LOOK) {
       if (comp) {
         b1 = ~0ull; b2 = ~0ull;
       } else {   // every untouched host outside the list ranks at or after the bound (bid + 1)
@@ -401,7 +405,10 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k
               S.la[3][myq]);
     }
   }
-  if (lane == 0) { R.res[R_NU] = nU; R.res[R_NT] = nT; }
+  if (lane == 0) {
+    if (PART != 2) R.res[R_NU] = nU;
+    if (PART != 1) R.res[R_NT] = nT;
+  }
 }
 
 // A scout fills ring slot i % RING with task i's list head, skipping entries that can no longer
@@ -409,12 +416,63 @@ __device__ void scout(const CommitArgs& A, WalkLDS& S, RingSlot& R, int w, int k
 // first-fit drops dead ones. Touched-ness only grows, so an entry skipped here is unusable later
 // too. The ring holds the first 64 kept entries and the list position after the last of them.
 // Then it waits for the walk to reach task i - LOOK and scouts task i.
+//
+// cost_aware best-fit tasks are scouted by two waves at once (the walker waits for both):
+// split_a() waves load the ring and check its entries (part 1), the other PRODUCERS - split_a()
+// scan the live touched hosts (part 2, produce_touched). Its many zero-score touched hosts make
+// the live scan long; vbp best-fit rarely has live touched hosts, so there the fewer ring
+// loaders in flight cost more than the split saves (walk 13.0 -> 19.7 ms;
+// profiles/r02f/g11_bench_vbp_bf.log) and one wave does both parts.
+#ifndef PVT_SPLIT_CA
+#define PVT_SPLIT_CA 4
+#endif
+#ifndef PVT_SPLIT_VBP
+#define PVT_SPLIT_VBP 0
+#endif
+template <int MODE>
+__device__ constexpr int split_a() {
+  return MODE == CA_BF ? PVT_SPLIT_CA : MODE == VBP_BF ? PVT_SPLIT_VBP : 0;
+}
+static_assert(PVT_SPLIT_CA >= 0 && PVT_SPLIT_CA < PRODUCERS, "PVT_SPLIT_CA");
+static_assert(PVT_SPLIT_VBP >= 0 && PVT_SPLIT_VBP < PRODUCERS, "PVT_SPLIT_VBP");
+
+template <int MODE>
+__device__ void produce_touched(const CommitArgs& A, WalkLDS& S, int pb) {
+  const int lane = lane_id();
+  for (int i = pb; i < A.nt; i += PRODUCERS - split_a<MODE>()) {
+    const int w = widx(A, i);
+    const int32_t rv = reinterpret_cast<const int32_t*>(A.L.t + w)[lane & 15];
+    const int grp = (MODE == CA_BF && A.rtb) ? __builtin_amdgcn_readfirstlane(A.grp[w]) : 0;
+    const int slot = i % RING;
+    for (int spin = 0; vload(&S.done) < i - RING + 1; spin++) {
+      if (vload(&S.stop) || spin > SPIN_LIMIT) return;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    for (int spin = 0;; spin++) {
+      const int c = vload(&S.committed);
+      if (c >= 0 && c >= i - LOOK + 1) break;
+      if (vload(&S.stop) || spin > SPIN_LIMIT) return;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    cbarrier();
+    __builtin_amdgcn_s_setprio(2);
+    scout<MODE, 2>(A, S, S.ring[slot], w, 0, rv,
+                   (MODE == CA_BF && A.rtb) ? A.rtb + (size_t)grp * A.H : nullptr);
+    lds_drain();
+    if (lane == 0) publish(&S.flagB[slot], i);
+    __builtin_amdgcn_s_setprio(0);
+  }
+}
+
 template <int MODE>
 __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
   constexpr bool BEST = (MODE == CA_BF || MODE == VBP_BF);
+  constexpr int SA = split_a<MODE>();
+  constexpr int NA = SA ? SA : PRODUCERS;
+  if (SA && pw >= SA) { produce_touched<MODE>(A, S, pw - SA); return; }
   const int lane = lane_id();
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int i = pw; i < A.nt; i += PRODUCERS) {
+  for (int i = pw; i < A.nt; i += NA) {
     const int w = widx(A, i);
     const ListEntry* le = A.L.e + (size_t)w * LMAX;
     const int32_t rv = reinterpret_cast<const int32_t*>(A.L.t + w)[lane & 15];
@@ -486,7 +544,8 @@ __device__ void produce(const CommitArgs& A, WalkLDS& S, int pw) {
     // the scout is on the walk's critical path (the walker needs its result one task from now):
     // it outranks the other scouts' list loading, not the walker
     __builtin_amdgcn_s_setprio(2);
-    scout<MODE>(A, S, R, w, k, rv, (MODE == CA_BF && A.rtb) ? A.rtb + (size_t)grp * A.H : nullptr);
+    scout<MODE, SA ? 1 : 0>(A, S, R, w, k, rv,
+                              (MODE == CA_BF && A.rtb) ? A.rtb + (size_t)grp * A.H : nullptr);
     lds_drain();
     if (lane == 0) publish(&S.flag[slot], i);
     __builtin_amdgcn_s_setprio(0);
@@ -576,7 +635,9 @@ __device__ void walk(const CommitArgs& A, WalkLDS& S) {
 #endif
   for (int i = 0; i < A.nt; i++) {
     const int slot = i % RING;
-    for (int spin = 0; __builtin_amdgcn_readfirstlane(vload(&S.flag[slot])) != i; spin++) {
+    for (int spin = 0; __builtin_amdgcn_readfirstlane(vload(&S.flag[slot])) != i ||
+                       (split_a<MODE>() && __builtin_amdgcn_readfirstlane(vload(&S.flagB[slot])) != i);
+         spin++) {
       if (spin > SPIN_LIMIT) { status = -1; break; }
       __builtin_amdgcn_s_sleep(1);
     }
@@ -837,7 +898,7 @@ __global__ __launch_bounds__(WALK_THREADS) void commit_kernel(CommitArgs A) {
   for (int i = tid; i < WH_SLOTS; i += WALK_THREADS) { S.hk[i].key = H_EMPTY; S.hk[i].val = H_PENDING; }
   if (MODE == CA_BF)
     for (int i = tid; i < A.Z * A.Z; i += WALK_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
-  if (tid < RING) S.flag[tid] = -1;
+  if (tid < RING) { S.flag[tid] = -1; S.flagB[tid] = -1; }
   if (A.cmap) {                               // the chain's segment starts (chain-local), then nt
     const int s0 = A.csoff[blockIdx.x], ns = min(A.csoff[blockIdx.x + 1] - s0, MAX_CHAIN_SEGS);
     for (int k = tid; k <= MAX_CHAIN_SEGS; k += WALK_THREADS) {
