@@ -243,6 +243,36 @@ def roofline(args, ks, mode, B):
     return out
 
 
+# Latency roofline of a sequential walk: each task reads state the previous commit wrote, so a
+# walk can never beat one dependent LDS round trip per task (MI355X_MICROARCH.md, per-instruction
+# constants: ds_read_b32 issue -> use in a dependent chain, one wave, ~50 cycles) at 2.4 GHz.
+LDS_DEP_CYCLES = 50
+SHADER_HZ = 2.4e9
+
+
+def walk_roofline(ks, ep, steps):
+    """The dominant kernel when no candidate lists are scored (cost_aware best-fit epochs whose
+    chains the zero-cost frontier walk proves, pvt_zwalk.hip): the chain walks run side by side,
+    so the round waits for the longest. `achieved` = its tasks per second, `peak` = one task per
+    dependent LDS round trip."""
+    c = ks["commit"]
+    ms = c["ms"] / max(steps, 1)
+    longest = ep.get("longest_chain_tasks", 0)
+    out = {"kernel": "zwalk (zero-cost frontier walk: one wave per epoch chain, window in LDS)",
+           "bound": "latency", "unit": "tasks/s (longest chain)", "traffic": None,
+           "walk_ms_per_step": ms, "longest_chain_tasks": longest,
+           "peak_basis": "one dependent LDS round trip (%d cycles) per task at %.1f GHz"
+                         % (LDS_DEP_CYCLES, SHADER_HZ / 1e9)}
+    if ms <= 0 or longest <= 0:
+        out.update({"achieved": None, "peak": None, "frac": None})
+        return out
+    achieved = longest / (ms * 1e-3)
+    peak = SHADER_HZ / LDS_DEP_CYCLES
+    out.update({"achieved": achieved, "peak": peak, "frac": achieved / peak,
+                "cycles_per_task": SHADER_HZ / achieved})
+    return out
+
+
 # ---------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -348,13 +378,17 @@ def main():
                                 if hosts_sharded else
                                 "scenario-sharded x%d (no data-path collective)" % world),
             },
-            "roofline": roofline(args, ks, mode, B),
+            "roofline": (walk_roofline(ks, ep, args.steps)
+                         if not B and ks["score"]["launches"] == 0 and ks["commit"]["launches"] > 0
+                         else roofline(args, ks, mode, B)),
             "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items()},
             "walk_us_per_task": (ks["commit"]["ms"] * 1e3 / args.steps / max(T * (B or 1), 1)
                                  if not B else None),
             "windows_per_step": stats["windows"], "refills_per_step": stats["refills"],
             "epochs_per_step": ep["epochs"], "segments_per_step": ep["segments"],
             "rejected_segments_per_step": ep["rejected"],
+            "frontier_chains_per_step": ep.get("frontier_chains"),
+            "list_chains_per_step": ep.get("list_chains"),
         }
         ref = None
         if world == 1 and args.cpu_baseline_seconds > 0:

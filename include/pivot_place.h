@@ -153,6 +153,17 @@ int  pvt_set_pipeline(pvt_ctx* ctx, int on);
  */
 int  pvt_set_epochs(pvt_ctx* ctx, int on);
 int  pvt_epoch_stats(pvt_ctx* ctx, int64_t* epochs, int64_t* segments, int64_t* rejected);
+/*
+ * Zero-cost frontier walk (default on; results identical either way): an epoch chain whose
+ * tasks all find a zero-egress-cost host (score exactly 0) among the first 1024 hosts of its
+ * zones is walked as a first fit over those hosts in LDS, with no candidate lists; the walk
+ * proves each winner exact (pvt_zwalk.hip) and leaves any chain it cannot prove to the
+ * list-based walk. pvt_zero_walk_stats: chains of the last pvt_place walked each way, and the
+ * tasks of each epoch's longest chain (summed over its epochs: the walks' critical path).
+ */
+int  pvt_set_zero_walk(pvt_ctx* ctx, int on);
+int  pvt_zero_walk_stats(pvt_ctx* ctx, int64_t* frontier_chains, int64_t* list_chains,
+                         int64_t* longest_chain);
 /* Counters of the last pvt_place call: windows run and refills forced by exhausted lists. */
 int  pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills);
 /*

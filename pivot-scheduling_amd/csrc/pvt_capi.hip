@@ -107,7 +107,11 @@ struct pvt_ctx {
   int resident_max = PVT_RESIDENT_MAX_HOSTS;   // pvt_place: resident kernel up to this many hosts
   int epochs = 1;                 // cost_aware best-fit: group-parallel speculative epochs
   int64_t n_epochs = 0, n_segs = 0, n_rejected = 0;
+  int64_t n_zchains = 0, n_gchains = 0;   // epoch chains walked by the frontier / list walk
+  int64_t n_longest = 0;                  // tasks of the longest epoch chain (sum over epochs)
+  int zwalk = 1;                          // zero-cost frontier walk of epoch chains
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
+  Buf hmin;                       // frontier walk: per-dimension host minima (partials)
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
   std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
   std::vector<uint32_t> rmt_host;
@@ -271,7 +275,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
-                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres};
+                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -335,6 +339,19 @@ extern "C" int pvt_epoch_stats(pvt_ctx* ctx, int64_t* epochs, int64_t* segments,
   if (epochs) *epochs = ctx->n_epochs;
   if (segments) *segments = ctx->n_segs;
   if (rejected) *rejected = ctx->n_rejected;
+  return PVT_OK;
+}
+extern "C" int pvt_set_zero_walk(pvt_ctx* ctx, int on) {
+  if (!ctx) return PVT_EINVAL;
+  ctx->zwalk = on != 0;
+  return PVT_OK;
+}
+extern "C" int pvt_zero_walk_stats(pvt_ctx* ctx, int64_t* frontier_chains, int64_t* list_chains,
+                                   int64_t* longest_chain) {
+  if (!ctx) return PVT_EINVAL;
+  if (frontier_chains) *frontier_chains = ctx->n_zchains;
+  if (list_chains) *list_chains = ctx->n_gchains;
+  if (longest_chain) *longest_chain = ctx->n_longest;
   return PVT_OK;
 }
 extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) {
@@ -990,7 +1007,10 @@ static int place_epochs(pvt_ctx* ctx) {
     const int nseg = (int)E.chain.size(), nch = (int)E.segs.size(), nt = E.off.back();
     ctx->n_epochs++;
     ctx->n_segs += nseg;
-    if ((rc = window_lists(ctx, t0, nt, 0, st))) return rc;
+    // chains the zero-cost frontier walk can prove need no candidate lists (pvt_zwalk.hip);
+    // the lists are scored only for the others
+    const bool zw = ctx->zwalk && nch > 1 && !r->rt_bw && R.Z <= ZMAX;
+    if (!zw && (rc = window_lists(ctx, t0, nt, 0, st))) return rc;
     Lists L;
     lists_from(ctx, L, 0);
     if (nch == 1) {                           // one chain: the plain walk (writes avail)
@@ -1017,12 +1037,38 @@ static int place_epochs(pvt_ctx* ctx) {
     host[EP_CSOFF + nch] = ns;
     HIPCHK(hipMemcpyAsync(dev, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(dev + EP_BAD, 0, sizeof(int32_t) * nseg, st));
+    int need = nch;                           // chains left to the list walk
+    if (zw) {
+      ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+      ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
+                   P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
+                   P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
+                   P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps};
+      {
+        Scope sc(ctx, PVT_K_OTHER, 0, 0);
+        launch_host_min(r->avail, R.H, P<double>(ctx->hmin), st);
+      }
+      {
+        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+        launch_zwalk(za, nch, st);
+      }
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * 2 * nch,
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      need = 0;
+      for (int c = 0; c < nch; c++) need += host[EP_STATUS + 2 * c] != E.len[c];
+      ctx->n_zchains += nch - need;
+      if (need && (rc = window_lists(ctx, t0, nt, 0, st))) return rc;
+    }
+    ctx->n_gchains += need;
+    ctx->n_longest += *std::max_element(E.len.begin(), E.len.end());
     CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
                    P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
                    r->placement, nullptr, 0, P<int32_t>(ctx->owned[0]), dev + EP_STATUS,
                    r->rt_bw, P<int32_t>(ctx->grp_ord) + t0, ctx->stamps, dev + EP_COFF, dev + EP_CMAP, dev + EP_CSOFF, dev + EP_CSEG,
-                   P<WinRec>(ctx->wres)};
-    {
+                   P<WinRec>(ctx->wres), zw ? 1 : 0};
+    if (need) {
       Scope sc(ctx, PVT_K_COMMIT, 0, 0);
       launch_commit_chains(ca_, nch, st);
     }
@@ -1219,6 +1265,7 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
   }
   if ((rc = round_begin(ctx, r, 0, r->n_hosts, 1))) return rc;
   ctx->n_epochs = ctx->n_segs = ctx->n_rejected = 0;
+  ctx->n_zchains = ctx->n_gchains = ctx->n_longest = 0;
   if ((rc = epoch_groups(ctx))) return rc;
   rc = ctx->rs.egs.empty() ? place_pipelined(ctx) : place_epochs(ctx);
   ctx->rs.active = false;

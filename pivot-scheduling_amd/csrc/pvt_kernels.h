@@ -157,6 +157,7 @@ struct CommitArgs {
   const int32_t* csoff;
   const int32_t* cseg;
   WinRec* wlog;
+  int skip_done;          // chain mode: a chain whose status already says "all walked" is skipped
 };
 
 // Speculative epochs, cost_aware best-fit. The epoch's group segments (processing order,
@@ -187,6 +188,31 @@ void launch_epoch_validate(const EpochArgs& a, hipStream_t st);
 // apply: the accepted segments [0, n_accept) of each chain, chain by chain in segment order
 void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st);
 void launch_commit_chains(const CommitArgs& a, int nchains, hipStream_t st);
+
+// Zero-cost frontier walk of epoch chains (pvt_zwalk.hip): workgroup b walks chain b like the
+// list walk's chain mode (same tables, WinRec log, status[2b] = tasks walked) while it can prove
+// every winner is the lowest-index fitting zero-cost host of its window; otherwise it writes
+// status[2b] = -2 and leaves the chain to the list walk (CommitArgs.skip_done).
+struct ZwalkArgs {
+  const double* avail;    // epoch-start capacities [4][H]
+  const int32_t* zone;
+  int H, Z;
+  const double* dem;      // window tasks [nt][4]
+  const int32_t* anc;     // window tasks' anchors
+  const int32_t* ord;     // window task -> caller index (placement)
+  const double* csum;
+  const double* bsum;
+  const int32_t* coff;
+  const int32_t* cmap;
+  int32_t* status;
+  WinRec* wlog;
+  int32_t* placement;
+  const double* hmin;     // per-dimension host minima, launch_host_min partials
+  uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS)
+};
+constexpr int ZW_MIN_PARTS = 256;
+void launch_host_min(const double* avail, int H, double* part, hipStream_t st);   // [256][4]
+void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st);
 
 // cost_aware first-fit with sort_hosts, as the reference runs it (cost_aware.py:118-124): the
 // hosts sorted once per group by the frozen key (perm, skey = sorted key bits; the radix sort

@@ -889,6 +889,7 @@ __global__ __launch_bounds__(WALK_THREADS) void commit_kernel(CommitArgs A) {
     A.nt = A.coff[b + 1] - base;
     A.cmap += base;
     A.status += 2 * b;
+    if (A.skip_done && A.status[0] == A.nt) return;   // walked by the zero-cost frontier walk
   }
   extern __shared__ __attribute__((aligned(16))) char smem[];
   WalkLDS& S = *reinterpret_cast<WalkLDS*>(smem);

@@ -1,0 +1,404 @@
+// pvt_zwalk.hip — the zero-cost frontier walk of an epoch chain (cost_aware best-fit).
+//
+// A cost_aware best-fit task takes the host of minimum key (score, index), score =
+// (c * ||avail - d||) / bw (scheduler/cost_aware.py:85-97). Hosts in a zone its anchor reaches
+// at zero egress cost (csum = 0) score exactly +0, the smallest key, so while one of them fits,
+// the winner is simply the LOWEST-INDEX fitting host of those zones. An epoch chain
+// (pvt_epoch.hip) holds the groups anchored in one zero-cost component, whose tasks pile onto
+// the first hosts of the component's zones (config 5: the 1500 tasks of the longest chain use
+// fewer than 200 of them). This kernel walks such a chain without candidate lists:
+//
+//   window   the first ZW_M hosts, in index order, of the zones U = the union of the chain's
+//            anchors' zero-cost zones, with their capacities at the epoch start, in LDS;
+//   task     the first window host (index order) that fits and scores exactly 0 -- found 64
+//            hosts per step by one wave (a ballot) -- is committed in LDS and logged (WinRec);
+//
+// exactly the host the sequential reference picks, given three certificates checked here
+// (any failure: the chain is left to the list-based walk, which then runs for it):
+//
+//   (1) a winner exists in the window: every zero-cost host of lower index is in the window
+//       (U contains the anchor's zero-cost zones; the window is U's index-order prefix);
+//   (2) no host outside U scores 0: for every zone z outside U, c = csum[a][z] >= 2^-300 and
+//       bw = bsum[a][z] <= 2^300, and some capacity dimension r separates hosts from tasks,
+//       min_h avail[r][h] - max_t d[r] >= 2^-288 (so s2 >= fl(x_r^2) >= 2^-578 for every such
+//       pair and the score is >= 2^-900 > 0 -- the same bound ca_score_bits uses); hosts outside
+//       U are never committed to by this walk, so their epoch-start state is their state;
+//   (3) zero-cost scores are exactly +0: bw > 0 for the anchor's zero-cost zones and every
+//       window capacity and chain demand is finite with |x| <= 2^500 (s2 finite);
+//
+// and window hosts of U outside the anchor's zero-cost zones are scored exactly (ca_score_bits,
+// a key of 0 only when the score's bits are 0). The log and the chain's progress have the
+// format of the list walk's chain mode, so validation, finality and apply are unchanged.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pvt_device.h"
+#include "pvt_kernels.h"
+
+namespace pvt {
+
+constexpr int ZW_M = 1024;                 // window hosts
+constexpr int ZW_CH = ZW_M / 64;           // window chunks (one wave step each)
+constexpr int ZW_THREADS = 256;
+constexpr int ZW_WAVES = ZW_THREADS / 64;
+constexpr int ZW_SCAN = 16;                // hosts per thread per window-build pass
+constexpr int ZW_MINB = ZW_MIN_PARTS;      // blocks of the host-minimum pass
+constexpr double ZW_BIG = 0x1p500;
+
+struct ZwalkLDS {
+  double wa[4][ZW_M];                      // window capacities (live)
+  int32_t wid[ZW_M];                       // window hosts (ascending index)
+  int32_t wz[ZW_M];                        // their zones
+  uint64_t zm[ZW_CH];                      // current anchor: zero-cost window hosts, per chunk
+  double csum[ZMAX * ZMAX], bsum[ZMAX * ZMAX];
+  int32_t cnt[ZW_SCAN][ZW_WAVES];          // window build: hits per (pass row, wave)
+  double red[ZW_WAVES][12];                // block reductions: max d, min d, min avail
+  double lg[64][4];                        // the batch's log: capacities after each commit
+  int32_t lgid[64];                        //   and the host
+  uint32_t amask[ZMAX];                    // anchor -> its zero-cost zones
+  uint32_t umask;
+  int32_t nwin, bail;
+};
+
+__device__ __forceinline__ double wave_max_d(double v) {
+  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
+  return v;
+}
+__device__ __forceinline__ double wave_min_d(double v) {
+  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
+  return v;
+}
+
+// Per-dimension minimum capacity over all hosts (certificate 2), ZW_MINB partials.
+__global__ __launch_bounds__(256) void host_min_kernel(const double* avail, int H, double* part) {
+  __shared__ double red[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double m[4] = {DINF, DINF, DINF, DINF};
+  for (int h = blockIdx.x * 256 + tid; h < H; h += gridDim.x * 256)
+#pragma unroll
+    for (int r = 0; r < 4; r++) m[r] = fmin(m[r], avail[(size_t)r * H + h]);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    m[r] = wave_min_d(m[r]);
+    if (lane == 0) red[wave][r] = m[r];
+  }
+  __syncthreads();
+  if (tid < 4) {
+    double v = red[0][tid];
+    for (int w = 1; w < 4; w++) v = fmin(v, red[w][tid]);
+    part[blockIdx.x * 4 + tid] = v;
+  }
+}
+
+#ifdef PVT_STAMPS
+__device__ __forceinline__ uint64_t zstamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
+
+__global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
+  __shared__ ZwalkLDS S;
+#ifdef PVT_STAMPS
+  const uint64_t t_start = zstamp();
+  uint64_t n_chunks = 0, n_switch = 0;
+#endif
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int base = A.coff[b];
+  const int nt = A.coff[b + 1] - base;
+  const int32_t* cmap = A.cmap + base;
+  int32_t* status = A.status + 2 * b;
+  const int Z = A.Z, H = A.H;
+
+  for (int i = tid; i < Z * Z; i += ZW_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
+  if (tid == 0) { S.umask = 0; S.nwin = 0; S.bail = 0; }
+  __syncthreads();
+  if (tid < Z) {                             // anchor row -> zero-cost zone mask
+    uint32_t m = 0;
+    for (int z = 0; z < Z; z++) m |= (S.csum[tid * Z + z] == 0.0) ? (1u << z) : 0u;
+    S.amask[tid] = m;
+  }
+  __syncthreads();
+
+  // the chain's zones U, demand extremes and finiteness (certificates 2, 3)
+  uint32_t um = 0;
+  double mx[4] = {-DINF, -DINF, -DINF, -DINF}, mn[4] = {DINF, DINF, DINF, DINF};
+  bool bad = false;
+  for (int i = tid; i < nt; i += ZW_THREADS) {
+    const int w = cmap[i];
+    const int a = A.anc[w];
+    if (a < 0 || a >= Z) { bad = true; continue; }
+    um |= S.amask[a];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const double d = A.dem[(size_t)w * 4 + r];
+      bad |= !(__builtin_fabs(d) <= ZW_BIG);
+      mx[r] = fmax(mx[r], d);
+      mn[r] = fmin(mn[r], d);
+    }
+  }
+  // host minima from the partials
+  double ha[4] = {DINF, DINF, DINF, DINF};
+  for (int k = tid; k < ZW_MINB; k += ZW_THREADS)
+#pragma unroll
+    for (int r = 0; r < 4; r++) ha[r] = fmin(ha[r], A.hmin[k * 4 + r]);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    mx[r] = wave_max_d(mx[r]);
+    mn[r] = wave_min_d(mn[r]);
+    ha[r] = wave_min_d(ha[r]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) { S.red[wave][r] = mx[r]; S.red[wave][4 + r] = mn[r]; S.red[wave][8 + r] = ha[r]; }
+  }
+  if (bad) S.bail = 1;                        // benign race: every writer stores 1
+  if (um) atomicOr(&S.umask, um);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    for (int w = 1; w < ZW_WAVES; w++) {
+      mx[r] = fmax(mx[r], S.red[w][r]);
+      mn[r] = fmin(mn[r], S.red[w][4 + r]);
+      ha[r] = fmin(ha[r], S.red[w][8 + r]);
+    }
+    mx[r] = fmax(mx[r], S.red[0][r]);
+    mn[r] = fmin(mn[r], S.red[0][4 + r]);
+    ha[r] = fmin(ha[r], S.red[0][8 + r]);
+  }
+  bool sep = false;
+#pragma unroll
+  for (int r = 0; r < 4; r++) sep |= (ha[r] - mx[r] >= 0x1p-288);
+  const uint32_t U = S.umask;
+  if (S.bail || !sep || nt <= 0) {
+    if (tid == 0) { status[0] = -2; status[1] = 0; }
+    return;
+  }
+
+  // window: U's hosts in index order (passes of ZW_SCAN x 256 hosts, stable compaction)
+  for (int h0 = 0; h0 < H; h0 += ZW_SCAN * ZW_THREADS) {
+    const int have = S.nwin;
+    if (have >= ZW_M) break;
+    bool hit[ZW_SCAN];
+    int zz[ZW_SCAN];
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) {      // every load in flight at once
+      const int h = h0 + k * ZW_THREADS + tid;
+      zz[k] = h < H ? A.zone[h] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) {
+      const int z = zz[k];
+      hit[k] = z >= 0 && z < Z && ((U >> z) & 1u);
+      const uint64_t m = __ballot(hit[k]);
+      if (lane == 0) S.cnt[k][wave] = __popcll(m);
+    }
+    __syncthreads();
+    int pre = have;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) {
+      int before = 0;
+      for (int w = 0; w < ZW_WAVES; w++) before += (w < wave) ? S.cnt[k][w] : 0;
+      const uint64_t m = __ballot(hit[k]);
+      const int pos = pre + before + __popcll(m & below);
+      if (hit[k] && pos < ZW_M) {
+        const int h = h0 + k * ZW_THREADS + tid;
+        S.wid[pos] = h;
+        S.wz[pos] = zz[k];
+      }
+      for (int w = 0; w < ZW_WAVES; w++) pre += S.cnt[k][w];
+    }
+    __syncthreads();
+    if (tid == 0) S.nwin = min(pre, ZW_M);
+    __syncthreads();
+  }
+  const int nwin = S.nwin;
+  bool wbad = false;
+  for (int p = tid; p < nwin; p += ZW_THREADS) {
+    const int h = S.wid[p];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const double v = A.avail[(size_t)r * H + h];
+      wbad |= !(__builtin_fabs(v) <= ZW_BIG);
+      S.wa[r][p] = v;
+    }
+  }
+  if (wbad) S.bail = 1;
+  __syncthreads();
+  if (S.bail || nwin == 0) {
+    if (tid == 0) { status[0] = -2; status[1] = 0; }
+    return;
+  }
+  if (wave != 0) return;
+#ifdef PVT_STAMPS
+  const uint64_t t_walk = zstamp();
+#endif
+
+  // ---- the walk (one wave). Lane l of chunk c holds window host c * 64 + l. Chunk p0 (the
+  // first that can still fit a chain task) stays in registers, where nearly every task finds its
+  // winner: a task is then four compares, a ballot and a one-lane update, with no memory access
+  // on its path. Otherwise the chunk is written back and the later chunks are scanned in LDS.
+  // The winning lane writes the task's log entry into an LDS batch buffer, flushed to HBM every
+  // 64 tasks.
+  const int nch = (nwin + 63) >> 6;
+  int p0 = 0;                                // chunks before p0 cannot fit any chain task
+  int cur = -1;                              // anchor the zero-cost masks are for
+  int done = 0;
+  bool failed = false;
+  // chunk p0 in registers
+  double ra0, ra1, ra2, ra3;
+  int32_t rid;
+  uint64_t rzm = 0, rvalid = 0;              // its zero-cost lanes (anchor cur), its real lanes
+  bool dirty = false;
+  auto load_chunk = [&](int c) {
+    const int p = c * 64 + lane;
+    const int q = min(p, nwin - 1);
+    ra0 = S.wa[0][q]; ra1 = S.wa[1][q]; ra2 = S.wa[2][q]; ra3 = S.wa[3][q];
+    rid = S.wid[q];
+    rvalid = __ballot(p < nwin);
+    dirty = false;
+  };
+  auto store_chunk = [&](int c) {
+    const int p = c * 64 + lane;
+    if (dirty && p < nwin) { S.wa[0][p] = ra0; S.wa[1][p] = ra1; S.wa[2][p] = ra2; S.wa[3][p] = ra3; }
+    dirty = false;
+  };
+  load_chunk(0);
+  for (int i0 = 0; i0 < nt && !failed; i0 += 64) {
+    const int ti = i0 + lane;
+    const int tw = ti < nt ? cmap[ti] : 0;
+    double td[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) td[r] = A.dem[(size_t)tw * 4 + r];
+    const int tanc = A.anc[tw];
+    const int tcal = A.ord[tw];
+    const int kn = min(64, nt - i0);
+    int k = 0;
+    for (; k < kn; k++) {
+      const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
+      const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
+      const int a = readlane_i(tanc, k);
+      if (a != cur) {
+        // certificates 2 / 3 for this anchor's zone row
+        bool ok = true;
+        if (lane < Z) {
+          const double c = S.csum[a * Z + lane], bw = S.bsum[a * Z + lane];
+          if (c == 0.0) ok = bw > 0.0;
+          else if (!((U >> lane) & 1u)) ok = (c >= 0x1p-300) && (bw <= 0x1p300);
+        }
+        if (__ballot(!ok)) { failed = true; break; }
+        const uint32_t am = S.amask[a];
+        for (int c = 0; c < nch; c++) {
+          const int p = c * 64 + lane;
+          const uint64_t m = __ballot(p < nwin && ((am >> S.wz[min(p, nwin - 1)]) & 1u));
+          if (lane == 0) S.zm[c] = m;
+          if (c == p0) rzm = m;
+        }
+        cur = a;
+#ifdef PVT_STAMPS
+        n_switch++;
+#endif
+      }
+      // exact scores for this lane's host when it fits but is not zero-cost for `a`
+      auto zero_exact = [&](bool f, bool k0, double a0, double a1, double a2, double a3, int q) {
+        if (__builtin_expect(__ballot(f && !k0) != 0, 0)) {
+          if (f && !k0) {
+            const int z = S.wz[q];
+            const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
+            const double sc = (S.csum[a * Z + z] * __builtin_sqrt(s2)) / S.bsum[a * Z + z];
+            k0 = __double_as_longlong(sc) == 0;
+          }
+        }
+        return k0;
+      };
+      bool found = false;
+      for (;;) {                               // the register chunk (advancing past dead ones)
+#ifdef PVT_STAMPS
+        n_chunks++;
+#endif
+        const bool f = ((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, d0, d1, d2, d3);
+        const bool k0 = zero_exact(f, (rzm >> lane) & 1ull, ra0, ra1, ra2, ra3,
+                                   min(p0 * 64 + lane, nwin - 1));
+        const uint64_t m = __ballot(f && k0);
+        if (m) {
+          // commit: resc[h] -= t_demand (cost_aware.py:95), by the lowest such lane, which logs
+          if (lane == __builtin_ctzll(m)) {
+            ra0 -= d0; ra1 -= d1; ra2 -= d2; ra3 -= d3;
+            S.lg[k][0] = ra0; S.lg[k][1] = ra1; S.lg[k][2] = ra2; S.lg[k][3] = ra3;
+            S.lgid[k] = rid;
+          }
+          dirty = true;
+          found = true;
+          break;
+        }
+        if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
+          break;                               // chunk p0 still useful: look further in LDS
+        store_chunk(p0);                       // dead: move the register chunk on
+        if (++p0 >= nch) break;
+        load_chunk(p0);
+        rzm = S.zm[p0];
+      }
+      if (!found && p0 < nch) {
+        store_chunk(p0);
+        for (int c = p0 + 1; c < nch; c++) {
+#ifdef PVT_STAMPS
+          n_chunks++;
+#endif
+          const int p = c * 64 + lane;
+          const int q = min(p, nwin - 1);
+          const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
+          const int32_t id = S.wid[q];
+          const uint64_t zm = S.zm[c];
+          const bool f = p < nwin && fits<false>(a0, a1, a2, a3, d0, d1, d2, d3);
+          const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
+          const uint64_t m = __ballot(f && k0);
+          if (m) {
+            if (lane == __builtin_ctzll(m)) {
+              const double n0 = a0 - d0, n1 = a1 - d1, n2 = a2 - d2, n3 = a3 - d3;
+              S.wa[0][q] = n0; S.wa[1][q] = n1; S.wa[2][q] = n2; S.wa[3][q] = n3;
+              S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
+              S.lgid[k] = id;
+            }
+            found = true;
+            break;
+          }
+        }
+      }
+      if (!found) { failed = true; break; }  // certificate 1 fails: the list walk decides
+      done++;
+    }
+    if (lane < k) {                          // the batch's log (WinRec; sup: epoch_final_kernel)
+      WinRec& e = A.wlog[tw];
+      const int32_t id = S.lgid[lane];
+      e.s = 0.0;
+      e.id = id;
+      e.a[0] = S.lg[lane][0]; e.a[1] = S.lg[lane][1]; e.a[2] = S.lg[lane][2]; e.a[3] = S.lg[lane][3];
+      A.placement[tcal] = id;
+    }
+  }
+  if (lane == 0) { status[0] = failed ? -2 : done; status[1] = 0; }
+#ifdef PVT_STAMPS
+  if (lane == 0 && A.stamps) {
+    const uint64_t t_end = zstamp();
+    atomicAdd((unsigned long long*)&A.stamps[0], (unsigned long long)(t_walk - t_start));
+    atomicAdd((unsigned long long*)&A.stamps[1], (unsigned long long)(t_end - t_walk));
+    atomicAdd((unsigned long long*)&A.stamps[2], (unsigned long long)n_chunks);
+    atomicAdd((unsigned long long*)&A.stamps[3], (unsigned long long)done);
+    atomicAdd((unsigned long long*)&A.stamps[4], (unsigned long long)n_switch);
+  }
+#endif
+}
+
+void launch_host_min(const double* avail, int H, double* part, hipStream_t st) {
+  hipLaunchKernelGGL(host_min_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, part);
+}
+
+void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st) {
+  hipLaunchKernelGGL(zwalk_kernel, dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+}
+
+}  // namespace pvt

@@ -46,6 +46,8 @@ def load_library(path=None):
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
         "pvt_set_score_tw": ([c_void_p, c_int], c_int),
         "pvt_set_epochs": ([c_void_p, c_int], c_int),
+        "pvt_set_zero_walk": ([c_void_p, c_int], c_int),
+        "pvt_zero_walk_stats": ([c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 3, c_int),
         "pvt_epoch_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                              ctypes.POINTER(ctypes.c_int64)], c_int),
         "pvt_last_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64),
@@ -375,10 +377,19 @@ class PlacementEngine:
         """cost_aware best-fit: group-parallel speculative epochs (default on; identical results)."""
         self._check(self.lib.pvt_set_epochs(self.ctx, int(bool(on))))
 
+    def set_zero_walk(self, on=True):
+        """Epoch chains: the zero-cost frontier walk where it proves its winners (default on;
+        identical results)."""
+        self._check(self.lib.pvt_set_zero_walk(self.ctx, int(bool(on))))
+
     def epoch_stats(self):
         e, s, r = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         self._check(self.lib.pvt_epoch_stats(self.ctx, ctypes.byref(e), ctypes.byref(s), ctypes.byref(r)))
-        return {"epochs": e.value, "segments": s.value, "rejected": r.value}
+        zf, zl, zc = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.pvt_zero_walk_stats(self.ctx, ctypes.byref(zf), ctypes.byref(zl),
+                                                 ctypes.byref(zc)))
+        return {"epochs": e.value, "segments": s.value, "rejected": r.value,
+                "frontier_chains": zf.value, "list_chains": zl.value, "longest_chain_tasks": zc.value}
 
     def set_profiling(self, on=True):
         self._check(self.lib.pvt_set_profiling(self.ctx, int(bool(on))))

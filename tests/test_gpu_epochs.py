@@ -9,7 +9,16 @@ import pytest
 from oracle import oracle
 from pivot_place import _abi, synthetic
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("zero_walk")]
+
+
+@pytest.fixture(params=[True, False], ids=["frontier", "lists"])
+def zero_walk(engine, request):
+    """Every epoch test runs with the zero-cost frontier walk (pvt_zwalk.hip) and without it
+    (every chain on the list walk)."""
+    engine.set_zero_walk(request.param)
+    yield request.param
+    engine.set_zero_walk(True)
 
 
 def _same(res, ref):
@@ -43,12 +52,16 @@ def _regroup(r, anchors):
 
 @pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70_000, 2600, 2), (200_000, 12_000, 3),
                                       (9000, 4000, 4)])
-def test_epochs_match_oracle(engine, H, T, seed):
+def test_epochs_match_oracle(engine, zero_walk, H, T, seed):
     r = synthetic.make_round(_abi.PVT_CA_BF, H, T, seed=seed)
     ref = oracle.place(r, threads=8)
     res, st = _place(engine, r)
     _same(res, ref)
     assert st["epochs"] >= 1 and st["segments"] >= 2
+    if zero_walk:       # plenty of zero-cost capacity: the frontier walk proves every chain
+        assert st["frontier_chains"] > 0 and st["list_chains"] == 0, st
+    else:
+        assert st["frontier_chains"] == 0, st
     seq, st0 = _place(engine, r, epochs=False)
     _same(seq, ref)
     assert st0["epochs"] == 0
@@ -105,8 +118,12 @@ def test_epochs_exact_fits_tie_at_zero(engine):
     r.dem[0, :] = 0.5
     r.dem[1, :] = 3932.16
     ref = oracle.place(r, threads=8)
-    res, _ = _place(engine, r)
+    res, st = _place(engine, r)
     _same(res, ref)
+    # once hosts were filled to 0.5 cpus (an exact fit) no capacity dimension separates hosts
+    # from tasks: the frontier walk cannot rule out a score-0 host outside its zones and leaves
+    # those epochs' chains to the lists
+    assert st["list_chains"] > 0, st
 
 
 def test_epochs_long_chains_split(engine):
@@ -124,3 +141,61 @@ def test_epochs_long_chains_split(engine):
     res, st = _place(engine, r)
     _same(res, ref)
     assert st["epochs"] >= 2
+
+
+def test_zero_walk_non_transitive_zero_cost(engine, zero_walk):
+    """Zones 0-1 and 1-2 exchange data for free but 0-2 do not: one component {0, 1, 2} whose
+    window holds zone-2 hosts that score > 0 for anchor 0 (scored exactly, never taken as 0)."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 40_000, 5000, seed=13)
+    cost = np.array(r.cost, dtype=np.float64)
+    for a, b in ((0, 1), (1, 2)):
+        cost[a, b] = cost[b, a] = 0.0
+    cost[0, 2], cost[2, 0] = 0.03, 0.02
+    r.cost = cost
+    # zone-1 hosts nearly full, so anchor-0 tasks must look past them
+    r.avail[0, r.zone == 1] = 0.5
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    if zero_walk:
+        assert st["frontier_chains"] > 0, st
+
+
+def test_zero_walk_exact_fit_hosts_elsewhere(engine, zero_walk):
+    """A few hosts of other components fit some tasks exactly (score 0 at a lower index than
+    the zero-cost winner): the frontier walk must hand such chains to the lists."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 30_000, 4000, seed=14)
+    # disk / gpus of every host 0 (tasks ask for 0): only cpus / mem could separate, and some
+    # hosts take the exact (cpus, mem) of a task
+    r.avail[2, :] = 0.0
+    r.avail[3, :] = 0.0
+    for k, h in enumerate(range(3, 400, 7)):
+        r.avail[0, h] = r.dem[0, k * 11]
+        r.avail[1, h] = r.dem[1, k * 11]
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+
+
+def test_zero_walk_window_exhausted(engine, zero_walk):
+    """Zero-cost capacity runs out inside the 1024-host window: chains fall back to the lists
+    (positive-score hosts, then no host at all) and stay exact."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 6000, 5000, seed=15)
+    r.avail[0, :] = 0.5         # one small task per host; larger tasks fit nowhere
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    if zero_walk:
+        assert st["list_chains"] > 0, st
+
+
+def test_zero_walk_tiny_egress_costs(engine, zero_walk):
+    """Subnormal egress costs to some zones: a positive score can round to 0 there, so the
+    frontier walk leaves those anchors' chains to the lists."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, 20_000, 3000, seed=16)
+    cost = np.array(r.cost, dtype=np.float64)
+    cost[5, 11] = cost[11, 5] = 5e-324
+    r.cost = cost
+    ref = oracle.place(r, threads=8)
+    res, _ = _place(engine, r)
+    _same(res, ref)
