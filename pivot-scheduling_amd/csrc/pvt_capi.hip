@@ -495,28 +495,24 @@ static void lists_from(pvt_ctx* ctx, Lists& L, int b = 0) {
 static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   const int T = r->n_tasks, H = r->n_hosts;
   hipStream_t st = ctx->stream;
-  // Window: the walk rescans the window's touched hosts for every task, so short windows keep
-  // that scan short; the count pass then spreads each window over more host segments.
-  // (bench sweep at 1M hosts x 10k tasks, DESIGN.md §5: pipelined 64 -> 34.6 ms, 128 -> 35.6,
-  // 192 -> 39.7, 256 -> 42.8; sequential 256 -> 39.2)
+  // Window: the walk's per-range passes rescan the window's touched hosts, so windows stay
+  // short; longer windows cut the per-window launches and hand-offs. (bench sweep at 1M hosts x
+  // 10k tasks with the speculative-range walk, profiles/r02h: pipelined 64 -> 20.1 ms,
+  // 128 -> 18.5, 256 -> 19.4)
   const int wdef = ctx->pipeline ? OPP_WINDOW_PIPE : OPP_WINDOW_DEFAULT;
   const int W = std::max(1, std::min(ctx->window > 0 ? ctx->window : wdef, OPP_MAXW));
   const int nq = (H + OPP_CH - 1) / OPP_CH, nsq = (nq + OPP_SUP - 1) / OPP_SUP;
-  const int task_waves = (std::min(W, std::max(T, 1)) + OPP_TW - 1) / OPP_TW;
-  int S = std::max(1, std::min(nsq, (4096 + task_waves - 1) / task_waves));
-  const int seg_sup = (nsq + S - 1) / S;
-  S = (nsq + seg_sup - 1) / seg_sup;
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   launch_gather_tasks(r->dem, r->order, nullptr, nullptr, T, P<double>(ctx->dem_ord),
                       P<int32_t>(ctx->anc_ord), nullptr, st);
-  // Pipelined windows (W <= OPP_MAXW / 2, so a walk's inherited + own touched hosts fit its
-  // LDS): window k+1's count pass runs on the side stream while window k is walked. Walk k
-  // leaves global availability untouched and hands its hosts to walk k+1, which applies them
-  // on entry and then releases count k+2; so every count pass reads the capacities its walk's
+  // Pipelined windows (a walk's inherited + own touched hosts, 2 x OPP_MAXW, fit its LDS):
+  // window k+1's count pass runs on the side stream while window k is walked. Walk k leaves
+  // global availability untouched and hands its hosts to walk k+1, which applies them on entry
+  // and then releases count k+2; so every count pass reads the capacities its walk's
   // predecessor started from, and the hosts that walk touched are touched for the next walk.
   const int nwin = (T + W - 1) / W;
-  const bool pipe = ctx->pipeline && nwin > 1 && W <= OPP_MAXW / 2;
+  const bool pipe = ctx->pipeline && nwin > 1;
   const int nbuf = pipe ? 2 : 1;
   const size_t bm_bytes = sizeof(uint64_t) * 4 * (size_t)nq * W;
   const size_t sc_bytes = sizeof(int32_t) * (size_t)nsq * W;
@@ -532,7 +528,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   const double bpc = bytes_per_candidate(r->mode);
   auto count = [&](int k, hipStream_t s) {
     const int t0 = k * W, nt = std::min(W, T - t0);
-    OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, S, seg_sup, nq, nsq,
+    OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, 0, 0, nq, nsq,
                     W, bm_of(k % nbuf), sc_of(k % nbuf), 0, nsq, nq, nsq};
     Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc, s);
     launch_opp_count(ca, s);
@@ -542,6 +538,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
     const int t0 = k * W, nt = std::min(W, T - t0);
     const bool next = pipe && k + 1 < nwin;
     ctx->windows++;
+    if (!pipe && k > 0) count(k, st);   // sequential: window k counted after walk k-1 wrote back
     const OppTouched* in = (pipe && k > 0) ? tl_of((k - 1) % nbuf) : nullptr;
     if (in) launch_opp_apply(in, r->avail, H, st);   // walk k-1's commits, before count k+1
     if (next) {
@@ -1345,15 +1342,11 @@ static int opp_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out, in
   }
   const int nt = std::min(R.opp_W, R.T - R.t0);
   const int nsr = std::max(0, R.opp_sq_hi - R.opp_sq_lo);
-  const int task_waves = (nt + OPP_TW - 1) / OPP_TW;
-  int S = std::max(1, std::min(std::max(nsr, 1), (4096 + task_waves - 1) / task_waves));
-  const int seg_sup = (std::max(nsr, 1) + S - 1) / S;
-  S = (std::max(nsr, 1) + seg_sup - 1) / seg_sup;
   uint64_t* bm = reinterpret_cast<uint64_t*>(package);
   int32_t* sc = reinterpret_cast<int32_t*>(reinterpret_cast<char*>(package) +
                                            (size_t)nt * R.opp_Psq * OPP_SUP * 4 * sizeof(uint64_t));
   if (nsr > 0) {
-    OppCountArgs ca{R.r.avail, P<double>(ctx->dem_ord) + (size_t)R.t0 * 4, R.H, nt, S, seg_sup,
+    OppCountArgs ca{R.r.avail, P<double>(ctx->dem_ord) + (size_t)R.t0 * 4, R.H, nt, 0, 0,
                     R.opp_nq, R.opp_nsq, nt, bm, sc, R.opp_sq_lo, R.opp_sq_hi,
                     R.opp_Psq * OPP_SUP, R.opp_Psq};
     Scope s(ctx, PVT_K_SCORE, (double)nt * (R.hi - R.lo), (double)nt * (R.hi - R.lo) * 32.0);

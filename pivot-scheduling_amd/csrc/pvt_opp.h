@@ -4,9 +4,10 @@
 // randomizer.choice(qualified) (= randint(0, n), no draw when n == 1) and commits. On the GPU:
 //   count kernel   per window task, the snapshot feasibility bitmap of every chunk of OPP_CH
 //                  hosts and the count of every super-chunk of OPP_SUP chunks (fit-mask pass)
-//   commit walk    one wave, tasks in order: n = snapshot count minus the touched hosts that
-//                  stopped fitting; MT19937 randint(n) in LDS; select the k-th currently
-//                  feasible host super-chunk -> chunk -> host; commit.
+//   commit walk    one workgroup: per range of OPP_R tasks, the draws (MT19937 randint(n) in
+//                  LDS, n = snapshot count minus the touched hosts that stopped fitting) and
+//                  the candidate hosts from the k-th feasible on are computed in parallel; one
+//                  wave then verifies and commits them in task order (pvt_opp.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -16,14 +17,14 @@ namespace pvt {
 constexpr int OPP_CH = 256;     // hosts per chunk
 constexpr int OPP_SUP = 64;     // chunks per super-chunk (16384 hosts)
 constexpr int OPP_TW = 8;       // tasks per wave in the count kernel
-constexpr int OPP_MAXW = 1024;  // tasks per window (commit-walk LDS: touched snapshot + current)
+constexpr int OPP_MAXW = 256;   // tasks per window (commit-walk LDS holds 2 x OPP_MAXW touched hosts)
 constexpr int OPP_WINDOW_DEFAULT = 256;   // sequential count / walk
-constexpr int OPP_WINDOW_PIPE = 64;       // pipelined: the walk (touched scan) is the bound
+constexpr int OPP_WINDOW_PIPE = 128;      // pipelined windows
 
 struct OppCountArgs {
   const double* avail;
   const double* dem;      // window tasks [nt][4]
-  int H, nt, S, seg_sup, nq, nsq, ldc;
+  int H, nt, S, seg_q, nq, nsq, ldc;   // S, seg_q: set by launch_opp_count
   uint64_t* bm;           // [ldc][ldq][4] per-chunk feasibility bitmaps (bit = host), task-major
   int32_t* sc;            // [ldc][lds] super-chunk counts, task-major
   // super-chunks [sq_lo, sq_hi) are counted (a rank's share under host sharding; [0, nsq)

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "pvt_device.h"
 #include "pvt_kernels.h"
 #include "pvt_mt.h"
@@ -19,12 +21,15 @@
 namespace pvt {
 
 // ------------------------------------------------------------------------------------------
-// Count kernel: block = 4 waves, each wave OPP_TW tasks over one host segment (a run of
-// super-chunks); blockIdx % S picks the segment (XCD-affine, as in score_kernel). For every
-// (task, 256-host chunk) it stores the chunk's feasibility bitmap (the four wave ballots,
-// 32 B) and, per super-chunk, the feasible count, task-major: the walk's dependent read of one
-// super-chunk's 64 chunk bitmaps for one task is then 2 KiB contiguous. A chunk's host loads are issued one chunk
-// ahead (register double buffer, clamped indices instead of branches).
+// Count kernel: block = 4 waves, each wave OPP_TW tasks over one host segment of seg_q chunks
+// (a power of two <= OPP_SUP, so a segment lies inside one super-chunk); blockIdx % S picks the
+// segment (all task tiles of a segment on one XCD's L2). For every (task, 256-host chunk) it
+// stores the chunk's feasibility bitmap (the four wave ballots, 32 B) and adds the segment's
+// feasible count to its super-chunk's (zeroed first), task-major: the walk's read of one
+// super-chunk's 64 chunk bitmaps for one task is then 2 KiB contiguous. A chunk's host loads
+// are issued one chunk ahead (register double buffer, clamped indices instead of branches).
+// Segments are sized for ~2048 blocks: with whole super-chunks per segment a 64-task window
+// was 124 blocks, each walking 64 chunks with its load latency exposed (136 us per window).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
   constexpr int U = OPP_CH / WAVE;
@@ -43,8 +48,8 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
       d0[k] = d1[k] = d2[k] = d3[k] = DINF;
     }
   }
-  const int Q0 = A.sq_lo + seg * A.seg_sup, Q1 = min(A.sq_hi, Q0 + A.seg_sup);
-  const int qa = Q0 * OPP_SUP, qb = min(A.nq, Q1 * OPP_SUP);
+  const int qlo = A.sq_lo * OPP_SUP, qhi = min(A.nq, A.sq_hi * OPP_SUP);
+  const int qa = qlo + seg * A.seg_q, qb = min(qhi, qa + A.seg_q);
   double n0[U], n1[U], n2[U], n3[U];
   auto fetch = [&](int q) {
 #pragma unroll
@@ -79,11 +84,11 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
       }
     }
     if (lane < nt) {
-      uint64_t* o = A.bm + ((size_t)(t0 + lane) * A.ldq + (q - A.sq_lo * OPP_SUP)) * U;
+      uint64_t* o = A.bm + ((size_t)(t0 + lane) * A.ldq + (q - qlo)) * U;
 #pragma unroll
       for (int u = 0; u < U; u++) o[u] = mine[u];
     }
-    if ((q + 1) % OPP_SUP == 0 || q + 1 == qb) {   // super-chunk boundary
+    if ((q + 1) % OPP_SUP == 0 || q + 1 == qb) {   // super-chunk (or segment) end
       const int Q = q / OPP_SUP;
       int v = 0;
 #pragma unroll
@@ -91,36 +96,75 @@ __global__ __launch_bounds__(256) void opp_count_kernel(OppCountArgs A) {
         if (lane == k) v = sup[k];
         sup[k] = 0;
       }
-      if (lane < nt) A.sc[(size_t)(t0 + lane) * A.lds + (Q - A.sq_lo)] = v;
+      if (lane < nt && v != 0) atomicAdd(&A.sc[(size_t)(t0 + lane) * A.lds + (Q - A.sq_lo)], v);
     }
   }
 }
 
-void launch_opp_count(const OppCountArgs& a, hipStream_t st) {
+void launch_opp_count(const OppCountArgs& a0, hipStream_t st) {
+  OppCountArgs a = a0;
   const int tiles = (a.nt + 4 * OPP_TW - 1) / (4 * OPP_TW);
+  const int nqr = std::max(1, std::min(a.nq, a.sq_hi * OPP_SUP) - a.sq_lo * OPP_SUP);
+  a.seg_q = OPP_SUP;
+  while (a.seg_q > 1 && (long long)tiles * ((nqr + a.seg_q - 1) / a.seg_q) < 2048) a.seg_q >>= 1;
+  a.S = (nqr + a.seg_q - 1) / a.seg_q;
+  (void)hipMemsetAsync(a.sc, 0, sizeof(int32_t) * (size_t)a.nt * a.lds, st);
   hipLaunchKernelGGL(opp_count_kernel, dim3(tiles * a.S), dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------
-// Commit walk (one wave).
+// Commit walk: speculative ranges (one workgroup of OPP_NW waves).
+//
+// The walk takes a window's tasks in ranges of up to OPP_R. For a range starting at task s,
+// every task's draw and candidates are computed up front, in parallel, on the state at s:
+//   n_j  snapshot count minus the touched hosts that stopped fitting ("lost" at s),
+//   k_j  randint(0, n_j), drawn in task order from the live MT19937 state,
+//   c_j  the OPP_C hosts feasible at s from position k_j on, in host order, inside k_j's
+//        super-chunk, with their availability loaded from HBM.
+// One wave then walks the range in order without a memory round trip. A commit of host h by
+// task i can only take h out of a later task's feasible set ("new lost"); every lane (= a later
+// task of the range) records that from h's capacities before and after the commit. Task i:
+//   * n_true = n_i - (new lost of i). randint draws masked outputs until one is <= n - 1, so
+//     with the same mask and k_i <= n_true - 1 the true draw consumed the same outputs and
+//     returned k_i (every output rejected for n_i is rejected for n_true < n_i);
+//   * the k-th feasible host: m = new lost hosts below c_i[0] shift it to the m-th candidate
+//     that still fits (a candidate touched in this walk reads its capacity from the LDS hash).
+// A task whose draw changed or whose candidates ran out starts a new range (the MT19937 state
+// saved at the range start is restored and the range's consumed outputs replayed). A range's
+// first task always verifies, so every range makes progress. Measured (config 5):
+// the single-wave walk it replaces spent ~8000 cycles per task, most of it on two dependent HBM
+// loads (the drawn super-chunk's bitmaps, then the chosen host) and a rescan of every touched
+// host per task.
 // ------------------------------------------------------------------------------------------
-constexpr int OPP_HASH_BITS = 12;
-constexpr int OPP_NSQ_MAX = 1024;   // super-chunks supported: 16.7M hosts
+constexpr int OPP_R = 64;               // tasks per speculation range (one walker lane each)
+constexpr int OPP_C = 16;               // candidates per task (4 lanes each load one)
+constexpr int OPP_NW = 8;               // waves of the walk workgroup
+constexpr int OPP_TB = OPP_R / OPP_NW;  // range tasks per wave in the parallel passes
+constexpr int OPP_MAXT = 2 * OPP_MAXW;  // touched hosts: inherited + own
+constexpr int OPP_HASH_BITS = 11;
 constexpr int OPP_HASH = 1 << OPP_HASH_BITS;
+static_assert(OPP_C * 4 == WAVE, "one lane per (candidate, resource)");
+static_assert(OPP_HASH >= 4 * OPP_MAXT, "touched-host hash load factor");
 
 struct OppLDS {
   int32_t hkey[OPP_HASH];
   int32_t hval[OPP_HASH];
-  int32_t tid[OPP_MAXW];
-  int32_t lost[OPP_MAXW];
-  double sa[4][OPP_MAXW];   // snapshot availability of touched hosts (the count pass's view)
-  double ta[4][OPP_MAXW];   // current availability of touched hosts
-  double sb[4][OPP_MAXW];   // availability when this walk started (pipelined hand-off)
-  int32_t own[OPP_MAXW];    // touched by this walk
-  int32_t slost[OPP_NSQ_MAX];   // per task: lost hosts per super-chunk
-  uint64_t lmask[OPP_SUP][4];   // per task: lost hosts of the chosen super-chunk, as chunk bitmaps
+  int32_t tid[OPP_MAXT];
+  int32_t own[OPP_MAXT];        // touched by this walk
+  double sa[4][OPP_MAXT];       // touched hosts in the count pass's view
+  double ta[4][OPP_MAXT];       // current
+  double sb[4][OPP_MAXT];       // when this walk started (pipelined hand-off)
+  double cav[OPP_R][4][OPP_C];  // candidates' availability at the walk's start (HBM)
+  int32_t cand[OPP_R][OPP_C];
+  int32_t nspec[OPP_R];
+  uint32_t kdraw[OPP_R];
+  int32_t cnt[OPP_R];           // MT19937 outputs the draw consumed
+  int32_t ccount[OPP_R];
   uint32_t mt[625];
+  uint32_t mtb[625];            // state at the range start
   int32_t pl[OPP_MAXW];         // placements of the window, written out when the walk ends
+  int32_t wl[OPP_NW][WAVE];     // per wave: a task's lost hosts (pass 1)
+  int32_t ctl[4];               // next range start, touched count
 };
 
 static_assert(sizeof(OppLDS) <= 160 * 1024, "opportunistic walk LDS exceeds a CU's 160 KiB");
@@ -157,6 +201,55 @@ __device__ __forceinline__ int select_bit(uint64_t x, int r) {
   return pos;
 }
 
+// numpy legacy randint's mask for range rng: the next power of two minus one.
+__device__ __forceinline__ uint32_t rint_mask(uint32_t rng) {
+  rng |= rng >> 1; rng |= rng >> 2; rng |= rng >> 4; rng |= rng >> 8; rng |= rng >> 16;
+  return rng;
+}
+// mt_randint that also counts the outputs it consumed. The rejection loop runs over the wave's
+// 64 buffered outputs at once: the first buffered output (from w.used on) whose masked value
+// is <= rng is the draw (a ballot), so a draw costs one ballot per buffer instead of one
+// readlane per output.
+__device__ inline uint32_t mt_randint_cnt(uint32_t* key, MtWave& w, uint32_t n, int& used) {
+  const uint32_t rng = n - 1;
+  if (rng == 0) return 0;
+  const uint32_t mask = rint_mask(rng);
+  const int lane = lane_id();
+  for (;;) {
+    if (w.used >= w.limit) mt_refill(key, w);
+    const uint64_t ok = __ballot(lane >= w.used && lane < w.limit && (w.buf & mask) <= rng);
+    if (ok) {
+      const int j = __builtin_ctzll(ok);
+      used += j + 1 - w.used;
+      w.used = j + 1;
+      return (uint32_t)__builtin_amdgcn_readlane((int)w.buf, j) & mask;
+    }
+    used += w.limit - w.used;
+    w.used = w.limit;
+  }
+}
+
+// The touched hosts [q0, q0 + 64) lost for demand d -- they fitted in the count pass's view and
+// no longer fit -- as a ballot over lanes; th = lane's host id.
+__device__ __forceinline__ uint64_t lost_piece(const OppLDS& S, int m, int q0, double d0, double d1,
+                                               double d2, double d3, int32_t& th) {
+  const int q = q0 + lane_id(), qq = min(q, m - 1);
+  const bool lf = q < m &&
+                  fits<false>(S.sa[0][qq], S.sa[1][qq], S.sa[2][qq], S.sa[3][qq], d0, d1, d2, d3) &&
+                  !fits<false>(S.ta[0][qq], S.ta[1][qq], S.ta[2][qq], S.ta[3][qq], d0, d1, d2, d3);
+  th = S.tid[qq];
+  return __ballot(lf);
+}
+__device__ __forceinline__ int count_lost(const OppLDS& S, int m, double d0, double d1, double d2,
+                                          double d3) {
+  int n = 0;
+  for (int q0 = 0; q0 < m; q0 += WAVE) {
+    int32_t th;
+    n += __popcll(lost_piece(S, m, q0, d0, d1, d2, d3, th));
+  }
+  return n;
+}
+
 #ifdef PVT_STAMPS
 __device__ __forceinline__ uint64_t ostamp() {
   uint64_t t;
@@ -176,234 +269,478 @@ __device__ __forceinline__ uint64_t ostamp() {
 #endif
 
 // One wave orders its own LDS operations: a compiler fence plus lgkmcnt(0). (__syncthreads
-// would also wait vmcnt(0), i.e. for the next task's prefetched HBM loads.)
+// would also wait vmcnt(0).)
 __device__ __forceinline__ void wave_lds_fence() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-__global__ __launch_bounds__(64) void opp_commit_kernel(OppCommitArgs A) {
+__global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs A) {
   constexpr int U = OPP_CH / WAVE;
   constexpr int SUPH = OPP_SUP * OPP_CH;
+  constexpr int NT = OPP_NW * WAVE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   OppLDS& S = *reinterpret_cast<OppLDS*>(smem);
-  const int lane = lane_id();
-  for (int i = lane; i < OPP_HASH; i += WAVE) S.hkey[i] = -1;
-  for (int i = lane; i < A.nt; i += WAVE) S.pl[i] = -1;
-  for (int i = lane; i < 625; i += WAVE) S.mt[i] = A.mt[i];
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  int m = 0;
-  if (A.in) {
-    // the previous walk's commits (already in global availability, launch_opp_apply): touched,
-    // with the count pass's snapshot as sa
-    m = __builtin_amdgcn_readfirstlane(A.in->n);
-    for (int q = lane; q < m; q += WAVE) {
-      const int32_t h = A.in->tid[q];
-      for (int r = 0; r < 4; r++) {
-        const double t = A.in->ta[r][q];
-        S.sa[r][q] = A.in->sb[r][q];
-        S.ta[r][q] = t;
-        S.sb[r][q] = t;
-      }
-      S.tid[q] = h;
-      S.own[q] = 0;
-      uint32_t p = ohslot(h);
-      while (atomicCAS(&S.hkey[p], -1, h) != -1) p = (p + 1) & (OPP_HASH - 1);
-      S.hval[p] = q;
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tx = threadIdx.x;
+  for (int i = tx; i < OPP_HASH; i += NT) S.hkey[i] = -1;
+  for (int i = tx; i < A.nt; i += NT) S.pl[i] = -1;
+  for (int i = tx; i < 625; i += NT) S.mt[i] = A.mt[i];
+  __syncthreads();
+  // the previous walk's commits (already in global availability, launch_opp_apply): touched,
+  // with the count pass's snapshot as sa
+  const int m0 = A.in ? A.in->n : 0;
+  for (int q = tx; q < m0; q += NT) {
+    const int32_t h = A.in->tid[q];
+    for (int r = 0; r < 4; r++) {
+      const double t = A.in->ta[r][q];
+      S.sa[r][q] = A.in->sb[r][q];
+      S.ta[r][q] = t;
+      S.sb[r][q] = t;
     }
+    S.tid[q] = h;
+    S.own[q] = 0;
+    uint32_t p = ohslot(h);
+    while (atomicCAS(&S.hkey[p], -1, h) != -1) p = (p + 1) & (OPP_HASH - 1);
+    S.hval[p] = q;
   }
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  if (tx == 0) { S.ctl[0] = 0; S.ctl[1] = m0; }
+  __syncthreads();
   const bool fast = A.nsq <= WAVE;   // one super-chunk count per lane (H <= 1,048,576)
-  MtWave mw;
-  mw.buf = 0; mw.used = 0; mw.limit = 0;
-  // next task's super-chunk counts and demand, prefetched with vector loads (lanes 0-3 hold
-  // the demand), so no scalar-memory wait is mixed with the walk's LDS traffic
-  int scn = (fast && A.nt > 0 && lane < A.nsq) ? A.sc[lane] : 0;
-  double dn = (A.nt > 0) ? A.dem[lane & 3] : 0.0;
-
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #ifdef PVT_STAMPS
-  uint64_t ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tl = ostamp();
 #endif
-  for (int i = 0; i < A.nt; i++) {
-    OSTAMP(6);
-    const double dv = dn;
-    const double d0 = readlane_d(dv, 0), d1 = readlane_d(dv, 1), d2 = readlane_d(dv, 2), d3 = readlane_d(dv, 3);
-    const int scv = scn;
-    if (i + 1 < A.nt) {
-      dn = A.dem[(size_t)(i + 1) * 4 + (lane & 3)];
-      if (fast) scn = lane < A.nsq ? A.sc[(size_t)(i + 1) * A.nsq + lane] : 0;
+
+  int s = 0;
+  while (s < A.nt) {
+    const int e = min(A.nt, s + OPP_R);
+    const int m = __builtin_amdgcn_readfirstlane(S.ctl[1]);
+    // ---- pass 1 (all waves): n_j = snapshot count - lost, for the range's tasks; each task's
+    // lost hosts stay in a register (lane l = the l-th; nlost > 64: rescanned in pass 3)
+    double t0[OPP_TB], t1[OPP_TB], t2[OPP_TB], t3[OPP_TB];
+    int scr[OPP_TB], lh[OPP_TB], nlost[OPP_TB];
+#pragma unroll
+    for (int t = 0; t < OPP_TB; t++) {
+      const int j = s + wave * OPP_TB + t;
+      const bool ok = j < e;
+      const double dv = ok ? A.dem[(size_t)j * 4 + (lane & 3)] : 0.0;
+      scr[t] = (ok && fast && lane < A.nsq) ? A.sc[(size_t)j * A.nsq + lane] : 0;
+      t0[t] = readlane_d(dv, 0); t1[t] = readlane_d(dv, 1);
+      t2[t] = readlane_d(dv, 2); t3[t] = readlane_d(dv, 3);
     }
+#pragma unroll
+    for (int t = 0; t < OPP_TB; t++) {
+      const int j = s + wave * OPP_TB + t;
+      lh[t] = -1;
+      nlost[t] = 0;
+      if (j < e) {
+        long long tot = 0;
+        if (fast) {
+          tot = __builtin_amdgcn_readlane(wave_incl_scan_dpp(scr[t]), 63);
+        } else {
+          for (int Q0 = 0; Q0 < A.nsq; Q0 += WAVE) {
+            const int Q = Q0 + lane;
+            tot += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)j * A.nsq + Q] : 0);
+          }
+        }
+        int nl = 0;
+        for (int q0 = 0; q0 < m; q0 += WAVE) {
+          int32_t th;
+          const uint64_t b = lost_piece(S, m, q0, t0[t], t1[t], t2[t], t3[t], th);
+          const int pos = nl + __popcll(b & below);
+          if (((b >> lane) & 1) && pos < WAVE) S.wl[wave][pos] = th;
+          nl += __popcll(b);
+        }
+        wave_lds_fence();
+        lh[t] = lane < nl ? S.wl[wave][lane] : -1;
+        nlost[t] = nl;
+        wave_lds_fence();
+        if (lane == 0) S.nspec[j - s] = (int)(tot - nl);
+      }
+    }
+    __syncthreads();
     OSTAMP(0);
-    // Touched hosts that fitted at the snapshot and no longer fit ("lost"), listed and counted
-    // per super-chunk with LDS atomics (4 x 64 touched hosts per loop trip).
-    // (the fences order the zeroing, the other lanes' atomics and the reads: without them the
-    // compiler may forward a lane's own zero store to its later read)
-    for (int Q = lane; Q < A.nsq; Q += WAVE) S.slost[Q] = 0;
-    wave_lds_fence();
-    int nl = 0;
-    for (int q0 = 0; q0 < m; q0 += 4 * WAVE) {
-      bool lf[4];
-      int32_t th[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int q = q0 + u * WAVE + lane;
-        const int qq = min(q, m - 1);
-        th[u] = S.tid[qq];
-        lf[u] = (q < m) &&
-                fits<false>(S.sa[0][qq], S.sa[1][qq], S.sa[2][qq], S.sa[3][qq], d0, d1, d2, d3) &&
-                !fits<false>(S.ta[0][qq], S.ta[1][qq], S.ta[2][qq], S.ta[3][qq], d0, d1, d2, d3);
+    // ---- pass 2 (wave 0): the draws, in task order, from the live state (saved first)
+    if (wave == 0) {
+      for (int i = lane; i < 625; i += WAVE) S.mtb[i] = S.mt[i];
+      wave_lds_fence();
+      MtWave mw;
+      mw.buf = 0; mw.used = 0; mw.limit = 0;
+      const int nsv = lane < e - s ? S.nspec[lane] : 0;
+      uint32_t kv = 0xffffffffu;
+      int cv = 0;
+      for (int j = 0; j < e - s; j++) {
+        const int n = __builtin_amdgcn_readlane(nsv, j);
+        if (n <= 0) continue;
+        int used = 0;
+        const uint32_t k = mt_randint_cnt(S.mt, mw, (uint32_t)n, used);
+        if (lane == j) { kv = k; cv = used; }
       }
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint64_t b = __ballot(lf[u]);
-        if (lf[u]) {
-          S.lost[nl + __popcll(b & below)] = th[u];
-          atomicAdd(&S.slost[th[u] / SUPH], 1);
-        }
-        nl += __popcll(b);
-      }
+      if (lane < e - s) { S.kdraw[lane] = kv; S.cnt[lane] = cv; }
+      mt_unbuffer(S.mt, mw);
     }
-    wave_lds_fence();
+    __syncthreads();
     OSTAMP(1);
-    long long n = 0;
-    if (fast) {
-      n = wave_sum_ll(scv);
-    } else {
-      for (int Q0 = 0; Q0 < A.nsq; Q0 += WAVE) {
+    // ---- pass 3 (all waves): super-chunk of k_j, its bitmaps, the OPP_C candidates from k_j on
+    int qsel[OPP_TB], ksel[OPP_TB];
+    uint64_t bits[OPP_TB][U];
+#pragma unroll
+    for (int t = 0; t < OPP_TB; t++) {
+      const int j = s + wave * OPP_TB + t;
+      qsel[t] = -1; ksel[t] = 0;
+#pragma unroll
+      for (int u = 0; u < U; u++) bits[t][u] = 0;
+      if (j >= e) continue;
+      const int n = __builtin_amdgcn_readfirstlane(S.nspec[j - s]);
+      if (n <= 0) continue;
+      const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.kdraw[j - s]);
+      int Qs = -1;
+      long long acc = 0;
+      for (int Q0 = 0; Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
         const int Q = Q0 + lane;
-        n += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)i * A.nsq + Q] : 0);
-      }
-    }
-    n -= nl;
-    if (n <= 0) continue;
-    const uint32_t k = mt_randint(S.mt, mw, (uint32_t)n);
-    OSTAMP(2);
-    // super-chunk
-    int Qs = -1;
-    long long acc = 0;
-    for (int Q0 = 0; Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
-      const int Q = Q0 + lane;
-      int v = 0;
-      if (Q < A.nsq) v = (fast ? scv : A.sc[(size_t)i * A.nsq + Q]) - S.slost[Q];
-      const int inc = wave_incl_scan(v);
-      const int tot = __builtin_amdgcn_readlane(inc, 63);
-      if ((long long)k < acc + tot) {
-        const uint64_t hit = __ballot(acc + inc > (long long)k);
-        const int L = __builtin_ctzll(hit);
-        Qs = Q0 + L;
-        acc += __builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(v, L);
-      } else {
-        acc += tot;
-      }
-    }
-    if (Qs < 0) continue;   // unreachable when counts are consistent
-    OSTAMP(3);
-    int k1 = (int)(k - (uint32_t)acc);
-    // chunk within the super-chunk: lane = chunk; its current bitmap is the snapshot bitmap
-    // minus the lost hosts, collected into per-chunk masks with LDS atomics
-    const int q = Qs * OPP_SUP + lane;
-    uint64_t bits[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) bits[u] = 0;
-    if (q < A.nq) {
-      const uint64_t* bp = A.bm + ((size_t)i * A.nq + q) * U;
-#pragma unroll
-      for (int u = 0; u < U; u++) bits[u] = bp[u];
-    }
-#pragma unroll
-    for (int u = 0; u < U; u++) S.lmask[lane][u] = 0;
-    wave_lds_fence();
-    for (int j = lane; j < nl; j += WAVE) {
-      const int h = S.lost[j];
-      if (h / SUPH == Qs) {
-        const int o = h % OPP_CH;
-        atomicOr((unsigned long long*)&S.lmask[(h / OPP_CH) % OPP_SUP][o / WAVE], 1ull << (o % WAVE));
-      }
-    }
-    wave_lds_fence();
-    int c = 0;
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      bits[u] &= ~S.lmask[lane][u];
-      c += __popcll(bits[u]);
-    }
-    const int inc = wave_incl_scan(c);
-    const uint64_t hit = __ballot(inc > k1);
-    if (hit == 0) continue;   // unreachable when counts are consistent
-    const int L = __builtin_ctzll(hit);
-    k1 -= __builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(c, L);
-    int off = -1;
-    if (lane == L) {
-      int r = k1;
-#pragma unroll
-      for (int u = 0; u < U; u++) {
-        const int cu = __popcll(bits[u]);
-        if (off < 0) {
-          if (r < cu) off = u * WAVE + select_bit(bits[u], r);
-          else r -= cu;
+        int v = 0;
+        if (Q < A.nsq) v = fast ? scr[t] : A.sc[(size_t)j * A.nsq + Q];
+        if (nlost[t] <= WAVE) {   // minus the lost hosts in super-chunk Q
+          for (int l = 0; l < nlost[t]; l++) v -= (__builtin_amdgcn_readlane(lh[t], l) / SUPH == Q);
+        } else {   // (rare) rescan, with the demand reloaded
+          const double dv = A.dem[(size_t)j * 4 + (lane & 3)];
+          const double f0 = readlane_d(dv, 0), f1 = readlane_d(dv, 1);
+          const double f2 = readlane_d(dv, 2), f3 = readlane_d(dv, 3);
+          for (int p0 = 0; p0 < m; p0 += WAVE) {
+            int32_t th;
+            uint64_t b = lost_piece(S, m, p0, f0, f1, f2, f3, th);
+            while (b) {
+              const int l = __builtin_ctzll(b);
+              b &= b - 1;
+              v -= (__builtin_amdgcn_readlane(th, l) / SUPH == Q);
+            }
+          }
+        }
+        const int inc = wave_incl_scan_dpp(v);
+        const int tot = __builtin_amdgcn_readlane(inc, 63);
+        if ((long long)k < acc + tot) {
+          const uint64_t hit = __ballot(acc + inc > (long long)k);
+          const int L = __builtin_ctzll(hit);
+          Qs = Q0 + L;
+          acc += __builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(v, L);
+        } else {
+          acc += tot;
         }
       }
-    }
-    off = __builtin_amdgcn_readlane(off, L);
-    const int w = (Qs * OPP_SUP + L) * OPP_CH + off;
-    OSTAMP(4);
-    int ws = ohash_find(S, w);
-    ws = __builtin_amdgcn_readfirstlane(ws);
-    double w0, w1, w2, w3;
-    if (ws >= 0) {
-      w0 = S.ta[0][ws]; w1 = S.ta[1][ws]; w2 = S.ta[2][ws]; w3 = S.ta[3][ws];
-    } else {   // lanes 0-3 load the four resources (vector loads)
-      const double av = A.avail[(size_t)(lane & 3) * A.H + w];
-      w0 = readlane_d(av, 0); w1 = readlane_d(av, 1); w2 = readlane_d(av, 2); w3 = readlane_d(av, 3);
+      if (Qs < 0) continue;   // unreachable when counts are consistent (no candidates)
+      qsel[t] = Qs;
+      ksel[t] = (int)(k - (uint32_t)acc);
+      const int q = Qs * OPP_SUP + lane;   // lane = chunk of the super-chunk
+      if (q < A.nq) {
+        const uint64_t* bp = A.bm + ((size_t)j * A.nq + q) * U;
+#pragma unroll
+        for (int u = 0; u < U; u++) bits[t][u] = bp[u];
+      }
     }
     OSTAMP(5);
-    const double n0 = w0 - d0, n1 = w1 - d1, n2 = w2 - d2, n3 = w3 - d3;
-    if (ws < 0) {
-      ws = m++;
-      if (lane == 0) {
-        ohash_put(S, w, ws);
-        S.tid[ws] = w;
-        S.sa[0][ws] = w0; S.sa[1][ws] = w1; S.sa[2][ws] = w2; S.sa[3][ws] = w3;
-        S.sb[0][ws] = w0; S.sb[1][ws] = w1; S.sb[2][ws] = w2; S.sb[3][ws] = w3;
+#pragma unroll
+    for (int t = 0; t < OPP_TB; t++) {
+      const int j = s + wave * OPP_TB + t;
+      if (j >= e) continue;
+      int cc = 0;
+      const int Qs = qsel[t];
+      if (Qs >= 0) {
+        // current bitmaps: the snapshot's minus the lost hosts of this super-chunk
+        auto clear = [&](int h) {
+          if (h / SUPH == Qs && (h / OPP_CH) % OPP_SUP == lane) {
+            const int o = h % OPP_CH;
+#pragma unroll
+            for (int u = 0; u < U; u++)
+              if (o / WAVE == u) bits[t][u] &= ~(1ull << (o % WAVE));
+          }
+        };
+        if (nlost[t] <= WAVE) {
+          for (int l = 0; l < nlost[t]; l++) clear(__builtin_amdgcn_readlane(lh[t], l));
+        } else {
+          const double dv = A.dem[(size_t)j * 4 + (lane & 3)];
+          const double f0 = readlane_d(dv, 0), f1 = readlane_d(dv, 1);
+          const double f2 = readlane_d(dv, 2), f3 = readlane_d(dv, 3);
+          for (int p0 = 0; p0 < m; p0 += WAVE) {
+            int32_t th;
+            uint64_t b = lost_piece(S, m, p0, f0, f1, f2, f3, th);
+            while (b) {
+              const int l = __builtin_ctzll(b);
+              b &= b - 1;
+              clear(__builtin_amdgcn_readlane(th, l));
+            }
+          }
+        }
+        int c = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++) c += __popcll(bits[t][u]);
+        const int inc = wave_incl_scan_dpp(c);
+        int k1 = ksel[t];
+        const uint64_t hit = __ballot(inc > k1);
+        if (hit) {
+          const int L = __builtin_ctzll(hit);
+          k1 -= __builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(c, L);
+          int off = -1;
+          if (lane == L) {
+            int r = k1;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+              const int cu = __popcll(bits[t][u]);
+              if (off < 0) {
+                if (r < cu) off = u * WAVE + select_bit(bits[t][u], r);
+                else r -= cu;
+              }
+            }
+          }
+          off = __builtin_amdgcn_readlane(off, L);
+          // hosts from (chunk L, bit off) on, in host order: the first OPP_C are the candidates
+          uint64_t kb[U];
+          int c2 = 0;
+#pragma unroll
+          for (int u = 0; u < U; u++) {
+            const int lo = u * WAVE;
+            uint64_t keep;
+            if (lane < L) keep = 0;
+            else if (lane > L) keep = ~0ull;
+            else keep = off >= lo + WAVE ? 0ull : (off <= lo ? ~0ull : (~0ull << (off - lo)));
+            kb[u] = bits[t][u] & keep;
+            c2 += __popcll(kb[u]);
+          }
+          const int inc2 = wave_incl_scan_dpp(c2);
+          cc = min(OPP_C, __builtin_amdgcn_readlane(inc2, 63));
+          int slot = inc2 - c2;
+          if (slot < OPP_C) {
+            const int base = (Qs * OPP_SUP + lane) * OPP_CH;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+              uint64_t x = kb[u];
+              while (x && slot < OPP_C) {
+                const int b = __builtin_ctzll(x);
+                x &= x - 1;
+                S.cand[j - s][slot++] = base + u * WAVE + b;
+              }
+            }
+          }
+        }
+      }
+      if (lane == 0) S.ccount[j - s] = cc;
+    }
+    wave_lds_fence();
+    OSTAMP(6);
+    // candidates' capacity at the range start: lane = (candidate lane / 4, resource lane % 4);
+    // touched hosts from the table, the others from HBM (the walk has not written them)
+    double cv[OPP_TB];
+    const int cx = lane >> 2, cr = lane & 3;
+#pragma unroll
+    for (int t = 0; t < OPP_TB; t++) {
+      const int j = s + wave * OPP_TB + t;
+      cv[t] = 0.0;
+      if (j < e && cx < S.ccount[j - s]) cv[t] = A.avail[(size_t)cr * A.H + S.cand[j - s][cx]];
+    }
+#pragma unroll
+    for (int t = 0; t < OPP_TB; t++) {
+      const int j = s + wave * OPP_TB + t;
+      if (j < e && cx < S.ccount[j - s]) {
+        const int ws = ohash_find(S, S.cand[j - s][cx]);
+        S.cav[j - s][cr][cx] = ws >= 0 ? S.ta[cr][ws] : cv[t];
       }
     }
-    // commit in LDS only: a global store here would put its round trip on the next task (the
-    // next task's prefetched loads share the in-order vmcnt counter with it)
-    if (lane == 0) {
-      S.ta[0][ws] = n0; S.ta[1][ws] = n1; S.ta[2][ws] = n2; S.ta[3][ws] = n3;
-      S.own[ws] = 1;
-      S.pl[i] = w;
+    __syncthreads();
+    OSTAMP(2);
+    // ---- pass 4 (wave 0): walk the range. Lane l holds range task s + l: its demand, draw,
+    // candidates, the capacity of its first candidate c_0 now (z) and after taking it (y), the
+    // candidates that stopped fitting (lm), the lost hosts below c_0 (mm) and its new-lost count
+    // (nnew). A task no commit of this range has affected (nnew == 0) takes c_0 from its lane's
+    // registers; the others verify their draw and select among their candidates. Nothing is
+    // written to the touched table until the range ends.
+    if (wave == 0) {
+      const int R = e - s;
+      const bool mine = lane < R;
+      double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0, z0 = 0.0, z1 = 0.0, z2 = 0.0, z3 = 0.0;
+      int nsv = 0, ccv = 0;
+      uint32_t kv = 0;
+      int cd[OPP_C];
+#pragma unroll
+      for (int x = 0; x < OPP_C; x++) cd[x] = 0x7fffffff;
+      if (mine) {
+        const double* dp = A.dem + (size_t)(s + lane) * 4;
+        e0 = dp[0]; e1 = dp[1]; e2 = dp[2]; e3 = dp[3];
+        nsv = S.nspec[lane];
+        kv = S.kdraw[lane];
+        ccv = nsv > 0 ? S.ccount[lane] : 0;
+#pragma unroll
+        for (int x = 0; x < OPP_C; x++)
+          if (x < ccv) cd[x] = S.cand[lane][x];
+        if (ccv > 0) { z0 = S.cav[lane][0][0]; z1 = S.cav[lane][1][0]; z2 = S.cav[lane][2][0]; z3 = S.cav[lane][3][0]; }
+      }
+      const int c0l = cd[0];
+      double y0 = z0 - e0, y1 = z1 - e1, y2 = z2 - e2, y3 = z3 - e3;
+      // (a task with feasible hosts but no candidates cannot happen when the counts are
+      // consistent; nnew = 1 sends it to the slow path, which stops there)
+      int nnew = (nsv > 0 && ccv == 0) ? 1 : 0, mm = 0;
+      uint32_t lm = 0;
+      int rch = -1;   // commit of a task that took the slow path, with capacities after / before
+      double ra0 = 0.0, ra1 = 0.0, ra2 = 0.0, ra3 = 0.0, rb0 = 0.0, rb1 = 0.0, rb2 = 0.0, rb3 = 0.0;
+      uint64_t fcm = 0;   // tasks that took c_0 on the fast path (commit = c0l, z -> y)
+      int stop = e;
+      for (int i = s; i < e; i++) {
+        const int L = i - s;
+        const int n = __builtin_amdgcn_readlane(nsv, L);
+        if (n <= 0) continue;   // no feasible host at s: none now (capacities only decrease)
+        const int nn = __builtin_amdgcn_readlane(nnew, L);
+        int w;
+        double w0, w1, w2, w3, n0, n1, n2, n3;
+        if (nn == 0) {
+          w = __builtin_amdgcn_readlane(c0l, L);
+          w0 = readlane_d(z0, L); w1 = readlane_d(z1, L); w2 = readlane_d(z2, L); w3 = readlane_d(z3, L);
+          n0 = readlane_d(y0, L); n1 = readlane_d(y1, L); n2 = readlane_d(y2, L); n3 = readlane_d(y3, L);
+          fcm |= 1ull << L;
+        } else {
+          const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)kv, L);
+          const int ntrue = n - nn;
+          if (ntrue <= 0 || rint_mask((uint32_t)(ntrue - 1)) != rint_mask((uint32_t)(n - 1)) ||
+              k > (uint32_t)(ntrue - 1)) {
+            stop = i;
+            break;
+          }
+          const int cc = __builtin_amdgcn_readlane(ccv, L);
+          const int mi = __builtin_amdgcn_readlane(mm, L);
+          const uint32_t valid = ((1u << cc) - 1u) & ~(uint32_t)__builtin_amdgcn_readlane((int)lm, L);
+          if (__popc(valid) <= mi) {   // the answer lies beyond the candidates
+            stop = i;
+            break;
+          }
+          const int xs = select_bit(valid, mi);
+          if (xs == 0) {   // c_0 at its current capacity
+            w = __builtin_amdgcn_readlane(c0l, L);
+            w0 = readlane_d(z0, L); w1 = readlane_d(z1, L); w2 = readlane_d(z2, L); w3 = readlane_d(z3, L);
+          } else {         // range-start capacity, unless committed earlier in this range
+            w = __builtin_amdgcn_readfirstlane(S.cand[L][xs]);
+            w0 = S.cav[L][0][xs]; w1 = S.cav[L][1][xs]; w2 = S.cav[L][2][xs]; w3 = S.cav[L][3][xs];
+            const bool fl = (fcm >> lane) & 1;
+            const uint64_t hit = __ballot((fl ? c0l : rch) == w);
+            if (hit) {
+              const int l = 63 - __builtin_clzll(hit);
+              const bool f = (fcm >> l) & 1;
+              w0 = f ? readlane_d(y0, l) : readlane_d(ra0, l);
+              w1 = f ? readlane_d(y1, l) : readlane_d(ra1, l);
+              w2 = f ? readlane_d(y2, l) : readlane_d(ra2, l);
+              w3 = f ? readlane_d(y3, l) : readlane_d(ra3, l);
+            }
+          }
+          n0 = w0 - readlane_d(e0, L); n1 = w1 - readlane_d(e1, L);
+          n2 = w2 - readlane_d(e2, L); n3 = w3 - readlane_d(e3, L);
+          if (lane == L) {
+            rch = w;
+            ra0 = n0; ra1 = n1; ra2 = n2; ra3 = n3;
+            rb0 = w0; rb1 = w1; rb2 = w2; rb3 = w3;
+          }
+        }
+        // the later tasks of the range: does this commit take w away from them?
+        const bool act = lane > L && mine;
+        const bool lost = act & fits<false>(w0, w1, w2, w3, e0, e1, e2, e3) &
+                          !fits<false>(n0, n1, n2, n3, e0, e1, e2, e3);
+        nnew += lost;
+        mm += lost & (w < c0l);
+        if (__ballot(lost & (w >= c0l))) {
+#pragma unroll
+          for (int x = 0; x < OPP_C; x++) lm |= ((lost & (cd[x] == w)) ? 1u : 0u) << x;
+        }
+        if (__ballot(act & (c0l == w))) {   // their c_0 was taken: its capacity now
+          if (act & (c0l == w)) {
+            z0 = n0; z1 = n1; z2 = n2; z3 = n3;
+            y0 = n0 - e0; y1 = n1 - e1; y2 = n2 - e2; y3 = n3 - e3;
+          }
+        }
+      }
+      if ((fcm >> lane) & 1) {   // fast-path commits: c_0, capacity z before, y after
+        rch = c0l;
+        ra0 = y0; ra1 = y1; ra2 = y2; ra3 = y3;
+        rb0 = z0; rb1 = z1; rb2 = z2; rb3 = z3;
+      }
+      // A range whose first task fails cannot happen when the counts are consistent (its state
+      // is exact); leave that task unplaced rather than loop.
+      if (stop == s) stop = s + 1;
+      // the range's commits: placements, then the touched table (first commit of a host
+      // creates or keeps its entry with the capacity before it; its last commit sets ta)
+      const int done = stop - s;
+      if (lane >= done) rch = -1;
+      if (rch >= 0) S.pl[s + lane] = rch;
+      bool first = rch >= 0, last = rch >= 0;
+      for (int l = 0; l < done; l++) {
+        const int h = __builtin_amdgcn_readlane(rch, l);
+        if (h >= 0 && h == rch) {
+          first = first && !(l < lane);
+          last = last && !(l > lane);
+        }
+      }
+      int ws = first ? ohash_find(S, rch) : -1;
+      const bool fresh = first && ws < 0;
+      const uint64_t fb = __ballot(fresh);
+      if (fresh) {
+        ws = m + __popcll(fb & below);
+        S.tid[ws] = rch;
+        S.sa[0][ws] = rb0; S.sa[1][ws] = rb1; S.sa[2][ws] = rb2; S.sa[3][ws] = rb3;
+        S.sb[0][ws] = rb0; S.sb[1][ws] = rb1; S.sb[2][ws] = rb2; S.sb[3][ws] = rb3;
+        uint32_t p = ohslot(rch);
+        while (atomicCAS(&S.hkey[p], -1, rch) != -1) p = (p + 1) & (OPP_HASH - 1);
+        S.hval[p] = ws;
+      }
+      wave_lds_fence();
+      if (last) {
+        const int wl = ohash_find(S, rch);
+        S.ta[0][wl] = ra0; S.ta[1][wl] = ra1; S.ta[2][wl] = ra2; S.ta[3][wl] = ra3;
+        S.own[wl] = 1;
+      }
+      if (lane == 0) { S.ctl[0] = stop; S.ctl[1] = m + __popcll(fb); }
+      if (stop < e) {   // next range at stop: the MT19937 state after the draws of [s, stop)
+        wave_lds_fence();
+        int skip = 0;
+        for (int i = s; i < stop; i++) skip += __builtin_amdgcn_readfirstlane(S.cnt[i - s]);
+        for (int i = lane; i < 625; i += WAVE) S.mt[i] = S.mtb[i];
+        wave_lds_fence();
+        MtWave mw;
+        mw.buf = 0; mw.used = 0; mw.limit = 0;
+        for (int q = 0; q < skip; q++) (void)mt_next(S.mt, mw);
+        mt_unbuffer(S.mt, mw);
+      }
     }
+    __syncthreads();
+    OSTAMP(3);
+#ifdef PVT_STAMPS
+    ph[4] += 1;
+#endif
+    s = S.ctl[0];
   }
   // the window's commits (hosts this walk touched): to global availability, or handed to the
   // next walk, which applies them once the next count pass (running now) has read the old state
-  __builtin_amdgcn_s_waitcnt(0xc07f);
-  int no = 0;
-  for (int q0 = 0; q0 < m; q0 += WAVE) {
-    const int q = q0 + lane;
-    const bool own = q < m && S.own[q];
-    const uint64_t b = __ballot(own);
-    if (own) {
-      const int32_t h = S.tid[q];
-      if (A.writeback)
-        for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + h] = S.ta[r][q];
-      if (A.out) {
-        const int o = no + __popcll(b & below);
-        A.out->tid[o] = h;
-        for (int r = 0; r < 4; r++) { A.out->sb[r][o] = S.sb[r][q]; A.out->ta[r][o] = S.ta[r][q]; }
+  if (wave == 0) {
+    const int m = __builtin_amdgcn_readfirstlane(S.ctl[1]);
+    int no = 0;
+    for (int q0 = 0; q0 < m; q0 += WAVE) {
+      const int q = q0 + lane;
+      const bool own = q < m && S.own[q];
+      const uint64_t b = __ballot(own);
+      if (own) {
+        const int32_t h = S.tid[q];
+        if (A.writeback)
+          for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + h] = S.ta[r][q];
+        if (A.out) {
+          const int o = no + __popcll(b & below);
+          A.out->tid[o] = h;
+          for (int r = 0; r < 4; r++) { A.out->sb[r][o] = S.sb[r][q]; A.out->ta[r][o] = S.ta[r][q]; }
+        }
       }
+      no += __popcll(b);
     }
-    no += __popcll(b);
+    if (A.out && lane == 0) A.out->n = no;
   }
-  if (A.out && lane == 0) A.out->n = no;
-  for (int i = lane; i < A.nt; i += WAVE) A.placement[i] = S.pl[i];
-  mt_unbuffer(S.mt, mw);
-  for (int i = lane; i < 625; i += WAVE) A.mt[i] = S.mt[i];
+  for (int i = tx; i < A.nt; i += NT) A.placement[i] = S.pl[i];
+  for (int i = tx; i < 625; i += NT) A.mt[i] = S.mt[i];
 #ifdef PVT_STAMPS
-  if (lane == 0 && A.stamps) {
+  if (tx == 0 && A.stamps) {
     for (int k = 0; k < 7; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
     atomicAdd((unsigned long long*)&A.stamps[7], (unsigned long long)A.nt);
   }
@@ -416,7 +753,7 @@ hipError_t opp_init_attrs() {
 }
 
 void launch_opp_commit(const OppCommitArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(opp_commit_kernel, dim3(1), dim3(64), sizeof(OppLDS), st, a);
+  hipLaunchKernelGGL(opp_commit_kernel, dim3(1), dim3(OPP_NW * WAVE), sizeof(OppLDS), st, a);
 }
 
 // Rank packages -> full tables: package r holds, task-major, the chunk bitmaps ([nt][ldq][4]

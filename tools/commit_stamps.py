@@ -26,12 +26,17 @@ eng.run(dr)
 torch.cuda.synchronize()
 assert f(eng.ctx, buf, 8) == 0
 if mode == 2:
-    names = ["prefetch/decode", "lost-scan", "count+draw", "super-select", "chunk-select",
-             "host-avail", "commit"]
-    tot = sum(buf[k] for k in range(7))
-    print("opportunistic H=%d T=%d tasks=%d stats=%s" % (H, T, buf[7], eng.last_stats()))
-    for k in range(7):
-        print("  %-16s %6.1f%%  %8.0f cycles/task" % (names[k], 100.0 * buf[k] / tot, buf[k] / max(buf[7], 1)))
+    # speculative range walk (pvt_opp.hip): counts per range, draws, candidates, verified walk
+    names = ["pass1-counts", "pass2-draws", "pass3-candidates", "pass4-walk"]
+    sub = {5: "  pass3a-select+load", 6: "  pass3b-candidates", 2: "  pass3c-capacities"}
+    tot = sum(buf[k] for k in range(4))
+    print("opportunistic H=%d T=%d tasks=%d ranges=%d stats=%s"
+          % (H, T, buf[7], buf[4], eng.last_stats()))
+    for k in range(4):
+        print("  %-16s %6.1f%%  %8.0f cycles/task" % (names[k], 100.0 * buf[k] / max(tot, 1),
+                                                      buf[k] / max(buf[7], 1)))
+    for k in (5, 6, 2):   # pass 3 split (stamp 2 then holds only its last part)
+        print("  %-20s %8.0f cycles/task" % (sub[k], buf[k] / max(buf[7], 1)))
     sys.exit(0)
 names = ["wait-prefetch", "hash-lookup", "untouched-pick", "touched-rescore", "commit"]
 tot = sum(buf[k] for k in range(5))
