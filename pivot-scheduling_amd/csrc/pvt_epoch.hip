@@ -42,7 +42,7 @@ __device__ __forceinline__ int seg_adv(const EpochArgs& A, int j) {
 // chains' segments) 256 at a time in LDS -- host, capacities, and the zone-table (or realtime)
 // c and bw for j's anchor, which every task of j shares -- so the pair checks are LDS broadcasts
 // only. Slices split each segment's checks over VAL_SPLIT blocks.
-constexpr int VAL_SPLIT = 8;
+constexpr int VAL_SPLIT = 32;
 __device__ __forceinline__ int seg_of(const EpochArgs& A, int e) {
   int lo = 0, hi = A.nseg - 1;                // the segment holding window task e
   while (lo < hi) {
@@ -109,7 +109,8 @@ __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
         if (h < 0) continue;
         const double f0 = e_a[0][k], f1 = e_a[1][k], f2 = e_a[2][k], f3 = e_a[3][k];
         bool hit = (h == w.id);
-        if (!hit && fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) {
+        // a winner scoring +0 is beaten only by a host of lower index scoring +0
+        if (!hit && (w1 != 0ull || h < w.id) && fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) {
           const double s2 = norm2_seq(f0 - d0, f1 - d1, f2 - d2, f3 - d3);
           const double c = e_c[k], bw = e_b[k];
           if (c == 0.0) {
@@ -133,21 +134,38 @@ __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
 }
 
 // Finality of the log entries: per segment, an entry is its host's final state unless a later
-// walked task of the same segment committed to the same host (sup = 1). One block per segment,
-// its walked hosts staged in LDS (a segment never exceeds CHAIN_MAX tasks).
-__global__ __launch_bounds__(256) void epoch_final_kernel(EpochArgs A) {
-  __shared__ int32_t ids[CHAIN_MAX];
+// walked task of the same segment committed to the same host (sup = 1). One block per segment:
+// every walked entry records its index in an LDS hash keyed by host (atomicMax: the host's last
+// entry), then an entry is final iff it is its host's last. (A segment never exceeds CHAIN_MAX
+// tasks; 2 x CHAIN_MAX slots. The pairwise scan it replaces was O(n^2): 70 us per config-5
+// epoch.)
+constexpr int FIN_SLOTS = 2 * CHAIN_MAX;
+__device__ __forceinline__ int fin_slot(int32_t h, const int32_t* hk) {
+  uint32_t p = ((uint32_t)h * 2654435761u) & (FIN_SLOTS - 1);
+  while (hk[p] != h) p = (p + 1) & (FIN_SLOTS - 1);
+  return (int)p;
+}
+__global__ __launch_bounds__(1024) void epoch_final_kernel(EpochArgs A) {
+  __shared__ int32_t hk[FIN_SLOTS], hv[FIN_SLOTS];
   const int j = blockIdx.x, tid = threadIdx.x;
   const int s0 = A.seg_off[j], n = seg_adv(A, j);
-  for (int k = tid; k < n; k += 256) ids[k] = A.wlog[s0 + k].id;
+  for (int q = tid; q < FIN_SLOTS; q += blockDim.x) { hk[q] = -1; hv[q] = -1; }
   __syncthreads();
-  for (int k = tid; k < n; k += 256) {
-    const int32_t h = ids[k];
-    int sup = 0;
-    if (h >= 0)
-      for (int m = k + 1; m < n; m++)
-        if (ids[m] == h) { sup = 1; break; }
-    A.wlog[s0 + k].sup = sup;
+  for (int k = tid; k < n; k += blockDim.x) {
+    const int32_t h = A.wlog[s0 + k].id;
+    if (h < 0) continue;
+    uint32_t p = ((uint32_t)h * 2654435761u) & (FIN_SLOTS - 1);
+    for (;;) {
+      const int32_t o = atomicCAS(&hk[p], -1, h);
+      if (o == -1 || o == h) break;
+      p = (p + 1) & (FIN_SLOTS - 1);
+    }
+    atomicMax(&hv[p], k);
+  }
+  __syncthreads();
+  for (int k = tid; k < n; k += blockDim.x) {
+    const int32_t h = A.wlog[s0 + k].id;
+    A.wlog[s0 + k].sup = (h >= 0 && hv[fin_slot(h, hk)] != k) ? 1 : 0;
   }
 }
 
@@ -170,7 +188,7 @@ __global__ __launch_bounds__(256) void epoch_apply_kernel(EpochArgs A, int n_acc
 }
 
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
   const int tiles = (CHAIN_MAX + 255) / 256;   // a segment never exceeds its chain's cap
   hipLaunchKernelGGL(epoch_validate_kernel, dim3(tiles, a.nseg, VAL_SPLIT), dim3(256), 0, st, a);
 }

@@ -261,6 +261,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     rid = S.wid[q];
     rvalid = __ballot(p < nwin);
     dirty = false;
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // loads landed here, so the hot loop carries no wait
   };
   auto store_chunk = [&](int c) {
     const int p = c * 64 + lane;
@@ -299,6 +300,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           if (c == p0) rzm = m;
         }
         cur = a;
+        __builtin_amdgcn_s_waitcnt(0xc07f);
 #ifdef PVT_STAMPS
         n_switch++;
 #endif
@@ -315,58 +317,74 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         }
         return k0;
       };
-      bool found = false;
-      for (;;) {                               // the register chunk (advancing past dead ones)
+      // Hot path, straight-line: the register chunk holds a fitting zero-cost host and every
+      // fitting host of it is zero-cost for this anchor. The fit test is the minimum residual:
+      // every window capacity and chain demand is finite with |x| <= 2^500 (certificate 3), so
+      // a - d is exact in sign (a >= d iff a - d >= +-0) and is the capacity after a commit.
+      double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
+      uint64_t fm = __ballot(fmin(fmin(n0, n1), fmin(n2, n3)) >= 0.0) & rvalid;
+      uint64_t m = fm & rzm;
+      bool found = true;
 #ifdef PVT_STAMPS
-        n_chunks++;
+      n_chunks++;
 #endif
-        const bool f = ((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, d0, d1, d2, d3);
-        const bool k0 = zero_exact(f, (rzm >> lane) & 1ull, ra0, ra1, ra2, ra3,
-                                   min(p0 * 64 + lane, nwin - 1));
-        const uint64_t m = __ballot(f && k0);
-        if (m) {
-          // commit: resc[h] -= t_demand (cost_aware.py:95), by the lowest such lane, which logs
-          if (lane == __builtin_ctzll(m)) {
-            ra0 -= d0; ra1 -= d1; ra2 -= d2; ra3 -= d3;
-            S.lg[k][0] = ra0; S.lg[k][1] = ra1; S.lg[k][2] = ra2; S.lg[k][3] = ra3;
-            S.lgid[k] = rid;
-          }
-          dirty = true;
-          found = true;
-          break;
+      if (__builtin_expect(m == 0 || (fm & ~rzm) != 0, 0)) {
+        found = false;
+        for (int pass = 0;; pass++) {          // the register chunk (advancing past dead ones)
+#ifdef PVT_STAMPS
+          n_chunks += pass > 0;
+#endif
+          if (fm & ~rzm)                       // fitting hosts of U outside the anchor's
+            m = __ballot(zero_exact((fm >> lane) & 1ull, (rzm >> lane) & 1ull, ra0, ra1, ra2,
+                                    ra3, min(p0 * 64 + lane, nwin - 1))) & fm;   // zero-cost zones
+          if (m) { found = true; break; }
+          if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
+            break;                             // chunk p0 still useful: look further in LDS
+          store_chunk(p0);                     // dead: move the register chunk on
+          if (++p0 >= nch) break;
+          rzm = S.zm[p0];
+          load_chunk(p0);
+          n0 = ra0 - d0; n1 = ra1 - d1; n2 = ra2 - d2; n3 = ra3 - d3;
+          fm = __ballot(fmin(fmin(n0, n1), fmin(n2, n3)) >= 0.0) & rvalid;
+          m = fm & rzm;
         }
-        if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
-          break;                               // chunk p0 still useful: look further in LDS
-        store_chunk(p0);                       // dead: move the register chunk on
-        if (++p0 >= nch) break;
-        load_chunk(p0);
-        rzm = S.zm[p0];
-      }
-      if (!found && p0 < nch) {
-        store_chunk(p0);
-        for (int c = p0 + 1; c < nch; c++) {
+        if (!found && p0 < nch) {
+          store_chunk(p0);
+          for (int c = p0 + 1; c < nch; c++) {
 #ifdef PVT_STAMPS
-          n_chunks++;
+            n_chunks++;
 #endif
-          const int p = c * 64 + lane;
-          const int q = min(p, nwin - 1);
-          const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
-          const int32_t id = S.wid[q];
-          const uint64_t zm = S.zm[c];
-          const bool f = p < nwin && fits<false>(a0, a1, a2, a3, d0, d1, d2, d3);
-          const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
-          const uint64_t m = __ballot(f && k0);
-          if (m) {
-            if (lane == __builtin_ctzll(m)) {
-              const double n0 = a0 - d0, n1 = a1 - d1, n2 = a2 - d2, n3 = a3 - d3;
-              S.wa[0][q] = n0; S.wa[1][q] = n1; S.wa[2][q] = n2; S.wa[3][q] = n3;
-              S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
-              S.lgid[k] = id;
+            const int p = c * 64 + lane;
+            const int q = min(p, nwin - 1);
+            const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
+            const int32_t id = S.wid[q];
+            const uint64_t zm = S.zm[c];
+            const bool f = p < nwin && fits<false>(a0, a1, a2, a3, d0, d1, d2, d3);
+            const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
+            const uint64_t mc = __ballot(f && k0);
+            if (mc) {
+              if (lane == __builtin_ctzll(mc)) {
+                const double c0 = a0 - d0, c1 = a1 - d1, c2 = a2 - d2, c3 = a3 - d3;
+                S.wa[0][q] = c0; S.wa[1][q] = c1; S.wa[2][q] = c2; S.wa[3][q] = c3;
+                S.lg[k][0] = c0; S.lg[k][1] = c1; S.lg[k][2] = c2; S.lg[k][3] = c3;
+                S.lgid[k] = id;
+              }
+              found = true;
+              m = 0;                           // committed here, not in the register chunk
+              break;
             }
-            found = true;
-            break;
           }
         }
+      }
+      if (m) {
+        // commit: resc[h] -= t_demand (cost_aware.py:95) on the lowest such lane, which logs
+        const bool win = lane == __builtin_ctzll(m);
+        ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
+        if (win) {
+          S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
+          S.lgid[k] = rid;
+        }
+        dirty = true;
       }
       if (!found) { failed = true; break; }  // certificate 1 fails: the list walk decides
       done++;
