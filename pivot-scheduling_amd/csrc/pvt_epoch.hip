@@ -53,12 +53,35 @@ __device__ __forceinline__ int seg_of(const EpochArgs& A, int e) {
   return lo;
 }
 
+// Pair check of task t (demand d, winner w with score bits w1) against log entry k.
+__device__ __forceinline__ bool beats(int32_t h, double f0, double f1, double f2, double f3,
+                                      double c, double bw, double d0, double d1, double d2,
+                                      double d3, const WinRec& w, uint64_t w1) {
+  if (h == w.id) return true;
+  // a winner scoring +0 is beaten only by a host of lower index scoring +0
+  if ((w1 == 0ull && h > w.id) || !fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) return false;
+  const double s2 = norm2_seq(f0 - d0, f1 - d1, f2 - d2, f3 - d3);
+  if (c == 0.0)   // zero egress cost: the score is exactly +0 (finite s2, bw > 0)
+    return (0ull < w1) | ((0ull == w1) & (h < w.id));
+  if (w1 == 0ull && s2 >= 0x1p-600 && c >= 0x1p-300 && bw <= 0x1p300)
+    return false;   // c * sqrt(s2) >= 2^-600 and / bw >= 2^-900: the score is > 0
+  const double sc = (c * __builtin_sqrt(s2)) / bw;
+  const uint64_t k1 = (uint64_t)__double_as_longlong(sc);
+  return (k1 < w1) | ((k1 == w1) & (h < w.id));
+}
+
+constexpr int VAL_HASH = 512;
+
 __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
   __shared__ int32_t e_id[256];
   __shared__ double e_a[4][256];
   __shared__ double e_c[256], e_b[256];
+  __shared__ int32_t e_full[256];             // entries that need the pair check
+  __shared__ int32_t hk[VAL_HASH];            // hosts of the others ("id-only" entries)
+  __shared__ double wmx[4][4];
+  __shared__ int32_t wfull[4];
   __shared__ int32_t stop;
-  const int j = blockIdx.y, tid = threadIdx.x;
+  const int j = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (j == 0 || j >= A.nseg) return;
   const int s0 = A.seg_off[j], adv = seg_adv(A, j);
   if ((int)blockIdx.x * 256 >= adv) return;
@@ -81,50 +104,89 @@ __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
     d2 = A.dem[(size_t)t * 4 + 2]; d3 = A.dem[(size_t)t * 4 + 3];
   }
   const uint64_t w1 = (uint64_t)__double_as_longlong(w.s);
+  // The block's largest demand per dimension. An entry with c >= 2^-300, bw <= 2^300 whose
+  // capacity exceeds it by 2^-287 in some dimension has s2 >= 2^-576 against every task here,
+  // so its score is > 0: against a winner scoring +0 only host identity matters (LDS hash).
+  double x0 = active ? d0 : -DINF, x1 = active ? d1 : -DINF;
+  double x2 = active ? d2 : -DINF, x3 = active ? d3 : -DINF;
+  for (int off = 32; off > 0; off >>= 1) {
+    x0 = fmax(x0, __shfl_xor(x0, off)); x1 = fmax(x1, __shfl_xor(x1, off));
+    x2 = fmax(x2, __shfl_xor(x2, off)); x3 = fmax(x3, __shfl_xor(x3, off));
+  }
+  if (lane == 0) { wmx[wave][0] = x0; wmx[wave][1] = x1; wmx[wave][2] = x2; wmx[wave][3] = x3; }
   if (tid == 0) stop = __hip_atomic_load(&A.bad[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  double mx[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) mx[r] = fmax(fmax(wmx[0][r], wmx[1][r]), fmax(wmx[2][r], wmx[3][r]));
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   bool beaten = false;
   for (int c0 = lo; c0 < hi && !stop; c0 += 256) {
     const int e = c0 + tid;
     int32_t id = -1;
+    bool idonly = false;
     if (e < hi) {
       const int s = seg_of(A, e);
       if (A.seg_chain[s] != cj && e - A.seg_off[s] < seg_adv(A, s)) {
         const WinRec& x = A.wlog[e];
         if (x.id >= 0 && !x.sup) {
           id = x.id;
-          e_a[0][tid] = x.a[0]; e_a[1][tid] = x.a[1]; e_a[2][tid] = x.a[2]; e_a[3][tid] = x.a[3];
+          const double f0 = x.a[0], f1 = x.a[1], f2 = x.a[2], f3 = x.a[3];
+          e_a[0][tid] = f0; e_a[1][tid] = f1; e_a[2][tid] = f2; e_a[3][tid] = f3;
           const int z = A.zone[id];
-          e_c[tid] = A.csum[a * A.Z + z];
-          e_b[tid] = rtrow ? rtrow[id] : A.bsum[a * A.Z + z];
+          const double c = A.csum[a * A.Z + z];
+          const double bw = rtrow ? rtrow[id] : A.bsum[a * A.Z + z];
+          e_c[tid] = c;
+          e_b[tid] = bw;
+          idonly = c >= 0x1p-300 && bw <= 0x1p300 &&
+                   (f0 - mx[0] >= 0x1p-287 || f1 - mx[1] >= 0x1p-287 ||
+                    f2 - mx[2] >= 0x1p-287 || f3 - mx[3] >= 0x1p-287);
         }
       }
     }
     e_id[tid] = id;
+    hk[tid] = -1;
+    hk[tid + 256] = -1;
+    const bool full = id >= 0 && !idonly;
+    const uint64_t fb = __ballot(full);
+    if (lane == 0) wfull[wave] = __popcll(fb);
+    __syncthreads();
+    if (idonly) {
+      uint32_t p = ((uint32_t)id * 2654435761u) & (VAL_HASH - 1);
+      for (;;) {
+        const int32_t o = atomicCAS(&hk[p], -1, id);
+        if (o == -1 || o == id) break;
+        p = (p + 1) & (VAL_HASH - 1);
+      }
+    }
+    int pos = __popcll(fb & below);
+    for (int q = 0; q < wave; q++) pos += wfull[q];
+    if (full) e_full[pos] = tid;
+    const int nfull = wfull[0] + wfull[1] + wfull[2] + wfull[3];
     __syncthreads();
     if (active && !beaten) {
-      const int n = min(256, hi - c0);
-      for (int k = 0; k < n; k++) {
-        const int32_t h = e_id[k];
-        if (h < 0) continue;
-        const double f0 = e_a[0][k], f1 = e_a[1][k], f2 = e_a[2][k], f3 = e_a[3][k];
-        bool hit = (h == w.id);
-        // a winner scoring +0 is beaten only by a host of lower index scoring +0
-        if (!hit && (w1 != 0ull || h < w.id) && fits<false>(f0, f1, f2, f3, d0, d1, d2, d3)) {
-          const double s2 = norm2_seq(f0 - d0, f1 - d1, f2 - d2, f3 - d3);
-          const double c = e_c[k], bw = e_b[k];
-          if (c == 0.0) {
-            // zero egress cost: the score is exactly +0 (finite s2, bw > 0)
-            hit = (0ull < w1) | ((0ull == w1) & (h < w.id));
-          } else if (w1 == 0ull && s2 >= 0x1p-600 && c >= 0x1p-300 && bw <= 0x1p300) {
-            hit = false;   // c * sqrt(s2) >= 2^-600 and / bw >= 2^-900: the score is > 0
-          } else {
-            const double sc = (c * __builtin_sqrt(s2)) / bw;
-            const uint64_t k1 = (uint64_t)__double_as_longlong(sc);
-            hit = (k1 < w1) | ((k1 == w1) & (h < w.id));
-          }
+      if (w1 == 0ull) {
+        // the id-only entries: only t's winner host
+        uint32_t p = ((uint32_t)w.id * 2654435761u) & (VAL_HASH - 1);
+        for (;;) {
+          const int32_t o = hk[p];
+          if (o == w.id) { beaten = true; break; }
+          if (o == -1) break;
+          p = (p + 1) & (VAL_HASH - 1);
         }
-        if (hit) { beaten = true; break; }
+        for (int q = 0; q < nfull && !beaten; q++) {
+          const int k = e_full[q];
+          beaten = beats(e_id[k], e_a[0][k], e_a[1][k], e_a[2][k], e_a[3][k], e_c[k], e_b[k],
+                         d0, d1, d2, d3, w, w1);
+        }
+      } else {
+        const int n = min(256, hi - c0);
+        for (int k = 0; k < n && !beaten; k++) {
+          const int32_t h = e_id[k];
+          if (h < 0) continue;
+          beaten = beats(h, e_a[0][k], e_a[1][k], e_a[2][k], e_a[3][k], e_c[k], e_b[k],
+                         d0, d1, d2, d3, w, w1);
+        }
       }
     }
     if (beaten) stop = 1;                    // benign race: every writer stores 1

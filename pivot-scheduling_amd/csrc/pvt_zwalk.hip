@@ -90,6 +90,13 @@ __global__ __launch_bounds__(256) void host_min_kernel(const double* avail, int 
   }
 }
 
+// One wave orders its LDS stores before its later loads (compiler fence + lgkmcnt(0)).
+__device__ __forceinline__ void wave_lds_sync() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 #ifdef PVT_STAMPS
 __device__ __forceinline__ uint64_t zstamp() {
   uint64_t t;
@@ -268,7 +275,32 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     if (dirty && p < nwin) { S.wa[0][p] = ra0; S.wa[1][p] = ra1; S.wa[2][p] = ra2; S.wa[3][p] = ra3; }
     dirty = false;
   };
+  // chunk pb = p0 + 1 in registers too (pb < 0: none): a task whose demand no host of chunk p0
+  // fits usually finds its winner there
+  double rb0 = 0.0, rb1 = 0.0, rb2 = 0.0, rb3 = 0.0;
+  int32_t bid = 0;
+  uint64_t bzm = 0, bvalid = 0;
+  bool bdirty = false;
+  int pb = -1;
+  auto load_b = [&](int c) {
+    bdirty = false;
+    if (c >= nch) { pb = -1; bvalid = 0; bzm = 0; return; }
+    pb = c;
+    const int p = c * 64 + lane;
+    const int q = min(p, nwin - 1);
+    rb0 = S.wa[0][q]; rb1 = S.wa[1][q]; rb2 = S.wa[2][q]; rb3 = S.wa[3][q];
+    bid = S.wid[q];
+    bvalid = __ballot(p < nwin);
+    bzm = cur >= 0 ? S.zm[c] : 0;
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  };
+  auto store_b = [&]() {
+    const int p = pb * 64 + lane;
+    if (bdirty && pb >= 0 && p < nwin) { S.wa[0][p] = rb0; S.wa[1][p] = rb1; S.wa[2][p] = rb2; S.wa[3][p] = rb3; }
+    bdirty = false;
+  };
   load_chunk(0);
+  load_b(1);
   for (int i0 = 0; i0 < nt && !failed; i0 += 64) {
     const int ti = i0 + lane;
     const int tw = ti < nt ? cmap[ti] : 0;
@@ -298,6 +330,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           const uint64_t m = __ballot(p < nwin && ((am >> S.wz[min(p, nwin - 1)]) & 1u));
           if (lane == 0) S.zm[c] = m;
           if (c == p0) rzm = m;
+          if (c == pb) bzm = m;
         }
         cur = a;
         __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -324,12 +357,22 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
       uint64_t fm = __ballot(fmin(fmin(n0, n1), fmin(n2, n3)) >= 0.0) & rvalid;
       uint64_t m = fm & rzm;
-      bool found = true;
+      bool found = true, inb = false;
+      double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
 #ifdef PVT_STAMPS
       n_chunks++;
 #endif
-      if (__builtin_expect(m == 0 || (fm & ~rzm) != 0, 0)) {
+      if (fm == 0 && pb >= 0) {
+        // no host of chunk p0 fits this task: chunk pb, from registers, unless p0 is dead
+        if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3]))) {
+          q0 = rb0 - d0; q1 = rb1 - d1; q2 = rb2 - d2; q3 = rb3 - d3;
+          const uint64_t fb = __ballot(fmin(fmin(q0, q1), fmin(q2, q3)) >= 0.0) & bvalid;
+          if ((fb & bzm) != 0 && (fb & ~bzm) == 0) { m = fb & bzm; inb = true; }
+        }
+      }
+      if (__builtin_expect(!inb && (m == 0 || (fm & ~rzm) != 0), 0)) {
         found = false;
+        store_b();                             // the general path works on LDS from p0 + 1 on
         for (int pass = 0;; pass++) {          // the register chunk (advancing past dead ones)
 #ifdef PVT_STAMPS
           n_chunks += pass > 0;
@@ -375,16 +418,27 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
             }
           }
         }
+        wave_lds_sync();
+        load_b(p0 + 1);
       }
       if (m) {
         // commit: resc[h] -= t_demand (cost_aware.py:95) on the lowest such lane, which logs
         const bool win = lane == __builtin_ctzll(m);
-        ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
-        if (win) {
-          S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
-          S.lgid[k] = rid;
+        if (inb) {
+          rb0 = win ? q0 : rb0; rb1 = win ? q1 : rb1; rb2 = win ? q2 : rb2; rb3 = win ? q3 : rb3;
+          if (win) {
+            S.lg[k][0] = q0; S.lg[k][1] = q1; S.lg[k][2] = q2; S.lg[k][3] = q3;
+            S.lgid[k] = bid;
+          }
+          bdirty = true;
+        } else {
+          ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
+          if (win) {
+            S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
+            S.lgid[k] = rid;
+          }
+          dirty = true;
         }
-        dirty = true;
       }
       if (!found) { failed = true; break; }  // certificate 1 fails: the list walk decides
       done++;
