@@ -82,6 +82,11 @@ struct RoundState {
   std::vector<int> egs, ega;      // cost_aware best-fit epochs: group starts (+ T) and anchors
   std::vector<int> ecomp;         // zone -> its component of zones joined by zero egress cost
   bool in_epoch = false;          // lists scored for an epoch (place_epochs)
+  // grouped rounds: per-group task counts, group anchors and (cost_aware) the cost table,
+  // copied to the host once by build_order (one synchronisation) for the group plans
+  bool ginfo = false;
+  std::vector<int32_t> gcnt, ga_host;
+  std::vector<double> cost_host;
 };
 
 struct pvt_ctx {
@@ -99,6 +104,7 @@ struct pvt_ctx {
   std::vector<hipEvent_t> evpool;
   std::vector<TimedLaunch> pending;
   // scratch
+  Buf gcnt, goff, gskey, gsidx;   // grouped order: counts, offsets + cursors, scattered pairs
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, grp_ord, csum, bsum, key,
       seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, kskey, kperm, kiota, ksorttmp, kflag;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
@@ -117,6 +123,8 @@ struct pvt_ctx {
   std::vector<uint32_t> rmt_host;
   RoundState rs;
   int32_t* next_host = nullptr;   // pinned
+  int32_t* goff_pin = nullptr;    // grouped order: offsets + cursors staged for the device
+  size_t goff_cap = 0;            //   (pinned; rewritten only after the previous round synced)
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
 };
 
@@ -281,6 +289,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->next_host) (void)hipHostFree(ctx->next_host);
   if (ctx->ep_host) (void)hipHostFree(ctx->ep_host);
+  if (ctx->goff_pin) (void)hipHostFree(ctx->goff_pin);
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
   if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -432,8 +441,62 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
   ENSURE(ctx->ord2, sizeof(int32_t) * T);
   int32_t* cur = P<int32_t>(ctx->ord);
   int32_t* alt = P<int32_t>(ctx->ord2);
-  launch_iota(cur, T, st);
   const bool grouped = r->task_group != nullptr && r->n_groups > 1;
+  RoundState& R = ctx->rs;
+  R.ginfo = false;
+  if (grouped && r->n_groups <= (1 << 20)) {
+    // one synchronisation: group counts, group anchors and the cost table to the host
+    const int G = r->n_groups;
+    ENSURE(ctx->gcnt, sizeof(int32_t) * (G + 1));
+    HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, sizeof(int32_t) * (G + 1), st));
+    launch_group_hist(r->task_group, T, G, P<int32_t>(ctx->gcnt), st);
+    R.gcnt.resize(G + 1);
+    R.ga_host.resize(G);
+    HIPCHK(hipMemcpyAsync(R.gcnt.data(), ctx->gcnt.p, sizeof(int32_t) * (G + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(R.ga_host.data(), r->group_anchor, sizeof(int32_t) * G, hipMemcpyDeviceToHost, st));
+    const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
+    if (ca) {
+      R.cost_host.resize((size_t)r->n_zones * r->n_zones);
+      HIPCHK(hipMemcpyAsync(R.cost_host.data(), r->cost, sizeof(double) * R.cost_host.size(),
+                            hipMemcpyDeviceToHost, st));
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    if (R.gcnt[G] != 0) return fail(ctx, PVT_EINVAL, "task_group out of range");
+    R.ginfo = ca;
+    int mx = 0;
+    for (int g = 0; g < G; g++) mx = std::max(mx, R.gcnt[g]);
+    if (mx <= GSORT_MAX) {
+      const size_t need = 2 * (size_t)(G + 1);
+      if (ctx->goff_cap < need) {
+        if (ctx->goff_pin) (void)hipHostFree(ctx->goff_pin);
+        ctx->goff_pin = nullptr;
+        ctx->goff_cap = 0;
+        HIPCHK(hipHostMalloc((void**)&ctx->goff_pin, sizeof(int32_t) * need));
+        ctx->goff_cap = need;
+      }
+      int32_t* off = ctx->goff_pin;
+      off[0] = 0;
+      for (int g = 0; g < G; g++) off[g + 1] = off[g] + R.gcnt[g];
+      std::copy(off, off + G + 1, off + G + 1);   // cursors
+      ENSURE(ctx->goff, sizeof(int32_t) * 2 * (G + 1));
+      ENSURE(ctx->gskey, sizeof(uint64_t) * T);
+      ENSURE(ctx->gsidx, sizeof(int32_t) * T);
+      HIPCHK(hipMemcpyAsync(ctx->goff.p, off, sizeof(int32_t) * 2 * (G + 1), hipMemcpyHostToDevice, st));
+      const uint64_t* keys = nullptr;
+      if (r->sort_tasks) {
+        ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
+        launch_norm_keys(r->dem, T, nullptr, P<uint64_t>(ctx->keys64a), st);
+        keys = P<uint64_t>(ctx->keys64a);
+      }
+      launch_group_scatter(r->task_group, keys, T, G, P<int32_t>(ctx->goff) + G + 1,
+                           P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx), st);
+      launch_group_sort(P<int32_t>(ctx->goff), G, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx),
+                        cur, st);
+      *ord_out = cur;
+      return PVT_OK;
+    }
+  }
+  launch_iota(cur, T, st);
   if (r->sort_tasks) {
     ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
     ENSURE(ctx->keys64b, sizeof(uint64_t) * T);
@@ -606,17 +669,23 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   R.kmode = 0; R.kn = 0; R.kstall = false;
   R.ordered = (r->mode == PVT_VBP_FF) || (r->mode == PVT_CA_FF && !r->sort_hosts);
   if (R.keyed) {
-    std::vector<int32_t> tg(T), ga;
+    std::vector<int32_t> tg, ga;
     if (r->task_group) {
-      HIPCHK(hipMemcpyAsync(tg.data(), r->task_group, sizeof(int32_t) * T, hipMemcpyDeviceToHost, st));
-      ga.resize(r->n_groups);
-      HIPCHK(hipMemcpyAsync(ga.data(), r->group_anchor, sizeof(int32_t) * r->n_groups,
-                            hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
       std::vector<int> cnt(r->n_groups, 0);
-      for (int t = 0; t < T; t++) {
-        if (tg[t] < 0 || tg[t] >= r->n_groups) return fail(ctx, PVT_EINVAL, "task_group out of range");
-        cnt[tg[t]]++;
+      if (R.ginfo) {                          // copied by build_order
+        for (int g = 0; g < r->n_groups; g++) cnt[g] = R.gcnt[g];
+        ga = R.ga_host;
+      } else {
+        tg.resize(T);
+        ga.resize(r->n_groups);
+        HIPCHK(hipMemcpyAsync(tg.data(), r->task_group, sizeof(int32_t) * T, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(ga.data(), r->group_anchor, sizeof(int32_t) * r->n_groups,
+                              hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int t = 0; t < T; t++) {
+          if (tg[t] < 0 || tg[t] >= r->n_groups) return fail(ctx, PVT_EINVAL, "task_group out of range");
+          cnt[tg[t]]++;
+        }
       }
       int off = 0;
       R.gstart.clear();
@@ -901,16 +970,23 @@ static int epoch_groups(pvt_ctx* ctx) {
   R.ega.clear();
   const int T = R.T;
   if (!ctx->epochs || r->mode != PVT_CA_BF || !r->task_group || r->n_groups < 2 || T < 2) return PVT_OK;
-  std::vector<int32_t> tg(T), ga(r->n_groups);
   hipStream_t st = ctx->stream;
-  HIPCHK(hipMemcpyAsync(tg.data(), r->task_group, sizeof(int32_t) * T, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(ga.data(), r->group_anchor, sizeof(int32_t) * r->n_groups,
-                        hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
   std::vector<int> cnt(r->n_groups, 0);
-  for (int t = 0; t < T; t++) {
-    if (tg[t] < 0 || tg[t] >= r->n_groups) return fail(ctx, PVT_EINVAL, "task_group out of range");
-    cnt[tg[t]]++;
+  std::vector<int32_t> ga;
+  if (R.ginfo) {                              // copied by build_order
+    for (int g = 0; g < r->n_groups; g++) cnt[g] = R.gcnt[g];
+    ga = R.ga_host;
+  } else {
+    std::vector<int32_t> tg(T);
+    ga.resize(r->n_groups);
+    HIPCHK(hipMemcpyAsync(tg.data(), r->task_group, sizeof(int32_t) * T, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ga.data(), r->group_anchor, sizeof(int32_t) * r->n_groups,
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    for (int t = 0; t < T; t++) {
+      if (tg[t] < 0 || tg[t] >= r->n_groups) return fail(ctx, PVT_EINVAL, "task_group out of range");
+      cnt[tg[t]]++;
+    }
   }
   int off = 0, ng = 0;
   for (int g = 0; g < r->n_groups; g++) {
@@ -926,8 +1002,12 @@ static int epoch_groups(pvt_ctx* ctx) {
   // one component compete for the same hosts and an epoch never holds both.
   const int Z = R.Z;
   std::vector<double> cost((size_t)Z * Z);
-  HIPCHK(hipMemcpyAsync(cost.data(), r->cost, sizeof(double) * Z * Z, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  if (R.ginfo && R.cost_host.size() == cost.size()) {
+    cost = R.cost_host;
+  } else {
+    HIPCHK(hipMemcpyAsync(cost.data(), r->cost, sizeof(double) * Z * Z, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   R.ecomp.resize(Z);
   for (int z = 0; z < Z; z++) R.ecomp[z] = z;
   auto root = [&](int z) { while (R.ecomp[z] != z) z = R.ecomp[z] = R.ecomp[R.ecomp[z]]; return z; };
@@ -1035,6 +1115,21 @@ static int place_epochs(pvt_ctx* ctx) {
     HIPCHK(hipMemcpyAsync(dev, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemsetAsync(dev + EP_BAD, 0, sizeof(int32_t) * nseg, st));
     int need = nch;                           // chains left to the list walk
+    EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
+                 P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_SEG_OFF,
+                 dev + EP_SEG_CHAIN, dev + EP_SEG_CSTART, dev + EP_STATUS, P<WinRec>(ctx->wres),
+                 r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD, r->rt_bw, P<int32_t>(ctx->grp_ord) + t0};
+    auto validate_and_read = [&]() -> int {
+      {
+        Scope sc(ctx, PVT_K_OTHER, 0, 0);
+        launch_epoch_validate(ea, st);
+      }
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      return PVT_OK;
+    };
     if (zw) {
       ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
       ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
@@ -1050,13 +1145,17 @@ static int place_epochs(pvt_ctx* ctx) {
         launch_zwalk(za, nch, st);
       }
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * 2 * nch,
-                            hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
+      // validated optimistically, read back with the walks' status in one synchronisation: when
+      // every chain was proven, that is the epoch's validation; otherwise the chains left to the
+      // list walk are walked and the epoch validated again
+      if ((rc = validate_and_read())) return rc;
       need = 0;
       for (int c = 0; c < nch; c++) need += host[EP_STATUS + 2 * c] != E.len[c];
       ctx->n_zchains += nch - need;
-      if (need && (rc = window_lists(ctx, t0, nt, 0, st))) return rc;
+      if (need) {
+        HIPCHK(hipMemsetAsync(dev + EP_BAD, 0, sizeof(int32_t) * nseg, st));
+        if ((rc = window_lists(ctx, t0, nt, 0, st))) return rc;
+      }
     }
     ctx->n_gchains += need;
     ctx->n_longest += *std::max_element(E.len.begin(), E.len.end());
@@ -1066,21 +1165,12 @@ static int place_epochs(pvt_ctx* ctx) {
                    r->rt_bw, P<int32_t>(ctx->grp_ord) + t0, ctx->stamps, dev + EP_COFF, dev + EP_CMAP, dev + EP_CSOFF, dev + EP_CSEG,
                    P<WinRec>(ctx->wres), zw ? 1 : 0};
     if (need) {
-      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
-      launch_commit_chains(ca_, nch, st);
+      {
+        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+        launch_commit_chains(ca_, nch, st);
+      }
+      if ((rc = validate_and_read())) return rc;
     }
-    EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
-                 P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_SEG_OFF,
-                 dev + EP_SEG_CHAIN, dev + EP_SEG_CSTART, dev + EP_STATUS, P<WinRec>(ctx->wres),
-                 r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD, r->rt_bw, P<int32_t>(ctx->grp_ord) + t0};
-    {
-      Scope sc(ctx, PVT_K_OTHER, 0, 0);
-      launch_epoch_validate(ea, st);
-    }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
-                          hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
     // the exact prefix: segments before the first rejected one, up to and including the first
     // that its chain did not finish (its walked tasks are exact; the next epoch starts there)
     for (int c = 0; c < nch; c++)

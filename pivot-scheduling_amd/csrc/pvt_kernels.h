@@ -281,6 +281,14 @@ void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a,
 hipError_t resident_init_attrs();
 size_t commit_lds_bytes();
 hipError_t init_kernel_attrs();
+// grouped processing order: group counts (cnt[G] = out-of-range ids), scatter by group, one
+// LDS bitonic sort of (key, task index) per group of at most GSORT_MAX tasks
+constexpr int GSORT_MAX = 4096;
+void launch_group_hist(const int32_t* tg, int T, int G, int32_t* cnt, hipStream_t st);
+void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,
+                          uint64_t* skey, int32_t* sidx, hipStream_t st);
+void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
+                       int32_t* ord, hipStream_t st);
 void launch_iota(int32_t* out, int n, hipStream_t st);
 // gather tasks into processing order: dem_ord[p][r] = dem[r*T + ord[p]], anc_ord[p]
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,

@@ -867,6 +867,101 @@ void launch_group_keys(const int32_t* task_group, const int32_t* idx, int T, uin
                      T, keys);
 }
 
+// a2, grouped rounds: the processing order as a group scatter + one LDS sort per group. The
+// stable order by (group, key) of the two LSD radix passes equals the order by (group, key,
+// task index), and within a group (key, index) is unique, so the scatter order inside a group
+// does not matter: group_hist counts, the host scans, group_scatter places (key, index) pairs
+// by atomics, group_sort bitonic-sorts each group's pairs in LDS.
+// Blocks of 1024 tasks count (and place) in LDS first when G <= GAGG_MAX groups, so a
+// group's global counter sees one atomic per block, not one per task (20 groups of 500 tasks
+// serialised 26 us of same-address atomics).
+constexpr int GAGG_MAX = 4096;
+__global__ __launch_bounds__(1024) void group_hist_kernel(const int32_t* tg, int T, int G, int32_t* cnt) {
+  __shared__ int32_t loc[GAGG_MAX + 1];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool agg = G <= GAGG_MAX;
+  if (agg) {
+    for (int q = threadIdx.x; q <= G; q += blockDim.x) loc[q] = 0;
+    __syncthreads();
+  }
+  if (i < T) {
+    const int g = tg[i];
+    const int b = (g >= 0 && g < G) ? g : G;   // G: out of range
+    atomicAdd(agg ? &loc[b] : &cnt[b], 1);
+  }
+  if (agg) {
+    __syncthreads();
+    for (int q = threadIdx.x; q <= G; q += blockDim.x)
+      if (loc[q]) atomicAdd(&cnt[q], loc[q]);
+  }
+}
+void launch_group_hist(const int32_t* tg, int T, int G, int32_t* cnt, hipStream_t st) {
+  hipLaunchKernelGGL(group_hist_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, T, G, cnt);
+}
+__global__ __launch_bounds__(1024) void group_scatter_kernel(const int32_t* tg, const uint64_t* keys, int T,
+                                                             int G, int32_t* cursor, uint64_t* skey,
+                                                             int32_t* sidx) {
+  __shared__ int32_t loc[GAGG_MAX];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = i < T ? tg[i] : -1;
+  if (G <= GAGG_MAX) {
+    // rank within the block's share of the group, then one reservation per (block, group)
+    for (int q = threadIdx.x; q < G; q += blockDim.x) loc[q] = 0;
+    __syncthreads();
+    const int r = g >= 0 ? atomicAdd(&loc[g], 1) : 0;
+    __syncthreads();
+    for (int q = threadIdx.x; q < G; q += blockDim.x)
+      if (loc[q]) loc[q] = atomicAdd(&cursor[q], loc[q]);
+    __syncthreads();
+    if (g >= 0) {
+      const int pos = loc[g] + r;
+      skey[pos] = keys ? keys[i] : 0ull;
+      sidx[pos] = i;
+    }
+  } else if (g >= 0) {
+    const int pos = atomicAdd(&cursor[g], 1);
+    skey[pos] = keys ? keys[i] : 0ull;
+    sidx[pos] = i;
+  }
+}
+void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,
+                          uint64_t* skey, int32_t* sidx, hipStream_t st) {
+  hipLaunchKernelGGL(group_scatter_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, keys, T,
+                     G, cursor, skey, sidx);
+}
+__global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, const uint64_t* skey,
+                                                          const int32_t* sidx, int32_t* ord) {
+  __shared__ uint64_t k[GSORT_MAX];
+  __shared__ int32_t v[GSORT_MAX];
+  const int a = off[blockIdx.x], n = off[blockIdx.x + 1] - a, tid = threadIdx.x;
+  if (n <= 0) return;
+  int P = 2;
+  while (P < n) P <<= 1;
+  for (int i = tid; i < P; i += blockDim.x) {
+    k[i] = i < n ? skey[a + i] : ~0ull;
+    v[i] = i < n ? sidx[a + i] : 0x7fffffff;
+  }
+  __syncthreads();
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int j = tid; j < (P >> 1); j += blockDim.x) {
+        const int lo = 2 * stride * (j / stride) + (j % stride), hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const uint64_t kl = k[lo], kh = k[hi];
+        const int32_t vl = v[lo], vh = v[hi];
+        const bool gt = kl > kh || (kl == kh && vl > vh);
+        if (gt == up) { k[lo] = kh; k[hi] = kl; v[lo] = vh; v[hi] = vl; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < n; i += blockDim.x) ord[a + i] = v[i];
+}
+void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
+                       int32_t* ord, hipStream_t st) {
+  hipLaunchKernelGGL(group_sort_kernel, dim3(G), dim3(1024), 0, st, off, skey, sidx, ord);
+}
+
 __global__ void iota_kernel(int32_t* out, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = i;
