@@ -1,0 +1,10 @@
+# r02 session 21: opportunistic walk fast path + DPP scans; kernel-trace stats of the opp bench.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() { local name=$1 secs=$2; shift 2; echo "=== $name"; timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -3 "gpurun_out/$name.log" | cut -c1-400; return $rc; }
+step g21_tests 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_opp_walk.py tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_sharded.py || exit 1
+step g21_bench_opp 300 python bench.py --mode opp --steps 10 --warmup 3 --extra 0 --cpu-baseline-seconds 0 || exit 1
+step g21_stamps_opp 300 python -u tools/commit_stamps.py 2 || exit 1
+step g21_prof_opp 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_g21 -o run --output-format csv -- python bench.py --mode opp --steps 10 --warmup 3 --extra 0 --cpu-baseline-seconds 0 --parity 0 || exit 1

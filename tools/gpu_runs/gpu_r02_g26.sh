@@ -1,0 +1,10 @@
+# r02 session 26: epoch finality by last-occurrence hash, 32 validation slices, winner-index
+# prefilter; full GPU suite, bench with extras, kernel stats.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+step() { local name=$1 secs=$2; shift 2; echo "=== $name"; timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -1 "gpurun_out/$name.log" | cut -c1-300; return $rc; }
+step g26_tests 900 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/ || exit 1
+step g26_bench 600 python bench.py --steps 20 --warmup 5 || exit 1
+step g26_prof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_g26 -o run --output-format csv -- python bench.py --steps 20 --warmup 5 --extra 0 --cpu-baseline-seconds 0 --parity 0 || exit 1
