@@ -363,12 +363,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       n_chunks++;
 #endif
       if (fm == 0 && pb >= 0) {
-        // no host of chunk p0 fits this task: chunk pb, from registers, unless p0 is dead
-        if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3]))) {
-          q0 = rb0 - d0; q1 = rb1 - d1; q2 = rb2 - d2; q3 = rb3 - d3;
-          const uint64_t fb = __ballot(fmin(fmin(q0, q1), fmin(q2, q3)) >= 0.0) & bvalid;
-          if ((fb & bzm) != 0 && (fb & ~bzm) == 0) { m = fb & bzm; inb = true; }
-        }
+        // no host of chunk p0 fits this task: its winner is chunk pb's first fitting zero-cost
+        // host, from registers (a dead chunk p0 is moved on by the general path below)
+        q0 = rb0 - d0; q1 = rb1 - d1; q2 = rb2 - d2; q3 = rb3 - d3;
+        const uint64_t fb = __ballot(fmin(fmin(q0, q1), fmin(q2, q3)) >= 0.0) & bvalid;
+        if ((fb & bzm) != 0 && (fb & ~bzm) == 0) { m = fb & bzm; inb = true; }
       }
       if (__builtin_expect(!inb && (m == 0 || (fm & ~rzm) != 0), 0)) {
         found = false;
