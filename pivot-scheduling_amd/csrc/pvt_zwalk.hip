@@ -354,89 +354,102 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // fitting host of it is zero-cost for this anchor. The fit test is the minimum residual:
       // every window capacity and chain demand is finite with |x| <= 2^500 (certificate 3), so
       // a - d is exact in sign (a >= d iff a - d >= +-0) and is the capacity after a commit.
-      double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
-      uint64_t fm = __ballot(fmin(fmin(n0, n1), fmin(n2, n3)) >= 0.0) & rvalid;
-      uint64_t m = fm & rzm;
-      bool found = true, inb = false;
-      double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0;
+      const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
+      const uint64_t fm0 = __ballot(fmin(fmin(n0, n1), fmin(n2, n3)) >= 0.0) & rvalid;
+      bool found = true;
 #ifdef PVT_STAMPS
       n_chunks++;
 #endif
-      if (fm == 0 && pb >= 0) {
-        // no host of chunk p0 fits this task: its winner is chunk pb's first fitting zero-cost
-        // host, from registers (a dead chunk p0 is moved on by the general path below)
-        q0 = rb0 - d0; q1 = rb1 - d1; q2 = rb2 - d2; q3 = rb3 - d3;
-        const uint64_t fb = __ballot(fmin(fmin(q0, q1), fmin(q2, q3)) >= 0.0) & bvalid;
-        if ((fb & bzm) != 0 && (fb & ~bzm) == 0) { m = fb & bzm; inb = true; }
-      }
-      if (__builtin_expect(!inb && (m == 0 || (fm & ~rzm) != 0), 0)) {
-        found = false;
-        store_b();                             // the general path works on LDS from p0 + 1 on
-        for (int pass = 0;; pass++) {          // the register chunk (advancing past dead ones)
-#ifdef PVT_STAMPS
-          n_chunks += pass > 0;
-#endif
-          if (fm & ~rzm)                       // fitting hosts of U outside the anchor's
-            m = __ballot(zero_exact((fm >> lane) & 1ull, (rzm >> lane) & 1ull, ra0, ra1, ra2,
-                                    ra3, min(p0 * 64 + lane, nwin - 1))) & fm;   // zero-cost zones
-          if (m) { found = true; break; }
-          if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
-            break;                             // chunk p0 still useful: look further in LDS
-          store_chunk(p0);                     // dead: move the register chunk on
-          if (++p0 >= nch) break;
-          rzm = S.zm[p0];
-          load_chunk(p0);
-          n0 = ra0 - d0; n1 = ra1 - d1; n2 = ra2 - d2; n3 = ra3 - d3;
-          fm = __ballot(fmin(fmin(n0, n1), fmin(n2, n3)) >= 0.0) & rvalid;
-          m = fm & rzm;
+      // Each path commits in place (no shared commit block: merging the paths made the compiler
+      // copy the chunk registers on every task). commit: resc[h] -= t_demand
+      // (cost_aware.py:95) on the lowest such lane, which logs.
+      if (__builtin_expect((fm0 & rzm) != 0 && (fm0 & ~rzm) == 0, 1)) {
+        const bool win = lane == __builtin_ctzll(fm0 & rzm);
+        ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
+        if (win) {
+          S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
+          S.lgid[k] = rid;
         }
-        if (!found && p0 < nch) {
-          store_chunk(p0);
-          for (int c = p0 + 1; c < nch; c++) {
+        dirty = true;
+      } else {
+        bool inb = false;
+        if (fm0 == 0 && pb >= 0) {
+          // no host of chunk p0 fits this task: its winner is chunk pb's first fitting zero-cost
+          // host, from registers (a dead chunk p0 is moved on by the general path below)
+          const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
+          const uint64_t fb = __ballot(fmin(fmin(q0, q1), fmin(q2, q3)) >= 0.0) & bvalid;
+          if ((fb & bzm) != 0 && (fb & ~bzm) == 0) {
+            const bool win = lane == __builtin_ctzll(fb & bzm);
+            rb0 = win ? q0 : rb0; rb1 = win ? q1 : rb1; rb2 = win ? q2 : rb2; rb3 = win ? q3 : rb3;
+            if (win) {
+              S.lg[k][0] = q0; S.lg[k][1] = q1; S.lg[k][2] = q2; S.lg[k][3] = q3;
+              S.lgid[k] = bid;
+            }
+            bdirty = true;
+            inb = true;
+          }
+        }
+        if (!inb) {                            // the general path
+          found = false;
+          store_b();                           // it works on LDS from p0 + 1 on
+          double g0 = n0, g1 = n1, g2 = n2, g3 = n3;
+          uint64_t fm = fm0, m = fm0 & rzm;
+          for (int pass = 0;; pass++) {        // the register chunk (advancing past dead ones)
 #ifdef PVT_STAMPS
-            n_chunks++;
+            n_chunks += pass > 0;
 #endif
-            const int p = c * 64 + lane;
-            const int q = min(p, nwin - 1);
-            const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
-            const int32_t id = S.wid[q];
-            const uint64_t zm = S.zm[c];
-            const bool f = p < nwin && fits<false>(a0, a1, a2, a3, d0, d1, d2, d3);
-            const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
-            const uint64_t mc = __ballot(f && k0);
-            if (mc) {
-              if (lane == __builtin_ctzll(mc)) {
-                const double c0 = a0 - d0, c1 = a1 - d1, c2 = a2 - d2, c3 = a3 - d3;
-                S.wa[0][q] = c0; S.wa[1][q] = c1; S.wa[2][q] = c2; S.wa[3][q] = c3;
-                S.lg[k][0] = c0; S.lg[k][1] = c1; S.lg[k][2] = c2; S.lg[k][3] = c3;
-                S.lgid[k] = id;
+            if (fm & ~rzm)                     // fitting hosts of U outside the anchor's
+              m = __ballot(zero_exact((fm >> lane) & 1ull, (rzm >> lane) & 1ull, ra0, ra1, ra2,
+                                      ra3, min(p0 * 64 + lane, nwin - 1))) & fm;   // zero-cost zones
+            if (m) {
+              const bool win = lane == __builtin_ctzll(m);
+              ra0 = win ? g0 : ra0; ra1 = win ? g1 : ra1; ra2 = win ? g2 : ra2; ra3 = win ? g3 : ra3;
+              if (win) {
+                S.lg[k][0] = g0; S.lg[k][1] = g1; S.lg[k][2] = g2; S.lg[k][3] = g3;
+                S.lgid[k] = rid;
               }
+              dirty = true;
               found = true;
-              m = 0;                           // committed here, not in the register chunk
               break;
             }
+            if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
+              break;                           // chunk p0 still useful: look further in LDS
+            store_chunk(p0);                   // dead: move the register chunk on
+            if (++p0 >= nch) break;
+            rzm = S.zm[p0];
+            load_chunk(p0);
+            g0 = ra0 - d0; g1 = ra1 - d1; g2 = ra2 - d2; g3 = ra3 - d3;
+            fm = __ballot(fmin(fmin(g0, g1), fmin(g2, g3)) >= 0.0) & rvalid;
+            m = fm & rzm;
           }
-        }
-        wave_lds_sync();
-        load_b(p0 + 1);
-      }
-      if (m) {
-        // commit: resc[h] -= t_demand (cost_aware.py:95) on the lowest such lane, which logs
-        const bool win = lane == __builtin_ctzll(m);
-        if (inb) {
-          rb0 = win ? q0 : rb0; rb1 = win ? q1 : rb1; rb2 = win ? q2 : rb2; rb3 = win ? q3 : rb3;
-          if (win) {
-            S.lg[k][0] = q0; S.lg[k][1] = q1; S.lg[k][2] = q2; S.lg[k][3] = q3;
-            S.lgid[k] = bid;
+          if (!found && p0 < nch) {
+            store_chunk(p0);
+            for (int c = p0 + 1; c < nch; c++) {
+#ifdef PVT_STAMPS
+              n_chunks++;
+#endif
+              const int p = c * 64 + lane;
+              const int q = min(p, nwin - 1);
+              const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
+              const int32_t id = S.wid[q];
+              const uint64_t zm = S.zm[c];
+              const bool f = p < nwin && fits<false>(a0, a1, a2, a3, d0, d1, d2, d3);
+              const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
+              const uint64_t mc = __ballot(f && k0);
+              if (mc) {
+                if (lane == __builtin_ctzll(mc)) {
+                  const double c0 = a0 - d0, c1 = a1 - d1, c2 = a2 - d2, c3 = a3 - d3;
+                  S.wa[0][q] = c0; S.wa[1][q] = c1; S.wa[2][q] = c2; S.wa[3][q] = c3;
+                  S.lg[k][0] = c0; S.lg[k][1] = c1; S.lg[k][2] = c2; S.lg[k][3] = c3;
+                  S.lgid[k] = id;
+                }
+                found = true;
+                break;
+              }
+            }
           }
-          bdirty = true;
-        } else {
-          ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
-          if (win) {
-            S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
-            S.lgid[k] = rid;
-          }
-          dirty = true;
+          wave_lds_sync();
+          load_b(p0 + 1);
         }
       }
       if (!found) { failed = true; break; }  // certificate 1 fails: the list walk decides
