@@ -577,9 +577,13 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       }
       const int c0l = cd[0];
       double y0 = z0 - e0, y1 = z1 - e1, y2 = z2 - e2, y3 = z3 - e3;
-      // (a task with feasible hosts but no candidates cannot happen when the counts are
-      // consistent; nnew = 1 sends it to the slow path, which stops there)
-      int nnew = (nsv > 0 && ccv == 0) ? 1 : 0, mm = 0;
+      // dok: the speculative draw still holds for the new-lost count (same mask, k <= n - 1;
+      // recomputed when a commit takes a host away). A task whose draw holds and whose c_0 still
+      // fits with no lost host below it (mm == 0) takes c_0 from its lane's registers whatever
+      // hosts above c_0 it lost. (A task with feasible hosts but no candidates cannot happen
+      // when the counts are consistent; dok = 0 sends it to the slow path, which stops there.)
+      int nnew = 0, mm = 0;
+      bool dok = !(nsv > 0 && ccv == 0);
       uint32_t lm = 0;
       int rch = -1;   // commit of a task that took the slow path, with capacities after / before
       double ra0 = 0.0, ra1 = 0.0, ra2 = 0.0, ra3 = 0.0, rb0 = 0.0, rb1 = 0.0, rb2 = 0.0, rb3 = 0.0;
@@ -589,15 +593,16 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
         const int L = i - s;
         const int n = __builtin_amdgcn_readlane(nsv, L);
         if (n <= 0) continue;   // no feasible host at s: none now (capacities only decrease)
-        const int nn = __builtin_amdgcn_readlane(nnew, L);
+        const bool fast = __builtin_amdgcn_readlane((int)(dok & (mm == 0) & !(lm & 1u)), L) != 0;
         int w;
         double w0, w1, w2, w3, n0, n1, n2, n3;
-        if (nn == 0) {
+        if (fast) {
           w = __builtin_amdgcn_readlane(c0l, L);
           w0 = readlane_d(z0, L); w1 = readlane_d(z1, L); w2 = readlane_d(z2, L); w3 = readlane_d(z3, L);
           n0 = readlane_d(y0, L); n1 = readlane_d(y1, L); n2 = readlane_d(y2, L); n3 = readlane_d(y3, L);
           fcm |= 1ull << L;
         } else {
+          const int nn = __builtin_amdgcn_readlane(nnew, L);
           const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)kv, L);
           const int ntrue = n - nn;
           if (ntrue <= 0 || rint_mask((uint32_t)(ntrue - 1)) != rint_mask((uint32_t)(n - 1)) ||
@@ -644,6 +649,11 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
                           !fits<false>(n0, n1, n2, n3, e0, e1, e2, e3);
         nnew += lost;
         mm += lost & (w < c0l);
+        if (lost) {
+          const int ntrue = nsv - nnew;
+          dok = dok & (ntrue > 0) & (rint_mask((uint32_t)(ntrue - 1)) == rint_mask((uint32_t)(nsv - 1))) &
+                (kv <= (uint32_t)(ntrue - 1));
+        }
         if (__ballot(lost & (w >= c0l))) {
 #pragma unroll
           for (int x = 0; x < OPP_C; x++) lm |= ((lost & (cd[x] == w)) ? 1u : 0u) << x;
