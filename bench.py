@@ -243,33 +243,61 @@ def roofline(args, ks, mode, B):
     return out
 
 
-# Latency roofline of a sequential walk: each task reads state the previous commit wrote, so a
-# walk can never beat one dependent LDS round trip per task (MI355X_MICROARCH.md, per-instruction
-# constants: ds_read_b32 issue -> use in a dependent chain, one wave, ~50 cycles) at 2.4 GHz.
+# Roofline of the sequential frontier walk. Each task reads the capacities the previous commit
+# wrote, so the chain runs on ONE wave, and what bounds it is that wave's instruction issue: a
+# wave issues at most one instruction per 4 cycles (MI355X_MICROARCH.md, 'vector-instruction
+# ISSUE cost, one wave': v_add_f32 4 cycles, s_nop 4). `achieved` = the walk's instructions per
+# second on its longest chain (instructions per task from the rocprofv3 PMC profile of this
+# binary: SQ_INSTS_VALU + SALU + LDS + SMEM + VMEM over the chain tasks), `peak` = 2.4 GHz / 4.
+# The latency floor (one dependent LDS round trip per task, ~50 cycles) is kept beside it.
+ISSUE_CYCLES = 4
 LDS_DEP_CYCLES = 50
 SHADER_HZ = 2.4e9
+WALK_PMC = os.path.join(ROOT, "profiles", "r02p", "pmc_r02p_zwalk.json")
 
 
-def walk_roofline(ks, ep, steps):
+def walk_roofline(ks, ep, steps, T):
     """The dominant kernel when no candidate lists are scored (cost_aware best-fit epochs whose
     chains the zero-cost frontier walk proves, pvt_zwalk.hip): the chain walks run side by side,
-    so the round waits for the longest. `achieved` = its tasks per second, `peak` = one task per
-    dependent LDS round trip."""
+    so the round waits for the longest."""
     c = ks["commit"]
     ms = c["ms"] / max(steps, 1)
     longest = ep.get("longest_chain_tasks", 0)
     out = {"kernel": "zwalk (zero-cost frontier walk: one wave per epoch chain, window in LDS)",
-           "bound": "latency", "unit": "tasks/s (longest chain)", "traffic": None,
+           "bound": "issue", "unit": "instructions/s (one wave)", "traffic": None,
            "walk_ms_per_step": ms, "longest_chain_tasks": longest,
-           "peak_basis": "one dependent LDS round trip (%d cycles) per task at %.1f GHz"
-                         % (LDS_DEP_CYCLES, SHADER_HZ / 1e9)}
+           "peak_basis": "one instruction per %d cycles of one wave at %.1f GHz"
+                         % (ISSUE_CYCLES, SHADER_HZ / 1e9)}
     if ms <= 0 or longest <= 0:
         out.update({"achieved": None, "peak": None, "frac": None})
         return out
-    achieved = longest / (ms * 1e-3)
-    peak = SHADER_HZ / LDS_DEP_CYCLES
-    out.update({"achieved": achieved, "peak": peak, "frac": achieved / peak,
-                "cycles_per_task": SHADER_HZ / achieved})
+    tasks_per_s = longest / (ms * 1e-3)
+    ipt = None
+    try:
+        with open(WALK_PMC) as f:
+            pmc = json.load(f)
+        cnt = pmc["counters_per_launch"]
+        ipt = sum(cnt.get(k, 0.0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
+                                            "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD",
+                                            "SQ_INSTS_VMEM_WR")) / max(T, 1)
+        out["pmc_source"] = os.path.relpath(WALK_PMC, ROOT)
+        out["instructions_per_task"] = ipt
+        out["issue_active_frac_pmc"] = cnt["SQ_ACTIVE_INST_ANY"] / cnt["SQ_WAVE_CYCLES"]
+        out["wait_frac_pmc"] = cnt["SQ_WAIT_ANY"] / cnt["SQ_WAVE_CYCLES"]
+        traffic = 2.0 * cnt.get("FETCH_SIZE", 0.0) * 1024 + cnt.get("WRITE_SIZE", 0.0) * 1024
+        out["traffic"] = traffic if traffic > 0 else None
+    except (OSError, ValueError, KeyError):
+        out["note"] = "no PMC profile of the walk (tools/pmc_profile.py --kernel zwalk_kernel)"
+    out["cycles_per_task"] = SHADER_HZ / tasks_per_s
+    out["latency_floor"] = {"peak_tasks_per_s": SHADER_HZ / LDS_DEP_CYCLES,
+                            "achieved_tasks_per_s": tasks_per_s,
+                            "frac": tasks_per_s / (SHADER_HZ / LDS_DEP_CYCLES)}
+    if ipt is None:
+        out.update({"achieved": None, "peak": None, "frac": None})
+        return out
+    achieved = ipt * tasks_per_s
+    peak = SHADER_HZ / ISSUE_CYCLES
+    out.update({"achieved": achieved, "peak": peak, "frac": achieved / peak})
     return out
 
 
@@ -378,7 +406,7 @@ def main():
                                 if hosts_sharded else
                                 "scenario-sharded x%d (no data-path collective)" % world),
             },
-            "roofline": (walk_roofline(ks, ep, args.steps)
+            "roofline": (walk_roofline(ks, ep, args.steps, T)
                          if not B and ks["score"]["launches"] == 0 and ks["commit"]["launches"] > 0
                          else roofline(args, ks, mode, B)),
             "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items()},
