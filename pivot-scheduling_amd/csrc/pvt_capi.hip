@@ -41,8 +41,8 @@ static constexpr int EP_SEG_OFF = 0, EP_SEG_CHAIN = EP_SEG_OFF + EPOCH_SEGS + 1,
                      EP_SEG_CSTART = EP_SEG_CHAIN + EPOCH_SEGS, EP_COFF = EP_SEG_CSTART + EPOCH_SEGS,
                      EP_CSOFF = EP_COFF + EPOCH_SEGS + 1, EP_CSEG = EP_CSOFF + EPOCH_SEGS + 1,
                      EP_CMAP = EP_CSEG + EPOCH_SEGS, EP_STATUS = EP_CMAP + EPOCH_MAX,
-                     EP_BAD = EP_STATUS + 2 * EPOCH_SEGS;
-static constexpr int EP_WORDS = EP_BAD + EPOCH_SEGS;
+                     EP_BAD = EP_STATUS + 2 * EPOCH_SEGS, EP_RES = EP_BAD + EPOCH_SEGS;
+static constexpr int EP_WORDS = EP_RES + 8;
 
 struct Buf {
   void* p = nullptr;
@@ -123,6 +123,8 @@ struct pvt_ctx {
   std::vector<uint32_t> rmt_host;
   RoundState rs;
   int32_t* next_host = nullptr;   // pinned
+  void* gstage = nullptr;         // grouped order: counts, anchors, cost table (pinned)
+  size_t gstage_cap = 0;
   int32_t* goff_pin = nullptr;    // grouped order: offsets + cursors staged for the device
   size_t goff_cap = 0;            //   (pinned; rewritten only after the previous round synced)
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
@@ -290,6 +292,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   if (ctx->next_host) (void)hipHostFree(ctx->next_host);
   if (ctx->ep_host) (void)hipHostFree(ctx->ep_host);
   if (ctx->goff_pin) (void)hipHostFree(ctx->goff_pin);
+  if (ctx->gstage) (void)hipHostFree(ctx->gstage);
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
   if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -450,17 +453,28 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
     ENSURE(ctx->gcnt, sizeof(int32_t) * (G + 1));
     HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, sizeof(int32_t) * (G + 1), st));
     launch_group_hist(r->task_group, T, G, P<int32_t>(ctx->gcnt), st);
-    R.gcnt.resize(G + 1);
-    R.ga_host.resize(G);
-    HIPCHK(hipMemcpyAsync(R.gcnt.data(), ctx->gcnt.p, sizeof(int32_t) * (G + 1), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(R.ga_host.data(), r->group_anchor, sizeof(int32_t) * G, hipMemcpyDeviceToHost, st));
+    // staged in pinned memory: pageable destinations made each copy a ~20 us synchronous
+    // staging step (profiles/r02q kernel trace)
     const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
-    if (ca) {
-      R.cost_host.resize((size_t)r->n_zones * r->n_zones);
-      HIPCHK(hipMemcpyAsync(R.cost_host.data(), r->cost, sizeof(double) * R.cost_host.size(),
-                            hipMemcpyDeviceToHost, st));
+    const size_t nz2 = ca ? (size_t)r->n_zones * r->n_zones : 0;
+    const size_t need = sizeof(double) * nz2 + sizeof(int32_t) * (2 * (size_t)G + 1);
+    if (ctx->gstage_cap < need) {
+      if (ctx->gstage) (void)hipHostFree(ctx->gstage);
+      ctx->gstage = nullptr;
+      ctx->gstage_cap = 0;
+      HIPCHK(hipHostMalloc(&ctx->gstage, need));
+      ctx->gstage_cap = need;
     }
+    double* cst = reinterpret_cast<double*>(ctx->gstage);
+    int32_t* cnt = reinterpret_cast<int32_t*>(cst + nz2);
+    int32_t* gan = cnt + G + 1;
+    HIPCHK(hipMemcpyAsync(cnt, ctx->gcnt.p, sizeof(int32_t) * (G + 1), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(gan, r->group_anchor, sizeof(int32_t) * G, hipMemcpyDeviceToHost, st));
+    if (ca) HIPCHK(hipMemcpyAsync(cst, r->cost, sizeof(double) * nz2, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    R.gcnt.assign(cnt, cnt + G + 1);
+    R.ga_host.assign(gan, gan + G);
+    R.cost_host.assign(cst, cst + nz2);
     if (R.gcnt[G] != 0) return fail(ctx, PVT_EINVAL, "task_group out of range");
     R.ginfo = ca;
     int mx = 0;
@@ -1077,6 +1091,7 @@ static int place_epochs(pvt_ctx* ctx) {
   int32_t* host = ctx->ep_host;
   EpochPlan E;
   int t0 = 0, rc;
+  bool force_lists = false;       // the last epoch's frontier walk left chains unproven
   R.in_epoch = true;
   struct Reset { bool& f; ~Reset() { f = false; } } reset_{R.in_epoch};
   while (t0 < R.T) {
@@ -1086,7 +1101,8 @@ static int place_epochs(pvt_ctx* ctx) {
     ctx->n_segs += nseg;
     // chains the zero-cost frontier walk can prove need no candidate lists (pvt_zwalk.hip);
     // the lists are scored only for the others
-    const bool zw = ctx->zwalk && nch > 1 && !r->rt_bw && R.Z <= ZMAX;
+    const bool zw = ctx->zwalk && nch > 1 && !r->rt_bw && R.Z <= ZMAX && !force_lists;
+    force_lists = false;
     if (!zw && (rc = window_lists(ctx, t0, nt, 0, st))) return rc;
     Lists L;
     lists_from(ctx, L, 0);
@@ -1145,17 +1161,31 @@ static int place_epochs(pvt_ctx* ctx) {
         launch_zwalk(za, nch, st);
       }
       HIPCHK(hipGetLastError());
-      // validated optimistically, read back with the walks' status in one synchronisation: when
-      // every chain was proven, that is the epoch's validation; otherwise the chains left to the
-      // list walk are walked and the epoch validated again
-      if ((rc = validate_and_read())) return rc;
+      // validation, the accepted prefix and its apply all on the device, then one readback. A
+      // chain the frontier walk could not prove is not accepted past its first segment; the
+      // next epoch then walks its chains with candidate lists (force_lists).
+      {
+        Scope sc(ctx, PVT_K_OTHER, 0, 0);
+        launch_epoch_validate(ea, st);
+        launch_epoch_accept_apply(ea, dev + EP_RES, nch, st);
+      }
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
+                            hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
       need = 0;
       for (int c = 0; c < nch; c++) need += host[EP_STATUS + 2 * c] != E.len[c];
       ctx->n_zchains += nch - need;
-      if (need) {
-        HIPCHK(hipMemsetAsync(dev + EP_BAD, 0, sizeof(int32_t) * nseg, st));
-        if ((rc = window_lists(ctx, t0, nt, 0, st))) return rc;
-      }
+      ctx->n_longest += *std::max_element(E.len.begin(), E.len.end());
+      if (host[EP_RES + 4])
+        return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out (epoch at task %d)", t0);
+      const int adv = host[EP_RES + 1];
+      ctx->refills += host[EP_RES + 2];
+      ctx->n_rejected += host[EP_RES + 3];
+      if (need && adv < nt) force_lists = true;
+      if (adv <= 0 && !need) return fail(ctx, PVT_EHIP, "epoch made no progress at task %d", t0);
+      t0 += adv;
+      continue;
     }
     ctx->n_gchains += need;
     ctx->n_longest += *std::max_element(E.len.begin(), E.len.end());

@@ -249,6 +249,52 @@ __global__ __launch_bounds__(256) void epoch_apply_kernel(EpochArgs A, int n_acc
   }
 }
 
+// The accepted prefix, decided on the device right after validation (no host round trip
+// between validation and apply): segments before the first rejected one, up to and including
+// the first its chain did not finish (its walked tasks are exact; the next epoch starts there).
+// Every block derives it; block 0 reports it (res: accepted segments, next task relative to the
+// epoch, refill, rejected segments, a chain walk timed out); block c then writes chain c's
+// accepted segments' final entries, as epoch_apply_kernel. A timed-out walk applies nothing.
+__global__ __launch_bounds__(256) void epoch_accept_apply_kernel(EpochArgs A, int32_t* res) {
+  __shared__ int32_t acc_s, tout_s;
+  const int c = blockIdx.x;
+  if (threadIdx.x == 0) {
+    int acc = 0, next = 0, refill = 0, rej = 0, tout = 0;
+    for (int j = 0; j < A.nseg; j++) tout |= A.status[2 * A.seg_chain[j]] == -1;
+    if (!tout) {
+      for (int j = 0; j < A.nseg; j++) {
+        const int len = A.seg_off[j + 1] - A.seg_off[j];
+        const int adv = seg_adv(A, j);
+        if (j > 0 && A.bad[j]) { rej = A.nseg - j; break; }
+        acc = j + 1;
+        next = A.seg_off[j] + adv;
+        if (adv < len) { refill = 1; rej = A.nseg - j - 1; break; }
+      }
+    }
+    acc_s = acc;
+    tout_s = tout;
+    if (c == 0) { res[0] = acc; res[1] = next; res[2] = refill; res[3] = rej; res[4] = tout; }
+  }
+  __syncthreads();
+  if (tout_s) return;
+  const int n_accept = acc_s;
+  for (int s = 0; s < n_accept; s++) {
+    if (A.seg_chain[s] != c) continue;
+    const int e0 = A.seg_off[s], ne = seg_adv(A, s);
+    for (int k = threadIdx.x; k < ne; k += blockDim.x) {
+      const WinRec& e = A.wlog[e0 + k];
+      if (e.id < 0 || e.sup) continue;
+#pragma unroll
+      for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + e.id] = e.a[r];
+    }
+    __syncthreads();
+  }
+}
+
+void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st) {
+  hipLaunchKernelGGL(epoch_accept_apply_kernel, dim3(nchains), dim3(256), 0, st, a, res);
+}
+
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
   const int tiles = (CHAIN_MAX + 255) / 256;   // a segment never exceeds its chain's cap

@@ -187,6 +187,8 @@ struct EpochArgs {
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st);
 // apply: the accepted segments [0, n_accept) of each chain, chain by chain in segment order
 void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st);
+// validate's verdict to the accepted prefix and its apply, on the device; res[5] reported
+void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st);
 void launch_commit_chains(const CommitArgs& a, int nchains, hipStream_t st);
 
 // Zero-cost frontier walk of epoch chains (pvt_zwalk.hip): workgroup b walks chain b like the
