@@ -1094,7 +1094,15 @@ static int place_epochs(pvt_ctx* ctx) {
   bool force_lists = false;       // the last epoch's frontier walk left chains unproven
   R.in_epoch = true;
   struct Reset { bool& f; ~Reset() { f = false; } } reset_{R.in_epoch};
+  const bool zw_possible = ctx->zwalk && !r->rt_bw && R.Z <= ZMAX;
   while (t0 < R.T) {
+    // the frontier walk's host minima (certificate 2) depend only on the epoch's start state:
+    // reduced while the host plans the epoch
+    if (zw_possible && !force_lists) {
+      ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_host_min(r->avail, R.H, P<double>(ctx->hmin), st);
+    }
     epoch_plan(R, t0, E);
     const int nseg = (int)E.chain.size(), nch = (int)E.segs.size(), nt = E.off.back();
     ctx->n_epochs++;
@@ -1129,7 +1137,7 @@ static int place_epochs(pvt_ctx* ctx) {
     host[EP_COFF + nch] = nm;
     host[EP_CSOFF + nch] = ns;
     HIPCHK(hipMemcpyAsync(dev, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemsetAsync(dev + EP_BAD, 0, sizeof(int32_t) * nseg, st));
+    // (the rejection flags are zeroed by epoch_final_kernel, launched before every validation)
     int need = nch;                           // chains left to the list walk
     EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
                  P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_SEG_OFF,
@@ -1147,15 +1155,10 @@ static int place_epochs(pvt_ctx* ctx) {
       return PVT_OK;
     };
     if (zw) {
-      ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
       ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
                    P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                    P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
                    P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps};
-      {
-        Scope sc(ctx, PVT_K_OTHER, 0, 0);
-        launch_host_min(r->avail, R.H, P<double>(ctx->hmin), st);
-      }
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0);
         launch_zwalk(za, nch, st);

@@ -211,6 +211,7 @@ __global__ __launch_bounds__(1024) void epoch_final_kernel(EpochArgs A) {
   __shared__ int32_t hk[FIN_SLOTS], hv[FIN_SLOTS];
   const int j = blockIdx.x, tid = threadIdx.x;
   const int s0 = A.seg_off[j], n = seg_adv(A, j);
+  if (tid == 0) A.bad[j] = 0;                 // validation (next launch) starts with no verdict
   for (int q = tid; q < FIN_SLOTS; q += blockDim.x) { hk[q] = -1; hv[q] = -1; }
   __syncthreads();
   for (int k = tid; k < n; k += blockDim.x) {
