@@ -927,6 +927,54 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
   return PVT_OK;
 }
 
+// cost_aware first-fit with sort_hosts while the group's zero-key prefix lasts (kmode 1): every
+// task takes the first prefix host, in host order, that strictly fits -- the frontier walk
+// (pvt_zwalk.hip, keyed mode) does exactly that over the prefix's first ZW_M hosts from the
+// group start, in registers, and stops at the first task none of them fits; the windowed list
+// path (frozen key and prefix unchanged) continues from there. Unsharded rounds only.
+static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a launch + synchronisation
+static int keyed_frontier(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  if (!ctx->zwalk || !R.keyed || !R.kscan || R.kmode != 1 || R.lo != 0 || R.hi != R.H ||
+      R.world != 1 || R.g >= R.ngroups || R.t0 != R.gstart[R.g] || r->rt_bw || R.Z > ZMAX)
+    return PVT_OK;
+  const int n = R.gstart[R.g + 1] - R.t0;
+  if (n < KEYED_FRONTIER_MIN || R.kn <= 0) return PVT_OK;
+  hipStream_t st = ctx->stream;
+  ENSURE(ctx->wres, sizeof(WinRec) * (size_t)n);
+  int32_t* status = P<int32_t>(ctx->next);
+  ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)R.t0 * 4,
+               P<int32_t>(ctx->anc_ord) + R.t0, R.ord + R.t0, P<double>(ctx->csum),
+               P<double>(ctx->bsum), nullptr, nullptr, status, P<WinRec>(ctx->wres),
+               r->placement, nullptr, ctx->stamps, P<int32_t>(ctx->kperm), R.kn, R.lo, n,
+               r->avail};
+  {
+    Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+    launch_zwalk_keyed(za, st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const int done = ctx->next_host[0];
+  if (done < 0 || done > n) return fail(ctx, PVT_EHIP, "keyed frontier walk returned %d of %d", done, n);
+  ctx->n_zchains += done > 0;
+  R.t0 += done;
+  return PVT_OK;
+}
+
+// The next window, after the keyed frontier walk has taken what it can at a group start.
+static int next_window(pvt_ctx* ctx, int* nt) {
+  RoundState& R = ctx->rs;
+  for (;;) {
+    int rc = round_next_window(ctx, nt);
+    if (rc || *nt == 0) return rc;
+    const int t = R.t0;
+    if ((rc = keyed_frontier(ctx))) return rc;
+    if (R.t0 == t) return PVT_OK;
+  }
+}
+
 // pvt_place for the list policies. While window k is walked on the caller's stream, the side
 // stream scores window k+1 on the capacities as they stand (the walk of k-1 is complete; the
 // walk of k is in flight): an event recorded just before walk k releases it. The side stream
@@ -938,7 +986,7 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
 static int place_pipelined(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   int rc, nt = 0;
-  if ((rc = round_next_window(ctx, &nt))) return rc;
+  if ((rc = next_window(ctx, &nt))) return rc;
   if (nt == 0) return PVT_OK;
   int lb = 0, t0 = R.t0;
   if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
@@ -966,7 +1014,7 @@ static int place_pipelined(pvt_ctx* ctx) {
     }
     if (nnt > 0) HIPCHK(hipStreamSynchronize(ctx->side));   // discard the speculation
     R.t0 = t0 + adv;
-    if ((rc = round_next_window(ctx, &nt))) return rc;
+    if ((rc = next_window(ctx, &nt))) return rc;
     if (nt == 0) break;
     t0 = R.t0; lb = 0; n_prev = 0; inherited = false;
     if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
@@ -1158,7 +1206,8 @@ static int place_epochs(pvt_ctx* ctx) {
       ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
                    P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                    P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
-                   P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps};
+                   P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
+                   nullptr, 0, 0, 0, nullptr};
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0);
         launch_zwalk(za, nch, st);

@@ -211,10 +211,16 @@ struct ZwalkArgs {
   int32_t* placement;
   const double* hmin;     // per-dimension host minima, launch_host_min partials
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS)
+  // keyed first-fit mode (launch_zwalk_keyed): one group of knt tasks, window = the first hosts
+  // of the zero-key prefix kperm[0, kn) (+ lo), capacities written back to wb at the end
+  const int32_t* kperm;
+  int kn, lo, knt;
+  double* wb;
 };
 constexpr int ZW_MIN_PARTS = 256;
 void launch_host_min(const double* avail, int H, double* part, hipStream_t st);   // [256][4]
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st);
+void launch_zwalk_keyed(const ZwalkArgs& a, hipStream_t st);
 
 // cost_aware first-fit with sort_hosts, as the reference runs it (cost_aware.py:118-124): the
 // hosts sorted once per group by the frozen key (perm, skey = sorted key bits; the radix sort

@@ -90,6 +90,11 @@ __global__ __launch_bounds__(256) void host_min_kernel(const double* avail, int 
   }
 }
 
+// Fit from the minimum residual min(a - d): a >= d (best-fit) or a > d (first-fit, strict) in
+// every dimension; exact in sign for finite values (certificate 3).
+template <bool STRICT>
+__device__ __forceinline__ bool fit_res(double m) { return STRICT ? (m > 0.0) : (m >= 0.0); }
+
 // One wave orders its LDS stores before its later loads (compiler fence + lgkmcnt(0)).
 __device__ __forceinline__ void wave_lds_sync() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -107,6 +112,11 @@ __device__ __forceinline__ uint64_t zstamp() {
 }
 #endif
 
+// KEYED: cost_aware first-fit with sort_hosts (pvt_capi.hip keyed_frontier): one group, its
+// window the first ZW_M hosts of the group's zero-key prefix (perm, index order), strict fit,
+// no zone certificates (the order is the keyed path's own); the window's capacities are written
+// back at the end and status[0] = tasks walked.
+template <bool KEYED>
 __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   __shared__ ZwalkLDS S;
 #ifdef PVT_STAMPS
@@ -114,9 +124,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   uint64_t n_chunks = 0, n_switch = 0;
 #endif
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int base = A.coff[b];
-  const int nt = A.coff[b + 1] - base;
-  const int32_t* cmap = A.cmap + base;
+  const int base = KEYED ? 0 : A.coff[b];
+  const int nt = KEYED ? A.knt : A.coff[b + 1] - base;
+  const int32_t* cmap = KEYED ? nullptr : A.cmap + base;
   int32_t* status = A.status + 2 * b;
   const int Z = A.Z, H = A.H;
 
@@ -135,7 +145,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   double mx[4] = {-DINF, -DINF, -DINF, -DINF}, mn[4] = {DINF, DINF, DINF, DINF};
   bool bad = false;
   for (int i = tid; i < nt; i += ZW_THREADS) {
-    const int w = cmap[i];
+    const int w = KEYED ? i : cmap[i];
     const int a = A.anc[w];
     if (a < 0 || a >= Z) { bad = true; continue; }
     um |= S.amask[a];
@@ -149,9 +159,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   }
   // host minima from the partials
   double ha[4] = {DINF, DINF, DINF, DINF};
-  for (int k = tid; k < ZW_MINB; k += ZW_THREADS)
+  if (!KEYED)
+    for (int k = tid; k < ZW_MINB; k += ZW_THREADS)
 #pragma unroll
-    for (int r = 0; r < 4; r++) ha[r] = fmin(ha[r], A.hmin[k * 4 + r]);
+      for (int r = 0; r < 4; r++) ha[r] = fmin(ha[r], A.hmin[k * 4 + r]);
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     mx[r] = wave_max_d(mx[r]);
@@ -176,17 +187,23 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     mn[r] = fmin(mn[r], S.red[0][4 + r]);
     ha[r] = fmin(ha[r], S.red[0][8 + r]);
   }
-  bool sep = false;
+  bool sep = KEYED;
 #pragma unroll
   for (int r = 0; r < 4; r++) sep |= (ha[r] - mx[r] >= 0x1p-288);
   const uint32_t U = S.umask;
   if (S.bail || !sep || nt <= 0) {
-    if (tid == 0) { status[0] = -2; status[1] = 0; }
+    if (tid == 0) { status[0] = KEYED ? 0 : -2; status[1] = 0; }
     return;
+  }
+  if (KEYED) {                               // window: the zero-key prefix's first hosts
+    const int nw = min(A.kn, ZW_M);
+    for (int p = tid; p < nw; p += ZW_THREADS) { S.wid[p] = A.lo + A.kperm[p]; S.wz[p] = 0; }
+    if (tid == 0) S.nwin = nw;
+    __syncthreads();
   }
 
   // window: U's hosts in index order (passes of ZW_SCAN x 256 hosts, stable compaction)
-  for (int h0 = 0; h0 < H; h0 += ZW_SCAN * ZW_THREADS) {
+  for (int h0 = 0; h0 < (KEYED ? 0 : H); h0 += ZW_SCAN * ZW_THREADS) {
     const int have = S.nwin;
     if (have >= ZW_M) break;
     bool hit[ZW_SCAN];
@@ -237,7 +254,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   if (wbad) S.bail = 1;
   __syncthreads();
   if (S.bail || nwin == 0) {
-    if (tid == 0) { status[0] = -2; status[1] = 0; }
+    if (tid == 0) { status[0] = KEYED ? 0 : -2; status[1] = 0; }
     return;
   }
   if (wave != 0) return;
@@ -303,7 +320,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   load_b(1);
   for (int i0 = 0; i0 < nt && !failed; i0 += 64) {
     const int ti = i0 + lane;
-    const int tw = ti < nt ? cmap[ti] : 0;
+    const int tw = ti < nt ? (KEYED ? ti : cmap[ti]) : 0;
     double td[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) td[r] = A.dem[(size_t)tw * 4 + r];
@@ -318,16 +335,16 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       if (a != cur) {
         // certificates 2 / 3 for this anchor's zone row
         bool ok = true;
-        if (lane < Z) {
+        if (!KEYED && lane < Z) {
           const double c = S.csum[a * Z + lane], bw = S.bsum[a * Z + lane];
           if (c == 0.0) ok = bw > 0.0;
           else if (!((U >> lane) & 1u)) ok = (c >= 0x1p-300) && (bw <= 0x1p300);
         }
         if (__ballot(!ok)) { failed = true; break; }
-        const uint32_t am = S.amask[a];
+        const uint32_t am = KEYED ? ~0u : S.amask[a];   // keyed: every prefix host is zero-key
         for (int c = 0; c < nch; c++) {
           const int p = c * 64 + lane;
-          const uint64_t m = __ballot(p < nwin && ((am >> S.wz[min(p, nwin - 1)]) & 1u));
+          const uint64_t m = __ballot(p < nwin && (KEYED || ((am >> S.wz[min(p, nwin - 1)]) & 1u)));
           if (lane == 0) S.zm[c] = m;
           if (c == p0) rzm = m;
           if (c == pb) bzm = m;
@@ -355,7 +372,8 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // every window capacity and chain demand is finite with |x| <= 2^500 (certificate 3), so
       // a - d is exact in sign (a >= d iff a - d >= +-0) and is the capacity after a commit.
       const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
-      const uint64_t fm0 = __ballot(fmin(fmin(n0, n1), fmin(n2, n3)) >= 0.0) & rvalid;
+      // (keyed first-fit: strict fit, a > d iff a - d > 0)
+      const uint64_t fm0 = __ballot(fit_res<KEYED>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
       bool found = true;
 #ifdef PVT_STAMPS
       n_chunks++;
@@ -377,7 +395,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           // no host of chunk p0 fits this task: its winner is chunk pb's first fitting zero-cost
           // host, from registers (a dead chunk p0 is moved on by the general path below)
           const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
-          const uint64_t fb = __ballot(fmin(fmin(q0, q1), fmin(q2, q3)) >= 0.0) & bvalid;
+          const uint64_t fb = __ballot(fit_res<KEYED>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
           if ((fb & bzm) != 0 && (fb & ~bzm) == 0) {
             const bool win = lane == __builtin_ctzll(fb & bzm);
             rb0 = win ? q0 : rb0; rb1 = win ? q1 : rb1; rb2 = win ? q2 : rb2; rb3 = win ? q3 : rb3;
@@ -412,14 +430,14 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
               found = true;
               break;
             }
-            if (__ballot(((rvalid >> lane) & 1ull) && fits<false>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
+            if (__ballot(((rvalid >> lane) & 1ull) && fits<KEYED>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
               break;                           // chunk p0 still useful: look further in LDS
             store_chunk(p0);                   // dead: move the register chunk on
             if (++p0 >= nch) break;
             rzm = S.zm[p0];
             load_chunk(p0);
             g0 = ra0 - d0; g1 = ra1 - d1; g2 = ra2 - d2; g3 = ra3 - d3;
-            fm = __ballot(fmin(fmin(g0, g1), fmin(g2, g3)) >= 0.0) & rvalid;
+            fm = __ballot(fit_res<KEYED>(fmin(fmin(g0, g1), fmin(g2, g3)))) & rvalid;
             m = fm & rzm;
           }
           if (!found && p0 < nch) {
@@ -433,7 +451,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
               const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
               const int32_t id = S.wid[q];
               const uint64_t zm = S.zm[c];
-              const bool f = p < nwin && fits<false>(a0, a1, a2, a3, d0, d1, d2, d3);
+              const bool f = p < nwin && fits<KEYED>(a0, a1, a2, a3, d0, d1, d2, d3);
               const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
               const uint64_t mc = __ballot(f && k0);
               if (mc) {
@@ -464,7 +482,17 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       A.placement[tcal] = id;
     }
   }
-  if (lane == 0) { status[0] = failed ? -2 : done; status[1] = 0; }
+  if (KEYED) {   // the window's capacities to global availability: the keyed path goes on there
+    store_chunk(p0);
+    store_b();
+    wave_lds_sync();
+    for (int p = lane; p < nwin; p += 64) {
+      const int h = S.wid[p];
+#pragma unroll
+      for (int r = 0; r < 4; r++) A.wb[(size_t)r * H + h] = S.wa[r][p];
+    }
+  }
+  if (lane == 0) { status[0] = (failed && !KEYED) ? -2 : done; status[1] = 0; }
 #ifdef PVT_STAMPS
   if (lane == 0 && A.stamps) {
     const uint64_t t_end = zstamp();
@@ -482,7 +510,10 @@ void launch_host_min(const double* avail, int H, double* part, hipStream_t st) {
 }
 
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st) {
-  hipLaunchKernelGGL(zwalk_kernel, dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+  hipLaunchKernelGGL(zwalk_kernel<false>, dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+}
+void launch_zwalk_keyed(const ZwalkArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(zwalk_kernel<true>, dim3(1), dim3(ZW_THREADS), 0, st, a);
 }
 
 }  // namespace pvt
