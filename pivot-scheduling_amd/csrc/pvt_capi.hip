@@ -783,12 +783,15 @@ static int keyed_full_sort(pvt_ctx* ctx) {
   return PVT_OK;
 }
 
+static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a frontier-walk launch
+
 // Size of the next window at R.t0 (0: the round is done). Computes the frozen first-fit key of
 // this context's hosts at a group start (cost_aware.py:118-119, on the current capacities).
 static int round_next_window(pvt_ctx* ctx, int* nt_out) {
   RoundState& R = ctx->rs;
   *nt_out = 0;
   if (!R.active) return fail(ctx, PVT_EINVAL, "no round in progress");
+  for (;;) {                      // (a group the keyed frontier walk completed: the next one)
   while (R.g < R.ngroups && R.t0 >= (R.keyed ? R.gstart[R.g + 1] : R.T)) R.g++;
   if (R.g >= R.ngroups || R.T == 0) return PVT_OK;
   const int ge = R.keyed ? R.gstart[R.g + 1] : R.T;
@@ -801,23 +804,57 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
     KeyArgs ka{R.r.avail, R.r.zone, R.r.decay, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z,
                R.ganchor[R.g], R.lo, R.hi, P<double>(ctx->key),
                R.r.rt_bw ? R.r.rt_bw + (size_t)R.gid[R.g] * R.H : nullptr};
-    Scope sc(ctx, PVT_K_OTHER, 0, 0);
-    launch_key(ka, ctx->stream);
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_key(ka, ctx->stream);
+    }
     if (R.kscan) {
       // The group's host order (cost_aware.py:118-119). Hosts of zero key (the anchor zone's:
       // no egress cost) come first, in host order; when there are enough of them the rest is
       // sorted only if a walk ever exhausts that prefix (kstall).
       const int n = R.hi - R.lo;
       const double* kin = P<double>(ctx->key) + R.lo;
-      launch_zero_key_flags(kin, n, P<uint8_t>(ctx->kflag), ctx->stream);
-      size_t tmp = ctx->ksorttmp.n;
-      HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(ctx->ksorttmp), tmp, P<int32_t>(ctx->kiota),
-                                           P<uint8_t>(ctx->kflag), P<int32_t>(ctx->kperm),
-                                           P<int32_t>(ctx->next) + 2, n, ctx->stream));
-      HIPCHK(hipMemcpyAsync(ctx->next_host + 2, P<int32_t>(ctx->next) + 2, sizeof(int32_t),
+      {
+        Scope sc(ctx, PVT_K_OTHER, 0, 0);
+        launch_zero_key_flags(kin, n, P<uint8_t>(ctx->kflag), ctx->stream);
+        size_t tmp = ctx->ksorttmp.n;
+        HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(ctx->ksorttmp), tmp, P<int32_t>(ctx->kiota),
+                                             P<uint8_t>(ctx->kflag), P<int32_t>(ctx->kperm),
+                                             P<int32_t>(ctx->next) + 2, n, ctx->stream));
+      }
+      // The frontier walk (pvt_zwalk.hip, keyed mode) takes the group's first tasks from the
+      // group start: each takes the first prefix host, in host order, that strictly fits, which
+      // is the keyed order's answer whatever the prefix length (zero-key hosts lead it in both
+      // modes below); it stops at the first task no host of the prefix's first ZW_M fits, and
+      // the windowed list path goes on from there with the same frozen key. Launched on the
+      // prefix length as the device holds it, read back with it in one synchronisation.
+      const int n_g = ge - R.t0;
+      const bool zk = ctx->zwalk && R.lo == 0 && R.hi == R.H && R.world == 1 &&
+                      R.t0 == R.gstart[R.g] && n_g >= KEYED_FRONTIER_MIN && !R.r.rt_bw &&
+                      R.Z <= ZMAX;
+      if (zk) {
+        ENSURE(ctx->wres, sizeof(WinRec) * (size_t)n_g);
+        const pvt_round* r = &R.r;
+        ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)R.t0 * 4,
+                     P<int32_t>(ctx->anc_ord) + R.t0, R.ord + R.t0, P<double>(ctx->csum),
+                     P<double>(ctx->bsum), nullptr, nullptr, P<int32_t>(ctx->next),
+                     P<WinRec>(ctx->wres), r->placement, nullptr, ctx->stamps,
+                     P<int32_t>(ctx->kperm), 0, R.lo, n_g, r->avail, P<int32_t>(ctx->next) + 2};
+        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+        launch_zwalk_keyed(za, ctx->stream);
+      }
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t) * 3,
                             hipMemcpyDeviceToHost, ctx->stream));
       HIPCHK(hipStreamSynchronize(ctx->stream));
       const int nz = ctx->next_host[2];
+      if (zk) {
+        const int done = ctx->next_host[0];
+        if (done < 0 || done > n_g)
+          return fail(ctx, PVT_EHIP, "keyed frontier walk returned %d of %d", done, n_g);
+        ctx->n_zchains += done > 0;
+        R.t0 += done;
+      }
       if (nz >= KPREFIX_MIN && nz < n) {
         R.kmode = 1;
         R.kn = nz;
@@ -828,9 +865,11 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
     }
     R.key_group = (int)R.g;
   }
+  if (R.t0 >= ge) continue;       // the frontier walk took the whole group
   R.nt = std::min(R.W, ge - R.t0);
   *nt_out = R.nt;
   return PVT_OK;
+  }
 }
 
 // Exact candidate lists of tasks [t0, t0 + nt) over hosts [lo, hi) into list buffer `lb`, on
@@ -927,54 +966,6 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
   return PVT_OK;
 }
 
-// cost_aware first-fit with sort_hosts while the group's zero-key prefix lasts (kmode 1): every
-// task takes the first prefix host, in host order, that strictly fits -- the frontier walk
-// (pvt_zwalk.hip, keyed mode) does exactly that over the prefix's first ZW_M hosts from the
-// group start, in registers, and stops at the first task none of them fits; the windowed list
-// path (frozen key and prefix unchanged) continues from there. Unsharded rounds only.
-static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a launch + synchronisation
-static int keyed_frontier(pvt_ctx* ctx) {
-  RoundState& R = ctx->rs;
-  const pvt_round* r = &R.r;
-  if (!ctx->zwalk || !R.keyed || !R.kscan || R.kmode != 1 || R.lo != 0 || R.hi != R.H ||
-      R.world != 1 || R.g >= R.ngroups || R.t0 != R.gstart[R.g] || r->rt_bw || R.Z > ZMAX)
-    return PVT_OK;
-  const int n = R.gstart[R.g + 1] - R.t0;
-  if (n < KEYED_FRONTIER_MIN || R.kn <= 0) return PVT_OK;
-  hipStream_t st = ctx->stream;
-  ENSURE(ctx->wres, sizeof(WinRec) * (size_t)n);
-  int32_t* status = P<int32_t>(ctx->next);
-  ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)R.t0 * 4,
-               P<int32_t>(ctx->anc_ord) + R.t0, R.ord + R.t0, P<double>(ctx->csum),
-               P<double>(ctx->bsum), nullptr, nullptr, status, P<WinRec>(ctx->wres),
-               r->placement, nullptr, ctx->stamps, P<int32_t>(ctx->kperm), R.kn, R.lo, n,
-               r->avail};
-  {
-    Scope sc(ctx, PVT_K_COMMIT, 0, 0);
-    launch_zwalk_keyed(za, st);
-  }
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
-  const int done = ctx->next_host[0];
-  if (done < 0 || done > n) return fail(ctx, PVT_EHIP, "keyed frontier walk returned %d of %d", done, n);
-  ctx->n_zchains += done > 0;
-  R.t0 += done;
-  return PVT_OK;
-}
-
-// The next window, after the keyed frontier walk has taken what it can at a group start.
-static int next_window(pvt_ctx* ctx, int* nt) {
-  RoundState& R = ctx->rs;
-  for (;;) {
-    int rc = round_next_window(ctx, nt);
-    if (rc || *nt == 0) return rc;
-    const int t = R.t0;
-    if ((rc = keyed_frontier(ctx))) return rc;
-    if (R.t0 == t) return PVT_OK;
-  }
-}
-
 // pvt_place for the list policies. While window k is walked on the caller's stream, the side
 // stream scores window k+1 on the capacities as they stand (the walk of k-1 is complete; the
 // walk of k is in flight): an event recorded just before walk k releases it. The side stream
@@ -986,7 +977,7 @@ static int next_window(pvt_ctx* ctx, int* nt) {
 static int place_pipelined(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   int rc, nt = 0;
-  if ((rc = next_window(ctx, &nt))) return rc;
+  if ((rc = round_next_window(ctx, &nt))) return rc;
   if (nt == 0) return PVT_OK;
   int lb = 0, t0 = R.t0;
   if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
@@ -1014,7 +1005,7 @@ static int place_pipelined(pvt_ctx* ctx) {
     }
     if (nnt > 0) HIPCHK(hipStreamSynchronize(ctx->side));   // discard the speculation
     R.t0 = t0 + adv;
-    if ((rc = next_window(ctx, &nt))) return rc;
+    if ((rc = round_next_window(ctx, &nt))) return rc;
     if (nt == 0) break;
     t0 = R.t0; lb = 0; n_prev = 0; inherited = false;
     if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
@@ -1207,7 +1198,7 @@ static int place_epochs(pvt_ctx* ctx) {
                    P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                    P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
                    P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
-                   nullptr, 0, 0, 0, nullptr};
+                   nullptr, 0, 0, 0, nullptr, nullptr};
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0);
         launch_zwalk(za, nch, st);

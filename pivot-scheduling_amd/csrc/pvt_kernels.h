@@ -216,6 +216,7 @@ struct ZwalkArgs {
   const int32_t* kperm;
   int kn, lo, knt;
   double* wb;
+  const int32_t* kn_dev;  // keyed: prefix length read on the device (NULL: kn)
 };
 constexpr int ZW_MIN_PARTS = 256;
 void launch_host_min(const double* avail, int H, double* part, hipStream_t st);   // [256][4]

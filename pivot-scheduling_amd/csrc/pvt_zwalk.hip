@@ -196,7 +196,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     return;
   }
   if (KEYED) {                               // window: the zero-key prefix's first hosts
-    const int nw = min(A.kn, ZW_M);
+    const int nw = min(A.kn_dev ? *A.kn_dev : A.kn, ZW_M);
     for (int p = tid; p < nw; p += ZW_THREADS) { S.wid[p] = A.lo + A.kperm[p]; S.wz[p] = 0; }
     if (tid == 0) S.nwin = nw;
     __syncthreads();
