@@ -43,6 +43,10 @@ static constexpr int EP_SEG_OFF = 0, EP_SEG_CHAIN = EP_SEG_OFF + EPOCH_SEGS + 1,
                      EP_CMAP = EP_CSEG + EPOCH_SEGS, EP_STATUS = EP_CMAP + EPOCH_MAX,
                      EP_BAD = EP_STATUS + 2 * EPOCH_SEGS, EP_RES = EP_BAD + EPOCH_SEGS;
 static constexpr int EP_WORDS = EP_RES + 8;
+static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a frontier-walk launch
+static constexpr int ORDERED_FRONTIER_MIN = 32;  // tasks a frontier attempt must place to go on
+static int ORDERED_FRONTIER_TASKS = 1024;         // tasks per frontier attempt (PVT_OF_TASKS)
+static constexpr int ORDERED_FRONTIER_HOSTS = 65536;   // first span of hosts the window is taken from
 
 struct Buf {
   void* p = nullptr;
@@ -82,6 +86,8 @@ struct RoundState {
   std::vector<int> egs, ega;      // cost_aware best-fit epochs: group starts (+ T) and anchors
   std::vector<int> ecomp;         // zone -> its component of zones joined by zero egress cost
   bool in_epoch = false;          // lists scored for an epoch (place_epochs)
+  bool ofront = false;            // ordered first-fit rounds walked by the frontier walk
+  int ofh = 0;                    // hosts the frontier window is taken from
   // grouped rounds: per-group task counts, group anchors and (cost_aware) the cost table,
   // copied to the host once by build_order (one synchronisation) for the group plans
   bool ginfo = false;
@@ -736,6 +742,25 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
       launch_iota(P<int32_t>(ctx->kiota), n, st);
     }
   }
+  // vbp first-fit / unsorted cost_aware first-fit: the frontier walk over the first alive hosts
+  // (ordered_frontier); its scratch is the keyed path's (the modes exclude each other)
+  R.ofront = ctx->zwalk && R.ordered && lo == 0 && hi == H && world == 1 &&
+             T >= ORDERED_FRONTIER_MIN && H >= 64;
+  if (R.ofront) {
+    if (const char* e = getenv("PVT_OF_TASKS")) ORDERED_FRONTIER_TASKS = std::max(32, atoi(e));   // tuning
+    R.ofh = ORDERED_FRONTIER_HOSTS;
+    if (const char* e = getenv("PVT_OF_HOSTS")) R.ofh = std::max(ZW_M, atoi(e));   // tuning
+    ENSURE(ctx->next, sizeof(int32_t) * 4);
+    ENSURE(ctx->kperm, sizeof(int32_t) * (size_t)H);
+    ENSURE(ctx->kiota, sizeof(int32_t) * (size_t)H);
+    ENSURE(ctx->kflag, (size_t)H);
+    ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+    size_t tmp2 = 0;
+    HIPCHK(hipcub::DeviceSelect::Flagged(nullptr, tmp2, P<int32_t>(ctx->kiota), P<uint8_t>(ctx->kflag),
+                                         P<int32_t>(ctx->kperm), P<int32_t>(ctx->next) + 2, H, st));
+    ENSURE(ctx->ksorttmp, tmp2);
+    launch_iota(P<int32_t>(ctx->kiota), H, st);
+  }
   R.gstart.push_back(T);
   R.ngroups = R.keyed ? R.ganchor.size() : 1;
   R.key_group = -1;
@@ -782,8 +807,6 @@ static int keyed_full_sort(pvt_ctx* ctx) {
   R.kn = n;
   return PVT_OK;
 }
-
-static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a frontier-walk launch
 
 // Size of the next window at R.t0 (0: the round is done). Computes the frozen first-fit key of
 // this context's hosts at a group start (cost_aware.py:118-119, on the current capacities).
@@ -841,7 +864,7 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
                      P<WinRec>(ctx->wres), r->placement, nullptr, ctx->stamps,
                      P<int32_t>(ctx->kperm), 0, R.lo, n_g, r->avail, P<int32_t>(ctx->next) + 2};
         Scope sc(ctx, PVT_K_COMMIT, 0, 0);
-        launch_zwalk_keyed(za, ctx->stream);
+        launch_zwalk_keyed(za, true, ctx->stream);
       }
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t) * 3,
@@ -966,6 +989,63 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
   return PVT_OK;
 }
 
+// vbp first-fit and unsorted cost_aware first-fit (host index order; fit >= / strict): the
+// frontier walk (pvt_zwalk.hip, keyed mode) over the first ZW_M alive hosts -- those fitting the
+// smallest demand of the remaining tasks, in index order; no other host can take any of them --
+// takes tasks until one fits no window host; the window is rebuilt from the current capacities
+// and the walk goes on while each attempt places at least ORDERED_FRONTIER_MIN tasks, then one
+// list window (which handles tasks that fit far away or nowhere) and the frontier again.
+static int ordered_frontier(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  if (!R.ofront) return PVT_OK;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  const bool strict = r->mode == PVT_CA_FF;
+  while (R.T - R.t0 >= ORDERED_FRONTIER_MIN) {
+    // a bounded task prefix: its smallest demand is close to each task's own (decreasing
+    // orders), so hosts filled too far for it leave the window
+    const int n = std::min(R.T - R.t0, ORDERED_FRONTIER_TASKS);
+    const double* dem = P<double>(ctx->dem_ord) + (size_t)R.t0 * 4;
+    // the window comes from the first R.ofh hosts (a window of fewer than ZW_M hosts stops the
+    // walk at the first task fitting none of them, which is still the answer for the tasks
+    // before it); the span doubles when an attempt stops on a short window
+    const int hs = std::min(R.ofh, R.H);
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_alive_flags(r->avail, R.H, hs, dem, n, strict ? 1 : 0, P<double>(ctx->hmin),
+                         P<uint8_t>(ctx->kflag), st);
+      size_t tmp = ctx->ksorttmp.n;
+      HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(ctx->ksorttmp), tmp, P<int32_t>(ctx->kiota),
+                                           P<uint8_t>(ctx->kflag), P<int32_t>(ctx->kperm),
+                                           P<int32_t>(ctx->next) + 2, hs, st));
+    }
+    ENSURE(ctx->wres, sizeof(WinRec) * (size_t)n);
+    ZwalkArgs za{r->avail, r->zone, R.H, R.Z, dem, P<int32_t>(ctx->anc_ord) + R.t0, R.ord + R.t0,
+                 nullptr, nullptr, nullptr, nullptr, P<int32_t>(ctx->next), P<WinRec>(ctx->wres),
+                 r->placement, nullptr, ctx->stamps, P<int32_t>(ctx->kperm), 0, 0, n, r->avail,
+                 P<int32_t>(ctx->next) + 2};
+    {
+      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+      launch_zwalk_keyed(za, strict, st);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t) * 3,
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    const int done = ctx->next_host[0];
+    if (done < 0 || done > n) return fail(ctx, PVT_EHIP, "ordered frontier walk returned %d of %d", done, n);
+    ctx->n_zchains += done > 0;
+    R.t0 += done;
+    const bool short_window = ctx->next_host[2] < ZW_M && hs < R.H;
+    if (done < n && short_window) {
+      R.ofh = (int)std::min<int64_t>((int64_t)R.ofh * 2, R.H);
+      if (done == 0) continue;
+    }
+    if (done < ORDERED_FRONTIER_MIN) break;
+  }
+  return PVT_OK;
+}
+
 // pvt_place for the list policies. While window k is walked on the caller's stream, the side
 // stream scores window k+1 on the capacities as they stand (the walk of k-1 is complete; the
 // walk of k is in flight): an event recorded just before walk k releases it. The side stream
@@ -977,6 +1057,7 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
 static int place_pipelined(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   int rc, nt = 0;
+  if ((rc = ordered_frontier(ctx))) return rc;
   if ((rc = round_next_window(ctx, &nt))) return rc;
   if (nt == 0) return PVT_OK;
   int lb = 0, t0 = R.t0;
@@ -986,7 +1067,8 @@ static int place_pipelined(pvt_ctx* ctx) {
   for (;;) {
     // Walk k, and beside it window k+1 (same group) scored on the state walk k-1 left.
     const int nt0 = t0 + nt, ge = group_end(R, t0);
-    const int nnt = (ctx->pipeline && nt0 < ge) ? std::min(R.W, ge - nt0) : 0;
+    // (ordered frontier rounds: no speculative window; the frontier walk is tried after each)
+    const int nnt = (ctx->pipeline && nt0 < ge && !R.ofront) ? std::min(R.W, ge - nt0) : 0;
     if (nnt > 0) HIPCHK(hipEventRecord(ctx->ev_walk, ctx->stream));
     if ((rc = walk_launch(ctx, t0, nt, lb, n_prev))) return rc;
     if (nnt > 0) {
@@ -1005,6 +1087,7 @@ static int place_pipelined(pvt_ctx* ctx) {
     }
     if (nnt > 0) HIPCHK(hipStreamSynchronize(ctx->side));   // discard the speculation
     R.t0 = t0 + adv;
+    if ((rc = ordered_frontier(ctx))) return rc;
     if ((rc = round_next_window(ctx, &nt))) return rc;
     if (nt == 0) break;
     t0 = R.t0; lb = 0; n_prev = 0; inherited = false;

@@ -221,7 +221,11 @@ struct ZwalkArgs {
 constexpr int ZW_MIN_PARTS = 256;
 void launch_host_min(const double* avail, int H, double* part, hipStream_t st);   // [256][4]
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st);
-void launch_zwalk_keyed(const ZwalkArgs& a, hipStream_t st);
+constexpr int ZW_M = 1024;                 // frontier-walk window hosts
+void launch_zwalk_keyed(const ZwalkArgs& a, bool strict, hipStream_t st);
+// ordered first-fit frontier: flags[h] = host h fits the smallest demand of tasks dem[0, n)
+void launch_alive_flags(const double* avail, int H, int hs, const double* dem, int n, int strict,
+                        double* dmin, uint8_t* flags, hipStream_t st);
 
 // cost_aware first-fit with sort_hosts, as the reference runs it (cost_aware.py:118-124): the
 // hosts sorted once per group by the frozen key (perm, skey = sorted key bits; the radix sort

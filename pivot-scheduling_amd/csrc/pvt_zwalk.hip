@@ -37,7 +37,6 @@
 
 namespace pvt {
 
-constexpr int ZW_M = 1024;                 // window hosts
 constexpr int ZW_CH = ZW_M / 64;           // window chunks (one wave step each)
 constexpr int ZW_THREADS = 256;
 constexpr int ZW_WAVES = ZW_THREADS / 64;
@@ -45,6 +44,7 @@ constexpr int ZW_SCAN = 16;                // hosts per thread per window-build 
 constexpr int ZW_MINB = ZW_MIN_PARTS;      // blocks of the host-minimum pass
 constexpr double ZW_BIG = 0x1p500;
 
+constexpr int ZW_SB = 64;                  // suffix-minimum batches (the last one holds the rest)
 struct ZwalkLDS {
   double wa[4][ZW_M];                      // window capacities (live)
   int32_t wid[ZW_M];                       // window hosts (ascending index)
@@ -53,6 +53,7 @@ struct ZwalkLDS {
   double csum[ZMAX * ZMAX], bsum[ZMAX * ZMAX];
   int32_t cnt[ZW_SCAN][ZW_WAVES];          // window build: hits per (pass row, wave)
   double red[ZW_WAVES][12];                // block reductions: max d, min d, min avail
+  double smin[ZW_SB][4];                   // suffix minima of the demands, per 64-task batch
   double lg[64][4];                        // the batch's log: capacities after each commit
   int32_t lgid[64];                        //   and the host
   uint32_t amask[ZMAX];                    // anchor -> its zero-cost zones
@@ -116,7 +117,9 @@ __device__ __forceinline__ uint64_t zstamp() {
 // window the first ZW_M hosts of the group's zero-key prefix (perm, index order), strict fit,
 // no zone certificates (the order is the keyed path's own); the window's capacities are written
 // back at the end and status[0] = tasks walked.
-template <bool KEYED>
+// KEYED with STRICT = false: vbp first-fit (index order, fit >=) over a window of the first
+// alive hosts (pvt_capi.hip ordered_frontier), same mechanics.
+template <bool KEYED, bool STRICT>
 __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   __shared__ ZwalkLDS S;
 #ifdef PVT_STAMPS
@@ -130,10 +133,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   int32_t* status = A.status + 2 * b;
   const int Z = A.Z, H = A.H;
 
-  for (int i = tid; i < Z * Z; i += ZW_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
+  if (!KEYED)   // (keyed / ordered rounds: no zone tables; vbp rounds have none)
+    for (int i = tid; i < Z * Z; i += ZW_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
   if (tid == 0) { S.umask = 0; S.nwin = 0; S.bail = 0; }
   __syncthreads();
-  if (tid < Z) {                             // anchor row -> zero-cost zone mask
+  if (!KEYED && tid < Z) {                   // anchor row -> zero-cost zone mask
     uint32_t m = 0;
     for (int z = 0; z < Z; z++) m |= (S.csum[tid * Z + z] == 0.0) ? (1u << z) : 0u;
     S.amask[tid] = m;
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     const int w = KEYED ? i : cmap[i];
     const int a = A.anc[w];
     if (a < 0 || a >= Z) { bad = true; continue; }
-    um |= S.amask[a];
+    if (!KEYED) um |= S.amask[a];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const double d = A.dem[(size_t)w * 4 + r];
@@ -257,6 +261,28 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     if (tid == 0) { status[0] = KEYED ? 0 : -2; status[1] = 0; }
     return;
   }
+  // suffix minima of the chain's demands per 64-task batch: a chunk no host of which fits the
+  // smallest demand still ahead is dead (the walk moves its register chunk past it)
+  const int nsb = min((nt + 63) >> 6, ZW_SB);
+  for (int blk = wave; blk < nsb; blk += ZW_WAVES) {
+    const int i1 = blk == ZW_SB - 1 ? nt : min(nt, blk * 64 + 64);
+    double bm[4] = {DINF, DINF, DINF, DINF};
+    for (int i = blk * 64 + lane; i < i1; i += 64) {
+      const int w = KEYED ? i : cmap[i];
+#pragma unroll
+      for (int r = 0; r < 4; r++) bm[r] = fmin(bm[r], A.dem[(size_t)w * 4 + r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) bm[r] = wave_min_d(bm[r]);
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) S.smin[blk][r] = bm[r];
+    }
+  }
+  __syncthreads();
+  if (tid < 4)
+    for (int blk = nsb - 2; blk >= 0; blk--) S.smin[blk][tid] = fmin(S.smin[blk][tid], S.smin[blk + 1][tid]);
+  __syncthreads();
   if (wave != 0) return;
 #ifdef PVT_STAMPS
   const uint64_t t_walk = zstamp();
@@ -319,6 +345,8 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   load_chunk(0);
   load_b(1);
   for (int i0 = 0; i0 < nt && !failed; i0 += 64) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) mn[r] = S.smin[min(i0 >> 6, ZW_SB - 1)][r];
     const int ti = i0 + lane;
     const int tw = ti < nt ? (KEYED ? ti : cmap[ti]) : 0;
     double td[4];
@@ -373,7 +401,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // a - d is exact in sign (a >= d iff a - d >= +-0) and is the capacity after a commit.
       const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
       // (keyed first-fit: strict fit, a > d iff a - d > 0)
-      const uint64_t fm0 = __ballot(fit_res<KEYED>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
+      const uint64_t fm0 = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
       bool found = true;
 #ifdef PVT_STAMPS
       n_chunks++;
@@ -395,7 +423,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           // no host of chunk p0 fits this task: its winner is chunk pb's first fitting zero-cost
           // host, from registers (a dead chunk p0 is moved on by the general path below)
           const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
-          const uint64_t fb = __ballot(fit_res<KEYED>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
+          const uint64_t fb = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
           if ((fb & bzm) != 0 && (fb & ~bzm) == 0) {
             const bool win = lane == __builtin_ctzll(fb & bzm);
             rb0 = win ? q0 : rb0; rb1 = win ? q1 : rb1; rb2 = win ? q2 : rb2; rb3 = win ? q3 : rb3;
@@ -430,14 +458,14 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
               found = true;
               break;
             }
-            if (__ballot(((rvalid >> lane) & 1ull) && fits<KEYED>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
+            if (__ballot(((rvalid >> lane) & 1ull) && fits<STRICT>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
               break;                           // chunk p0 still useful: look further in LDS
             store_chunk(p0);                   // dead: move the register chunk on
             if (++p0 >= nch) break;
             rzm = S.zm[p0];
             load_chunk(p0);
             g0 = ra0 - d0; g1 = ra1 - d1; g2 = ra2 - d2; g3 = ra3 - d3;
-            fm = __ballot(fit_res<KEYED>(fmin(fmin(g0, g1), fmin(g2, g3)))) & rvalid;
+            fm = __ballot(fit_res<STRICT>(fmin(fmin(g0, g1), fmin(g2, g3)))) & rvalid;
             m = fm & rzm;
           }
           if (!found && p0 < nch) {
@@ -451,7 +479,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
               const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
               const int32_t id = S.wid[q];
               const uint64_t zm = S.zm[c];
-              const bool f = p < nwin && fits<KEYED>(a0, a1, a2, a3, d0, d1, d2, d3);
+              const bool f = p < nwin && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
               const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
               const uint64_t mc = __ballot(f && k0);
               if (mc) {
@@ -510,10 +538,48 @@ void launch_host_min(const double* avail, int H, double* part, hipStream_t st) {
 }
 
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st) {
-  hipLaunchKernelGGL(zwalk_kernel<false>, dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+  hipLaunchKernelGGL((zwalk_kernel<false, false>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
 }
-void launch_zwalk_keyed(const ZwalkArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(zwalk_kernel<true>, dim3(1), dim3(ZW_THREADS), 0, st, a);
+void launch_zwalk_keyed(const ZwalkArgs& a, bool strict, hipStream_t st) {
+  if (strict) hipLaunchKernelGGL((zwalk_kernel<true, true>), dim3(1), dim3(ZW_THREADS), 0, st, a);
+  else hipLaunchKernelGGL((zwalk_kernel<true, false>), dim3(1), dim3(ZW_THREADS), 0, st, a);
+}
+
+// Ordered frontier: the smallest demand (per dimension) of tasks [0, n), then the hosts that
+// fit it (the alive hosts: no other can fit any of those tasks), as flags for a compaction.
+__global__ __launch_bounds__(1024) void dem_min_kernel(const double* dem, int n, double* out) {
+  __shared__ double red[16][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double m[4] = {DINF, DINF, DINF, DINF};
+  for (int i = tid; i < n; i += 1024)
+#pragma unroll
+    for (int r = 0; r < 4; r++) m[r] = fmin(m[r], dem[(size_t)i * 4 + r]);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    m[r] = wave_min_d(m[r]);
+    if (lane == 0) red[wave][r] = m[r];
+  }
+  __syncthreads();
+  if (tid < 4) {
+    double v = red[0][tid];
+    for (int w = 1; w < 16; w++) v = fmin(v, red[w][tid]);
+    out[tid] = v;
+  }
+}
+__global__ void alive_flags_kernel(const double* avail, int H, int hs, const double* dmin,
+                                   int strict, uint8_t* flags) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= hs) return;
+  const double a0 = avail[h], a1 = avail[(size_t)H + h], a2 = avail[2 * (size_t)H + h],
+               a3 = avail[3 * (size_t)H + h];
+  flags[h] = strict ? fits<true>(a0, a1, a2, a3, dmin[0], dmin[1], dmin[2], dmin[3])
+                    : fits<false>(a0, a1, a2, a3, dmin[0], dmin[1], dmin[2], dmin[3]);
+}
+void launch_alive_flags(const double* avail, int H, int hs, const double* dem, int n, int strict,
+                        double* dmin, uint8_t* flags, hipStream_t st) {
+  hipLaunchKernelGGL(dem_min_kernel, dim3(1), dim3(1024), 0, st, dem, n, dmin);
+  hipLaunchKernelGGL(alive_flags_kernel, dim3((hs + 255) / 256), dim3(256), 0, st, avail, H, hs,
+                     dmin, strict, flags);
 }
 
 }  // namespace pvt
