@@ -263,6 +263,11 @@ def walk_roofline(ks, ep, steps, T):
     c = ks["commit"]
     ms = c["ms"] / max(steps, 1)
     longest = ep.get("longest_chain_tasks", 0)
+    sequential = longest <= 0 and ep.get("frontier_chains", 0) > 0
+    if sequential:
+        # first-fit rounds (keyed / ordered frontier walks): the walks run one after another,
+        # every task of the round on one of them
+        longest = T
     out = {"kernel": "zwalk (zero-cost frontier walk: one wave per epoch chain, window in LDS)",
            "bound": "issue", "unit": "instructions/s (one wave)", "traffic": None,
            "walk_ms_per_step": ms, "longest_chain_tasks": longest,
@@ -273,7 +278,12 @@ def walk_roofline(ks, ep, steps, T):
         return out
     tasks_per_s = longest / (ms * 1e-3)
     ipt = None
+    if sequential:
+        out["kernel"] = "zwalk (keyed / ordered frontier walks in sequence, window in LDS)"
+        out["note"] = "the walk's PMC profile is of the default line's launch; no instruction count here"
     try:
+        if sequential:
+            raise KeyError("no PMC profile of this mode")
         with open(WALK_PMC) as f:
             pmc = json.load(f)
         cnt = pmc["counters_per_launch"]
@@ -287,7 +297,7 @@ def walk_roofline(ks, ep, steps, T):
         traffic = 2.0 * cnt.get("FETCH_SIZE", 0.0) * 1024 + cnt.get("WRITE_SIZE", 0.0) * 1024
         out["traffic"] = traffic if traffic > 0 else None
     except (OSError, ValueError, KeyError):
-        out["note"] = "no PMC profile of the walk (tools/pmc_profile.py --kernel zwalk_kernel)"
+        out.setdefault("note", "no PMC profile of the walk (tools/pmc_profile.py --kernel zwalk_kernel)")
     out["cycles_per_task"] = SHADER_HZ / tasks_per_s
     out["latency_floor"] = {"peak_tasks_per_s": SHADER_HZ / LDS_DEP_CYCLES,
                             "achieved_tasks_per_s": tasks_per_s,
