@@ -344,16 +344,29 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   };
   load_chunk(0);
   load_b(1);
+  // task records, software-pipelined across 64-task batches: while batch b is walked, batch
+  // b + 1's records and batch b + 2's chain positions are in flight (no HBM latency at a batch
+  // start)
+  auto task_at = [&](int i) { return i < nt ? (KEYED ? i : cmap[i]) : 0; };
+  int nw = task_at(lane);
+  double nd0 = A.dem[(size_t)nw * 4 + 0], nd1 = A.dem[(size_t)nw * 4 + 1];
+  double nd2 = A.dem[(size_t)nw * 4 + 2], nd3 = A.dem[(size_t)nw * 4 + 3];
+  int nanc = A.anc[nw], ncal = A.ord[nw];
+  int nw1 = task_at(64 + lane);
   for (int i0 = 0; i0 < nt && !failed; i0 += 64) {
 #pragma unroll
     for (int r = 0; r < 4; r++) mn[r] = S.smin[min(i0 >> 6, ZW_SB - 1)][r];
-    const int ti = i0 + lane;
-    const int tw = ti < nt ? (KEYED ? ti : cmap[ti]) : 0;
-    double td[4];
-#pragma unroll
-    for (int r = 0; r < 4; r++) td[r] = A.dem[(size_t)tw * 4 + r];
-    const int tanc = A.anc[tw];
-    const int tcal = A.ord[tw];
+    const int tw = nw;
+    const double td[4] = {nd0, nd1, nd2, nd3};
+    const int tanc = nanc;
+    const int tcal = ncal;
+    if (i0 + 64 < nt) {                      // (uniform) batch b + 1's records, b + 2's positions
+      nw = nw1;
+      nd0 = A.dem[(size_t)nw * 4 + 0]; nd1 = A.dem[(size_t)nw * 4 + 1];
+      nd2 = A.dem[(size_t)nw * 4 + 2]; nd3 = A.dem[(size_t)nw * 4 + 3];
+      nanc = A.anc[nw]; ncal = A.ord[nw];
+      nw1 = task_at(i0 + 128 + lane);
+    }
     const int kn = min(64, nt - i0);
     int k = 0;
     for (; k < kn; k++) {
