@@ -38,6 +38,14 @@ if mode == 2:
     for k in (5, 6, 2):   # pass 3 split (stamp 2 then holds only its last part)
         print("  %-20s %8.0f cycles/task" % (sub[k], buf[k] / max(buf[7], 1)))
     sys.exit(0)
+if mode == 3 or os.environ.get("ZWALK"):
+    # frontier walk (pvt_zwalk.hip; vbp first-fit: ordered frontier attempts): prologue
+    # (window build, certificates, suffix minima), walk, chunk visits per task
+    print("frontier walk mode %d H=%d T=%d tasks=%d stats=%s %s" % (mode, H, T, buf[3], eng.last_stats(),
+                                                                    eng.epoch_stats()))
+    print("  prologue cycles total %.0f  walk cycles/task %.0f  chunk visits/task %.2f  anchor switches %d"
+          % (buf[0], buf[1] / max(buf[3], 1), buf[2] / max(buf[3], 1), buf[4]))
+    sys.exit(0)
 names = ["wait-prefetch", "hash-lookup", "untouched-pick", "touched-rescore", "commit"]
 tot = sum(buf[k] for k in range(5))
 print("mode %d H=%d T=%d tasks walked=%d stats=%s mean live touched=%.1f"
