@@ -139,6 +139,12 @@ int  pvt_set_window(pvt_ctx* ctx, int tasks);
 /* Tuning knob: tasks per wave of the best-fit score kernel, 0 (the policy's default: 2 for vbp
  * best-fit and for cost_aware below 262144 hosts, else 4), 2 or 4. Results are identical. */
 int  pvt_set_score_tw(pvt_ctx* ctx, int tw);
+/* Tuning knob: vbp best-fit rounds of at least min_hosts hosts (per shard) build their candidate
+ * lists from a memory band over the hosts sorted once per round by snapshot memory (hosts
+ * committed to since the snapshot are scanned with their live state) instead of streaming every
+ * host per task; 0 disables it. Default 65536. Results are identical either way. Replaces the
+ * per-task host scan of scheduler/vbp.py:43-47. */
+int  pvt_set_band(pvt_ctx* ctx, int32_t min_hosts);
 /* Window pipelining (default on): score window k+1 on a side stream while window k is walked.
  * Results are identical either way; off runs windows strictly one after the other. */
 int  pvt_set_pipeline(pvt_ctx* ctx, int on);

@@ -1,0 +1,215 @@
+// pvt_band.hip — vbp best-fit candidate lists by a memory band over hosts sorted once per round.
+//
+// vbp best-fit (reference scheduler/vbp.py:39-50) takes, per task in sorted order, the strictly
+// fitting host of least ||avail - d||2 (ties: host-id string), and commits. Every term of the
+// squared norm is >= 0, so a host can only enter a task's top-KL list if |a1 - d1| is within the
+// radius of the list's current last entry (the score kernel's memory prefilter, vbp_rad), and it
+// must fit strictly: a1 > d1. Host memory spreads over [0, 131072) while the best residuals are a
+// few hundred, so the prefilter rejects nearly every host -- but the streaming score kernel still
+// loads all of them for every task.
+//
+// Here the hosts are sorted by their snapshot memory ONCE per round (hipCUB radix sort of the
+// orderable bits of avail[1], then a gather of the snapshot SoA into sorted order). A host nobody
+// has committed to since keeps its snapshot state, so for it the sorted copy is exact; per task
+// and list segment a wave then finds the first position with a1 >= d1 (a 64-ary search: four
+// dependent loads) and scans upward until the chunk's smallest a1 leaves the radius -- the same
+// exact list the streaming kernel builds, from ~10^3 hosts instead of 10^6. Hosts committed to
+// since the snapshot ("touched", flagged and listed by touch_update_kernel after each walk) are
+// skipped in the sorted copy and scanned from the touched list with their live capacities. The
+// output is the streaming kernel's segment format (exact top-KL of a host subset + feasible
+// count), so merge and commit walk are unchanged; hosts a concurrent walk is committing to are
+// inherited by the next walk as touched, exactly as with the streaming kernel.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pvt_device.h"
+#include "pvt_kernels.h"
+#include "pvt_list.h"
+
+namespace pvt {
+
+__device__ __forceinline__ uint64_t order_bits(double v) {   // total order of doubles
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__global__ void band_keys_kernel(const double* avail, int H, int lo, int n, uint64_t* key,
+                                 int32_t* idx) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  key[p] = order_bits(avail[(size_t)H + lo + p]);
+  idx[p] = lo + p;
+}
+
+__global__ void band_gather_kernel(const double* avail, const uint32_t* tb, int H, int n,
+                                   const int32_t* sid, double* sa, uint32_t* stb) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const int h = sid[p];
+#pragma unroll
+  for (int r = 0; r < 4; r++) sa[(size_t)r * n + p] = avail[(size_t)r * H + h];
+  stb[p] = tb[h];
+}
+
+// After a walk: the hosts it committed to (own_ids, count status[1]) that were not touched yet
+// are flagged and appended to the touched list, in own_ids order (one block, ballot compaction).
+__global__ __launch_bounds__(1024) void touch_update_kernel(const int32_t* own, const int32_t* status,
+                                                            uint8_t* flags, int32_t* tlist,
+                                                            int32_t* tcount) {
+  __shared__ int32_t wcnt[16];
+  __shared__ int32_t base;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = status[1];
+  if (tid == 0) base = *tcount;
+  __syncthreads();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int i = c0 + tid;
+    const int32_t h = i < n ? own[i] : -1;
+    const bool add = h >= 0 && flags[h] == 0;
+    const uint64_t m = __ballot(add);
+    if (lane == 0) wcnt[wave] = __popcll(m);
+    __syncthreads();
+    int pos = base + __popcll(m & below);
+    for (int w = 0; w < wave; w++) pos += wcnt[w];
+    if (add) {
+      flags[h] = 1;
+      tlist[pos] = h;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int t = 0;
+      for (int w = 0; w < 16; w++) t += wcnt[w];
+      base += t;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *tcount = base;
+}
+
+// First sorted position whose key is >= k (a 64-ary search: each step one probe per lane).
+__device__ __forceinline__ int band_lower_bound(const uint64_t* key, int n, uint64_t k) {
+  const int lane = lane_id();
+  int lo = 0, hi = n;
+  while (hi - lo > WAVE) {
+    const int step = (hi - lo + WAVE - 1) / WAVE;
+    const int p = lo + lane * step;
+    const bool ge = p < hi && key[p] >= k;
+    const uint64_t m = __ballot(ge);
+    if (m & 1ull) return lo;                  // (never after the first step: lo's key < k)
+    const int L = m ? __builtin_ctzll(m) : WAVE;
+    const int nlo = lo + (L - 1) * step + 1;
+    hi = min(hi, lo + L * step);
+    lo = nlo;
+  }
+  const int p = lo + lane;
+  const uint64_t m = __ballot(p < hi && key[p] >= k);
+  return m ? lo + __builtin_ctzll(m) : hi;
+}
+
+// One wave per (task, segment): segment s takes the sorted copy's 64-host chunks c with
+// c % S == s from the task's lower bound upward, then the touched list's chunks likewise.
+__global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
+  __shared__ uint64_t s_m1[WPB][KL], s_m2[WPB][KL];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = blockIdx.x * WPB + wave;
+  const int t = g / A.S, seg = g % A.S;
+  if (t >= A.nt) return;
+  const double* dp = A.dem + (size_t)t * 4;
+  const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+  double ls = DINF;
+  uint32_t lt = 0xffffffffu;
+  int32_t li = 0x7fffffff;
+  double ts = DINF, lim = DINF, rd = DINF;
+  uint32_t tt = 0xffffffffu;
+  int32_t ti = 0x7fffffff;
+  const int n = A.n;
+
+  // one 64-host block of candidates (lane = host): prefilter, strict fit, exact score, merge
+  auto consider = [&](bool ok, double a0, double a1, double a2, double a3, uint32_t tbh, int32_t h) {
+    const bool pre = ok && (__builtin_fabs(a1 - d1) <= rd);
+    if (__ballot(pre) == 0) return;
+    const bool fit = pre && fits<true>(a0, a1, a2, a3, d0, d1, d2, d3);
+    const double s2 = norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3);
+    const bool pass = fit && (s2 <= lim);
+    if (__ballot(pass) == 0) return;
+    const double sc = pass ? __builtin_sqrt(s2) : DINF;
+    const uint64_t tk1 = (uint64_t)__double_as_longlong(ts);
+    const uint64_t tk2 = ((uint64_t)tt << 32) | (uint32_t)ti;
+    const uint64_t ck1 = (uint64_t)__double_as_longlong(sc);
+    const uint64_t ck2 = ((uint64_t)tbh << 32) | (uint32_t)h;
+    const uint64_t pm = __ballot(pass && (ck1 < tk1 || (ck1 == tk1 && ck2 < tk2)));
+    if (pm) {
+      list_merge(ls, lt, li, sc, tbh, h, pm, s_m1[wave], s_m2[wave]);
+      ts = readlane_d(ls, KL - 1);
+      tt = readlane_u(lt, KL - 1);
+      ti = readlane_i(li, KL - 1);
+      lim = vbp_lim(ts);
+      rd = vbp_rad(ts);
+    }
+  };
+
+  // sorted snapshot: untouched hosts
+  const int lb = band_lower_bound(A.key, n, order_bits(d1));
+  const int c0 = lb >> 6;
+  int c = c0 + ((seg - c0 % A.S) + A.S) % A.S;
+  const int nch = (n + WAVE - 1) / WAVE;
+  double n0 = 0, n1 = 0, n2 = 0, n3 = 0;
+  uint32_t ntb = 0;
+  int32_t nid = 0;
+  auto fetch = [&](int cc) {
+    const int p = min(cc * WAVE + lane, n - 1);
+    n0 = A.sa[p]; n1 = A.sa[(size_t)n + p]; n2 = A.sa[2 * (size_t)n + p]; n3 = A.sa[3 * (size_t)n + p];
+    ntb = A.stb[p];
+    nid = A.sid[p];
+  };
+  if (c < nch) fetch(c);
+  for (; c < nch; c += A.S) {
+    const double a0 = n0, a1 = n1, a2 = n2, a3 = n3;
+    const uint32_t tbh = ntb;
+    const int32_t h = nid;
+    if (c + A.S < nch) fetch(c + A.S);
+    const int p = c * WAVE + lane;
+    // the chunk's smallest memory is lane 0's (or its first position at or after lb): once it
+    // is beyond the radius, so is every later chunk's -- the segment's list is final
+    if (readlane_d(a1, 0) - d1 > rd) break;
+    const bool ok = p < n && p >= lb && A.touched[h] == 0;   // (h: clamped past n, read anyway)
+    consider(ok, a0, a1, a2, a3, tbh, h);
+  }
+  // touched hosts: live capacities
+  const int nt_ = *A.tcount;
+  for (int cc = seg; cc * WAVE < nt_; cc += A.S) {
+    const int j = cc * WAVE + lane;
+    const int32_t hj = j < nt_ ? A.tlist[j] : -1;
+    const bool ok = hj >= A.lo && hj < A.hi;   // (host-sharded: this rank's hosts only)
+    const int32_t h = ok ? hj : 0;
+    const double a0 = ok ? A.avail[h] : 0.0, a1 = ok ? A.avail[(size_t)A.H + h] : 0.0;
+    const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : 0.0, a3 = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
+    consider(ok, a0, a1, a2, a3, ok ? A.tb[h] : 0u, h);
+  }
+  const size_t row = (size_t)t * A.S + seg;
+  SegEntry e;
+  e.s = ls; e.tb = lt; e.id = li;
+  A.seg[row * KL + lane] = e;
+  const int filled = __popcll(__ballot(li != 0x7fffffff));
+  if (lane == 0) A.seg_feas[row] = filled == KL ? KL + 1 : filled;
+}
+
+void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,
+                      hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(band_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, H, lo, n, key, idx);
+}
+void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, const int32_t* sid,
+                        double* sa, uint32_t* stb, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(band_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, tb, H, n, sid, sa, stb);
+}
+void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* flags, int32_t* tlist,
+                         int32_t* tcount, hipStream_t st) {
+  hipLaunchKernelGGL(touch_update_kernel, dim3(1), dim3(1024), 0, st, own, status, flags, tlist, tcount);
+}
+void launch_band_score(const BandArgs& a, hipStream_t st) {
+  const int waves = a.nt * a.S;
+  if (waves > 0) hipLaunchKernelGGL(band_score_kernel, dim3((waves + WPB - 1) / WPB), dim3(WPB * WAVE), 0, st, a);
+}
+
+}  // namespace pvt

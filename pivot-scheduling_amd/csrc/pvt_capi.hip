@@ -45,8 +45,12 @@ static constexpr int EP_SEG_OFF = 0, EP_SEG_CHAIN = EP_SEG_OFF + EPOCH_SEGS + 1,
 static constexpr int EP_WORDS = EP_RES + 8;
 static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a frontier-walk launch
 static constexpr int ORDERED_FRONTIER_MIN = 32;  // tasks a frontier attempt must place to go on
-static int ORDERED_FRONTIER_TASKS = 1024;         // tasks per frontier attempt (PVT_OF_TASKS)
+static constexpr int ORDERED_FRONTIER_TASKS = 1024;   // tasks per frontier attempt (default)
 static constexpr int ORDERED_FRONTIER_HOSTS = 65536;   // first span of hosts the window is taken from
+// vbp best-fit: candidate lists by a memory band over hosts sorted once per round (pvt_band.hip)
+// from this many hosts (per shard) on, with this many list segments per task
+static constexpr int BAND_MIN_HOSTS = 65536;
+static constexpr int BAND_SEGS = 16;
 
 struct Buf {
   void* p = nullptr;
@@ -58,6 +62,20 @@ struct TimedLaunch {
   double candidates, bytes;
   hipEvent_t a, b;
 };
+
+// The next epoch from task t0: consecutive group segments (processing order), each assigned to
+// the chain of its anchor's zero-cost component (two groups of one component compete for the
+// same hosts: one walk takes them in order). A chain holds at most CHAIN_MAX tasks; a segment
+// that ends inside its group ends the epoch (the rest of the group depends on it).
+struct EpochPlan {
+  std::vector<int> off, chain, cstart;     // segments: window offsets (+ end), chain, start in it
+  std::vector<std::vector<int>> segs;      // chains: their segments
+  std::vector<int> len;                    // chains: tasks
+};
+
+// Package kinds of a host-sharded round (pvt_shard_*): candidate lists of a window, or the
+// window candidates of a frontier walk (FrontierHdr + FrontierSlot per chain / walk).
+enum { PK_LIST = 0, PK_EPOCH = 1, PK_KEYED = 2, PK_ORDERED = 3 };
 
 struct RoundState {
   pvt_round r;                    // the caller's round (arrays stay caller-owned)
@@ -93,6 +111,24 @@ struct RoundState {
   bool ginfo = false;
   std::vector<int32_t> gcnt, ga_host;
   std::vector<double> cost_host;
+  int of_tasks = ORDERED_FRONTIER_TASKS;   // tasks per ordered frontier attempt
+  // host-sharded rounds (pvt_shard_*) on the frontier walks: the scored package's kind and size,
+  // and what comes next
+  bool sharded = false;
+  int pkind = PK_LIST;
+  int64_t pbytes = 0;
+  bool sh_epochs = false;         // cost_aware best-fit: frontier epochs between list windows
+  int list_until = 0;             //   list windows up to this task (a chain left unproven), then
+                                  //   epochs again
+  EpochPlan E;                    //   the epoch of the scored package
+  bool of_try = false;            // ordered rounds: a frontier attempt comes next
+  int of_n = 0, of_hs = 0;        //   the scored attempt's tasks and host span
+  bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
+  // vbp best-fit band lists (pvt_band.hip): the sorted snapshot of hosts [lo, hi) is built; a
+  // walk whose committed hosts are not yet flagged as touched (its own-ids buffer)
+  bool band = false;
+  int band_S = BAND_SEGS;
+  int touch_lb = -1;
 };
 
 struct pvt_ctx {
@@ -122,6 +158,10 @@ struct pvt_ctx {
   int64_t n_zchains = 0, n_gchains = 0;   // epoch chains walked by the frontier / list walk
   int64_t n_longest = 0;                  // tasks of the longest epoch chain (sum over epochs)
   int zwalk = 1;                          // zero-cost frontier walk of epoch chains
+  int of_tasks = ORDERED_FRONTIER_TASKS;  // ordered frontier tasks per attempt (PVT_OF_TASKS)
+  Buf fwin;                               // host-sharded frontier walks: merged windows
+  int band_min = BAND_MIN_HOSTS;          // vbp best-fit band lists from this many hosts (0: off)
+  Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
@@ -276,6 +316,8 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
     return PVT_EHIP;
   }
   ctx->stream = ctx->own;
+  if (const char* e = getenv("PVT_OF_TASKS")) ctx->of_tasks = std::max(32, atoi(e));   // tuning
+  if (const char* e = getenv("PVT_BAND")) ctx->band_min = std::max(0, atoi(e));       // A/B
   *out = ctx;
   return PVT_OK;
 }
@@ -291,7 +333,9 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
-                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin};
+                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->fwin,
+                 &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
+                 &ctx->btcnt, &ctx->bsorttmp};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -357,6 +401,11 @@ extern "C" int pvt_epoch_stats(pvt_ctx* ctx, int64_t* epochs, int64_t* segments,
   if (epochs) *epochs = ctx->n_epochs;
   if (segments) *segments = ctx->n_segs;
   if (rejected) *rejected = ctx->n_rejected;
+  return PVT_OK;
+}
+extern "C" int pvt_set_band(pvt_ctx* ctx, int32_t min_hosts) {
+  if (!ctx || min_hosts < 0) return PVT_EINVAL;
+  ctx->band_min = min_hosts;
   return PVT_OK;
 }
 extern "C" int pvt_set_zero_walk(pvt_ctx* ctx, int on) {
@@ -645,6 +694,49 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   return PVT_OK;
 }
 
+// vbp best-fit band lists: hosts [lo, hi) sorted by snapshot memory (stable radix sort of the
+// orderable bits of avail[1]) and their snapshot state gathered in that order; no host touched.
+static int band_snapshot(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  const int n = R.hi - R.lo;
+  ENSURE(ctx->bkey, sizeof(uint64_t) * 2 * (size_t)n);
+  ENSURE(ctx->bidx, sizeof(int32_t) * 2 * (size_t)n);
+  ENSURE(ctx->bsa, sizeof(double) * 4 * (size_t)n);
+  ENSURE(ctx->bstb, sizeof(uint32_t) * (size_t)n);
+  ENSURE(ctx->btouch, (size_t)R.H);
+  ENSURE(ctx->btlist, sizeof(int32_t) * (size_t)R.H);
+  ENSURE(ctx->btcnt, 16);
+  uint64_t* k0 = P<uint64_t>(ctx->bkey);
+  int32_t* i0 = P<int32_t>(ctx->bidx);
+  size_t tmp = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k0, k0 + n, i0, i0 + n, n, 0, 64, st));
+  ENSURE(ctx->bsorttmp, tmp);
+  int bs = BAND_SEGS;
+  if (const char* e = getenv("PVT_BAND_SEGS")) bs = atoi(e);   // tuning (2, 4, 8, 16, 32)
+  R.band_S = (bs == 1 || bs == 2 || bs == 4 || bs == 8 || bs == 16 || bs == 32) ? bs : BAND_SEGS;
+  Scope sc(ctx, PVT_K_OTHER, 0, 0);
+  launch_band_keys(r->avail, R.H, R.lo, n, k0, i0, st);
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->bsorttmp.p, tmp, k0, k0 + n, i0, i0 + n, n, 0, 64, st));
+  launch_band_gather(r->avail, r->tiebreak, R.H, n, i0 + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb), st);
+  HIPCHK(hipMemsetAsync(ctx->btouch.p, 0, (size_t)R.H, st));
+  HIPCHK(hipMemsetAsync(ctx->btcnt.p, 0, 16, st));
+  HIPCHK(hipGetLastError());
+  return PVT_OK;
+}
+
+// The last walk's committed hosts flagged and listed as touched (band lists), on the context's
+// stream. Called only where no band score pass is in flight (it would read the touched table).
+static void flush_touched(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  if (!R.band || R.touch_lb < 0) return;
+  launch_touch_update(P<int32_t>(ctx->owned[R.touch_lb]), P<int32_t>(ctx->next),
+                      P<uint8_t>(ctx->btouch), P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt),
+                      ctx->stream);
+  R.touch_lb = -1;
+}
+
 // ---------------------------------------------------------------- round state machine
 // pvt_place() and the sharded calls share one round: begin (order, gathers, zone tables, group
 // boundaries), then per window: candidate lists over this context's host range (optionally
@@ -744,10 +836,13 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   }
   // vbp first-fit / unsorted cost_aware first-fit: the frontier walk over the first alive hosts
   // (ordered_frontier); its scratch is the keyed path's (the modes exclude each other)
-  R.ofront = ctx->zwalk && R.ordered && lo == 0 && hi == H && world == 1 &&
-             T >= ORDERED_FRONTIER_MIN && H >= 64;
+  R.sh_epochs = false;
+  R.list_until = 0;
+  R.ofront = ctx->zwalk && R.ordered && T >= ORDERED_FRONTIER_MIN && H >= 64;
+  R.of_try = R.ofront;
+  R.of_tasks = ctx->of_tasks;
+  R.kf_pending = false;
   if (R.ofront) {
-    if (const char* e = getenv("PVT_OF_TASKS")) ORDERED_FRONTIER_TASKS = std::max(32, atoi(e));   // tuning
     R.ofh = ORDERED_FRONTIER_HOSTS;
     if (const char* e = getenv("PVT_OF_HOSTS")) R.ofh = std::max(ZW_M, atoi(e));   // tuning
     ENSURE(ctx->next, sizeof(int32_t) * 4);
@@ -764,6 +859,9 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   R.gstart.push_back(T);
   R.ngroups = R.keyed ? R.ganchor.size() : 1;
   R.key_group = -1;
+  R.touch_lb = -1;
+  R.band = r->mode == PVT_VBP_BF && ctx->band_min > 0 && hi - lo >= ctx->band_min;
+  if (R.band && (rc = band_snapshot(ctx))) return rc;
 
   // Windows adapt to how far commit walks get before a list is exhausted: a walk that stops
   // early means the next window only needs about that many tasks (the score pass costs the
@@ -823,6 +921,14 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
     R.kstall = false;
     if (R.key_group == (int)R.g && R.kmode == 1 && (rc = keyed_full_sort(ctx))) return rc;
   }
+  if (R.keyed && R.key_group != (int)R.g && R.hi == R.lo && R.kscan && R.sharded) {
+    // a rank with no hosts: no key, an empty prefix -- but the group start's frontier walk is a
+    // collective step every rank takes (round_next_window decides it the same way everywhere)
+    R.kf_pending = ctx->zwalk && R.t0 == R.gstart[R.g] && ge - R.t0 >= KEYED_FRONTIER_MIN &&
+                   !R.r.rt_bw && R.Z <= ZMAX;
+    HIPCHK(hipMemsetAsync(P<int32_t>(ctx->next) + 2, 0, sizeof(int32_t), ctx->stream));
+    R.key_group = (int)R.g;
+  }
   if (R.keyed && R.key_group != (int)R.g && R.hi > R.lo) {
     KeyArgs ka{R.r.avail, R.r.zone, R.r.decay, P<double>(ctx->csum), P<double>(ctx->bsum), R.H, R.Z,
                R.ganchor[R.g], R.lo, R.hi, P<double>(ctx->key),
@@ -852,9 +958,12 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
       // the windowed list path goes on from there with the same frozen key. Launched on the
       // prefix length as the device holds it, read back with it in one synchronisation.
       const int n_g = ge - R.t0;
-      const bool zk = ctx->zwalk && R.lo == 0 && R.hi == R.H && R.world == 1 &&
-                      R.t0 == R.gstart[R.g] && n_g >= KEYED_FRONTIER_MIN && !R.r.rt_bw &&
-                      R.Z <= ZMAX;
+      const bool zk_any = ctx->zwalk && R.t0 == R.gstart[R.g] && n_g >= KEYED_FRONTIER_MIN &&
+                          !R.r.rt_bw && R.Z <= ZMAX;
+      const bool zk = zk_any && !R.sharded;
+      // host-sharded: the walk runs on the merged window of every rank's first prefix hosts
+      // (pvt_shard_score packs this rank's, PK_KEYED), after the prefix lengths are known
+      R.kf_pending = zk_any && R.sharded;
       if (zk) {
         ENSURE(ctx->wres, sizeof(WinRec) * (size_t)n_g);
         const pvt_round* r = &R.r;
@@ -919,6 +1028,23 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
                    r->mode == PVT_CA_FF ? 1 : 0, R.lo, R.hi, L};
     Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
     launch_ordered(oa, st);
+  } else if (R.band) {
+    const int S = R.band_S;
+    ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)nt * S * KL);
+    ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)nt * S);
+    const int n = R.hi - R.lo;
+    BandArgs ba{P<uint64_t>(ctx->bkey) + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb),
+                P<int32_t>(ctx->bidx) + n, n, R.lo, R.hi, P<uint8_t>(ctx->btouch),
+                P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt), r->avail, r->tiebreak, R.H, dem_w,
+                nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
+    {
+      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
+      launch_band_score(ba, st);
+    }
+    MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
+                 anc_w, R.ord + t0, R.H, nt, S, KL, L};
+    Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
+    launch_merge(ma, st);
   } else {
     const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw, R.in_epoch);
     ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)nt * S * KL);
@@ -960,6 +1086,7 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
+  if (R.band) R.touch_lb = lb;    // its hosts become touched before the next band score
   return PVT_OK;
 }
 
@@ -1004,7 +1131,7 @@ static int ordered_frontier(pvt_ctx* ctx) {
   while (R.T - R.t0 >= ORDERED_FRONTIER_MIN) {
     // a bounded task prefix: its smallest demand is close to each task's own (decreasing
     // orders), so hosts filled too far for it leave the window
-    const int n = std::min(R.T - R.t0, ORDERED_FRONTIER_TASKS);
+    const int n = std::min(R.T - R.t0, R.of_tasks);
     const double* dem = P<double>(ctx->dem_ord) + (size_t)R.t0 * 4;
     // the window comes from the first R.ofh hosts (a window of fewer than ZW_M hosts stops the
     // walk at the first task fitting none of them, which is still the answer for the tasks
@@ -1012,7 +1139,7 @@ static int ordered_frontier(pvt_ctx* ctx) {
     const int hs = std::min(R.ofh, R.H);
     {
       Scope sc(ctx, PVT_K_OTHER, 0, 0);
-      launch_alive_flags(r->avail, R.H, hs, dem, n, strict ? 1 : 0, P<double>(ctx->hmin),
+      launch_alive_flags(r->avail, R.H, 0, hs, dem, n, strict ? 1 : 0, P<double>(ctx->hmin),
                          P<uint8_t>(ctx->kflag), st);
       size_t tmp = ctx->ksorttmp.n;
       HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(ctx->ksorttmp), tmp, P<int32_t>(ctx->kiota),
@@ -1069,6 +1196,7 @@ static int place_pipelined(pvt_ctx* ctx) {
     const int nt0 = t0 + nt, ge = group_end(R, t0);
     // (ordered frontier rounds: no speculative window; the frontier walk is tried after each)
     const int nnt = (ctx->pipeline && nt0 < ge && !R.ofront) ? std::min(R.W, ge - nt0) : 0;
+    flush_touched(ctx);   // the previous walk's hosts, seen by the score pass launched next
     if (nnt > 0) HIPCHK(hipEventRecord(ctx->ev_walk, ctx->stream));
     if ((rc = walk_launch(ctx, t0, nt, lb, n_prev))) return rc;
     if (nnt > 0) {
@@ -1086,6 +1214,7 @@ static int place_pipelined(pvt_ctx* ctx) {
       continue;
     }
     if (nnt > 0) HIPCHK(hipStreamSynchronize(ctx->side));   // discard the speculation
+    flush_touched(ctx);
     R.t0 = t0 + adv;
     if ((rc = ordered_frontier(ctx))) return rc;
     if ((rc = round_next_window(ctx, &nt))) return rc;
@@ -1159,16 +1288,6 @@ static int epoch_groups(pvt_ctx* ctx) {
   return PVT_OK;
 }
 
-// The next epoch from task t0: consecutive group segments (processing order), each assigned to
-// the chain of its anchor's zero-cost component (two groups of one component compete for the
-// same hosts: one walk takes them in order). A chain holds at most CHAIN_MAX tasks; a segment
-// that ends inside its group ends the epoch (the rest of the group depends on it).
-struct EpochPlan {
-  std::vector<int> off, chain, cstart;     // segments: window offsets (+ end), chain, start in it
-  std::vector<std::vector<int>> segs;      // chains: their segments
-  std::vector<int> len;                    // chains: tasks
-};
-
 static void epoch_plan(const RoundState& R, int t0, EpochPlan& P) {
   P.off.assign(1, 0);
   P.chain.clear(); P.cstart.clear(); P.segs.clear(); P.len.clear();
@@ -1199,6 +1318,50 @@ static void epoch_plan(const RoundState& R, int t0, EpochPlan& P) {
   }
 }
 
+// The epoch's chain tables to the device (one upload): segment offsets / chains / chain-local
+// starts, per chain its task range in cmap and its segments' chain-local starts.
+static int upload_chain_tables(pvt_ctx* ctx, const EpochPlan& E) {
+  int32_t* host = ctx->ep_host;
+  const int nseg = (int)E.chain.size(), nch = (int)E.segs.size();
+  for (int k = 0; k <= nseg; k++) host[EP_SEG_OFF + k] = E.off[k];
+  for (int k = 0; k < nseg; k++) { host[EP_SEG_CHAIN + k] = E.chain[k]; host[EP_SEG_CSTART + k] = E.cstart[k]; }
+  int nm = 0, ns = 0;
+  for (int c = 0; c < nch; c++) {
+    host[EP_COFF + c] = nm;
+    host[EP_CSOFF + c] = ns;
+    for (int sg : E.segs[c]) {
+      host[EP_CSEG + ns++] = E.cstart[sg];
+      for (int w = E.off[sg]; w < E.off[sg + 1]; w++) host[EP_CMAP + nm++] = w;
+    }
+  }
+  host[EP_COFF + nch] = nm;
+  host[EP_CSOFF + nch] = ns;
+  HIPCHK(hipMemcpyAsync(ctx->ep_dev.p, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice,
+                        ctx->stream));
+  return PVT_OK;
+}
+
+// A frontier-walked epoch's verdict (validation, accepted prefix and its apply ran on the
+// device; ctx->ep_host holds the readback): chains left unproven, and the tasks accepted.
+static int epoch_frontier_verdict(pvt_ctx* ctx, const EpochPlan& E, int t0, int* need_out, int* adv_out) {
+  const int32_t* host = ctx->ep_host;
+  const int nch = (int)E.segs.size();
+  int need = 0;
+  for (int c = 0; c < nch; c++) need += host[EP_STATUS + 2 * c] != E.len[c];
+  ctx->n_zchains += nch - need;
+  ctx->n_longest += *std::max_element(E.len.begin(), E.len.end());
+  if (host[EP_RES + 4])
+    return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out (epoch at task %d)", t0);
+  const int adv = host[EP_RES + 1];
+  // (a segment cut short here is a frontier-walk fallback, not a list refill: the chains the
+  // walk could not prove are walked with lists next; the tasks it proved are accepted)
+  ctx->n_rejected += host[EP_RES + 3];
+  if (adv <= 0 && !need) return fail(ctx, PVT_EHIP, "epoch made no progress at task %d", t0);
+  *need_out = need;
+  *adv_out = adv;
+  return PVT_OK;
+}
+
 static int place_epochs(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   const pvt_round* r = &R.r;
@@ -1223,7 +1386,7 @@ static int place_epochs(pvt_ctx* ctx) {
     if (zw_possible && !force_lists) {
       ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
       Scope sc(ctx, PVT_K_OTHER, 0, 0);
-      launch_host_min(r->avail, R.H, P<double>(ctx->hmin), st);
+      launch_host_min(r->avail, R.H, 0, R.H, P<double>(ctx->hmin), st);
     }
     epoch_plan(R, t0, E);
     const int nseg = (int)E.chain.size(), nch = (int)E.segs.size(), nt = E.off.back();
@@ -1244,21 +1407,7 @@ static int place_epochs(pvt_ctx* ctx) {
       t0 += adv;
       continue;
     }
-    // chain tables, in one upload
-    for (int k = 0; k <= nseg; k++) host[EP_SEG_OFF + k] = E.off[k];
-    for (int k = 0; k < nseg; k++) { host[EP_SEG_CHAIN + k] = E.chain[k]; host[EP_SEG_CSTART + k] = E.cstart[k]; }
-    int nm = 0, ns = 0;
-    for (int c = 0; c < nch; c++) {
-      host[EP_COFF + c] = nm;
-      host[EP_CSOFF + c] = ns;
-      for (int sg : E.segs[c]) {
-        host[EP_CSEG + ns++] = E.cstart[sg];
-        for (int w = E.off[sg]; w < E.off[sg + 1]; w++) host[EP_CMAP + nm++] = w;
-      }
-    }
-    host[EP_COFF + nch] = nm;
-    host[EP_CSOFF + nch] = ns;
-    HIPCHK(hipMemcpyAsync(dev, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice, st));
+    if ((rc = upload_chain_tables(ctx, E))) return rc;
     // (the rejection flags are zeroed by epoch_final_kernel, launched before every validation)
     int need = nch;                           // chains left to the list walk
     EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
@@ -1299,17 +1448,9 @@ static int place_epochs(pvt_ctx* ctx) {
       HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
                             hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      need = 0;
-      for (int c = 0; c < nch; c++) need += host[EP_STATUS + 2 * c] != E.len[c];
-      ctx->n_zchains += nch - need;
-      ctx->n_longest += *std::max_element(E.len.begin(), E.len.end());
-      if (host[EP_RES + 4])
-        return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out (epoch at task %d)", t0);
-      const int adv = host[EP_RES + 1];
-      ctx->refills += host[EP_RES + 2];
-      ctx->n_rejected += host[EP_RES + 3];
+      int adv = 0;
+      if ((rc = epoch_frontier_verdict(ctx, E, t0, &need, &adv))) return rc;
       if (need && adv < nt) force_lists = true;
-      if (adv <= 0 && !need) return fail(ctx, PVT_EHIP, "epoch made no progress at task %d", t0);
       t0 += adv;
       continue;
     }
@@ -1506,6 +1647,7 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
     launch_iota(r->order, r->n_tasks, ctx->stream);
     return opp_round(ctx, r);
   }
+  ctx->rs.sharded = false;
   if ((rc = round_begin(ctx, r, 0, r->n_hosts, 1))) return rc;
   ctx->n_epochs = ctx->n_segs = ctx->n_rejected = 0;
   ctx->n_zchains = ctx->n_gchains = ctx->n_longest = 0;
@@ -1522,6 +1664,9 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
 
 // ---------------------------------------------------------------- host-dimension sharding
 static int shard_depth(int world) { return std::max(KL, LMAX / std::max(world, 1)); }
+static int64_t frontier_pkg_bytes(int nslots) {
+  return (int64_t)sizeof(FrontierHdr) + (int64_t)sizeof(FrontierSlot) * nslots;
+}
 
 // ---- host-sharded opportunistic rounds (per-rank feasible counts, exchanged;
 // the draw and the k-th selection replicated). Each rank counts its super-chunks of a window
@@ -1644,17 +1789,38 @@ extern "C" int pvt_shard_begin(pvt_ctx* ctx, const pvt_round* r, int32_t host_lo
     return fail(ctx, PVT_EINVAL, "bad host range [%d, %d) of %d", host_lo, host_hi, r->n_hosts);
   ctx->rs.opp = false;
   ctx->rs.inflight = ctx->rs.spec = false;
+  ctx->rs.nt = 0;
+  ctx->rs.pkind = PK_LIST;
+  ctx->n_epochs = ctx->n_segs = ctx->n_rejected = 0;
+  ctx->n_zchains = ctx->n_gchains = ctx->n_longest = 0;
   if (r->mode == PVT_OPP) {
     int rc = check_round(ctx, r);
     if (rc) return rc;
     ctx->windows = ctx->refills = 0;
     return opp_shard_begin(ctx, r, host_lo, host_hi, world, max_package_bytes);
   }
+  RoundState& R = ctx->rs;
+  R.sharded = true;
   int rc = round_begin(ctx, r, host_lo, host_hi, world);
   if (rc) return rc;
+  // cost_aware best-fit: frontier-walked epochs (the walk's exchange is its window candidates),
+  // list windows for what they cannot prove
+  if ((rc = epoch_groups(ctx))) return rc;
+  R.sh_epochs = !R.egs.empty() && ctx->zwalk && !R.r.rt_bw && R.Z <= ZMAX;
+  R.list_until = 0;
+  if (R.sh_epochs) {
+    ENSURE(ctx->ep_dev, sizeof(int32_t) * EP_WORDS);
+    ENSURE(ctx->wres, sizeof(WinRec) * (size_t)EPOCH_MAX);
+    ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+  }
+  if (R.sh_epochs || R.ofront || R.keyed) {
+    ENSURE(ctx->fwin, sizeof(FrontierSlot) * (size_t)EPOCH_SEGS);
+    ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+  }
   const int PK = shard_depth(world);
-  ENSURE(ctx->pkg, sizeof(SegEntry) * (size_t)(PK + 1) * ctx->rs.Wmax);
-  if (max_package_bytes) *max_package_bytes = (int64_t)sizeof(SegEntry) * (PK + 1) * ctx->rs.Wmax;
+  ENSURE(ctx->pkg, sizeof(SegEntry) * (size_t)(PK + 1) * R.Wmax);
+  const int64_t lists = (int64_t)sizeof(SegEntry) * (PK + 1) * R.Wmax;
+  if (max_package_bytes) *max_package_bytes = std::max(lists, frontier_pkg_bytes(EPOCH_SEGS));
   return PVT_OK;
 }
 
@@ -1667,6 +1833,193 @@ static int shard_finish_walk(pvt_ctx* ctx) {
   if ((rc = walk_status(ctx, R.if_t0, R.if_nt, R.if_inh, &adv))) return rc;
   adapt_window(ctx, adv, R.if_nt);
   R.t0 = R.if_t0 + adv;
+  R.of_try = R.ofront;            // (place_pipelined: ordered_frontier after every list walk)
+  return PVT_OK;
+}
+
+// Last task (exclusive) a list window starting at t0 may reach: keyed rounds stop at the group
+// end (frozen keys), sharded best-fit epochs at list_until (frontier epochs go on from there).
+static int list_end(const RoundState& R, int t0) {
+  int ge = group_end(R, t0);
+  if (R.sh_epochs) ge = std::min(ge, std::max(R.list_until, t0));
+  return ge;
+}
+
+// ---- host-sharded frontier walks. A step's package is this rank's window candidates
+// (FrontierHdr, then a FrontierSlot per epoch chain or for the one keyed / ordered walk); after
+// the all-gather every rank merges them (launch_zwin_merge) into exactly the window the unsharded
+// walk builds over all hosts, and runs the same walk, validation and apply on identical inputs.
+// Returns with *made = false when the next step is a list window.
+static int shard_frontier_score(pvt_ctx* ctx, void* package, int* nt_out, int64_t* bytes_out,
+                                bool* made) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  *made = false;
+  FrontierHdr* hdr = reinterpret_cast<FrontierHdr*>(package);
+  FrontierSlot* slots = reinterpret_cast<FrontierSlot*>(hdr + 1);
+  if (R.sh_epochs && R.t0 < R.T && R.t0 >= R.list_until) {
+    epoch_plan(R, R.t0, R.E);
+    const int nch = (int)R.E.segs.size(), nt = R.E.off.back();
+    if (nch <= 1) {                 // one chain: list windows (as place_epochs)
+      R.list_until = R.t0 + nt;
+      return PVT_OK;
+    }
+    int rc;
+    if ((rc = upload_chain_tables(ctx, R.E))) return rc;
+    int32_t* dev = P<int32_t>(ctx->ep_dev);
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_host_min(r->avail, R.H, R.lo, R.hi, &hdr->hmin[0][0], st);
+      ZwinArgs za{r->avail, r->zone, R.H, R.Z, R.lo, R.hi, P<double>(ctx->csum),
+                  P<int32_t>(ctx->anc_ord) + R.t0, dev + EP_COFF, dev + EP_CMAP, slots};
+      launch_zwin_build(za, nch, st);
+    }
+    ctx->n_epochs++;
+    ctx->n_segs += (int)R.E.chain.size();
+    R.pkind = PK_EPOCH;
+    *nt_out = nt;
+    *bytes_out = frontier_pkg_bytes(nch);
+    *made = true;
+  } else if (R.ofront && R.of_try && R.T - R.t0 >= ORDERED_FRONTIER_MIN) {
+    // this rank's first hosts alive for the next tasks' smallest demand, among the first R.ofh
+    // hosts of the cluster (ordered_frontier)
+    const int n = std::min(R.T - R.t0, R.of_tasks);
+    const int hs = std::min(R.ofh, R.H);
+    const int he = std::min(R.hi, hs), nloc = std::max(0, he - R.lo);
+    const double* dem = P<double>(ctx->dem_ord) + (size_t)R.t0 * 4;
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_alive_flags(r->avail, R.H, R.lo, he, dem, n, r->mode == PVT_CA_FF ? 1 : 0,
+                         P<double>(ctx->hmin), P<uint8_t>(ctx->kflag), st);
+      if (nloc > 0) {
+        size_t tmp = ctx->ksorttmp.n;
+        HIPCHK(hipcub::DeviceSelect::Flagged(P<void>(ctx->ksorttmp), tmp, P<int32_t>(ctx->kiota),
+                                             P<uint8_t>(ctx->kflag), P<int32_t>(ctx->kperm),
+                                             P<int32_t>(ctx->next) + 2, nloc, st));
+      } else {
+        HIPCHK(hipMemsetAsync(P<int32_t>(ctx->next) + 2, 0, sizeof(int32_t), st));
+      }
+      launch_zwin_gather(r->avail, R.H, R.lo, P<int32_t>(ctx->kperm), P<int32_t>(ctx->next) + 2,
+                         slots, st);
+    }
+    R.pkind = PK_ORDERED;
+    R.of_n = n;
+    R.of_hs = hs;
+    *nt_out = n;
+    *bytes_out = frontier_pkg_bytes(1);
+    *made = true;
+  }
+  if (*made) {
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(st));   // the package is complete when pvt_shard_score returns
+  }
+  return PVT_OK;
+}
+
+// Keyed first-fit at a group start (round_next_window set kf_pending): this rank's first hosts
+// of the group's zero-key prefix (its own sorted range, kperm; length on the device).
+static int shard_keyed_score(pvt_ctx* ctx, void* package, int* nt_out, int64_t* bytes_out) {
+  RoundState& R = ctx->rs;
+  hipStream_t st = ctx->stream;
+  FrontierSlot* slots = reinterpret_cast<FrontierSlot*>(reinterpret_cast<FrontierHdr*>(package) + 1);
+  {
+    Scope sc(ctx, PVT_K_OTHER, 0, 0);
+    launch_zwin_gather(R.r.avail, R.H, R.lo, P<int32_t>(ctx->kperm), P<int32_t>(ctx->next) + 2,
+                       slots, st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  R.pkind = PK_KEYED;
+  *nt_out = group_end(R, R.t0) - R.t0;
+  *bytes_out = frontier_pkg_bytes(1);
+  return PVT_OK;
+}
+
+// The exchanged frontier packages: merge, walk, and (epochs) validate + apply; the round goes on
+// from the tasks the walk proved. Synchronous.
+static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  const int kind = R.pkind, nt = R.nt, t0 = R.t0;
+  const int nslots = kind == PK_EPOCH ? (int)R.E.segs.size() : 1;
+  FrontierSlot* win = P<FrontierSlot>(ctx->fwin);
+  {
+    Scope sc(ctx, PVT_K_MERGE, 0, 0);
+    launch_zwin_merge(reinterpret_cast<const uint8_t*>(packages), R.pbytes, R.world, nslots, win,
+                      kind == PK_EPOCH ? P<double>(ctx->hmin) : nullptr, st);
+  }
+  R.nt = 0;
+  R.pkind = PK_LIST;
+  int rc;
+  if (kind == PK_EPOCH) {
+    const EpochPlan& E = R.E;
+    const int nseg = (int)E.chain.size(), nch = nslots;
+    int32_t* dev = P<int32_t>(ctx->ep_dev);
+    int32_t* host = ctx->ep_host;
+    ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
+                 P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
+                 P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
+                 P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
+                 nullptr, 0, 0, 0, nullptr, nullptr, win};
+    {
+      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+      launch_zwalk(za, nch, st);
+    }
+    EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
+                 P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_SEG_OFF,
+                 dev + EP_SEG_CHAIN, dev + EP_SEG_CSTART, dev + EP_STATUS, P<WinRec>(ctx->wres),
+                 r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD, r->rt_bw, P<int32_t>(ctx->grp_ord) + t0};
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_epoch_validate(ea, st);
+      launch_epoch_accept_apply(ea, dev + EP_RES, nch, st);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    int need = 0, adv = 0;
+    if ((rc = epoch_frontier_verdict(ctx, E, t0, &need, &adv))) return rc;
+    // chains the walk could not prove: list windows over the rest of this epoch's tasks
+    if (need && adv < nt) R.list_until = t0 + nt;
+    R.t0 = t0 + adv;
+    return PVT_OK;
+  }
+  // keyed / ordered: one walk over the merged window, capacities written back
+  const bool strict = r->mode == PVT_CA_FF;
+  const int n = kind == PK_ORDERED ? R.of_n : nt;
+  ENSURE(ctx->wres, sizeof(WinRec) * (size_t)n);
+  const double* dem = P<double>(ctx->dem_ord) + (size_t)t0 * 4;
+  ZwalkArgs za{r->avail, r->zone, R.H, R.Z, dem, P<int32_t>(ctx->anc_ord) + t0, R.ord + t0,
+               nullptr, nullptr, nullptr, nullptr, P<int32_t>(ctx->next), P<WinRec>(ctx->wres),
+               r->placement, nullptr, ctx->stamps, nullptr, 0, R.lo, n, r->avail, nullptr, win};
+  {
+    Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+    launch_zwalk_keyed(za, strict, st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t) * 2,
+                        hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ctx->next_host + 2, &win->total, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  const int done = ctx->next_host[0];
+  if (done < 0 || done > n) return fail(ctx, PVT_EHIP, "sharded frontier walk returned %d of %d", done, n);
+  ctx->n_zchains += done > 0;
+  R.t0 = t0 + done;
+  if (kind == PK_KEYED) {
+    R.kf_pending = false;
+    return PVT_OK;
+  }
+  // ordered: as ordered_frontier -- a short window that stopped the walk doubles the span, an
+  // attempt that placed too few tasks hands over to one list window
+  const bool short_window = ctx->next_host[2] < ZW_M && R.of_hs < R.H;
+  if (done < n && short_window) {
+    R.ofh = (int)std::min<int64_t>((int64_t)R.ofh * 2, R.H);
+    if (done == 0) return PVT_OK;
+  }
+  if (done < ORDERED_FRONTIER_MIN) R.of_try = false;
   return PVT_OK;
 }
 
@@ -1688,8 +2041,9 @@ extern "C" int pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out
   hipStream_t st = ctx->stream;
   R.spec = false;
   if (R.inflight) {
-    const int t1 = R.if_t0 + R.if_nt, ge = group_end(R, R.if_t0);
-    if (ctx->pipeline && t1 < ge) {           // speculative: the window after the walk in flight
+    const int t1 = R.if_t0 + R.if_nt, ge = list_end(R, R.if_t0);
+    // (ordered rounds: no speculative window; the frontier walk is tried after each)
+    if (ctx->pipeline && t1 < ge && !R.ofront) {   // speculative: the window after the walk in flight
       nt = std::min(R.W, ge - t1);
       lb = 1 - R.if_lb;
       st = ctx->side;
@@ -1701,16 +2055,36 @@ extern "C" int pvt_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out
       return rc;
     }
   }
+  if (!R.spec) flush_touched(ctx);   // (no band score in flight)
   if (!R.spec) {
-    if ((rc = round_next_window(ctx, &nt))) return rc;
+    bool made = false;
+    int64_t fb = 0;
+    if ((rc = shard_frontier_score(ctx, package, &nt, &fb, &made))) return rc;
+    if (!made) {
+      if ((rc = round_next_window(ctx, &nt))) return rc;
+      if (nt > 0 && R.kf_pending) {
+        if ((rc = shard_keyed_score(ctx, package, &nt, &fb))) return rc;
+        made = true;
+      }
+    }
+    if (made) {
+      R.nt = nt;
+      R.pt0 = R.t0;
+      R.pbytes = fb;
+      *n_tasks_out = nt;
+      *package_bytes = fb;
+      return PVT_OK;
+    }
     if (nt == 0) {
       R.active = false;
       HIPCHK(hipStreamSynchronize(ctx->stream));
       return PVT_OK;
     }
+    if (R.sh_epochs) nt = std::min(nt, list_end(R, R.t0) - R.t0);
     if ((rc = window_lists(ctx, R.t0, nt, lb, st))) return rc;
     R.pt0 = R.t0;
   }
+  R.pkind = PK_LIST;
   Lists L;
   lists_from(ctx, L, lb);
   PackArgs pa{L, nt, PK, R.ordered ? 1 : 0, reinterpret_cast<SegEntry*>(package)};
@@ -1732,6 +2106,7 @@ extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
   RoundState& R = ctx->rs;
   if (!R.active || R.nt == 0) return fail(ctx, PVT_EINVAL, "pvt_shard_commit without a scored window");
   if (R.opp) return opp_shard_commit(ctx, packages);
+  if (R.pkind != PK_LIST) return shard_frontier_commit(ctx, packages);
   int rc, n_prev = 0;
   if (R.spec) {                               // wait for the walk the package speculated past
     if ((rc = shard_finish_walk(ctx))) return rc;
@@ -1743,6 +2118,7 @@ extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
     n_prev = ctx->next_host[1];               // its hosts: stale in these lists, so touched
   }
   const int PK = shard_depth(R.world), t0 = R.pt0, nt = R.nt, lb = R.plb;
+  flush_touched(ctx);   // the walk before: its package's score pass has completed
   Lists L;
   lists_from(ctx, L, lb);
   MergeArgs ma{reinterpret_cast<const SegEntry*>(packages), nullptr, R.r.avail, R.r.zone,

@@ -217,15 +217,55 @@ struct ZwalkArgs {
   int kn, lo, knt;
   double* wb;
   const int32_t* kn_dev;  // keyed: prefix length read on the device (NULL: kn)
+  // host-sharded rounds: the merged window of chain b (keyed / ordered: of the walk) -- hosts
+  // in index order with their capacities, as the unsharded walk builds it -- or NULL (build it)
+  const struct FrontierSlot* pwin;
 };
 constexpr int ZW_MIN_PARTS = 256;
-void launch_host_min(const double* avail, int H, double* part, hipStream_t st);   // [256][4]
+// per-dimension minima of avail over hosts [lo, hi) into part[ZW_MIN_PARTS][4]
+void launch_host_min(const double* avail, int H, int lo, int hi, double* part, hipStream_t st);
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st);
 constexpr int ZW_M = 1024;                 // frontier-walk window hosts
 void launch_zwalk_keyed(const ZwalkArgs& a, bool strict, hipStream_t st);
-// ordered first-fit frontier: flags[h] = host h fits the smallest demand of tasks dem[0, n)
-void launch_alive_flags(const double* avail, int H, int hs, const double* dem, int n, int strict,
-                        double* dmin, uint8_t* flags, hipStream_t st);
+// ordered first-fit frontier: flags[h - lo] = host h in [lo, hs) fits the smallest demand of
+// tasks dem[0, n)
+void launch_alive_flags(const double* avail, int H, int lo, int hs, const double* dem, int n,
+                        int strict, double* dmin, uint8_t* flags, hipStream_t st);
+
+// Host-sharded frontier walks (pvt_capi.hip pvt_shard_*). A rank's package carries, per chain
+// (cost_aware best-fit epochs) or for the one keyed / ordered walk, the first ZW_M window hosts
+// of ITS host range in index order with their capacities, plus its host minima (certificate 2).
+// After the all-gather every rank merges the packages -- ranks own ascending contiguous ranges,
+// so the concatenation in rank order truncated to ZW_M is the window the unsharded walk builds
+// -- and runs the same walk on identical inputs.
+struct FrontierSlot {
+  int32_t n;              // window hosts listed (<= ZW_M)
+  int32_t total;          // candidates counted in the range (ordered walk: alive hosts)
+  int32_t pad[2];
+  int32_t id[ZW_M];       // global host index, ascending
+  double a[4][ZW_M];      // capacities
+};
+struct FrontierHdr {
+  int32_t kind, nslots, pad[14];
+  double hmin[ZW_MIN_PARTS][4];   // host-minimum partials over the rank's range
+};
+struct ZwinArgs {         // window candidates of one rank, per epoch chain
+  const double* avail;
+  const int32_t* zone;
+  int H, Z, lo, hi;
+  const double* csum;
+  const int32_t* anc;     // epoch tasks' anchors
+  const int32_t* coff;    // chain c: epoch tasks cmap[coff[c] .. coff[c+1])
+  const int32_t* cmap;
+  FrontierSlot* out;      // [nchains]
+};
+void launch_zwin_build(const ZwinArgs& a, int nchains, hipStream_t st);
+// keyed / ordered walks: slot from a compacted local host list (host lo + perm[p], p < *count)
+void launch_zwin_gather(const double* avail, int H, int lo, const int32_t* perm,
+                        const int32_t* count, FrontierSlot* out, hipStream_t st);
+// after the all-gather: merged slots [nslots] and host-minimum partials (ZW_MIN_PARTS x 4)
+void launch_zwin_merge(const uint8_t* pkgs, int64_t pkg_bytes, int world, int nslots,
+                       FrontierSlot* out, double* hmin, hipStream_t st);
 
 // cost_aware first-fit with sort_hosts, as the reference runs it (cost_aware.py:118-124): the
 // hosts sorted once per group by the frozen key (perm, skey = sorted key bits; the radix sort
@@ -258,6 +298,34 @@ struct KeyArgs {          // CA_FF sort_hosts: key[h] = c*df / (||avail_h|| * bw
   double* key;
   const double* rtb;      // realtime_bw: the group's bandwidth row [H], or NULL
 };
+
+// vbp best-fit lists by a memory band (pvt_band.hip): hosts [lo, hi) sorted once per round by
+// snapshot memory (sorted copy of their snapshot state), plus the hosts committed to since
+// (touched: flags[H], list, count), scanned with their live state.
+struct BandArgs {
+  const uint64_t* key;    // [n] orderable bits of the snapshot avail[1], ascending
+  const double* sa;       // [4][n] snapshot capacities in sorted order
+  const uint32_t* stb;    // [n] host-id ranks in sorted order
+  const int32_t* sid;     // [n] host index at each sorted position
+  int n, lo, hi;          // sorted hosts = [lo, hi)
+  const uint8_t* touched; // [H] 1: committed to since the snapshot
+  const int32_t* tlist;   // touched hosts
+  const int32_t* tcount;  // [1]
+  const double* avail;    // live state [4][H]
+  const uint32_t* tb;     // [H]
+  int H;
+  const double* dem;      // window tasks [nt][4]
+  int nt, S;              // S list segments per task
+  SegEntry* seg;          // [nt][S][KL]
+  int32_t* seg_feas;      // [nt][S]
+};
+void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,
+                      hipStream_t st);
+void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, const int32_t* sid,
+                        double* sa, uint32_t* stb, hipStream_t st);
+void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* flags, int32_t* tlist,
+                         int32_t* tcount, hipStream_t st);
+void launch_band_score(const BandArgs& a, hipStream_t st);
 
 int score_tasks_per_wave(int mode, int hosts, int force = 0);
 int score_diag(uint64_t* out, int n, int reset);   // PVT_DIAG builds; else PVT_EUNSUPPORTED

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "pivot_place.h"
 #include "pvt_device.h"
 #include "pvt_kernels.h"
 
@@ -70,12 +71,13 @@ __device__ __forceinline__ double wave_min_d(double v) {
   return v;
 }
 
-// Per-dimension minimum capacity over all hosts (certificate 2), ZW_MINB partials.
-__global__ __launch_bounds__(256) void host_min_kernel(const double* avail, int H, double* part) {
+// Per-dimension minimum capacity over hosts [lo, hi) (certificate 2), ZW_MINB partials.
+__global__ __launch_bounds__(256) void host_min_kernel(const double* avail, int H, int lo, int hi,
+                                                       double* part) {
   __shared__ double red[4][4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double m[4] = {DINF, DINF, DINF, DINF};
-  for (int h = blockIdx.x * 256 + tid; h < H; h += gridDim.x * 256)
+  for (int h = lo + blockIdx.x * 256 + tid; h < hi; h += gridDim.x * 256)
 #pragma unroll
     for (int r = 0; r < 4; r++) m[r] = fmin(m[r], avail[(size_t)r * H + h]);
 #pragma unroll
@@ -101,6 +103,51 @@ __device__ __forceinline__ void wave_lds_sync() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   __builtin_amdgcn_s_waitcnt(0xc07f);
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// The first ZW_M hosts of [h_lo, h_hi), in index order, whose zone is in the mask U, appended
+// to wid / wz from *nwin on (passes of ZW_SCAN x 256 hosts, every zone load of a pass in flight
+// at once, a stable block compaction; the block stops at the pass that fills the window).
+__device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, uint32_t U,
+                                                    int h_lo, int h_hi, int32_t* wid, int32_t* wz,
+                                                    int32_t (*cnt)[ZW_WAVES], int32_t* nwin) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int h0 = h_lo; h0 < h_hi; h0 += ZW_SCAN * ZW_THREADS) {
+    const int have = *nwin;
+    if (have >= ZW_M) break;
+    bool hit[ZW_SCAN];
+    int zz[ZW_SCAN];
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) {
+      const int h = h0 + k * ZW_THREADS + tid;
+      zz[k] = h < h_hi ? zone[h] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) {
+      const int z = zz[k];
+      hit[k] = z >= 0 && z < Z && ((U >> z) & 1u);
+      const uint64_t m = __ballot(hit[k]);
+      if (lane == 0) cnt[k][wave] = __popcll(m);
+    }
+    __syncthreads();
+    int pre = have;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) {
+      int before = 0;
+      for (int w = 0; w < ZW_WAVES; w++) before += (w < wave) ? cnt[k][w] : 0;
+      const uint64_t m = __ballot(hit[k]);
+      const int pos = pre + before + __popcll(m & below);
+      if (hit[k] && pos < ZW_M) {
+        wid[pos] = h0 + k * ZW_THREADS + tid;
+        if (wz) wz[pos] = zz[k];
+      }
+      for (int w = 0; w < ZW_WAVES; w++) pre += cnt[k][w];
+    }
+    __syncthreads();
+    if (tid == 0) *nwin = min(pre, ZW_M);
+    __syncthreads();
+  }
 }
 
 #ifdef PVT_STAMPS
@@ -196,53 +243,26 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   for (int r = 0; r < 4; r++) sep |= (ha[r] - mx[r] >= 0x1p-288);
   const uint32_t U = S.umask;
   if (S.bail || !sep || nt <= 0) {
-    if (tid == 0) { status[0] = KEYED ? 0 : -2; status[1] = 0; }
+    if (tid == 0) { status[0] = 0; status[1] = (KEYED || nt <= 0) ? 0 : 1; }
     return;
   }
-  if (KEYED) {                               // window: the zero-key prefix's first hosts
+  const FrontierSlot* pw = A.pwin ? A.pwin + (KEYED ? 0 : b) : nullptr;
+  if (pw) {                                  // host-sharded: the merged window, capacities too
+    const int nw = min(pw->n, ZW_M);
+    for (int p = tid; p < nw; p += ZW_THREADS) {
+      const int32_t h = pw->id[p];
+      S.wid[p] = h;
+      S.wz[p] = KEYED ? 0 : A.zone[h];
+    }
+    if (tid == 0) S.nwin = nw;
+    __syncthreads();
+  } else if (KEYED) {                        // window: the zero-key prefix's first hosts
     const int nw = min(A.kn_dev ? *A.kn_dev : A.kn, ZW_M);
     for (int p = tid; p < nw; p += ZW_THREADS) { S.wid[p] = A.lo + A.kperm[p]; S.wz[p] = 0; }
     if (tid == 0) S.nwin = nw;
     __syncthreads();
-  }
-
-  // window: U's hosts in index order (passes of ZW_SCAN x 256 hosts, stable compaction)
-  for (int h0 = 0; h0 < (KEYED ? 0 : H); h0 += ZW_SCAN * ZW_THREADS) {
-    const int have = S.nwin;
-    if (have >= ZW_M) break;
-    bool hit[ZW_SCAN];
-    int zz[ZW_SCAN];
-#pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) {      // every load in flight at once
-      const int h = h0 + k * ZW_THREADS + tid;
-      zz[k] = h < H ? A.zone[h] : -1;
-    }
-#pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) {
-      const int z = zz[k];
-      hit[k] = z >= 0 && z < Z && ((U >> z) & 1u);
-      const uint64_t m = __ballot(hit[k]);
-      if (lane == 0) S.cnt[k][wave] = __popcll(m);
-    }
-    __syncthreads();
-    int pre = have;
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-#pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) {
-      int before = 0;
-      for (int w = 0; w < ZW_WAVES; w++) before += (w < wave) ? S.cnt[k][w] : 0;
-      const uint64_t m = __ballot(hit[k]);
-      const int pos = pre + before + __popcll(m & below);
-      if (hit[k] && pos < ZW_M) {
-        const int h = h0 + k * ZW_THREADS + tid;
-        S.wid[pos] = h;
-        S.wz[pos] = zz[k];
-      }
-      for (int w = 0; w < ZW_WAVES; w++) pre += S.cnt[k][w];
-    }
-    __syncthreads();
-    if (tid == 0) S.nwin = min(pre, ZW_M);
-    __syncthreads();
+  } else {                                   // window: U's hosts in index order
+    compact_zone_window(A.zone, Z, U, 0, H, S.wid, S.wz, S.cnt, &S.nwin);
   }
   const int nwin = S.nwin;
   bool wbad = false;
@@ -250,7 +270,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     const int h = S.wid[p];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      const double v = A.avail[(size_t)r * H + h];
+      const double v = pw ? pw->a[r][p] : A.avail[(size_t)r * H + h];
       wbad |= !(__builtin_fabs(v) <= ZW_BIG);
       S.wa[r][p] = v;
     }
@@ -258,7 +278,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   if (wbad) S.bail = 1;
   __syncthreads();
   if (S.bail || nwin == 0) {
-    if (tid == 0) { status[0] = KEYED ? 0 : -2; status[1] = 0; }
+    if (tid == 0) { status[0] = 0; status[1] = KEYED ? 0 : 1; }
     return;
   }
   // suffix minima of the chain's demands per 64-task batch: a chunk no host of which fits the
@@ -533,7 +553,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       for (int r = 0; r < 4; r++) A.wb[(size_t)r * H + h] = S.wa[r][p];
     }
   }
-  if (lane == 0) { status[0] = (failed && !KEYED) ? -2 : done; status[1] = 0; }
+  // status[0]: tasks proven (their log entries are exact; validation accepts them), status[1]:
+  // 1 when a certificate failed there (the rest of the chain is left to the list walk)
+  if (lane == 0) { status[0] = done; status[1] = (failed && !KEYED) ? 1 : 0; }
 #ifdef PVT_STAMPS
   if (lane == 0 && A.stamps) {
     const uint64_t t_end = zstamp();
@@ -546,8 +568,8 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #endif
 }
 
-void launch_host_min(const double* avail, int H, double* part, hipStream_t st) {
-  hipLaunchKernelGGL(host_min_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, part);
+void launch_host_min(const double* avail, int H, int lo, int hi, double* part, hipStream_t st) {
+  hipLaunchKernelGGL(host_min_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, lo, hi, part);
 }
 
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st) {
@@ -579,20 +601,121 @@ __global__ __launch_bounds__(1024) void dem_min_kernel(const double* dem, int n,
     out[tid] = v;
   }
 }
-__global__ void alive_flags_kernel(const double* avail, int H, int hs, const double* dmin,
+__global__ void alive_flags_kernel(const double* avail, int H, int lo, int hs, const double* dmin,
                                    int strict, uint8_t* flags) {
-  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  const int h = lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (h >= hs) return;
   const double a0 = avail[h], a1 = avail[(size_t)H + h], a2 = avail[2 * (size_t)H + h],
                a3 = avail[3 * (size_t)H + h];
-  flags[h] = strict ? fits<true>(a0, a1, a2, a3, dmin[0], dmin[1], dmin[2], dmin[3])
+  flags[h - lo] = strict ? fits<true>(a0, a1, a2, a3, dmin[0], dmin[1], dmin[2], dmin[3])
                     : fits<false>(a0, a1, a2, a3, dmin[0], dmin[1], dmin[2], dmin[3]);
 }
-void launch_alive_flags(const double* avail, int H, int hs, const double* dem, int n, int strict,
-                        double* dmin, uint8_t* flags, hipStream_t st) {
+void launch_alive_flags(const double* avail, int H, int lo, int hs, const double* dem, int n,
+                        int strict, double* dmin, uint8_t* flags, hipStream_t st) {
   hipLaunchKernelGGL(dem_min_kernel, dim3(1), dim3(1024), 0, st, dem, n, dmin);
-  hipLaunchKernelGGL(alive_flags_kernel, dim3((hs + 255) / 256), dim3(256), 0, st, avail, H, hs,
-                     dmin, strict, flags);
+  if (hs <= lo) return;
+  hipLaunchKernelGGL(alive_flags_kernel, dim3((hs - lo + 255) / 256), dim3(256), 0, st, avail, H,
+                     lo, hs, dmin, strict, flags);
+}
+
+// ---- host-sharded frontier walks: a rank's window candidates, and their merge
+
+// Chain b of the epoch: its zero-cost zones U (the union of its anchors' zero-cost zones, as the
+// walk computes them) and the first ZW_M hosts of U in this rank's range [lo, hi), index order,
+// with their capacities; block 0 also stamps the package header.
+__global__ __launch_bounds__(ZW_THREADS) void zwin_build_kernel(ZwinArgs A) {
+  __shared__ uint32_t amask[ZMAX];
+  __shared__ uint32_t umask;
+  __shared__ int32_t cnt[ZW_SCAN][ZW_WAVES];
+  __shared__ int32_t nwin;
+  const int b = blockIdx.x, tid = threadIdx.x, Z = A.Z;
+  FrontierSlot* out = A.out + b;
+  if (tid == 0) { umask = 0; nwin = 0; }
+  if (tid < Z) {
+    uint32_t m = 0;
+    for (int z = 0; z < Z; z++) m |= (A.csum[tid * Z + z] == 0.0) ? (1u << z) : 0u;
+    amask[tid] = m;
+  }
+  __syncthreads();
+  uint32_t um = 0;
+  for (int i = A.coff[b] + tid; i < A.coff[b + 1]; i += ZW_THREADS) {
+    const int a = A.anc[A.cmap[i]];
+    if (a >= 0 && a < Z) um |= amask[a];    // (a bad anchor: the walk bails on it)
+  }
+  if (um) atomicOr(&umask, um);
+  __syncthreads();
+  compact_zone_window(A.zone, Z, umask, A.lo, A.hi, out->id, nullptr, cnt, &nwin);
+  const int n = nwin;
+  for (int p = tid; p < n; p += ZW_THREADS) {
+    const int h = out->id[p];
+#pragma unroll
+    for (int r = 0; r < 4; r++) out->a[r][p] = A.avail[(size_t)r * A.H + h];
+  }
+  if (tid == 0) { out->n = n; out->total = n; }
+}
+
+__global__ __launch_bounds__(256) void zwin_gather_kernel(const double* avail, int H, int lo,
+                                                          const int32_t* perm, const int32_t* count,
+                                                          FrontierSlot* out) {
+  const int c = *count, n = min(c, ZW_M);
+  for (int p = threadIdx.x; p < n; p += 256) {
+    const int h = lo + perm[p];
+    out->id[p] = h;
+#pragma unroll
+    for (int r = 0; r < 4; r++) out->a[r][p] = avail[(size_t)r * H + h];
+  }
+  if (threadIdx.x == 0) { out->n = n; out->total = c; }
+}
+
+// Block b < nslots: slot b of every rank, concatenated in rank order and cut at ZW_M (ranks own
+// ascending ranges, so this is the index-order window); block nslots: the host-minimum partials,
+// the minimum over ranks.
+__global__ __launch_bounds__(256) void zwin_merge_kernel(const uint8_t* pkgs, int64_t pkg_bytes,
+                                                         int world, int nslots, FrontierSlot* out,
+                                                         double* hmin) {
+  __shared__ int32_t off[PVT_SHARD_MAX_WORLD + 1];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  auto hdr = [&](int k) { return reinterpret_cast<const FrontierHdr*>(pkgs + (size_t)k * pkg_bytes); };
+  if (b == nslots) {               // (keyed / ordered walks: hmin NULL, no minima exchanged)
+    for (int i = tid; hmin && i < ZW_MIN_PARTS * 4; i += 256) {
+      double m = DINF;
+      for (int k = 0; k < world; k++) m = fmin(m, (&hdr(k)->hmin[0][0])[i]);
+      (&hmin[0])[i] = m;
+    }
+    return;
+  }
+  auto slot = [&](int k) { return reinterpret_cast<const FrontierSlot*>(hdr(k) + 1) + b; };
+  if (tid == 0) {
+    int o = 0, tot = 0;
+    for (int k = 0; k < world; k++) { off[k] = o; o += slot(k)->n; tot += slot(k)->total; }
+    off[world] = o;
+    out[b].n = min(o, ZW_M);
+    out[b].total = tot;
+  }
+  __syncthreads();
+  for (int k = 0; k < world && off[k] < ZW_M; k++) {
+    const FrontierSlot* s = slot(k);
+    const int n = min(s->n, ZW_M - off[k]);
+    for (int p = tid; p < n; p += 256) {
+      const int q = off[k] + p;
+      out[b].id[q] = s->id[p];
+#pragma unroll
+      for (int r = 0; r < 4; r++) out[b].a[r][q] = s->a[r][p];
+    }
+  }
+}
+
+void launch_zwin_build(const ZwinArgs& a, int nchains, hipStream_t st) {
+  hipLaunchKernelGGL(zwin_build_kernel, dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+}
+void launch_zwin_gather(const double* avail, int H, int lo, const int32_t* perm,
+                        const int32_t* count, FrontierSlot* out, hipStream_t st) {
+  hipLaunchKernelGGL(zwin_gather_kernel, dim3(1), dim3(256), 0, st, avail, H, lo, perm, count, out);
+}
+void launch_zwin_merge(const uint8_t* pkgs, int64_t pkg_bytes, int world, int nslots,
+                       FrontierSlot* out, double* hmin, hipStream_t st) {
+  hipLaunchKernelGGL(zwin_merge_kernel, dim3(nslots + 1), dim3(256), 0, st, pkgs, pkg_bytes, world,
+                     nslots, out, hmin);
 }
 
 }  // namespace pvt

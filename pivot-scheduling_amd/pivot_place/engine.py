@@ -47,6 +47,7 @@ def load_library(path=None):
         "pvt_set_score_tw": ([c_void_p, c_int], c_int),
         "pvt_set_epochs": ([c_void_p, c_int], c_int),
         "pvt_set_zero_walk": ([c_void_p, c_int], c_int),
+        "pvt_set_band": ([c_void_p, ctypes.c_int32], c_int),
         "pvt_zero_walk_stats": ([c_void_p] + [ctypes.POINTER(ctypes.c_int64)] * 3, c_int),
         "pvt_epoch_stats": ([c_void_p, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64),
                              ctypes.POINTER(ctypes.c_int64)], c_int),
@@ -376,6 +377,11 @@ class PlacementEngine:
     def set_epochs(self, on=True):
         """cost_aware best-fit: group-parallel speculative epochs (default on; identical results)."""
         self._check(self.lib.pvt_set_epochs(self.ctx, int(bool(on))))
+
+    def set_band(self, min_hosts=65536):
+        """vbp best-fit: band lists over hosts sorted by snapshot memory from ``min_hosts`` hosts
+        on (0: the streaming score pass always; identical results)."""
+        self._check(self.lib.pvt_set_band(self.ctx, int(min_hosts)))
 
     def set_zero_walk(self, on=True):
         """Epoch chains: the zero-cost frontier walk where it proves its winners (default on;

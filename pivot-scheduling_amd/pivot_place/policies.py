@@ -97,6 +97,24 @@ class _ClusterTables:
         else:
             self.cost = np.zeros((1, 1))
             self.bw = np.ones((1, 1))
+        self._routes = {}
+
+    def routes_of(self, cluster, anchor):
+        """(in routes, out routes) between storage ``anchor`` and every host, in host order,
+        looked up once per cluster (the route objects are the cluster's own; their queues are
+        read when a round needs their realtime bandwidth). A missing route raises what the
+        reference's host_score_func raises reading it (cost_aware.py:73-79, 106-112)."""
+        if getattr(self, "_routes_cluster", None) is not cluster:
+            self._routes, self._routes_cluster = {}, cluster
+        got = self._routes.get(anchor.id)
+        if got is None:
+            get_route = cluster.get_route
+            ins = [get_route(anchor.id, h) for h in self.host_ids]
+            outs = [get_route(h, anchor.id) for h in self.host_ids]
+            if any(x is None for x in ins) or any(x is None for x in outs):
+                raise AttributeError("'NoneType' object has no attribute 'realtime_bw'")
+            got = self._routes[anchor.id] = (ins, outs)
+        return got
 
     def matches(self, cluster):
         hosts = cluster.hosts
@@ -122,12 +140,12 @@ class PlacementMixin:
             self._pvt_tables = tab
         return tab
 
-    @staticmethod
-    def _snapshot(hosts, resc):
-        a = np.empty((4, len(hosts)), dtype=np.float64)
-        for j, h in enumerate(hosts):
-            a[:, j] = resc[h.id]
-        return a
+    def _snapshot(self, resc):
+        """The round snapshot as SoA avail[4][H] (one stack of the per-host arrays)."""
+        ids = self._tables().host_ids
+        if not ids:
+            return np.empty((4, 0), dtype=np.float64)
+        return np.ascontiguousarray(np.stack([resc[i] for i in ids], axis=1), dtype=np.float64)
 
     @staticmethod
     def _demand(tasks):
@@ -137,12 +155,12 @@ class PlacementMixin:
         return d
 
     def _apply(self, tasks, hosts, resc, res, before):
-        for t, p in zip(tasks, res.placement):
-            if p >= 0:
-                t.placement = hosts[p].id
+        ids = self._tables().host_ids
+        for j in np.nonzero(res.placement >= 0)[0]:
+            tasks[j].placement = ids[res.placement[j]]
         changed = np.nonzero((res.avail != before).any(axis=0))[0]
         for j in changed:
-            resc[hosts[j].id][:] = res.avail[:, j]
+            resc[ids[j]][:] = res.avail[:, j]
 
 
 class CostAwarePlacement(PlacementMixin):
@@ -197,14 +215,19 @@ class CostAwarePlacement(PlacementMixin):
             groups.setdefault(key, []).append(t)
         return groups
 
-    def _realtime_row(self, anchor, hosts):
+    def _realtime_row(self, anchor, memo):
         """realtime_bw=True (cost_aware.py:73-79, :106-112): per host, the bandwidth the
         reference's host_score_func uses, in_route.realtime_bw + out_route.realtime_bw of the
         routes between the anchor storage and the host (resources/network.py:70-73), read from
-        the cluster's own route objects and summed in the reference's order."""
-        get_route = self.cluster.get_route
-        return [get_route(anchor.id, h.id).realtime_bw + get_route(h.id, anchor.id).realtime_bw
-                for h in hosts]
+        the cluster's own route objects (looked up once per cluster) and summed elementwise in
+        the reference's order. Queues do not move inside schedule(), so groups sharing an
+        anchor share the row."""
+        row = memo.get(anchor.id)
+        if row is None:
+            ins, outs = self._tables().routes_of(self.cluster, anchor)
+            row = memo[anchor.id] = (np.array([x.realtime_bw for x in ins], dtype=np.float64)
+                                     + np.array([x.realtime_bw for x in outs], dtype=np.float64))
+        return row
 
     def schedule(self, tasks):
         algo = self._pvt_algo
@@ -220,9 +243,13 @@ class CostAwarePlacement(PlacementMixin):
         T = len(tasks)
         task_group = np.zeros(T, dtype=np.int32)
         anchors, rt_rows = [], []
-        avail = self._snapshot(hosts, resc)
+        avail = self._snapshot(resc)
         dem = self._demand(tasks)
         best_fit = algo == 'best-fit'
+        # the reference reads routes only through host_score_func: best-fit, and first-fit with
+        # sort_hosts (cost_aware.py:92, 118-119); unsorted first-fit never does
+        rt = self._pvt_realtime_bw and (best_fit or self._pvt_sort_hosts)
+        rt_memo = {}
         for g, ((kind, obj), members) in enumerate(groups.items()):
             anchor = self.randomizer.choice(storage) if kind == 'app' else obj
             if best_fit and self._pvt_host_decay:
@@ -233,8 +260,8 @@ class CostAwarePlacement(PlacementMixin):
             anchors.append(tab.zone_of[anchor.locality])
             for t in members:
                 task_group[task_pos[id(t)]] = g
-            if self._pvt_realtime_bw:
-                rt_rows.append(self._realtime_row(anchor, hosts))
+            if rt:
+                rt_rows.append(self._realtime_row(anchor, rt_memo))
         if best_fit and self._pvt_host_decay:
             return tasks
         decay = None
@@ -244,8 +271,7 @@ class CostAwarePlacement(PlacementMixin):
                         zone=tab.zone, dem=dem, cost=tab.cost, bw=tab.bw, decay=decay,
                         task_group=task_group, group_anchor=np.array(anchors, dtype=np.int32),
                         sort_tasks=self._pvt_sort_tasks, sort_hosts=self._pvt_sort_hosts,
-                        rt_bw=np.array(rt_rows, dtype=np.float64).reshape(len(rt_rows), -1)
-                        if rt_rows else None)
+                        rt_bw=np.stack(rt_rows) if rt_rows else None)
         if T:
             res = self._engine().place(r)
             self._apply(tasks, hosts, resc, res, avail)
@@ -265,7 +291,7 @@ class OpportunisticPlacement(PlacementMixin):
         mt = np.empty(625, dtype=np.uint32)
         mt[:624] = st[1]
         mt[624] = st[2]
-        avail = self._snapshot(hosts, resc)
+        avail = self._snapshot(resc)
         r = RoundArrays(mode=_abi.PVT_OPP, avail=avail, zone=tab.zone, dem=self._demand(tasks),
                         mt_state=mt)
         res = self._engine().place(r)
@@ -290,7 +316,7 @@ class _VbpPlacement(PlacementMixin):
         if not tasks:
             return list(tasks) if self._pvt_decreasing else tasks
         tab = self._tables()
-        avail = self._snapshot(hosts, resc)
+        avail = self._snapshot(resc)
         r = RoundArrays(mode=self._mode, avail=avail, zone=tab.zone, dem=self._demand(tasks),
                         tiebreak=tab.rank, sort_tasks=bool(self._pvt_decreasing))
         res = self._engine().place(r)

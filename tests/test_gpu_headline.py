@@ -69,9 +69,11 @@ def test_config5_both_score_instances(engine, mode, tw):
     r, ref = headline(mode)
     try:
         engine.set_score_tw(tw)
+        engine.set_band(0)      # vbp best-fit: the streaming score pass (band lists: default)
         res = engine.place(r)
     finally:
         engine.set_score_tw(0)
+        engine.set_band(65536)
     assert_same(res, ref, "config 5 %s tw=%d" % (_abi.MODE_NAMES[mode], tw))
 
 
@@ -93,3 +95,25 @@ def test_config4_batch_per_gpu_matches_oracle(engine, mode):
     got = engine.place_batch(rounds)
     for s, (r, res) in enumerate(zip(rounds, got)):
         assert_same(res, oracle.place(r), "config 4 %s scenario %d" % (_abi.MODE_NAMES[mode], s))
+
+
+@pytest.fixture(scope="module")
+def shard_engines():
+    from pivot_place.engine import PlacementEngine
+    return [PlacementEngine(0) for _ in range(8)]
+
+
+@pytest.mark.parametrize("mode", ALL_MODES, ids=lambda m: _abi.MODE_NAMES[m])
+def test_config5_host_sharded_world8(shard_engines, mode):
+    """BASELINE config 5 as written: the host dimension split 8 ways (8 contexts in lock-step on
+    one GPU, exchange by concatenation -- the same packages an RCCL all-gather carries). cost_aware
+    best-fit runs frontier-walked epochs, first-fit the keyed / ordered frontier walks, the others
+    their list windows; every rank equals the oracle."""
+    from pivot_place.sharded import place_lockstep
+    r, ref = headline(mode)
+    outs = place_lockstep(shard_engines, r)
+    for k, o in enumerate(outs):
+        assert_same(o, ref, "config 5 %s host-sharded rank %d/8" % (_abi.MODE_NAMES[mode], k))
+    if mode in (_abi.PVT_CA_BF, _abi.PVT_CA_FF, _abi.PVT_VBP_FF):
+        st = shard_engines[0].epoch_stats()
+        assert st["frontier_chains"] > 0, st

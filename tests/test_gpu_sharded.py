@@ -178,3 +178,62 @@ def test_sharded_keyed_prefix_runs_dry(engines, world):
     ref = oracle.place(r)
     assert (ref.placement >= 0).sum() > 0
     _assert_same(_lockstep(engines, world, r), ref)
+
+
+def _frontier_round(kind, H, T, seed):
+    if kind == "ca_ff_unsorted":
+        return synthetic.make_round(_abi.PVT_CA_FF, H, T, seed=seed, sort_hosts=False)
+    return synthetic.make_round({"ca_bf": _abi.PVT_CA_BF, "ca_ff": _abi.PVT_CA_FF,
+                                 "vbp_ff": _abi.PVT_VBP_FF}[kind], H, T, seed=seed)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+@pytest.mark.parametrize("kind", ["ca_bf", "ca_ff", "vbp_ff", "ca_ff_unsorted"])
+def test_sharded_frontier_walks(engines, kind, world):
+    """The frontier walks on a host-sharded round: cost_aware best-fit epochs (every rank packs
+    its first hosts of each chain's zero-cost zones + its host minima), the keyed walk at each
+    cost_aware first-fit group start (its first zero-key hosts) and the ordered walk of vbp /
+    unsorted cost_aware first-fit (its first alive hosts). After the all-gather every rank walks
+    the merged window; all ranks equal the oracle, and the walks did place tasks on every rank."""
+    r = _frontier_round(kind, 40_000, 2600, seed=21)
+    ref = oracle.place(r, threads=8)
+    _assert_same(_lockstep(engines, world, r), ref)
+    for e in engines[:world]:
+        st = e.epoch_stats()
+        assert st["frontier_chains"] > 0, (kind, world, st)
+        if kind == "ca_bf":
+            assert st["epochs"] >= 1 and st["list_chains"] == 0, st
+
+
+def _loaded(case, seed):
+    r = synthetic.make_round(_abi.PVT_CA_BF, 20_000, 6000, seed=seed)
+    if case == "spill":          # zones 0-9 empty: groups spill and collide (rejected segments)
+        r.avail[:2, r.zone < 10] = 0.0
+    elif case == "window":       # one small task per host: chains outgrow the 1024-host window
+        r.avail[0, :] = 0.5
+    elif case == "exact":        # exact fits in other zones: certificate 2 fails -> lists
+        r.avail[2, :] = 0.0
+        r.avail[3, :] = 0.0
+        for k, h in enumerate(range(3, 400, 7)):
+            r.avail[0, h] = r.dem[0, k * 11]
+            r.avail[1, h] = r.dem[1, k * 11]
+    return r
+
+
+@pytest.mark.parametrize("world", [1, 3, 8])
+@pytest.mark.parametrize("case", ["spill", "window", "exact"])
+def test_sharded_epochs_fall_back_to_lists(engines, case, world):
+    """Sharded cost_aware best-fit rounds the frontier walk cannot carry alone: rejected
+    segments are walked again, unproven chains go to list windows up to the end of their epoch
+    and the frontier epochs resume after them. Equal to the oracle on every rank."""
+    r = _loaded(case, 30 + world)
+    _assert_same(_lockstep(engines, world, r), oracle.place(r, threads=8))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_ordered_frontier_empty_ranks(engines, world):
+    """vbp first-fit where only the last ranks' hosts are alive at first (the first span holds
+    no alive host: the span doubles) and ranks past the span pack nothing."""
+    r = synthetic.make_round(_abi.PVT_VBP_FF, 200_000, 3000, seed=23)
+    r.avail[0, :150_000] = 0.0
+    _assert_same(_lockstep(engines, world, r), oracle.place(r, threads=8))

@@ -75,3 +75,50 @@ def test_policy_host_logic(name, idx):
 @pytest.mark.parametrize("name,idx", golden_io.all_runs(skip_errors=False))
 def test_policy_on_engine(engine, name, idx):
     _run(name, idx, engine)
+
+
+def _rt_case():
+    """A recorded realtime_bw state (storage <-> host routes with queued packets)."""
+    case = golden_io.load("rt_h12")
+    run = next(r for r in case["runs"] if r["kwargs"].get("realtime_bw"))
+    return case, run
+
+
+@pytest.mark.parametrize("algo,sort_hosts,raises", [("first-fit", False, False),
+                                                   ("first-fit", True, True),
+                                                   ("best-fit", False, True)])
+def test_realtime_bw_missing_route(algo, sort_hosts, raises):
+    """realtime_bw with one storage <-> host route missing: the reference reads routes only in
+    host_score_func (best-fit, and first-fit with sort_hosts; cost_aware.py:69-83, 104-119), so
+    unsorted first-fit places as usual while the other two raise AttributeError."""
+    case, run = _rt_case()
+    cluster, tasks = fakes.build(case)
+    h0 = cluster.hosts[0].id
+    for s in cluster.storage:
+        cluster._routes.pop((s.id, h0), None)
+    sched = policies.CostAwareGlobalScheduler(None, cluster, seed=run["seed"],
+                                              bin_pack_algo=algo, sort_tasks=True,
+                                              sort_hosts=sort_hosts, realtime_bw=True)
+    sched.engine = OracleEngine()
+    sched._update_resource_info()
+    if raises:
+        with pytest.raises(AttributeError):
+            sched.schedule(list(tasks))
+    else:
+        sched.schedule(list(tasks))
+        assert any(t.placement is not None for t in tasks)
+
+
+def test_realtime_rows_shared_by_anchor():
+    """Groups of one anchor storage share one realtime row, read from the cluster's route
+    objects once per round (the queues do not move inside schedule())."""
+    case, run = _rt_case()
+    cluster, tasks = fakes.build(case)
+    sched = policies.CostAwareGlobalScheduler(None, cluster, seed=run["seed"], **run["kwargs"])
+    memo = {}
+    a = cluster.storage[0]
+    row = sched._realtime_row(a, memo)
+    assert sched._realtime_row(a, memo) is row
+    want = [cluster.get_route(a.id, h.id).realtime_bw + cluster.get_route(h.id, a.id).realtime_bw
+            for h in cluster.hosts]
+    assert row.tolist() == want

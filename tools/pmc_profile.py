@@ -25,12 +25,21 @@ Writes gpurun_out/pmc_<tag>.json and gpurun_out/pmc_<tag>.csv.
 import argparse
 import csv
 import glob
+import hashlib
 import json
 import os
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "pivot-scheduling_amd", "pivot_place", "libpivot_place.so")
+
+
+def lib_sha256(path=LIB):
+    """sha256 of the engine library the probe loads: bench.py uses a PMC profile only for the
+    binary it was collected on."""
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
 PASSES = {
     "sq": ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_LDS", "SQ_LDS_IDX_ACTIVE",
            "SQ_LDS_BANK_CONFLICT", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "GRBM_GUI_ACTIVE"],
@@ -111,7 +120,7 @@ def main():
         durs += list(dur.values())
         avg.setdefault("dispatches_" + name, len(vals))
     dur_s = (sum(durs) / len(durs)) * 1e-9 if durs else None
-    out = {"kernel": kname, "probe": probe, "counters_per_launch": avg,
+    out = {"kernel": kname, "probe": probe, "lib_sha256": lib_sha256(), "counters_per_launch": avg,
            "profiled_duration_ms": dur_s * 1e3 if dur_s else None}
     if "SQ_ACTIVE_INST_VALU" in avg:
         out["valu_busy_cycles_per_launch"] = 4.0 * avg["SQ_ACTIVE_INST_VALU"]
