@@ -22,6 +22,7 @@ With --gpus N > 1 and no WORLD_SIZE in the environment, bench.py starts N rank p
 itself (before anything touches the GPU); under torchrun WORLD_SIZE must equal N.
 """
 import argparse
+import hashlib
 import json
 import os
 import socket
@@ -31,6 +32,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "pivot-scheduling_amd"), ROOT]
+LIB = os.path.join(ROOT, "pivot-scheduling_amd", "pivot_place", "libpivot_place.so")
 
 import numpy as np  # noqa: E402
 
@@ -74,9 +76,13 @@ def parse():
     p.add_argument("--extra", type=int, default=-1,
                    help="1: also time (and parity-check) the other policies at config 5 and all "
                         "policies at config 3; -1 (default): only for the default workload at N=1")
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02c_score_pmc.json"),
-                   help="rocprofv3 PMC summary of the score kernel of this binary "
-                        "(tools/pmc_profile.py); absent or another config = counters null")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo: ranks may "
+                        "share a GPU, e.g. to rehearse the multi-rank path on one card)")
+    p.add_argument("--replay", type=int, default=-1,
+                   help="1: also time BASELINE configs 1 and 2 -- every schedule() round of the "
+                        "recorded reference simulations through the drop-in policy classes; -1 "
+                        "(default): with the default workload's extras")
     return p.parse_args()
 
 
@@ -152,162 +158,323 @@ def check_parity(got, r, ref=None):
 
 
 # ---------------------------------------------------------------------------- extra workloads
-def time_round(eng, r, steps, warmup):
-    """ms per step of pvt_place on a resident round (reset + place), and the placed result."""
+KCLASSES = (("score", 0), ("merge", 1), ("commit", 2), ("other", 3))
+
+
+def kstats_all(eng):
+    return {name: eng.kstats(k) for name, k in KCLASSES}
+
+
+def time_round(eng, r, steps, warmup, batch=None):
+    """ms per step of pvt_place on a resident round (reset + place) -- or of pvt_place_batch on
+    a resident batch -- the placed result(s) and the kernel-class times of the timed steps."""
     import torch
-    from pivot_place.engine import DeviceRound
-    dr = DeviceRound(r, eng.device)
+    from pivot_place.engine import DeviceBatch, DeviceRound
+    dr = DeviceBatch(batch, eng.device) if batch else DeviceRound(r, eng.device)
+    run = eng.run_batch if batch else eng.run
     for _ in range(warmup):
         dr.reset()
-        eng.run(dr)
+        run(dr)
     torch.cuda.synchronize()
+    eng.reset_kstats()
+    eng.set_profiling(True)
     t0 = time.perf_counter()
     for _ in range(steps):
         dr.reset()
-        eng.run(dr)
+        run(dr)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / steps
-    return ms, dr.result()
+    eng.set_profiling(False)
+    ks = kstats_all(eng)
+    return ms, (dr.results() if batch else dr.result()), ks
+
+
+def loaded_round(seed):
+    """Config 5 with every host holding at most 1 cpu free: a host takes one or two tasks, so the
+    longest zero-cost chains need more than the frontier walk's 1024-host window and fall back to
+    candidate lists (the list-walk cliff of the default line's engine)."""
+    from pivot_place import synthetic
+    r = synthetic.make_round(MODES["ca_bf"], DEFAULT_H, DEFAULT_T, seed=seed)
+    r.avail[0] = np.minimum(r.avail[0], 1.0)
+    return r
 
 
 def extra_workloads(eng, args, skip_mode):
-    """Config 5 (1M x 10k) for the other policies and config 3 (100k x 1k) for all five, each
-    timed on the same engine and checked against the oracle."""
+    """Config 5 (1M x 10k) for the other policies, a loaded config-5 cost_aware best-fit round,
+    config 3 (100k x 1k) and config 4 at its per-GPU size (512 scenarios x 1000 hosts x 1000
+    tasks, one pvt_place_batch launch) for all five; each timed on the same engine, with its
+    kernel-class times, and checked against the oracle."""
+    from oracle import oracle
     from pivot_place import synthetic
     out = {}
     steps, warm = max(1, min(args.steps, 5)), 1
-    for tag, H, T, modes in (("c5", DEFAULT_H, DEFAULT_T, [m for m in MODES if m != skip_mode]),
-                             ("c3", 100_000, 1000, list(MODES))):
-        for m in modes:
-            r = synthetic.make_round(MODES[m], H, T, seed=args.seed)
-            ms, got = time_round(eng, r, steps, warm)
+    jobs = [("c5_%s" % m, MODES[m], DEFAULT_H, DEFAULT_T, None) for m in MODES if m != skip_mode]
+    jobs.append(("c5_ca_bf_loaded", MODES["ca_bf"], DEFAULT_H, DEFAULT_T, "loaded"))
+    jobs += [("c3_%s" % m, MODES[m], 100_000, 1000, None) for m in MODES]
+    jobs += [("c4_%s" % m, MODES[m], 1000, 1000, "batch") for m in MODES]
+    for tag, mode, H, T, kind in jobs:
+        if kind == "batch":
+            B = 512
+            rounds = [synthetic.make_round(mode, H, T, seed=args.seed + s) for s in range(B)]
+            ms, got, ks = time_round(eng, None, steps, warm, batch=rounds)
+            ok = (all(same_result(g, oracle.place(x)) for g, x in zip(got, rounds))
+                  if args.parity else None)
+            cand = float(B) * T * H
+        else:
+            B = 0
+            r = loaded_round(args.seed) if kind == "loaded" else synthetic.make_round(mode, H, T, seed=args.seed)
+            ms, got, ks = time_round(eng, r, steps, warm)
             ok = check_parity(got, r) if args.parity else None
-            out["%s_%s" % (tag, m)] = {"value": float(T) * H / (ms * 1e-3), "ms_per_step": ms,
-                                       "hosts": H, "tasks": T, "steps": steps, "parity": ok}
-            log("[rank 0] extra %s %s: %.3e cand/s, %.2f ms, parity %s"
-                % (tag, m, float(T) * H / (ms * 1e-3), ms, ok))
+            cand = float(T) * H
+        ep = eng.epoch_stats()
+        e = {"value": cand / (ms * 1e-3), "ms_per_step": ms, "hosts": H, "tasks": T, "steps": steps,
+             "parity": ok, "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items()}}
+        if B:
+            e["scenarios"] = B
+        if mode == MODES["ca_bf"] and not B:
+            e["frontier_chains_per_step"] = ep["frontier_chains"]
+            e["list_chains_per_step"] = ep["list_chains"]
+        rl = extra_roofline(tag, mode, H, T, ks, steps)
+        if rl is not None:
+            e["roofline"] = rl
+        out[tag] = e
+        log("[rank 0] extra %s: %.3e cand/s, %.2f ms, parity %s" % (tag, e["value"], ms, ok))
     return out
 
 
 # ---------------------------------------------------------------------------- roofline
-def roofline(args, ks, mode, B):
-    """The score (candidate evaluation) kernel's roofline. `achieved` is the kernel's measured
-    per-launch work from the rocprofv3 PMC profile of this binary and config (VALU busy cycles,
-    LDS-array cycles, DRAM bytes; tools/pmc_profile.py -> profiles/) divided by the launch time
-    measured live here with HIP events on the launch's stream. The bound is the resource with
-    the highest utilisation. The SURVEY §8(d) figure (36 B per candidate) is kept as
-    `hbm_equivalent_*`: bytes a per-task streaming scan would move, not bytes moved."""
+# PMC profiles (tools/pmc_profile.py, collected into profiles/pmc_index.json by
+# tools/pmc_index.py) are used only for the binary they were collected on: each entry carries the
+# sha256 of libpivot_place.so, and an entry of another binary leaves the roofline's counters null.
+PMC_INDEX = os.path.join(ROOT, "profiles", "pmc_index.json")
+SIMDS, CUS = 1024, 256
+SHADER_HZ = 2.4e9
+ISSUE_CYCLES = 4          # one wave issues at most one instruction per 4 cycles
+LDS_DEP_CYCLES = 50       # one dependent LDS round trip (MI355X_MICROARCH.md constants table)
+INSTS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD",
+         "SQ_INSTS_VMEM_WR")
+_SHA = []
+
+
+def lib_sha256():
+    if not _SHA:
+        with open(LIB, "rb") as f:
+            _SHA.append(hashlib.sha256(f.read()).hexdigest())
+    return _SHA[0]
+
+
+def pmc_entry(mode, H, T, kernel):
+    """(PMC entry, note): the counter profile of ``kernel`` on this config, if it was collected
+    on THIS binary."""
+    name = [k for k, v in MODES.items() if v == mode][0]
+    key = "%s_%d_%d:%s" % (name, H, T, kernel)
+    try:
+        with open(PMC_INDEX) as f:
+            e = json.load(f).get("entries", {}).get(key)
+    except (OSError, ValueError):
+        return None, "no PMC index (tools/pmc_index.py)"
+    if e is None:
+        return None, "no PMC profile of %s for this config (tools/pmc_profile.py)" % key
+    if e.get("lib_sha256") != lib_sha256():
+        return None, ("the PMC profile of %s was collected on another build (lib sha256 %s..., "
+                      "this %s...): counters not used" % (key, str(e.get("lib_sha256"))[:12],
+                                                           lib_sha256()[:12]))
+    return e, None
+
+
+def score_roofline(mode, H, T, ks, kernel):
+    """A parallel candidate pass (streaming score, band score or resident kernel): its PMC
+    per-launch work (VALU busy cycles, LDS-array cycles, DRAM bytes) over the launch time
+    measured here with HIP events on the launch's stream; the bound is the most utilised
+    resource. The SURVEY §8(d) 36 / 32 B per logical candidate is kept as hbm_equivalent_*:
+    what a per-task streaming scan would move, not what moves."""
     from pivot_place import _abi
-    score = ks["score"]
-    launches = max(score["launches"], 1)
-    avg_ms = score["ms"] / launches
-    cand = score["candidates"] / launches
-    hbm_eq = score["bytes"] / launches / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    out = {"kernel": ("resident (registers-held hosts, full rescan per task)" if B
-                      else "score (fused fit-mask + score + top-K)"),
-           "avg_launch_ms": avg_ms, "candidates_per_launch": cand,
-           "hbm_equivalent_GBs": hbm_eq,
+    k = ks["score"]
+    launches = max(k["launches"], 1)
+    avg_ms = k["ms"] / launches
+    out = {"kernel": kernel, "avg_launch_ms": avg_ms, "launches": k["launches"],
+           "candidates_per_launch": k["candidates"] / launches,
+           "hbm_equivalent_GBs": (k["bytes"] / launches / (avg_ms * 1e-3) / 1e9) if avg_ms > 0 else 0.0,
            "hbm_equivalent_bytes_per_candidate": _abi.BYTES_PER_CANDIDATE[mode],
-           "bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
-           "traffic": None}
-    pmc = None
-    if os.path.exists(args.pmc_json):
-        try:
-            with open(args.pmc_json) as f:
-                allp = json.load(f)
-            key = "%s_%d_%d" % (args.mode, args.hosts, args.tasks)
-            pmc = allp.get("configs", {}).get(key)
-        except (OSError, ValueError):
-            pmc = None
+           "bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
+    pmc, note = pmc_entry(mode, H, T, kernel)
     if pmc is None or avg_ms <= 0:
-        out["note"] = "no PMC profile of this config (tools/pmc_profile.py)"
+        out["note"] = note or "no launch timed"
         return out
-    # per-launch work scaled to this run's candidates per launch (windows may differ)
-    scale = cand / max(pmc["candidates_per_launch"], 1.0)
     t = avg_ms * 1e-3
-    res = {
-        "valu": (pmc["valu_busy_cycles_per_launch"] * scale / t, pmc["valu_peak_cycles_per_s"],
-                 "SIMD-cycles/s"),
-        "lds": (pmc["lds_busy_cycles_per_launch"] * scale / t, pmc["lds_peak_cycles_per_s"],
-                "CU-LDS-cycles/s"),
-        "hbm": (pmc["hbm_bytes_per_launch"] * scale / t / 1e9, HBM_PEAK_GBS, "GB/s"),
-    }
-    bound = max(res, key=lambda k: res[k][0] / res[k][1])
+    res = {"valu": (pmc["valu_busy_cycles_per_launch"] / t, SIMDS * SHADER_HZ, "SIMD-cycles/s"),
+           "lds": (pmc["lds_busy_cycles_per_launch"] / t, CUS * SHADER_HZ, "CU-LDS-cycles/s"),
+           "hbm": (pmc["hbm_bytes_per_launch"] / t / 1e9, HBM_PEAK_GBS, "GB/s")}
+    bound = max(res, key=lambda x: res[x][0] / res[x][1])
     a, p, u = res[bound]
     out.update({"bound": bound, "achieved": a, "peak": p, "unit": u, "frac": a / p,
-                "traffic": pmc["hbm_bytes_per_launch"] * scale,
-                "utilisation": {k: v[0] / v[1] for k, v in res.items()},
-                "pmc_source": os.path.relpath(args.pmc_json, ROOT),
-                "pmc_kernel": pmc.get("kernel"),
-                "prefilter_survivor_frac": pmc.get("prefilter_survivor_frac")})
+                "traffic": pmc["hbm_bytes_per_launch"],
+                "utilisation": {x: v[0] / v[1] for x, v in res.items()},
+                "pmc_source": pmc.get("source"), "pmc_lib_sha256": pmc.get("lib_sha256"),
+                "pmc_profiled_launch_ms": pmc.get("profiled_duration_ms")})
     return out
 
 
-# Roofline of the sequential frontier walk. Each task reads the capacities the previous commit
-# wrote, so the chain runs on ONE wave, and what bounds it is that wave's instruction issue: a
-# wave issues at most one instruction per 4 cycles (MI355X_MICROARCH.md, 'vector-instruction
-# ISSUE cost, one wave': v_add_f32 4 cycles, s_nop 4). `achieved` = the walk's instructions per
-# second on its longest chain (instructions per task from the rocprofv3 PMC profile of this
-# binary: SQ_INSTS_VALU + SALU + LDS + SMEM + VMEM over the chain tasks), `peak` = 2.4 GHz / 4.
-# The latency floor (one dependent LDS round trip per task, ~50 cycles) is kept beside it.
-ISSUE_CYCLES = 4
-LDS_DEP_CYCLES = 50
-SHADER_HZ = 2.4e9
-WALK_PMC = os.path.join(ROOT, "profiles", "r02p", "pmc_r02p_zwalk.json")
-
-
-def walk_roofline(ks, ep, steps, T):
-    """The dominant kernel when no candidate lists are scored (cost_aware best-fit epochs whose
-    chains the zero-cost frontier walk proves, pvt_zwalk.hip): the chain walks run side by side,
-    so the round waits for the longest."""
+def walk_roofline(mode, H, T, ks, ep, steps, kernel="zwalk_kernel"):
+    """A sequential walk (the frontier walk, the list commit walk, the opportunistic walk): each
+    task reads the capacities the previous commit wrote, so the chain is one wave's dependent
+    instruction stream, bounded by that wave's issue: at most one instruction per 4 cycles
+    (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost, one wave'). achieved = instructions
+    per task (PMC, every wave of the kernel, over the round's tasks) x tasks per second on the
+    critical path (the longest frontier chain, or every task for the one-workgroup walks);
+    peak = 2.4 GHz / 4. The latency floor (one dependent LDS round trip per task) is beside it."""
     c = ks["commit"]
     ms = c["ms"] / max(steps, 1)
-    longest = ep.get("longest_chain_tasks", 0)
-    sequential = longest <= 0 and ep.get("frontier_chains", 0) > 0
-    if sequential:
-        # first-fit rounds (keyed / ordered frontier walks): the walks run one after another,
-        # every task of the round on one of them
-        longest = T
-    out = {"kernel": "zwalk (zero-cost frontier walk: one wave per epoch chain, window in LDS)",
-           "bound": "issue", "unit": "instructions/s (one wave)", "traffic": None,
-           "walk_ms_per_step": ms, "longest_chain_tasks": longest,
+    longest = ep.get("longest_chain_tasks", 0) if kernel == "zwalk_kernel" else 0
+    if longest <= 0:
+        longest = T                      # every task of the round on one walk after another
+    out = {"kernel": kernel, "bound": "issue", "unit": "instructions/s (one wave)", "traffic": None,
+           "walk_ms_per_step": ms, "critical_path_tasks": longest,
            "peak_basis": "one instruction per %d cycles of one wave at %.1f GHz"
-                         % (ISSUE_CYCLES, SHADER_HZ / 1e9)}
-    if ms <= 0 or longest <= 0:
-        out.update({"achieved": None, "peak": None, "frac": None})
+                         % (ISSUE_CYCLES, SHADER_HZ / 1e9),
+           "achieved": None, "peak": None, "frac": None}
+    if ms <= 0:
         return out
     tasks_per_s = longest / (ms * 1e-3)
-    ipt = None
-    if sequential:
-        out["kernel"] = "zwalk (keyed / ordered frontier walks in sequence, window in LDS)"
-        out["note"] = "the walk's PMC profile is of the default line's launch; no instruction count here"
-    try:
-        if sequential:
-            raise KeyError("no PMC profile of this mode")
-        with open(WALK_PMC) as f:
-            pmc = json.load(f)
-        cnt = pmc["counters_per_launch"]
-        ipt = sum(cnt.get(k, 0.0) for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
-                                            "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD",
-                                            "SQ_INSTS_VMEM_WR")) / max(T, 1)
-        out["pmc_source"] = os.path.relpath(WALK_PMC, ROOT)
-        out["instructions_per_task"] = ipt
-        out["issue_active_frac_pmc"] = cnt["SQ_ACTIVE_INST_ANY"] / cnt["SQ_WAVE_CYCLES"]
-        out["wait_frac_pmc"] = cnt["SQ_WAIT_ANY"] / cnt["SQ_WAVE_CYCLES"]
-        traffic = 2.0 * cnt.get("FETCH_SIZE", 0.0) * 1024 + cnt.get("WRITE_SIZE", 0.0) * 1024
-        out["traffic"] = traffic if traffic > 0 else None
-    except (OSError, ValueError, KeyError):
-        out.setdefault("note", "no PMC profile of the walk (tools/pmc_profile.py --kernel zwalk_kernel)")
     out["cycles_per_task"] = SHADER_HZ / tasks_per_s
     out["latency_floor"] = {"peak_tasks_per_s": SHADER_HZ / LDS_DEP_CYCLES,
                             "achieved_tasks_per_s": tasks_per_s,
                             "frac": tasks_per_s / (SHADER_HZ / LDS_DEP_CYCLES)}
-    if ipt is None:
-        out.update({"achieved": None, "peak": None, "frac": None})
+    pmc, note = pmc_entry(mode, H, T, kernel)
+    if pmc is None:
+        out["note"] = note
         return out
+    cnt = pmc["counters_per_launch"]
+    launches = float(pmc.get("launches_per_round", 1.0))
+    ipt = sum(cnt.get(k, 0.0) for k in INSTS) * launches / max(T, 1)
+    out.update({"instructions_per_task": ipt, "pmc_source": pmc.get("source"),
+                "pmc_lib_sha256": pmc.get("lib_sha256"),
+                "issue_active_frac_pmc": cnt["SQ_ACTIVE_INST_ANY"] / cnt["SQ_WAVE_CYCLES"],
+                "wait_frac_pmc": cnt["SQ_WAIT_ANY"] / cnt["SQ_WAVE_CYCLES"],
+                "waves_per_launch": cnt.get("SQ_WAVES")})
+    traffic = 2.0 * cnt.get("FETCH_SIZE", 0.0) * 1024 + cnt.get("WRITE_SIZE", 0.0) * 1024
+    out["traffic"] = traffic if traffic > 0 else None
     achieved = ipt * tasks_per_s
     peak = SHADER_HZ / ISSUE_CYCLES
     out.update({"achieved": achieved, "peak": peak, "frac": achieved / peak})
+    if out["waves_per_launch"] and out["waves_per_launch"] > 1 and kernel != "zwalk_kernel":
+        out["note"] = ("instructions of every wave of the walk's workgroup (walker and scouts, "
+                       "spin waits included) per task of the critical path")
+    return out
+
+
+def dominant_roofline(mode, H, T, ks, ep, steps, batch=False):
+    """The roofline of the kernel class that takes the most device time in the timed steps."""
+    if batch:
+        return score_roofline(mode, H, T, ks, "resident_kernel")
+    if ks["commit"]["ms"] >= ks["score"]["ms"]:
+        kernel = ("opp_commit_kernel" if mode == MODES["opp"] else
+                  "zwalk_kernel" if ks["score"]["launches"] == 0 and mode != MODES["vbp_bf"]
+                  else "commit_kernel")
+        return walk_roofline(mode, H, T, ks, ep, steps, kernel)
+    kernel = ("band_score_kernel" if mode == MODES["vbp_bf"] and H >= 65536 else
+              "opp_count_kernel" if mode == MODES["opp"] else "score_kernel")
+    return score_roofline(mode, H, T, ks, kernel)
+
+
+def extra_roofline(tag, mode, H, T, ks, steps):
+    if not tag.startswith("c5_"):
+        return None
+    return dominant_roofline(mode, H, T, ks, {}, steps)
+
+
+# ---------------------------------------------------------------------------- configs 1 and 2
+# BASELINE configs 1 and 2 run the reference's own simulator (alibaba/sim.py), which needs the
+# reference sources and SimPy: the box has neither. tests/golden/sim_*.json.gz hold every
+# schedule() round of those simulations (tests/golden/make_golden_sim.py, recorded in the build
+# container): the snapshot, the ready queue with its predecessor placements, and the reference's
+# placements. They are replayed here through the drop-in policy classes (pivot_place.policies)
+# exactly as the reference's round loop calls them (scheduler/__init__.py:100-103): per round
+# _update_resource_info() and schedule(ready tasks), timed end to end -- grouping, anchors (a3 on
+# the GPU), marshalling, H2D, kernels, D2H and applying the results. Beside it the same replay
+# with the C restatement behind the engine contract, on 1 thread and on all the job's cores.
+REPLAYS = ("sim_c1_cost_aware", "sim_c2a1000_cost_aware", "sim_c2a1000_opportunistic",
+           "sim_c2a1000_vbp_ff")
+
+
+_REPLAY_CACHE = {}
+
+
+class _OracleEngine:
+    """The C restatement behind PlacementEngine's place() / anchor() contract (CPU baseline)."""
+
+    def __init__(self, threads):
+        self.threads = threads
+
+    def place(self, r):
+        from oracle import oracle
+        return oracle.place(r, threads=self.threads)
+
+    def anchor(self, off, lst, zone, inst_host=None):
+        from oracle import oracle
+        mode, az, rc = oracle.anchor(off, lst, zone, len(zone), inst_host)
+        if rc != 0:
+            raise RuntimeError("oracle anchor rc %d" % rc)
+        return mode, az
+
+
+def _replay(name, engine):
+    """One pass over a recorded simulation's rounds: (seconds spent in the rounds, candidates,
+    rounds, placements equal to the reference's in every round)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import fakes
+    import golden_io
+    from pivot_place import policies
+    classes = {"cost_aware": policies.CostAwareGlobalScheduler,
+               "opportunistic": policies.OpportunisticGlobalScheduler,
+               "vbp_ff": policies.FirstFitGlobalScheduler, "vbp_bf": policies.BestFitGlobalScheduler}
+    tr, cases = _REPLAY_CACHE.get(name) or _REPLAY_CACHE.setdefault(name, golden_io.sim_rounds(name))
+    cluster, _ = fakes.build(cases[0])               # one cluster, its hosts set per round
+    cls = classes[tr["policy"]]
+    sched = cls(None, cluster, seed=tr["seed"], **tr["kwargs"])
+    sched.engine = engine
+    hidx = {h.id: i for i, h in enumerate(cluster.hosts)}
+    cand, ok, secs = 0.0, True, 0.0
+    for case in cases:
+        fakes.refresh(cluster, case)                 # (the simulation's state this round)
+        tasks = fakes.build_tasks(case, cluster)
+        t0 = time.perf_counter()
+        sched._update_resource_info()
+        sched.schedule(list(tasks))
+        secs += time.perf_counter() - t0
+        cand += float(len(tasks)) * len(cluster.hosts)
+        got = [-1 if t.placement is None else hidx[t.placement] for t in tasks]
+        ok = ok and got == case["runs"][0]["placement"]
+    return secs, cand, len(cases), ok, tr
+
+
+def replay_workloads(eng):
+    out = {}
+    threads = oracle_threads()
+    for name in REPLAYS:
+        try:
+            _replay(name, eng)                               # warm-up (tables, scratch)
+            secs, cand, nr, ok, tr = _replay(name, eng)
+            c1, _, _, ok1, _ = _replay(name, _OracleEngine(0))
+            ca, _, _, oka, _ = _replay(name, _OracleEngine(threads))
+        except Exception as e:                               # (a missing fixture is reported)
+            out["replay_" + name] = {"error": "%s: %s" % (type(e).__name__, e)}
+            continue
+        cfg = "c1" if name.startswith("sim_c1") else "c2"
+        out["%s_replay_%s" % (cfg, name[4:].split("_", 1)[1])] = {
+            "workload": "%s: every schedule() round of the recorded reference simulation (%d "
+                        "hosts, %d apps, %s %s), through the drop-in policy class"
+                        % (name, tr["n_hosts"], tr["n_apps"], tr["policy"], tr["kwargs"]),
+            "rounds": nr, "candidates": cand, "value": cand / secs, "unit": "candidates/s",
+            "seconds": secs, "ms_per_round": secs * 1e3 / nr, "parity": bool(ok),
+            "cpu_1thread": {"seconds": c1, "value": cand / c1, "parity": bool(ok1)},
+            "cpu_all": {"seconds": ca, "value": cand / ca, "cores": threads, "parity": bool(oka)},
+            "reference_sim_wall_s": tr["e2e"].get("reference_wall_s"),
+            "note": "times the whole drop-in round (Python grouping / marshalling included); "
+                    "reference_sim_wall_s is the reference's whole simulation in the build "
+                    "container (SimPy events included), for scale only"}
+        log("[rank 0] replay %s: %d rounds, %.3f s (%.2f ms/round) vs CPU 1T %.3f s, %d T %.3f s, "
+            "parity %s" % (name, nr, secs, secs * 1e3 / nr, c1, threads, ca, ok))
     return out
 
 
@@ -328,15 +495,22 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local
+    gloo = world > 1 and args.dist_backend == "gloo"
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # (gloo: ranks may share the card -- a rehearsal of the multi-rank path on one GPU)
+        dev = local % max(torch.cuda.device_count(), 1) if gloo else local
+        torch.cuda.set_device(dev)
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
     mode = MODES[args.mode]
     H, T = args.hosts, args.tasks
     log("[rank %d] building synthetic round: %s, H=%d T=%d" % (rank, args.mode, H, T))
     hosts_sharded = args.shard == "hosts" and not args.batch
     B = max(args.batch, 0)
-    eng = PlacementEngine(local, window=args.window)
+    eng = PlacementEngine(dev, window=args.window)
     eng.set_pipeline(bool(args.pipeline))
     eng.set_epochs(bool(args.epochs))
     if B:
@@ -380,14 +554,13 @@ def main():
     elapsed = time.perf_counter() - t0
     eng.set_profiling(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=eng.device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else eng.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed * 1e3 / args.steps
     cand_per_step = float(T) * H * (1 if hosts_sharded else world) * (B if B else 1)
     value = cand_per_step / (elapsed / args.steps)
-    ks = {name: eng.kstats(k) for name, k in (("score", _abi.PVT_K_SCORE), ("merge", _abi.PVT_K_MERGE),
-                                               ("commit", _abi.PVT_K_COMMIT), ("other", _abi.PVT_K_OTHER))}
+    ks = kstats_all(eng)
 
     if rank == 0:
         out = {
@@ -412,13 +585,12 @@ def main():
                                else "one independent scenario per GPU"),
                 "scenarios_per_gpu": B if B else 1,
                 "hosts": H, "tasks_per_round": T, "zones": 20, "policy": args.mode,
-                "parallelism": ("host-sharded x%d (per-window candidate all-gather)" % world
-                                if hosts_sharded else
+                "parallelism": ("host-sharded x%d (per-step all-gather of window candidates / "
+                                "candidate lists)" % world if hosts_sharded else
                                 "scenario-sharded x%d (no data-path collective)" % world),
+                "dist_backend": (("gloo" if gloo else "nccl") if world > 1 else None),
             },
-            "roofline": (walk_roofline(ks, ep, args.steps, T)
-                         if not B and ks["score"]["launches"] == 0 and ks["commit"]["launches"] > 0
-                         else roofline(args, ks, mode, B)),
+            "roofline": dominant_roofline(mode, H, T, ks, ep, args.steps, batch=bool(B)),
             "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items()},
             "walk_us_per_task": (ks["commit"]["ms"] * 1e3 / args.steps / max(T * (B or 1), 1)
                                  if not B else None),
@@ -444,6 +616,8 @@ def main():
                    and T == DEFAULT_T and args.window == 0 and args.pipeline == 1 and args.epochs == 1)
         if args.extra == 1 or (args.extra < 0 and default):
             out["extra"] = extra_workloads(eng, args, args.mode)
+        if args.replay == 1 or (args.replay < 0 and default and args.extra != 0):
+            out.setdefault("extra", {}).update(replay_workloads(eng))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

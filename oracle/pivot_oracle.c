@@ -289,6 +289,11 @@ int oracle_place(const pvt_round* r) {
  */
 #include <omp.h>
 
+/* Scans of fewer hosts stay on one thread: a parallel region per task costs more than the
+ * scan (and stalls under CPU contention), so the all-cores baseline of small rounds is the
+ * 1-thread one. */
+#define MT_MIN_HOSTS 4096
+
 typedef struct { double s; uint32_t tb; int32_t h; } cand;
 static inline int cand_less(cand a, cand b) {   /* (s, tb, h) lexicographic; h < 0 = none */
   if (a.h < 0) return 0;
@@ -304,7 +309,7 @@ static int32_t mt_pick(const pvt_round* r, int mode, const double d[4], int g, i
                        const keyed* hs, int threads) {
   const int H = r->n_hosts, Z = r->n_zones;
   cand best = {0.0, 0u, -1};
-#pragma omp parallel num_threads(threads)
+#pragma omp parallel num_threads(threads) if (H >= MT_MIN_HOSTS)
   {
     cand mine = {0.0, 0u, -1};
 #pragma omp for schedule(static) nowait
@@ -349,7 +354,7 @@ int oracle_place_mt(const pvt_round* r, int threads) {
       r->placement[t] = -1;
       double d[4]; task_vec(r->dem, T, t, d);
       int64_t nq = 0;
-#pragma omp parallel for num_threads(threads) reduction(+ : nq) schedule(static)
+#pragma omp parallel for num_threads(threads) reduction(+ : nq) schedule(static) if (H >= MT_MIN_HOSTS)
       for (int h = 0; h < H; h++) { double a[4]; host_vec(r->avail, H, h, a); nq += fits_ge(a, d); }
       if (nq == 0) continue;
       uint32_t k = oracle_randint(r->mt_state, (uint64_t)nq);
@@ -377,7 +382,7 @@ int oracle_place_mt(const pvt_round* r, int threads) {
     const int n = group_tasks(r, ca ? g : 0, r->sort_tasks, ks, r->order + off);
     const keyed* order = NULL;
     if (r->mode == PVT_CA_FF && r->sort_hosts) {   /* frozen keys of the group (:104-119) */
-#pragma omp parallel for num_threads(threads) schedule(static)
+#pragma omp parallel for num_threads(threads) schedule(static) if (H >= MT_MIN_HOSTS)
       for (int h = 0; h < H; h++) {
         double a[4]; host_vec(r->avail, H, h, a);
         int z = r->zone[h];

@@ -129,6 +129,8 @@ struct RoundState {
   bool band = false;
   int band_S = BAND_SEGS;
   int touch_lb = -1;
+  bool lw_last = false;           // the walk in flight is the one-wave list walk (pvt_lwalk.hip)
+  int lw_lb = 0, lw_prev = 0;     //   its list buffer and inherited hosts (for the fallback)
 };
 
 struct pvt_ctx {
@@ -161,6 +163,7 @@ struct pvt_ctx {
   int of_tasks = ORDERED_FRONTIER_TASKS;  // ordered frontier tasks per attempt (PVT_OF_TASKS)
   Buf fwin;                               // host-sharded frontier walks: merged windows
   int band_min = BAND_MIN_HOSTS;          // vbp best-fit band lists from this many hosts (0: off)
+  int lwalk = 1;                          // vbp best-fit windows: the one-wave list walk
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
@@ -309,7 +312,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_lists, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_walk, hipEventDisableTiming) != hipSuccess ||
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
-      resident_init_attrs() != hipSuccess ||
+      resident_init_attrs() != hipSuccess || lwalk_init_attrs() != hipSuccess ||
       hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess ||
       hipHostMalloc((void**)&ctx->ep_host, sizeof(int32_t) * EP_WORDS) != hipSuccess) {
     delete ctx;
@@ -318,6 +321,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   ctx->stream = ctx->own;
   if (const char* e = getenv("PVT_OF_TASKS")) ctx->of_tasks = std::max(32, atoi(e));   // tuning
   if (const char* e = getenv("PVT_BAND")) ctx->band_min = std::max(0, atoi(e));       // A/B
+  if (const char* e = getenv("PVT_LWALK")) ctx->lwalk = atoi(e) != 0;                  // A/B
   *out = ctx;
   return PVT_OK;
 }
@@ -1080,9 +1084,13 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
                  r->placement, P<int32_t>(ctx->owned[1 - lb]), n_prev, P<int32_t>(ctx->owned[lb]),
                  status, r->mode == PVT_CA_BF ? r->rt_bw : nullptr, P<int32_t>(ctx->grp_ord) + t0,
                  ctx->stamps};
+  R.lw_last = r->mode == PVT_VBP_BF && ctx->lwalk && n_prev <= 2048;
+  R.lw_lb = lb;
+  R.lw_prev = n_prev;
   {
     Scope sc(ctx, PVT_K_COMMIT, 0, 0);
-    launch_commit(ca_, st);
+    if (R.lw_last) launch_lwalk(ca_, st);
+    else launch_commit(ca_, st);
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
@@ -1104,6 +1112,29 @@ static void adapt_window(pvt_ctx* ctx, int adv, int nt) {
 static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
   HIPCHK(hipStreamSynchronize(ctx->stream));
   *adv = ctx->next_host[0];
+  if (*adv == 0 && ctx->rs.lw_last) {
+    // the one-wave list walk could not start this window (its first task's list ends before
+    // its bound, or too many inherited hosts): the list walk walks it, on the same lists
+    RoundState& R = ctx->rs;
+    const pvt_round* r = &R.r;
+    Lists L;
+    lists_from(ctx, L, R.lw_lb);
+    CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
+                   P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
+                   r->placement, P<int32_t>(ctx->owned[1 - R.lw_lb]), R.lw_prev,
+                   P<int32_t>(ctx->owned[R.lw_lb]), P<int32_t>(ctx->next), nullptr,
+                   P<int32_t>(ctx->grp_ord) + t0, ctx->stamps};
+    R.lw_last = false;
+    {
+      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+      launch_commit(ca_, ctx->stream);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t) * 2,
+                          hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    *adv = ctx->next_host[0];
+  }
   if (*adv == -1) return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out at task %d", t0);
   if (*adv < 0 || *adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", *adv, nt);
   if (*adv == 0 && !inherited) {

@@ -190,6 +190,10 @@ void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream
 // validate's verdict to the accepted prefix and its apply, on the device; res[5] reported
 void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st);
 void launch_commit_chains(const CommitArgs& a, int nchains, hipStream_t st);
+// vbp best-fit windows: the one-wave list walk with list cursors (pvt_lwalk.hip); CommitArgs as
+// for launch_commit (no epochs, no stamps). status[0] < nt: refill there (0: the list walk decides)
+void launch_lwalk(const CommitArgs& a, hipStream_t st);
+hipError_t lwalk_init_attrs();
 
 // Zero-cost frontier walk of epoch chains (pvt_zwalk.hip): workgroup b walks chain b like the
 // list walk's chain mode (same tables, WinRec log, status[2b] = tasks walked) while it can prove

@@ -56,6 +56,9 @@ struct ZwalkLDS {
   double red[ZW_WAVES][12];                // block reductions: max d, min d, min avail
   double smin[ZW_SB][4];                   // suffix minima of the demands, per 64-task batch
   double lg[64][4];                        // the batch's log: capacities after each commit
+#ifdef PVT_ZW_LDSDEM
+  double bd[64][4];                        // the batch's demands (hot-loop broadcast reads)
+#endif
   int32_t lgid[64];                        //   and the host
   uint32_t amask[ZMAX];                    // anchor -> its zero-cost zones
   uint32_t umask;
@@ -388,11 +391,56 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       nw1 = task_at(i0 + 128 + lane);
     }
     const int kn = min(64, nt - i0);
+#ifdef PVT_ZW_LDSDEM
+    S.bd[lane][0] = td[0]; S.bd[lane][1] = td[1]; S.bd[lane][2] = td[2]; S.bd[lane][3] = td[3];
+    wave_lds_sync();
+#endif
+    // (uniform) every task of the batch has the anchor the zero-cost masks are for: the tasks
+    // need no anchor test (a chain's groups are long, so nearly every batch)
+    const bool uni = __ballot(lane < kn && tanc != cur) == 0;
     int k = 0;
-    for (; k < kn; k++) {
+    while (k < kn) {
+      // The hot loop: the batch's tasks while each finds a fitting zero-cost host in the
+      // register chunk and every fitting host of it is zero-cost for the anchor. Per task: the
+      // demand from registers, four subtractions, three minima, one ballot, the winner's mask
+      // bit (lowest set bit, scalar), four selects on it and the winner lane's log entry -- no
+      // compare of a lane id and no branch back to the vector unit. Any other task leaves it for
+      // the general step below, then the hot loop goes on.
+      if (uni) {
+#ifdef PVT_ZW_LDSDEM
+        // (variant: the demands as broadcast LDS reads, task k + 1's issued while task k runs)
+        double e0 = S.bd[k][0], e1 = S.bd[k][1], e2 = S.bd[k][2], e3 = S.bd[k][3];
+#endif
+        for (; k < kn; k++) {
+#ifdef PVT_ZW_LDSDEM
+          const double d0 = e0, d1 = e1, d2 = e2, d3 = e3;
+          const int kk = min(k + 1, 63);
+          e0 = S.bd[kk][0]; e1 = S.bd[kk][1]; e2 = S.bd[kk][2]; e3 = S.bd[kk][3];
+#else
+          const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
+          const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
+#endif
+          const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
+          const uint64_t fm0 = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
+          const uint64_t m0 = fm0 & rzm;
+          if (m0 == 0 || (fm0 & ~rzm) != 0) break;
+          const bool win = __builtin_amdgcn_inverse_ballot_w64(m0 & (0ull - m0));
+          ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
+          if (win) {
+            S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
+            S.lgid[k] = rid;
+          }
+          dirty = true;
+#ifdef PVT_STAMPS
+          n_chunks++;
+#endif
+          done++;
+        }
+        if (k >= kn) break;
+      }
       const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
       const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
-      const int a = readlane_i(tanc, k);
+      const int a = uni ? cur : readlane_i(tanc, k);
       if (a != cur) {
         // certificates 2 / 3 for this anchor's zone row
         bool ok = true;
@@ -442,8 +490,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // Each path commits in place (no shared commit block: merging the paths made the compiler
       // copy the chunk registers on every task). commit: resc[h] -= t_demand
       // (cost_aware.py:95) on the lowest such lane, which logs.
-      if (__builtin_expect((fm0 & rzm) != 0 && (fm0 & ~rzm) == 0, 1)) {
-        const bool win = lane == __builtin_ctzll(fm0 & rzm);
+      // (the winner's lane from its mask bit in scalar registers: no lane-id compare, and the
+      // commit is four selects on that mask)
+      const uint64_t m0 = fm0 & rzm;
+      if (__builtin_expect(m0 != 0 && (fm0 & ~rzm) == 0, 1)) {
+        const bool win = __builtin_amdgcn_inverse_ballot_w64(m0 & (0ull - m0));
         ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
         if (win) {
           S.lg[k][0] = n0; S.lg[k][1] = n1; S.lg[k][2] = n2; S.lg[k][3] = n3;
@@ -457,8 +508,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           // host, from registers (a dead chunk p0 is moved on by the general path below)
           const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
           const uint64_t fb = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
-          if ((fb & bzm) != 0 && (fb & ~bzm) == 0) {
-            const bool win = lane == __builtin_ctzll(fb & bzm);
+          const uint64_t mb = fb & bzm;
+          if (mb != 0 && (fb & ~bzm) == 0) {
+            const bool win = __builtin_amdgcn_inverse_ballot_w64(mb & (0ull - mb));
             rb0 = win ? q0 : rb0; rb1 = win ? q1 : rb1; rb2 = win ? q2 : rb2; rb3 = win ? q3 : rb3;
             if (win) {
               S.lg[k][0] = q0; S.lg[k][1] = q1; S.lg[k][2] = q2; S.lg[k][3] = q3;
@@ -533,6 +585,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       }
       if (!found) { failed = true; break; }  // certificate 1 fails: the list walk decides
       done++;
+      k++;
     }
     if (lane < k) {                          // the batch's log (WinRec; sup: epoch_final_kernel)
       WinRec& e = A.wlog[tw];

@@ -100,6 +100,32 @@ class Application:
         return self.preds.get(cid, [])
 
 
+def refresh(cluster, case):
+    """Set the hosts of a cluster built for an earlier round of the same simulation to this
+    round's state (availability, running tasks)."""
+    for h, a, nr in zip(cluster.hosts, case["avail"], case["n_running"]):
+        h.resource = Resource(a)
+        if len(h.tasks) != nr:
+            h.tasks = [("running", i) for i in range(nr)]
+
+
+def build_tasks(case, cluster):
+    """The ready tasks of a fixture's round (containers, predecessor placements) on ``cluster``."""
+    hosts = cluster.hosts
+    apps, conts = {}, []
+    for k, c in enumerate(case["containers"]):
+        app = apps.setdefault(c["app"], Application("app%d" % c["app"]))
+        cont = Container("c%d" % k, app)
+        pred = Container("p%d" % k, app)
+        for hi in c["pred_hosts"]:
+            t = Task(pred, (1, 1.0, 0, 0))
+            t.placement = hosts[hi].id
+            pred.tasks.append(t)
+        app.preds[cont.id] = [pred] if c["pred_hosts"] else []
+        conts.append(cont)
+    return [Task(conts[ci], tuple(d)) for d, ci in zip(case["tasks"]["dem"], case["tasks"]["container"])]
+
+
 def build(case):
     """(cluster, tasks) reproducing a fixture's state."""
     cost, bw, names = golden_io.zones()
@@ -118,16 +144,4 @@ def build(case):
                 routes[(s.id, h.id)] = Route(float(bw[zs][zh]), case["rt_in"][k][j])
                 routes[(h.id, s.id)] = Route(float(bw[zh][zs]), case["rt_out"][k][j])
     cluster = Cluster(hosts, storage, Meta(zones, cost, bw), routes)
-    apps, conts = {}, []
-    for k, c in enumerate(case["containers"]):
-        app = apps.setdefault(c["app"], Application("app%d" % c["app"]))
-        cont = Container("c%d" % k, app)
-        pred = Container("p%d" % k, app)
-        for hi in c["pred_hosts"]:
-            t = Task(pred, (1, 1.0, 0, 0))
-            t.placement = hosts[hi].id
-            pred.tasks.append(t)
-        app.preds[cont.id] = [pred] if c["pred_hosts"] else []
-        conts.append(cont)
-    tasks = [Task(conts[ci], tuple(d)) for d, ci in zip(case["tasks"]["dem"], case["tasks"]["container"])]
-    return cluster, tasks
+    return cluster, build_tasks(case, cluster)

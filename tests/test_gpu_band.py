@@ -86,3 +86,31 @@ def test_band_host_sharded(world):
     ref = oracle.place(r, threads=8)
     for o in place_lockstep(engines, r):
         _same(o, ref)
+
+
+@pytest.mark.parametrize("H,T,seed", [(70_000, 2600, 9), (20_000, 4000, 10)])
+def test_one_wave_list_walk_equals_list_walk(H, T, seed):
+    """vbp best-fit windows walked by the one-wave list walk with list cursors (pvt_lwalk.hip,
+    the default) and by the scout list walk (PVT_LWALK=0) give the oracle's round; the second
+    case has hosts that fit one task each (every commit kills its host, lists run deep)."""
+    import os
+    from pivot_place.engine import PlacementEngine
+    r = synthetic.make_round(_abi.PVT_VBP_BF, H, T, seed=seed)
+    if seed == 10:
+        r.avail[0, :] = 1.5
+    ref = oracle.place(r, threads=8)
+    old = os.environ.get("PVT_LWALK")
+    try:
+        os.environ["PVT_LWALK"] = "0"
+        scout = PlacementEngine(0)
+    finally:
+        if old is None:
+            os.environ.pop("PVT_LWALK", None)
+        else:
+            os.environ["PVT_LWALK"] = old
+    one = PlacementEngine(0)
+    for e in (scout, one):
+        e.set_resident(0)
+        e.set_band(1)
+    _same(one.place(r), ref)
+    _same(scout.place(r), ref)

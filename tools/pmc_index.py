@@ -1,21 +1,50 @@
 #!/usr/bin/env python3
-"""Collect tools/pmc_profile.py outputs into the index bench.py reads (profiles/<name>.json):
-    python tools/pmc_index.py profiles/r02_score_pmc.json ca_bf:1000000:10000:1024:gpurun_out/pmc_r02_ca_bf.json ...
-Each argument after the output is mode:hosts:tasks:window_tasks:pmc_json; candidates per launch
-of the profiled probe = window_tasks x hosts."""
+"""Collect tools/pmc_profile.py outputs into the index bench.py reads (profiles/pmc_index.json):
+
+    python tools/pmc_index.py profiles/pmc_index.json ca_bf:1000000:10000:gpurun_out/pmc_r03_zwalk.json ...
+
+Each argument after the output is mode:hosts:tasks:pmc_json. The entry key is
+"<mode>_<hosts>_<tasks>:<kernel>" (kernel = the short __global__ name the profile matched); the
+entry keeps the profile (with the sha256 of the library it was collected on: bench.py ignores an
+entry of another build) plus launches_per_round = dispatches / the probe's --reps."""
 import json
 import os
 import sys
 
-out_path = sys.argv[1]
-idx = {"configs": {}}
-if os.path.exists(out_path):
-    idx = json.load(open(out_path))
-for spec in sys.argv[2:]:
-    mode, hosts, tasks, wt, path = spec.split(":", 4)
-    p = json.load(open(path))
-    p["candidates_per_launch"] = float(wt) * float(hosts)
-    p["source"] = path
-    idx["configs"]["%s_%s_%s" % (mode, hosts, tasks)] = p
-json.dump(idx, open(out_path, "w"), indent=1)
-print("wrote", out_path, sorted(idx["configs"]))
+KERNELS = ("zwalk_kernel", "opp_commit_kernel", "opp_count_kernel", "band_score_kernel",
+           "score_kernel", "commit_kernel", "resident_kernel", "merge_kernel")
+
+
+def short(name):
+    base = name.split("(")[0].split("<")[0].split("::")[-1]
+    for k in KERNELS:
+        if base == k:
+            return k
+    return base
+
+
+def main():
+    out_path = sys.argv[1]
+    idx = {"entries": {}}
+    if os.path.exists(out_path):
+        with open(out_path) as f:
+            idx = json.load(f)
+        idx.setdefault("entries", {})
+    for spec in sys.argv[2:]:
+        mode, hosts, tasks, path = spec.split(":", 3)
+        with open(path) as f:
+            p = json.load(f)
+        probe = p.get("probe", [])
+        reps = int(probe[probe.index("--reps") + 1]) if "--reps" in probe else 1
+        disp = p["counters_per_launch"].get("dispatches_sq", reps)
+        p["launches_per_round"] = disp / float(max(reps, 1))
+        p["source"] = os.path.relpath(path)
+        key = "%s_%s_%s:%s" % (mode, hosts, tasks, short(p["kernel"]))
+        idx["entries"][key] = p
+        print(key, "launches/round %.1f" % p["launches_per_round"], p.get("lib_sha256", "?")[:12])
+    with open(out_path, "w") as f:
+        json.dump(idx, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
