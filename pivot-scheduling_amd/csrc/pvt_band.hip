@@ -96,8 +96,10 @@ __device__ __forceinline__ int band_lower_bound(const uint64_t* key, int n, uint
     const int p = lo + lane * step;
     const bool ge = p < hi && key[p] >= k;
     const uint64_t m = __ballot(ge);
-    if (m & 1ull) return lo;                  // (never after the first step: lo's key < k)
-    const int L = m ? __builtin_ctzll(m) : WAVE;
+    if (m & 1ull) return lo;
+    // the first probe at or past k (none: one past the last probe inside [lo, hi)); the answer
+    // lies after the probe before it and at or before it
+    const int L = m ? __builtin_ctzll(m) : (hi - lo - 1) / step + 1;
     const int nlo = lo + (L - 1) * step + 1;
     hi = min(hi, lo + L * step);
     lo = nlo;

@@ -655,6 +655,9 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   const size_t tl_bytes = pipe ? sizeof(OppTouched) : 0;
   const size_t slot = (bm_bytes + sc_bytes + tl_bytes + 255) / 256 * 256;
   ENSURE(ctx->opp, slot * nbuf + sizeof(uint32_t) * 640);
+  ENSURE(ctx->anc_scr, 16);
+  int32_t* fault = P<int32_t>(ctx->anc_scr);
+  HIPCHK(hipMemsetAsync(fault, 0, sizeof(int32_t), st));
   char* base = reinterpret_cast<char*>(ctx->opp.p);
   auto bm_of = [&](int b) { return reinterpret_cast<uint64_t*>(base + slot * b); };
   auto sc_of = [&](int b) { return reinterpret_cast<int32_t*>(base + slot * b + bm_bytes); };
@@ -685,7 +688,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
     }
     OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm_of(k % nbuf),
                      sc_of(k % nbuf), H, nt, nq, nsq, W, r->placement + t0, mt, ctx->stamps,
-                     in, next ? tl_of(k % nbuf) : nullptr, next ? 0 : 1};
+                     in, next ? tl_of(k % nbuf) : nullptr, next ? 0 : 1, fault};
     {
       Scope s(ctx, PVT_K_COMMIT, 0, 0);
       launch_opp_commit(oa, st);
@@ -694,7 +697,11 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(r->mt_state, mt, sizeof(uint32_t) * 625, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(ctx->next_host + 3, fault, sizeof(int32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  if (ctx->next_host[3])
+    return fail(ctx, PVT_EHIP, "opportunistic walk: inconsistent feasible counts (a range's first "
+                "task, window-local %d, failed its verification)", ctx->next_host[3] - 1);
   return PVT_OK;
 }
 
@@ -1746,6 +1753,8 @@ static int opp_shard_begin(pvt_ctx* ctx, const pvt_round* r, int lo, int hi, int
     uint32_t* mt = reinterpret_cast<uint32_t*>(P<char>(ctx->opp) + opp_table_bytes(R));
     HIPCHK(hipMemcpyAsync(mt, r->mt_state, sizeof(uint32_t) * 625, hipMemcpyHostToDevice, st));
   }
+  ENSURE(ctx->anc_scr, 16);
+  HIPCHK(hipMemsetAsync(ctx->anc_scr.p, 0, sizeof(int32_t), st));   // the walks' fault word
   R.active = true;
   return PVT_OK;
 }
@@ -1758,8 +1767,11 @@ static int opp_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out, in
       uint32_t* mt = reinterpret_cast<uint32_t*>(P<char>(ctx->opp) + opp_table_bytes(R));
       HIPCHK(hipMemcpyAsync(R.r.mt_state, mt, sizeof(uint32_t) * 625, hipMemcpyDeviceToHost, st));
     }
+    HIPCHK(hipMemcpyAsync(ctx->next_host + 3, ctx->anc_scr.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     R.active = false;
+    if (ctx->next_host[3])
+      return fail(ctx, PVT_EHIP, "opportunistic walk: inconsistent feasible counts");
     return PVT_OK;
   }
   const int nt = std::min(R.opp_W, R.T - R.t0);
@@ -1799,7 +1811,8 @@ static int opp_shard_commit(pvt_ctx* ctx, const void* packages) {
     launch_opp_unpack(ua, st);
   }
   OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm, sc, R.H, nt, R.opp_nq,
-                   R.opp_nsq, R.opp_W, r->placement + t0, mt, ctx->stamps, nullptr, nullptr, 1};
+                   R.opp_nsq, R.opp_W, r->placement + t0, mt, ctx->stamps, nullptr, nullptr, 1,
+                   P<int32_t>(ctx->anc_scr)};
   {
     Scope s(ctx, PVT_K_COMMIT, 0, 0);
     launch_opp_commit(oa, st);

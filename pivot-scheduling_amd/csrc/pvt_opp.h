@@ -67,6 +67,8 @@ struct OppCommitArgs {
                           // launch_opp_apply): touched for this walk
   OppTouched* out;        // this walk's own hosts for the next walk (NULL: none)
   int writeback;          // write this walk's own hosts to avail at the end
+  int32_t* fault;         // set to 1 + task (window-local) when a range's first task fails its
+                          // verification: inconsistent counts / bitmaps (the host reports EHIP)
 };
 
 void launch_opp_count(const OppCountArgs& a, hipStream_t st);

@@ -671,8 +671,12 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
         rb0 = z0; rb1 = z1; rb2 = z2; rb3 = z3;
       }
       // A range whose first task fails cannot happen when the counts are consistent (its state
-      // is exact); leave that task unplaced rather than loop.
-      if (stop == s) stop = s + 1;
+      // is exact). If it does (inconsistent counts or bitmaps), report it -- the host returns
+      // PVT_EHIP -- and leave that task unplaced rather than loop.
+      if (stop == s) {
+        if (lane == 0 && A.fault) atomicCAS(A.fault, 0, s + 1);
+        stop = s + 1;
+      }
       // the range's commits: placements, then the touched table (first commit of a host
       // creates or keeps its entry with the capacity before it; its last commit sets ta)
       const int done = stop - s;
