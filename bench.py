@@ -369,8 +369,8 @@ def dominant_roofline(mode, H, T, ks, ep, steps, batch=False):
         return score_roofline(mode, H, T, ks, "resident_kernel")
     if ks["commit"]["ms"] >= ks["score"]["ms"]:
         kernel = ("opp_commit_kernel" if mode == MODES["opp"] else
-                  "zwalk_kernel" if ks["score"]["launches"] == 0 and mode != MODES["vbp_bf"]
-                  else "commit_kernel")
+                  "lwalk_kernel" if mode == MODES["vbp_bf"] else
+                  "zwalk_kernel" if ks["score"]["launches"] == 0 else "commit_kernel")
         return walk_roofline(mode, H, T, ks, ep, steps, kernel)
     kernel = ("band_score_kernel" if mode == MODES["vbp_bf"] and H >= 65536 else
               "opp_count_kernel" if mode == MODES["opp"] else "score_kernel")

@@ -90,35 +90,7 @@ def parse(path, kernel):
     return vals, names, dur
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--tag", default="r02")
-    ap.add_argument("--kernel", default="score_kernel")
-    ap.add_argument("--passes", default="sq,sq2,fetch,write")
-    ap.add_argument("--secs", type=int, default=90)
-    ap.add_argument("--candidates-per-launch", type=float, default=0.0)
-    ap.add_argument("probe", nargs=argparse.REMAINDER)
-    a = ap.parse_args()
-    probe = [x for x in a.probe if x != "--"]
-    probe[0] = os.path.join(ROOT, probe[0]) if not os.path.isabs(probe[0]) else probe[0]
-    listing = known_counters()
-    avg, kname, durs = {}, None, []
-    for name in a.passes.split(","):
-        counters = PASSES[name]
-        if listing is not None:
-            counters = [c for c in counters if c in listing]
-        if not counters:
-            continue
-        vals, names, dur = parse(run_pass(name, counters, a.tag, probe, a.secs), a.kernel)
-        if not vals:
-            raise RuntimeError("pass %s: no dispatch of %s" % (name, a.kernel))
-        kname = kname or sorted(set(names.values()))[0]
-        for c in counters:
-            xs = [v[c] for v in vals.values() if c in v]
-            if xs:
-                avg[c] = sum(xs) / len(xs)
-        durs += list(dur.values())
-        avg.setdefault("dispatches_" + name, len(vals))
+def summarise(kname, avg, durs, probe, cand):
     dur_s = (sum(durs) / len(durs)) * 1e-9 if durs else None
     out = {"kernel": kname, "probe": probe, "lib_sha256": lib_sha256(), "counters_per_launch": avg,
            "profiled_duration_ms": dur_s * 1e3 if dur_s else None}
@@ -139,17 +111,59 @@ def main():
                 out[k.replace("_cycles_per_launch", "_frac_profiled")] = out[k] / dur_s / peak
         if "hbm_bytes_per_launch" in out:
             out["hbm_frac_profiled"] = out["hbm_bytes_per_launch"] / dur_s / 8.0e12
-    if a.candidates_per_launch:
-        out["candidates_per_launch"] = a.candidates_per_launch
+    if cand:
+        out["candidates_per_launch"] = cand
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", default="r02")
+    ap.add_argument("--kernel", default="score_kernel",
+                    help="kernel name substring; several, comma-separated, are taken from the same "
+                         "passes (one pmc_<tag>_<kernel>.json each)")
+    ap.add_argument("--passes", default="sq,sq2,fetch,write")
+    ap.add_argument("--secs", type=int, default=90)
+    ap.add_argument("--candidates-per-launch", type=float, default=0.0)
+    ap.add_argument("probe", nargs=argparse.REMAINDER)
+    a = ap.parse_args()
+    probe = [x for x in a.probe if x != "--"]
+    probe[0] = os.path.join(ROOT, probe[0]) if not os.path.isabs(probe[0]) else probe[0]
+    kernels = a.kernel.split(",")
+    listing = known_counters()
+    avg = {k: {} for k in kernels}
+    kname = {k: None for k in kernels}
+    durs = {k: [] for k in kernels}
+    for name in a.passes.split(","):
+        counters = PASSES[name]
+        if listing is not None:
+            counters = [c for c in counters if c in listing]
+        if not counters:
+            continue
+        path = run_pass(name, counters, a.tag, probe, a.secs)
+        for kern in kernels:
+            vals, names, dur = parse(path, kern)
+            if not vals:
+                raise RuntimeError("pass %s: no dispatch of %s" % (name, kern))
+            kname[kern] = kname[kern] or sorted(set(names.values()))[0]
+            for c in counters:
+                xs = [v[c] for v in vals.values() if c in v]
+                if xs:
+                    avg[kern][c] = sum(xs) / len(xs)
+            durs[kern] += list(dur.values())
+            avg[kern].setdefault("dispatches_" + name, len(vals))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "pmc_%s.json" % a.tag), "w") as f:
-        json.dump(out, f, indent=1)
-    with open(os.path.join(ROOT, "gpurun_out", "pmc_%s.csv" % a.tag), "w") as f:
-        w = csv.writer(f)
-        w.writerow(["kernel", "counter", "value_per_launch"])
-        for c, v in sorted(avg.items()):
-            w.writerow([kname, c, v])
-    print(json.dumps(out), flush=True)
+    for kern in kernels:
+        out = summarise(kname[kern], avg[kern], durs[kern], probe, a.candidates_per_launch)
+        stem = "pmc_%s" % a.tag if len(kernels) == 1 else "pmc_%s_%s" % (a.tag, kern)
+        with open(os.path.join(ROOT, "gpurun_out", stem + ".json"), "w") as f:
+            json.dump(out, f, indent=1)
+        with open(os.path.join(ROOT, "gpurun_out", stem + ".csv"), "w") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "counter", "value_per_launch"])
+            for c, v in sorted(avg[kern].items()):
+                w.writerow([kname[kern], c, v])
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
