@@ -56,9 +56,6 @@ struct ZwalkLDS {
   double red[ZW_WAVES][12];                // block reductions: max d, min d, min avail
   double smin[ZW_SB][4];                   // suffix minima of the demands, per 64-task batch
   double lg[64][4];                        // the batch's log: capacities after each commit
-#ifdef PVT_ZW_LDSDEM
-  double bd[64][4];                        // the batch's demands (hot-loop broadcast reads)
-#endif
   int32_t lgid[64];                        //   and the host
   uint32_t amask[ZMAX];                    // anchor -> its zero-cost zones
   uint32_t umask;
@@ -174,7 +171,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   __shared__ ZwalkLDS S;
 #ifdef PVT_STAMPS
   const uint64_t t_start = zstamp();
-  uint64_t n_chunks = 0, n_switch = 0;
+  uint64_t n_chunks = 0, n_switch = 0, n_bulk = 0, n_runs = 0;
 #endif
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int base = KEYED ? 0 : A.coff[b];
@@ -365,6 +362,55 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     if (bdirty && pb >= 0 && p < nwin) { S.wa[0][p] = rb0; S.wa[1][p] = rb1; S.wa[2][p] = rb2; S.wa[3][p] = rb3; }
     bdirty = false;
   };
+  // A run of R tasks with the same demand d from batch task k, placed on one 64-host chunk
+  // (registers c0..c3, host cid; m0 = its lanes that fit d, all of them zero-cost). Sequentially
+  // each task takes the lowest fitting lane; a lane that no longer fits d never fits it again
+  // (capacities only fall), and the lanes that do not fit now never will, so the run fills the
+  // fitting lanes in index order, each until it cannot take another copy of d. Pass 1: every
+  // lane subtracts d again and again in parallel (cnt = copies taken; the active set only
+  // shrinks), until the lanes up to the lowest active one u have taken R copies (fb = copies of
+  // the finished lanes below u, u itself has taken t) or no lane takes another. Lane l then takes
+  // asg = clamp(R - (copies of the lanes before it), 0, cnt) tasks; pass 2 replays exactly those
+  // subtractions on the chunk's registers, logging the capacities after each commit at the
+  // task's batch position. Returns the tasks placed (>= 1; fewer than R when the chunk runs
+  // out). Bit-exact: the same sequential subtractions as one task after the other.
+  auto run_bulk = [&](double& c0, double& c1, double& c2, double& c3, int32_t cid, double d0,
+                      double d1, double d2, double d3, uint64_t m0, int R, int k) -> int {
+    const bool on1 = __builtin_amdgcn_inverse_ballot_w64(m0);
+    double x0 = c0 - d0, x1 = c1 - d1, x2 = c2 - d2, x3 = c3 - d3;
+    x0 = on1 ? x0 : c0; x1 = on1 ? x1 : c1; x2 = on1 ? x2 : c2; x3 = on1 ? x3 : c3;
+    int cnt = on1 ? 1 : 0;
+    uint64_t act = m0;
+    int t = 1, u = __builtin_ctzll(m0), fb = 0;
+    while (fb + t < R) {
+      const double q0 = x0 - d0, q1 = x1 - d1, q2 = x2 - d2, q3 = x3 - d3;
+      const uint64_t an = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & act;
+      if (an == 0) break;
+      const bool on = __builtin_amdgcn_inverse_ballot_w64(an);
+      x0 = on ? q0 : x0; x1 = on ? q1 : x1; x2 = on ? q2 : x2; x3 = on ? q3 : x3;
+      cnt += on ? 1 : 0;
+      act = an;
+      t++;
+      const int un = __builtin_ctzll(an);
+      if (un != u) {                           // (u only rises: every lane below un is done)
+        u = un;
+        fb = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cnt), u - 1);
+      }
+    }
+    const int incl = wave_incl_scan_dpp(cnt);
+    const int pre = incl - cnt;
+    const int asg = max(0, min(cnt, R - pre));
+    const int covered = min(R, __builtin_amdgcn_readlane(incl, 63));
+    for (int m = 0; m < t; m++) {
+      if (m < asg) {
+        c0 -= d0; c1 -= d1; c2 -= d2; c3 -= d3;
+        const int pos = k + pre + m;
+        S.lg[pos][0] = c0; S.lg[pos][1] = c1; S.lg[pos][2] = c2; S.lg[pos][3] = c3;
+        S.lgid[pos] = cid;
+      }
+    }
+    return covered;
+  };
   load_chunk(0);
   load_b(1);
   // task records, software-pipelined across 64-task batches: while batch b is walked, batch
@@ -391,13 +437,75 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       nw1 = task_at(i0 + 128 + lane);
     }
     const int kn = min(64, nt - i0);
-#ifdef PVT_ZW_LDSDEM
-    S.bd[lane][0] = td[0]; S.bd[lane][1] = td[1]; S.bd[lane][2] = td[2]; S.bd[lane][3] = td[3];
-    wave_lds_sync();
-#endif
     // (uniform) every task of the batch has the anchor the zero-cost masks are for: the tasks
     // need no anchor test (a chain's groups are long, so nearly every batch)
-    const bool uni = __ballot(lane < kn && tanc != cur) == 0;
+    bool uni = __ballot(lane < kn && tanc != cur) == 0;
+    // runs: bit i is set iff task i of the batch has task i - 1's demand vector, bit for bit (the
+    // trace has few distinct demand rows, and sorted order puts equal ones next to each other)
+    uint64_t E;
+    {
+      bool same = lane > 0 && lane < kn;
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        same &= __double_as_longlong(__shfl_up(td[r], 1)) == __double_as_longlong(td[r]);
+      E = __ballot(same);
+    }
+    auto run_len = [&](int k) { return k < 63 ? min(kn - k, 1 + __builtin_ctzll(~(E >> (k + 1)))) : 1; };
+    // The run step, for a task k of a uniform batch that the register chunk p0 cannot take: its
+    // run (R tasks with its demand, R >= 1) is placed by run_bulk on the first chunk that can
+    // take a copy of it -- chunk p0 (moved on past chunks no task ahead can use), chunk pb, then
+    // the LDS chunks in index order -- with the per-task path's exactness conditions: every
+    // chunk before it fits no copy (for the chunks before p0: no task ahead), and no fitting
+    // host of a chunk it looks at is outside the anchor's zero-cost zones (else 0: the per-task
+    // path decides, with exact scores). Returns the tasks placed (0: none).
+    auto run_step = [&](int k) -> int {
+      const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
+      const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
+      const int R = run_len(k);
+      for (;;) {
+        const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
+        const uint64_t fm = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
+        if (fm & ~rzm) return 0;
+        if (fm) {
+          dirty = true;
+          return run_bulk(ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, fm, R, k);
+        }
+        if (__ballot(((rvalid >> lane) & 1ull) && fits<STRICT>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
+          break;                               // chunk p0 can still take a task ahead
+        if (p0 + 1 >= nch) return 0;
+        store_b();                             // dead: move the register chunks on
+        store_chunk(p0);
+        ++p0;
+        rzm = S.zm[p0];
+        load_chunk(p0);
+        load_b(p0 + 1);
+      }
+      if (pb >= 0) {
+        const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
+        const uint64_t fb = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
+        if (fb & ~bzm) return 0;
+        if (fb) {
+          bdirty = true;
+          return run_bulk(rb0, rb1, rb2, rb3, bid, d0, d1, d2, d3, fb, R, k);
+        }
+      }
+      for (int c = (pb >= 0 ? pb : p0) + 1; c < nch; c++) {
+        const int p = c * 64 + lane;
+        const int q = min(p, nwin - 1);
+        double x0 = S.wa[0][q], x1 = S.wa[1][q], x2 = S.wa[2][q], x3 = S.wa[3][q];
+        const int32_t xid = S.wid[q];
+        const uint64_t xzm = S.zm[c];
+        const uint64_t fm = __ballot(p < nwin && fit_res<STRICT>(fmin(fmin(x0 - d0, x1 - d1),
+                                                                      fmin(x2 - d2, x3 - d3))));
+        if (fm & ~xzm) return 0;
+        if (fm) {
+          const int got = run_bulk(x0, x1, x2, x3, xid, d0, d1, d2, d3, fm, R, k);
+          if (p < nwin) { S.wa[0][p] = x0; S.wa[1][p] = x1; S.wa[2][p] = x2; S.wa[3][p] = x3; }
+          return got;
+        }
+      }
+      return 0;
+    };
     int k = 0;
     while (k < kn) {
       // The hot loop: the batch's tasks while each finds a fitting zero-cost host in the
@@ -407,23 +515,27 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // compare of a lane id and no branch back to the vector unit. Any other task leaves it for
       // the general step below, then the hot loop goes on.
       if (uni) {
-#ifdef PVT_ZW_LDSDEM
-        // (variant: the demands as broadcast LDS reads, task k + 1's issued while task k runs)
-        double e0 = S.bd[k][0], e1 = S.bd[k][1], e2 = S.bd[k][2], e3 = S.bd[k][3];
-#endif
-        for (; k < kn; k++) {
-#ifdef PVT_ZW_LDSDEM
-          const double d0 = e0, d1 = e1, d2 = e2, d3 = e3;
-          const int kk = min(k + 1, 63);
-          e0 = S.bd[kk][0]; e1 = S.bd[kk][1]; e2 = S.bd[kk][2]; e3 = S.bd[kk][3];
-#else
+        for (; k < kn;) {
           const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
           const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
-#endif
           const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
           const uint64_t fm0 = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
           const uint64_t m0 = fm0 & rzm;
           if (m0 == 0 || (fm0 & ~rzm) != 0) break;
+          // a run of tasks with this demand: placed in one pass over the chunk (run_bulk)
+          const int R = run_len(k);
+          if (R >= 2) {
+            const int c = run_bulk(ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, m0, R, k);
+            k += c;
+            done += c;
+            dirty = true;
+#ifdef PVT_STAMPS
+            n_chunks += c;
+            n_bulk += c;
+            n_runs++;
+#endif
+            continue;
+          }
           const bool win = __builtin_amdgcn_inverse_ballot_w64(m0 & (0ull - m0));
           ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
           if (win) {
@@ -435,8 +547,20 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           n_chunks++;
 #endif
           done++;
+          k++;
         }
         if (k >= kn) break;
+        const int got = run_step(k);
+        if (got > 0) {
+          k += got;
+          done += got;
+#ifdef PVT_STAMPS
+          n_chunks += got;
+          n_bulk += got;
+          n_runs++;
+#endif
+          continue;
+        }
       }
       const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
       const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
@@ -459,6 +583,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           if (c == pb) bzm = m;
         }
         cur = a;
+        uni = __ballot(lane >= k && lane < kn && tanc != cur) == 0;   // the rest of the batch
         __builtin_amdgcn_s_waitcnt(0xc07f);
 #ifdef PVT_STAMPS
         n_switch++;
@@ -617,6 +742,8 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     atomicAdd((unsigned long long*)&A.stamps[2], (unsigned long long)n_chunks);
     atomicAdd((unsigned long long*)&A.stamps[3], (unsigned long long)done);
     atomicAdd((unsigned long long*)&A.stamps[4], (unsigned long long)n_switch);
+    atomicAdd((unsigned long long*)&A.stamps[5], (unsigned long long)n_bulk);
+    atomicAdd((unsigned long long*)&A.stamps[6], (unsigned long long)n_runs);
   }
 #endif
 }

@@ -14,20 +14,23 @@ from pivot_place.engine import DeviceRound, PlacementEngine  # noqa: E402
 H = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 10_000
 lib = sys.argv[3] if len(sys.argv) > 3 else "libpivot_place_stamps.so"
+MODES = {"ca_ff": _abi.PVT_CA_FF, "ca_bf": _abi.PVT_CA_BF, "vbp_ff": _abi.PVT_VBP_FF}
+mode = sys.argv[4] if len(sys.argv) > 4 else "ca_bf"
 eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "diag", lib))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
 buf = (ctypes.c_uint64 * 8)()
 assert f(eng.ctx, buf, 8) == 0
-r = synthetic.make_round(_abi.PVT_CA_BF, H, T)
+r = synthetic.make_round(MODES[mode], H, T)
 dr = DeviceRound(r, eng.device)
 eng.run(dr)
 torch.cuda.synchronize()
 assert f(eng.ctx, buf, 8) == 0
 st = eng.epoch_stats()
 nch = max(st["frontier_chains"] + st["list_chains"], 1)
-print("H=%d T=%d stats=%s" % (H, T, st))
+print("%s H=%d T=%d stats=%s" % (mode, H, T, st))
 print("  prologue   %10.0f cycles per chain" % (buf[0] / nch))
 print("  walk       %10.0f cycles per chain, %.0f per task" % (buf[1] / nch, buf[1] / max(buf[3], 1)))
 print("  chunks     %10.2f per task" % (buf[2] / max(buf[3], 1)))
 print("  tasks      %10d, anchor switches %d" % (buf[3], buf[4]))
+print("  bulk runs  %10d runs placed %d tasks (%.1f per run)" % (buf[6], buf[5], buf[5] / max(buf[6], 1)))
