@@ -436,12 +436,13 @@ extern "C" int pvt_debug_commit_stamps(pvt_ctx* ctx, uint64_t* out, int n) {
   if (!ctx || !out || n < 8) return PVT_EINVAL;
 #ifdef PVT_STAMPS
   if (!ctx->stamps) {
-    if (hipMalloc((void**)&ctx->stamps, 64) != hipSuccess) return PVT_ENOMEM;
-    (void)hipMemset(ctx->stamps, 0, 64);
-    std::memset(out, 0, sizeof(uint64_t) * 8);
+    if (hipMalloc((void**)&ctx->stamps, 128) != hipSuccess) return PVT_ENOMEM;
+    (void)hipMemset(ctx->stamps, 0, 128);
+    std::memset(out, 0, sizeof(uint64_t) * std::min(n, 16));
     return PVT_OK;
   }
-  if (hipMemcpy(out, ctx->stamps, 64, hipMemcpyDeviceToHost) != hipSuccess) return PVT_EHIP;
+  if (hipMemcpy(out, ctx->stamps, sizeof(uint64_t) * std::min(n, 16), hipMemcpyDeviceToHost) != hipSuccess)
+    return PVT_EHIP;
   return PVT_OK;
 #else
   return PVT_EUNSUPPORTED;

@@ -60,6 +60,13 @@ __device__ __forceinline__ uint32_t readlane_u(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int32_t)v, l);
 }
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// A value the wave holds uniformly, as the compiler's uniformity analysis cannot always prove
+// (values loaded from LDS at uniform addresses, loop-carried scalars): keeps it in SGPRs.
+__device__ __forceinline__ uint64_t rfl_u64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
 
 // Orders one wave's LDS accesses across its lanes: the LDS unit executes a wave's DS operations
 // in issue order, so only the compiler's reordering needs fencing.
@@ -112,6 +119,16 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
   m = r1 < m ? r1 : m;
   m = r2 < m ? r2 : m;
   return r3 < m ? r3 : m;
+}
+// Wave-wide maximum of an int, uniform: DPP row prefix maxima, then the four row maxima.
+__device__ __forceinline__ int wave_max_i32(int v) {
+  v = max(v, (int)dpp_u32<DPP_ROW_SHR1>((uint32_t)v, (uint32_t)v));
+  v = max(v, (int)dpp_u32<DPP_ROW_SHR2>((uint32_t)v, (uint32_t)v));
+  v = max(v, (int)dpp_u32<DPP_ROW_SHR4>((uint32_t)v, (uint32_t)v));
+  v = max(v, (int)dpp_u32<DPP_ROW_SHR8>((uint32_t)v, (uint32_t)v));
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+  const int r2 = __builtin_amdgcn_readlane(v, 47), r3 = __builtin_amdgcn_readlane(v, 63);
+  return max(max(r0, r1), max(r2, r3));
 }
 // Wave-wide inclusive prefix sum (lane order) with DPP row scans and row offsets.
 __device__ __forceinline__ int wave_incl_scan_dpp(int v) {

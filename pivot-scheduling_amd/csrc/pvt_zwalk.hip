@@ -45,6 +45,7 @@ constexpr int ZW_SCAN = 16;                // hosts per thread per window-build 
 constexpr int ZW_MINB = ZW_MIN_PARTS;      // blocks of the host-minimum pass
 constexpr double ZW_BIG = 0x1p500;
 
+constexpr int ZW_UNROLL = 4;               // run_bulk pass 1: copies per stop check
 constexpr int ZW_SB = 64;                  // suffix-minimum batches (the last one holds the rest)
 struct ZwalkLDS {
   double wa[4][ZW_M];                      // window capacities (live)
@@ -95,6 +96,13 @@ __global__ __launch_bounds__(256) void host_min_kernel(const double* avail, int 
 
 // Fit from the minimum residual min(a - d): a >= d (best-fit) or a > d (first-fit, strict) in
 // every dimension; exact in sign for finite values (certificate 3).
+template <int N> struct IntC { static constexpr int value = N; };
+
+// A branch condition the wave holds uniformly: through readfirstlane, so that the compiler's
+// divergence analysis (which loses track across this walk's nested loops) keeps the branch scalar
+// instead of building exec-mask loops around it.
+#define UNI(c) (__builtin_amdgcn_readfirstlane((int)(c)) != 0)
+
 template <bool STRICT>
 __device__ __forceinline__ bool fit_res(double m) { return STRICT ? (m > 0.0) : (m >= 0.0); }
 
@@ -172,6 +180,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #ifdef PVT_STAMPS
   const uint64_t t_start = zstamp();
   uint64_t n_chunks = 0, n_switch = 0, n_bulk = 0, n_runs = 0;
+  uint64_t st_search = 0, st_p1 = 0, st_p2 = 0, n_probe = 0, n_iter = 0, st_batch = 0, n_single = 0;
 #endif
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int base = KEYED ? 0 : A.coff[b];
@@ -354,7 +363,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     rb0 = S.wa[0][q]; rb1 = S.wa[1][q]; rb2 = S.wa[2][q]; rb3 = S.wa[3][q];
     bid = S.wid[q];
     bvalid = __ballot(p < nwin);
-    bzm = cur >= 0 ? S.zm[c] : 0;
+    bzm = cur >= 0 ? rfl_u64(S.zm[c]) : 0;
     __builtin_amdgcn_s_waitcnt(0xc07f);
   };
   auto store_b = [&]() {
@@ -376,39 +385,80 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   // out). Bit-exact: the same sequential subtractions as one task after the other.
   auto run_bulk = [&](double& c0, double& c1, double& c2, double& c3, int32_t cid, double d0,
                       double d1, double d2, double d3, uint64_t m0, int R, int k) -> int {
+#ifdef PVT_STAMPS
+    const uint64_t tA = zstamp();
+#endif
+    // Pass 1 without per-lane masks: with d >= 0 a lane that fails a copy fails every later one
+    // (its residual only falls further), so every lane just keeps subtracting, recording the last
+    // copy that fit (= the copies it takes); lanes outside m0 start at -inf. ZW_UNROLL copies per check
+    // (a check past the stop only raises counts of lanes that get no task or no more tasks: asg
+    // clamps them). Dimensions of demand +0 keep their capacity (x - +0 == x bit for bit) and fit
+    // as they did for m0, so with d2 = d3 = +0 (the trace's disk and gpus) the loop updates and
+    // tests cpus and memory only.
+    if (!(d0 >= 0.0 && d1 >= 0.0 && d2 >= 0.0 && d3 >= 0.0)) R = 1;   // (then one task only)
     const bool on1 = __builtin_amdgcn_inverse_ballot_w64(m0);
-    double x0 = c0 - d0, x1 = c1 - d1, x2 = c2 - d2, x3 = c3 - d3;
-    x0 = on1 ? x0 : c0; x1 = on1 ? x1 : c1; x2 = on1 ? x2 : c2; x3 = on1 ? x3 : c3;
-    int cnt = on1 ? 1 : 0;
-    uint64_t act = m0;
-    int t = 1, u = __builtin_ctzll(m0), fb = 0;
-    while (fb + t < R) {
-      const double q0 = x0 - d0, q1 = x1 - d1, q2 = x2 - d2, q3 = x3 - d3;
-      const uint64_t an = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & act;
-      if (an == 0) break;
-      const bool on = __builtin_amdgcn_inverse_ballot_w64(an);
-      x0 = on ? q0 : x0; x1 = on ? q1 : x1; x2 = on ? q2 : x2; x3 = on ? q3 : x3;
-      cnt += on ? 1 : 0;
-      act = an;
-      t++;
-      const int un = __builtin_ctzll(an);
-      if (un != u) {                           // (u only rises: every lane below un is done)
-        u = un;
-        fb = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cnt), u - 1);
+    const bool two = __double_as_longlong(d2) == 0 && __double_as_longlong(d3) == 0;
+    double x0 = on1 ? c0 : -DINF, x1 = on1 ? c1 : -DINF, x2 = on1 ? c2 : -DINF, x3 = on1 ? c3 : -DINF;
+    int cnt = 0;
+    int t = 0;
+    R = __builtin_amdgcn_readfirstlane(R);
+    // (one loop per dimension count: the compiler does not unswitch it)
+    auto pass1 = [&](auto dims) {
+      constexpr int D = decltype(dims)::value;
+      int u = __builtin_ctzll(m0), fb = 0;
+      for (;;) {
+        // (wave-uniform, which the compiler cannot prove here: keeps the loop scalar)
+        t = __builtin_amdgcn_readfirstlane(t);
+        u = __builtin_amdgcn_readfirstlane(u);
+        fb = __builtin_amdgcn_readfirstlane(fb);
+        bool f = false;
+#pragma unroll
+        for (int j = 1; j <= ZW_UNROLL; j++) {
+          x0 -= d0; x1 -= d1;
+          if (D == 4) { x2 -= d2; x3 -= d3; }
+          f = fit_res<STRICT>(D == 4 ? fmin(fmin(x0, x1), fmin(x2, x3)) : fmin(x0, x1));
+          cnt = f ? t + j : cnt;
+        }
+        t += ZW_UNROLL;
+        const uint64_t an = __ballot(f);       // lanes that took copy t
+        if (UNI(an == 0)) break;
+        const int un = __builtin_ctzll(an);
+        if (un != u) {                         // (u only rises: every lane below un is done)
+          u = un;
+          fb = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cnt), u - 1);
+        }
+        if (UNI(fb + t >= R)) break;
       }
-    }
+    };
+    if (two) pass1(IntC<2>{});
+    else pass1(IntC<4>{});
     const int incl = wave_incl_scan_dpp(cnt);
     const int pre = incl - cnt;
     const int asg = max(0, min(cnt, R - pre));
     const int covered = min(R, __builtin_amdgcn_readlane(incl, 63));
-    for (int m = 0; m < t; m++) {
-      if (m < asg) {
+#ifdef PVT_STAMPS
+    const uint64_t tB = zstamp();
+    st_p1 += tB - tA;
+    n_iter += t;
+#endif
+    // Pass 2: each lane replays its own copies (a per-lane loop; measured faster than one
+    // uniform loop with selects or with masked log writes).
+    if (two) {
+      for (int m = 0, pos = k + pre; m < asg; m++, pos++) {
+        c0 -= d0; c1 -= d1;
+        S.lg[pos][0] = c0; S.lg[pos][1] = c1; S.lg[pos][2] = c2; S.lg[pos][3] = c3;
+        S.lgid[pos] = cid;
+      }
+    } else {
+      for (int m = 0, pos = k + pre; m < asg; m++, pos++) {
         c0 -= d0; c1 -= d1; c2 -= d2; c3 -= d3;
-        const int pos = k + pre + m;
         S.lg[pos][0] = c0; S.lg[pos][1] = c1; S.lg[pos][2] = c2; S.lg[pos][3] = c3;
         S.lgid[pos] = cid;
       }
     }
+#ifdef PVT_STAMPS
+    st_p2 += zstamp() - tB;
+#endif
     return covered;
   };
   load_chunk(0);
@@ -422,7 +472,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   double nd2 = A.dem[(size_t)nw * 4 + 2], nd3 = A.dem[(size_t)nw * 4 + 3];
   int nanc = A.anc[nw], ncal = A.ord[nw];
   int nw1 = task_at(64 + lane);
-  for (int i0 = 0; i0 < nt && !failed; i0 += 64) {
+  for (int i0 = 0; UNI(i0 < nt && !failed); i0 += 64) {
+#ifdef PVT_STAMPS
+    uint64_t tb0 = zstamp();
+#endif
 #pragma unroll
     for (int r = 0; r < 4; r++) mn[r] = S.smin[min(i0 >> 6, ZW_SB - 1)][r];
     const int tw = nw;
@@ -459,15 +512,22 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     // host of a chunk it looks at is outside the anchor's zero-cost zones (else 0: the per-task
     // path decides, with exact scores). Returns the tasks placed (0: none).
     auto run_step = [&](int k) -> int {
+#ifdef PVT_STAMPS
+      const uint64_t t0 = zstamp();
+#define ZW_SEARCH_DONE() (st_search += zstamp() - t0)
+#else
+#define ZW_SEARCH_DONE() ((void)0)
+#endif
       const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
       const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
       const int R = run_len(k);
       for (;;) {
         const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
         const uint64_t fm = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
-        if (fm & ~rzm) return 0;
-        if (fm) {
+        if (UNI((fm & ~rzm) != 0)) return 0;
+        if (UNI(fm != 0)) {
           dirty = true;
+          ZW_SEARCH_DONE();
           return run_bulk(ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, fm, R, k);
         }
         if (__ballot(((rvalid >> lane) & 1ull) && fits<STRICT>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
@@ -476,16 +536,17 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         store_b();                             // dead: move the register chunks on
         store_chunk(p0);
         ++p0;
-        rzm = S.zm[p0];
+        rzm = rfl_u64(S.zm[p0]);
         load_chunk(p0);
         load_b(p0 + 1);
       }
       if (pb >= 0) {
         const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
         const uint64_t fb = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
-        if (fb & ~bzm) return 0;
-        if (fb) {
+        if (UNI((fb & ~bzm) != 0)) return 0;
+        if (UNI(fb != 0)) {
           bdirty = true;
+          ZW_SEARCH_DONE();
           return run_bulk(rb0, rb1, rb2, rb3, bid, d0, d1, d2, d3, fb, R, k);
         }
       }
@@ -494,20 +555,36 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         const int q = min(p, nwin - 1);
         double x0 = S.wa[0][q], x1 = S.wa[1][q], x2 = S.wa[2][q], x3 = S.wa[3][q];
         const int32_t xid = S.wid[q];
-        const uint64_t xzm = S.zm[c];
+        const uint64_t xzm = rfl_u64(S.zm[c]);
+#ifdef PVT_STAMPS
+        n_probe++;
+#endif
         const uint64_t fm = __ballot(p < nwin && fit_res<STRICT>(fmin(fmin(x0 - d0, x1 - d1),
                                                                       fmin(x2 - d2, x3 - d3))));
-        if (fm & ~xzm) return 0;
-        if (fm) {
+        if (UNI((fm & ~xzm) != 0)) return 0;
+        if (UNI(fm != 0)) {
+          ZW_SEARCH_DONE();
           const int got = run_bulk(x0, x1, x2, x3, xid, d0, d1, d2, d3, fm, R, k);
           if (p < nwin) { S.wa[0][p] = x0; S.wa[1][p] = x1; S.wa[2][p] = x2; S.wa[3][p] = x3; }
           return got;
         }
       }
+      ZW_SEARCH_DONE();
       return 0;
     };
+#undef ZW_SEARCH_DONE
+#ifdef PVT_STAMPS
+    st_batch += zstamp() - tb0;
+#endif
     int k = 0;
-    while (k < kn) {
+    while (UNI(k < kn)) {
+      // (wave-uniform state the compiler cannot prove uniform: keeps the loops below scalar)
+      k = __builtin_amdgcn_readfirstlane(k);
+      p0 = __builtin_amdgcn_readfirstlane(p0);
+      pb = __builtin_amdgcn_readfirstlane(pb);
+      done = __builtin_amdgcn_readfirstlane(done);
+      rzm = rfl_u64(rzm);
+      bzm = rfl_u64(bzm);
       // The hot loop: the batch's tasks while each finds a fitting zero-cost host in the
       // register chunk and every fitting host of it is zero-cost for the anchor. Per task: the
       // demand from registers, four subtractions, three minima, one ballot, the winner's mask
@@ -516,15 +593,16 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // the general step below, then the hot loop goes on.
       if (uni) {
         for (; k < kn;) {
+          k = __builtin_amdgcn_readfirstlane(k);
           const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
           const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
           const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
           const uint64_t fm0 = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
           const uint64_t m0 = fm0 & rzm;
-          if (m0 == 0 || (fm0 & ~rzm) != 0) break;
+          if (UNI(m0 == 0 || (fm0 & ~rzm) != 0)) break;
           // a run of tasks with this demand: placed in one pass over the chunk (run_bulk)
           const int R = run_len(k);
-          if (R >= 2) {
+          if (UNI(R >= 2)) {
             const int c = run_bulk(ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, m0, R, k);
             k += c;
             done += c;
@@ -545,13 +623,14 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           dirty = true;
 #ifdef PVT_STAMPS
           n_chunks++;
+          n_single++;
 #endif
           done++;
           k++;
         }
-        if (k >= kn) break;
+        if (UNI(k >= kn)) break;
         const int got = run_step(k);
-        if (got > 0) {
+        if (UNI(got > 0)) {
           k += got;
           done += got;
 #ifdef PVT_STAMPS
@@ -672,7 +751,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
               break;                           // chunk p0 still useful: look further in LDS
             store_chunk(p0);                   // dead: move the register chunk on
             if (++p0 >= nch) break;
-            rzm = S.zm[p0];
+            rzm = rfl_u64(S.zm[p0]);
             load_chunk(p0);
             g0 = ra0 - d0; g1 = ra1 - d1; g2 = ra2 - d2; g3 = ra3 - d3;
             fm = __ballot(fit_res<STRICT>(fmin(fmin(g0, g1), fmin(g2, g3)))) & rvalid;
@@ -688,7 +767,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
               const int q = min(p, nwin - 1);
               const double a0 = S.wa[0][q], a1 = S.wa[1][q], a2 = S.wa[2][q], a3 = S.wa[3][q];
               const int32_t id = S.wid[q];
-              const uint64_t zm = S.zm[c];
+              const uint64_t zm = rfl_u64(S.zm[c]);
               const bool f = p < nwin && fits<STRICT>(a0, a1, a2, a3, d0, d1, d2, d3);
               const bool k0 = zero_exact(f, (zm >> lane) & 1ull, a0, a1, a2, a3, q);
               const uint64_t mc = __ballot(f && k0);
@@ -708,10 +787,13 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           load_b(p0 + 1);
         }
       }
-      if (!found) { failed = true; break; }  // certificate 1 fails: the list walk decides
+      if (UNI(!found)) { failed = true; break; }  // certificate 1 fails: the list walk decides
       done++;
       k++;
     }
+#ifdef PVT_STAMPS
+    tb0 = zstamp();
+#endif
     if (lane < k) {                          // the batch's log (WinRec; sup: epoch_final_kernel)
       WinRec& e = A.wlog[tw];
       const int32_t id = S.lgid[lane];
@@ -720,6 +802,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       e.a[0] = S.lg[lane][0]; e.a[1] = S.lg[lane][1]; e.a[2] = S.lg[lane][2]; e.a[3] = S.lg[lane][3];
       A.placement[tcal] = id;
     }
+#ifdef PVT_STAMPS
+    st_batch += zstamp() - tb0;
+#endif
   }
   if (KEYED) {   // the window's capacities to global availability: the keyed path goes on there
     store_chunk(p0);
@@ -744,6 +829,13 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     atomicAdd((unsigned long long*)&A.stamps[4], (unsigned long long)n_switch);
     atomicAdd((unsigned long long*)&A.stamps[5], (unsigned long long)n_bulk);
     atomicAdd((unsigned long long*)&A.stamps[6], (unsigned long long)n_runs);
+    atomicAdd((unsigned long long*)&A.stamps[7], (unsigned long long)st_search);
+    atomicAdd((unsigned long long*)&A.stamps[8], (unsigned long long)st_p1);
+    atomicAdd((unsigned long long*)&A.stamps[9], (unsigned long long)st_p2);
+    atomicAdd((unsigned long long*)&A.stamps[10], (unsigned long long)n_probe);
+    atomicAdd((unsigned long long*)&A.stamps[11], (unsigned long long)n_iter);
+    atomicAdd((unsigned long long*)&A.stamps[12], (unsigned long long)st_batch);
+    atomicAdd((unsigned long long*)&A.stamps[13], (unsigned long long)n_single);
   }
 #endif
 }

@@ -19,13 +19,13 @@ mode = sys.argv[4] if len(sys.argv) > 4 else "ca_bf"
 eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "diag", lib))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-buf = (ctypes.c_uint64 * 8)()
-assert f(eng.ctx, buf, 8) == 0
+buf = (ctypes.c_uint64 * 16)()
+assert f(eng.ctx, buf, 16) == 0
 r = synthetic.make_round(MODES[mode], H, T)
 dr = DeviceRound(r, eng.device)
 eng.run(dr)
 torch.cuda.synchronize()
-assert f(eng.ctx, buf, 8) == 0
+assert f(eng.ctx, buf, 16) == 0
 st = eng.epoch_stats()
 nch = max(st["frontier_chains"] + st["list_chains"], 1)
 print("%s H=%d T=%d stats=%s" % (mode, H, T, st))
@@ -34,3 +34,8 @@ print("  walk       %10.0f cycles per chain, %.0f per task" % (buf[1] / nch, buf
 print("  chunks     %10.2f per task" % (buf[2] / max(buf[3], 1)))
 print("  tasks      %10d, anchor switches %d" % (buf[3], buf[4]))
 print("  bulk runs  %10d runs placed %d tasks (%.1f per run)" % (buf[6], buf[5], buf[5] / max(buf[6], 1)))
+print("  run search %10.0f cycles per run, %.2f LDS chunk probes per run" % (buf[7] / max(buf[6], 1), buf[10] / max(buf[6], 1)))
+print("  pass 1     %10.0f cycles per bulk call, %.1f iterations" % (buf[8] / max(buf[6], 1), buf[11] / max(buf[6], 1)))
+print("  pass 2     %10.0f cycles per bulk call" % (buf[9] / max(buf[6], 1)))
+print("  batches    %10.0f cycles per task (records, run masks, log flush)" % (buf[12] / max(buf[3], 1)))
+print("  single     %10d tasks on the one-task hot path" % buf[13])
