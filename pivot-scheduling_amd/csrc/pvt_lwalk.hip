@@ -87,7 +87,24 @@ __device__ __forceinline__ void lw_key(double a0, double a1, double a2, double a
   k2 = ((uint64_t)tb << 32) | (uint32_t)id;
 }
 
+#ifdef PVT_STAMPS
+__device__ __forceinline__ uint64_t lstamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#endif
+
 __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
+#ifdef PVT_STAMPS
+  uint64_t ph[4] = {0, 0, 0, 0}, n_task = 0, n_load = 0, n_liveit = 0, n_twin = 0, n_live = 0;
+  uint64_t ts = lstamp();
+#define LW_PHASE(k) do { const uint64_t t2 = lstamp(); ph[k] += t2 - ts; ts = t2; } while (0)
+#else
+#define LW_PHASE(k) ((void)0)
+#endif
   extern __shared__ __attribute__((aligned(16))) char smem[];
   LwalkLDS& S = *reinterpret_cast<LwalkLDS*>(smem);
   const int lane = lane_id();
@@ -145,14 +162,47 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
     ce0 = e->a[0]; ce1 = e->a[1]; ce2 = e->a[2]; ce3 = e->a[3];
     ce_u = v && lw_find(S, ce_id) < 0;
     cw = w; cbase = base; ccnt = cnt;
+#ifdef PVT_STAMPS
+    n_load++;
+#endif
   };
 
-  for (int i = 0; i < A.nt && status == A.nt; i++) {
-    const int32_t rv = reinterpret_cast<const int32_t*>(A.L.t + i)[lane & 15];
-    const double d0 = rec_dw(rv, 0), d1 = rec_dw(rv, 1), d2 = rec_dw(rv, 2), d3 = rec_dw(rv, 3);
-    const int cnt = __builtin_amdgcn_readlane(rv, 8);
-    const bool comp = __builtin_amdgcn_readlane(rv, 9) != 0;
-    const int caller = __builtin_amdgcn_readlane(rv, 11);
+  // task records, 64 per batch in lanes (lane l: task b0 + l's demand, list count, completeness,
+  // caller), the next batch's loads in flight while a batch is walked
+  auto rec_load = [&](int b0, double& r0, double& r1, double& r2, double& r3, int4& ri) {
+    const TaskRec* tr = A.L.t + min(b0 + lane, max(A.nt - 1, 0));
+    const double2 x = *reinterpret_cast<const double2*>(&tr->d[0]);
+    const double2 y = *reinterpret_cast<const double2*>(&tr->d[2]);
+    ri = *reinterpret_cast<const int4*>(&tr->cnt);   // cnt, complete, anc, ord
+    r0 = x.x; r1 = x.y; r2 = y.x; r3 = y.y;
+  };
+  double nr0, nr1, nr2, nr3;
+  int4 nri;
+  rec_load(0, nr0, nr1, nr2, nr3, nri);
+  for (int b0 = 0; b0 < A.nt && status == A.nt; b0 += WAVE) {
+  const double rd0 = nr0, rd1 = nr1, rd2 = nr2, rd3 = nr3;
+  const int4 rri = nri;
+  if (b0 + WAVE < A.nt) rec_load(b0 + WAVE, nr0, nr1, nr2, nr3, nri);
+  const int kn = min(WAVE, A.nt - b0);
+  // runs: bit k set iff batch task k has task k - 1's demand (bit for bit) and list shape
+  uint64_t E;
+  {
+    bool eq = lane > 0 && lane < kn;
+    eq &= __double_as_longlong(__shfl_up(rd0, 1)) == __double_as_longlong(rd0);
+    eq &= __double_as_longlong(__shfl_up(rd1, 1)) == __double_as_longlong(rd1);
+    eq &= __double_as_longlong(__shfl_up(rd2, 1)) == __double_as_longlong(rd2);
+    eq &= __double_as_longlong(__shfl_up(rd3, 1)) == __double_as_longlong(rd3);
+    eq &= __shfl_up(rri.x, 1) == rri.x && __shfl_up(rri.y, 1) == rri.y;
+    E = __ballot(eq);
+  }
+  for (int k = 0; k < kn && status == A.nt; k++) {
+    k = __builtin_amdgcn_readfirstlane(k);
+    const int i = b0 + k;
+    const double d0 = readlane_d(rd0, k), d1 = readlane_d(rd1, k);
+    const double d2 = readlane_d(rd2, k), d3 = readlane_d(rd3, k);
+    const int cnt = __builtin_amdgcn_readlane(rri.x, k);
+    const bool comp = __builtin_amdgcn_readlane(rri.y, k) != 0;
+    const int caller = __builtin_amdgcn_readlane(rri.w, k);
     // same demand vector (bitwise): the same list, continued from the cursor
     const bool same = cw >= 0 && __double_as_longlong(d0) == __double_as_longlong(pd0) &&
                       __double_as_longlong(d1) == __double_as_longlong(pd1) &&
@@ -165,6 +215,11 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
       ccomp = comp;
       pd0 = d0; pd1 = d1; pd2 = d2; pd3 = d3;
     }
+#ifdef PVT_STAMPS
+    n_task++;
+    n_live += nlive;
+#endif
+    LW_PHASE(0);
     // the first untouched entry at or after the cursor
     int L = -1;
     for (;;) {
@@ -175,14 +230,63 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
       load_chunk(cw, cbase + WAVE, ccnt);
     }
     if (L < 0 && !ccomp) { status = i; break; }   // past the list's bound: refill from here
+    // A run of tasks with this demand, no live touched host: each task's winner is simply the
+    // next untouched entry (the list's order is the key order; no touched host can fit), as
+    // long as every winner is dead after its commit. The run takes the chunk's untouched
+    // entries from the cursor in order -- up to and including the first winner that stays alive
+    // (it becomes the live host the next task must rescore) -- in one parallel commit.
+    if (nlive == 0 && L >= 0 && k + 1 < kn && ((E >> (k + 1)) & 1ull)) {
+      const int R = min(kn - k, 1 + (int)__builtin_ctzll(~(E >> (k + 1))));
+      const uint64_t U = __ballot(ce_u && cbase + lane >= cur);
+      const bool in = (U >> lane) & 1ull;
+      const int rank = __popcll(U & ((1ull << lane) - 1ull));
+      const double n0 = ce0 - d0, n1 = ce1 - d1, n2 = ce2 - d2, n3 = ce3 - d3;
+      const uint64_t Am = __ballot(in && fits<true>(n0, n1, n2, n3, m0, m1, m2, m3));
+      int Rb = min(min(R, __popcll(U)), LW_TAB - ntab);
+      if (Am) Rb = min(Rb, __popcll(U & ((1ull << __builtin_ctzll(Am)) - 1ull)) + 1);
+      Rb = __builtin_amdgcn_readfirstlane(Rb);
+      if (Rb <= 0) { status = i; break; }         // (touched-host table full: refill)
+      const bool win = in && rank < Rb;
+      const int callr = __shfl(rri.w, min(k + rank, WAVE - 1));
+      lw_fence();
+      if (win) {
+        const int t = ntab + rank;
+        S.ta[0][t] = n0; S.ta[1][t] = n1; S.ta[2][t] = n2; S.ta[3][t] = n3;
+        S.tid[t] = ce_id; S.ttb[t] = ce_tb; S.town[t] = 1;
+        uint32_t p = lw_slot(ce_id);
+        while (atomicCAS(&S.hkey[p], LW_EMPTY, ce_id) != LW_EMPTY) p = (p + 1) & (LW_HSLOTS - 1);
+        S.hval[p] = t;
+        A.own_ids[n_own + rank] = ce_id;
+        A.placement[callr] = ce_id;
+        if (((Am >> lane) & 1ull) && rank == Rb - 1) S.live[0] = t;   // the alive last winner
+      }
+      const uint64_t Wm = __ballot(win);
+      const int last = 63 - __builtin_clzll(Wm);
+      if ((Am >> last) & 1ull) nlive = 1;
+      ce_u = ce_u && !win;
+      cur = cbase + last + 1;
+      ntab += Rb;
+      n_own += Rb;
+      k += Rb - 1;                               // (the loop adds the last one)
+      lw_fence();
+#ifdef PVT_STAMPS
+      n_task += Rb - 1;
+#endif
+      LW_PHASE(3);
+      continue;
+    }
     uint64_t b1 = ~0ull, b2 = ~0ull;
     if (L >= 0) {
       b1 = readlane_u64((uint64_t)__double_as_longlong(ce_s), L);
       b2 = ((uint64_t)readlane_u(ce_tb, L) << 32) | (uint32_t)readlane_i(ce_id, L);
     }
+    LW_PHASE(1);
     // live touched hosts, rescored exactly
     int wq = -1;
     for (int q0 = 0; q0 < nlive; q0 += WAVE) {
+#ifdef PVT_STAMPS
+      n_liveit++;
+#endif
       const int qi = q0 + lane;
       const int q = qi < nlive ? S.live[qi] : 0;
       const double a0 = S.ta[0][q], a1 = S.ta[1][q], a2 = S.ta[2][q], a3 = S.ta[3][q];
@@ -198,6 +302,10 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
         b1 = mk1; b2 = mk2;
       }
     }
+    LW_PHASE(2);
+#ifdef PVT_STAMPS
+    n_twin += wq >= 0;
+#endif
     if (L < 0 && wq < 0) {                     // no host fits: the task waits
       if (lane == 0) A.placement[caller] = -1;
       continue;
@@ -254,6 +362,8 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
     }
     if (lane == 0) A.placement[caller] = wid;
     lw_fence();                                // this commit's LDS writes before the next reads
+    LW_PHASE(3);
+  }
   }
   // the capacities of the hosts this walk committed to
   lw_fence();
@@ -264,6 +374,17 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
       for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + id] = S.ta[r][t];
     }
   if (lane == 0) { A.status[0] = status; A.status[1] = n_own; }
+#ifdef PVT_STAMPS
+  if (lane == 0 && A.stamps) {
+    for (int k = 0; k < 4; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
+    atomicAdd((unsigned long long*)&A.stamps[4], (unsigned long long)n_task);
+    atomicAdd((unsigned long long*)&A.stamps[5], (unsigned long long)n_load);
+    atomicAdd((unsigned long long*)&A.stamps[6], (unsigned long long)n_liveit);
+    atomicAdd((unsigned long long*)&A.stamps[7], (unsigned long long)n_twin);
+    atomicAdd((unsigned long long*)&A.stamps[8], (unsigned long long)n_live);
+  }
+#endif
+#undef LW_PHASE
 }
 
 constexpr size_t LWALK_LDS_BYTES = sizeof(LwalkLDS);
