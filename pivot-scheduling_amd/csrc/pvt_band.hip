@@ -116,7 +116,7 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = blockIdx.x * WPB + wave;
   const int t = g / A.S, seg = g % A.S;
-  if (t >= A.nt) return;
+  if (t >= A.nt || (A.nt_dev && t >= *A.nt_dev)) return;
   const double* dp = A.dem + (size_t)t * 4;
   const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
   double ls = DINF;
@@ -195,6 +195,37 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
   A.seg[row * KL + lane] = e;
   const int filled = __popcll(__ballot(li != 0x7fffffff));
   if (lane == 0) A.seg_feas[row] = filled == KL ? KL + 1 : filled;
+}
+
+// Window tasks -> list rows (vbp best-fit lists depend on the demand vector only, so each run of
+// equal demands -- adjacent in the sorted order -- is scored and merged once): row[w] = the run's
+// row, rdem[row] = its demand, *nrep = rows. One block; a block scan of the run heads.
+__global__ __launch_bounds__(1024) void band_reps_kernel(const double* dem, int nt, int32_t* row,
+                                                         double* rdem, int32_t* nrep) {
+  __shared__ int32_t wsum[16];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  bool head = false;
+  if (t < nt) {
+    head = t == 0;
+    for (int r = 0; r < 4 && !head; r++)
+      head = __double_as_longlong(dem[(size_t)t * 4 + r]) != __double_as_longlong(dem[(size_t)(t - 1) * 4 + r]);
+  }
+  const uint64_t m = __ballot(head);
+  int incl = __popcll(lane == 63 ? m : (m & ((2ull << lane) - 1ull)));
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  for (int w = 0; w < wave; w++) incl += wsum[w];
+  if (t < nt) {
+    row[t] = incl - 1;
+    if (head)
+      for (int r = 0; r < 4; r++) rdem[(size_t)(incl - 1) * 4 + r] = dem[(size_t)t * 4 + r];
+    if (t == nt - 1) *nrep = incl;
+  }
+}
+
+void launch_band_reps(const double* dem, int nt, int32_t* row, double* rdem, int32_t* nrep,
+                      hipStream_t st) {
+  if (nt > 0) hipLaunchKernelGGL(band_reps_kernel, dim3(1), dim3(1024), 0, st, dem, nt, row, rdem, nrep);
 }
 
 void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,

@@ -129,6 +129,8 @@ struct RoundState {
   bool band = false;
   int band_S = BAND_SEGS;
   int touch_lb = -1;
+  bool reps[2] = {false, false};  //   list buffer b holds representative rows (band_reps)
+  bool full_lists = false;        //   (one list per task: the list walk's fallback)
   bool lw_last = false;           // the walk in flight is the one-wave list walk (pvt_lwalk.hip)
   int lw_lb = 0, lw_prev = 0;     //   its list buffer and inherited hosts (for the fallback)
 };
@@ -165,6 +167,7 @@ struct pvt_ctx {
   int band_min = BAND_MIN_HOSTS;          // vbp best-fit band lists from this many hosts (0: off)
   int lwalk = 1;                          // vbp best-fit windows: the one-wave list walk
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
+  Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
@@ -339,7 +342,8 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
                  &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
-                 &ctx->btcnt, &ctx->bsorttmp};
+                 &ctx->btcnt, &ctx->bsorttmp, &ctx->brow[0], &ctx->brow[1], &ctx->brdem[0],
+                 &ctx->brdem[1], &ctx->bnrep[0], &ctx->bnrep[1]};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -1045,16 +1049,32 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
     ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)nt * S * KL);
     ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)nt * S);
     const int n = R.hi - R.lo;
+    // Representative rows (unsharded rounds, walked by the one-wave list walk, which maps each
+    // task to its row): one list per run of equal demands instead of one per task.
+    const bool reps = ctx->lwalk && !R.sharded && !R.full_lists;
+    R.reps[lb] = reps;
+    const double* dem_l = dem_w;
+    const int32_t* nt_dev = nullptr;
+    if (reps) {
+      ENSURE(ctx->brow[lb], sizeof(int32_t) * MAX_WINDOW);
+      ENSURE(ctx->brdem[lb], sizeof(double) * 4 * MAX_WINDOW);
+      ENSURE(ctx->bnrep[lb], sizeof(int32_t) * 4);
+      Scope sc(ctx, PVT_K_OTHER, 0, 0, st);
+      launch_band_reps(dem_w, nt, P<int32_t>(ctx->brow[lb]), P<double>(ctx->brdem[lb]),
+                       P<int32_t>(ctx->bnrep[lb]), st);
+      dem_l = P<double>(ctx->brdem[lb]);
+      nt_dev = P<int32_t>(ctx->bnrep[lb]);
+    }
     BandArgs ba{P<uint64_t>(ctx->bkey) + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb),
                 P<int32_t>(ctx->bidx) + n, n, R.lo, R.hi, P<uint8_t>(ctx->btouch),
-                P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt), r->avail, r->tiebreak, R.H, dem_w,
-                nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas)};
+                P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt), r->avail, r->tiebreak, R.H, dem_l,
+                nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), nt_dev};
     {
       Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
       launch_band_score(ba, st);
     }
-    MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
-                 anc_w, R.ord + t0, R.H, nt, S, KL, L};
+    MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_l,
+                 anc_w, R.ord + t0, R.H, nt, S, KL, L, nt_dev};
     Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
     launch_merge(ma, st);
   } else {
@@ -1095,6 +1115,11 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
   R.lw_last = r->mode == PVT_VBP_BF && ctx->lwalk && n_prev <= 2048;
   R.lw_lb = lb;
   R.lw_prev = n_prev;
+  if (R.band && R.reps[lb]) {
+    if (!R.lw_last) return fail(ctx, PVT_EHIP, "representative lists need the one-wave list walk");
+    ca_.rowmap = P<int32_t>(ctx->brow[lb]);
+    ca_.ordw = R.ord + t0;
+  }
   {
     Scope sc(ctx, PVT_K_COMMIT, 0, 0);
     if (R.lw_last) launch_lwalk(ca_, st);
@@ -1125,6 +1150,16 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
     // its bound, or too many inherited hosts): the list walk walks it, on the same lists
     RoundState& R = ctx->rs;
     const pvt_round* r = &R.r;
+    if (R.reps[R.lw_lb]) {
+      // representative rows: the list walk reads one list per task, so the window is scored
+      // again with one (on the current state: capacities only fall, and the inherited hosts are
+      // rescored as touched). The side stream's scoring shares the segment scratch: wait for it.
+      if (ctx->side) HIPCHK(hipStreamSynchronize(ctx->side));
+      R.full_lists = true;
+      const int rc = window_lists(ctx, t0, nt, R.lw_lb, ctx->stream);
+      R.full_lists = false;
+      if (rc) return rc;
+    }
     Lists L;
     lists_from(ctx, L, R.lw_lb);
     CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),

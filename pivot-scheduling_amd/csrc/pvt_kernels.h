@@ -97,6 +97,7 @@ struct MergeArgs {
   int H, nt, S;
   int SL;                 // entries per source list (KL, or the package depth)
   Lists L;
+  const int32_t* nt_dev;  // or NULL: only tasks [0, *nt_dev) (vbp best-fit representative lists)
 };
 
 // Host-dimension sharding: a rank's exact local lists -> its exchange package (see MergeArgs).
@@ -158,6 +159,11 @@ struct CommitArgs {
   const int32_t* cseg;
   WinRec* wlog;
   int skip_done;          // chain mode: a chain whose status already says "all walked" is skipped
+  // vbp best-fit representative lists (pvt_band.hip band_reps): window task w's list is row
+  // rowmap[w], its caller index ordw[w] (the list rows' TaskRec.ord belong to other tasks);
+  // NULL: row w, TaskRec.ord
+  const int32_t* rowmap;
+  const int32_t* ordw;
 };
 
 // Speculative epochs, cost_aware best-fit. The epoch's group segments (processing order,
@@ -322,6 +328,7 @@ struct BandArgs {
   int nt, S;              // S list segments per task
   SegEntry* seg;          // [nt][S][KL]
   int32_t* seg_feas;      // [nt][S]
+  const int32_t* nt_dev;  // or NULL: only tasks [0, *nt_dev) (representative lists)
 };
 void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,
                       hipStream_t st);
@@ -330,6 +337,10 @@ void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, c
 void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* flags, int32_t* tlist,
                          int32_t* tcount, hipStream_t st);
 void launch_band_score(const BandArgs& a, hipStream_t st);
+// Window tasks -> list rows: each run of equal demand vectors (bit for bit) shares one list row;
+// rdem = the rows' demands, *nrep = rows (nt <= MAX_WINDOW)
+void launch_band_reps(const double* dem, int nt, int32_t* row, double* rdem, int32_t* nrep,
+                      hipStream_t st);
 
 int score_tasks_per_wave(int mode, int hosts, int force = 0);
 int score_diag(uint64_t* out, int n, int reset);   // PVT_DIAG builds; else PVT_EUNSUPPORTED

@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
   __shared__ long long tot;
   __shared__ int cnt_sh;
   const int task = blockIdx.x, tid = threadIdx.x;
+  if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
   const int SL = A.SL, batch = LMAX / SL;   // source lists per sort batch
   const bool packed = A.seg_feas == nullptr;
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
   __shared__ Key out[4][MERGE_SMALL_S * KL];
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int task = blockIdx.x * 4 + wave;
-  if (task >= A.nt) return;
+  if (task >= A.nt || (A.nt_dev && task >= *A.nt_dev)) return;
   const int S = A.S, n = S * KL;
   Key* L = lk[wave];
   Key* O = out[wave];
@@ -519,6 +520,7 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   __shared__ Key bound;
   __shared__ int cnt_sh, tot_sh;
   const int task = blockIdx.x, tid = threadIdx.x;
+  if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
   const int W = A.S, SL = A.SL, n = W * SL;
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
   if (tid == 0) { bound = inv; cnt_sh = 0; tot_sh = 0; }

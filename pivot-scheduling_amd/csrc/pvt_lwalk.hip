@@ -169,12 +169,25 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
 
   // task records, 64 per batch in lanes (lane l: task b0 + l's demand, list count, completeness,
   // caller), the next batch's loads in flight while a batch is walked
+  // ri = (list count, completeness, list row, caller); representative rows (A.rowmap): the
+  // demand and caller are the task's own, the list (and its count) its row's
   auto rec_load = [&](int b0, double& r0, double& r1, double& r2, double& r3, int4& ri) {
-    const TaskRec* tr = A.L.t + min(b0 + lane, max(A.nt - 1, 0));
-    const double2 x = *reinterpret_cast<const double2*>(&tr->d[0]);
-    const double2 y = *reinterpret_cast<const double2*>(&tr->d[2]);
-    ri = *reinterpret_cast<const int4*>(&tr->cnt);   // cnt, complete, anc, ord
-    r0 = x.x; r1 = x.y; r2 = y.x; r3 = y.y;
+    const int w = min(b0 + lane, max(A.nt - 1, 0));
+    if (A.rowmap) {
+      const int row = A.rowmap[w];
+      const double2 x = *reinterpret_cast<const double2*>(A.dem + (size_t)w * 4);
+      const double2 y = *reinterpret_cast<const double2*>(A.dem + (size_t)w * 4 + 2);
+      const int2 cc = *reinterpret_cast<const int2*>(&A.L.t[row].cnt);
+      ri = make_int4(cc.x, cc.y, row, A.ordw[w]);
+      r0 = x.x; r1 = x.y; r2 = y.x; r3 = y.y;
+    } else {
+      const TaskRec* tr = A.L.t + w;
+      const double2 x = *reinterpret_cast<const double2*>(&tr->d[0]);
+      const double2 y = *reinterpret_cast<const double2*>(&tr->d[2]);
+      const int4 c4 = *reinterpret_cast<const int4*>(&tr->cnt);   // cnt, complete, anc, ord
+      ri = make_int4(c4.x, c4.y, w, c4.w);
+      r0 = x.x; r1 = x.y; r2 = y.x; r3 = y.y;
+    }
   };
   double nr0, nr1, nr2, nr3;
   int4 nri;
@@ -203,6 +216,7 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
     const int cnt = __builtin_amdgcn_readlane(rri.x, k);
     const bool comp = __builtin_amdgcn_readlane(rri.y, k) != 0;
     const int caller = __builtin_amdgcn_readlane(rri.w, k);
+    const int lrow = __builtin_amdgcn_readlane(rri.z, k);
     // same demand vector (bitwise): the same list, continued from the cursor
     const bool same = cw >= 0 && __double_as_longlong(d0) == __double_as_longlong(pd0) &&
                       __double_as_longlong(d1) == __double_as_longlong(pd1) &&
@@ -210,7 +224,7 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
                       __double_as_longlong(d3) == __double_as_longlong(pd3) && cnt == ccnt &&
                       comp == ccomp;
     if (!same) {
-      load_chunk(i, 0, cnt);
+      load_chunk(lrow, 0, cnt);
       cur = 0;
       ccomp = comp;
       pd0 = d0; pd1 = d1; pd2 = d2; pd3 = d3;
