@@ -164,6 +164,8 @@ struct OppLDS {
   uint32_t mtb[625];            // state at the range start
   int32_t pl[OPP_MAXW];         // placements of the window, written out when the walk ends
   int32_t wl[OPP_NW][WAVE];     // per wave: a task's lost hosts (pass 1)
+  int32_t lhist[OPP_NW][WAVE];  // per wave: a task's lost hosts per super-chunk (pass 3)
+  uint64_t lclr[OPP_NW][OPP_SUP][OPP_CH / WAVE];   // per wave: lost bits of the drawn super-chunk
   int32_t ctl[4];               // next range start, touched count
 };
 
@@ -399,7 +401,35 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       const uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)S.kdraw[j - s]);
       int Qs = -1;
       long long acc = 0;
-      for (int Q0 = 0; Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
+      if (fast) {
+        // one super-chunk per lane: its snapshot count minus the task's lost hosts in it, the
+        // lost hosts counted by an LDS histogram (one atomic per lost host, not a readlane loop)
+        S.lhist[wave][lane] = 0;
+        wave_lds_fence();
+        if (nlost[t] <= WAVE) {
+          if (lane < nlost[t]) atomicAdd(&S.lhist[wave][lh[t] / SUPH], 1);
+        } else {   // (rare) rescan, with the demand reloaded
+          const double dv = A.dem[(size_t)j * 4 + (lane & 3)];
+          const double f0 = readlane_d(dv, 0), f1 = readlane_d(dv, 1);
+          const double f2 = readlane_d(dv, 2), f3 = readlane_d(dv, 3);
+          for (int p0 = 0; p0 < m; p0 += WAVE) {
+            int32_t th;
+            const uint64_t b = lost_piece(S, m, p0, f0, f1, f2, f3, th);
+            if ((b >> lane) & 1ull) atomicAdd(&S.lhist[wave][th / SUPH], 1);
+          }
+        }
+        wave_lds_fence();
+        const int v = lane < A.nsq ? scr[t] - S.lhist[wave][lane] : 0;
+        const int inc = wave_incl_scan_dpp(v);
+        const int tot = __builtin_amdgcn_readlane(inc, 63);
+        if ((long long)k < tot) {
+          const uint64_t hit = __ballot(inc > (long long)k);
+          const int L = __builtin_ctzll(hit);
+          Qs = L;
+          acc = __builtin_amdgcn_readlane(inc, L) - __builtin_amdgcn_readlane(v, L);
+        }
+      }
+      for (int Q0 = 0; !fast && Q0 < A.nsq && Qs < 0; Q0 += WAVE) {
         const int Q = Q0 + lane;
         int v = 0;
         if (Q < A.nsq) v = fast ? scr[t] : A.sc[(size_t)j * A.nsq + Q];
@@ -448,31 +478,33 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       int cc = 0;
       const int Qs = qsel[t];
       if (Qs >= 0) {
-        // current bitmaps: the snapshot's minus the lost hosts of this super-chunk
-        auto clear = [&](int h) {
-          if (h / SUPH == Qs && (h / OPP_CH) % OPP_SUP == lane) {
-            const int o = h % OPP_CH;
+        // current bitmaps: the snapshot's minus the lost hosts of this super-chunk (lane = its
+        // chunk), collected by LDS atomics -- one per lost host -- instead of a readlane loop
 #pragma unroll
-            for (int u = 0; u < U; u++)
-              if (o / WAVE == u) bits[t][u] &= ~(1ull << (o % WAVE));
+        for (int u = 0; u < U; u++) S.lclr[wave][lane][u] = 0;
+        wave_lds_fence();
+        auto mark = [&](int h, bool on) {
+          if (on && h / SUPH == Qs) {
+            const int o = h % OPP_CH;
+            atomicOr((unsigned long long*)&S.lclr[wave][(h / OPP_CH) % OPP_SUP][o / WAVE],
+                     1ull << (o % WAVE));
           }
         };
         if (nlost[t] <= WAVE) {
-          for (int l = 0; l < nlost[t]; l++) clear(__builtin_amdgcn_readlane(lh[t], l));
+          mark(lh[t], lane < nlost[t]);
         } else {
           const double dv = A.dem[(size_t)j * 4 + (lane & 3)];
           const double f0 = readlane_d(dv, 0), f1 = readlane_d(dv, 1);
           const double f2 = readlane_d(dv, 2), f3 = readlane_d(dv, 3);
           for (int p0 = 0; p0 < m; p0 += WAVE) {
             int32_t th;
-            uint64_t b = lost_piece(S, m, p0, f0, f1, f2, f3, th);
-            while (b) {
-              const int l = __builtin_ctzll(b);
-              b &= b - 1;
-              clear(__builtin_amdgcn_readlane(th, l));
-            }
+            const uint64_t b = lost_piece(S, m, p0, f0, f1, f2, f3, th);
+            mark(th, (b >> lane) & 1ull);
           }
         }
+        wave_lds_fence();
+#pragma unroll
+        for (int u = 0; u < U; u++) bits[t][u] &= ~S.lclr[wave][lane][u];
         int c = 0;
 #pragma unroll
         for (int u = 0; u < U; u++) c += __popcll(bits[t][u]);
@@ -576,6 +608,9 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
         if (ccv > 0) { z0 = S.cav[lane][0][0]; z1 = S.cav[lane][1][0]; z2 = S.cav[lane][2][0]; z3 = S.cav[lane][3][0]; }
       }
       const int c0l = cd[0];
+      int cmax = ccv > 0 ? cd[0] : -1;   // the largest candidate (candidates ascend)
+#pragma unroll
+      for (int x = 1; x < OPP_C; x++) cmax = x < ccv ? cd[x] : cmax;
       double y0 = z0 - e0, y1 = z1 - e1, y2 = z2 - e2, y3 = z3 - e3;
       // dok: the speculative draw still holds for the new-lost count (same mask, k <= n - 1;
       // recomputed when a commit takes a host away). A task whose draw holds and whose c_0 still
@@ -654,7 +689,9 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
           dok = dok & (ntrue > 0) & (rint_mask((uint32_t)(ntrue - 1)) == rint_mask((uint32_t)(nsv - 1))) &
                 (kv <= (uint32_t)(ntrue - 1));
         }
-        if (__ballot(lost & (w >= c0l))) {
+        // (a lost host can only be one of the lane's candidates inside their id range: the
+        // 16-way compare runs only then, rarely -- a commit's host is random among ~1M)
+        if (__ballot(lost & (w >= c0l) & (w <= cmax))) {
 #pragma unroll
           for (int x = 0; x < OPP_C; x++) lm |= ((lost & (cd[x] == w)) ? 1u : 0u) << x;
         }

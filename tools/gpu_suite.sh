@@ -1,0 +1,32 @@
+#!/bin/bash
+# The GPU steps of this round's runs, by name:  tools/gpu_suite.sh STEP [STEP ...]
+# Each step runs under its own time limit through tools/gpu_step.sh (log: gpurun_out/STEP.log);
+# the suite stops at the first step that fails, times out or faults.
+#   gpurun -- 'tools/gpu_suite.sh tests smoke bench profbench pmc'
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+T="python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread"
+NB="--extra 0 --replay 0 --cpu-baseline-seconds 0"
+run() { tools/gpu_step.sh "$@" || exit $?; }
+for s in "$@"; do
+  case $s in
+    tests)      run tests 900 $T tests ;;
+    t_zw)       run t_zw 400 $T tests/test_gpu_headline.py tests/test_gpu_epochs.py tests/test_gpu_ordered_frontier.py tests/test_gpu_parity.py ;;
+    t_runs)     run t_runs 400 $T tests/test_gpu_runs.py ;;
+    t_vbp)      run t_vbp 400 $T tests/test_gpu_band.py tests/test_gpu_headline.py tests/test_gpu_parity.py -k "vbp or VBP or band or headline or config5" ;;
+    t_opp)      run t_opp 500 $T tests/test_gpu_opp_walk.py tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_sharded.py tests/test_gpu_batch.py -k "opp or OPP or opportunistic" ;;
+    smoke)      run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)      run bench 400 python bench.py ;;
+    b_cabf)     run b_cabf 150 python bench.py $NB --steps 20 ;;
+    b_vbpff)    run b_vbpff 150 python bench.py --mode vbp_ff $NB ;;
+    b_caff)     run b_caff 150 python bench.py --mode ca_ff $NB ;;
+    b_vbpbf)    run b_vbpbf 200 python bench.py --mode vbp_bf $NB ;;
+    b_opp)      run b_opp 200 python bench.py --mode opp $NB ;;
+    b_shard)    run b_shard 200 python bench.py --shard hosts $NB ;;
+    st_zw)      for m in ca_bf vbp_ff ca_ff; do run st_$m 120 python tools/zwalk_stamps.py 1000000 10000 libpivot_place_stamps.so $m; done ;;
+    st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
+    st_opp)     run st_opp 150 python tools/commit_stamps.py 2 1000000 10000 ;;
+    profbench)  mkdir -p gpurun_out/prof; run profbench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 $NB ;;
+    pmc)        run pmc 900 tools/pmc_all.sh "${PMC_TAG:-r03z}" ;;
+    *)          echo "unknown step $s"; exit 2 ;;
+  esac
+done

@@ -1,3 +1,4 @@
+# vbp best-fit config-5 sweep: window sizes x band list segments (PVT_BAND_SEGS), parity checked
 for w in 512 1024; do for sg in 16; do
 PVT_BAND_SEGS=$sg timeout -k 10 120 python bench.py --mode vbp_bf --window $w --extra 0 --replay 0 --cpu-baseline-seconds 0 > gpurun_out/sw_${w}_${sg}.log 2>&1 || exit 1
 tail -1 gpurun_out/sw_${w}_${sg}.log | python -c "
