@@ -200,21 +200,56 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   }
   __syncthreads();
 
-  // the chain's zones U, demand extremes and finiteness (certificates 2, 3)
+  // the chain's zones U, demand extremes and finiteness (certificates 2, 3), and the minima of
+  // the demands per 64-task batch (for the suffix minima below: a wave's 64 lanes of one pass
+  // are one batch); four rows per thread in flight at once
   uint32_t um = 0;
   double mx[4] = {-DINF, -DINF, -DINF, -DINF}, mn[4] = {DINF, DINF, DINF, DINF};
   bool bad = false;
-  for (int i = tid; i < nt; i += ZW_THREADS) {
-    const int w = KEYED ? i : cmap[i];
-    const int a = A.anc[w];
-    if (a < 0 || a >= Z) { bad = true; continue; }
-    if (!KEYED) um |= S.amask[a];
+  for (int i0 = 0; i0 < nt; i0 += 4 * ZW_THREADS) {
+    int wv[4], av[4];
+    double dv[4][4];
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const double d = A.dem[(size_t)w * 4 + r];
-      bad |= !(__builtin_fabs(d) <= ZW_BIG);
-      mx[r] = fmax(mx[r], d);
-      mn[r] = fmin(mn[r], d);
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + u * ZW_THREADS + tid;
+      wv[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int w = max(wv[u], 0);
+      av[u] = A.anc[w];
+#pragma unroll
+      for (int r = 0; r < 4; r++) dv[u][r] = A.dem[(size_t)w * 4 + r];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const bool ok = wv[u] >= 0;
+      double bm[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) bm[r] = ok ? dv[u][r] : DINF;
+      if (ok) {
+        const int a = av[u];
+        if (a < 0 || a >= Z) {
+          bad = true;
+        } else {
+          if (!KEYED) um |= S.amask[a];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            bad |= !(__builtin_fabs(dv[u][r]) <= ZW_BIG);
+            mx[r] = fmax(mx[r], dv[u][r]);
+            mn[r] = fmin(mn[r], dv[u][r]);
+          }
+        }
+      }
+      const int blk = (i0 + u * ZW_THREADS) / 64 + wave;   // (uniform: the wave's batch)
+      if (blk < ZW_SB - 1 && blk * 64 < nt) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) bm[r] = wave_min_d(bm[r]);
+        if (lane == 0) {
+#pragma unroll
+          for (int r = 0; r < 4; r++) S.smin[blk][r] = bm[r];
+        }
+      }
     }
   }
   // host minima from the partials
@@ -275,13 +310,27 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   }
   const int nwin = S.nwin;
   bool wbad = false;
-  for (int p = tid; p < nwin; p += ZW_THREADS) {
-    const int h = S.wid[p];
+  static_assert(ZW_M == 4 * ZW_THREADS, "window capacities: four hosts per thread");
+  {
+    double v[4][4];                          // every gather of the thread in flight at once
 #pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const double v = pw ? pw->a[r][p] : A.avail[(size_t)r * H + h];
-      wbad |= !(__builtin_fabs(v) <= ZW_BIG);
-      S.wa[r][p] = v;
+    for (int u = 0; u < 4; u++) {
+      const int p = u * ZW_THREADS + tid;
+      const int h = p < nwin ? S.wid[p] : 0;   // (host 0: a valid address, never used)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        v[u][r] = p >= nwin ? 0.0 : (pw ? pw->a[r][p] : A.avail[(size_t)r * H + h]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int p = u * ZW_THREADS + tid;
+      if (p < nwin) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          wbad |= !(__builtin_fabs(v[u][r]) <= ZW_BIG);
+          S.wa[r][p] = v[u][r];
+        }
+      }
     }
   }
   if (wbad) S.bail = 1;
@@ -293,7 +342,8 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   // suffix minima of the chain's demands per 64-task batch: a chunk no host of which fits the
   // smallest demand still ahead is dead (the walk moves its register chunk past it)
   const int nsb = min((nt + 63) >> 6, ZW_SB);
-  for (int blk = wave; blk < nsb; blk += ZW_WAVES) {
+  // (batches before the last were reduced with the certificates above; the last holds the rest)
+  for (int blk = ZW_SB - 1 + wave; blk < nsb; blk += ZW_WAVES) {
     const int i1 = blk == ZW_SB - 1 ? nt : min(nt, blk * 64 + 64);
     double bm[4] = {DINF, DINF, DINF, DINF};
     for (int i = blk * 64 + lane; i < i1; i += 64) {
