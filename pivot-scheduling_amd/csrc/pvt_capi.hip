@@ -177,8 +177,6 @@ struct pvt_ctx {
   int32_t* next_host = nullptr;   // pinned
   void* gstage = nullptr;         // grouped order: counts, anchors, cost table (pinned)
   size_t gstage_cap = 0;
-  int32_t* goff_pin = nullptr;    // grouped order: offsets + cursors staged for the device
-  size_t goff_cap = 0;            //   (pinned; rewritten only after the previous round synced)
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
 };
 
@@ -349,7 +347,6 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->next_host) (void)hipHostFree(ctx->next_host);
   if (ctx->ep_host) (void)hipHostFree(ctx->ep_host);
-  if (ctx->goff_pin) (void)hipHostFree(ctx->goff_pin);
   if (ctx->gstage) (void)hipHostFree(ctx->gstage);
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
   if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
@@ -532,9 +529,16 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
     double* cst = reinterpret_cast<double*>(ctx->gstage);
     int32_t* cnt = reinterpret_cast<int32_t*>(cst + nz2);
     int32_t* gan = cnt + G + 1;
-    HIPCHK(hipMemcpyAsync(cnt, ctx->gcnt.p, sizeof(int32_t) * (G + 1), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(gan, r->group_anchor, sizeof(int32_t) * G, hipMemcpyDeviceToHost, st));
-    if (ca) HIPCHK(hipMemcpyAsync(cst, r->cost, sizeof(double) * nz2, hipMemcpyDeviceToHost, st));
+    // counts, anchors and cost table written into the pinned buffer by one kernel, which also
+    // leaves the groups' offsets and scatter cursors on the device
+    ENSURE(ctx->goff, sizeof(int32_t) * 2 * (G + 1));
+    void* dstage = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dstage, ctx->gstage, 0));
+    double* dcst = reinterpret_cast<double*>(dstage);
+    int32_t* dcnt = reinterpret_cast<int32_t*>(dcst + nz2);
+    launch_group_stage(P<int32_t>(ctx->gcnt), G, r->group_anchor, r->cost, (int)nz2,
+                       P<int32_t>(ctx->goff), dcnt, dcnt + G + 1, dcst, st);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(st));
     R.gcnt.assign(cnt, cnt + G + 1);
     R.ga_host.assign(gan, gan + G);
@@ -543,23 +547,9 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
     R.ginfo = ca;
     int mx = 0;
     for (int g = 0; g < G; g++) mx = std::max(mx, R.gcnt[g]);
-    if (mx <= GSORT_MAX) {
-      const size_t need = 2 * (size_t)(G + 1);
-      if (ctx->goff_cap < need) {
-        if (ctx->goff_pin) (void)hipHostFree(ctx->goff_pin);
-        ctx->goff_pin = nullptr;
-        ctx->goff_cap = 0;
-        HIPCHK(hipHostMalloc((void**)&ctx->goff_pin, sizeof(int32_t) * need));
-        ctx->goff_cap = need;
-      }
-      int32_t* off = ctx->goff_pin;
-      off[0] = 0;
-      for (int g = 0; g < G; g++) off[g + 1] = off[g] + R.gcnt[g];
-      std::copy(off, off + G + 1, off + G + 1);   // cursors
-      ENSURE(ctx->goff, sizeof(int32_t) * 2 * (G + 1));
+    if (mx <= GSORT_MAX) {                    // (offsets and cursors: group_stage_kernel)
       ENSURE(ctx->gskey, sizeof(uint64_t) * T);
       ENSURE(ctx->gsidx, sizeof(int32_t) * T);
-      HIPCHK(hipMemcpyAsync(ctx->goff.p, off, sizeof(int32_t) * 2 * (G + 1), hipMemcpyHostToDevice, st));
       const uint64_t* keys = nullptr;
       if (r->sort_tasks) {
         ENSURE(ctx->keys64a, sizeof(uint64_t) * T);

@@ -381,6 +381,8 @@ hipError_t init_kernel_attrs();
 // LDS bitonic sort of (key, task index) per group of at most GSORT_MAX tasks
 constexpr int GSORT_MAX = 4096;
 void launch_group_hist(const int32_t* tg, int T, int G, int32_t* cnt, hipStream_t st);
+void launch_group_stage(const int32_t* cnt, int G, const int32_t* ganc, const double* cost, int nz2,
+                        int32_t* off, int32_t* hcnt, int32_t* hgan, double* hcst, hipStream_t st);
 void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,
                           uint64_t* skey, int32_t* sidx, hipStream_t st);
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,

@@ -845,6 +845,52 @@ __global__ __launch_bounds__(1024) void group_hist_kernel(const int32_t* tg, int
       if (loc[q]) atomicAdd(&cnt[q], loc[q]);
   }
 }
+// The group plan's inputs in one step: the group counts (cnt[G] counts out-of-range groups), the
+// group anchors and the cost table written straight into the host's pinned staging buffer (one
+// kernel instead of three DMA copies), and the groups' offsets in processing order plus scatter
+// cursors (off[0..G], off[G+1..2G+1]) computed here instead of uploaded. One block.
+__global__ __launch_bounds__(1024) void group_stage_kernel(const int32_t* cnt, int G,
+                                                           const int32_t* ganc, const double* cost,
+                                                           int nz2, int32_t* off, int32_t* hcnt,
+                                                           int32_t* hgan, double* hcst) {
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int i = t; i <= G; i += 1024) hcnt[i] = cnt[i];
+  for (int i = t; i < G; i += 1024) hgan[i] = ganc[i];
+  for (int i = t; i < nz2; i += 1024) hcst[i] = cost[i];
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int g0 = 0; g0 < G; g0 += 1024) {
+    const int g = g0 + t;
+    const int v = g < G ? cnt[g] : 0;
+    int x = v;                                  // inclusive scan within the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int pre = carry;
+    for (int w = 0; w < wave; w++) pre += wsum[w];
+    if (g < G) {
+      off[g] = pre + x - v;
+      off[G + 1 + g] = pre + x - v;
+    }
+    __syncthreads();
+    if (t == 1023) carry = pre + x;
+    __syncthreads();
+  }
+  if (t == 0) { off[G] = carry; off[2 * G + 1] = carry; }
+  __threadfence_system();
+}
+void launch_group_stage(const int32_t* cnt, int G, const int32_t* ganc, const double* cost, int nz2,
+                        int32_t* off, int32_t* hcnt, int32_t* hgan, double* hcst, hipStream_t st) {
+  hipLaunchKernelGGL(group_stage_kernel, dim3(1), dim3(1024), 0, st, cnt, G, ganc, cost, nz2, off,
+                     hcnt, hgan, hcst);
+}
+
 void launch_group_hist(const int32_t* tg, int T, int G, int32_t* cnt, hipStream_t st) {
   hipLaunchKernelGGL(group_hist_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, T, G, cnt);
 }
