@@ -492,19 +492,24 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     n_iter += t;
 #endif
     // Pass 2: each lane replays its own copies (a per-lane loop; measured faster than one
-    // uniform loop with selects or with masked log writes).
+    // uniform loop with selects or with masked log writes), logging the host of every copy and
+    // the capacities after its last one only: a host's earlier entries in a segment are never
+    // final (epoch_final_kernel marks them; validation and apply read the capacities of final
+    // entries only, and the keyed / ordered walks read no log).
     if (two) {
       for (int m = 0, pos = k + pre; m < asg; m++, pos++) {
         c0 -= d0; c1 -= d1;
-        S.lg[pos][0] = c0; S.lg[pos][1] = c1; S.lg[pos][2] = c2; S.lg[pos][3] = c3;
         S.lgid[pos] = cid;
       }
     } else {
       for (int m = 0, pos = k + pre; m < asg; m++, pos++) {
         c0 -= d0; c1 -= d1; c2 -= d2; c3 -= d3;
-        S.lg[pos][0] = c0; S.lg[pos][1] = c1; S.lg[pos][2] = c2; S.lg[pos][3] = c3;
         S.lgid[pos] = cid;
       }
+    }
+    if (asg > 0) {
+      const int q = k + pre + asg - 1;
+      S.lg[q][0] = c0; S.lg[q][1] = c1; S.lg[q][2] = c2; S.lg[q][3] = c3;
     }
 #ifdef PVT_STAMPS
     st_p2 += zstamp() - tB;
