@@ -160,10 +160,13 @@ struct OppLDS {
   uint32_t kdraw[OPP_R];
   int32_t cnt[OPP_R];           // MT19937 outputs the draw consumed
   int32_t ccount[OPP_R];
+  double pz[OPP_R][8];          // pass 4: each task's chosen host's capacity now / after it
+  int32_t pw[OPP_R];            // pass 4: each task's chosen host
+  int32_t dl[OPP_R];            // pass 2: the range's draw tasks (n >= 2), in order
   uint32_t mt[625];
   uint32_t mtb[625];            // state at the range start
   int32_t pl[OPP_MAXW];         // placements of the window, written out when the walk ends
-  int32_t wl[OPP_NW][WAVE];     // per wave: a task's lost hosts (pass 1)
+  int32_t wl[OPP_NW][OPP_TB][WAVE];   // per wave and task: its lost hosts (pass 1)
   int32_t lhist[OPP_NW][WAVE];  // per wave: a task's lost hosts per super-chunk (pass 3)
   uint64_t lclr[OPP_NW][OPP_SUP][OPP_CH / WAVE];   // per wave: lost bits of the drawn super-chunk
   int32_t ctl[4];               // next range start, touched count
@@ -188,6 +191,14 @@ __device__ __forceinline__ void ohash_put(OppLDS& S, int32_t id, int32_t v) {
   while (S.hkey[p] >= 0) p = (p + 1) & (OPP_HASH - 1);
   S.hkey[p] = id;
   S.hval[p] = v;
+}
+
+// A wave-uniform double (an LDS broadcast) as a scalar.
+__device__ __forceinline__ double rfl_d(double v) {
+  union { double d; uint64_t u; } x;
+  x.d = v;
+  x.u = rfl_u64(x.u);
+  return x.d;
 }
 
 // Position of the r-th (0-based) set bit of x (r < popcount(x)).
@@ -312,7 +323,7 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
   const bool fast = A.nsq <= WAVE;   // one super-chunk count per lane (H <= 1,048,576)
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #ifdef PVT_STAMPS
-  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tl = ostamp();
 #endif
 
@@ -322,22 +333,46 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
     const int m = __builtin_amdgcn_readfirstlane(S.ctl[1]);
     // ---- pass 1 (all waves): n_j = snapshot count - lost, for the range's tasks; each task's
     // lost hosts stay in a register (lane l = the l-th; nlost > 64: rescanned in pass 3)
-    double t0[OPP_TB], t1[OPP_TB], t2[OPP_TB], t3[OPP_TB];
+    // Lanes = touched hosts: a 64-host piece of the table is read from LDS once and tested
+    // against the wave's OPP_TB tasks (demands broadcast from registers).
+    double dv[OPP_TB];
     int scr[OPP_TB], lh[OPP_TB], nlost[OPP_TB];
 #pragma unroll
     for (int t = 0; t < OPP_TB; t++) {
       const int j = s + wave * OPP_TB + t;
       const bool ok = j < e;
-      const double dv = ok ? A.dem[(size_t)j * 4 + (lane & 3)] : 0.0;
+      dv[t] = ok ? A.dem[(size_t)j * 4 + (lane & 3)] : 0.0;
       scr[t] = (ok && fast && lane < A.nsq) ? A.sc[(size_t)j * A.nsq + lane] : 0;
-      t0[t] = readlane_d(dv, 0); t1[t] = readlane_d(dv, 1);
-      t2[t] = readlane_d(dv, 2); t3[t] = readlane_d(dv, 3);
+      nlost[t] = 0;
     }
+    const int ntw = max(0, min(OPP_TB, e - (s + wave * OPP_TB)));   // this wave's tasks
+    for (int q0 = 0; q0 < m; q0 += WAVE) {
+      const int q = q0 + lane, qq = min(q, m - 1);
+      const double a0 = S.sa[0][qq], a1 = S.sa[1][qq], a2 = S.sa[2][qq], a3 = S.sa[3][qq];
+      const double b0 = S.ta[0][qq], b1 = S.ta[1][qq], b2 = S.ta[2][qq], b3 = S.ta[3][qq];
+      const int32_t th = S.tid[qq];
+      const uint64_t vm = __ballot(q < m);
+#pragma unroll
+      for (int t = 0; t < OPP_TB; t++) {
+        if (t >= ntw) break;
+        const double d0 = readlane_d(dv[t], 0), d1 = readlane_d(dv[t], 1);
+        const double d2 = readlane_d(dv[t], 2), d3 = readlane_d(dv[t], 3);
+        // fitted in the count pass's view (sa), no longer fits (ta); fits<false> per lane =
+        // the AND of the per-dimension ballots
+        const uint64_t b = vm & __ballot(a0 >= d0) & __ballot(a1 >= d1) & __ballot(a2 >= d2) &
+                           __ballot(a3 >= d3) &
+                           ~(__ballot(b0 >= d0) & __ballot(b1 >= d1) & __ballot(b2 >= d2) &
+                             __ballot(b3 >= d3));
+        const int pos = nlost[t] + __popcll(b & below);
+        if (((b >> lane) & 1) && pos < WAVE) S.wl[wave][t][pos] = th;
+        nlost[t] += __popcll(b);
+      }
+    }
+    wave_lds_fence();
 #pragma unroll
     for (int t = 0; t < OPP_TB; t++) {
       const int j = s + wave * OPP_TB + t;
       lh[t] = -1;
-      nlost[t] = 0;
       if (j < e) {
         long long tot = 0;
         if (fast) {
@@ -348,40 +383,50 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
             tot += wave_sum_ll(Q < A.nsq ? (long long)A.sc[(size_t)j * A.nsq + Q] : 0);
           }
         }
-        int nl = 0;
-        for (int q0 = 0; q0 < m; q0 += WAVE) {
-          int32_t th;
-          const uint64_t b = lost_piece(S, m, q0, t0[t], t1[t], t2[t], t3[t], th);
-          const int pos = nl + __popcll(b & below);
-          if (((b >> lane) & 1) && pos < WAVE) S.wl[wave][pos] = th;
-          nl += __popcll(b);
-        }
-        wave_lds_fence();
-        lh[t] = lane < nl ? S.wl[wave][lane] : -1;
-        nlost[t] = nl;
-        wave_lds_fence();
-        if (lane == 0) S.nspec[j - s] = (int)(tot - nl);
+        lh[t] = lane < nlost[t] ? S.wl[wave][t][lane] : -1;
+        if (lane == 0) S.nspec[j - s] = (int)(tot - nlost[t]);
       }
     }
     __syncthreads();
     OSTAMP(0);
-    // ---- pass 2 (wave 0): the draws, in task order, from the live state (saved first)
+    // ---- pass 2 (wave 0): the draws, in task order, from the live state (saved first). Most
+    // draws accept their first output (n is close to the mask's power of two), so each pending
+    // draw is first tried against one buffered output (lane q: the (q - used)-th pending draw);
+    // the accepted prefix commits at once and the first rejected draw runs the rejection loop.
+    // Draws for n = 1 consume nothing (randint's range 0), as in mt_randint_cnt.
     if (wave == 0) {
       for (int i = lane; i < 625; i += WAVE) S.mtb[i] = S.mt[i];
+      const int R = e - s;
+      const int nsv = lane < R ? S.nspec[lane] : 0;
+      if (lane < R) { S.kdraw[lane] = nsv == 1 ? 0u : 0xffffffffu; S.cnt[lane] = 0; }
+      const uint64_t dm = __ballot(lane < R && nsv >= 2);
+      if ((dm >> lane) & 1ull) S.dl[__popcll(dm & below)] = lane;
       wave_lds_fence();
+      const int nd = __popcll(dm);
       MtWave mw;
       mw.buf = 0; mw.used = 0; mw.limit = 0;
-      const int nsv = lane < e - s ? S.nspec[lane] : 0;
-      uint32_t kv = 0xffffffffu;
-      int cv = 0;
-      for (int j = 0; j < e - s; j++) {
-        const int n = __builtin_amdgcn_readlane(nsv, j);
-        if (n <= 0) continue;
-        int used = 0;
-        const uint32_t k = mt_randint_cnt(S.mt, mw, (uint32_t)n, used);
-        if (lane == j) { kv = k; cv = used; }
+      int d = 0;
+      while (d < nd) {
+        if (mw.used >= mw.limit) mt_refill(S.mt, mw);
+        const int r = d + lane - mw.used;
+        const bool in = lane >= mw.used && lane < mw.limit && r < nd;
+        const int t = in ? S.dl[r] : 0;
+        const uint32_t rg = (uint32_t)(S.nspec[t] - 1), mk = rint_mask(rg);
+        const uint32_t kq = mw.buf & mk;
+        const uint64_t inm = __ballot(in), bad = __ballot(in && kq > rg);
+        const uint64_t acc = bad ? (inm & ((1ull << __builtin_ctzll(bad)) - 1ull)) : inm;
+        if ((acc >> lane) & 1ull) { S.kdraw[t] = kq; S.cnt[t] = 1; }
+        const int na = __popcll(acc);
+        d += na;
+        mw.used += na;
+        if (bad) {   // draw d rejects its first output: the rejection loop from that output
+          const int tb = __builtin_amdgcn_readfirstlane(S.dl[d]);
+          int used = 0;
+          const uint32_t k = mt_randint_cnt(S.mt, mw, (uint32_t)__builtin_amdgcn_readfirstlane(S.nspec[tb]), used);
+          if (lane == 0) { S.kdraw[tb] = k; S.cnt[tb] = used; }
+          d++;
+        }
       }
-      if (lane < e - s) { S.kdraw[lane] = kv; S.cnt[lane] = cv; }
       mt_unbuffer(S.mt, mw);
     }
     __syncthreads();
@@ -404,9 +449,13 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       if (fast) {
         // one super-chunk per lane: its snapshot count minus the task's lost hosts in it, the
         // lost hosts counted by an LDS histogram (one atomic per lost host, not a readlane loop)
-        S.lhist[wave][lane] = 0;
-        wave_lds_fence();
-        if (nlost[t] <= WAVE) {
+        const bool none = nlost[t] == 0;   // (common: no lost host, the snapshot counts hold)
+        if (!none) {
+          S.lhist[wave][lane] = 0;
+          wave_lds_fence();
+        }
+        if (none) {
+        } else if (nlost[t] <= WAVE) {
           if (lane < nlost[t]) atomicAdd(&S.lhist[wave][lh[t] / SUPH], 1);
         } else {   // (rare) rescan, with the demand reloaded
           const double dv = A.dem[(size_t)j * 4 + (lane & 3)];
@@ -419,7 +468,7 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
           }
         }
         wave_lds_fence();
-        const int v = lane < A.nsq ? scr[t] - S.lhist[wave][lane] : 0;
+        const int v = lane < A.nsq ? scr[t] - (none ? 0 : S.lhist[wave][lane]) : 0;
         const int inc = wave_incl_scan_dpp(v);
         const int tot = __builtin_amdgcn_readlane(inc, 63);
         if ((long long)k < tot) {
@@ -480,31 +529,35 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       if (Qs >= 0) {
         // current bitmaps: the snapshot's minus the lost hosts of this super-chunk (lane = its
         // chunk), collected by LDS atomics -- one per lost host -- instead of a readlane loop
+        // (common: none of the task's lost hosts lies in this super-chunk -- the bitmaps hold)
+        const bool clear = nlost[t] > WAVE || __ballot(lane < nlost[t] && lh[t] / SUPH == Qs) != 0;
+        if (clear) {
 #pragma unroll
-        for (int u = 0; u < U; u++) S.lclr[wave][lane][u] = 0;
-        wave_lds_fence();
-        auto mark = [&](int h, bool on) {
-          if (on && h / SUPH == Qs) {
-            const int o = h % OPP_CH;
-            atomicOr((unsigned long long*)&S.lclr[wave][(h / OPP_CH) % OPP_SUP][o / WAVE],
-                     1ull << (o % WAVE));
+          for (int u = 0; u < U; u++) S.lclr[wave][lane][u] = 0;
+          wave_lds_fence();
+          auto mark = [&](int h, bool on) {
+            if (on && h / SUPH == Qs) {
+              const int o = h % OPP_CH;
+              atomicOr((unsigned long long*)&S.lclr[wave][(h / OPP_CH) % OPP_SUP][o / WAVE],
+                       1ull << (o % WAVE));
+            }
+          };
+          if (nlost[t] <= WAVE) {
+            mark(lh[t], lane < nlost[t]);
+          } else {
+            const double dv = A.dem[(size_t)j * 4 + (lane & 3)];
+            const double f0 = readlane_d(dv, 0), f1 = readlane_d(dv, 1);
+            const double f2 = readlane_d(dv, 2), f3 = readlane_d(dv, 3);
+            for (int p0 = 0; p0 < m; p0 += WAVE) {
+              int32_t th;
+              const uint64_t b = lost_piece(S, m, p0, f0, f1, f2, f3, th);
+              mark(th, (b >> lane) & 1ull);
+            }
           }
-        };
-        if (nlost[t] <= WAVE) {
-          mark(lh[t], lane < nlost[t]);
-        } else {
-          const double dv = A.dem[(size_t)j * 4 + (lane & 3)];
-          const double f0 = readlane_d(dv, 0), f1 = readlane_d(dv, 1);
-          const double f2 = readlane_d(dv, 2), f3 = readlane_d(dv, 3);
-          for (int p0 = 0; p0 < m; p0 += WAVE) {
-            int32_t th;
-            const uint64_t b = lost_piece(S, m, p0, f0, f1, f2, f3, th);
-            mark(th, (b >> lane) & 1ull);
-          }
+          wave_lds_fence();
+#pragma unroll
+          for (int u = 0; u < U; u++) bits[t][u] &= ~S.lclr[wave][lane][u];
         }
-        wave_lds_fence();
-#pragma unroll
-        for (int u = 0; u < U; u++) bits[t][u] &= ~S.lclr[wave][lane][u];
         int c = 0;
 #pragma unroll
         for (int u = 0; u < U; u++) c += __popcll(bits[t][u]);
@@ -582,15 +635,19 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
     __syncthreads();
     OSTAMP(2);
     // ---- pass 4 (wave 0): walk the range. Lane l holds range task s + l: its demand, draw,
-    // candidates, the capacity of its first candidate c_0 now (z) and after taking it (y), the
+    // candidates (S.cav keeps their capacities current through the range's commits), the
     // candidates that stopped fitting (lm), the lost hosts below c_0 (mm) and its new-lost count
-    // (nnew). A task no commit of this range has affected (nnew == 0) takes c_0 from its lane's
-    // registers; the others verify their draw and select among their candidates. Nothing is
+    // (nnew). Task i's draw holds while dok (same mask, k <= n - 1 for n - nnew), and its host is
+    // then the mm-th candidate that still fits (the k-th feasible host, shifted by the lost hosts
+    // below c_0) -- unless fewer candidates fit, when the range stops there. Every lane keeps that
+    // choice (host, capacity now, capacity after) in an LDS row, recomputed in parallel when a
+    // commit takes a host from it or changes a candidate's capacity, so the walk itself is one
+    // LDS broadcast, the fit tests of the later tasks and two ballots per task. Nothing is
     // written to the touched table until the range ends.
     if (wave == 0) {
       const int R = e - s;
       const bool mine = lane < R;
-      double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0, z0 = 0.0, z1 = 0.0, z2 = 0.0, z3 = 0.0;
+      double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0;
       int nsv = 0, ccv = 0;
       uint32_t kv = 0;
       int cd[OPP_C];
@@ -605,107 +662,110 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
 #pragma unroll
         for (int x = 0; x < OPP_C; x++)
           if (x < ccv) cd[x] = S.cand[lane][x];
-        if (ccv > 0) { z0 = S.cav[lane][0][0]; z1 = S.cav[lane][1][0]; z2 = S.cav[lane][2][0]; z3 = S.cav[lane][3][0]; }
       }
       const int c0l = cd[0];
       int cmax = ccv > 0 ? cd[0] : -1;   // the largest candidate (candidates ascend)
 #pragma unroll
       for (int x = 1; x < OPP_C; x++) cmax = x < ccv ? cd[x] : cmax;
-      double y0 = z0 - e0, y1 = z1 - e1, y2 = z2 - e2, y3 = z3 - e3;
-      // dok: the speculative draw still holds for the new-lost count (same mask, k <= n - 1;
-      // recomputed when a commit takes a host away). A task whose draw holds and whose c_0 still
-      // fits with no lost host below it (mm == 0) takes c_0 from its lane's registers whatever
-      // hosts above c_0 it lost. (A task with feasible hosts but no candidates cannot happen
-      // when the counts are consistent; dok = 0 sends it to the slow path, which stops there.)
       int nnew = 0, mm = 0;
-      bool dok = !(nsv > 0 && ccv == 0);
+      bool dok = true;
       uint32_t lm = 0;
-      int rch = -1;   // commit of a task that took the slow path, with capacities after / before
-      double ra0 = 0.0, ra1 = 0.0, ra2 = 0.0, ra3 = 0.0, rb0 = 0.0, rb1 = 0.0, rb2 = 0.0, rb3 = 0.0;
-      uint64_t fcm = 0;   // tasks that took c_0 on the fast path (commit = c0l, z -> y)
+      // the lane's choice: the mm-th candidate still fitting, into its LDS row; false if none
+      auto choose = [&]() -> bool {
+        const uint32_t valid = ((1u << ccv) - 1u) & ~lm;
+        if (!mine || !dok || __popc(valid) <= mm) return false;
+        const int xs = select_bit(valid, mm);
+        const double z0 = S.cav[lane][0][xs], z1 = S.cav[lane][1][xs];
+        const double z2 = S.cav[lane][2][xs], z3 = S.cav[lane][3][xs];
+        S.pw[lane] = cd[xs];
+        S.pz[lane][0] = z0; S.pz[lane][1] = z1; S.pz[lane][2] = z2; S.pz[lane][3] = z3;
+        S.pz[lane][4] = z0 - e0; S.pz[lane][5] = z1 - e1; S.pz[lane][6] = z2 - e2; S.pz[lane][7] = z3 - e3;
+        return true;
+      };
+      // Uniform masks over the range's lanes:
+      //   posm  tasks with a feasible host at s (the others place nothing and change nothing);
+      //   okm   tasks whose choice holds now;  done  tasks committed.
+      const uint64_t minem = __ballot(mine);
+      const uint64_t posm = __ballot(mine && nsv > 0);
+      uint64_t okm = __ballot(choose());
+      wave_lds_fence();
+      uint64_t cmt = 0;
       int stop = e;
-      for (int i = s; i < e; i++) {
-        const int L = i - s;
-        const int n = __builtin_amdgcn_readlane(nsv, L);
-        if (n <= 0) continue;   // no feasible host at s: none now (capacities only decrease)
-        const bool fast = __builtin_amdgcn_readlane((int)(dok & (mm == 0) & !(lm & 1u)), L) != 0;
-        int w;
-        double w0, w1, w2, w3, n0, n1, n2, n3;
-        if (fast) {
-          w = __builtin_amdgcn_readlane(c0l, L);
-          w0 = readlane_d(z0, L); w1 = readlane_d(z1, L); w2 = readlane_d(z2, L); w3 = readlane_d(z3, L);
-          n0 = readlane_d(y0, L); n1 = readlane_d(y1, L); n2 = readlane_d(y2, L); n3 = readlane_d(y3, L);
-          fcm |= 1ull << L;
-        } else {
-          const int nn = __builtin_amdgcn_readlane(nnew, L);
-          const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)kv, L);
-          const int ntrue = n - nn;
-          if (ntrue <= 0 || rint_mask((uint32_t)(ntrue - 1)) != rint_mask((uint32_t)(n - 1)) ||
-              k > (uint32_t)(ntrue - 1)) {
-            stop = i;
-            break;
-          }
-          const int cc = __builtin_amdgcn_readlane(ccv, L);
-          const int mi = __builtin_amdgcn_readlane(mm, L);
-          const uint32_t valid = ((1u << cc) - 1u) & ~(uint32_t)__builtin_amdgcn_readlane((int)lm, L);
-          if (__popc(valid) <= mi) {   // the answer lies beyond the candidates
-            stop = i;
-            break;
-          }
-          const int xs = select_bit(valid, mi);
-          if (xs == 0) {   // c_0 at its current capacity
-            w = __builtin_amdgcn_readlane(c0l, L);
-            w0 = readlane_d(z0, L); w1 = readlane_d(z1, L); w2 = readlane_d(z2, L); w3 = readlane_d(z3, L);
-          } else {         // range-start capacity, unless committed earlier in this range
-            w = __builtin_amdgcn_readfirstlane(S.cand[L][xs]);
-            w0 = S.cav[L][0][xs]; w1 = S.cav[L][1][xs]; w2 = S.cav[L][2][xs]; w3 = S.cav[L][3][xs];
-            const bool fl = (fcm >> lane) & 1;
-            const uint64_t hit = __ballot((fl ? c0l : rch) == w);
-            if (hit) {
-              const int l = 63 - __builtin_clzll(hit);
-              const bool f = (fcm >> l) & 1;
-              w0 = f ? readlane_d(y0, l) : readlane_d(ra0, l);
-              w1 = f ? readlane_d(y1, l) : readlane_d(ra1, l);
-              w2 = f ? readlane_d(y2, l) : readlane_d(ra2, l);
-              w3 = f ? readlane_d(y3, l) : readlane_d(ra3, l);
+      OSTAMP(9);
+      // Software-pipelined: the row of the next task with a feasible host is read while this
+      // task's commit is tested (and read again if that commit rewrote it).
+      int L = posm ? __builtin_ctzll(posm) : R;
+      int w = 0;
+      double w0 = 0.0, w1 = 0.0, w2 = 0.0, w3 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
+      auto row = [&](int l) {
+        w = S.pw[l];
+        w0 = S.pz[l][0]; w1 = S.pz[l][1]; w2 = S.pz[l][2]; w3 = S.pz[l][3];
+        n0 = S.pz[l][4]; n1 = S.pz[l][5]; n2 = S.pz[l][6]; n3 = S.pz[l][7];
+      };
+      if (L < R) row(L);
+      while (L < R) {   // (tasks without a feasible host at s place nothing and change nothing)
+        if (!((okm >> L) & 1ull)) {   // the draw changed, or the answer lies beyond the
+          stop = s + L;               // candidates: the range stops here
+          break;
+        }
+        const int cw = w;
+        const double c0 = w0, c1 = w1, c2 = w2, c3 = w3, m0 = n0, m1 = n1, m2 = n2, m3 = n3;
+        const uint64_t nx = posm & ~((2ull << L) - 1ull);
+        const int Ln = nx ? __builtin_ctzll(nx) : R;
+        if (Ln < R) row(Ln);
+        cmt |= 1ull << L;
+        // the later tasks of the range: does this commit take cw away from them (lostm: fitted
+        // before, not after -- fits<false> per lane is the AND of the per-dimension ballots),
+        // or is cw inside their candidates' id range (rngm; rare: a commit's host is random
+        // among ~1M)?
+        const uint64_t am = minem & ~((2ull << L) - 1ull);
+        const uint64_t fw = __ballot(c0 >= e0) & __ballot(c1 >= e1) & __ballot(c2 >= e2) & __ballot(c3 >= e3);
+        const uint64_t fn = __ballot(m0 >= e0) & __ballot(m1 >= e1) & __ballot(m2 >= e2) & __ballot(m3 >= e3);
+        const uint64_t lostm = am & fw & ~fn;
+        const uint64_t rngm = am & __ballot(cw >= c0l) & __ballot(cw <= cmax);
+#ifdef PVT_STAMPS
+        ph[13] += 1;
+        ph[11] += lostm ? 1 : 0;
+        ph[12] += rngm ? 1 : 0;
+#endif
+        if (lostm | rngm) {
+          const bool lost = (lostm >> lane) & 1ull;
+          if ((rngm >> lane) & 1ull) {   // cw's capacity is now m; a lost cw stops fitting
+#pragma unroll
+            for (int x = 0; x < OPP_C; x++) {
+              if (cd[x] == cw) {
+                S.cav[lane][0][x] = m0; S.cav[lane][1][x] = m1;
+                S.cav[lane][2][x] = m2; S.cav[lane][3][x] = m3;
+                if (lost) lm |= 1u << x;
+              }
             }
           }
-          n0 = w0 - readlane_d(e0, L); n1 = w1 - readlane_d(e1, L);
-          n2 = w2 - readlane_d(e2, L); n3 = w3 - readlane_d(e3, L);
-          if (lane == L) {
-            rch = w;
-            ra0 = n0; ra1 = n1; ra2 = n2; ra3 = n3;
-            rb0 = w0; rb1 = w1; rb2 = w2; rb3 = w3;
+          if (lost) {
+            nnew += 1;
+            mm += cw < c0l;
+            const int ntrue = nsv - nnew;
+            dok = dok & (ntrue > 0) & (rint_mask((uint32_t)(ntrue - 1)) == rint_mask((uint32_t)(nsv - 1))) &
+                  (kv <= (uint32_t)(ntrue - 1));
           }
+          wave_lds_fence();
+          const bool redo = ((lostm | rngm) >> lane) & 1ull;
+          bool ok = (okm >> lane) & 1ull;
+          if (redo) ok = choose();
+          okm = __ballot(ok);
+          wave_lds_fence();
+          if (Ln < R) row(Ln);
         }
-        // the later tasks of the range: does this commit take w away from them?
-        const bool act = lane > L && mine;
-        const bool lost = act & fits<false>(w0, w1, w2, w3, e0, e1, e2, e3) &
-                          !fits<false>(n0, n1, n2, n3, e0, e1, e2, e3);
-        nnew += lost;
-        mm += lost & (w < c0l);
-        if (lost) {
-          const int ntrue = nsv - nnew;
-          dok = dok & (ntrue > 0) & (rint_mask((uint32_t)(ntrue - 1)) == rint_mask((uint32_t)(nsv - 1))) &
-                (kv <= (uint32_t)(ntrue - 1));
-        }
-        // (a lost host can only be one of the lane's candidates inside their id range: the
-        // 16-way compare runs only then, rarely -- a commit's host is random among ~1M)
-        if (__ballot(lost & (w >= c0l) & (w <= cmax))) {
-#pragma unroll
-          for (int x = 0; x < OPP_C; x++) lm |= ((lost & (cd[x] == w)) ? 1u : 0u) << x;
-        }
-        if (__ballot(act & (c0l == w))) {   // their c_0 was taken: its capacity now
-          if (act & (c0l == w)) {
-            z0 = n0; z1 = n1; z2 = n2; z3 = n3;
-            y0 = n0 - e0; y1 = n1 - e1; y2 = n2 - e2; y3 = n3 - e3;
-          }
-        }
+        L = Ln;
       }
-      if ((fcm >> lane) & 1) {   // fast-path commits: c_0, capacity z before, y after
-        rch = c0l;
-        ra0 = y0; ra1 = y1; ra2 = y2; ra3 = y3;
-        rb0 = z0; rb1 = z1; rb2 = z2; rb3 = z3;
+      OSTAMP(8);
+      // the range's commits: lane l's row still holds its choice (later commits only rewrite
+      // the rows of the tasks after them)
+      int rch = -1;
+      double ra0 = 0.0, ra1 = 0.0, ra2 = 0.0, ra3 = 0.0, rb0 = 0.0, rb1 = 0.0, rb2 = 0.0, rb3 = 0.0;
+      if ((cmt >> lane) & 1ull) {
+        rch = S.pw[lane];
+        rb0 = S.pz[lane][0]; rb1 = S.pz[lane][1]; rb2 = S.pz[lane][2]; rb3 = S.pz[lane][3];
+        ra0 = S.pz[lane][4]; ra1 = S.pz[lane][5]; ra2 = S.pz[lane][6]; ra3 = S.pz[lane][7];
       }
       // A range whose first task fails cannot happen when the counts are consistent (its state
       // is exact). If it does (inconsistent counts or bitmaps), report it -- the host returns
@@ -792,7 +852,8 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
   for (int i = tx; i < 625; i += NT) A.mt[i] = S.mt[i];
 #ifdef PVT_STAMPS
   if (tx == 0 && A.stamps) {
-    for (int k = 0; k < 7; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
+    for (int k = 0; k < 14; k++)
+      if (k != 7) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
     atomicAdd((unsigned long long*)&A.stamps[7], (unsigned long long)A.nt);
   }
 #endif

@@ -14,29 +14,31 @@ from pivot_place.engine import DeviceRound, PlacementEngine  # noqa: E402
 mode = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 H = int(sys.argv[2]) if len(sys.argv) > 2 else 1_000_000
 T = int(sys.argv[3]) if len(sys.argv) > 3 else 10_000
-eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "diag",
-                                               "libpivot_place_stamps.so"))
+eng = PlacementEngine(0, lib_path=os.environ.get("STAMPS_LIB") or os.path.join(
+    ROOT, "pivot-scheduling_amd", "diag", "libpivot_place_stamps.so"))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-buf = (ctypes.c_uint64 * 8)()
-assert f(eng.ctx, buf, 8) == 0          # allocates and zeroes the device counters
+buf = (ctypes.c_uint64 * 16)()
+assert f(eng.ctx, buf, 16) == 0         # allocates and zeroes the device counters
 r = synthetic.make_round(mode, H, T)
 dr = DeviceRound(r, eng.device)
 eng.run(dr)
 torch.cuda.synchronize()
-assert f(eng.ctx, buf, 8) == 0
+assert f(eng.ctx, buf, 16) == 0
 if mode == 2:
     # speculative range walk (pvt_opp.hip): counts per range, draws, candidates, verified walk
-    names = ["pass1-counts", "pass2-draws", "pass3-candidates", "pass4-walk"]
-    sub = {5: "  pass3a-select+load", 6: "  pass3b-candidates", 2: "  pass3c-capacities"}
-    tot = sum(buf[k] for k in range(4))
+    # stamp 2 holds only pass 3's last part (5 and 6 are its first two)
+    names = [(0, "pass1-counts"), (1, "pass2-draws"), (5, "pass3a-select+load"),
+             (6, "pass3b-candidates"), (2, "pass3c-capacities"), (9, "pass4-setup"),
+             (8, "pass4-loop"), (3, "pass4-commits")]
+    tot = sum(buf[k] for k, _ in names)
     print("opportunistic H=%d T=%d tasks=%d ranges=%d stats=%s"
           % (H, T, buf[7], buf[4], eng.last_stats()))
-    for k in range(4):
-        print("  %-16s %6.1f%%  %8.0f cycles/task" % (names[k], 100.0 * buf[k] / max(tot, 1),
+    for k, nm in names:
+        print("  %-20s %6.1f%%  %8.0f cycles/task" % (nm, 100.0 * buf[k] / max(tot, 1),
                                                       buf[k] / max(buf[7], 1)))
-    for k in (5, 6, 2):   # pass 3 split (stamp 2 then holds only its last part)
-        print("  %-20s %8.0f cycles/task" % (sub[k], buf[k] / max(buf[7], 1)))
+    print("  pass-4 commits %d: lost to a later task %d, among a later task's candidates' id "
+          "range %d" % (buf[13], buf[11], buf[12]))
     sys.exit(0)
 if mode == 3 or os.environ.get("ZWALK"):
     # frontier walk (pvt_zwalk.hip; vbp first-fit: ordered frontier attempts): prologue
