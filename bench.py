@@ -250,6 +250,10 @@ PMC_INDEX = os.path.join(ROOT, "profiles", "pmc_index.json")
 SIMDS, CUS = 1024, 256
 SHADER_HZ = 2.4e9
 ISSUE_CYCLES = 4          # one wave issues at most one instruction per 4 cycles
+# Waves per workgroup of the one-workgroup-per-walk kernels (pvt_zwalk.hip ZW_THREADS, pvt_lwalk.hip,
+# pvt_walk.hip WALK_THREADS, pvt_opp.hip OPP_NW). Their PMC instruction counts cover every wave,
+# so the issue peak is that of min(waves, 4 SIMDs) waves of one CU.
+WALK_WAVES = {"zwalk_kernel": 4, "lwalk_kernel": 1, "commit_kernel": 8, "opp_commit_kernel": 8}
 LDS_DEP_CYCLES = 50       # one dependent LDS round trip (MI355X_MICROARCH.md constants table)
 INSTS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD",
          "SQ_INSTS_VMEM_WR")
@@ -318,20 +322,24 @@ def score_roofline(mode, H, T, ks, kernel):
 def walk_roofline(mode, H, T, ks, ep, steps, kernel="zwalk_kernel"):
     """A sequential walk (the frontier walk, the list commit walk, the opportunistic walk): each
     task reads the capacities the previous commit wrote, so the chain is one wave's dependent
-    instruction stream, bounded by that wave's issue: at most one instruction per 4 cycles
-    (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost, one wave'). achieved = instructions
-    per task (PMC, every wave of the kernel, over the round's tasks) x tasks per second on the
-    critical path (the longest frontier chain, or every task for the one-workgroup walks);
-    peak = 2.4 GHz / 4. The latency floor (one dependent LDS round trip per task) is beside it."""
+    instruction stream, bounded by issue: at most one instruction per 4 cycles per wave
+    (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost, one wave'), for the min(waves, 4)
+    waves of the walk's workgroup (the helper waves' instructions are counted too). achieved =
+    instructions per task (PMC, every wave of the kernel, over the round's tasks) x tasks per
+    second on the critical path (the longest frontier chain, or every task for the
+    one-workgroup walks); peak = min(waves, 4) x 2.4 GHz / 4. The latency floor (one dependent
+    LDS round trip per task) is beside it."""
     c = ks["commit"]
     ms = c["ms"] / max(steps, 1)
     longest = ep.get("longest_chain_tasks", 0) if kernel == "zwalk_kernel" else 0
     if longest <= 0:
         longest = T                      # every task of the round on one walk after another
-    out = {"kernel": kernel, "bound": "issue", "unit": "instructions/s (one wave)", "traffic": None,
-           "walk_ms_per_step": ms, "critical_path_tasks": longest,
-           "peak_basis": "one instruction per %d cycles of one wave at %.1f GHz"
-                         % (ISSUE_CYCLES, SHADER_HZ / 1e9),
+    issue_waves = min(4, WALK_WAVES.get(kernel, 1))
+    out = {"kernel": kernel, "bound": "issue", "unit": "instructions/s (one workgroup)",
+           "traffic": None, "walk_ms_per_step": ms, "critical_path_tasks": longest,
+           "peak_basis": "one instruction per %d cycles per wave at %.1f GHz, %d wave(s) of %d "
+                         "in the workgroup issuing (one per SIMD)"
+                         % (ISSUE_CYCLES, SHADER_HZ / 1e9, issue_waves, WALK_WAVES.get(kernel, 1)),
            "achieved": None, "peak": None, "frac": None}
     if ms <= 0:
         return out
@@ -355,8 +363,11 @@ def walk_roofline(mode, H, T, ks, ep, steps, kernel="zwalk_kernel"):
     traffic = 2.0 * cnt.get("FETCH_SIZE", 0.0) * 1024 + cnt.get("WRITE_SIZE", 0.0) * 1024
     out["traffic"] = traffic if traffic > 0 else None
     achieved = ipt * tasks_per_s
-    peak = SHADER_HZ / ISSUE_CYCLES
-    out.update({"achieved": achieved, "peak": peak, "frac": achieved / peak})
+    peak = SHADER_HZ / ISSUE_CYCLES * issue_waves
+    # (frac_one_wave: against a single wave's issue, as if the helper waves' instructions were
+    # the walker's -- above 1 when the helpers do much of the work, as in the opportunistic walk)
+    out.update({"achieved": achieved, "peak": peak, "frac": achieved / peak,
+                "frac_one_wave": achieved / (SHADER_HZ / ISSUE_CYCLES)})
     if out["waves_per_launch"] and out["waves_per_launch"] > 1 and kernel != "zwalk_kernel":
         out["note"] = ("instructions of every wave of the walk's workgroup (walker and scouts, "
                        "spin waits included) per task of the critical path")

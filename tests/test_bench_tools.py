@@ -47,4 +47,6 @@ def test_pmc_index_and_binary_check(tmp_path, monkeypatch):
     ks = {"commit": {"ms": 1.0, "launches": 1}, "score": {"ms": 0.0, "launches": 0}}
     rl = bench.walk_roofline(bench.MODES["ca_bf"], 1000, 10, ks, {"longest_chain_tasks": 10}, 1)
     assert rl["instructions_per_task"] == pytest.approx(400.0 * 2 / 10)
-    assert rl["frac"] == pytest.approx(80.0 * (10 / 1e-3) / (2.4e9 / 4))
+    # zwalk_kernel: 4 waves per workgroup, all of them counted and all of them issuing
+    assert rl["frac"] == pytest.approx(80.0 * (10 / 1e-3) / (4 * 2.4e9 / 4))
+    assert rl["frac_one_wave"] == pytest.approx(80.0 * (10 / 1e-3) / (2.4e9 / 4))
