@@ -253,7 +253,7 @@ ISSUE_CYCLES = 4          # one wave issues at most one instruction per 4 cycles
 # Waves per workgroup of the one-workgroup-per-walk kernels (pvt_zwalk.hip ZW_THREADS, pvt_lwalk.hip,
 # pvt_walk.hip WALK_THREADS, pvt_opp.hip OPP_NW). Their PMC instruction counts cover every wave,
 # so the issue peak is that of min(waves, 4 SIMDs) waves of one CU.
-WALK_WAVES = {"zwalk_kernel": 4, "lwalk_kernel": 1, "commit_kernel": 8, "opp_commit_kernel": 8}
+WALK_WAVES = {"zwalk_kernel": 4, "lwalk_kernel": 1, "commit_kernel": 8, "opp_commit_kernel": 16}
 LDS_DEP_CYCLES = 50       # one dependent LDS round trip (MI355X_MICROARCH.md constants table)
 INSTS = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_VMEM_RD",
          "SQ_INSTS_VMEM_WR")

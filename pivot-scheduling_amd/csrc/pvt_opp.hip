@@ -138,7 +138,9 @@ void launch_opp_count(const OppCountArgs& a0, hipStream_t st) {
 // ------------------------------------------------------------------------------------------
 constexpr int OPP_R = 64;               // tasks per speculation range (one walker lane each)
 constexpr int OPP_C = 16;               // candidates per task (4 lanes each load one)
-constexpr int OPP_NW = 8;               // waves of the walk workgroup
+constexpr int OPP_NW = 16;              // waves of the walk workgroup (4 range tasks each in
+                                        // the parallel passes; measured: 12.3 ms -> 11.4 ms at
+                                        // config 5 against 8 waves, EXPERIMENTS.md)
 constexpr int OPP_TB = OPP_R / OPP_NW;  // range tasks per wave in the parallel passes
 constexpr int OPP_MAXT = 2 * OPP_MAXW;  // touched hosts: inherited + own
 constexpr int OPP_HASH_BITS = 11;
@@ -166,9 +168,11 @@ struct OppLDS {
   uint32_t mt[625];
   uint32_t mtb[625];            // state at the range start
   int32_t pl[OPP_MAXW];         // placements of the window, written out when the walk ends
-  int32_t wl[OPP_NW][OPP_TB][WAVE];   // per wave and task: its lost hosts (pass 1)
   int32_t lhist[OPP_NW][WAVE];  // per wave: a task's lost hosts per super-chunk (pass 3)
-  uint64_t lclr[OPP_NW][OPP_SUP][OPP_CH / WAVE];   // per wave: lost bits of the drawn super-chunk
+  union {                       // (pass 1 reads wl into registers before pass 3 uses lclr)
+    int32_t wl[OPP_NW][OPP_TB][WAVE];                // per wave and task: its lost hosts (pass 1)
+    uint64_t lclr[OPP_NW][OPP_SUP][OPP_CH / WAVE];   // per wave: lost bits of the drawn super-chunk
+  };
   int32_t ctl[4];               // next range start, touched count
 };
 
