@@ -152,7 +152,7 @@ struct pvt_ctx {
   // scratch
   Buf gcnt, goff, gskey, gsidx;   // grouped order: counts, offsets + cursors, scattered pairs
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, grp_ord, csum, bsum, key,
-      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, kskey, kperm, kiota, ksorttmp, kflag;
+      seg, seg_feas, l_e[2], l_ids[2], l_t[2], next, opp, pkg, owned[2], rdesc, rmt, anc_scr, oppfault, kskey, kperm, kiota, ksorttmp, kflag;
   int pipeline = 1;               // overlap scoring of window k+1 with the walk of window k
   int keyed_scan = 1;             // keyed first-fit: sorted host order + early-exit scan
   int score_tw = 0;               // score kernel tasks per wave (0: policy default; 2 or 4)
@@ -166,6 +166,13 @@ struct pvt_ctx {
   Buf fwin;                               // host-sharded frontier walks: merged windows
   int band_min = BAND_MIN_HOSTS;          // vbp best-fit band lists from this many hosts (0: off)
   int lwalk = 1;                          // vbp best-fit windows: the one-wave list walk
+  // tuning / A-B knobs, read from the environment once, at pvt_ctx_create (never per round):
+  int t_segments = 0;             // PVT_SEGMENTS: score-pass host segments (0: by policy)
+  int t_band_segs = 0;            // PVT_BAND_SEGS: vbp best-fit band list segments (0: default)
+  int t_keyed_scan = -1;          // PVT_KEYED_SCAN: keyed first-fit scan on / off (-1: keyed_scan)
+  int t_of_hosts = 0;             // PVT_OF_HOSTS: ordered frontier host span (0: default)
+  int t_epoch_plan = 1;           // PVT_EPOCH_PLAN: 0 = epoch chains by distinct zone only
+  int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
@@ -323,6 +330,12 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_OF_TASKS")) ctx->of_tasks = std::max(32, atoi(e));   // tuning
   if (const char* e = getenv("PVT_BAND")) ctx->band_min = std::max(0, atoi(e));       // A/B
   if (const char* e = getenv("PVT_LWALK")) ctx->lwalk = atoi(e) != 0;                  // A/B
+  if (const char* e = getenv("PVT_SEGMENTS")) ctx->t_segments = std::max(1, atoi(e));  // tuning
+  if (const char* e = getenv("PVT_BAND_SEGS")) ctx->t_band_segs = atoi(e);             // tuning
+  if (const char* e = getenv("PVT_KEYED_SCAN")) ctx->t_keyed_scan = atoi(e) != 0;      // A/B
+  if (const char* e = getenv("PVT_OF_HOSTS")) ctx->t_of_hosts = std::max(ZW_M, atoi(e));   // tuning
+  if (const char* e = getenv("PVT_EPOCH_PLAN")) ctx->t_epoch_plan = atoi(e);           // A/B
+  if (const char* e = getenv("PVT_MERGE_SMALL")) ctx->t_merge_bitonic = atoi(e) == 0;  // A/B
   *out = ctx;
   return PVT_OK;
 }
@@ -337,7 +350,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->grp_ord, &ctx->csum, &ctx->bsum, &ctx->key,
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
-                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->kskey, &ctx->kperm, &ctx->kiota,
+                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->oppfault, &ctx->kskey, &ctx->kperm, &ctx->kiota,
                  &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
                  &ctx->btcnt, &ctx->bsorttmp, &ctx->brow[0], &ctx->brow[1], &ctx->brdem[0],
@@ -468,7 +481,7 @@ static constexpr size_t SEG_ENTRIES_MAX = (size_t)MAX_WINDOW * MAX_SEG * KL;
 // about KL * (1 + ln(H / (S * KL))) serial insertions per segment, S times per task. Fewer,
 // longer segments halve those insertions at 16 (measured: 29.7 -> 26.2 ms of score per
 // 1M x 10k round); cost_aware's zero-cost zone fills its lists at once and wants the waves.
-static int choose_segments(int H, int nt, int mode, int force_tw, bool epoch) {
+static int choose_segments(int H, int nt, int mode, int force_tw, bool epoch, int force_S) {
   const int tw = score_tasks_per_wave(mode, H, force_tw);
   const int task_waves = (nt + tw - 1) / tw;
   int S = (4096 + task_waves - 1) / task_waves;
@@ -479,7 +492,7 @@ static int choose_segments(int H, int nt, int mode, int force_tw, bool epoch) {
   // (config 5 ca_bf epoch of 10k tasks: S = 2 -> 5.6 ms, 4 -> 4.1, 8 -> 4.8; S = 2 refills;
   // config 3, 1k tasks: 8 -> 0.82 ms, 4 -> 0.73)
   if (mode == PVT_CA_BF && epoch) S = 4;
-  if (const char* e = getenv("PVT_SEGMENTS")) S = std::max(1, atoi(e));   // tuning experiments
+  if (force_S > 0) S = force_S;   // (PVT_SEGMENTS, read at context creation)
   S = std::min(S, std::max(1, H / 4096));
   S = std::min(S, std::max(MAX_SEG, (int)(SEG_ENTRIES_MAX / ((size_t)nt * KL))));
   S = std::max(1, std::min(S, 256));
@@ -650,8 +663,8 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   const size_t tl_bytes = pipe ? sizeof(OppTouched) : 0;
   const size_t slot = (bm_bytes + sc_bytes + tl_bytes + 255) / 256 * 256;
   ENSURE(ctx->opp, slot * nbuf + sizeof(uint32_t) * 640);
-  ENSURE(ctx->anc_scr, 16);
-  int32_t* fault = P<int32_t>(ctx->anc_scr);
+  ENSURE(ctx->oppfault, 16);
+  int32_t* fault = P<int32_t>(ctx->oppfault);
   HIPCHK(hipMemsetAsync(fault, 0, sizeof(int32_t), st));
   char* base = reinterpret_cast<char*>(ctx->opp.p);
   auto bm_of = [&](int b) { return reinterpret_cast<uint64_t*>(base + slot * b); };
@@ -719,8 +732,7 @@ static int band_snapshot(pvt_ctx* ctx) {
   size_t tmp = 0;
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, k0, k0 + n, i0, i0 + n, n, 0, 64, st));
   ENSURE(ctx->bsorttmp, tmp);
-  int bs = BAND_SEGS;
-  if (const char* e = getenv("PVT_BAND_SEGS")) bs = atoi(e);   // tuning (2, 4, 8, 16, 32)
+  const int bs = ctx->t_band_segs ? ctx->t_band_segs : BAND_SEGS;   // (PVT_BAND_SEGS: 2 ... 32)
   R.band_S = (bs == 1 || bs == 2 || bs == 4 || bs == 8 || bs == 16 || bs == 32) ? bs : BAND_SEGS;
   Scope sc(ctx, PVT_K_OTHER, 0, 0);
   launch_band_keys(r->avail, R.H, R.lo, n, k0, i0, st);
@@ -821,7 +833,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
     ENSURE(ctx->key, sizeof(double) * H);
     ENSURE(ctx->next, sizeof(int32_t) * 4);
     R.kscan = ctx->keyed_scan != 0;
-    if (const char* e = getenv("PVT_KEYED_SCAN")) R.kscan = atoi(e) != 0;   // A/B experiments
+    if (ctx->t_keyed_scan >= 0) R.kscan = ctx->t_keyed_scan != 0;   // (PVT_KEYED_SCAN)
     if (R.kscan && hi > lo) {
       const int n = hi - lo;
       ENSURE(ctx->kskey, sizeof(uint64_t) * 2 * (size_t)std::max(n, 1));
@@ -850,7 +862,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   R.kf_pending = false;
   if (R.ofront) {
     R.ofh = ORDERED_FRONTIER_HOSTS;
-    if (const char* e = getenv("PVT_OF_HOSTS")) R.ofh = std::max(ZW_M, atoi(e));   // tuning
+    if (ctx->t_of_hosts) R.ofh = ctx->t_of_hosts;   // (PVT_OF_HOSTS)
     ENSURE(ctx->next, sizeof(int32_t) * 4);
     ENSURE(ctx->kperm, sizeof(int32_t) * (size_t)H);
     ENSURE(ctx->kiota, sizeof(int32_t) * (size_t)H);
@@ -1064,11 +1076,11 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
       launch_band_score(ba, st);
     }
     MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_l,
-                 anc_w, R.ord + t0, R.H, nt, S, KL, L, nt_dev};
+                 anc_w, R.ord + t0, R.H, nt, S, KL, L, nt_dev, ctx->t_merge_bitonic};
     Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
     launch_merge(ma, st);
   } else {
-    const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw, R.in_epoch);
+    const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw, R.in_epoch, ctx->t_segments);
     ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)nt * S * KL);
     ENSURE(ctx->seg_feas, sizeof(int32_t) * (size_t)nt * S);
     ScoreArgs sa{r->avail, r->zone, r->tiebreak, R.keyed ? P<double>(ctx->key) : nullptr,
@@ -1080,7 +1092,7 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
       launch_score(r->mode, sa, st);
     }
     MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
-                 anc_w, R.ord + t0, R.H, nt, S, KL, L};
+                 anc_w, R.ord + t0, R.H, nt, S, KL, L, nullptr, ctx->t_merge_bitonic};
     Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
     launch_merge(ma, st);
   }
@@ -1340,8 +1352,7 @@ static int epoch_groups(pvt_ctx* ctx) {
   R.ecomp.resize(Z);
   for (int z = 0; z < Z; z++) R.ecomp[z] = z;
   auto root = [&](int z) { while (R.ecomp[z] != z) z = R.ecomp[z] = R.ecomp[R.ecomp[z]]; return z; };
-  int plan = 1;
-  if (const char* e = getenv("PVT_EPOCH_PLAN")) plan = atoi(e);   // 0: distinct zones only
+  const int plan = ctx->t_epoch_plan;   // (PVT_EPOCH_PLAN=0: distinct zones only)
   for (int a = 0; a < Z && plan; a++)
     for (int z = 0; z < Z; z++)
       if (cost[(size_t)a * Z + z] + cost[(size_t)z * Z + a] == 0.0) R.ecomp[root(a)] = root(z);
@@ -1494,7 +1505,7 @@ static int place_epochs(pvt_ctx* ctx) {
                    P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                    P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
                    P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
-                   nullptr, 0, 0, 0, nullptr, nullptr};
+                   nullptr, 0, 0, 0, nullptr, nullptr, nullptr, dev + EP_CSOFF, dev + EP_CSEG};
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0);
         launch_zwalk(za, nch, st);
@@ -1779,8 +1790,8 @@ static int opp_shard_begin(pvt_ctx* ctx, const pvt_round* r, int lo, int hi, int
     uint32_t* mt = reinterpret_cast<uint32_t*>(P<char>(ctx->opp) + opp_table_bytes(R));
     HIPCHK(hipMemcpyAsync(mt, r->mt_state, sizeof(uint32_t) * 625, hipMemcpyHostToDevice, st));
   }
-  ENSURE(ctx->anc_scr, 16);
-  HIPCHK(hipMemsetAsync(ctx->anc_scr.p, 0, sizeof(int32_t), st));   // the walks' fault word
+  ENSURE(ctx->oppfault, 16);
+  HIPCHK(hipMemsetAsync(ctx->oppfault.p, 0, sizeof(int32_t), st));   // the walks' fault word
   R.active = true;
   return PVT_OK;
 }
@@ -1793,7 +1804,7 @@ static int opp_shard_score(pvt_ctx* ctx, void* package, int32_t* n_tasks_out, in
       uint32_t* mt = reinterpret_cast<uint32_t*>(P<char>(ctx->opp) + opp_table_bytes(R));
       HIPCHK(hipMemcpyAsync(R.r.mt_state, mt, sizeof(uint32_t) * 625, hipMemcpyDeviceToHost, st));
     }
-    HIPCHK(hipMemcpyAsync(ctx->next_host + 3, ctx->anc_scr.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ctx->next_host + 3, ctx->oppfault.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     R.active = false;
     if (ctx->next_host[3])
@@ -1838,7 +1849,7 @@ static int opp_shard_commit(pvt_ctx* ctx, const void* packages) {
   }
   OppCommitArgs oa{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, bm, sc, R.H, nt, R.opp_nq,
                    R.opp_nsq, R.opp_W, r->placement + t0, mt, ctx->stamps, nullptr, nullptr, 1,
-                   P<int32_t>(ctx->anc_scr)};
+                   P<int32_t>(ctx->oppfault)};
   {
     Scope s(ctx, PVT_K_COMMIT, 0, 0);
     launch_opp_commit(oa, st);
@@ -2032,7 +2043,7 @@ static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
                  P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                  P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
                  P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
-                 nullptr, 0, 0, 0, nullptr, nullptr, win};
+                 nullptr, 0, 0, 0, nullptr, nullptr, win, dev + EP_CSOFF, dev + EP_CSEG};
     {
       Scope sc(ctx, PVT_K_COMMIT, 0, 0);
       launch_zwalk(za, nch, st);
@@ -2193,7 +2204,7 @@ extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
   lists_from(ctx, L, lb);
   MergeArgs ma{reinterpret_cast<const SegEntry*>(packages), nullptr, R.r.avail, R.r.zone,
                P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
-               R.ord + t0, R.H, nt, R.world, PK, L};
+               R.ord + t0, R.H, nt, R.world, PK, L, nullptr, ctx->t_merge_bitonic};
   {
     Scope sc(ctx, PVT_K_MERGE, 0, 0);
     launch_merge(ma, ctx->stream);

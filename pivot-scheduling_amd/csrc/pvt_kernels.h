@@ -98,6 +98,7 @@ struct MergeArgs {
   int SL;                 // entries per source list (KL, or the package depth)
   Lists L;
   const int32_t* nt_dev;  // or NULL: only tasks [0, *nt_dev) (vbp best-fit representative lists)
+  int bitonic;            // 1: the bitonic merge_kernel always (A/B; PVT_MERGE_SMALL=0 at ctx create)
 };
 
 // Host-dimension sharding: a rank's exact local lists -> its exchange package (see MergeArgs).
@@ -230,6 +231,11 @@ struct ZwalkArgs {
   // host-sharded rounds: the merged window of chain b (keyed / ordered: of the walk) -- hosts
   // in index order with their capacities, as the unsharded walk builds it -- or NULL (build it)
   const struct FrontierSlot* pwin;
+  // chain mode: chain b's group segments start at chain-local positions cseg[csoff[b] ..
+  // csoff[b+1]) (a run of equal demands never crosses one: finality and apply work per
+  // segment, so every segment's last copy on a host must be logged); NULL in keyed mode
+  const int32_t* csoff;
+  const int32_t* cseg;
 };
 constexpr int ZW_MIN_PARTS = 256;
 // per-dimension minima of avail over hosts [lo, hi) into part[ZW_MIN_PARTS][4]

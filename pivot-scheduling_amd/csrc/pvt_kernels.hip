@@ -592,10 +592,7 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
 }
 
 void launch_merge(const MergeArgs& a, hipStream_t st) {
-  static const int small = [] {
-    const char* e = getenv("PVT_MERGE_SMALL");   // A/B experiments: 0 = bitonic merge always
-    return e ? atoi(e) : 1;
-  }();
+  const bool small = !a.bitonic;
   if (small && a.seg_feas != nullptr && a.SL == KL && a.S <= MERGE_SMALL_S)
     hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
   else if (small && a.seg_feas == nullptr && (size_t)a.S * a.SL <= LMAX)

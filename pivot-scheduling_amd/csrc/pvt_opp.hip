@@ -169,7 +169,12 @@ struct OppLDS {
   uint32_t mtb[625];            // state at the range start
   int32_t pl[OPP_MAXW];         // placements of the window, written out when the walk ends
   int32_t lhist[OPP_NW][WAVE];  // per wave: a task's lost hosts per super-chunk (pass 3)
-  union {                       // (pass 1 reads wl into registers before pass 3 uses lclr)
+  // wl and lclr overlap ACROSS waves (with OPP_NW = 16, wave w's lclr covers the wl rows of
+  // waves 2w and 2w + 1), not only within a wave. That is safe only because of the block
+  // barriers between pass 1 (every wave reads its wl rows into registers) and pass 3 (lclr
+  // written), and at the end of each range (before the next pass 1 writes wl): an edit that
+  // removes or moves one of those __syncthreads lets one wave clobber another's lost-host list.
+  union {
     int32_t wl[OPP_NW][OPP_TB][WAVE];                // per wave and task: its lost hosts (pass 1)
     uint64_t lclr[OPP_NW][OPP_SUP][OPP_CH / WAVE];   // per wave: lost bits of the drawn super-chunk
   };

@@ -58,6 +58,7 @@ struct ZwalkLDS {
   double smin[ZW_SB][4];                   // suffix minima of the demands, per 64-task batch
   double lg[64][4];                        // the batch's log: capacities after each commit
   int32_t lgid[64];                        //   and the host
+  uint64_t sbits[CHAIN_MAX / 64];          // chain mode: bit i = a group segment starts at task i
   uint32_t amask[ZMAX];                    // anchor -> its zero-cost zones
   uint32_t umask;
   int32_t nwin, bail;
@@ -192,11 +193,18 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   if (!KEYED)   // (keyed / ordered rounds: no zone tables; vbp rounds have none)
     for (int i = tid; i < Z * Z; i += ZW_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
   if (tid == 0) { S.umask = 0; S.nwin = 0; S.bail = 0; }
+  if (tid < CHAIN_MAX / 64) S.sbits[tid] = 0;
   __syncthreads();
   if (!KEYED && tid < Z) {                   // anchor row -> zero-cost zone mask
     uint32_t m = 0;
     for (int z = 0; z < Z; z++) m |= (S.csum[tid * Z + z] == 0.0) ? (1u << z) : 0u;
     S.amask[tid] = m;
+  }
+  if (!KEYED && A.cseg) {                    // segment starts (chain-local positions)
+    for (int k = A.csoff[b] + tid; k < A.csoff[b + 1]; k += ZW_THREADS) {
+      const int p = A.cseg[k];
+      if (p > 0 && p < CHAIN_MAX) atomicOr(&S.sbits[p >> 6], 1ull << (p & 63));
+    }
   }
   __syncthreads();
 
@@ -286,7 +294,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #pragma unroll
   for (int r = 0; r < 4; r++) sep |= (ha[r] - mx[r] >= 0x1p-288);
   const uint32_t U = S.umask;
-  if (S.bail || !sep || nt <= 0) {
+  if (S.bail || !sep || nt <= 0 || (!KEYED && nt > CHAIN_MAX)) {
     if (tid == 0) { status[0] = 0; status[1] = (KEYED || nt <= 0) ? 0 : 1; }
     return;
   }
@@ -557,6 +565,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       for (int r = 0; r < 4; r++)
         same &= __double_as_longlong(__shfl_up(td[r], 1)) == __double_as_longlong(td[r]);
       E = __ballot(same);
+      // (chain mode: a run stops at a group segment start -- pass 2 logs a host's capacities
+      // at its last copy of the run only, and the segment before must hold its own last copy)
+      if (!KEYED && A.cseg) E &= ~rfl_u64(S.sbits[i0 >> 6]);
     }
     auto run_len = [&](int k) { return k < 63 ? min(kn - k, 1 + __builtin_ctzll(~(E >> (k + 1)))) : 1; };
     // The run step, for a task k of a uniform batch that the register chunk p0 cannot take: its

@@ -97,24 +97,20 @@ class _ClusterTables:
         else:
             self.cost = np.zeros((1, 1))
             self.bw = np.ones((1, 1))
-        self._routes = {}
 
     def routes_of(self, cluster, anchor):
         """(in routes, out routes) between storage ``anchor`` and every host, in host order,
-        looked up once per cluster (the route objects are the cluster's own; their queues are
-        read when a round needs their realtime bandwidth). A missing route raises what the
-        reference's host_score_func raises reading it (cost_aware.py:73-79, 106-112)."""
-        if getattr(self, "_routes_cluster", None) is not cluster:
-            self._routes, self._routes_cluster = {}, cluster
-        got = self._routes.get(anchor.id)
-        if got is None:
-            get_route = cluster.get_route
-            ins = [get_route(anchor.id, h) for h in self.host_ids]
-            outs = [get_route(h, anchor.id) for h in self.host_ids]
-            if any(x is None for x in ins) or any(x is None for x in outs):
-                raise AttributeError("'NoneType' object has no attribute 'realtime_bw'")
-            got = self._routes[anchor.id] = (ins, outs)
-        return got
+        looked up afresh in every schedule() call (the caller memoises per call): the
+        reference's cluster.add_route may replace a (src, dst) route between rounds
+        (resources/__init__.py:106-109), and its get_route then returns the new object. A
+        missing route raises what the reference's host_score_func raises reading it
+        (cost_aware.py:73-79, 106-112)."""
+        get_route = cluster.get_route
+        ins = [get_route(anchor.id, h) for h in self.host_ids]
+        outs = [get_route(h, anchor.id) for h in self.host_ids]
+        if any(x is None for x in ins) or any(x is None for x in outs):
+            raise AttributeError("'NoneType' object has no attribute 'realtime_bw'")
+        return ins, outs
 
     def matches(self, cluster):
         hosts = cluster.hosts
@@ -219,7 +215,7 @@ class CostAwarePlacement(PlacementMixin):
         """realtime_bw=True (cost_aware.py:73-79, :106-112): per host, the bandwidth the
         reference's host_score_func uses, in_route.realtime_bw + out_route.realtime_bw of the
         routes between the anchor storage and the host (resources/network.py:70-73), read from
-        the cluster's own route objects (looked up once per cluster) and summed elementwise in
+        the cluster's own route objects (looked up once per call) and summed elementwise in
         the reference's order. Queues do not move inside schedule(), so groups sharing an
         anchor share the row."""
         row = memo.get(anchor.id)

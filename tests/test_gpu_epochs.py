@@ -199,3 +199,34 @@ def test_zero_walk_tiny_egress_costs(engine, zero_walk):
     ref = oracle.place(r, threads=8)
     res, _ = _place(engine, r)
     _same(res, ref)
+
+
+def test_zero_walk_run_stops_at_segment_start(engine, zero_walk):
+    """Two groups anchored in zone 0 walk in one chain, back to back in one 64-task batch, with
+    the same demand: the frontier walk's run of equal demands must stop at the second group's
+    start (a host whose copies straddle the boundary logs its capacities after the first group's
+    last copy). The group between them (zone 1, no capacity there) leaves its chain unproven, so
+    the epoch accepts the first group only and applies that group's final entries."""
+    H = 4000
+    r = synthetic.make_round(_abi.PVT_CA_BF, H, 77, seed=17)
+    cost = np.full((20, 20), 0.01)
+    np.fill_diagonal(cost, 0.0)
+    r.cost = cost
+    r.avail[0, :] = 16.0
+    r.avail[1, :] = 131072.0
+    r.avail[2, :] = 100.0
+    r.avail[3, :] = 1.0
+    z0 = r.zone == 0
+    r.avail[0, z0] = 4.0        # four copies of (1, 1000) per zone-0 host: 42 = 10 x 4 + 2
+    r.avail[1, z0] = 4000.0
+    r.avail[:2, r.zone == 1] = 0.0
+    r.dem[:, :] = 0.0
+    r.dem[0, :] = 1.0
+    r.dem[1, :] = 1000.0
+    r.task_group = np.array([0] * 42 + [1] * 5 + [2] * 30, dtype=np.int32)
+    r.group_anchor = np.array([0, 1, 0], dtype=np.int32)
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    if zero_walk:
+        assert st["frontier_chains"] > 0, st

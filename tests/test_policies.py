@@ -122,3 +122,20 @@ def test_realtime_rows_shared_by_anchor():
     want = [cluster.get_route(a.id, h.id).realtime_bw + cluster.get_route(h.id, a.id).realtime_bw
             for h in cluster.hosts]
     assert row.tolist() == want
+
+
+def test_realtime_rows_see_replaced_routes():
+    """A route replaced between rounds (the reference's cluster.add_route overwrites the
+    (src, dst) entry, resources/__init__.py:106-109) is read in the next round: routes are
+    looked up per schedule() call, never cached across rounds."""
+    case, run = _rt_case()
+    cluster, tasks = fakes.build(case)
+    sched = policies.CostAwareGlobalScheduler(None, cluster, seed=run["seed"], **run["kwargs"])
+    a, h0 = cluster.storage[0], cluster.hosts[0]
+    first = sched._realtime_row(a, {})
+    old = cluster.get_route(a.id, h0.id)
+    cluster._routes[(a.id, h0.id)] = fakes.Route(old.bw, old.realtime_bw * 0.5 + 1.0)
+    second = sched._realtime_row(a, {})
+    assert second[0] == (old.realtime_bw * 0.5 + 1.0) + cluster.get_route(h0.id, a.id).realtime_bw
+    assert second[0] != first[0]
+    assert second[1:].tolist() == first[1:].tolist()
