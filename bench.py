@@ -72,6 +72,8 @@ def parse():
                         "placed by ONE pvt_place_batch launch per step (resident kernel)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=10.0,
                    help="target CPU time of the oracle baseline sample (0 = skip)")
+    p.add_argument("--extra-cpu-seconds", type=float, default=3.0,
+                   help="target CPU time of each extra line's oracle baseline sample")
     p.add_argument("--parity", type=int, default=1, help="1: check the placed round against the oracle")
     p.add_argument("--extra", type=int, default=-1,
                    help="1: also time (and parity-check) the other policies at config 5 and all "
@@ -79,6 +81,11 @@ def parse():
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="N > 1: torch.distributed backend (nccl = RCCL over xGMI; gloo: ranks may "
                         "share a GPU, e.g. to rehearse the multi-rank path on one card)")
+    p.add_argument("--c4-batch", type=int, default=512,
+                   help="N > 1: also run BASELINE config 4 as written -- this many independent "
+                        "1000-host x 1000-task scenarios per rank (512 x 8 = 4096 at N = 8), one "
+                        "pvt_place_batch launch per step, barrier + MAX-over-ranks timing, parity "
+                        "of every rank's scenarios against the oracle (0 = off)")
     p.add_argument("--replay", type=int, default=-1,
                    help="1: also time BASELINE configs 1 and 2 -- every schedule() round of the "
                         "recorded reference simulations through the drop-in policy classes; -1 "
@@ -161,8 +168,24 @@ def check_parity(got, r, ref=None):
 KCLASSES = (("score", 0), ("merge", 1), ("commit", 2), ("other", 3))
 
 
+# the kernels of the path that can dominate a step, timed one by one (pvt_get_kernel_kstats)
+WALK_KERNELS = ("zwalk_kernel", "commit_kernel", "lwalk_kernel", "opp_commit_kernel")
+PAR_KERNELS = ("score_kernel", "band_score_kernel", "opp_count_kernel", "perm_scan_kernel",
+               "ordered_kernel", "resident_kernel", "merge_kernel", "merge_small_kernel",
+               "merge_pkg_kernel")
+
+
 def kstats_all(eng):
     return {name: eng.kstats(k) for name, k in KCLASSES}
+
+
+def kernel_times(eng):
+    out = {}
+    for name in WALK_KERNELS + PAR_KERNELS:
+        k = eng.kernel_kstats(name)
+        if k["launches"]:
+            out[name] = k
+    return out
 
 
 def time_round(eng, r, steps, warmup, batch=None):
@@ -186,6 +209,7 @@ def time_round(eng, r, steps, warmup, batch=None):
     ms = (time.perf_counter() - t0) * 1e3 / steps
     eng.set_profiling(False)
     ks = kstats_all(eng)
+    ks["kernels"] = kernel_times(eng)
     return ms, (dr.results() if batch else dr.result()), ks
 
 
@@ -212,34 +236,124 @@ def extra_workloads(eng, args, skip_mode):
     jobs.append(("c5_ca_bf_loaded", MODES["ca_bf"], DEFAULT_H, DEFAULT_T, "loaded"))
     jobs += [("c3_%s" % m, MODES[m], 100_000, 1000, None) for m in MODES]
     jobs += [("c4_%s" % m, MODES[m], 1000, 1000, "batch") for m in MODES]
+    threads = oracle_threads()
     for tag, mode, H, T, kind in jobs:
         if kind == "batch":
             B = 512
             rounds = [synthetic.make_round(mode, H, T, seed=args.seed + s) for s in range(B)]
             ms, got, ks = time_round(eng, None, steps, warm, batch=rounds)
-            ok = (all(same_result(g, oracle.place(x)) for g, x in zip(got, rounds))
-                  if args.parity else None)
+            ep = eng.epoch_stats()
             cand = float(B) * T * H
+            cpu, refs = batch_cpu_baseline(rounds, threads)
+            ok = all(same_result(g, x) for g, x in zip(got, refs)) if args.parity else None
         else:
             B = 0
             r = loaded_round(args.seed) if kind == "loaded" else synthetic.make_round(mode, H, T, seed=args.seed)
             ms, got, ks = time_round(eng, r, steps, warm)
-            ok = check_parity(got, r) if args.parity else None
+            ep = eng.epoch_stats()
             cand = float(T) * H
-        ep = eng.epoch_stats()
+            cpu, ref = round_cpu_baseline(r, threads, args.extra_cpu_seconds)
+            ok = check_parity(got, r, ref) if args.parity else None
         e = {"value": cand / (ms * 1e-3), "ms_per_step": ms, "hosts": H, "tasks": T, "steps": steps,
-             "parity": ok, "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items()}}
+             "parity": ok, "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items()
+                                                   if k != "kernels"},
+             "kernel_ms_per_step": {k: v["ms"] / steps for k, v in ks["kernels"].items()}}
         if B:
             e["scenarios"] = B
         if mode == MODES["ca_bf"] and not B:
             e["frontier_chains_per_step"] = ep["frontier_chains"]
             e["list_chains_per_step"] = ep["list_chains"]
-        rl = extra_roofline(tag, mode, H, T, ks, steps)
-        if rl is not None:
-            e["roofline"] = rl
+        variant = "_b%d" % B if B else ("_loaded" if kind == "loaded" else "")
+        e["roofline"] = dominant_roofline(mode, H, T, ks, ep, steps, variant=variant,
+                                          rounds_per_step=B or 1, warm=warm)
+        e["cpu_baseline"] = cpu
         out[tag] = e
-        log("[rank 0] extra %s: %.3e cand/s, %.2f ms, parity %s" % (tag, e["value"], ms, ok))
+        log("[rank 0] extra %s: %.3e cand/s, %.2f ms, parity %s, roofline %s frac %s, cpu %.3e"
+            % (tag, e["value"], ms, ok, e["roofline"].get("kernel"), e["roofline"].get("frac"),
+               cpu["value"]))
     return out
+
+
+def round_cpu_baseline(r, threads, budget_s):
+    """CPU baseline of one extra round: the C restatement on all the job's cores over the WHOLE
+    round when that fits the budget (the same run is the parity reference), else over a
+    bounded sample of its first tasks; 1 thread on a sample beside it."""
+    v_all, n_all, dt_all, res_all = _time_oracle(r, budget_s, threads)
+    v_one, n_one, dt_one, _ = _time_oracle(r, budget_s / 3.0, 0)
+    out = {"value": v_all, "unit": "candidates/s", "cores": threads, "kind": "port",
+           "value_1thread": v_one,
+           "sample": "oracle/pivot_oracle.c (naive T x H scan, OpenMP host scans over %d threads) "
+                     "on %s x %d hosts (%.2f s); 1 thread: first %d tasks (%.2f s)"
+                     % (threads, "all %d tasks" % n_all if n_all >= r.n_tasks else
+                        "the first %d tasks" % n_all, r.n_hosts, dt_all, n_one, dt_one)}
+    return out, (res_all if n_all >= r.n_tasks else None)
+
+
+def batch_cpu_baseline(rounds, threads):
+    """CPU baseline of a scenario batch (config 4): every scenario through the C restatement,
+    one scenario per thread on all the job's cores (ctypes releases the GIL), the whole batch;
+    then the first scenarios on 1 thread. Returns (baseline, the per-scenario results)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle
+    cand = float(sum(r.n_tasks * r.n_hosts for r in rounds))
+    t = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=max(threads, 1)) as ex:
+        refs = list(ex.map(lambda x: oracle.place(x, threads=0), rounds))
+    dt_all = max(time.perf_counter() - t, 1e-6)
+    n1 = max(1, len(rounds) // 16)
+    t = time.perf_counter()
+    for x in rounds[:n1]:
+        oracle.place(x, threads=0)
+    dt_one = max(time.perf_counter() - t, 1e-6)
+    c1 = float(sum(r.n_tasks * r.n_hosts for r in rounds[:n1]))
+    out = {"value": cand / dt_all, "unit": "candidates/s", "cores": threads, "kind": "port",
+           "value_1thread": c1 / dt_one,
+           "sample": "oracle/pivot_oracle.c on all %d scenarios, one scenario per thread over %d "
+                     "threads (%.2f s); 1 thread: the first %d scenarios (%.2f s)"
+                     % (len(rounds), threads, dt_all, n1, dt_one)}
+    return out, refs
+
+
+def scenario_batch_line(eng, args, rank, world, gloo, B, H=1000, T=1000):
+    """BASELINE config 4 as written, on every rank of an N-GPU job: B independent scenarios per
+    rank (seeds seed + rank * B + s; H hosts x T tasks each), placed by ONE pvt_place_batch launch
+    per step (resident kernel), timed between barriers with the MAX over ranks, no collective on
+    the data path (reference fan-out: alibaba/sim.py:187-195, runner.py:13-52). Parity: every rank
+    checks its own scenarios against the oracle; the flags are reduced with a MIN. Returns the
+    line on rank 0 (None elsewhere)."""
+    import torch
+    import torch.distributed as dist
+    from oracle import oracle
+    from pivot_place import synthetic
+    mode = MODES[args.mode]
+    steps, warm = max(1, min(args.steps, 5)), 1
+    rounds = [synthetic.make_round(mode, H, T, seed=args.seed + rank * B + s) for s in range(B)]
+    if world > 1:
+        dist.barrier()
+    ms, got, ks = time_round(eng, None, steps, warm, batch=rounds)   # (this rank's own clock)
+    if world > 1:
+        dist.barrier()
+    ok = all(same_result(g, oracle.place(x)) for g, x in zip(got, rounds)) if args.parity else True
+    if world > 1:
+        dev = "cpu" if gloo else eng.device
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+        f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        ok = bool(f.item())
+    if rank != 0:
+        return None
+    cand = float(B) * world * T * H
+    return {"workload": "BASELINE config 4: %d independent scenarios (%d per GPU) x %d hosts x %d "
+                        "tasks, %s, one pvt_place_batch launch per GPU per step, scenario-sharded "
+                        "(no data-path collective)" % (B * world, B, H, T, POLICY[args.mode]),
+            "value": cand / (ms * 1e-3), "unit": "candidates/s", "ms_per_step": ms,
+            "n_gpus": world, "scenarios": B * world, "scenarios_per_gpu": B, "hosts": H,
+            "tasks": T, "steps": steps, "scaling": "weak", "timing": "max over ranks of each "
+            "rank's timed steps, between barriers", "parity": (ok if args.parity else None),
+            "parity_scope": "every rank's scenarios vs the oracle (MIN-reduced)",
+            "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items()}}
 
 
 # ---------------------------------------------------------------------------- roofline
@@ -267,11 +381,12 @@ def lib_sha256():
     return _SHA[0]
 
 
-def pmc_entry(mode, H, T, kernel):
-    """(PMC entry, note): the counter profile of ``kernel`` on this config, if it was collected
-    on THIS binary."""
+def pmc_entry(mode, H, T, kernel, variant=""):
+    """(PMC entry, note): the counter profile of ``kernel`` on this config (variant "_b512": a
+    512-scenario batch of H x T rounds; "_loaded": the loaded config-5 round), if it was
+    collected on THIS binary."""
     name = [k for k, v in MODES.items() if v == mode][0]
-    key = "%s_%d_%d:%s" % (name, H, T, kernel)
+    key = "%s_%d_%d%s:%s" % (name, H, T, variant, kernel)
     try:
         with open(PMC_INDEX) as f:
             e = json.load(f).get("entries", {}).get(key)
@@ -286,14 +401,13 @@ def pmc_entry(mode, H, T, kernel):
     return e, None
 
 
-def score_roofline(mode, H, T, ks, kernel):
-    """A parallel candidate pass (streaming score, band score or resident kernel): its PMC
-    per-launch work (VALU busy cycles, LDS-array cycles, DRAM bytes) over the launch time
-    measured here with HIP events on the launch's stream; the bound is the most utilised
-    resource. The SURVEY §8(d) 36 / 32 B per logical candidate is kept as hbm_equivalent_*:
-    what a per-task streaming scan would move, not what moves."""
+def score_roofline(mode, H, T, k, kernel, variant=""):
+    """A parallel pass (streaming score, band score, count pass, merge or the resident kernel):
+    its PMC per-launch work (VALU busy cycles, LDS-array cycles, DRAM bytes) over the launch time
+    measured here with HIP events on the launch's stream (``k``: that kernel's own timing); the
+    bound is the most utilised resource. The SURVEY §8(d) 36 / 32 B per logical candidate is
+    kept as hbm_equivalent_*: what a per-task streaming scan would move, not what moves."""
     from pivot_place import _abi
-    k = ks["score"]
     launches = max(k["launches"], 1)
     avg_ms = k["ms"] / launches
     out = {"kernel": kernel, "avg_launch_ms": avg_ms, "launches": k["launches"],
@@ -301,7 +415,7 @@ def score_roofline(mode, H, T, ks, kernel):
            "hbm_equivalent_GBs": (k["bytes"] / launches / (avg_ms * 1e-3) / 1e9) if avg_ms > 0 else 0.0,
            "hbm_equivalent_bytes_per_candidate": _abi.BYTES_PER_CANDIDATE[mode],
            "bound": None, "achieved": None, "peak": None, "unit": None, "frac": None, "traffic": None}
-    pmc, note = pmc_entry(mode, H, T, kernel)
+    pmc, note = pmc_entry(mode, H, T, kernel, variant)
     if pmc is None or avg_ms <= 0:
         out["note"] = note or "no launch timed"
         return out
@@ -319,7 +433,8 @@ def score_roofline(mode, H, T, ks, kernel):
     return out
 
 
-def walk_roofline(mode, H, T, ks, ep, steps, kernel="zwalk_kernel"):
+def walk_roofline(mode, H, T, c, ep, steps, kernel="zwalk_kernel", variant="", rounds_per_step=1,
+                  warm=0):
     """A sequential walk (the frontier walk, the list commit walk, the opportunistic walk): each
     task reads the capacities the previous commit wrote, so the chain is one wave's dependent
     instruction stream, bounded by issue: at most one instruction per 4 cycles per wave
@@ -328,10 +443,12 @@ def walk_roofline(mode, H, T, ks, ep, steps, kernel="zwalk_kernel"):
     instructions per task (PMC, every wave of the kernel, over the round's tasks) x tasks per
     second on the critical path (the longest frontier chain, or every task for the
     one-workgroup walks); peak = min(waves, 4) x 2.4 GHz / 4. The latency floor (one dependent
-    LDS round trip per task) is beside it."""
-    c = ks["commit"]
+    LDS round trip per task) is beside it. ``c``: the walk kernel's own HIP-event timing."""
     ms = c["ms"] / max(steps, 1)
-    longest = ep.get("longest_chain_tasks", 0) if kernel == "zwalk_kernel" else 0
+    # epoch chains (cost_aware best-fit) run side by side: the longest chain per epoch is the
+    # critical path (engine counter of the last round, summed over its epochs)
+    longest = (ep.get("longest_chain_tasks", 0)
+               if kernel in ("zwalk_kernel", "commit_kernel") and mode == MODES["ca_bf"] else 0)
     if longest <= 0:
         longest = T                      # every task of the round on one walk after another
     issue_waves = min(4, WALK_WAVES.get(kernel, 1))
@@ -348,7 +465,7 @@ def walk_roofline(mode, H, T, ks, ep, steps, kernel="zwalk_kernel"):
     out["latency_floor"] = {"peak_tasks_per_s": SHADER_HZ / LDS_DEP_CYCLES,
                             "achieved_tasks_per_s": tasks_per_s,
                             "frac": tasks_per_s / (SHADER_HZ / LDS_DEP_CYCLES)}
-    pmc, note = pmc_entry(mode, H, T, kernel)
+    pmc, note = pmc_entry(mode, H, T, kernel, variant)
     if pmc is None:
         out["note"] = note
         return out
@@ -374,24 +491,21 @@ def walk_roofline(mode, H, T, ks, ep, steps, kernel="zwalk_kernel"):
     return out
 
 
-def dominant_roofline(mode, H, T, ks, ep, steps, batch=False):
-    """The roofline of the kernel class that takes the most device time in the timed steps."""
-    if batch:
-        return score_roofline(mode, H, T, ks, "resident_kernel")
-    if ks["commit"]["ms"] >= ks["score"]["ms"]:
-        kernel = ("opp_commit_kernel" if mode == MODES["opp"] else
-                  "lwalk_kernel" if mode == MODES["vbp_bf"] else
-                  "zwalk_kernel" if ks["score"]["launches"] == 0 else "commit_kernel")
-        return walk_roofline(mode, H, T, ks, ep, steps, kernel)
-    kernel = ("band_score_kernel" if mode == MODES["vbp_bf"] and H >= 65536 else
-              "opp_count_kernel" if mode == MODES["opp"] else "score_kernel")
-    return score_roofline(mode, H, T, ks, kernel)
-
-
-def extra_roofline(tag, mode, H, T, ks, steps):
-    if not tag.startswith("c5_"):
-        return None
-    return dominant_roofline(mode, H, T, ks, {}, steps)
+def dominant_roofline(mode, H, T, ks, ep, steps, variant="", rounds_per_step=1, warm=0):
+    """The roofline of the kernel that takes the most device time in the timed steps (HIP events
+    per kernel), with the PMC profile of that kernel on this config and this binary."""
+    kt = ks.get("kernels") or {}
+    if not kt:
+        return {"kernel": None, "bound": None, "achieved": None, "peak": None, "frac": None,
+                "traffic": None, "note": "no kernel of the path was timed"}
+    kernel = max(kt, key=lambda n: kt[n]["ms"])
+    share = kt[kernel]["ms"] / max(sum(v["ms"] for v in kt.values()), 1e-12)
+    if kernel in WALK_KERNELS:
+        out = walk_roofline(mode, H, T, kt[kernel], ep, steps, kernel, variant, rounds_per_step, warm)
+    else:
+        out = score_roofline(mode, H, T, kt[kernel], kernel, variant)
+    out["dominant_share_of_timed_kernels"] = share
+    return out
 
 
 # ---------------------------------------------------------------------------- configs 1 and 2
@@ -459,9 +573,25 @@ def _replay(name, engine):
     return secs, cand, len(cases), ok, tr
 
 
+def round_trip_floor_ms(eng, reps=200):
+    """The least time one drop-in round can take on this engine: a pvt_place of a 1-host x
+    1-task round from host arrays (H2D, one launch, D2H, one synchronisation), median of reps."""
+    from pivot_place import synthetic
+    r = synthetic.make_round(MODES["vbp_ff"], 1, 1, seed=1)
+    for _ in range(20):
+        eng.place(r)
+    ts = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        eng.place(r)
+        ts.append(time.perf_counter() - t)
+    return float(np.median(ts)) * 1e3
+
+
 def replay_workloads(eng):
     out = {}
     threads = oracle_threads()
+    floor = round_trip_floor_ms(eng)
     for name in REPLAYS:
         try:
             _replay(name, eng)                               # warm-up (tables, scratch)
@@ -480,6 +610,19 @@ def replay_workloads(eng):
             "seconds": secs, "ms_per_round": secs * 1e3 / nr, "parity": bool(ok),
             "cpu_1thread": {"seconds": c1, "value": cand / c1, "parity": bool(ok1)},
             "cpu_all": {"seconds": ca, "value": cand / ca, "cores": threads, "parity": bool(oka)},
+            "cpu_baseline": {"value": cand / ca, "unit": "candidates/s", "cores": threads,
+                             "kind": "port", "value_1thread": cand / c1,
+                             "sample": "the same %d recorded rounds through the same drop-in "
+                                       "policy class with the C restatement behind the engine "
+                                       "contract (%d threads; 1 thread beside it)" % (nr, threads)},
+            "roofline": {"kernel": None, "bound": "round trip", "unit": "rounds/s",
+                         "achieved": nr / secs, "peak": 1e3 / floor, "frac": floor / (secs * 1e3 / nr),
+                         "traffic": None, "floor_ms_per_round": floor,
+                         "peak_basis": "one synchronous pvt_place of a 1-host x 1-task round from "
+                                       "host arrays on this engine (H2D, one launch, D2H, one "
+                                       "synchronisation; median of 200): a round of these sizes "
+                                       "(~1e5 candidates) is bound by the round trip and the host "
+                                       "work around it, not by a kernel"},
             "reference_sim_wall_s": tr["e2e"].get("reference_wall_s"),
             "note": "times the whole drop-in round (Python grouping / marshalling included); "
                     "reference_sim_wall_s is the reference's whole simulation in the build "
@@ -572,6 +715,7 @@ def main():
     cand_per_step = float(T) * H * (1 if hosts_sharded else world) * (B if B else 1)
     value = cand_per_step / (elapsed / args.steps)
     ks = kstats_all(eng)
+    ks["kernels"] = kernel_times(eng)
 
     if rank == 0:
         out = {
@@ -601,8 +745,11 @@ def main():
                                 "scenario-sharded x%d (no data-path collective)" % world),
                 "dist_backend": (("gloo" if gloo else "nccl") if world > 1 else None),
             },
-            "roofline": dominant_roofline(mode, H, T, ks, ep, args.steps, batch=bool(B)),
-            "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items()},
+            "roofline": dominant_roofline(mode, H, T, ks, ep, args.steps,
+                                          variant=("_b%d" % B) if B else "",
+                                          rounds_per_step=B or 1, warm=args.warmup),
+            "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items() if k != "kernels"},
+            "kernel_ms_per_step": {k: v["ms"] / args.steps for k, v in ks["kernels"].items()},
             "walk_us_per_task": (ks["commit"]["ms"] * 1e3 / args.steps / max(T * (B or 1), 1)
                                  if not B else None),
             "windows_per_step": stats["windows"], "refills_per_step": stats["refills"],
@@ -629,6 +776,14 @@ def main():
             out["extra"] = extra_workloads(eng, args, args.mode)
         if args.replay == 1 or (args.replay < 0 and default and args.extra != 0):
             out.setdefault("extra", {}).update(replay_workloads(eng))
+    if world > 1 and args.c4_batch > 0 and not B:
+        # (every rank: the barriers and the MAX / MIN reductions are collective)
+        c4 = scenario_batch_line(eng, args, rank, world, gloo, args.c4_batch)
+        if rank == 0:
+            out.setdefault("extra", {})["c4_scenarios_%s_x%d" % (args.mode, world)] = c4
+            log("[rank 0] config 4 x%d: %.3e cand/s, %.2f ms, parity %s"
+                % (world, c4["value"], c4["ms_per_step"], c4["parity"]))
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -59,6 +60,7 @@ struct Buf {
 
 struct TimedLaunch {
   int kclass;
+  const char* kname;   // the one kernel the scope brackets (pvt_get_kernel_kstats), or NULL
   double candidates, bytes;
   hipEvent_t a, b;
 };
@@ -149,6 +151,7 @@ struct pvt_ctx {
   pvt_kstats ks[PVT_K_COUNT];
   std::vector<hipEvent_t> evpool;
   std::vector<TimedLaunch> pending;
+  std::map<std::string, pvt_kstats> kks;   // per kernel (scopes tagged with its name)
   // scratch
   Buf gcnt, goff, gskey, gsidx;   // grouped order: counts, offsets + cursors, scattered pairs
   Buf ord, ord2, keys64a, keys64b, keys32a, keys32b, sorttmp, dem_ord, anc_ord, grp_ord, csum, bsum, key,
@@ -242,9 +245,10 @@ struct Scope {
   pvt_ctx* ctx;
   hipStream_t st;
   TimedLaunch t;
-  Scope(pvt_ctx* c, int kclass, double cand, double bytes, hipStream_t s = nullptr)
+  Scope(pvt_ctx* c, int kclass, double cand, double bytes, hipStream_t s = nullptr,
+        const char* kname = nullptr)
       : ctx(c), st(s ? s : c->stream) {
-    t.kclass = kclass; t.candidates = cand; t.bytes = bytes; t.a = t.b = nullptr;
+    t.kclass = kclass; t.kname = kname; t.candidates = cand; t.bytes = bytes; t.a = t.b = nullptr;
     if (ctx->profiling) { t.a = take_event(ctx); (void)hipEventRecord(t.a, st); }
   }
   ~Scope() {
@@ -261,6 +265,10 @@ static void harvest(pvt_ctx* ctx) {
     (void)hipEventElapsedTime(&ms, t.a, t.b);
     pvt_kstats& k = ctx->ks[t.kclass];
     k.launches += 1; k.ms += ms; k.candidates += t.candidates; k.bytes += t.bytes;
+    if (t.kname) {
+      pvt_kstats& n = ctx->kks[t.kname];
+      n.launches += 1; n.ms += ms; n.candidates += t.candidates; n.bytes += t.bytes;
+    }
     ctx->evpool.push_back(t.a);
     ctx->evpool.push_back(t.b);
   }
@@ -385,6 +393,7 @@ extern "C" int pvt_reset_kstats(pvt_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   harvest(ctx);
   std::memset(ctx->ks, 0, sizeof(ctx->ks));
+  ctx->kks.clear();
   return PVT_OK;
 }
 extern "C" int pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out) {
@@ -392,6 +401,15 @@ extern "C" int pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out) {
   (void)hipStreamSynchronize(ctx->stream);
   harvest(ctx);
   *out = ctx->ks[kclass];
+  return PVT_OK;
+}
+extern "C" int pvt_get_kernel_kstats(pvt_ctx* ctx, const char* kernel, pvt_kstats* out) {
+  if (!ctx || !kernel || !out) return PVT_EINVAL;
+  (void)hipStreamSynchronize(ctx->stream);
+  harvest(ctx);
+  auto it = ctx->kks.find(kernel);
+  if (it == ctx->kks.end()) std::memset(out, 0, sizeof(*out));
+  else *out = it->second;
   return PVT_OK;
 }
 extern "C" int pvt_set_window(pvt_ctx* ctx, int tasks) {
@@ -677,7 +695,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
     const int t0 = k * W, nt = std::min(W, T - t0);
     OppCountArgs ca{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, H, nt, 0, 0, nq, nsq,
                     W, bm_of(k % nbuf), sc_of(k % nbuf), 0, nsq, nq, nsq};
-    Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc, s);
+    Scope sc(ctx, PVT_K_SCORE, (double)nt * H, (double)nt * H * bpc, s, "opp_count_kernel");
     launch_opp_count(ca, s);
   };
   if (nwin > 0) count(0, st);
@@ -698,7 +716,7 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
                      sc_of(k % nbuf), H, nt, nq, nsq, W, r->placement + t0, mt, ctx->stamps,
                      in, next ? tl_of(k % nbuf) : nullptr, next ? 0 : 1, fault};
     {
-      Scope s(ctx, PVT_K_COMMIT, 0, 0);
+      Scope s(ctx, PVT_K_COMMIT, 0, 0, nullptr, "opp_commit_kernel");
       launch_opp_commit(oa, st);
     }
     if (next) HIPCHK(hipStreamWaitEvent(st, ctx->ev_lists, 0));
@@ -990,7 +1008,7 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
                      P<double>(ctx->bsum), nullptr, nullptr, P<int32_t>(ctx->next),
                      P<WinRec>(ctx->wres), r->placement, nullptr, ctx->stamps,
                      P<int32_t>(ctx->kperm), 0, R.lo, n_g, r->avail, P<int32_t>(ctx->next) + 2};
-        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+        Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
         launch_zwalk_keyed(za, true, ctx->stream);
       }
       HIPCHK(hipGetLastError());
@@ -1039,12 +1057,12 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
     PermArgs pa{r->avail, r->zone, P<uint64_t>(ctx->kskey) + n, P<int32_t>(ctx->kperm), dem_w,
                 anc_w, R.ord + t0, R.H, nt, n > 0 ? R.kn : 0, KSCAN_DEPTH, R.lo,
                 R.kmode == 1 ? 1 : 0, std::numeric_limits<double>::denorm_min(), L};
-    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
+    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st, "perm_scan_kernel");
     launch_perm_scan(pa, st);
   } else if (R.ordered) {
     OrderedArgs oa{r->avail, r->zone, dem_w, anc_w, R.ord + t0, R.H, nt,
                    r->mode == PVT_CA_FF ? 1 : 0, R.lo, R.hi, L};
-    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
+    Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st, "ordered_kernel");
     launch_ordered(oa, st);
   } else if (R.band) {
     const int S = R.band_S;
@@ -1072,12 +1090,12 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
                 P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt), r->avail, r->tiebreak, R.H, dem_l,
                 nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), nt_dev};
     {
-      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
+      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st, "band_score_kernel");
       launch_band_score(ba, st);
     }
     MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_l,
                  anc_w, R.ord + t0, R.H, nt, S, KL, L, nt_dev, ctx->t_merge_bitonic};
-    Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
+    Scope sc(ctx, PVT_K_MERGE, 0, 0, st, merge_kernel_name(ma));
     launch_merge(ma, st);
   } else {
     const int S = choose_segments(Hl, nt, r->mode, ctx->score_tw, R.in_epoch, ctx->t_segments);
@@ -1088,12 +1106,12 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
                  R.lo, R.hi, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), ctx->score_tw,
                  r->mode == PVT_CA_BF ? r->rt_bw : nullptr, P<int32_t>(ctx->grp_ord) + t0};
     {
-      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st);
+      Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st, "score_kernel");
       launch_score(r->mode, sa, st);
     }
     MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_w,
                  anc_w, R.ord + t0, R.H, nt, S, KL, L, nullptr, ctx->t_merge_bitonic};
-    Scope sc(ctx, PVT_K_MERGE, 0, 0, st);
+    Scope sc(ctx, PVT_K_MERGE, 0, 0, st, merge_kernel_name(ma));
     launch_merge(ma, st);
   }
   HIPCHK(hipGetLastError());
@@ -1123,7 +1141,7 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
     ca_.ordw = R.ord + t0;
   }
   {
-    Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+    Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, R.lw_last ? "lwalk_kernel" : "commit_kernel");
     if (R.lw_last) launch_lwalk(ca_, st);
     else launch_commit(ca_, st);
   }
@@ -1171,7 +1189,7 @@ static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
                    P<int32_t>(ctx->grp_ord) + t0, ctx->stamps};
     R.lw_last = false;
     {
-      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+      Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "commit_kernel");
       launch_commit(ca_, ctx->stream);
     }
     HIPCHK(hipGetLastError());
@@ -1228,7 +1246,7 @@ static int ordered_frontier(pvt_ctx* ctx) {
                  r->placement, nullptr, ctx->stamps, P<int32_t>(ctx->kperm), 0, 0, n, r->avail,
                  P<int32_t>(ctx->next) + 2};
     {
-      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+      Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
       launch_zwalk_keyed(za, strict, st);
     }
     HIPCHK(hipGetLastError());
@@ -1507,7 +1525,7 @@ static int place_epochs(pvt_ctx* ctx) {
                    P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
                    nullptr, 0, 0, 0, nullptr, nullptr, nullptr, dev + EP_CSOFF, dev + EP_CSEG};
       {
-        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+        Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
         launch_zwalk(za, nch, st);
       }
       HIPCHK(hipGetLastError());
@@ -1538,7 +1556,7 @@ static int place_epochs(pvt_ctx* ctx) {
                    P<WinRec>(ctx->wres), zw ? 1 : 0};
     if (need) {
       {
-        Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+        Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "commit_kernel");
         launch_commit_chains(ca_, nch, st);
       }
       if ((rc = validate_and_read())) return rc;
@@ -1617,7 +1635,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n) {
     bytes += c * bytes_per_candidate(mode);
   }
   {
-    Scope sc(ctx, PVT_K_SCORE, cand, bytes);
+    Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mode, waves, hpl, n, ra, st);
   }
   HIPCHK(hipGetLastError());
@@ -1851,7 +1869,7 @@ static int opp_shard_commit(pvt_ctx* ctx, const void* packages) {
                    R.opp_nsq, R.opp_W, r->placement + t0, mt, ctx->stamps, nullptr, nullptr, 1,
                    P<int32_t>(ctx->oppfault)};
   {
-    Scope s(ctx, PVT_K_COMMIT, 0, 0);
+    Scope s(ctx, PVT_K_COMMIT, 0, 0, nullptr, "opp_commit_kernel");
     launch_opp_commit(oa, st);
   }
   HIPCHK(hipGetLastError());
@@ -2045,7 +2063,7 @@ static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
                  P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
                  nullptr, 0, 0, 0, nullptr, nullptr, win, dev + EP_CSOFF, dev + EP_CSEG};
     {
-      Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+      Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
       launch_zwalk(za, nch, st);
     }
     EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
@@ -2077,7 +2095,7 @@ static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
                nullptr, nullptr, nullptr, nullptr, P<int32_t>(ctx->next), P<WinRec>(ctx->wres),
                r->placement, nullptr, ctx->stamps, nullptr, 0, R.lo, n, r->avail, nullptr, win};
   {
-    Scope sc(ctx, PVT_K_COMMIT, 0, 0);
+    Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
     launch_zwalk_keyed(za, strict, st);
   }
   HIPCHK(hipGetLastError());
@@ -2206,7 +2224,7 @@ extern "C" int pvt_shard_commit(pvt_ctx* ctx, const void* packages) {
                P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
                R.ord + t0, R.H, nt, R.world, PK, L, nullptr, ctx->t_merge_bitonic};
   {
-    Scope sc(ctx, PVT_K_MERGE, 0, 0);
+    Scope sc(ctx, PVT_K_MERGE, 0, 0, nullptr, merge_kernel_name(ma));
     launch_merge(ma, ctx->stream);
   }
   HIPCHK(hipGetLastError());

@@ -352,6 +352,7 @@ int score_tasks_per_wave(int mode, int hosts, int force = 0);
 int score_diag(uint64_t* out, int n, int reset);   // PVT_DIAG builds; else PVT_EUNSUPPORTED
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st);
 void launch_merge(const MergeArgs& a, hipStream_t st);
+const char* merge_kernel_name(const MergeArgs& a);   // the kernel launch_merge picks
 void launch_pack(const PackArgs& a, hipStream_t st);
 void launch_ordered(const OrderedArgs& a, hipStream_t st);
 void launch_perm_scan(const PermArgs& a, hipStream_t st);

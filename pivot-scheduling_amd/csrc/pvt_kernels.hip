@@ -591,14 +591,22 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   }
 }
 
-void launch_merge(const MergeArgs& a, hipStream_t st) {
+static int merge_variant(const MergeArgs& a) {
   const bool small = !a.bitonic;
-  if (small && a.seg_feas != nullptr && a.SL == KL && a.S <= MERGE_SMALL_S)
-    hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
-  else if (small && a.seg_feas == nullptr && (size_t)a.S * a.SL <= LMAX)
-    hipLaunchKernelGGL(merge_pkg_kernel, dim3(a.nt), dim3(256), 0, st, a);
-  else
-    hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
+  if (small && a.seg_feas != nullptr && a.SL == KL && a.S <= MERGE_SMALL_S) return 1;
+  if (small && a.seg_feas == nullptr && (size_t)a.S * a.SL <= LMAX) return 2;
+  return 0;
+}
+const char* merge_kernel_name(const MergeArgs& a) {
+  static const char* names[3] = {"merge_kernel", "merge_small_kernel", "merge_pkg_kernel"};
+  return names[merge_variant(a)];
+}
+void launch_merge(const MergeArgs& a, hipStream_t st) {
+  switch (merge_variant(a)) {
+    case 1: hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(merge_pkg_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
+    default: hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
+  }
 }
 
 // ------------------------------------------------------------------------------------------

@@ -42,6 +42,7 @@ def load_library(path=None):
         "pvt_set_profiling": ([c_void_p, c_int], c_int),
         "pvt_reset_kstats": ([c_void_p], c_int),
         "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
+        "pvt_get_kernel_kstats": ([c_void_p, ctypes.c_char_p, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_set_window": ([c_void_p, c_int], c_int),
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
         "pvt_set_score_tw": ([c_void_p, c_int], c_int),
@@ -512,6 +513,12 @@ class PlacementEngine:
     def kstats(self, kclass):
         k = _abi.pvt_kstats()
         self._check(self.lib.pvt_get_kstats(self.ctx, int(kclass), ctypes.byref(k)))
+        return {"launches": k.launches, "ms": k.ms, "candidates": k.candidates, "bytes": k.bytes}
+
+    def kernel_kstats(self, name):
+        """HIP-event timing of one named kernel's launches while profiling was on."""
+        k = _abi.pvt_kstats()
+        self._check(self.lib.pvt_get_kernel_kstats(self.ctx, name.encode(), ctypes.byref(k)))
         return {"launches": k.launches, "ms": k.ms, "candidates": k.candidates, "bytes": k.bytes}
 
     def last_stats(self):

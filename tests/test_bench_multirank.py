@@ -1,8 +1,9 @@
 """bench.py's multi-rank path, before an 8-GPU node runs it: two ranks
 started by bench.py itself (--gpus 2, no WORLD_SIZE), both on cuda:0 over gloo -- the launcher,
 the process group, the barrier + MAX-over-ranks timing and, with --shard hosts, the
-torch.distributed exchange of host-sharded packages. The JSON line must report both ranks and
-parity with the CPU restatement."""
+torch.distributed exchange of host-sharded packages, and the config-4 scenario line every N > 1
+run adds (--c4-batch scenarios per rank, MAX-over-ranks timing, parity MIN-reduced). The JSON
+line must report both ranks and parity with the CPU restatement."""
 import json
 import os
 import subprocess
@@ -22,7 +23,7 @@ def test_bench_two_ranks_gloo(shard, mode):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
            "--hosts", "20000", "--tasks", "300", "--mode", mode, "--steps", "2", "--warmup", "1",
-           "--shard", shard, "--cpu-baseline-seconds", "0", "--extra", "0"]
+           "--shard", shard, "--cpu-baseline-seconds", "0", "--extra", "0", "--c4-batch", "16"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -31,3 +32,25 @@ def test_bench_two_ranks_gloo(shard, mode):
     assert res["n_gpus"] == 2 and res["parity"] is True, res
     assert res["scaling"] == ("strong" if shard == "hosts" else "weak")
     assert res["value"] > 0 and res["config"]["dist_backend"] == "gloo"
+    c4 = res["extra"]["c4_scenarios_%s_x2" % mode]
+    assert c4["parity"] is True and c4["n_gpus"] == 2 and c4["scenarios"] == 32, c4
+    assert c4["value"] > 0 and c4["scaling"] == "weak"
+
+
+@pytest.mark.parametrize("mode", ["ca_bf", "vbp_bf", "opp"])
+def test_bench_two_ranks_scenario_batch(mode):
+    """bench.py --gpus 2 --batch 64: each rank places its own 64 scenarios (1000 x 1000) with one
+    pvt_place_batch launch per step -- the config-4 workload as the main line."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--hosts", "1000", "--tasks", "1000", "--batch", "64", "--mode", mode, "--steps", "2",
+           "--warmup", "1", "--cpu-baseline-seconds", "0", "--extra", "0"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=110, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["parity"] is True and res["scaling"] == "weak", res
+    assert res["config"]["scenarios_per_gpu"] == 64
+    assert abs(res["value"] * res["ms_per_step"] * 1e-3 - 2 * 64 * 1e6) < 1e-3 * 2 * 64 * 1e6

@@ -44,9 +44,44 @@ def test_pmc_index_and_binary_check(tmp_path, monkeypatch):
     monkeypatch.setattr(bench, "lib_sha256", lambda: "0" * 64)
     e, note = bench.pmc_entry(bench.MODES["ca_bf"], 1000, 10, "zwalk_kernel")
     assert e is not None and note is None
-    ks = {"commit": {"ms": 1.0, "launches": 1}, "score": {"ms": 0.0, "launches": 0}}
-    rl = bench.walk_roofline(bench.MODES["ca_bf"], 1000, 10, ks, {"longest_chain_tasks": 10}, 1)
+    k = {"ms": 1.0, "launches": 1}
+    rl = bench.walk_roofline(bench.MODES["ca_bf"], 1000, 10, k, {"longest_chain_tasks": 10}, 1)
     assert rl["instructions_per_task"] == pytest.approx(400.0 * 2 / 10)
     # zwalk_kernel: 4 waves per workgroup, all of them counted and all of them issuing
     assert rl["frac"] == pytest.approx(80.0 * (10 / 1e-3) / (4 * 2.4e9 / 4))
     assert rl["frac_one_wave"] == pytest.approx(80.0 * (10 / 1e-3) / (2.4e9 / 4))
+    # the dominant kernel is the one with the most HIP-event time, whatever its class
+    ks = {"kernels": {"zwalk_kernel": {"ms": 1.0, "launches": 1},
+                      "merge_small_kernel": {"ms": 0.2, "launches": 3}}}
+    rl = bench.dominant_roofline(bench.MODES["ca_bf"], 1000, 10, ks, {"longest_chain_tasks": 10}, 1)
+    assert rl["kernel"] == "zwalk_kernel" and rl["frac"] == pytest.approx(80.0 * 1e4 / 2.4e9)
+    assert rl["dominant_share_of_timed_kernels"] == pytest.approx(1.0 / 1.2)
+
+
+def test_pmc_index_variant_keys(tmp_path, monkeypatch):
+    """Batch (config 4) and loaded (config 5) profiles are indexed under their own keys, and the
+    kernel name is matched whole (commit_kernel is not opp_commit_kernel)."""
+    idx = tmp_path / "index.json"
+    specs = []
+    for name, kern in (("a", "void pvt::resident_kernel<1, 4>(pvt::ResidentArgs)"),
+                       ("b", "void pvt::opp_commit_kernel(pvt::OppCommitArgs)")):
+        src = tmp_path / ("%s.json" % name)
+        src.write_text(json.dumps({"kernel": kern, "probe": ["--reps", "2"], "lib_sha256": "1" * 64,
+                                   "counters_per_launch": {"dispatches_sq": 2}}))
+        specs.append(src)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_index.py"), str(idx),
+                          "ca_bf:1000:1000_b512:%s" % specs[0], "opp:100000:1000:%s" % specs[1]],
+                         capture_output=True, text=True)
+    assert out.returncode == 0, out.stderr
+    keys = set(json.loads(idx.read_text())["entries"])
+    assert keys == {"ca_bf_1000_1000_b512:resident_kernel", "opp_100000_1000:opp_commit_kernel"}
+    monkeypatch.setattr(bench, "PMC_INDEX", str(idx))
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "1" * 64)
+    e, _ = bench.pmc_entry(bench.MODES["ca_bf"], 1000, 1000, "resident_kernel", "_b512")
+    assert e is not None
+    e, _ = bench.pmc_entry(bench.MODES["opp"], 100000, 1000, "commit_kernel")
+    assert e is None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_profile
+    assert pmc_profile.base_name("void pvt::opp_commit_kernel(pvt::OppCommitArgs)") == "opp_commit_kernel"
+    assert pmc_profile.base_name("void pvt::zwalk_kernel<true, false>(pvt::ZwalkArgs)") == "zwalk_kernel"

@@ -1,24 +1,36 @@
 #!/bin/bash
-# PMC profiles of every hot kernel of the bench lines on THIS build, indexed for bench.py
-# (profiles/pmc_index.json; entries carry the library's sha256, so bench.py uses them only for
-# the binary they were collected on). Run on the GPU box:  tools/pmc_all.sh TAG
-# Each tools/pmc_profile.py pass is its own `rocprofv3 --pmc` child under a hard time limit.
+# PMC profiles of the kernels that can dominate every bench.py line, on THIS build, indexed for
+# bench.py (profiles/pmc_index.json; entries carry the library's sha256, so bench.py uses them
+# only for the binary they were collected on). Run on the GPU box:  tools/pmc_all.sh TAG [SET..]
+# Sets: c5 (config 5, 1M x 10k, five policies), c5l (loaded config 5), c3 (100k x 1k), c4 (512
+# scenarios of 1000 x 1000, resident kernel); default all. Each tools/pmc_profile.py pass is its
+# own `rocprofv3 --pmc` child under a hard time limit (two passes per config).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
-tag=${1:-r03}
-H=1000000 T=10000
+tag=${1:-r04}
+shift
+sets=${*:-c5 c5l c3 c4}
 set -e
-prof() {   # prof MODE KERNELS
-  python tools/pmc_profile.py --tag "${tag}_$1" --kernel "$2" --secs 120 -- \
-    tools/walk_probe.py --mode "$1" --hosts $H --tasks $T --reps 2 > "gpurun_out/pmc_${tag}_$1.log" 2>&1
-  echo "pmc $1 ($2) ok"
+WALKS=zwalk_kernel,commit_kernel,lwalk_kernel,opp_commit_kernel
+PARS=score_kernel,band_score_kernel,opp_count_kernel,perm_scan_kernel,ordered_kernel,merge_kernel,merge_small_kernel
+idx=()
+prof() {   # prof NAME MODE HOSTS TASKS KEYSUFFIX KERNELS PROBE-ARGS...
+  local name=$1 mode=$2 h=$3 t=$4 suf=$5 kern=$6
+  shift 6
+  python tools/pmc_profile.py --tag "${tag}_${name}" --kernel "$kern" --secs 150 -- \
+    tools/walk_probe.py --mode "$mode" --hosts "$h" --tasks "$t" --reps 2 "$@" \
+    > "gpurun_out/pmc_${tag}_${name}.log" 2>&1
+  for f in gpurun_out/pmc_${tag}_${name}_*.json; do
+    [ -e "$f" ] && idx+=("$mode:$h:$t$suf:$f")
+  done
+  echo "pmc $name ok"
 }
-prof ca_bf zwalk_kernel
-prof vbp_ff zwalk_kernel
-prof ca_ff zwalk_kernel
-prof vbp_bf band_score_kernel,lwalk_kernel
-prof opp opp_count_kernel,opp_commit_kernel
-args=()
-for m in ca_bf vbp_ff ca_ff; do args+=("$m:$H:$T:gpurun_out/pmc_${tag}_$m.json"); done
-for k in band_score_kernel lwalk_kernel; do args+=("vbp_bf:$H:$T:gpurun_out/pmc_${tag}_vbp_bf_$k.json"); done
-for k in opp_count_kernel opp_commit_kernel; do args+=("opp:$H:$T:gpurun_out/pmc_${tag}_opp_$k.json"); done
-python tools/pmc_index.py gpurun_out/pmc_index.json "${args[@]}"
+for s in $sets; do
+  case $s in
+    c5)  for m in ca_bf vbp_ff ca_ff vbp_bf opp; do prof "c5_$m" $m 1000000 10000 "" "$WALKS,$PARS"; done ;;
+    c5l) prof c5_ca_bf_loaded ca_bf 1000000 10000 _loaded "$WALKS,$PARS" --loaded 1 ;;
+    c3)  for m in ca_bf vbp_ff ca_ff vbp_bf opp; do prof "c3_$m" $m 100000 1000 "" "$WALKS,$PARS"; done ;;
+    c4)  for m in ca_bf vbp_ff ca_ff vbp_bf opp; do prof "c4_$m" $m 1000 1000 _b512 resident_kernel --batch 512; done ;;
+    *)   echo "unknown set $s"; exit 2 ;;
+  esac
+done
+python tools/pmc_index.py gpurun_out/pmc_index.json "${idx[@]}"

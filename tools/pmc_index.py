@@ -16,7 +16,7 @@ KERNELS = ("zwalk_kernel", "opp_commit_kernel", "opp_count_kernel", "band_score_
 
 
 def short(name):
-    base = name.split("(")[0].split("<")[0].split("::")[-1]
+    base = name.split("(")[0].split("<")[0].split("::")[-1].split(" ")[-1]
     for k in KERNELS:
         if base == k:
             return k

@@ -2,12 +2,13 @@
 """rocprofv3 PMC profile of one kernel of the engine (run on the GPU box; never touches the GPU
 itself: every pass is a child `rocprofv3 --pmc ... -- python <probe>` under a hard time limit).
 
-Passes (one counter set each; gfx950 slot limits, MI355X_MICROARCH.md §rocprofv3 PMC slots):
-  sq     SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE
-         SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES + GRBM_GUI_ACTIVE
-  sq2    SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY
-         SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS
-  fetch  FETCH_SIZE           write  WRITE_SIZE
+Passes (one counter set each; gfx950 slot limits, MI355X_MICROARCH.md §rocprofv3 PMC slots:
+8 SQ, 4 TCC -- FETCH_SIZE takes 3, WRITE_SIZE 2 --, 2 GRBM per pass):
+  a      SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE
+         SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_BUSY_CYCLES + GRBM_GUI_ACTIVE + FETCH_SIZE
+  b      SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY
+         SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS + WRITE_SIZE
+(the older four-pass split sq / sq2 / fetch / write is still accepted by --passes)
 Counters missing from `rocprofv3 -L` (gpurun_out/counters.txt, when present) are dropped.
 
 Per dispatch of the kernels whose name contains --kernel, every counter is summed over its rows
@@ -20,7 +21,7 @@ Per dispatch of the kernels whose name contains --kernel, every counter is summe
 Peaks: 1024 SIMDs x 2.4 GHz of VALU issue cycles; 256 CUs x 2.4 GHz of LDS-array cycles.
 
     python tools/pmc_profile.py --tag r02 --kernel score_kernel -- tools/score_probe.py --mode ca_bf
-Writes gpurun_out/pmc_<tag>.json and gpurun_out/pmc_<tag>.csv.
+Writes gpurun_out/pmc_<tag>_<kernel>.json and .csv for every listed kernel the probe launched.
 """
 import argparse
 import csv
@@ -48,6 +49,8 @@ PASSES = {
     "fetch": ["FETCH_SIZE"],
     "write": ["WRITE_SIZE"],
 }
+PASSES["a"] = PASSES["sq"] + PASSES["fetch"]
+PASSES["b"] = PASSES["sq2"] + PASSES["write"]
 SIMDS, CUS, CLOCK = 1024, 256, 2.4e9
 
 
@@ -70,13 +73,19 @@ def run_pass(name, counters, tag, probe, secs):
     return files[0]
 
 
+def base_name(name):
+    """The __global__ function's own name: 'void pvt::zwalk_kernel<true, false>(pvt::ZwalkArgs)'
+    -> 'zwalk_kernel' (so 'commit_kernel' does not match opp_commit_kernel)."""
+    return name.split("(")[0].split("<")[0].split("::")[-1].split(" ")[-1]
+
+
 def parse(path, kernel):
     """{dispatch: {counter: value summed over rows}}, {dispatch: kernel name}, {dispatch: ns}."""
     vals, names, dur = {}, {}, {}
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "")
-            if kernel not in name:
+            if base_name(name) != kernel:
                 continue
             d = row.get("Dispatch_Id")
             c = row.get("Counter_Name")
@@ -122,7 +131,7 @@ def main():
     ap.add_argument("--kernel", default="score_kernel",
                     help="kernel name substring; several, comma-separated, are taken from the same "
                          "passes (one pmc_<tag>_<kernel>.json each)")
-    ap.add_argument("--passes", default="sq,sq2,fetch,write")
+    ap.add_argument("--passes", default="a,b")
     ap.add_argument("--secs", type=int, default=90)
     ap.add_argument("--candidates-per-launch", type=float, default=0.0)
     ap.add_argument("probe", nargs=argparse.REMAINDER)
@@ -143,8 +152,9 @@ def main():
         path = run_pass(name, counters, a.tag, probe, a.secs)
         for kern in kernels:
             vals, names, dur = parse(path, kern)
-            if not vals:
-                raise RuntimeError("pass %s: no dispatch of %s" % (name, kern))
+            if not vals:     # (a candidate kernel this workload never launches)
+                print("pass %s: no dispatch of %s" % (name, kern), flush=True)
+                continue
             kname[kern] = kname[kern] or sorted(set(names.values()))[0]
             for c in counters:
                 xs = [v[c] for v in vals.values() if c in v]
@@ -152,10 +162,15 @@ def main():
                     avg[kern][c] = sum(xs) / len(xs)
             durs[kern] += list(dur.values())
             avg[kern].setdefault("dispatches_" + name, len(vals))
+            avg[kern].setdefault("dispatches_sq", len(vals))   # (pmc_index: launches per round)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    if not any(kname.values()):
+        raise RuntimeError("no dispatch of any of %s" % a.kernel)
     for kern in kernels:
+        if kname[kern] is None:
+            continue
         out = summarise(kname[kern], avg[kern], durs[kern], probe, a.candidates_per_launch)
-        stem = "pmc_%s" % a.tag if len(kernels) == 1 else "pmc_%s_%s" % (a.tag, kern)
+        stem = "pmc_%s_%s" % (a.tag, kern)
         with open(os.path.join(ROOT, "gpurun_out", stem + ".json"), "w") as f:
             json.dump(out, f, indent=1)
         with open(os.path.join(ROOT, "gpurun_out", stem + ".csv"), "w") as f:

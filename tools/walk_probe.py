@@ -4,6 +4,13 @@
 stalls shows where). Exits non-zero if the engine reports an error (e.g. a hand-off timeout).
 
     python tools/walk_probe.py --mode ca_bf --hosts 100000 --tasks 2000 --pipeline 0 --reps 2
+    python tools/walk_probe.py --mode ca_bf --hosts 1000 --tasks 1000 --batch 512 --reps 2
+    python tools/walk_probe.py --mode ca_bf --hosts 1000000 --tasks 10000 --loaded 1 --reps 2
+
+--batch B: the config-4 shape, B scenarios (seeds seed + s) in one pvt_place_batch per rep.
+--loaded 1: bench.py's loaded config-5 round (every host capped at 1 free cpu).
+The shapes are exactly those of bench.py's lines, so a PMC profile of the probe prices the
+launches bench.py times.
 """
 import argparse
 import os
@@ -25,26 +32,39 @@ def main():
     p.add_argument("--pipeline", type=int, default=1)
     p.add_argument("--window", type=int, default=0)
     p.add_argument("--reps", type=int, default=2)
+    p.add_argument("--batch", type=int, default=0)
+    p.add_argument("--loaded", type=int, default=0)
     a = p.parse_args()
+    import numpy as np
     import torch
     from pivot_place import _abi, synthetic
     from pivot_place.engine import DeviceRound, PlacementEngine
-    r = synthetic.make_round(MODES[a.mode], a.hosts, a.tasks, seed=a.seed)
+    from pivot_place.engine import DeviceBatch
     eng = PlacementEngine(0, window=a.window)
-    eng.set_resident(0)
     eng.set_pipeline(bool(a.pipeline))
-    dr = DeviceRound(r, eng.device)
+    if a.batch:
+        rounds = [synthetic.make_round(MODES[a.mode], a.hosts, a.tasks, seed=a.seed + s)
+                  for s in range(a.batch)]
+        dr, run = DeviceBatch(rounds, eng.device), eng.run_batch
+    else:
+        r = synthetic.make_round(MODES[a.mode], a.hosts, a.tasks, seed=a.seed)
+        if a.loaded:
+            r.avail[0] = np.minimum(r.avail[0], 1.0)
+        if a.hosts > _abi.PVT_RESIDENT_MAX_HOSTS or a.tasks > _abi.PVT_RESIDENT_MAX_TASKS:
+            eng.set_resident(0)
+        dr, run = DeviceRound(r, eng.device), eng.run
     eng.reset_kstats()
     eng.set_profiling(True)
     for rep in range(a.reps):
         t = time.perf_counter()
         dr.reset()
-        eng.run(dr)
+        run(dr)
         torch.cuda.synchronize()
         st = eng.last_stats()
-        print("walk probe rep %d: mode %s H=%d T=%d pipeline=%d  %.2f ms  windows=%d refills=%d"
-              % (rep, a.mode, a.hosts, a.tasks, a.pipeline, (time.perf_counter() - t) * 1e3,
-                 st["windows"], st["refills"]), flush=True)
+        print("walk probe rep %d: mode %s H=%d T=%d batch=%d loaded=%d pipeline=%d  %.2f ms  "
+              "windows=%d refills=%d" % (rep, a.mode, a.hosts, a.tasks, a.batch, a.loaded,
+                                         a.pipeline, (time.perf_counter() - t) * 1e3,
+                                         st["windows"], st["refills"]), flush=True)
     eng.set_profiling(False)
     k = eng.kstats(_abi.PVT_K_COMMIT)
     print("commit launches=%d avg %.3f ms" % (k["launches"], k["ms"] / max(k["launches"], 1)),
