@@ -353,7 +353,8 @@ def scenario_batch_line(eng, args, rank, world, gloo, B, H=1000, T=1000):
             "tasks": T, "steps": steps, "scaling": "weak", "timing": "max over ranks of each "
             "rank's timed steps, between barriers", "parity": (ok if args.parity else None),
             "parity_scope": "every rank's scenarios vs the oracle (MIN-reduced)",
-            "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items()}}
+            "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items() if k != "kernels"},
+            "kernel_ms_per_step": {k: v["ms"] / steps for k, v in ks["kernels"].items()}}
 
 
 # ---------------------------------------------------------------------------- roofline

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define PVT_ABI_VERSION 2
+#define PVT_ABI_VERSION 3
 
 /* Return codes. */
 #define PVT_OK            0
@@ -270,6 +270,42 @@ typedef struct pvt_anchor_args {
   int64_t n_rows;             /* rows of off when item is set (0 when item is NULL)       */
 } pvt_anchor_args;
 int  pvt_anchor(pvt_ctx* ctx, const pvt_anchor_args* a);
+
+/*
+ * Drop-in round from HOST memory in one round trip (the reference's synchronous schedule()
+ * call, scheduler/__init__.py:100-103). Every array pointer of r is a HOST pointer: avail
+ * in/out, placement and order out, mt_state in/out. The context packs the inputs into its
+ * pinned staging buffer, copies them to the device with ONE copy, places the round, and copies
+ * avail, placement, order and the MT19937 states back with ONE copy and one synchronisation.
+ * On error the outputs are left untouched.
+ *
+ * cost_aware rounds may pass `items` and leave task_group / group_anchor NULL: the grouping of
+ * scheduler/cost_aware.py:30-58 then runs on the device in the same round trip -- per item the
+ * mode host of its predecessor placements (as pvt_anchor), groups keyed by the storage of that
+ * host's zone or, for items without predecessors, by their application, numbered in first-seen
+ * task order, and one randomizer.choice(storage) per application group, in group order, from
+ * items->mt_state (the policy's RandomState; in/out). items->status[0] returns the number of
+ * groups, status[1] an error kind with PVT_EINVAL: 1 a mode placement that is not a host of the
+ * cluster, 2 a zone without storage (the reference raises AttributeError for both), 3 malformed
+ * item lists. Rounds beyond the fused grouping's limits (T > 16384, n_storage + n_apps > 8192)
+ * return PVT_EUNSUPPORTED before any work (the caller then uses pvt_anchor + pvt_place).
+ */
+typedef struct pvt_ca_items {
+  int32_t n_items;             /* C: distinct containers of the ready tasks                 */
+  int32_t n_apps;              /* applications of the items (item_app in [0, n_apps))        */
+  int64_t n_pred;              /* length of pred_host                                       */
+  const int32_t* task_item;    /* [T] item of each task                                     */
+  const int64_t* pred_off;     /* [C+1] item c's predecessor placements pred_off[c..c+1)     */
+  const int32_t* pred_host;    /* [n_pred] host index of each placement, -1 = not a host     */
+  const int32_t* item_app;     /* [C] application of each item                               */
+  int32_t n_storage;           /* S = len(cluster.storage)                                   */
+  int32_t reserved;            /* must be 0                                                  */
+  const int32_t* storage_zone; /* [S] zone of each storage, cluster.storage order            */
+  const int32_t* zone_storage; /* [Z] storage index of get_storage_by_locality(zone), -1 None */
+  uint32_t* mt_state;          /* [625] in/out: the policy randomizer (MT19937 key + pos)    */
+  int32_t* status;             /* [2] out: groups formed, error kind                         */
+} pvt_ca_items;
+int  pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* items);
 
 /*
  * Meter aggregates of a batch of S scenarios (replaces the properties

@@ -13,13 +13,22 @@
 //     ONE launch, one block each, so the rounds' sequential walks run side by side on all CUs;
 //   - single rounds of the sim.py sizes (100-1000 hosts, configs 1-2) through pvt_place.
 //
-// A round runs on 4 waves (HPL <= 16 hosts per lane: H <= 4096). Per task each lane reduces
-// its HPL hosts to the best (score bits, tiebreak:host) 128-bit key (scores are >= +0, so bit
-// patterns order like values) and the wave reduces to its minimum with DPP row steps
-// (first-fit: one ballot). Lane 0 posts the wave's minimum in LDS (double-buffered by task
-// parity: ONE barrier per task) and every wave picks the same winner from the four posts. The owning lane commits in its registers. Opportunistic reduces
-// feasible counts instead; every wave draws the same randint(0, n) from its own copy of the
-// MT19937 state (no second barrier), and the lane holding the k-th feasible host commits it.
+// A round runs on WAVES = 4 or 8 waves (one workgroup; HPL = hosts per lane, H <= 256 * 16).
+// Per task, cost_aware and first-fit rounds first look for the FAST winner, a 32-bit host index:
+//   first-fit by index (vbp first-fit, cost_aware first-fit without sort_hosts): the lowest-
+//     index fitting host (blocked host mapping: lane order, then slot order, is index order);
+//   cost_aware best-fit: the lowest-index fitting host of score exactly 0 -- a zero-cost zone
+//     pair (c == 0, bw > 0) or an exact fit (s2 == 0) -- unless some fitting host's score might
+//     underflow to 0 (c < 2^-300, s2 < 2^-600, bw > 2^300, or bw not > 0 with c == 0: "risky");
+//   keyed cost_aware first-fit: the lowest-index fitting host of frozen key exactly +0.
+// Each wave finds its first candidate with one ballot, lane 0 posts it (or "risky") in LDS
+// (double-buffered by task parity: ONE barrier per task) and every wave reads all posts with one
+// LDS load and takes the minimum. Only when no wave has a fast winner (or one is risky) do the
+// waves compute the full 128-bit key (score bits, tiebreak:host) and exchange it after a second
+// barrier; vbp best-fit always does (its scores are norms). Measured at config 4 (512 x 1000 x
+// 1000): every cost_aware best-fit winner scores 0. Opportunistic rounds reduce feasible counts
+// (DPP scan); every wave draws the same randint(0, n) from its own copy of the MT19937 state,
+// and the lane holding the k-th feasible host commits it.
 //
 // Numerics as everywhere in the engine: -ffp-contract=off, sequential-FMA squared norms,
 // correctly rounded sqrt/div, scores computed in the reference's operation order.
@@ -33,7 +42,7 @@
 
 namespace pvt {
 
-constexpr int RES_WAVES = RES_THREADS / WAVE;   // LDS is laid out for the 4-wave variant
+constexpr int RES_MAXW = 8;              // LDS is laid out for up to 8 waves per round
 constexpr int RES_CHUNK = 256;           // tasks whose demand rows are staged in LDS at a time
 constexpr int RES_MT_STRIDE = 628;       // words per wave-private MT19937 copy (625 used)
 constexpr uint64_t NONE = ~0ull;
@@ -49,8 +58,8 @@ struct ResLds {
     cd = u;                                            // walk: demand rows f64[CHUNK][4]
     ci = cd + 32 * RES_CHUNK;                          //       anchor, group i32[2][CHUNK] (+pad)
     mt = ci + 12 * RES_CHUNK;                          //       MT copies u32[WAVES][628]
-    slot = mt + 4 * RES_WAVES * RES_MT_STRIDE;         //       posts u64[2][WAVES][2]
-    const int walk_end = slot + 32 * RES_WAVES;
+    slot = mt + 4 * RES_MAXW * RES_MT_STRIDE;          //       posts u64[2][WAVES][2], then
+    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW;   //   fast posts i32[2][WAVES]
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     total = walk_end > sort_end ? walk_end : sort_end;
   }
@@ -138,6 +147,10 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   // hosts -> registers (padding slots never fit: -inf capacities)
   const int h0 = tid * HPL;
   double a0[HPL], a1[HPL], a2[HPL], a3[HPL], key[HPL], cc[HPL], bb[HPL];
+  // per slot, for the current anchor (cost_aware best-fit) / group key (keyed first-fit):
+  // zmask bit j = a fitting host of slot j scores exactly 0 (c == 0 and bw > 0; keyed: key bits
+  // 0), rmask bit j = its score may underflow to 0 or is not a number (needs the full path)
+  uint32_t zmask = 0, rmask = 0;
   int32_t zz[HPL];
   uint32_t tb[HPL];
 #pragma unroll
@@ -172,6 +185,7 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   uint32_t* mk = reinterpret_cast<uint32_t*>(smem + Lo.mt) + wave * RES_MT_STRIDE;
   uint64_t* posts = reinterpret_cast<uint64_t*>(smem + Lo.slot);   // [2][WAVES][2]
   int32_t* cposts = reinterpret_cast<int32_t*>(posts);              // opp: [2][WAVES]
+  int32_t* fposts = reinterpret_cast<int32_t*>(smem + Lo.slot + 32 * RES_MAXW);   // [2][WAVES]
   MtWave mw;
   mw.buf = 0; mw.used = 0; mw.limit = 0;
   if (MODE == OPP) {
@@ -187,13 +201,13 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
     __syncthreads();                      // the previous chunk (and the sort keys) are consumed
     {
       // every load of the chunk is issued before the first one is waited for
-      constexpr int PER = RES_CHUNK / NT;
+      constexpr int PER = (RES_CHUNK + NT - 1) / NT;
       int tt[PER], gg[PER], aa[PER];
       double dd[PER][4];
 #pragma unroll
       for (int k = 0; k < PER; k++) {
         const int i = tid + k * NT;
-        tt[k] = i < n ? ord[p0 + i] : 0;
+        tt[k] = i < n ? ord[p0 + i] : 0;   // (i >= n: task 0's row, loaded and dropped)
       }
 #pragma unroll
       for (int k = 0; k < PER; k++) {
@@ -241,17 +255,32 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
             cc[j] = csum[anc * Z + zz[j]];
             bb[j] = rt ? (h0 + j < H ? R.rt_bw[(size_t)grp_q * H + h0 + j] : 1.0) : bsum[anc * Z + zz[j]];
           }
+          if (MODE == CA_BF) {
+            zmask = 0; rmask = 0;
+#pragma unroll
+            for (int j = 0; j < HPL; j++) {
+              // safe: bw in (0, 2^300] and c == 0 or c in [2^-300, inf): then a fitting host
+              // scores exactly +0 iff c == 0 or s2 == 0 (s2 finite), and otherwise >= 2^-900
+              // unless s2 < 2^-600
+              const bool safe = bb[j] > 0.0 && bb[j] <= 0x1p+300 &&
+                                (cc[j] == 0.0 || (cc[j] >= 0x1p-300 && cc[j] < DINF));
+              zmask |= ((safe && cc[j] == 0.0) ? 1u : 0u) << j;
+              rmask |= (safe ? 0u : 1u) << j;
+            }
+          }
         }
       }
       if (MODE == CA_FF && keyed) {
         const int g = grp_q;
         if (g != cur_grp) {               // frozen host key of the group (cost_aware.py:104-119)
           cur_grp = g;
+          zmask = 0;
 #pragma unroll
           for (int j = 0; j < HPL; j++) {
             const double r = __builtin_sqrt(norm2_seq(a0[j], a1[j], a2[j], a3[j]));
             const double df = (R.decay && h0 + j < H) ? (double)R.decay[h0 + j] : 1.0;
             key[j] = (cc[j] * df) / (r * bb[j]);
+            zmask |= (dbits(key[j]) == 0 ? 1u : 0u) << j;
           }
         }
       }
@@ -270,11 +299,11 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
         const int wt = __builtin_amdgcn_readlane(inc, 63);
         int ntot = wt, off = 0;
         if (WAVES > 1) {
-          if (lane == 0) cposts[par * RES_WAVES + wave] = wt;
+          if (lane == 0) cposts[par * RES_MAXW + wave] = wt;
           __syncthreads();
           int v[WAVES];
 #pragma unroll
-          for (int w = 0; w < WAVES; w++) v[w] = cposts[par * RES_WAVES + w];
+          for (int w = 0; w < WAVES; w++) v[w] = cposts[par * RES_MAXW + w];
           ntot = 0;
 #pragma unroll
           for (int w = 0; w < WAVES; w++) {
@@ -300,84 +329,113 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
         continue;
       }
 
-      // lane best: (score bits, tiebreak:host), first minimum in host order
-      uint64_t b1 = NONE, b2 = NONE;
-      bool full = true;
-      if (MODE == CA_BF) {
-        // Exact shortcut: 0 is the least score, and a feasible host scores exactly 0 when its
-        // zone pair is free (c == 0) or it fits exactly (s2 == 0). If the wave holds one, its
-        // best is the first such host and no sqrt/div is needed. A score that might underflow
-        // to 0 without c or s2 being 0 (c >= 2^-300, s2 >= 2^-600, b <= 2^300 keep
-        // c * sqrt(s2) / b >= 2^-900) sends the wave down the full path.
-        int32_t zh = 0x7fffffff;
+      // ---- fast winner (32-bit host index; see the header): the lane's first candidate slot
+      constexpr bool FIRST = (MODE == VBP_FF || MODE == CA_FF);   // (CA_FF: unkeyed rounds)
+      constexpr int RISKY = -1;
+      int hw = 0x7fffffff;
+      bool full = (MODE == VBP_BF) || (MODE == CA_FF && keyed);
+      if (MODE != VBP_BF) {
+        int c = 0x7fffffff;
         bool risky = false;
+        if (MODE == CA_BF) {
+          // from the largest residual mx = max(a - d) of a fitting host (all residuals >= +0):
+          // mx == 0 is an exact fit (s2 == 0, score 0); mx >= 2^-300 gives s2 >= 2^-600 (the FMA
+          // chain only adds non-negative terms), so with a safe slot and c > 0 the score is
+          // >= 2^-900; with c == 0 the score is 0 while s2 is finite (mx <= 2^500). Anything
+          // else is risky and goes to the full path.
+#pragma unroll
+          for (int j = HPL - 1; j >= 0; j--) {     // (descending: the lowest candidate slot wins)
+            const bool f = fits<false>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+            const double mx = fmax(fmax(a0[j] - d0, a1[j] - d1), fmax(a2[j] - d2, a3[j] - d3));
+            const bool safe = !((rmask >> j) & 1u), zc = (zmask >> j) & 1u;
+            const bool z = safe && ((zc && mx <= 0x1p+500) || mx == 0.0);
+            c = (f && z) ? h0 + j : c;
+            risky |= f && !z && (!safe || !(mx >= 0x1p-300) || zc);
+          }
+          // (a non-finite demand can leave a NaN residual that fmax drops: full path)
+          risky |= !(__builtin_fabs(d0) < DINF && __builtin_fabs(d1) < DINF &&
+                     __builtin_fabs(d2) < DINF && __builtin_fabs(d3) < DINF);
+        } else {
+#pragma unroll
+          for (int j = HPL - 1; j >= 0; j--) {
+            const bool f = fits<STRICT>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+            c = (f && (!keyed || ((zmask >> j) & 1u))) ? h0 + j : c;
+          }
+        }
+        const uint64_t any = __ballot(c != 0x7fffffff);
+        int wc = any ? __builtin_amdgcn_readlane(c, __builtin_ctzll(any)) : 0x7fffffff;
+        if (MODE == CA_BF && __ballot(risky)) wc = RISKY;   // (RISKY = -1: the signed minimum)
+        int g = wc;
+        if (WAVES > 1) {
+          if (lane == 0) fposts[par * RES_MAXW + wave] = wc;
+          __syncthreads();
+          int v[WAVES];                          // (one LDS load per 4 posts)
+#pragma unroll
+          for (int w = 0; w < WAVES; w++) v[w] = fposts[par * RES_MAXW + w];
+#pragma unroll
+          for (int w = 1; w < WAVES; w++) v[0] = min(v[0], v[w]);
+          g = v[0];
+        }
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (g >= 0 && g != 0x7fffffff) {
+          hw = g;
+          full = false;
+        } else {
+          // no fast winner anywhere: first-fit by index has none at all; cost_aware best-fit
+          // (no score-0 host, or a risky one) and keyed first-fit (no key-0 host) take the full path
+          full = !FIRST || keyed;
+        }
+      }
+      if (full) {
+        // lane best: (score bits, tiebreak:host), first minimum in host order
+        uint64_t b1 = NONE, b2 = NONE;
 #pragma unroll
         for (int j = 0; j < HPL; j++) {
-          const bool f = fits<false>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
-          const double s2 = norm2_seq(a0[j] - d0, a1[j] - d1, a2[j] - d2, a3[j] - d3);
-          if (f && (cc[j] == 0.0 || s2 == 0.0) && zh == 0x7fffffff) zh = h0 + j;
-          risky |= f && cc[j] != 0.0 && s2 != 0.0 &&
-                   (cc[j] < 0x1p-300 || s2 < 0x1p-600 || bb[j] > 0x1p+300);
-        }
-        if (__ballot(zh != 0x7fffffff) != 0 && __ballot(risky) == 0) {
-          full = false;
-          if (zh != 0x7fffffff) { b1 = 0; b2 = (uint32_t)zh; }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < HPL && full; j++) {
-        const bool f = fits<STRICT>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
-        uint64_t k1 = 0;
-        if (MODE == CA_BF || MODE == VBP_BF) {
-          if (f) {
-            const double s = __builtin_sqrt(norm2_seq(a0[j] - d0, a1[j] - d1, a2[j] - d2, a3[j] - d3));
-            // cost_aware.py:83 (c * r * decay / bw, decay == 1); vbp.py:45 (la.norm)
-            k1 = dbits(MODE == CA_BF ? (cc[j] * s) / bb[j] : s);
+          const bool f = fits<STRICT>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+          uint64_t k1 = 0;
+          if (MODE == CA_BF || MODE == VBP_BF) {
+            if (f) {
+              const double s = __builtin_sqrt(norm2_seq(a0[j] - d0, a1[j] - d1, a2[j] - d2, a3[j] - d3));
+              // cost_aware.py:83 (c * r * decay / bw, decay == 1); vbp.py:45 (la.norm)
+              k1 = dbits(MODE == CA_BF ? (cc[j] * s) / bb[j] : s);
+            }
+          } else if (MODE == CA_FF) {
+            k1 = dbits(key[j]);
           }
-        } else if (MODE == CA_FF) {
-          k1 = dbits(key[j]);
+          const uint64_t k2 = ((uint64_t)tb[j] << 32) | (uint32_t)(h0 + j);
+          if (f && (k1 < b1 || (k1 == b1 && k2 < b2))) { b1 = k1; b2 = k2; }
         }
-        const uint64_t k2 = ((uint64_t)tb[j] << 32) | (uint32_t)(h0 + j);
-        if (f && (k1 < b1 || (k1 == b1 && k2 < b2))) { b1 = k1; b2 = k2; }
-      }
-      // wave minimum: score bits first; among tied lanes the first holds the lowest host
-      // (blocked host mapping), except vbp best-fit, whose tiebreak rank precedes the host
-      uint64_t m1, m2;
-      if (MODE == VBP_FF || (MODE == CA_FF && !keyed)) {
-        // first fit by index: the first lane holding a feasible host (blocked host mapping)
-        const uint64_t any = __ballot(b1 != NONE);
-        m1 = any ? 0ull : NONE;
-        m2 = any ? readlane_u64(b2, __builtin_ctzll(any)) : NONE;
-      } else {
-        m1 = wave_min_u64(b1);
+        // wave minimum: score bits first; among tied lanes the first holds the lowest host
+        // (blocked host mapping), except vbp best-fit, whose tiebreak rank precedes the host
+        const uint64_t m1 = wave_min_u64(b1);
         const uint64_t tied = __ballot(b1 == m1);
-        m2 = readlane_u64(b2, __builtin_ctzll(tied));
+        uint64_t m2 = readlane_u64(b2, __builtin_ctzll(tied));
         if (MODE == VBP_BF && __popcll(tied) > 1) m2 = wave_min_u64((b1 == m1) ? b2 : NONE);
-      }
-      uint64_t g2 = m2;
-      if (WAVES > 1) {
-        if (lane == 0) {
-          posts[(par * RES_WAVES + wave) * 2 + 0] = m1;
-          posts[(par * RES_WAVES + wave) * 2 + 1] = m2;
-        }
-        __syncthreads();
-        uint64_t v1[WAVES], v2[WAVES];         // all posts in flight at once, then compared
+        uint64_t g2 = m2;
+        if (WAVES > 1) {
+          if (lane == 0) {
+            posts[(par * RES_MAXW + wave) * 2 + 0] = m1;
+            posts[(par * RES_MAXW + wave) * 2 + 1] = m2;
+          }
+          __syncthreads();
+          uint64_t v1[WAVES], v2[WAVES];         // all posts in flight at once, then compared
 #pragma unroll
-        for (int w = 0; w < WAVES; w++) {
-          v1[w] = posts[(par * RES_WAVES + w) * 2 + 0];
-          v2[w] = posts[(par * RES_WAVES + w) * 2 + 1];
-        }
-        uint64_t g1 = v1[0];
-        g2 = v2[0];
+          for (int w = 0; w < WAVES; w++) {
+            v1[w] = posts[(par * RES_MAXW + w) * 2 + 0];
+            v2[w] = posts[(par * RES_MAXW + w) * 2 + 1];
+          }
+          uint64_t g1 = v1[0];
+          g2 = v2[0];
 #pragma unroll
-        for (int w = 1; w < WAVES; w++) {
-          const bool lt = (v1[w] < g1) | ((v1[w] == g1) & (v2[w] < g2));
-          g1 = lt ? v1[w] : g1;
-          g2 = lt ? v2[w] : g2;
+          for (int w = 1; w < WAVES; w++) {
+            const bool lt = (v1[w] < g1) | ((v1[w] == g1) & (v2[w] < g2));
+            g1 = lt ? v1[w] : g1;
+            g2 = lt ? v2[w] : g2;
+          }
         }
+        if (g2 != NONE) hw = __builtin_amdgcn_readfirstlane((int)(uint32_t)g2);
       }
-      if (g2 == NONE) continue;          // no host fits: the task stays waiting
-      const int hw = __builtin_amdgcn_readfirstlane((int)(uint32_t)g2);
+      if (hw == 0x7fffffff) continue;    // no host fits: the task stays waiting
       const int jw = hw & (HPL - 1);     // uniform: the owning lane's register slot
       if (hw / HPL == tid) {
 #pragma unroll
@@ -407,27 +465,43 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   }
 }
 
-// Four waves per round (one per SIMD of a CU). Measured on MI355X with 512 rounds of 1000 hosts
-// x 1000 tasks: one wave per round (16 hosts per lane, no barrier) is ~2x slower -- a single
-// wave's dependent per-task chain cannot hide its own latencies.
-template <int MODE>
-static void launch_mode(int waves, int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
-  const dim3 grid(n), four(4 * WAVE);
-  (void)waves;
+// Four or eight waves per round (one or two per SIMD of a CU). Measured on MI355X with 512
+// rounds of 1000 hosts x 1000 tasks: one wave per round (16 hosts per lane, no barrier) is ~2x
+// slower than four -- a single wave's dependent per-task chain cannot hide its own latencies.
+template <int MODE, int W>
+static void launch_waves(int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
+  const dim3 grid(n), block(W * WAVE);
   switch (hpl) {
-    case 1: hipLaunchKernelGGL((resident_kernel<MODE, 4, 1>), grid, four, lds, st, a); break;
-    case 2: hipLaunchKernelGGL((resident_kernel<MODE, 4, 2>), grid, four, lds, st, a); break;
-    case 4: hipLaunchKernelGGL((resident_kernel<MODE, 4, 4>), grid, four, lds, st, a); break;
-    case 8: hipLaunchKernelGGL((resident_kernel<MODE, 4, 8>), grid, four, lds, st, a); break;
-    default: hipLaunchKernelGGL((resident_kernel<MODE, 4, 16>), grid, four, lds, st, a); break;
+    case 1: hipLaunchKernelGGL((resident_kernel<MODE, W, 1>), grid, block, lds, st, a); break;
+    case 2: hipLaunchKernelGGL((resident_kernel<MODE, W, 2>), grid, block, lds, st, a); break;
+    case 4: hipLaunchKernelGGL((resident_kernel<MODE, W, 4>), grid, block, lds, st, a); break;
+    case 8: hipLaunchKernelGGL((resident_kernel<MODE, W, 8>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((resident_kernel<MODE, 4, 16>), grid, dim3(4 * WAVE), lds, st, a); break;
   }
 }
+template <int MODE>
+static void launch_two(int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
+  const dim3 grid(n), block(2 * WAVE);
+  switch (hpl) {
+    case 8: hipLaunchKernelGGL((resident_kernel<MODE, 2, 8>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((resident_kernel<MODE, 2, 16>), grid, block, lds, st, a); break;
+  }
+}
+template <int MODE>
+static void launch_mode(int waves, int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
+  if (waves == 8 && hpl <= 8) launch_waves<MODE, 8>(hpl, n, lds, a, st);
+  else if (waves == 2 && hpl >= 8) launch_two<MODE>(hpl, n, lds, a, st);
+  else launch_waves<MODE, 4>(hpl, n, lds, a, st);
+}
 
-// Hosts per lane for a batch whose largest round has maxH hosts (4 waves: 256 lanes).
+// Waves and hosts per lane for a batch whose largest round has maxH hosts: `waves` (4 or 8) on
+// entry is the preference; 8 waves only while the round needs at most 8 hosts per lane.
 void resident_shape(int maxH, int* waves, int* hpl) {
+  const int w = (*waves == 8 && maxH <= 8 * 8 * WAVE) ? 8
+                : (*waves == 2 && maxH > 4 * 4 * WAVE && maxH <= 2 * 16 * WAVE) ? 2 : 4;
   int h = 1;
-  while (h * RES_THREADS < maxH) h <<= 1;
-  *waves = 4;
+  while (h * w * WAVE < maxH) h <<= 1;
+  *waves = w;
   *hpl = h;
 }
 
@@ -451,6 +525,8 @@ static hipError_t attrs_mode(int lds) {
                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);                      \
   if (r != hipSuccess) e = r;
   PVT_RES_ATTR(4, 1) PVT_RES_ATTR(4, 2) PVT_RES_ATTR(4, 4) PVT_RES_ATTR(4, 8) PVT_RES_ATTR(4, 16)
+  PVT_RES_ATTR(8, 1) PVT_RES_ATTR(8, 2) PVT_RES_ATTR(8, 4) PVT_RES_ATTR(8, 8)
+  PVT_RES_ATTR(2, 8) PVT_RES_ATTR(2, 16)
 #undef PVT_RES_ATTR
   return e;
 }

@@ -27,6 +27,7 @@
 #include "pvt_kernels.h"
 #include "pvt_opp.h"
 #include "pvt_anchor.h"
+#include "pvt_groups.h"
 #include "pvt_meter.h"
 
 using namespace pvt;
@@ -126,6 +127,8 @@ struct RoundState {
   bool of_try = false;            // ordered rounds: a frontier attempt comes next
   int of_n = 0, of_hs = 0;        //   the scored attempt's tasks and host span
   bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
+  bool ffe = false;               // keyed rounds: first-fit zero-key epochs (ff_epoch)
+  int ffe_skip = -1;              //   the group they could not start (the keyed path takes it)
   // vbp best-fit band lists (pvt_band.hip): the sorted snapshot of hosts [lo, hi) is built; a
   // walk whose committed hosts are not yet flagged as touched (its own-ids buffer)
   bool band = false;
@@ -176,6 +179,7 @@ struct pvt_ctx {
   int t_of_hosts = 0;             // PVT_OF_HOSTS: ordered frontier host span (0: default)
   int t_epoch_plan = 1;           // PVT_EPOCH_PLAN: 0 = epoch chains by distinct zone only
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
+  int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
@@ -188,6 +192,9 @@ struct pvt_ctx {
   void* gstage = nullptr;         // grouped order: counts, anchors, cost table (pinned)
   size_t gstage_cap = 0;
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
+  void* hst = nullptr;            // pvt_place_host: pinned staging of a host-memory round
+  size_t hst_cap = 0;
+  Buf hdev;                       //   and its device copy
 };
 
 static int fail(pvt_ctx* c, int code, const char* fmt, ...) {
@@ -344,6 +351,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_OF_HOSTS")) ctx->t_of_hosts = std::max(ZW_M, atoi(e));   // tuning
   if (const char* e = getenv("PVT_EPOCH_PLAN")) ctx->t_epoch_plan = atoi(e);           // A/B
   if (const char* e = getenv("PVT_MERGE_SMALL")) ctx->t_merge_bitonic = atoi(e) == 0;  // A/B
+  if (const char* e = getenv("PVT_RES_WAVES")) ctx->res_waves = atoi(e) == 8 ? 8 : atoi(e) == 2 ? 2 : 4;  // A/B
   *out = ctx;
   return PVT_OK;
 }
@@ -358,7 +366,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->sorttmp, &ctx->dem_ord, &ctx->anc_ord, &ctx->grp_ord, &ctx->csum, &ctx->bsum, &ctx->key,
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
-                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->oppfault, &ctx->kskey, &ctx->kperm, &ctx->kiota,
+                 &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->oppfault, &ctx->hdev, &ctx->kskey, &ctx->kperm, &ctx->kiota,
                  &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
                  &ctx->btcnt, &ctx->bsorttmp, &ctx->brow[0], &ctx->brow[1], &ctx->brdem[0],
@@ -369,6 +377,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   if (ctx->next_host) (void)hipHostFree(ctx->next_host);
   if (ctx->ep_host) (void)hipHostFree(ctx->ep_host);
   if (ctx->gstage) (void)hipHostFree(ctx->gstage);
+  if (ctx->hst) (void)hipHostFree(ctx->hst);
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
   if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -777,6 +786,8 @@ static void flush_touched(pvt_ctx* ctx) {
 // pvt_place() and the sharded calls share one round: begin (order, gathers, zone tables, group
 // boundaries), then per window: candidate lists over this context's host range (optionally
 // exchanged between ranks), then the commit walk, which decides where the next window starts.
+static int zero_cost_components(pvt_ctx* ctx);
+
 static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int world) {
   RoundState& R = ctx->rs;
   R.active = false;
@@ -894,6 +905,16 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   }
   R.gstart.push_back(T);
   R.ngroups = R.keyed ? R.ganchor.size() : 1;
+  // keyed first-fit: zero-key epochs (ff_epoch) over the groups, unsharded rounds
+  R.ffe = false;
+  R.ffe_skip = -1;
+  if (R.keyed && !R.sharded && ctx->zwalk && ctx->epochs && !r->rt_bw && Z <= ZMAX &&
+      T >= KEYED_FRONTIER_MIN) {
+    R.egs = R.gstart;
+    R.ega = R.ganchor;
+    if ((rc = zero_cost_components(ctx))) return rc;
+    R.ffe = true;
+  }
   R.key_group = -1;
   R.touch_lb = -1;
   R.band = r->mode == PVT_VBP_BF && ctx->band_min > 0 && hi - lo >= ctx->band_min;
@@ -942,8 +963,12 @@ static int keyed_full_sort(pvt_ctx* ctx) {
   return PVT_OK;
 }
 
+static int ff_epoch(pvt_ctx* ctx, int* adv_out);
+
 // Size of the next window at R.t0 (0: the round is done). Computes the frozen first-fit key of
 // this context's hosts at a group start (cost_aware.py:118-119, on the current capacities).
+// Keyed rounds first try zero-key epochs at each group start (ff_epoch): whole groups proven by
+// the first-fit chain walk need no key at all.
 static int round_next_window(pvt_ctx* ctx, int* nt_out) {
   RoundState& R = ctx->rs;
   *nt_out = 0;
@@ -953,6 +978,12 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
   if (R.g >= R.ngroups || R.T == 0) return PVT_OK;
   const int ge = R.keyed ? R.gstart[R.g + 1] : R.T;
   int rc = 0;
+  if (R.ffe && R.t0 == R.gstart[R.g] && R.key_group != (int)R.g && R.ffe_skip != (int)R.g) {
+    int adv = 0;
+    if ((rc = ff_epoch(ctx, &adv))) return rc;
+    if (adv > 0) { R.t0 += adv; continue; }
+    R.ffe_skip = (int)R.g;          // (this group goes to the keyed path below)
+  }
   if (R.kstall) {                 // same group, frozen keys: complete the order
     R.kstall = false;
     if (R.key_group == (int)R.g && R.kmode == 1 && (rc = keyed_full_sort(ctx))) return rc;
@@ -1320,6 +1351,31 @@ static int place_pipelined(pvt_ctx* ctx) {
 }
 
 // ---------------------------------------------------------------- group-parallel epochs
+// Zones joined by zero egress cost (csum = 0) form one component: a group's winners are the
+// lowest-index fitting hosts of its anchor's component (score 0), so two groups anchored in one
+// component compete for the same hosts and an epoch never holds both (R.ecomp: zone -> root).
+static int zero_cost_components(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  const int Z = R.Z;
+  std::vector<double> cost((size_t)Z * Z);
+  if (R.ginfo && R.cost_host.size() == cost.size()) {
+    cost = R.cost_host;
+  } else {
+    HIPCHK(hipMemcpyAsync(cost.data(), r->cost, sizeof(double) * Z * Z, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
+  R.ecomp.resize(Z);
+  for (int z = 0; z < Z; z++) R.ecomp[z] = z;
+  auto root = [&](int z) { while (R.ecomp[z] != z) z = R.ecomp[z] = R.ecomp[R.ecomp[z]]; return z; };
+  const int plan = ctx->t_epoch_plan;   // (PVT_EPOCH_PLAN=0: distinct zones only)
+  for (int a = 0; a < Z && plan; a++)
+    for (int z = 0; z < Z; z++)
+      if (cost[(size_t)a * Z + z] + cost[(size_t)z * Z + a] == 0.0) R.ecomp[root(a)] = root(z);
+  for (int z = 0; z < Z; z++) R.ecomp[z] = root(z);
+  return PVT_OK;
+}
+
 // cost_aware best-fit rounds of several groups (pvt_epoch.hip). The groups in processing
 // order, from the caller's task_group / group_anchor (a group's tasks are contiguous).
 static int epoch_groups(pvt_ctx* ctx) {
@@ -1330,6 +1386,7 @@ static int epoch_groups(pvt_ctx* ctx) {
   const int T = R.T;
   if (!ctx->epochs || r->mode != PVT_CA_BF || !r->task_group || r->n_groups < 2 || T < 2) return PVT_OK;
   hipStream_t st = ctx->stream;
+  int rc;
   std::vector<int> cnt(r->n_groups, 0);
   std::vector<int32_t> ga;
   if (R.ginfo) {                              // copied by build_order
@@ -1356,32 +1413,14 @@ static int epoch_groups(pvt_ctx* ctx) {
     ng++;
   }
   R.egs.push_back(T);
-  // Zones joined by zero egress cost (csum = 0) form one component: a group's winners are the
-  // lowest-index fitting hosts of its anchor's component (score 0), so two groups anchored in
-  // one component compete for the same hosts and an epoch never holds both.
-  const int Z = R.Z;
-  std::vector<double> cost((size_t)Z * Z);
-  if (R.ginfo && R.cost_host.size() == cost.size()) {
-    cost = R.cost_host;
-  } else {
-    HIPCHK(hipMemcpyAsync(cost.data(), r->cost, sizeof(double) * Z * Z, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-  }
-  R.ecomp.resize(Z);
-  for (int z = 0; z < Z; z++) R.ecomp[z] = z;
-  auto root = [&](int z) { while (R.ecomp[z] != z) z = R.ecomp[z] = R.ecomp[R.ecomp[z]]; return z; };
-  const int plan = ctx->t_epoch_plan;   // (PVT_EPOCH_PLAN=0: distinct zones only)
-  for (int a = 0; a < Z && plan; a++)
-    for (int z = 0; z < Z; z++)
-      if (cost[(size_t)a * Z + z] + cost[(size_t)z * Z + a] == 0.0) R.ecomp[root(a)] = root(z);
-  for (int z = 0; z < Z; z++) R.ecomp[z] = root(z);
+  if ((rc = zero_cost_components(ctx))) return rc;
   // worth it when groups are many and short (a group longer than a walk's window is walked in
   // sequential epochs of one segment, without the score / walk pipeline of place_pipelined)
   if (ng < 2 || T > ng * MAX_WINDOW) { R.egs.clear(); R.ega.clear(); }
   return PVT_OK;
 }
 
-static void epoch_plan(const RoundState& R, int t0, EpochPlan& P) {
+static void epoch_plan(const RoundState& R, int t0, EpochPlan& P, bool whole = false) {
   P.off.assign(1, 0);
   P.chain.clear(); P.cstart.clear(); P.segs.clear(); P.len.clear();
   size_t g = 0;
@@ -1399,7 +1438,10 @@ static void epoch_plan(const RoundState& R, int t0, EpochPlan& P) {
       P.len.push_back(0);
     }
     const int take = std::min({ge - t, CHAIN_MAX - P.len[c], t0 + EPOCH_MAX - t});
-    if (take <= 0) break;
+    if (take <= 0 || (whole && take < ge - t)) {
+      if (P.len[c] == 0) { P.segs.pop_back(); P.len.pop_back(); }   // (a chain opened for it)
+      break;
+    }
     P.segs[c].push_back((int)P.chain.size());
     P.chain.push_back(c);
     P.cstart.push_back(P.len[c]);
@@ -1431,6 +1473,71 @@ static int upload_chain_tables(pvt_ctx* ctx, const EpochPlan& E) {
   host[EP_CSOFF + nch] = ns;
   HIPCHK(hipMemcpyAsync(ctx->ep_dev.p, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice,
                         ctx->stream));
+  return PVT_OK;
+}
+
+// cost_aware first-fit with sort_hosts (cost_aware.py:99-127): an epoch of WHOLE groups from
+// the group start R.t0, chains of zero-cost components walked side by side by the first-fit
+// zero-key chain walk (pvt_zwalk.hip, FF). Every task it proves takes the lowest-index strictly
+// fitting host of its anchor's zero-cost zones -- the first host of the frozen key order -- and
+// chains of different components touch disjoint hosts that are never zero-key for another
+// chain's anchors, so no pair validation is needed. Groups are accepted whole, in order, up to
+// the first one a chain did not complete (the keyed path then takes that group from its start,
+// computing its frozen key on the capacities at the group start, as the reference does).
+static int ff_epoch(pvt_ctx* ctx, int* adv_out) {
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  hipStream_t st = ctx->stream;
+  *adv_out = 0;
+  const int t0 = R.t0;
+  EpochPlan E;
+  epoch_plan(R, t0, E, true);
+  const int nseg = (int)E.chain.size(), nch = (int)E.segs.size();
+  if (nseg == 0 || nch == 0) return PVT_OK;
+  const int nt = E.off.back();
+  ENSURE(ctx->ep_dev, sizeof(int32_t) * EP_WORDS);
+  ENSURE(ctx->wres, sizeof(WinRec) * (size_t)EPOCH_MAX);
+  ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+  int32_t* dev = P<int32_t>(ctx->ep_dev);
+  int32_t* host = ctx->ep_host;
+  int rc;
+  {
+    Scope sc(ctx, PVT_K_OTHER, 0, 0);
+    launch_host_absmax(r->avail, R.H, 0, R.H, P<double>(ctx->hmin), st);
+  }
+  if ((rc = upload_chain_tables(ctx, E))) return rc;
+  ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
+               P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
+               P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
+               P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
+               nullptr, 0, 0, 0, nullptr, nullptr, nullptr, dev + EP_CSOFF, dev + EP_CSEG};
+  {
+    Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
+    launch_zwalk_ff(za, nch, st);
+  }
+  EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
+               P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_SEG_OFF,
+               dev + EP_SEG_CHAIN, dev + EP_SEG_CSTART, dev + EP_STATUS, P<WinRec>(ctx->wres),
+               r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD, nullptr, P<int32_t>(ctx->grp_ord) + t0, 1};
+  {
+    Scope sc(ctx, PVT_K_OTHER, 0, 0);
+    launch_epoch_final(ea, st);
+    launch_epoch_accept_apply(ea, dev + EP_RES, nch, st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
+                        hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  ctx->n_epochs++;
+  ctx->n_segs += nseg;
+  int proven = 0;
+  for (int c = 0; c < nch; c++) proven += host[EP_STATUS + 2 * c] == E.len[c];
+  ctx->n_zchains += proven;
+  ctx->n_longest += *std::max_element(E.len.begin(), E.len.end());
+  ctx->n_rejected += host[EP_RES + 3];
+  const int adv = host[EP_RES + 1];
+  if (adv < 0 || adv > nt) return fail(ctx, PVT_EHIP, "first-fit epoch returned %d of %d tasks", adv, nt);
+  *adv_out = adv;
   return PVT_OK;
 }
 
@@ -1592,7 +1699,10 @@ static bool resident_fits(const pvt_round* r, int max_hosts) {
          r->n_tasks <= PVT_RESIDENT_MAX_TASKS;
 }
 
-static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n) {
+// desc_dev: the rounds' descriptors already on the device (pvt_place_host's staging, MT states
+// at mt_dev): nothing is copied and nothing waited for here; the caller copies back and syncs.
+static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
+                          const void* desc_dev = nullptr, uint32_t* mt_dev = nullptr) {
   const int mode = rounds[0].mode;
   int maxH = 1, maxT = 1, maxZ = 1;
   for (int i = 0; i < n; i++) {
@@ -1609,10 +1719,27 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n) {
   }
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
-  int waves = 1, hpl = 1;
+  int waves = ctx->res_waves, hpl = 1;
   resident_shape(maxH, &waves, &hpl);
   int tpad = 64;
   while (tpad < maxT) tpad <<= 1;
+  double cand = 0.0, bytes = 0.0;
+  for (int i = 0; i < n; i++) {
+    const double c = (double)rounds[i].n_tasks * rounds[i].n_hosts;
+    cand += c;
+    bytes += c * bytes_per_candidate(mode);
+  }
+  if (desc_dev) {
+    ResidentArgs ra{desc_dev, mt_dev, maxZ, tpad};
+    {
+      Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
+      launch_resident(mode, waves, hpl, n, ra, st);
+    }
+    HIPCHK(hipGetLastError());
+    ctx->windows = n;
+    ctx->refills = 0;
+    return PVT_OK;
+  }
   ctx->rstage.assign(rounds, rounds + n);
   ENSURE(ctx->rdesc, sizeof(pvt_round) * (size_t)n);
   uint32_t* mt = nullptr;
@@ -1628,12 +1755,6 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n) {
   }
   HIPCHK(hipMemcpyAsync(ctx->rdesc.p, ctx->rstage.data(), sizeof(pvt_round) * n, hipMemcpyHostToDevice, st));
   ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad};
-  double cand = 0.0, bytes = 0.0;
-  for (int i = 0; i < n; i++) {
-    const double c = (double)rounds[i].n_tasks * rounds[i].n_hosts;
-    cand += c;
-    bytes += c * bytes_per_candidate(mode);
-  }
   {
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mode, waves, hpl, n, ra, st);
@@ -1723,14 +1844,10 @@ extern "C" int pvt_set_resident(pvt_ctx* ctx, int32_t max_hosts) {
   return PVT_OK;
 }
 
-extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
-  if (!ctx) return PVT_EINVAL;
-  int rc = check_round(ctx, r);
-  if (rc) return rc;
-  if (r->n_tasks > 0 && resident_fits(r, ctx->resident_max)) {
-    ctx->rs.active = false;
-    return place_resident(ctx, r, 1);
-  }
+// The windowed / epoch / opportunistic engines on a checked round of device arrays (pvt_place
+// without the resident case); synchronises before returning.
+static int place_windowed(pvt_ctx* ctx, const pvt_round* r) {
+  int rc;
   if (r->mode == PVT_OPP) {
     ctx->rs.active = false;
     ctx->windows = ctx->refills = 0;
@@ -1752,6 +1869,194 @@ extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
     return rc;
   }
   HIPCHK(hipStreamSynchronize(ctx->stream));
+  return PVT_OK;
+}
+
+extern "C" int pvt_place(pvt_ctx* ctx, const pvt_round* r) {
+  if (!ctx) return PVT_EINVAL;
+  int rc = check_round(ctx, r);
+  if (rc) return rc;
+  if (r->n_tasks > 0 && resident_fits(r, ctx->resident_max)) {
+    ctx->rs.active = false;
+    return place_resident(ctx, r, 1);
+  }
+  return place_windowed(ctx, r);
+}
+
+// ---------------------------------------------------------------- drop-in rounds, host memory
+static int ensure_pinned(pvt_ctx* ctx, size_t bytes) {
+  if (ctx->hst_cap >= bytes) return PVT_OK;
+  const size_t want = std::max({bytes, ctx->hst_cap * 3 / 2, (size_t)1 << 16});
+  if (ctx->hst) (void)hipHostFree(ctx->hst);
+  ctx->hst = nullptr;
+  ctx->hst_cap = 0;
+  if (hipHostMalloc(&ctx->hst, want) != hipSuccess) {
+    ctx->hst = nullptr;
+    return fail(ctx, PVT_ENOMEM, "hipHostMalloc(%zu) failed", want);
+  }
+  ctx->hst_cap = want;
+  return PVT_OK;
+}
+
+extern "C" int pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* it) {
+  if (!ctx || !r) return PVT_EINVAL;
+  const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
+  const int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
+  if (it) {
+    if (!ca) return fail(ctx, PVT_EINVAL, "pvt_ca_items need a cost_aware round");
+    if (it->reserved != 0 || it->n_items < 0 || it->n_apps < 0 || it->n_pred < 0 || it->n_storage < 0)
+      return fail(ctx, PVT_EINVAL, "bad sizes in pvt_ca_items");
+    if (r->task_group || r->group_anchor || r->rt_bw)
+      return fail(ctx, PVT_EINVAL, "pvt_ca_items replace task_group / group_anchor (realtime_bw "
+                  "rows are per group: use pvt_anchor + pvt_place)");
+    if (!it->status || (T > 0 && (!it->task_item || !it->pred_off || (it->n_pred && !it->pred_host) ||
+                                  (it->n_items && !it->item_app) || !it->storage_zone ||
+                                  !it->zone_storage || !it->mt_state)))
+      return fail(ctx, PVT_EINVAL, "null pointer in pvt_ca_items");
+    it->status[0] = it->status[1] = 0;
+    if (T > GRP_MAX_TASKS || it->n_storage + it->n_apps > GRP_MAX_KEYS || it->n_storage < 1)
+      return fail(ctx, PVT_EUNSUPPORTED, "fused grouping limits: T=%d (max %d), %d storages + %d "
+                  "applications (max %d, at least one storage)", T, GRP_MAX_TASKS, it->n_storage,
+                  it->n_apps, GRP_MAX_KEYS);
+    if (Z < 1 || Z > ZMAX) return fail(ctx, PVT_EINVAL, "bad sizes H=%d T=%d Z=%d", H, T, Z);
+    for (int k = 0; k < it->n_storage; k++)
+      if (it->storage_zone[k] < 0 || it->storage_zone[k] >= Z)
+        return fail(ctx, PVT_EINVAL, "storage %d: zone %d outside [0, %d)", k, it->storage_zone[k], Z);
+    for (int z = 0; z < Z; z++)
+      if (it->zone_storage[z] < -1 || it->zone_storage[z] >= it->n_storage)
+        return fail(ctx, PVT_EINVAL, "zone %d: storage %d outside [-1, %d)", z, it->zone_storage[z], it->n_storage);
+    for (int c = 0; c <= it->n_items && T > 0; c++)   // (the anchor kernels check each range too)
+      if (it->pred_off[c] < 0 || it->pred_off[c] > it->n_pred || (c && it->pred_off[c] < it->pred_off[c - 1]))
+        return fail(ctx, PVT_EINVAL, "pred_off[%d] = %lld out of order or range", c, (long long)it->pred_off[c]);
+  }
+  pvt_round hr = *r;                  // (the grouped fields stand in for the device's groups)
+  static const int32_t one = 0;
+  if (it) { hr.task_group = &one; hr.group_anchor = &one; hr.n_groups = 1; }
+  int rc = check_round(ctx, &hr);
+  if (rc) return rc;
+  ctx->rs.active = false;
+  if (T == 0) return PVT_OK;
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const bool resident = resident_fits(&hr, ctx->resident_max);
+  const int C = it ? it->n_items : 0, S = it ? it->n_storage : 0;
+  const int64_t NP = it ? it->n_pred : 0;
+  const int G = it ? T : (r->task_group ? r->n_groups : 0);
+  const int GR = r->rt_bw ? std::max(r->task_group ? r->n_groups : 1, 1) : 0;
+  size_t o = 0;
+  auto take = [&](size_t bytes) { const size_t at = o; o = (o + bytes + 255) / 256 * 256; return at; };
+  // out region (copied back): avail, placement, order, MT states, grouping status
+  const size_t o_av = take(32 * (size_t)H), o_pl = take(4 * (size_t)T), o_or = take(4 * (size_t)T);
+  const size_t o_mt = r->mt_state ? take(4 * 625) : 0, o_cmt = it ? take(4 * 625) : 0;
+  const size_t o_st = it ? take(16) : 0;
+  const size_t n_out = o;
+  const size_t o_zone = take(4 * (size_t)H);
+  const size_t o_tb = r->tiebreak ? take(4 * (size_t)H) : 0, o_dc = r->decay ? take(4 * (size_t)H) : 0;
+  const size_t o_cost = take(8 * (size_t)Z * Z), o_bw = take(8 * (size_t)Z * Z);
+  const size_t o_dem = take(32 * (size_t)T);
+  const size_t o_tg = (it || r->task_group) ? take(4 * (size_t)T) : 0;
+  const size_t o_ga = (it || r->task_group) ? take(4 * (size_t)std::max(G, 1)) : 0;
+  const size_t o_rt = GR ? take(8 * (size_t)GR * H) : 0;
+  const size_t o_ti = it ? take(4 * (size_t)T) : 0, o_off = it ? take(8 * (size_t)(C + 1)) : 0;
+  const size_t o_ph = it ? take(4 * (size_t)std::max<int64_t>(NP, 1)) : 0;
+  const size_t o_ia = it ? take(4 * (size_t)std::max(C, 1)) : 0, o_sz = it ? take(4 * (size_t)S) : 0;
+  const size_t o_zs = it ? take(4 * (size_t)Z) : 0, o_mh = it ? take(4 * (size_t)std::max(C, 1)) : 0;
+  const size_t o_az = it ? take(4 * (size_t)std::max(C, 1)) : 0;
+  const size_t o_ab = it ? take(16 + 4 * (size_t)std::max(C, 1)) : 0;
+  const size_t o_desc = take(sizeof(pvt_round));
+  if ((rc = ensure_pinned(ctx, o))) return rc;
+  ENSURE(ctx->hdev, o);
+  char* hb = static_cast<char*>(ctx->hst);
+  char* db = static_cast<char*>(ctx->hdev.p);
+  auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) std::memcpy(hb + at, src, bytes); };
+  put(o_av, r->avail, 32 * (size_t)H);
+  if (r->mt_state) put(o_mt, r->mt_state, 4 * 625);
+  if (it) { put(o_cmt, it->mt_state, 4 * 625); std::memset(hb + o_st, 0, 16); }
+  put(o_zone, r->zone, 4 * (size_t)H);
+  if (r->tiebreak) put(o_tb, r->tiebreak, 4 * (size_t)H);
+  if (r->decay) put(o_dc, r->decay, 4 * (size_t)H);
+  put(o_cost, r->cost ? r->cost : nullptr, r->cost ? 8 * (size_t)Z * Z : 0);
+  put(o_bw, r->bw ? r->bw : nullptr, r->bw ? 8 * (size_t)Z * Z : 0);
+  put(o_dem, r->dem, 32 * (size_t)T);
+  if (r->task_group) { put(o_tg, r->task_group, 4 * (size_t)T); put(o_ga, r->group_anchor, 4 * (size_t)G); }
+  if (GR) put(o_rt, r->rt_bw, 8 * (size_t)GR * H);
+  if (it) {
+    put(o_ti, it->task_item, 4 * (size_t)T);
+    put(o_off, it->pred_off, 8 * (size_t)(C + 1));
+    put(o_ph, it->pred_host, 4 * (size_t)NP);
+    put(o_ia, it->item_app, 4 * (size_t)C);
+    put(o_sz, it->storage_zone, 4 * (size_t)S);
+    put(o_zs, it->zone_storage, 4 * (size_t)Z);
+    std::memset(hb + o_ab, 0, 16);
+  }
+  // the device round: arrays in the staging buffer (the MT state of a windowed opportunistic
+  // round stays a host pointer: opp_round moves it itself)
+  pvt_round d = hr;
+  d.avail = reinterpret_cast<double*>(db + o_av);
+  d.zone = reinterpret_cast<const int32_t*>(db + o_zone);
+  d.tiebreak = r->tiebreak ? reinterpret_cast<const uint32_t*>(db + o_tb) : nullptr;
+  d.decay = r->decay ? reinterpret_cast<const int32_t*>(db + o_dc) : nullptr;
+  d.cost = r->cost ? reinterpret_cast<const double*>(db + o_cost) : nullptr;
+  d.bw = r->bw ? reinterpret_cast<const double*>(db + o_bw) : nullptr;
+  d.dem = reinterpret_cast<const double*>(db + o_dem);
+  d.task_group = o_tg ? reinterpret_cast<const int32_t*>(db + o_tg) : nullptr;
+  d.group_anchor = o_ga ? reinterpret_cast<const int32_t*>(db + o_ga) : nullptr;
+  d.rt_bw = GR ? reinterpret_cast<const double*>(db + o_rt) : nullptr;
+  d.placement = reinterpret_cast<int32_t*>(db + o_pl);
+  d.order = reinterpret_cast<int32_t*>(db + o_or);
+  const bool dev_mt = r->mt_state && resident;
+  d.mt_state = dev_mt ? reinterpret_cast<uint32_t*>(db + o_mt) : r->mt_state;
+  std::memcpy(hb + o_desc, &d, sizeof(pvt_round));
+  HIPCHK(hipMemcpyAsync(db, hb, o, hipMemcpyHostToDevice, st));
+  if (it) {
+    int32_t* ab = reinterpret_cast<int32_t*>(db + o_ab);
+    AnchorArgs k{C, H, NP, 0, 0, reinterpret_cast<const int64_t*>(db + o_off), nullptr,
+                 reinterpret_cast<const int32_t*>(db + o_ph), nullptr, d.zone,
+                 reinterpret_cast<int32_t*>(db + o_mh), reinterpret_cast<int32_t*>(db + o_az), ab,
+                 ab + 4, ab + 1};
+    CaGroupArgs g{T, C, Z, S, it->n_apps, reinterpret_cast<const int32_t*>(db + o_ti),
+                  reinterpret_cast<const int32_t*>(db + o_az), reinterpret_cast<const int32_t*>(db + o_ia),
+                  reinterpret_cast<const int32_t*>(db + o_sz), reinterpret_cast<const int32_t*>(db + o_zs),
+                  reinterpret_cast<uint32_t*>(db + o_cmt), reinterpret_cast<int32_t*>(db + o_tg),
+                  reinterpret_cast<int32_t*>(db + o_ga), reinterpret_cast<int32_t*>(db + o_st),
+                  resident ? &reinterpret_cast<pvt_round*>(db + o_desc)->n_groups : nullptr};
+    {
+      Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * (double)NP);
+      if (C > 0) launch_anchor(k, st);
+      launch_ca_groups(g, st);
+    }
+    HIPCHK(hipGetLastError());
+  }
+  int32_t* hst_status = reinterpret_cast<int32_t*>(hb + o_st);
+  auto group_error = [&]() -> int {
+    const int e = hst_status[1];
+    it->status[0] = hst_status[0];
+    it->status[1] = e;
+    if (!e) return PVT_OK;
+    return fail(ctx, PVT_EINVAL, "%s", e == 1 ? "a mode predecessor placement is not a host of the cluster" :
+                e == 2 ? "an anchor zone has no storage (get_storage_by_locality -> None)" :
+                "malformed anchor item lists");
+  };
+  if (resident) {
+    if ((rc = place_resident(ctx, &d, 1, db + o_desc, dev_mt ? reinterpret_cast<uint32_t*>(db + o_mt) : nullptr)))
+      return rc;
+  } else {
+    if (it) {                         // the windowed engine plans groups on the host
+      HIPCHK(hipMemcpyAsync(hb + o_st, db + o_st, 16, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if ((rc = group_error())) return rc;
+      d.n_groups = std::max(hst_status[0], 1);
+    }
+    if ((rc = place_windowed(ctx, &d))) return rc;
+  }
+  HIPCHK(hipMemcpyAsync(hb, db, n_out, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (it && (rc = group_error())) return rc;
+  std::memcpy(r->avail, hb + o_av, 32 * (size_t)H);
+  std::memcpy(r->placement, hb + o_pl, 4 * (size_t)T);
+  std::memcpy(r->order, hb + o_or, 4 * (size_t)T);
+  if (dev_mt) std::memcpy(r->mt_state, hb + o_mt, 4 * 625);
+  if (it) std::memcpy(it->mt_state, hb + o_cmt, 4 * 625);
   return PVT_OK;
 }
 

@@ -267,6 +267,7 @@ __global__ __launch_bounds__(256) void epoch_accept_apply_kernel(EpochArgs A, in
         const int len = A.seg_off[j + 1] - A.seg_off[j];
         const int adv = seg_adv(A, j);
         if (j > 0 && A.bad[j]) { rej = A.nseg - j; break; }
+        if (A.whole && adv < len) { next = A.seg_off[j]; refill = 1; rej = A.nseg - j; break; }
         acc = j + 1;
         next = A.seg_off[j] + adv;
         if (adv < len) { refill = 1; rej = A.nseg - j - 1; break; }
@@ -300,6 +301,10 @@ void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
   const int tiles = (CHAIN_MAX + 255) / 256;   // a segment never exceeds its chain's cap
   hipLaunchKernelGGL(epoch_validate_kernel, dim3(tiles, a.nseg, VAL_SPLIT), dim3(256), 0, st, a);
+}
+
+void launch_epoch_final(const EpochArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
 }
 
 void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st) {

@@ -190,8 +190,11 @@ struct EpochArgs {
   int32_t* bad;           // [nseg] out: 1 = segment j is not exact (zeroed by the caller)
   const double* rtb;      // realtime_bw: bandwidth per (group, host) [G][H], or NULL
   const int32_t* grp;     // window tasks' groups [nt]
+  int whole;              // accept: whole segments only (first-fit zero-key epochs)
 };
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st);
+// finality only (no pair validation: first-fit zero-key epochs)
+void launch_epoch_final(const EpochArgs& a, hipStream_t st);
 // apply: the accepted segments [0, n_accept) of each chain, chain by chain in segment order
 void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st);
 // validate's verdict to the accepted prefix and its apply, on the device; res[5] reported
@@ -241,6 +244,10 @@ constexpr int ZW_MIN_PARTS = 256;
 // per-dimension minima of avail over hosts [lo, hi) into part[ZW_MIN_PARTS][4]
 void launch_host_min(const double* avail, int H, int lo, int hi, double* part, hipStream_t st);
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st);
+// cost_aware first-fit with sort_hosts: the zero-key chain walk (FF mode; hmin = the
+// launch_host_absmax partials)
+void launch_zwalk_ff(const ZwalkArgs& a, int nchains, hipStream_t st);
+void launch_host_absmax(const double* avail, int H, int lo, int hi, double* part, hipStream_t st);
 constexpr int ZW_M = 1024;                 // frontier-walk window hosts
 void launch_zwalk_keyed(const ZwalkArgs& a, bool strict, hipStream_t st);
 // ordered first-fit frontier: flags[h - lo] = host h in [lo, hs) fits the smallest demand of

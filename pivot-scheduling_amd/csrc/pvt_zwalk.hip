@@ -29,6 +29,18 @@
 // and window hosts of U outside the anchor's zero-cost zones are scored exactly (ca_score_bits,
 // a key of 0 only when the score's bits are 0). The log and the chain's progress have the
 // format of the list walk's chain mode, so validation, finality and apply are unchanged.
+//
+// FF: the same chain walk for cost_aware FIRST-fit with sort_hosts (scheduler/cost_aware.py:
+// 99-127). A group's hosts are taken in the order of the frozen key c*df/(||avail||*bw); hosts
+// of the anchor's zero-cost zones have key exactly 0 and lead that order in index order, so
+// while one of them strictly fits, the winner is the lowest-index such host -- the same window,
+// with strict fit, and fitting U hosts of other zones simply skipped (their key is > 0).
+// Certificates: (1) as above; (2') every zone has c == 0 with bw > 0 (key exactly 0 for r > 0)
+// or c >= 2^-300 with bw <= 2^300, and every host capacity is at most 2^298 (so r <= 2^299 and
+// a positive key is >= 2^-899, never 0); (3') as (3), and the chain's demands are >= 0 (a host
+// that strictly fits then has r > 0). Chains of different zero-cost components commit to
+// disjoint hosts, none of which is zero-key for another component's anchors, so every chain's
+// proven prefix is exact in the sequential order too (pvt_capi.hip ff_epoch: no validation).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -175,8 +187,9 @@ __device__ __forceinline__ uint64_t zstamp() {
 // back at the end and status[0] = tasks walked.
 // KEYED with STRICT = false: vbp first-fit (index order, fit >=) over a window of the first
 // alive hosts (pvt_capi.hip ordered_frontier), same mechanics.
-template <bool KEYED, bool STRICT>
+template <bool KEYED, bool STRICT, bool FF = false>
 __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
+  static_assert(!FF || (!KEYED && STRICT), "FF: chain mode, strict fit");
   __shared__ ZwalkLDS S;
 #ifdef PVT_STAMPS
   const uint64_t t_start = zstamp();
@@ -260,17 +273,17 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       }
     }
   }
-  // host minima from the partials
-  double ha[4] = {DINF, DINF, DINF, DINF};
+  // host minima (FF: maxima of |capacity|) from the partials
+  double ha[4] = {FF ? -DINF : DINF, FF ? -DINF : DINF, FF ? -DINF : DINF, FF ? -DINF : DINF};
   if (!KEYED)
     for (int k = tid; k < ZW_MINB; k += ZW_THREADS)
 #pragma unroll
-      for (int r = 0; r < 4; r++) ha[r] = fmin(ha[r], A.hmin[k * 4 + r]);
+      for (int r = 0; r < 4; r++) ha[r] = FF ? fmax(ha[r], A.hmin[k * 4 + r]) : fmin(ha[r], A.hmin[k * 4 + r]);
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     mx[r] = wave_max_d(mx[r]);
     mn[r] = wave_min_d(mn[r]);
-    ha[r] = wave_min_d(ha[r]);
+    ha[r] = FF ? wave_max_d(ha[r]) : wave_min_d(ha[r]);
   }
   if (lane == 0) {
 #pragma unroll
@@ -284,15 +297,21 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     for (int w = 1; w < ZW_WAVES; w++) {
       mx[r] = fmax(mx[r], S.red[w][r]);
       mn[r] = fmin(mn[r], S.red[w][4 + r]);
-      ha[r] = fmin(ha[r], S.red[w][8 + r]);
+      ha[r] = FF ? fmax(ha[r], S.red[w][8 + r]) : fmin(ha[r], S.red[w][8 + r]);
     }
     mx[r] = fmax(mx[r], S.red[0][r]);
     mn[r] = fmin(mn[r], S.red[0][4 + r]);
-    ha[r] = fmin(ha[r], S.red[0][8 + r]);
+    ha[r] = FF ? fmax(ha[r], S.red[0][8 + r]) : fmin(ha[r], S.red[0][8 + r]);
   }
   bool sep = KEYED;
+  if (FF) {                                  // certificates (2') and (3'): bounded capacities,
+    sep = true;                              // demands >= 0
 #pragma unroll
-  for (int r = 0; r < 4; r++) sep |= (ha[r] - mx[r] >= 0x1p-288);
+    for (int r = 0; r < 4; r++) sep &= (ha[r] <= 0x1p298) && (mn[r] >= 0.0);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; r++) sep |= (ha[r] - mx[r] >= 0x1p-288);
+  }
   const uint32_t U = S.umask;
   if (S.bail || !sep || nt <= 0 || (!KEYED && nt > CHAIN_MAX)) {
     if (tid == 0) { status[0] = 0; status[1] = (KEYED || nt <= 0) ? 0 : 1; }
@@ -589,8 +608,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       const int R = run_len(k);
       for (;;) {
         const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
-        const uint64_t fm = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
-        if (UNI((fm & ~rzm) != 0)) return 0;
+        uint64_t fm = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
+        if (FF) fm &= rzm;                     // (FF: other fitting hosts have key > 0)
+        if (!FF && UNI((fm & ~rzm) != 0)) return 0;
         if (UNI(fm != 0)) {
           dirty = true;
           ZW_SEARCH_DONE();
@@ -608,8 +628,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       }
       if (pb >= 0) {
         const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
-        const uint64_t fb = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
-        if (UNI((fb & ~bzm) != 0)) return 0;
+        uint64_t fb = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
+        if (FF) fb &= bzm;
+        if (!FF && UNI((fb & ~bzm) != 0)) return 0;
         if (UNI(fb != 0)) {
           bdirty = true;
           ZW_SEARCH_DONE();
@@ -625,9 +646,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #ifdef PVT_STAMPS
         n_probe++;
 #endif
-        const uint64_t fm = __ballot(p < nwin && fit_res<STRICT>(fmin(fmin(x0 - d0, x1 - d1),
-                                                                      fmin(x2 - d2, x3 - d3))));
-        if (UNI((fm & ~xzm) != 0)) return 0;
+        uint64_t fm = __ballot(p < nwin && fit_res<STRICT>(fmin(fmin(x0 - d0, x1 - d1),
+                                                                fmin(x2 - d2, x3 - d3))));
+        if (FF) fm &= xzm;
+        if (!FF && UNI((fm & ~xzm) != 0)) return 0;
         if (UNI(fm != 0)) {
           ZW_SEARCH_DONE();
           const int got = run_bulk(x0, x1, x2, x3, xid, d0, d1, d2, d3, fm, R, k);
@@ -665,7 +687,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           const double n0 = ra0 - d0, n1 = ra1 - d1, n2 = ra2 - d2, n3 = ra3 - d3;
           const uint64_t fm0 = __ballot(fit_res<STRICT>(fmin(fmin(n0, n1), fmin(n2, n3)))) & rvalid;
           const uint64_t m0 = fm0 & rzm;
-          if (UNI(m0 == 0 || (fm0 & ~rzm) != 0)) break;
+          if (UNI(m0 == 0 || (!FF && (fm0 & ~rzm) != 0))) break;
           // a run of tasks with this demand: placed in one pass over the chunk (run_bulk)
           const int R = run_len(k);
           if (UNI(R >= 2)) {
@@ -716,7 +738,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         if (!KEYED && lane < Z) {
           const double c = S.csum[a * Z + lane], bw = S.bsum[a * Z + lane];
           if (c == 0.0) ok = bw > 0.0;
-          else if (!((U >> lane) & 1u)) ok = (c >= 0x1p-300) && (bw <= 0x1p300);
+          else if (FF || !((U >> lane) & 1u)) ok = (c >= 0x1p-300) && (bw <= 0x1p300);
         }
         if (__ballot(!ok)) { failed = true; break; }
         const uint32_t am = KEYED ? ~0u : S.amask[a];   // keyed: every prefix host is zero-key
@@ -736,6 +758,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       }
       // exact scores for this lane's host when it fits but is not zero-cost for `a`
       auto zero_exact = [&](bool f, bool k0, double a0, double a1, double a2, double a3, int q) {
+        if (FF) return k0;                   // (first-fit: a fitting host of another zone has key > 0)
         if (__builtin_expect(__ballot(f && !k0) != 0, 0)) {
           if (f && !k0) {
             const int z = S.wz[q];
@@ -763,7 +786,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // (the winner's lane from its mask bit in scalar registers: no lane-id compare, and the
       // commit is four selects on that mask)
       const uint64_t m0 = fm0 & rzm;
-      if (__builtin_expect(m0 != 0 && (fm0 & ~rzm) == 0, 1)) {
+      if (__builtin_expect(m0 != 0 && (FF || (fm0 & ~rzm) == 0), 1)) {
         const bool win = __builtin_amdgcn_inverse_ballot_w64(m0 & (0ull - m0));
         ra0 = win ? n0 : ra0; ra1 = win ? n1 : ra1; ra2 = win ? n2 : ra2; ra3 = win ? n3 : ra3;
         if (win) {
@@ -779,7 +802,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           const double q0 = rb0 - d0, q1 = rb1 - d1, q2 = rb2 - d2, q3 = rb3 - d3;
           const uint64_t fb = __ballot(fit_res<STRICT>(fmin(fmin(q0, q1), fmin(q2, q3)))) & bvalid;
           const uint64_t mb = fb & bzm;
-          if (mb != 0 && (fb & ~bzm) == 0) {
+          if (mb != 0 && (FF || (fb & ~bzm) == 0)) {
             const bool win = __builtin_amdgcn_inverse_ballot_w64(mb & (0ull - mb));
             rb0 = win ? q0 : rb0; rb1 = win ? q1 : rb1; rb2 = win ? q2 : rb2; rb3 = win ? q3 : rb3;
             if (win) {
@@ -912,6 +935,41 @@ void launch_host_min(const double* avail, int H, int lo, int hi, double* part, h
 
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st) {
   hipLaunchKernelGGL((zwalk_kernel<false, false>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+}
+void launch_zwalk_ff(const ZwalkArgs& a, int nchains, hipStream_t st) {
+  hipLaunchKernelGGL((zwalk_kernel<false, true, true>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+}
+
+// Per-dimension maxima of |avail| over hosts [lo, hi) (the FF walk's certificate 2'), in
+// host_min_kernel's partial layout.
+__global__ __launch_bounds__(256) void host_absmax_kernel(const double* avail, int H, int lo, int hi,
+                                                          double* part) {
+  __shared__ double red[4][4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  double m[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int h = lo + blockIdx.x * 256 + tid; h < hi; h += gridDim.x * 256)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const double x = __builtin_fabs(avail[(size_t)r * H + h]);
+      m[r] = (x <= m[r]) ? m[r] : x;          // (a NaN capacity propagates: no certificate)
+    }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    for (int off = 32; off > 0; off >>= 1) {
+      const double o = __shfl_xor(m[r], off);
+      m[r] = (o <= m[r]) ? m[r] : o;
+    }
+    if (lane == 0) red[wave][r] = m[r];
+  }
+  __syncthreads();
+  if (tid < 4) {
+    double v = red[0][tid];
+    for (int w = 1; w < 4; w++) v = (red[w][tid] <= v) ? v : red[w][tid];
+    part[blockIdx.x * 4 + tid] = v;
+  }
+}
+void launch_host_absmax(const double* avail, int H, int lo, int hi, double* part, hipStream_t st) {
+  hipLaunchKernelGGL(host_absmax_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, lo, hi, part);
 }
 void launch_zwalk_keyed(const ZwalkArgs& a, bool strict, hipStream_t st) {
   if (strict) hipLaunchKernelGGL((zwalk_kernel<true, true>), dim3(1), dim3(ZW_THREADS), 0, st, a);

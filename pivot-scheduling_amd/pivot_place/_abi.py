@@ -10,7 +10,7 @@ from typing import Optional
 
 import numpy as np
 
-PVT_ABI_VERSION = 2
+PVT_ABI_VERSION = 3
 
 PVT_OK = 0
 PVT_EINVAL = -1
@@ -87,6 +87,27 @@ class pvt_meter_log(ctypes.Structure):
                                        "tr_size", "instance_hours", "egress_cost",
                                        "congestion_delay")]
 
+
+class pvt_ca_items(ctypes.Structure):
+    _fields_ = [
+        ("n_items", ctypes.c_int32),
+        ("n_apps", ctypes.c_int32),
+        ("n_pred", ctypes.c_int64),
+        ("task_item", ctypes.c_void_p),
+        ("pred_off", ctypes.c_void_p),
+        ("pred_host", ctypes.c_void_p),
+        ("item_app", ctypes.c_void_p),
+        ("n_storage", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("storage_zone", ctypes.c_void_p),
+        ("zone_storage", ctypes.c_void_p),
+        ("mt_state", ctypes.c_void_p),
+        ("status", ctypes.c_void_p),
+    ]
+
+
+# pvt_place_host grouping error kinds (pvt_ca_items.status[1])
+GROUP_OK, GROUP_UNPLACED, GROUP_NO_STORAGE, GROUP_INVALID = 0, 1, 2, 3
 
 # pvt_anchor anchor_zone codes (include/pivot_place.h)
 ANCHOR_NO_PREDS, ANCHOR_UNPLACED, ANCHOR_INVALID = -1, -2, -3

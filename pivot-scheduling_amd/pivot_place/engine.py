@@ -43,6 +43,7 @@ def load_library(path=None):
         "pvt_reset_kstats": ([c_void_p], c_int),
         "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_get_kernel_kstats": ([c_void_p, ctypes.c_char_p, ctypes.POINTER(_abi.pvt_kstats)], c_int),
+        "pvt_place_host": ([c_void_p, ctypes.POINTER(_abi.pvt_round), ctypes.POINTER(_abi.pvt_ca_items)], c_int),
         "pvt_set_window": ([c_void_p, c_int], c_int),
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
         "pvt_set_score_tw": ([c_void_p, c_int], c_int),
@@ -331,11 +332,69 @@ class PlacementEngine:
         self._check(self.lib.pvt_place(self.ctx, ctypes.addressof(dr.struct)))
 
     def place(self, r: RoundArrays) -> RoundResult:
-        """Place a host-array round: staged through one pinned buffer (_Stager)."""
+        """Place a host-array round in one round trip (pvt_place_host: the context stages the
+        inputs through one pinned buffer, one copy each way, one synchronisation)."""
+        res, rc = self._place_host(r, None)
+        self._check(rc)
+        return res
+
+    def place_staged_torch(self, r: RoundArrays) -> RoundResult:
+        """The previous drop-in path (kept for A/B timing): torch-pinned staging + pvt_place."""
         st = getattr(self, "_stager", None)
         if st is None:
             st = self._stager = _Stager(self.device)
         return st.place(self, r)
+
+    def _place_host(self, r: RoundArrays, items):
+        T = r.n_tasks
+        s = _abi.fill_struct(r)
+        avail = np.array(r.avail, dtype=np.float64, order="C")
+        placement = np.empty(T, dtype=np.int32)
+        order = np.empty(T, dtype=np.int32)
+        mt = None if r.mt_state is None else np.array(r.mt_state, dtype=np.uint32)
+        s.avail = avail.ctypes.data
+        for name in ("zone", "tiebreak", "decay", "cost", "bw", "dem", "task_group", "group_anchor",
+                     "rt_bw"):
+            a = getattr(r, name)
+            setattr(s, name, None if a is None else a.ctypes.data)
+        s.placement, s.order = placement.ctypes.data, order.ctypes.data
+        s.mt_state = None if mt is None else mt.ctypes.data
+        rc = self.lib.pvt_place_host(self.ctx, ctypes.byref(s),
+                                     None if items is None else ctypes.byref(items))
+        return (RoundResult(placement=placement, order=order, avail=avail, mt_state=mt), rc)
+
+    def place_cost_aware(self, r: RoundArrays, task_item, pred_off, pred_host, item_app, n_apps,
+                         storage_zone, zone_storage, mt_state):
+        """A cost_aware round whose grouping (scheduler/cost_aware.py:30-58: mode-host anchors,
+        first-seen groups, one randomizer.choice(storage) per application group) runs on the
+        device in the same round trip as the placement (pvt_place_host with pvt_ca_items).
+        Returns (RoundResult, groups, the randomizer's MT19937 state after the draws), or None
+        when the round is beyond the fused path's limits (use anchor() + place()). Raises
+        AttributeError where the reference does (a mode placement that is no host; an anchor
+        zone without storage)."""
+        ti = np.ascontiguousarray(task_item, dtype=np.int32)
+        off = np.ascontiguousarray(pred_off, dtype=np.int64)
+        ph = np.ascontiguousarray(pred_host, dtype=np.int32)
+        ia = np.ascontiguousarray(item_app, dtype=np.int32)
+        sz = np.ascontiguousarray(storage_zone, dtype=np.int32)
+        zs = np.ascontiguousarray(zone_storage, dtype=np.int32)
+        mt = np.array(mt_state, dtype=np.uint32)
+        status = np.zeros(2, dtype=np.int32)
+        it = _abi.pvt_ca_items()
+        it.n_items, it.n_apps, it.n_pred = ia.size, int(n_apps), ph.size
+        it.task_item, it.pred_off, it.pred_host = ti.ctypes.data, off.ctypes.data, ph.ctypes.data
+        it.item_app = ia.ctypes.data
+        it.n_storage, it.reserved = sz.size, 0
+        it.storage_zone, it.zone_storage = sz.ctypes.data, zs.ctypes.data
+        it.mt_state, it.status = mt.ctypes.data, status.ctypes.data
+        res, rc = self._place_host(r, it)
+        if rc == _abi.PVT_EUNSUPPORTED:
+            return None
+        if rc != _abi.PVT_OK and status[1] in (_abi.GROUP_UNPLACED, _abi.GROUP_NO_STORAGE):
+            # the reference: cluster.get_host(placement).locality / storage.locality on None
+            raise AttributeError("'NoneType' object has no attribute 'locality'")
+        self._check(rc)
+        return res, int(status[0]), mt
 
     # -- resident rounds and scenario batches (include/pivot_place.h, pvt_place_batch)
     def run_batch(self, batch: "DeviceBatch"):

@@ -97,6 +97,25 @@ class _ClusterTables:
         else:
             self.cost = np.zeros((1, 1))
             self.bw = np.ones((1, 1))
+        self._storage_key = None
+
+    def storage_tables(self, cluster):
+        """(storage_zone[S], zone_storage[Z]) for the device grouping: the zone of each storage in
+        cluster.storage order, and the index of get_storage_by_locality(zone) in that list (-1:
+        None), rebuilt when the storage list changes."""
+        storage = cluster.storage
+        key = (id(storage), len(storage), tuple(id(x) for x in storage))
+        if self._storage_key != key:
+            pos = {id(x): i for i, x in enumerate(storage)}
+            self._storage_zone = np.array([self.zone_of.get(x.locality, -1) for x in storage],
+                                          dtype=np.int32)
+            zs = []
+            for z in self.zones:
+                st = cluster.get_storage_by_locality(z)
+                zs.append(-1 if st is None else pos.get(id(st), -1))
+            self._zone_storage = np.array(zs, dtype=np.int32)
+            self._storage_key = key
+        return self._storage_zone, self._zone_storage
 
     def routes_of(self, cluster, anchor):
         """(in routes, out routes) between storage ``anchor`` and every host, in host order,
@@ -145,10 +164,9 @@ class PlacementMixin:
 
     @staticmethod
     def _demand(tasks):
-        d = np.empty((4, len(tasks)), dtype=np.float64)
-        for j, t in enumerate(tasks):
-            d[0, j], d[1, j], d[2, j], d[3, j] = t.cpus, t.mem, t.disk, t.gpus
-        return d
+        if not tasks:
+            return np.empty((4, 0), dtype=np.float64)
+        return np.array([(t.cpus, t.mem, t.disk, t.gpus) for t in tasks], dtype=np.float64).T.copy()
 
     def _apply(self, tasks, hosts, resc, res, before):
         ids = self._tables().host_ids
@@ -175,13 +193,20 @@ class CostAwarePlacement(PlacementMixin):
         self._pvt_realtime_bw = realtime_bw
         self._pvt_host_decay = host_decay
 
-    def _group_tasks(self, tasks):
-        """Groups keyed by anchor storage, or by application for source tasks, in first-seen
-        order (reference cost_aware.py:45-58). The anchor of a task with predecessors is the
-        zone of the MODE host of all predecessor task placements (first seen wins ties); the
-        mode is computed on the GPU (pvt_anchor), one item per distinct container."""
-        cluster = self.cluster
-        tab = self._tables()
+    def _pred_tasks(self, c):
+        """The predecessor tasks of container c, flattened in the reference's order
+        (cost_aware.py:50: [t for p in app.get_predecessors(c.id) for t in p.tasks]); the DAG
+        is static, so the list is kept per container (their placements are read every round)."""
+        cache = self.__dict__.setdefault("_pvt_preds", {})
+        e = cache.get(id(c))
+        if e is None or e[0] is not c:
+            e = cache[id(c)] = (c, [p for pc in c.application.get_predecessors(c.id) for p in pc.tasks])
+        return e[1]
+
+    def _items(self, tasks):
+        """One item per distinct container of the ready tasks (first-seen order): its
+        predecessor placements as host indices (-1: not a host), CSR."""
+        idx = self._tables().host_index
         items, item_of, off, lst = [], [], [0], []
         memo = {}
         for t in tasks:
@@ -190,11 +215,19 @@ class CostAwarePlacement(PlacementMixin):
             if i is None:
                 i = memo[id(c)] = len(items)
                 items.append(c)
-                idx = tab.host_index
-                for pc in c.application.get_predecessors(c.id):
-                    lst.extend(idx.get(p.placement, -1) for p in pc.tasks)
+                lst.extend([idx.get(p.placement, -1) for p in self._pred_tasks(c)])
                 off.append(len(lst))
             item_of.append(i)
+        return items, item_of, off, lst
+
+    def _group_tasks(self, tasks):
+        """Groups keyed by anchor storage, or by application for source tasks, in first-seen
+        order (reference cost_aware.py:45-58). The anchor of a task with predecessors is the
+        zone of the MODE host of all predecessor task placements (first seen wins ties); the
+        mode is computed on the GPU (pvt_anchor), one item per distinct container."""
+        cluster = self.cluster
+        tab = self._tables()
+        items, item_of, off, lst = self._items(tasks)
         zones = None
         if lst:
             _, zones = self._engine().anchor(np.array(off, dtype=np.int64),
@@ -225,6 +258,38 @@ class CostAwarePlacement(PlacementMixin):
                                      + np.array([x.realtime_bw for x in outs], dtype=np.float64))
         return row
 
+    def _schedule_fused(self, tasks, resc, best_fit):
+        """The whole round -- grouping, anchors, draws and placement -- in ONE device round trip
+        (engine.place_cost_aware); False when the engine or the round cannot take it."""
+        eng = self._engine()
+        if not hasattr(eng, "place_cost_aware") or not tasks:
+            return False
+        tab = self._tables()
+        items, item_of, off, lst = self._items(tasks)
+        apps = {}
+        item_app = [apps.setdefault(id(c.application), len(apps)) for c in items]
+        storage_zone, zone_storage = tab.storage_tables(self.cluster)
+        avail = self._snapshot(resc)
+        decay = None
+        if self._pvt_host_decay:
+            decay = np.array([max(len(h.tasks), 1) for h in self.cluster.hosts], dtype=np.int32)
+        r = RoundArrays(mode=_abi.PVT_CA_BF if best_fit else _abi.PVT_CA_FF, avail=avail,
+                        zone=tab.zone, dem=self._demand(tasks), cost=tab.cost, bw=tab.bw,
+                        decay=decay, sort_tasks=self._pvt_sort_tasks,
+                        sort_hosts=self._pvt_sort_hosts)
+        st = self.randomizer.get_state()
+        mt = np.empty(625, dtype=np.uint32)
+        mt[:624] = st[1]
+        mt[624] = st[2]
+        got = eng.place_cost_aware(r, item_of, off, lst, item_app, len(apps), storage_zone,
+                                   zone_storage, mt)
+        if got is None:
+            return False
+        res, _, mt = got
+        self.randomizer.set_state((st[0], mt[:624].copy(), int(mt[624]), st[3], st[4]))
+        self._apply(tasks, self.cluster.hosts, resc, res, avail)
+        return True
+
     def schedule(self, tasks):
         algo = self._pvt_algo
         if algo not in ('first-fit', 'best-fit'):
@@ -233,6 +298,12 @@ class CostAwarePlacement(PlacementMixin):
             return tasks
         storage, hosts = self.cluster.storage, self.cluster.hosts
         resc = self.resource_info
+        best_fit = algo == 'best-fit'
+        # one round trip when nothing needs the groups on the host: realtime_bw reads routes per
+        # group anchor, and best-fit with host_decay raises mid-loop (cost_aware.py:26,81)
+        if (not self._pvt_realtime_bw and not (best_fit and self._pvt_host_decay)
+                and self._schedule_fused(tasks, resc, best_fit)):
+            return tasks
         tab = self._tables()
         groups = self._group_tasks(tasks)
         task_pos = {id(t): i for i, t in enumerate(tasks)}
@@ -241,7 +312,6 @@ class CostAwarePlacement(PlacementMixin):
         anchors, rt_rows = [], []
         avail = self._snapshot(resc)
         dem = self._demand(tasks)
-        best_fit = algo == 'best-fit'
         # the reference reads routes only through host_score_func: best-fit, and first-fit with
         # sort_hosts (cost_aware.py:92, 118-119); unsorted first-fit never does
         rt = self._pvt_realtime_bw and (best_fit or self._pvt_sort_hosts)

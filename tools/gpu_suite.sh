@@ -14,6 +14,7 @@ for s in "$@"; do
     t_runs)     run t_runs 400 $T tests/test_gpu_runs.py ;;
     t_vbp)      run t_vbp 400 $T tests/test_gpu_band.py tests/test_gpu_headline.py tests/test_gpu_parity.py -k "vbp or VBP or band or headline or config5" ;;
     t_opp)      run t_opp 500 $T tests/test_gpu_opp_walk.py tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_sharded.py tests/test_gpu_batch.py -k "opp or OPP or opportunistic" ;;
+    t_multi)    run t_multi 600 $T tests/test_bench_multirank.py tests/test_gpu_batch.py ;;
     smoke)      run smoke 120 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)      run bench 400 python bench.py ;;
     b_cabf)     run b_cabf 150 python bench.py $NB --steps 20 ;;
@@ -21,12 +22,17 @@ for s in "$@"; do
     b_caff)     run b_caff 150 python bench.py --mode ca_ff $NB ;;
     b_vbpbf)    run b_vbpbf 200 python bench.py --mode vbp_bf $NB ;;
     b_opp)      run b_opp 200 python bench.py --mode opp $NB ;;
+    b_c4)       for w in ${C4W:-4 2}; do for m in ca_bf ca_ff opp vbp_ff vbp_bf; do PVT_RES_WAVES=$w run b_c4_${m}_w$w 120 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done; done ;;
+    t_res)      run t_res 600 $T tests/test_gpu_batch.py tests/test_gpu_parity.py tests/test_policies.py tests/test_sim_replay.py tests/test_lockstep.py tests/test_gpu_fused.py tests/test_anchor.py ;;
+    r_split)    run r_split 300 python tools/replay_split.py sim_c1_cost_aware sim_c2a1000_cost_aware sim_c2a1000_opportunistic sim_c2a1000_vbp_ff ;;
+    b_replay)   run b_replay 300 python bench.py --extra 0 --replay 1 --cpu-baseline-seconds 0 --steps 3 ;;
     b_shard)    run b_shard 200 python bench.py --shard hosts $NB ;;
     st_zw)      for m in ca_bf vbp_ff ca_ff; do run st_$m 120 python tools/zwalk_stamps.py 1000000 10000 libpivot_place_stamps.so $m; done ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
     st_opp)     run st_opp 150 python tools/commit_stamps.py 2 1000000 10000 ;;
     profbench)  mkdir -p gpurun_out/prof; run profbench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 $NB ;;
-    pmc)        run pmc 900 tools/pmc_all.sh "${PMC_TAG:-r03z}" ;;
+    pmc)        run pmc 1100 tools/pmc_all.sh "${PMC_TAG:-r04z}" ;;
+    pmc_c4)     run pmc_c4 400 tools/pmc_all.sh "${PMC_TAG:-r04z}" c4 ;;
     *)          echo "unknown step $s"; exit 2 ;;
   esac
 done
