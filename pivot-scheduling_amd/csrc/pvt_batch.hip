@@ -59,7 +59,8 @@ struct ResLds {
     ci = cd + 32 * RES_CHUNK;                          //       anchor, group i32[2][CHUNK] (+pad)
     mt = ci + 12 * RES_CHUNK;                          //       MT copies u32[WAVES][628]
     slot = mt + 4 * RES_MAXW * RES_MT_STRIDE;          //       posts u64[2][WAVES][2], then
-    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW;   //   fast posts i32[2][WAVES]
+    // fast posts i32[2][WAVES], then vbp best-fit s2 posts {u64, i32, i32}[2][WAVES]
+    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     total = walk_end > sort_end ? walk_end : sort_end;
   }
@@ -186,6 +187,7 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   uint64_t* posts = reinterpret_cast<uint64_t*>(smem + Lo.slot);   // [2][WAVES][2]
   int32_t* cposts = reinterpret_cast<int32_t*>(posts);              // opp: [2][WAVES]
   int32_t* fposts = reinterpret_cast<int32_t*>(smem + Lo.slot + 32 * RES_MAXW);   // [2][WAVES]
+  uint64_t* vposts = reinterpret_cast<uint64_t*>(smem + Lo.slot + 40 * RES_MAXW);  // [2][WAVES][2]
   MtWave mw;
   mw.buf = 0; mw.used = 0; mw.limit = 0;
   if (MODE == OPP) {
@@ -384,6 +386,70 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
           // no fast winner anywhere: first-fit by index has none at all; cost_aware best-fit
           // (no score-0 host, or a risky one) and keyed first-fit (no key-0 host) take the full path
           full = !FIRST || keyed;
+        }
+      }
+      if (MODE == VBP_BF) {
+        // vbp best-fit by the squared norm first (vbp.py:43-47): the winner has the least s2
+        // unless another fitting host's norm rounds to the same value -- which needs its s2
+        // within a factor 1 + 2^-49 of the least (sqrt halves relative gaps; a gap above
+        // 2^-52 of the exact roots separates the rounded ones). Each wave posts its least s2
+        // (bits: s2 >= +0), that host, and whether a second host of the wave lies within that
+        // factor; when no second host anywhere does, the least s2 is the winner and no square
+        // root is taken. Otherwise the full path below decides with the norms and tiebreaks.
+        uint64_t sb[HPL];
+        uint64_t ls = NONE;
+        int lh = 0x7fffffff;
+#pragma unroll
+        for (int j = 0; j < HPL; j++) {
+          const bool f = fits<true>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+          sb[j] = f ? dbits(norm2_seq(a0[j] - d0, a1[j] - d1, a2[j] - d2, a3[j] - d3)) : NONE;
+          if (sb[j] < ls) { ls = sb[j]; lh = h0 + j; }
+        }
+        const uint64_t m = wave_min_u64(ls);
+        int wh = 0x7fffffff, near = 0;
+        if (m != NONE) {
+          const uint64_t thr = dbits(__longlong_as_double((long long)m) * (1.0 + 0x1p-49));
+          int cnt = 0;
+#pragma unroll
+          for (int j = 0; j < HPL; j++) cnt += sb[j] <= thr ? 1 : 0;
+          const uint64_t any = __ballot(cnt > 0);
+          near = (__popcll(any) > 1 || __ballot(cnt > 1) != 0) ? 1 : 0;
+          wh = __builtin_amdgcn_readlane(lh, __builtin_ctzll(__ballot(ls == m)));
+        }
+        uint64_t gm = m;
+        int gh = wh, gnear = near;
+        if (WAVES > 1) {
+          if (lane == 0) {
+            vposts[(par * RES_MAXW + wave) * 2 + 0] = m;
+            vposts[(par * RES_MAXW + wave) * 2 + 1] = ((uint64_t)(uint32_t)near << 32) | (uint32_t)wh;
+          }
+          __syncthreads();
+          uint64_t vm[WAVES], vx[WAVES];
+#pragma unroll
+          for (int w = 0; w < WAVES; w++) {
+            vm[w] = vposts[(par * RES_MAXW + w) * 2 + 0];
+            vx[w] = vposts[(par * RES_MAXW + w) * 2 + 1];
+          }
+          gm = vm[0];
+#pragma unroll
+          for (int w = 1; w < WAVES; w++) gm = vm[w] < gm ? vm[w] : gm;
+          gnear = 0;
+          gh = 0x7fffffff;
+          if (gm != NONE) {
+            const uint64_t thr = dbits(__longlong_as_double((long long)gm) * (1.0 + 0x1p-49));
+            int within = 0;
+#pragma unroll
+            for (int w = 0; w < WAVES; w++) {
+              within += vm[w] <= thr ? 1 : 0;
+              if (vm[w] == gm && gh == 0x7fffffff) { gh = (int)(uint32_t)vx[w]; gnear |= (int)(vx[w] >> 32); }
+            }
+            gnear |= within > 1;
+          }
+        }
+        gnear = __builtin_amdgcn_readfirstlane(gnear);
+        if (!gnear) {
+          full = false;
+          hw = __builtin_amdgcn_readfirstlane(gh);
         }
       }
       if (full) {

@@ -1,0 +1,115 @@
+"""GPU parity of the first-fit zero-key epochs (keyed cost_aware first-fit, sort_hosts; the
+reference's own sim.py configuration, cost_aware.py:99-127): whole groups of different zero-cost
+components walked side by side by the first-fit chain walk (pvt_zwalk.hip FF mode) with no key
+computed, the rest left to the keyed path from its group start. Placements, order and
+availability must equal the CPU restatement and the same engine with epochs off -- including
+rounds built so that the chain walk cannot prove a group (zones without capacity, a group larger
+than a chain, subnormal egress costs, host decay)."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from pivot_place import _abi, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(res, ref):
+    np.testing.assert_array_equal(res.placement, ref.placement)
+    np.testing.assert_array_equal(res.order, ref.order)
+    bad = np.nonzero((res.avail != ref.avail).any(axis=0))[0]
+    assert bad.size == 0, "availability differs on hosts %s" % bad[:10]
+
+
+def _place(engine, r, epochs=True):
+    try:
+        engine.set_resident(0)
+        engine.set_epochs(epochs)
+        res = engine.place(r)
+        st = engine.epoch_stats()
+    finally:
+        engine.set_epochs(True)
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+    return res, st
+
+
+def _check(engine, r, expect_epochs=None):
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    off, st0 = _place(engine, r, epochs=False)
+    _same(off, ref)
+    assert st0["epochs"] == 0
+    if expect_epochs is not None:
+        assert (st["epochs"] > 0) == expect_epochs, st
+    return st
+
+
+@pytest.mark.parametrize("H,T,seed", [(5000, 300, 1), (70_000, 2600, 2), (200_000, 12_000, 3),
+                                      (1_000_000, 10_000, 20261015)])
+def test_ff_epochs_match_oracle(engine, H, T, seed):
+    r = synthetic.make_round(_abi.PVT_CA_FF, H, T, seed=seed)
+    st = _check(engine, r, expect_epochs=True)
+    assert st["frontier_chains"] > 0, st
+
+
+@pytest.mark.parametrize("seed", [10, 11])
+def test_ff_epochs_zones_without_capacity(engine, seed):
+    """Zones 0-9 have no capacity: groups anchored there find no zero-key host, the chain walk
+    cannot prove them and the keyed path places them on positive-key hosts, onto hosts other
+    groups want too."""
+    r = synthetic.make_round(_abi.PVT_CA_FF, 20_000, 6000, seed=seed)
+    r.avail[:2, r.zone < 10] = 0.0
+    _check(engine, r)
+
+
+def test_ff_epochs_repeated_anchors_and_runs(engine):
+    """40 groups over 20 zones (each zone anchors two groups) with a handful of demand rows:
+    chains of several segments, runs of equal demands crossing group boundaries in a batch."""
+    r = synthetic.make_round(_abi.PVT_CA_FF, 60_000, 8000, seed=8)
+    rs = np.random.RandomState(8)
+    groups = np.sort(rs.randint(0, 40, size=r.n_tasks))
+    first = {}
+    for g in groups:
+        first.setdefault(int(g), len(first))
+    r.task_group = np.array([first[int(g)] for g in groups], dtype=np.int32)
+    r.group_anchor = np.array([g % 20 for g in first.keys()], dtype=np.int32)
+    rows = rs.randint(0, 3, size=r.n_tasks)
+    r.dem[0] = np.array([0.5, 1.0, 2.0])[rows]
+    r.dem[1] = np.array([1000.0, 4000.0, 7864.32])[rows]
+    st = _check(engine, r, expect_epochs=True)
+    assert st["segments"] >= 40
+
+
+def test_ff_epochs_group_larger_than_chain(engine):
+    """One group of 5000 tasks (more than a chain walk holds) between small ones: the epoch plan
+    stops before it and the keyed path takes it from its start."""
+    r = synthetic.make_round(_abi.PVT_CA_FF, 50_000, 6000, seed=21)
+    tg = np.zeros(r.n_tasks, dtype=np.int32)
+    tg[:300] = 0
+    tg[300:5300] = 1
+    tg[5300:] = 2
+    r.task_group = tg
+    r.group_anchor = np.array([3, 7, 11], dtype=np.int32)
+    _check(engine, r)
+
+
+def test_ff_epochs_tiny_costs_and_decay(engine):
+    """Subnormal egress costs between some zones (a positive key could round to 0: no
+    certificate for those anchors) and per-host decay factors (host_decay)."""
+    r = synthetic.make_round(_abi.PVT_CA_FF, 30_000, 4000, seed=22)
+    cost = np.array(r.cost, dtype=np.float64)
+    cost[5, 11] = cost[11, 5] = 5e-324
+    r.cost = cost
+    r.decay = np.random.RandomState(22).randint(1, 5, size=r.n_hosts).astype(np.int32)
+    _check(engine, r)
+
+
+def test_ff_epochs_hosts_fill_exactly(engine):
+    """Hosts filled to exactly the demand: strict fit (a > d) excludes them afterwards."""
+    r = synthetic.make_round(_abi.PVT_CA_FF, 8000, 3000, seed=23)
+    r.avail[0, :] = 2.0
+    r.avail[1, :] = 2 * 3932.16
+    r.dem[0, :] = 1.0
+    r.dem[1, :] = 3932.16
+    _check(engine, r)
