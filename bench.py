@@ -589,6 +589,61 @@ def round_trip_floor_ms(eng, reps=200):
     return float(np.median(ts)) * 1e3
 
 
+LOCKSTEP = ("sim_c2_cost_aware", "sim_c2_opportunistic", "sim_c2_vbp_ff",
+            "sim_c2a1000_cost_aware", "sim_c2a1000_opportunistic", "sim_c2a1000_vbp_ff")
+
+
+class _BatchOracleEngine(_OracleEngine):
+    """The C restatement behind the batched engine contract (LockstepDriver)."""
+
+    def place_batch(self, rounds):
+        from oracle import oracle
+        return [oracle.place(r, threads=self.threads) for r in rounds]
+
+
+def lockstep_workload(eng):
+    """BASELINE config 2 as a sweep through the lock-step driver (pivot_place.lockstep, §8(f)
+    rank 2): the recorded reference simulations at 1000 hosts (two app counts x the three
+    schedulers) run side by side, each in its own thread behind the drop-in policy classes;
+    whenever every live simulation waits on the engine, their rounds go to one pvt_place_batch
+    per policy mode and their anchors to one pvt_anchor. Every round is compared with the
+    reference's. The same driver over the C restatement is timed beside it (1 thread)."""
+    from pivot_place.lockstep import LockstepDriver
+
+    def run(engine):
+        driver = LockstepDriver(engine)
+        t = time.perf_counter()
+        out = driver.run([lambda e, n=n: _replay(n, e) for n in LOCKSTEP])
+        return time.perf_counter() - t, out, driver.stats
+
+    secs, out, st = run(eng)              # (the replay lines before it warmed the tables up)
+    csecs, cout, cst = run(_BatchOracleEngine(0))
+    rounds = sum(o[2] for o in out)
+    cand = sum(o[1] for o in out)
+    ok = all(o[3] for o in out)
+    return {"workload": "config 2 sweep: %d recorded reference simulations (1000 hosts; %s) run "
+                        "side by side through the lock-step driver, drop-in policy classes, one "
+                        "pvt_place_batch per policy mode and one pvt_anchor per tick"
+                        % (len(LOCKSTEP), ", ".join(n[4:] for n in LOCKSTEP)),
+            "simulations": len(LOCKSTEP), "rounds": rounds, "candidates": cand,
+            "value": cand / secs, "unit": "candidates/s", "seconds": secs,
+            "ms_per_round": secs * 1e3 / rounds, "parity": bool(ok),
+            "ticks": st["batches"], "place_calls": st["place_calls"],
+            "place_launches": st["place_launches"], "anchor_calls": st["anchor_calls"],
+            "anchor_launches": st["anchor_launches"],
+            "max_rounds_per_launch": st["max_rounds_per_launch"],
+            "engine_seconds": st["serve_s"], "engine_ms_per_round": st["serve_s"] * 1e3 / rounds,
+            "note": "wall time of the whole lock-step run: the recorded rounds are rebuilt from "
+                    "their fixtures in every simulation thread (Python, under one interpreter "
+                    "lock) and only the engine calls are batched; engine_seconds is the time the "
+                    "driver spent serving the batched calls",
+            "cpu_baseline": {"value": cand / csecs, "unit": "candidates/s", "cores": 1,
+                             "kind": "port", "seconds": csecs, "engine_seconds": cst["serve_s"],
+                             "parity": bool(all(o[3] for o in cout)),
+                             "sample": "the same lock-step run with the C restatement behind the "
+                                       "batched engine contract (1 thread)"}}
+
+
 def replay_workloads(eng):
     out = {}
     threads = oracle_threads()
@@ -777,6 +832,12 @@ def main():
             out["extra"] = extra_workloads(eng, args, args.mode)
         if args.replay == 1 or (args.replay < 0 and default and args.extra != 0):
             out.setdefault("extra", {}).update(replay_workloads(eng))
+            try:
+                out["extra"]["c2_lockstep"] = lockstep_workload(eng)
+            except Exception as e:                       # (a missing fixture is reported)
+                out["extra"]["c2_lockstep"] = {"error": "%s: %s" % (type(e).__name__, e)}
+            log("[rank 0] lockstep: %s" % {k: v for k, v in out["extra"]["c2_lockstep"].items()
+                                           if k not in ("workload", "cpu_baseline")})
     if world > 1 and args.c4_batch > 0 and not B:
         # (every rank: the barriers and the MAX / MIN reductions are collective)
         c4 = scenario_batch_line(eng, args, rank, world, gloo, args.c4_batch)

@@ -233,6 +233,10 @@ int  pvt_shard_commit(pvt_ctx* ctx, const void* packages);
 #define PVT_RESIDENT_MAX_HOSTS 4096
 #define PVT_RESIDENT_MAX_TASKS 4096
 int  pvt_place_batch(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_rounds);
+/* pvt_place_batch with the rounds' MT19937 states resident on the device: mt_dev[n_rounds][625]
+ * (in/out, key then pos, as mt_state), so no state crosses PCIe; the rounds' mt_state fields are
+ * ignored. The scenario-batch driver (config 4) keeps its states on the device across rounds. */
+int  pvt_place_batch_mt(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_rounds, uint32_t* mt_dev);
 int  pvt_set_resident(pvt_ctx* ctx, int32_t max_hosts);
 /*
  * Anchor resolution for cost_aware groups (replaces the Counter/max of

@@ -554,17 +554,24 @@ static void launch_two(int hpl, int n, size_t lds, const ResidentArgs& a, hipStr
   }
 }
 template <int MODE>
+static void launch_one(int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((resident_kernel<MODE, 1, 16>), dim3(n), dim3(WAVE), lds, st, a);
+}
+template <int MODE>
 static void launch_mode(int waves, int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
   if (waves == 8 && hpl <= 8) launch_waves<MODE, 8>(hpl, n, lds, a, st);
   else if (waves == 2 && hpl >= 8) launch_two<MODE>(hpl, n, lds, a, st);
+  else if (waves == 1 && hpl == 16) launch_one<MODE>(n, lds, a, st);
   else launch_waves<MODE, 4>(hpl, n, lds, a, st);
 }
 
 // Waves and hosts per lane for a batch whose largest round has maxH hosts: `waves` (4 or 8) on
 // entry is the preference; 8 waves only while the round needs at most 8 hosts per lane.
 void resident_shape(int maxH, int* waves, int* hpl) {
+  // (waves 2 and 1 -- 8 and 16 hosts per lane -- only as A/B preferences, PVT_RES_WAVES)
   const int w = (*waves == 8 && maxH <= 8 * 8 * WAVE) ? 8
-                : (*waves == 2 && maxH > 4 * 4 * WAVE && maxH <= 2 * 16 * WAVE) ? 2 : 4;
+                : (*waves == 2 && maxH > 2 * 4 * WAVE && maxH <= 2 * 16 * WAVE) ? 2
+                : (*waves == 1 && maxH > 8 * WAVE && maxH <= 16 * WAVE) ? 1 : 4;
   int h = 1;
   while (h * w * WAVE < maxH) h <<= 1;
   *waves = w;
@@ -592,7 +599,7 @@ static hipError_t attrs_mode(int lds) {
   if (r != hipSuccess) e = r;
   PVT_RES_ATTR(4, 1) PVT_RES_ATTR(4, 2) PVT_RES_ATTR(4, 4) PVT_RES_ATTR(4, 8) PVT_RES_ATTR(4, 16)
   PVT_RES_ATTR(8, 1) PVT_RES_ATTR(8, 2) PVT_RES_ATTR(8, 4) PVT_RES_ATTR(8, 8)
-  PVT_RES_ATTR(2, 8) PVT_RES_ATTR(2, 16)
+  PVT_RES_ATTR(2, 8) PVT_RES_ATTR(2, 16) PVT_RES_ATTR(1, 16)
 #undef PVT_RES_ATTR
   return e;
 }

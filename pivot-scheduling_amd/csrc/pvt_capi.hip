@@ -185,8 +185,10 @@ struct pvt_ctx {
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
-  std::vector<pvt_round> rstage;  // pvt_place_batch: descriptors staged for the device
-  std::vector<uint32_t> rmt_host;
+  pvt_round* rstage = nullptr;    // pvt_place_batch: descriptors staged for the device (pinned)
+  size_t rstage_cap = 0;
+  uint32_t* rmt_host = nullptr;   //   and the rounds' MT19937 states (pinned)
+  size_t rmt_cap = 0;
   RoundState rs;
   int32_t* next_host = nullptr;   // pinned
   void* gstage = nullptr;         // grouped order: counts, anchors, cost table (pinned)
@@ -351,7 +353,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_OF_HOSTS")) ctx->t_of_hosts = std::max(ZW_M, atoi(e));   // tuning
   if (const char* e = getenv("PVT_EPOCH_PLAN")) ctx->t_epoch_plan = atoi(e);           // A/B
   if (const char* e = getenv("PVT_MERGE_SMALL")) ctx->t_merge_bitonic = atoi(e) == 0;  // A/B
-  if (const char* e = getenv("PVT_RES_WAVES")) ctx->res_waves = atoi(e) == 8 ? 8 : atoi(e) == 2 ? 2 : 4;  // A/B
+  if (const char* e = getenv("PVT_RES_WAVES")) ctx->res_waves = atoi(e) == 8 ? 8 : atoi(e) == 2 ? 2 : atoi(e) == 1 ? 1 : 4;  // A/B
   *out = ctx;
   return PVT_OK;
 }
@@ -378,6 +380,8 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   if (ctx->ep_host) (void)hipHostFree(ctx->ep_host);
   if (ctx->gstage) (void)hipHostFree(ctx->gstage);
   if (ctx->hst) (void)hipHostFree(ctx->hst);
+  if (ctx->rstage) (void)hipHostFree(ctx->rstage);
+  if (ctx->rmt_host) (void)hipHostFree(ctx->rmt_host);
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
   if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
@@ -1699,8 +1703,24 @@ static bool resident_fits(const pvt_round* r, int max_hosts) {
          r->n_tasks <= PVT_RESIDENT_MAX_TASKS;
 }
 
+template <class T>
+static int ensure_pinned_array(pvt_ctx* ctx, T*& p, size_t& cap, size_t n) {
+  if (cap >= n) return PVT_OK;
+  const size_t want = std::max(n, cap * 3 / 2);
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  cap = 0;
+  if (hipHostMalloc((void**)&p, sizeof(T) * want) != hipSuccess) {
+    p = nullptr;
+    return fail(ctx, PVT_ENOMEM, "hipHostMalloc(%zu) failed", sizeof(T) * want);
+  }
+  cap = want;
+  return PVT_OK;
+}
+
 // desc_dev: the rounds' descriptors already on the device (pvt_place_host's staging, MT states
 // at mt_dev): nothing is copied and nothing waited for here; the caller copies back and syncs.
+// mt_dev alone (pvt_place_batch_mt): the rounds' MT19937 states live on the device, [n][625].
 static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
                           const void* desc_dev = nullptr, uint32_t* mt_dev = nullptr) {
   const int mode = rounds[0].mode;
@@ -1740,32 +1760,38 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     ctx->refills = 0;
     return PVT_OK;
   }
-  ctx->rstage.assign(rounds, rounds + n);
+  int rc;
+  if ((rc = ensure_pinned_array(ctx, ctx->rstage, ctx->rstage_cap, (size_t)n))) return rc;
+  std::memcpy(ctx->rstage, rounds, sizeof(pvt_round) * n);
   ENSURE(ctx->rdesc, sizeof(pvt_round) * (size_t)n);
   uint32_t* mt = nullptr;
-  if (mode == PVT_OPP) {
+  const bool host_mt = mode == PVT_OPP && !mt_dev;
+  if (mode == PVT_OPP && mt_dev) {
+    mt = mt_dev;
+    for (int i = 0; i < n; i++) ctx->rstage[i].mt_state = mt + (size_t)i * 625;
+  } else if (host_mt) {
     ENSURE(ctx->rmt, sizeof(uint32_t) * 625 * (size_t)n);
     mt = P<uint32_t>(ctx->rmt);
-    ctx->rmt_host.resize((size_t)n * 625);
+    if ((rc = ensure_pinned_array(ctx, ctx->rmt_host, ctx->rmt_cap, (size_t)n * 625))) return rc;
     for (int i = 0; i < n; i++) {
-      std::memcpy(&ctx->rmt_host[(size_t)i * 625], rounds[i].mt_state, sizeof(uint32_t) * 625);
+      std::memcpy(ctx->rmt_host + (size_t)i * 625, rounds[i].mt_state, sizeof(uint32_t) * 625);
       ctx->rstage[i].mt_state = mt + (size_t)i * 625;   // device copy (the kernel never reads the field)
     }
-    HIPCHK(hipMemcpyAsync(mt, ctx->rmt_host.data(), sizeof(uint32_t) * 625 * n, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(mt, ctx->rmt_host, sizeof(uint32_t) * 625 * n, hipMemcpyHostToDevice, st));
   }
-  HIPCHK(hipMemcpyAsync(ctx->rdesc.p, ctx->rstage.data(), sizeof(pvt_round) * n, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(ctx->rdesc.p, ctx->rstage, sizeof(pvt_round) * n, hipMemcpyHostToDevice, st));
   ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad};
   {
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mode, waves, hpl, n, ra, st);
   }
   HIPCHK(hipGetLastError());
-  if (mode == PVT_OPP)
-    HIPCHK(hipMemcpyAsync(ctx->rmt_host.data(), mt, sizeof(uint32_t) * 625 * n, hipMemcpyDeviceToHost, st));
+  if (host_mt)
+    HIPCHK(hipMemcpyAsync(ctx->rmt_host, mt, sizeof(uint32_t) * 625 * n, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  if (mode == PVT_OPP)
+  if (host_mt)
     for (int i = 0; i < n; i++)
-      std::memcpy(rounds[i].mt_state, &ctx->rmt_host[(size_t)i * 625], sizeof(uint32_t) * 625);
+      std::memcpy(rounds[i].mt_state, ctx->rmt_host + (size_t)i * 625, sizeof(uint32_t) * 625);
   ctx->windows = n;
   ctx->refills = 0;
   return PVT_OK;
@@ -1777,6 +1803,18 @@ extern "C" int pvt_place_batch(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_
   ctx->rs.active = false;
   if (n_rounds == 0) return PVT_OK;
   return place_resident(ctx, rounds, n_rounds);
+}
+
+extern "C" int pvt_place_batch_mt(pvt_ctx* ctx, const pvt_round* rounds, int32_t n_rounds,
+                                  uint32_t* mt_dev) {
+  if (!ctx) return PVT_EINVAL;
+  if (n_rounds < 0 || (n_rounds > 0 && (!rounds || !mt_dev)))
+    return fail(ctx, PVT_EINVAL, "bad batch (%d rounds)", n_rounds);
+  ctx->rs.active = false;
+  if (n_rounds == 0) return PVT_OK;
+  std::vector<pvt_round> rr(rounds, rounds + n_rounds);   // (mt_state: the device rows, so
+  for (int i = 0; i < n_rounds; i++) rr[i].mt_state = mt_dev + (size_t)i * 625;   // checks pass)
+  return place_resident(ctx, rr.data(), n_rounds, nullptr, mt_dev);
 }
 
 // ---------------------------------------------------------------- anchor resolution (a3)

@@ -44,6 +44,7 @@ def load_library(path=None):
         "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_get_kernel_kstats": ([c_void_p, ctypes.c_char_p, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_place_host": ([c_void_p, ctypes.POINTER(_abi.pvt_round), ctypes.POINTER(_abi.pvt_ca_items)], c_int),
+        "pvt_place_batch_mt": ([c_void_p, c_void_p, ctypes.c_int32, c_void_p], c_int),
         "pvt_set_window": ([c_void_p, c_int], c_int),
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
         "pvt_set_score_tw": ([c_void_p, c_int], c_int),
@@ -175,6 +176,12 @@ class DeviceBatch:
                               for r in self.arrays]).astype(np.uint32) if any(has_mt) else None
         self._mt = None if self._mt0 is None else self._mt0.copy()
         self.mt = [self._mt[i] if has_mt[i] else None for i in range(n)]
+        # every round opportunistic: the states stay on the device (pvt_place_batch_mt), reset
+        # by a D2D copy, read back by results() only
+        self.mt_dev = self._mt_dev0 = None
+        if all(has_mt):
+            self._mt_dev0 = torch.from_numpy(self._mt0.view(np.int32).copy()).to(dev)
+            self.mt_dev = self._mt_dev0.clone()
         for i, r in enumerate(self.arrays):
             st = _abi.fill_struct(r)
             for name, dt in self._FIELDS:
@@ -193,7 +200,9 @@ class DeviceBatch:
         if not self.arrays:
             return
         self.bufs["avail"].copy_(self.avail0)
-        if self._mt is not None:
+        if self.mt_dev is not None:
+            self.mt_dev.copy_(self._mt_dev0)
+        elif self._mt is not None:
             self._mt[:] = self._mt0
 
     def placement_of(self, i):
@@ -205,6 +214,8 @@ class DeviceBatch:
         pl = self.placement.cpu().numpy()
         od = self.order.cpu().numpy()
         av = self.bufs["avail"].cpu().numpy()
+        if self.mt_dev is not None:
+            self._mt[:] = self.mt_dev.cpu().numpy().view(np.uint32).reshape(self._mt.shape)
         out = []
         for i, r in enumerate(self.arrays):
             t0, t1 = int(self._toff[i]), int(self._toff[i + 1])
@@ -402,7 +413,11 @@ class PlacementEngine:
         torch = _torch()
         stream = torch.cuda.current_stream(self.device)
         self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
-        self._check(self.lib.pvt_place_batch(self.ctx, ctypes.addressof(batch.structs), len(batch)))
+        if batch.mt_dev is not None:
+            self._check(self.lib.pvt_place_batch_mt(self.ctx, ctypes.addressof(batch.structs),
+                                                    len(batch), ctypes.c_void_p(batch.mt_dev.data_ptr())))
+        else:
+            self._check(self.lib.pvt_place_batch(self.ctx, ctypes.addressof(batch.structs), len(batch)))
 
     def place_batch(self, rounds) -> list:
         """Place independent rounds of one policy (each <= PVT_RESIDENT_MAX_HOSTS hosts and

@@ -22,6 +22,7 @@ only ever called from the driver's thread (the engine context is not thread-safe
     results = driver.run([lambda eng: simulate(..., engine=eng) for ...])
 """
 import threading
+import time
 
 import numpy as np
 
@@ -63,7 +64,7 @@ class LockstepDriver:
         self._pending = []
         self._live = 0
         self.stats = {"batches": 0, "place_calls": 0, "place_launches": 0, "anchor_calls": 0,
-                      "anchor_launches": 0, "max_rounds_per_launch": 0}
+                      "anchor_launches": 0, "max_rounds_per_launch": 0, "serve_s": 0.0}
 
     # -------------------------------------------------------------- simulation side
     def _call(self, sim, kind, args):
@@ -117,6 +118,7 @@ class LockstepDriver:
         return results
 
     def _serve(self, batch):
+        t = time.perf_counter()
         self.stats["batches"] += 1
         anchors = [c for c in batch if c.kind == "anchor"]
         places = [c for c in batch if c.kind == "place"]
@@ -124,6 +126,7 @@ class LockstepDriver:
             self._serve_anchors(anchors)
         if places:
             self._serve_places(places)
+        self.stats["serve_s"] += time.perf_counter() - t
 
     def _serve_anchors(self, calls):
         """One pvt_anchor over every simulation's items: lists are offset into one host space

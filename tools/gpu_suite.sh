@@ -13,6 +13,7 @@ for s in "$@"; do
     t_zw)       run t_zw 400 $T tests/test_gpu_headline.py tests/test_gpu_epochs.py tests/test_gpu_ordered_frontier.py tests/test_gpu_parity.py ;;
     t_ff)       run t_ff 600 $T tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_runs.py tests/test_gpu_sharded.py tests/test_gpu_ordered_frontier.py tests/test_gpu_epochs.py -k "ff or FF or keyed or headline or config5 or sharded" ;;
     b_c3ff)     run b_c3ff 150 python bench.py --mode ca_ff --hosts 100000 --tasks 1000 $NB ;;
+    t_ffe)      run t_ffe 500 $T tests/test_gpu_ff_epochs.py ;;
     t_runs)     run t_runs 400 $T tests/test_gpu_runs.py ;;
     t_vbp)      run t_vbp 400 $T tests/test_gpu_band.py tests/test_gpu_headline.py tests/test_gpu_parity.py -k "vbp or VBP or band or headline or config5" ;;
     t_opp)      run t_opp 500 $T tests/test_gpu_opp_walk.py tests/test_gpu_parity.py tests/test_gpu_headline.py tests/test_gpu_sharded.py tests/test_gpu_batch.py -k "opp or OPP or opportunistic" ;;
