@@ -43,8 +43,9 @@ static constexpr int EP_SEG_OFF = 0, EP_SEG_CHAIN = EP_SEG_OFF + EPOCH_SEGS + 1,
                      EP_SEG_CSTART = EP_SEG_CHAIN + EPOCH_SEGS, EP_COFF = EP_SEG_CSTART + EPOCH_SEGS,
                      EP_CSOFF = EP_COFF + EPOCH_SEGS + 1, EP_CSEG = EP_CSOFF + EPOCH_SEGS + 1,
                      EP_CMAP = EP_CSEG + EPOCH_SEGS, EP_STATUS = EP_CMAP + EPOCH_MAX,
-                     EP_BAD = EP_STATUS + 2 * EPOCH_SEGS, EP_RES = EP_BAD + EPOCH_SEGS;
-static constexpr int EP_WORDS = EP_RES + 8;
+                     EP_BAD = EP_STATUS + 2 * EPOCH_SEGS, EP_RES = EP_BAD + EPOCH_SEGS,
+                     EP_SAFE = EP_RES + 8;
+static constexpr int EP_WORDS = EP_SAFE + EPOCH_SEGS;
 static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a frontier-walk launch
 static constexpr int ORDERED_FRONTIER_MIN = 32;  // tasks a frontier attempt must place to go on
 static constexpr int ORDERED_FRONTIER_TASKS = 1024;   // tasks per frontier attempt (default)
@@ -184,6 +185,7 @@ struct pvt_ctx {
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
+  Buf cmax;                       // frontier-walked epochs: chains' largest demands
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
   pvt_round* rstage = nullptr;    // pvt_place_batch: descriptors staged for the device (pinned)
   size_t rstage_cap = 0;
@@ -369,7 +371,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->seg, &ctx->seg_feas, &ctx->l_e[0], &ctx->l_ids[0], &ctx->l_t[0],
                  &ctx->l_e[1], &ctx->l_ids[1], &ctx->l_t[1], &ctx->next, &ctx->opp, &ctx->pkg,
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->oppfault, &ctx->hdev, &ctx->kskey, &ctx->kperm, &ctx->kiota,
-                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->fwin,
+                 &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->cmax, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
                  &ctx->btcnt, &ctx->bsorttmp, &ctx->brow[0], &ctx->brow[1], &ctx->brdem[0],
                  &ctx->brdem[1], &ctx->bnrep[0], &ctx->bnrep[1]};
@@ -1630,11 +1632,17 @@ static int place_epochs(pvt_ctx* ctx) {
       return PVT_OK;
     };
     if (zw) {
+      ENSURE(ctx->cmax, sizeof(double) * 4 * EPOCH_SEGS);
       ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
                    P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                    P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
                    P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
-                   nullptr, 0, 0, 0, nullptr, nullptr, nullptr, dev + EP_CSOFF, dev + EP_CSEG};
+                   nullptr, 0, 0, 0, nullptr, nullptr, nullptr, dev + EP_CSOFF, dev + EP_CSEG,
+                   P<double>(ctx->cmax)};
+      ea.cmax = P<double>(ctx->cmax);
+      ea.coff = dev + EP_COFF;
+      ea.nch = nch;
+      ea.safe = dev + EP_SAFE;
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
         launch_zwalk(za, nch, st);
@@ -2400,11 +2408,13 @@ static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
     const int nseg = (int)E.chain.size(), nch = nslots;
     int32_t* dev = P<int32_t>(ctx->ep_dev);
     int32_t* host = ctx->ep_host;
+    ENSURE(ctx->cmax, sizeof(double) * 4 * EPOCH_SEGS);
     ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
                  P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                  P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
                  P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
-                 nullptr, 0, 0, 0, nullptr, nullptr, win, dev + EP_CSOFF, dev + EP_CSEG};
+                 nullptr, 0, 0, 0, nullptr, nullptr, win, dev + EP_CSOFF, dev + EP_CSEG,
+                 P<double>(ctx->cmax)};
     {
       Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
       launch_zwalk(za, nch, st);
@@ -2412,7 +2422,8 @@ static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
     EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
                  P<double>(ctx->csum), P<double>(ctx->bsum), r->zone, dev + EP_SEG_OFF,
                  dev + EP_SEG_CHAIN, dev + EP_SEG_CSTART, dev + EP_STATUS, P<WinRec>(ctx->wres),
-                 r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD, r->rt_bw, P<int32_t>(ctx->grp_ord) + t0};
+                 r->avail, R.H, R.Z, nt, nseg, dev + EP_BAD, r->rt_bw, P<int32_t>(ctx->grp_ord) + t0,
+                 0, P<double>(ctx->cmax), dev + EP_COFF, nch, dev + EP_SAFE};
     {
       Scope sc(ctx, PVT_K_OTHER, 0, 0);
       launch_epoch_validate(ea, st);

@@ -72,7 +72,18 @@ __device__ __forceinline__ bool beats(int32_t h, double f0, double f1, double f2
 
 constexpr int VAL_HASH = 512;
 
+// Every chain walked to its end and every final entry safe (EpochArgs.cmax): nothing to check.
+__device__ __forceinline__ bool epoch_fast(const EpochArgs& A) {
+  if (!A.cmax) return false;
+  for (int c = 0; c < A.nch; c++)
+    if (A.status[2 * c] != A.coff[c + 1] - A.coff[c]) return false;
+  for (int s = 0; s < A.nseg; s++)
+    if (!A.safe[s]) return false;
+  return true;
+}
+
 __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
+  if (epoch_fast(A)) return;
   __shared__ int32_t e_id[256];
   __shared__ double e_a[4][256];
   __shared__ double e_c[256], e_b[256];
@@ -209,9 +220,16 @@ __device__ __forceinline__ int fin_slot(int32_t h, const int32_t* hk) {
 }
 __global__ __launch_bounds__(1024) void epoch_final_kernel(EpochArgs A) {
   __shared__ int32_t hk[FIN_SLOTS], hv[FIN_SLOTS];
+  __shared__ double gmx[4];
+  __shared__ int32_t unsafe;
   const int j = blockIdx.x, tid = threadIdx.x;
   const int s0 = A.seg_off[j], n = seg_adv(A, j);
-  if (tid == 0) A.bad[j] = 0;                 // validation (next launch) starts with no verdict
+  if (tid == 0) { A.bad[j] = 0; unsafe = 0; }   // validation (next launch) starts with no verdict
+  if (A.cmax && tid < 4) {                    // the epoch's largest demand per dimension
+    double m = -DINF;
+    for (int c = 0; c < A.nch; c++) m = fmax(m, A.cmax[c * 4 + tid]);
+    gmx[tid] = m;
+  }
   for (int q = tid; q < FIN_SLOTS; q += blockDim.x) { hk[q] = -1; hv[q] = -1; }
   __syncthreads();
   for (int k = tid; k < n; k += blockDim.x) {
@@ -227,8 +245,18 @@ __global__ __launch_bounds__(1024) void epoch_final_kernel(EpochArgs A) {
   }
   __syncthreads();
   for (int k = tid; k < n; k += blockDim.x) {
-    const int32_t h = A.wlog[s0 + k].id;
-    A.wlog[s0 + k].sup = (h >= 0 && hv[fin_slot(h, hk)] != k) ? 1 : 0;
+    const WinRec& e = A.wlog[s0 + k];
+    const int32_t h = e.id;
+    const int sup = (h >= 0 && hv[fin_slot(h, hk)] != k) ? 1 : 0;
+    A.wlog[s0 + k].sup = sup;
+    if (A.cmax && h >= 0 && !sup &&
+        !(e.a[0] - gmx[0] >= 0x1p-287 || e.a[1] - gmx[1] >= 0x1p-287 ||
+          e.a[2] - gmx[2] >= 0x1p-287 || e.a[3] - gmx[3] >= 0x1p-287))
+      unsafe = 1;                             // (benign race: every writer stores 1)
+  }
+  if (A.cmax) {
+    __syncthreads();
+    if (tid == 0) A.safe[j] = unsafe ? 0 : 1;
   }
 }
 

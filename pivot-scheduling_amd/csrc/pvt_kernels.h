@@ -191,6 +191,14 @@ struct EpochArgs {
   const double* rtb;      // realtime_bw: bandwidth per (group, host) [G][H], or NULL
   const int32_t* grp;     // window tasks' groups [nt]
   int whole;              // accept: whole segments only (first-fit zero-key epochs)
+  // frontier-walked epochs (cost_aware best-fit): when every chain was walked to its end by the
+  // zero-cost frontier walk and every final log entry exceeds the epoch's largest demand by
+  // 2^-287 in some dimension (safe[j], set by the finality pass from the chains' cmax), no pair
+  // can beat a winner (hosts of different components, scores > 0) and validation is skipped
+  const double* cmax;     // [nch][4] or NULL
+  const int32_t* coff;    // [nch + 1] chains' task ranges (their lengths)
+  int nch;
+  int32_t* safe;          // [nseg]
 };
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st);
 // finality only (no pair validation: first-fit zero-key epochs)
@@ -239,6 +247,7 @@ struct ZwalkArgs {
   // segment, so every segment's last copy on a host must be logged); NULL in keyed mode
   const int32_t* csoff;
   const int32_t* cseg;
+  double* cmax;           // chain mode: [chains][4] out, each chain's largest demand per dimension
 };
 constexpr int ZW_MIN_PARTS = 256;
 // per-dimension minima of avail over hosts [lo, hi) into part[ZW_MIN_PARTS][4]

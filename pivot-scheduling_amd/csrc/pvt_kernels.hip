@@ -591,20 +591,102 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   }
 }
 
+// Merge of up to LMAX / KL score-segment lists (vbp best-fit band lists: 16 segments) with the
+// same rank-by-counting, one block per task: each entry's merged position is its index in its own
+// list plus its lower bound in every other list (binary searches in LDS), so no sorting network
+// and no barrier between the load and the store (the bitonic merge_kernel runs 55 barrier stages
+// over 1024 keys).
+__global__ __launch_bounds__(256) void merge_mid_kernel(MergeArgs A) {
+  __shared__ Key lk[LMAX];
+  __shared__ Key out[LMAX];
+  __shared__ int cnt_sh;
+  const int task = blockIdx.x, tid = threadIdx.x;
+  if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
+  const int S = A.S, n = S * KL;
+  const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
+  if (tid == 0) cnt_sh = 0;
+  for (int j = tid; j < n; j += 256) {
+    const SegEntry se = A.seg[(size_t)task * S * KL + j];
+    lk[j] = {se.s, se.tb, se.id};
+    out[j] = inv;
+  }
+  // bound: the smallest last entry of a segment with more than KL feasible hosts (every thread
+  // derives it: S loads, no barrier on its path)
+  Key bound = inv;
+  long long tot = 0;
+  for (int g = 0; g < S; g++) {
+    const int f = A.seg_feas[(size_t)task * S + g];
+    tot += f;
+    if (f > KL) {
+      const SegEntry se = A.seg[((size_t)task * S + g) * KL + KL - 1];
+      const Key k = {se.s, se.tb, se.id};
+      if (kless(k, bound)) bound = k;
+    }
+  }
+  __syncthreads();
+  int c = 0;
+  for (int j = tid; j < n; j += 256) {
+    const Key x = lk[j];
+    if (x.id == 0x7fffffff || !kless(x, bound)) continue;   // invalid, or at/after the bound
+    const int g = j / KL;
+    int pos = j - g * KL;
+    for (int h = 0; h < S; h++)
+      if (h != g) pos += lower_bound_key(lk + h * KL, KL, x);
+    out[pos] = x;
+    c++;
+  }
+  if (c) atomicAdd(&cnt_sh, c);
+  __syncthreads();
+  const int cnt = cnt_sh;
+  const bool complete = (bound.id == 0x7fffffff) && tot <= LMAX;
+  Key bnd = bound;
+  if (cnt == LMAX && kless(out[LMAX - 1], bnd)) bnd = out[LMAX - 1];
+  const int nw = max(cnt, KL);
+  for (int j = tid; j < nw; j += 256) {
+    ListEntry e;
+    const bool ok = j < cnt;
+    const Key k = ok ? out[j] : inv;
+    const int h = ok ? k.id : 0;
+    e.s = k.s; e.tb = k.tb; e.id = k.id; e.pad = 0; e.pad2 = 0.0;
+    e.zone = ok ? A.zone[h] : 0;
+    e.a[0] = ok ? A.avail[h] : 0.0;
+    e.a[1] = ok ? A.avail[(size_t)A.H + h] : 0.0;
+    e.a[2] = ok ? A.avail[2 * (size_t)A.H + h] : 0.0;
+    e.a[3] = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
+    A.L.e[(size_t)task * LMAX + j] = e;
+    A.L.ids[(size_t)task * LMAX + j] = ok ? k.id : 0x7fffffff;
+  }
+  if (tid < 4) {
+    double* tr = reinterpret_cast<double*>(&A.L.t[task]);
+    tr[tid] = A.dem[(size_t)task * 4 + tid];
+  }
+  if (tid == 0) {
+    TaskRec& r = A.L.t[task];
+    r.cnt = cnt;
+    r.complete = complete;
+    r.anc = A.anc[task];
+    r.ord = A.ord[task];
+    r.bs = bnd.s; r.btb = bnd.tb; r.bid = bnd.id;
+  }
+}
+
 static int merge_variant(const MergeArgs& a) {
   const bool small = !a.bitonic;
   if (small && a.seg_feas != nullptr && a.SL == KL && a.S <= MERGE_SMALL_S) return 1;
   if (small && a.seg_feas == nullptr && (size_t)a.S * a.SL <= LMAX) return 2;
+  if (small && a.seg_feas != nullptr && a.SL == KL && (size_t)a.S * KL <= LMAX) return 3;
   return 0;
 }
 const char* merge_kernel_name(const MergeArgs& a) {
-  static const char* names[3] = {"merge_kernel", "merge_small_kernel", "merge_pkg_kernel"};
+  static const char* names[4] = {"merge_kernel", "merge_small_kernel", "merge_pkg_kernel",
+                                 "merge_mid_kernel"};
   return names[merge_variant(a)];
 }
 void launch_merge(const MergeArgs& a, hipStream_t st) {
   switch (merge_variant(a)) {
     case 1: hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a); break;
     case 2: hipLaunchKernelGGL(merge_pkg_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(merge_mid_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
     default: hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
   }
 }
@@ -936,6 +1018,24 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
   __shared__ int32_t v[GSORT_MAX];
   const int a = off[blockIdx.x], n = off[blockIdx.x + 1] - a, tid = threadIdx.x;
   if (n <= 0) return;
+  if (n <= 1024) {
+    // rank by counting: the keys (sort key, task index) are distinct, so an element's place is
+    // the number of elements below it -- every thread scans the group's keys in LDS (broadcast
+    // reads), one barrier in all (the bitonic network below needs 55 for 1024 keys)
+    for (int i = tid; i < n; i += blockDim.x) { k[i] = skey[a + i]; v[i] = sidx[a + i]; }
+    __syncthreads();
+    if (tid < n) {
+      const uint64_t ki = k[tid];
+      const int32_t vi = v[tid];
+      int r = 0;
+      for (int j = 0; j < n; j++) {
+        const uint64_t kj = k[j];
+        r += (kj < ki || (kj == ki && v[j] < vi)) ? 1 : 0;
+      }
+      ord[a + r] = vi;
+    }
+    return;
+  }
   int P = 2;
   while (P < n) P <<= 1;
   for (int i = tid; i < P; i += blockDim.x) {

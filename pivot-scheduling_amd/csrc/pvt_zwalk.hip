@@ -303,6 +303,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     mn[r] = fmin(mn[r], S.red[0][4 + r]);
     ha[r] = FF ? fmax(ha[r], S.red[0][8 + r]) : fmin(ha[r], S.red[0][8 + r]);
   }
+  if (!KEYED && A.cmax && tid < 4) A.cmax[b * 4 + tid] = mx[tid];   // (the validation's fast path)
   bool sep = KEYED;
   if (FF) {                                  // certificates (2') and (3'): bounded capacities,
     sep = true;                              // demands >= 0

@@ -152,6 +152,7 @@ class DeviceBatch:
         self.structs = (_abi.pvt_round * max(n, 1))()
         self.bufs, offs = {}, {}
         self.mt, self._mt, self._mt0 = [], None, None
+        self.mt_dev = self._mt_dev0 = None
         if n == 0:
             return
         for name, dt in self._FIELDS:
