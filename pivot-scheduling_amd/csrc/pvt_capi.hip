@@ -1583,6 +1583,8 @@ static int place_epochs(pvt_ctx* ctx) {
   EpochPlan E;
   int t0 = 0, rc;
   bool force_lists = false;       // the last epoch's frontier walk left chains unproven
+  bool big = false;               // ... because a chain outgrew its window: retry with ZW_MBIG
+  int big_t0 = -1;                //   (at most once per epoch start)
   R.in_epoch = true;
   struct Reset { bool& f; ~Reset() { f = false; } } reset_{R.in_epoch};
   const bool zw_possible = ctx->zwalk && !r->rt_bw && R.Z <= ZMAX;
@@ -1645,12 +1647,16 @@ static int place_epochs(pvt_ctx* ctx) {
       ea.safe = dev + EP_SAFE;
       {
         Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
-        launch_zwalk(za, nch, st);
+        if (big) launch_zwalk_big(za, nch, st);
+        else launch_zwalk(za, nch, st);
       }
+      const bool was_big = big;
+      big = false;
       HIPCHK(hipGetLastError());
       // validation, the accepted prefix and its apply all on the device, then one readback. A
       // chain the frontier walk could not prove is not accepted past its first segment; the
-      // next epoch then walks its chains with candidate lists (force_lists).
+      // next epoch then walks its chains with candidate lists (force_lists) -- or, when a chain
+      // only ran out of window hosts, once more with the large window.
       {
         Scope sc(ctx, PVT_K_OTHER, 0, 0);
         launch_epoch_validate(ea, st);
@@ -1662,7 +1668,16 @@ static int place_epochs(pvt_ctx* ctx) {
       HIPCHK(hipStreamSynchronize(st));
       int adv = 0;
       if ((rc = epoch_frontier_verdict(ctx, E, t0, &need, &adv))) return rc;
-      if (need && adv < nt) force_lists = true;
+      if (need && adv < nt) {
+        bool exhausted = false;
+        for (int c = 0; c < nch; c++) exhausted |= host[EP_STATUS + 2 * c + 1] == 2;
+        if (exhausted && !was_big && big_t0 != t0 + adv) {
+          big = true;
+          big_t0 = t0 + adv;
+        } else {
+          force_lists = true;
+        }
+      }
       t0 += adv;
       continue;
     }

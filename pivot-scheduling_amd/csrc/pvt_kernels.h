@@ -253,6 +253,9 @@ constexpr int ZW_MIN_PARTS = 256;
 // per-dimension minima of avail over hosts [lo, hi) into part[ZW_MIN_PARTS][4]
 void launch_host_min(const double* avail, int H, int lo, int hi, double* part, hipStream_t st);
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st);
+// the same walk over a window of ZW_MBIG hosts (status[1] == 2: a chain's window of ZW_M was
+// exhausted while more of its zones' hosts exist -- config 5 with loaded hosts)
+void launch_zwalk_big(const ZwalkArgs& a, int nchains, hipStream_t st);
 // cost_aware first-fit with sort_hosts: the zero-key chain walk (FF mode; hmin = the
 // launch_host_absmax partials)
 void launch_zwalk_ff(const ZwalkArgs& a, int nchains, hipStream_t st);

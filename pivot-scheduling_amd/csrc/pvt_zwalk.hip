@@ -50,7 +50,7 @@
 
 namespace pvt {
 
-constexpr int ZW_CH = ZW_M / 64;           // window chunks (one wave step each)
+constexpr int ZW_MBIG = 3072;              // the large window (a retry for chains that outgrow ZW_M)
 constexpr int ZW_THREADS = 256;
 constexpr int ZW_WAVES = ZW_THREADS / 64;
 constexpr int ZW_SCAN = 16;                // hosts per thread per window-build pass
@@ -59,11 +59,12 @@ constexpr double ZW_BIG = 0x1p500;
 
 constexpr int ZW_UNROLL = 4;               // run_bulk pass 1: copies per stop check
 constexpr int ZW_SB = 64;                  // suffix-minimum batches (the last one holds the rest)
+template <int WM>
 struct ZwalkLDS {
-  double wa[4][ZW_M];                      // window capacities (live)
-  int32_t wid[ZW_M];                       // window hosts (ascending index)
-  int32_t wz[ZW_M];                        // their zones
-  uint64_t zm[ZW_CH];                      // current anchor: zero-cost window hosts, per chunk
+  double wa[4][WM];                        // window capacities (live)
+  int32_t wid[WM];                         // window hosts (ascending index)
+  int32_t wz[WM];                          // their zones
+  uint64_t zm[WM / 64];                    // current anchor: zero-cost window hosts, per chunk
   double csum[ZMAX * ZMAX], bsum[ZMAX * ZMAX];
   int32_t cnt[ZW_SCAN][ZW_WAVES];          // window build: hits per (pass row, wave)
   double red[ZW_WAVES][12];                // block reductions: max d, min d, min avail
@@ -126,16 +127,17 @@ __device__ __forceinline__ void wave_lds_sync() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// The first ZW_M hosts of [h_lo, h_hi), in index order, whose zone is in the mask U, appended
+// The first WM hosts of [h_lo, h_hi), in index order, whose zone is in the mask U, appended
 // to wid / wz from *nwin on (passes of ZW_SCAN x 256 hosts, every zone load of a pass in flight
 // at once, a stable block compaction; the block stops at the pass that fills the window).
+template <int WM = ZW_M>
 __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, uint32_t U,
                                                     int h_lo, int h_hi, int32_t* wid, int32_t* wz,
                                                     int32_t (*cnt)[ZW_WAVES], int32_t* nwin) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int h0 = h_lo; h0 < h_hi; h0 += ZW_SCAN * ZW_THREADS) {
     const int have = *nwin;
-    if (have >= ZW_M) break;
+    if (have >= WM) break;
     bool hit[ZW_SCAN];
     int zz[ZW_SCAN];
 #pragma unroll
@@ -159,14 +161,14 @@ __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, 
       for (int w = 0; w < ZW_WAVES; w++) before += (w < wave) ? cnt[k][w] : 0;
       const uint64_t m = __ballot(hit[k]);
       const int pos = pre + before + __popcll(m & below);
-      if (hit[k] && pos < ZW_M) {
+      if (hit[k] && pos < WM) {
         wid[pos] = h0 + k * ZW_THREADS + tid;
         if (wz) wz[pos] = zz[k];
       }
       for (int w = 0; w < ZW_WAVES; w++) pre += cnt[k][w];
     }
     __syncthreads();
-    if (tid == 0) *nwin = min(pre, ZW_M);
+    if (tid == 0) *nwin = min(pre, WM);
     __syncthreads();
   }
 }
@@ -187,10 +189,12 @@ __device__ __forceinline__ uint64_t zstamp() {
 // back at the end and status[0] = tasks walked.
 // KEYED with STRICT = false: vbp first-fit (index order, fit >=) over a window of the first
 // alive hosts (pvt_capi.hip ordered_frontier), same mechanics.
-template <bool KEYED, bool STRICT, bool FF = false>
+template <bool KEYED, bool STRICT, bool FF = false, int WM = ZW_M>
 __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   static_assert(!FF || (!KEYED && STRICT), "FF: chain mode, strict fit");
-  __shared__ ZwalkLDS S;
+  static_assert(WM == ZW_M || !KEYED, "keyed / ordered / sharded windows: ZW_M hosts");
+  constexpr int ZW_CH = WM / 64;           // window chunks (one wave step each)
+  __shared__ ZwalkLDS<WM> S;
 #ifdef PVT_STAMPS
   const uint64_t t_start = zstamp();
   uint64_t n_chunks = 0, n_switch = 0, n_bulk = 0, n_runs = 0;
@@ -334,16 +338,16 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     if (tid == 0) S.nwin = nw;
     __syncthreads();
   } else {                                   // window: U's hosts in index order
-    compact_zone_window(A.zone, Z, U, 0, H, S.wid, S.wz, S.cnt, &S.nwin);
+    compact_zone_window<WM>(A.zone, Z, U, 0, H, S.wid, S.wz, S.cnt, &S.nwin);
   }
   const int nwin = S.nwin;
   bool wbad = false;
-  static_assert(ZW_M == 4 * ZW_THREADS, "window capacities: four hosts per thread");
-  {
-    double v[4][4];                          // every gather of the thread in flight at once
+  static_assert(WM % (4 * ZW_THREADS) == 0, "window capacities: four hosts per thread per pass");
+  for (int p0 = 0; p0 < WM && p0 < nwin; p0 += 4 * ZW_THREADS) {
+    double v[4][4];                          // every gather of the pass in flight at once
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int p = u * ZW_THREADS + tid;
+      const int p = p0 + u * ZW_THREADS + tid;
       const int h = p < nwin ? S.wid[p] : 0;   // (host 0: a valid address, never used)
 #pragma unroll
       for (int r = 0; r < 4; r++)
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int p = u * ZW_THREADS + tid;
+      const int p = p0 + u * ZW_THREADS + tid;
       if (p < nwin) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -405,7 +409,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   int p0 = 0;                                // chunks before p0 cannot fit any chain task
   int cur = -1;                              // anchor the zero-cost masks are for
   int done = 0;
-  bool failed = false;
+  bool failed = false, exhausted = false;
   // chunk p0 in registers
   double ra0, ra1, ra2, ra3;
   int32_t rid;
@@ -877,7 +881,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           load_b(p0 + 1);
         }
       }
-      if (UNI(!found)) { failed = true; break; }  // certificate 1 fails: the list walk decides
+      if (UNI(!found)) {                     // certificate 1 fails: the list walk decides --
+        failed = true;                       // or, when the window is full, a larger one may do
+        exhausted = nwin >= WM;
+        break;
+      }
       done++;
       k++;
     }
@@ -908,7 +916,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   }
   // status[0]: tasks proven (their log entries are exact; validation accepts them), status[1]:
   // 1 when a certificate failed there (the rest of the chain is left to the list walk)
-  if (lane == 0) { status[0] = done; status[1] = (failed && !KEYED) ? 1 : 0; }
+  if (lane == 0) { status[0] = done; status[1] = (failed && !KEYED) ? (exhausted ? 2 : 1) : 0; }
 #ifdef PVT_STAMPS
   if (lane == 0 && A.stamps) {
     const uint64_t t_end = zstamp();
@@ -936,6 +944,9 @@ void launch_host_min(const double* avail, int H, int lo, int hi, double* part, h
 
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st) {
   hipLaunchKernelGGL((zwalk_kernel<false, false>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+}
+void launch_zwalk_big(const ZwalkArgs& a, int nchains, hipStream_t st) {
+  hipLaunchKernelGGL((zwalk_kernel<false, false, false, ZW_MBIG>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
 }
 void launch_zwalk_ff(const ZwalkArgs& a, int nchains, hipStream_t st) {
   hipLaunchKernelGGL((zwalk_kernel<false, true, true>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);

@@ -230,3 +230,17 @@ def test_zero_walk_run_stops_at_segment_start(engine, zero_walk):
     _same(res, ref)
     if zero_walk:
         assert st["frontier_chains"] > 0, st
+
+
+@pytest.mark.parametrize("H,T,seed", [(200_000, 6000, 24), (1_000_000, 10_000, 20261015)])
+def test_zero_walk_large_window_retry(engine, zero_walk, H, T, seed):
+    """Every host holds at most 1 cpu (bench.py's loaded config 5): chains need more than the
+    1024-host window, report it exhausted, and are walked again with the 3072-host window
+    before any falls back to the lists; placements stay exact."""
+    r = synthetic.make_round(_abi.PVT_CA_BF, H, T, seed=seed)
+    r.avail[0] = np.minimum(r.avail[0], 1.0)
+    ref = oracle.place(r, threads=8)
+    res, st = _place(engine, r)
+    _same(res, ref)
+    if zero_walk:
+        assert st["frontier_chains"] > 0, st
