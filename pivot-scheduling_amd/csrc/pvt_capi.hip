@@ -544,7 +544,12 @@ static double bytes_per_candidate(int mode) {
 
 // a2: processing order. Group-major (stable by group id), within a group caller order or, with
 // sort_tasks, stable descending ||d||2. Two LSD passes of a stable radix sort.
-static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
+// Processing order (a2). Grouped rounds take the optimistic path: group counts, offsets and the
+// pinned copies of counts / anchors / cost table, then the per-group sorts, all launched with no
+// synchronisation (*pending = true); the caller syncs once, later, and calls build_order_check.
+static int build_order_radix(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out);
+static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool* pending) {
+  *pending = false;
   const int T = r->n_tasks;
   hipStream_t st = ctx->stream;
   ENSURE(ctx->ord, sizeof(int32_t) * T);
@@ -585,31 +590,55 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
     launch_group_stage(P<int32_t>(ctx->gcnt), G, r->group_anchor, r->cost, (int)nz2,
                        P<int32_t>(ctx->goff), dcnt, dcnt + G + 1, dcst, st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(st));
-    R.gcnt.assign(cnt, cnt + G + 1);
-    R.ga_host.assign(gan, gan + G);
-    R.cost_host.assign(cst, cst + nz2);
-    if (R.gcnt[G] != 0) return fail(ctx, PVT_EINVAL, "task_group out of range");
-    R.ginfo = ca;
-    int mx = 0;
-    for (int g = 0; g < G; g++) mx = std::max(mx, R.gcnt[g]);
-    if (mx <= GSORT_MAX) {                    // (offsets and cursors: group_stage_kernel)
-      ENSURE(ctx->gskey, sizeof(uint64_t) * T);
-      ENSURE(ctx->gsidx, sizeof(int32_t) * T);
-      const uint64_t* keys = nullptr;
-      if (r->sort_tasks) {
-        ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
-        launch_norm_keys(r->dem, T, nullptr, P<uint64_t>(ctx->keys64a), st);
-        keys = P<uint64_t>(ctx->keys64a);
-      }
-      launch_group_scatter(r->task_group, keys, T, G, P<int32_t>(ctx->goff) + G + 1,
-                           P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx), st);
-      launch_group_sort(P<int32_t>(ctx->goff), G, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx),
-                        cur, st);
-      *ord_out = cur;
-      return PVT_OK;
+    // the per-group sorts, optimistically (a group over GSORT_MAX tasks is left unsorted by the
+    // kernel; build_order_check then redoes the order with radix passes)
+    ENSURE(ctx->gskey, sizeof(uint64_t) * T);
+    ENSURE(ctx->gsidx, sizeof(int32_t) * T);
+    const uint64_t* keys = nullptr;
+    if (r->sort_tasks) {
+      ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
+      launch_norm_keys(r->dem, T, nullptr, P<uint64_t>(ctx->keys64a), st);
+      keys = P<uint64_t>(ctx->keys64a);
     }
+    launch_group_scatter(r->task_group, keys, T, G, P<int32_t>(ctx->goff) + G + 1,
+                         P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx), st);
+    launch_group_sort(P<int32_t>(ctx->goff), G, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx),
+                      cur, st);
+    R.ginfo = ca;
+    *pending = true;
+    *ord_out = cur;
+    return PVT_OK;
   }
+  return build_order_radix(ctx, r, ord_out);
+}
+
+// After the caller's synchronisation: the group counts, anchors and cost table the optimistic
+// path staged; *redo = a group exceeded the LDS sort (the order must be rebuilt by radix passes).
+static int build_order_check(pvt_ctx* ctx, const pvt_round* r, bool* redo) {
+  RoundState& R = ctx->rs;
+  const int G = r->n_groups;
+  const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
+  const size_t nz2 = ca ? (size_t)r->n_zones * r->n_zones : 0;
+  const double* cst = reinterpret_cast<const double*>(ctx->gstage);
+  const int32_t* cnt = reinterpret_cast<const int32_t*>(cst + nz2);
+  const int32_t* gan = cnt + G + 1;
+  R.gcnt.assign(cnt, cnt + G + 1);
+  R.ga_host.assign(gan, gan + G);
+  R.cost_host.assign(cst, cst + nz2);
+  if (R.gcnt[G] != 0) return fail(ctx, PVT_EINVAL, "task_group out of range");
+  int mx = 0;
+  for (int g = 0; g < G; g++) mx = std::max(mx, R.gcnt[g]);
+  *redo = mx > GSORT_MAX;
+  return PVT_OK;
+}
+
+// Processing order by radix passes: stable by descending norm (sort_tasks), then stable by group.
+static int build_order_radix(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out) {
+  const int T = r->n_tasks;
+  hipStream_t st = ctx->stream;
+  int32_t* cur = P<int32_t>(ctx->ord);
+  int32_t* alt = P<int32_t>(ctx->ord2);
+  const bool grouped = r->task_group != nullptr && r->n_groups > 1;
   launch_iota(cur, T, st);
   if (r->sort_tasks) {
     ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
@@ -813,19 +842,32 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   hipStream_t st = ctx->stream;
   HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
 
-  if ((rc = build_order(ctx, r, &R.ord))) return rc;
-  HIPCHK(hipMemcpyAsync(r->order, R.ord, sizeof(int32_t) * T, hipMemcpyDeviceToDevice, st));
-
+  bool pending = false;
+  if ((rc = build_order(ctx, r, &R.ord, &pending))) return rc;
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   ENSURE(ctx->grp_ord, sizeof(int32_t) * T);
-  launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
-                      P<int32_t>(ctx->anc_ord), P<int32_t>(ctx->grp_ord), st);
+  auto order_out = [&]() -> int {
+    HIPCHK(hipMemcpyAsync(r->order, R.ord, sizeof(int32_t) * T, hipMemcpyDeviceToDevice, st));
+    launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
+                        P<int32_t>(ctx->anc_ord), P<int32_t>(ctx->grp_ord), st, r->n_groups);
+    return PVT_OK;
+  };
+  if ((rc = order_out())) return rc;
   const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
   if (ca) {
     ENSURE(ctx->csum, sizeof(double) * Z * Z);
     ENSURE(ctx->bsum, sizeof(double) * Z * Z);
     launch_zone_tables(r->cost, r->bw, Z, P<double>(ctx->csum), P<double>(ctx->bsum), st);
+  }
+  if (pending) {   // the one synchronisation of the grouped order: counts, anchors, cost table
+    HIPCHK(hipStreamSynchronize(st));
+    bool redo = false;
+    if ((rc = build_order_check(ctx, r, &redo))) return rc;
+    if (redo) {
+      if ((rc = build_order_radix(ctx, r, &R.ord))) return rc;
+      if ((rc = order_out())) return rc;
+    }
   }
 
   // group boundaries in processing order (only cost_aware first-fit with sort_hosts needs them)

@@ -417,6 +417,6 @@ void launch_iota(int32_t* out, int n, hipStream_t st);
 // gather tasks into processing order: dem_ord[p][r] = dem[r*T + ord[p]], anc_ord[p]
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
                          const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
-                         int32_t* grp_ord, hipStream_t st);
+                         int32_t* grp_ord, hipStream_t st, int G = 0x7fffffff);
 
 }  // namespace pvt

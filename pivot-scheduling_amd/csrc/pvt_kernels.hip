@@ -986,7 +986,8 @@ __global__ __launch_bounds__(1024) void group_scatter_kernel(const int32_t* tg, 
                                                              int32_t* sidx) {
   __shared__ int32_t loc[GAGG_MAX];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  const int g = i < T ? tg[i] : -1;
+  int g = i < T ? tg[i] : -1;
+  if (g >= G) g = -1;            // (out of range: the host rejects the round after its sync)
   if (G <= GAGG_MAX) {
     // rank within the block's share of the group, then one reservation per (block, group)
     for (int q = threadIdx.x; q < G; q += blockDim.x) loc[q] = 0;
@@ -1017,7 +1018,7 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
   __shared__ uint64_t k[GSORT_MAX];
   __shared__ int32_t v[GSORT_MAX];
   const int a = off[blockIdx.x], n = off[blockIdx.x + 1] - a, tid = threadIdx.x;
-  if (n <= 0) return;
+  if (n <= 0 || n > GSORT_MAX) return;   // (larger groups: the host sorts with radix passes)
   if (n <= 1024) {
     // rank by counting: the keys (sort key, task index) are distinct, so an element's place is
     // the number of elements below it -- every thread scans the group's keys in LDS (broadcast
@@ -1073,20 +1074,21 @@ void launch_iota(int32_t* out, int n, hipStream_t st) {
 
 __global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const int32_t* tg,
                                     const int32_t* ga, int T, double* dem_ord, int32_t* anc_ord,
-                                    int32_t* grp_ord) {
+                                    int32_t* grp_ord, int G) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= T) return;
   const int t = ord[p];
   double* o = dem_ord + (size_t)p * 4;
   o[0] = dem[t]; o[1] = dem[(size_t)T + t]; o[2] = dem[2 * (size_t)T + t]; o[3] = dem[3 * (size_t)T + t];
-  if (anc_ord) anc_ord[p] = (tg && ga) ? ga[tg[t]] : 0;
+  // (a group id out of range reads no anchor: the host rejects such a round after its sync)
+  if (anc_ord) anc_ord[p] = (tg && ga && tg[t] >= 0 && tg[t] < G) ? ga[tg[t]] : 0;
   if (grp_ord) grp_ord[p] = tg ? tg[t] : 0;
 }
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
                          const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
-                         int32_t* grp_ord, hipStream_t st) {
+                         int32_t* grp_ord, hipStream_t st, int G) {
   hipLaunchKernelGGL(gather_tasks_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, ord,
-                     task_group, group_anchor, T, dem_ord, anc_ord, grp_ord);
+                     task_group, group_anchor, T, dem_ord, anc_ord, grp_ord, G);
 }
 
 }  // namespace pvt
