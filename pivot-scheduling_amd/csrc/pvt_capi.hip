@@ -181,6 +181,7 @@ struct pvt_ctx {
   int t_epoch_plan = 1;           // PVT_EPOCH_PLAN: 0 = epoch chains by distinct zone only
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
+  int res_pairs = 0;              // PVT_RES_PAIRS: resident first-candidate rounds two tasks per exchange
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
@@ -355,6 +356,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_OF_HOSTS")) ctx->t_of_hosts = std::max(ZW_M, atoi(e));   // tuning
   if (const char* e = getenv("PVT_EPOCH_PLAN")) ctx->t_epoch_plan = atoi(e);           // A/B
   if (const char* e = getenv("PVT_MERGE_SMALL")) ctx->t_merge_bitonic = atoi(e) == 0;  // A/B
+  if (const char* e = getenv("PVT_RES_PAIRS")) ctx->res_pairs = atoi(e) != 0;          // A/B
   if (const char* e = getenv("PVT_RES_WAVES")) ctx->res_waves = atoi(e) == 8 ? 8 : atoi(e) == 2 ? 2 : atoi(e) == 1 ? 1 : 4;  // A/B
   *out = ctx;
   return PVT_OK;
@@ -555,7 +557,6 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
   ENSURE(ctx->ord, sizeof(int32_t) * T);
   ENSURE(ctx->ord2, sizeof(int32_t) * T);
   int32_t* cur = P<int32_t>(ctx->ord);
-  int32_t* alt = P<int32_t>(ctx->ord2);
   const bool grouped = r->task_group != nullptr && r->n_groups > 1;
   RoundState& R = ctx->rs;
   R.ginfo = false;
@@ -577,9 +578,6 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
       HIPCHK(hipHostMalloc(&ctx->gstage, need));
       ctx->gstage_cap = need;
     }
-    double* cst = reinterpret_cast<double*>(ctx->gstage);
-    int32_t* cnt = reinterpret_cast<int32_t*>(cst + nz2);
-    int32_t* gan = cnt + G + 1;
     // counts, anchors and cost table written into the pinned buffer by one kernel, which also
     // leaves the groups' offsets and scatter cursors on the device
     ENSURE(ctx->goff, sizeof(int32_t) * 2 * (G + 1));
@@ -1815,7 +1813,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     bytes += c * bytes_per_candidate(mode);
   }
   if (desc_dev) {
-    ResidentArgs ra{desc_dev, mt_dev, maxZ, tpad};
+    ResidentArgs ra{desc_dev, mt_dev, maxZ, tpad, ctx->stamps, ctx->res_pairs};
     {
       Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
       launch_resident(mode, waves, hpl, n, ra, st);
@@ -1845,7 +1843,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     HIPCHK(hipMemcpyAsync(mt, ctx->rmt_host, sizeof(uint32_t) * 625 * n, hipMemcpyHostToDevice, st));
   }
   HIPCHK(hipMemcpyAsync(ctx->rdesc.p, ctx->rstage, sizeof(pvt_round) * n, hipMemcpyHostToDevice, st));
-  ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad};
+  ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad, ctx->stamps, ctx->res_pairs};
   {
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mode, waves, hpl, n, ra, st);

@@ -659,23 +659,16 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       double e0 = 0.0, e1 = 0.0, e2 = 0.0, e3 = 0.0;
       int nsv = 0, ccv = 0;
       uint32_t kv = 0;
-      int cd[OPP_C];
-#pragma unroll
-      for (int x = 0; x < OPP_C; x++) cd[x] = 0x7fffffff;
       if (mine) {
         const double* dp = A.dem + (size_t)(s + lane) * 4;
         e0 = dp[0]; e1 = dp[1]; e2 = dp[2]; e3 = dp[3];
         nsv = S.nspec[lane];
         kv = S.kdraw[lane];
         ccv = nsv > 0 ? S.ccount[lane] : 0;
-#pragma unroll
-        for (int x = 0; x < OPP_C; x++)
-          if (x < ccv) cd[x] = S.cand[lane][x];
       }
-      const int c0l = cd[0];
-      int cmax = ccv > 0 ? cd[0] : -1;   // the largest candidate (candidates ascend)
-#pragma unroll
-      for (int x = 1; x < OPP_C; x++) cmax = x < ccv ? cd[x] : cmax;
+      // the candidates stay in S.cand (read there on the rare paths: registers kept for the walk)
+      const int c0l = ccv > 0 ? S.cand[lane][0] : 0x7fffffff;
+      const int cmax = ccv > 0 ? S.cand[lane][ccv - 1] : -1;   // the largest (candidates ascend)
       int nnew = 0, mm = 0;
       bool dok = true;
       uint32_t lm = 0;
@@ -686,7 +679,7 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
         const int xs = select_bit(valid, mm);
         const double z0 = S.cav[lane][0][xs], z1 = S.cav[lane][1][xs];
         const double z2 = S.cav[lane][2][xs], z3 = S.cav[lane][3][xs];
-        S.pw[lane] = cd[xs];
+        S.pw[lane] = S.cand[lane][xs];
         S.pz[lane][0] = z0; S.pz[lane][1] = z1; S.pz[lane][2] = z2; S.pz[lane][3] = z3;
         S.pz[lane][4] = z0 - e0; S.pz[lane][5] = z1 - e1; S.pz[lane][6] = z2 - e2; S.pz[lane][7] = z3 - e3;
         return true;
@@ -740,9 +733,8 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
         if (lostm | rngm) {
           const bool lost = (lostm >> lane) & 1ull;
           if ((rngm >> lane) & 1ull) {   // cw's capacity is now m; a lost cw stops fitting
-#pragma unroll
-            for (int x = 0; x < OPP_C; x++) {
-              if (cd[x] == cw) {
+            for (int x = 0; x < ccv; x++) {
+              if (S.cand[lane][x] == cw) {
                 S.cav[lane][0][x] = m0; S.cav[lane][1][x] = m1;
                 S.cav[lane][2][x] = m2; S.cav[lane][3][x] = m3;
                 if (lost) lm |= 1u << x;
@@ -756,13 +748,21 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
             dok = dok & (ntrue > 0) & (rint_mask((uint32_t)(ntrue - 1)) == rint_mask((uint32_t)(nsv - 1))) &
                   (kv <= (uint32_t)(ntrue - 1));
           }
-          wave_lds_fence();
-          const bool redo = ((lostm | rngm) >> lane) & 1ull;
-          bool ok = (okm >> lane) & 1ull;
-          if (redo) ok = choose();
-          okm = __ballot(ok);
-          wave_lds_fence();
-          if (Ln < R) row(Ln);
+          // The choice moves only for a lane whose candidates changed (rngm) or whose lost host
+          // lay below its candidates (mm grew); a lost host above them leaves it in place, and a
+          // draw that no longer holds only clears the lane's ok bit. Rows are rewritten (and the
+          // next row read again) only when some lane's choice moved.
+          const bool redo = (((rngm >> lane) & 1ull) != 0) | (lost & (cw < c0l));
+          bool ok = ((okm >> lane) & 1ull) & dok;
+          if (__ballot(redo)) {
+            wave_lds_fence();
+            if (redo) ok = choose();
+            okm = __ballot(ok);
+            wave_lds_fence();
+            if (Ln < R) row(Ln);
+          } else {
+            okm = __ballot(ok);
+          }
         }
         L = Ln;
       }

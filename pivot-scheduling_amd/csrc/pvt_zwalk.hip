@@ -193,7 +193,6 @@ template <bool KEYED, bool STRICT, bool FF = false, int WM = ZW_M>
 __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   static_assert(!FF || (!KEYED && STRICT), "FF: chain mode, strict fit");
   static_assert(WM == ZW_M || !KEYED, "keyed / ordered / sharded windows: ZW_M hosts");
-  constexpr int ZW_CH = WM / 64;           // window chunks (one wave step each)
   __shared__ ZwalkLDS<WM> S;
 #ifdef PVT_STAMPS
   const uint64_t t_start = zstamp();
@@ -823,9 +822,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           store_b();                           // it works on LDS from p0 + 1 on
           double g0 = n0, g1 = n1, g2 = n2, g3 = n3;
           uint64_t fm = fm0, m = fm0 & rzm;
-          for (int pass = 0;; pass++) {        // the register chunk (advancing past dead ones)
 #ifdef PVT_STAMPS
+          for (int pass = 0;; pass++) {        // the register chunk (advancing past dead ones)
             n_chunks += pass > 0;
+#else
+          for (;;) {                           // the register chunk (advancing past dead ones)
 #endif
             if (fm & ~rzm)                     // fitting hosts of U outside the anchor's
               m = __ballot(zero_exact((fm >> lane) & 1ull, (rzm >> lane) & 1ull, ra0, ra1, ra2,

@@ -85,6 +85,66 @@ def test_ca_bf_zero_scores_and_underflow(engine, resident):
         _assert_same(res, oracle.place(r), "scenario %d" % s)
 
 
+def test_ca_bf_screen_edges(engine):
+    """The resident best-fit screen's edges: capacities and demands beyond 2^498 (insane slots,
+    out-of-range demands), residuals of 2^-300 and just below (near-exact fits) and
+    negative demands that grow a host past 2^498 -- each must fall back to the exact test.
+    (Magnitudes stay below ~1e153 so no residual norm overflows: a NaN score -- 0 * inf -- is
+    outside the engine's numerics, DESIGN.md "Numerics".)"""
+    rounds = []
+    for s in range(8):
+        r = synthetic.make_round(_abi.PVT_CA_BF, 700, 500, seed=90 + s)
+        r.avail = r.avail.copy()
+        r.dem = r.dem.copy()
+        r.avail[:, 3::41] = 1e152                       # insane hosts (> 2^498 ~ 8.2e149)
+        r.avail[1, 5::43] = 2.0 ** 499
+        for k in range(7, 700, 29):                     # one residual 2^-300 / just under, rest 0
+            t = (k * 3 + s) % r.n_tasks
+            dim = (k // 2) % 2                          # (cpu or memory)
+            r.dem[dim, t] = 0.0
+            r.avail[:, k] = r.dem[:, t]
+            r.avail[dim, k] = 2.0 ** -300 if k % 2 else 2.0 ** -301
+        r.dem[:, 11::97] = -1e151                       # out-of-range (negative) demands
+        r.dem[2, 13::89] = 1e151
+        rounds.append(r)
+    got = engine.place_batch(rounds)
+    for s, (r, res) in enumerate(zip(rounds, got)):
+        _assert_same(res, oracle.place(r), "scenario %d" % s)
+
+
+@pytest.mark.parametrize("mode", ALL_MODES)
+def test_resident_dim_bounds(engine, mode):
+    """The third / fourth capacity bounds that let the resident kernel compare two dimensions:
+    demands that use those dimensions (bounds shrinking to failure), negative ones (bounds kept),
+    a NaN capacity there (bounds void), and -inf demands against padded lanes (H not a
+    multiple of the lanes: padding must never fit)."""
+    rounds = []
+    for s in range(12):
+        H = 700 + 37 * s
+        r = synthetic.make_round(mode, H, 600, seed=300 + s)
+        r.avail = r.avail.copy()
+        r.dem = r.dem.copy()
+        rs = np.random.RandomState(s)
+        if s % 4 == 0:
+            r.dem[2] = rs.uniform(0, 0.5, r.n_tasks)          # the bound shrinks every commit
+        elif s % 4 == 1:
+            r.dem[3, ::3] = -rs.uniform(0, 0.01, len(r.dem[3, ::3]))   # negative: bound kept
+            r.dem[2, ::7] = 30.0                                  # above some hosts' capacity
+            r.avail[2, ::5] = 20.0
+        elif s % 4 == 2:
+            r.avail[3, 11] = np.nan                               # the bounds are void
+            r.dem[3] = rs.uniform(0, 0.001, r.n_tasks)
+        else:
+            if mode in (_abi.PVT_VBP_FF, _abi.PVT_OPP, _abi.PVT_CA_FF):
+                r.dem[0, 5::50] = -np.inf                         # fits every real host
+                r.dem[1, 5::50] = -np.inf
+            r.dem[2, 9::11] = 100.0                               # exactly the capacity
+        rounds.append(r)
+    got = engine.place_batch(rounds)
+    for s, (r, res) in enumerate(zip(rounds, got)):
+        _assert_same(res, oracle.place(r), "scenario %d" % s)
+
+
 def test_batch_golden_runs(engine):
     """Every golden run (reference schedule() calls) batched per policy configuration."""
     by_mode = {}

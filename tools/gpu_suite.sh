@@ -32,6 +32,8 @@ for s in "$@"; do
     b_shard)    run b_shard 200 python bench.py --shard hosts $NB ;;
     st_zw)      for m in ca_bf vbp_ff ca_ff; do run st_$m 120 python tools/zwalk_stamps.py 1000000 10000 libpivot_place_stamps.so $m; done ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
+    t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
+    st_res)     for m in ${RES_MODES:-ca_bf vbp_bf vbp_ff ca_ff}; do run st_res_$m 120 python tools/resident_stamps.py $m; done ;;
     st_opp)     run st_opp 150 python tools/commit_stamps.py 2 1000000 10000 ;;
     profbench)  mkdir -p gpurun_out/prof; run profbench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 $NB ;;
     pmc)        run pmc 1100 tools/pmc_all.sh "${PMC_TAG:-r04z}" ;;
