@@ -172,7 +172,7 @@ KCLASSES = (("score", 0), ("merge", 1), ("commit", 2), ("other", 3))
 WALK_KERNELS = ("zwalk_kernel", "commit_kernel", "lwalk_kernel", "opp_commit_kernel")
 PAR_KERNELS = ("score_kernel", "band_score_kernel", "opp_count_kernel", "perm_scan_kernel",
                "ordered_kernel", "resident_kernel", "merge_kernel", "merge_small_kernel",
-               "merge_pkg_kernel", "merge_mid_kernel")
+               "merge_pkg_kernel", "merge_path_kernel")
 
 
 def kstats_all(eng):

@@ -138,7 +138,7 @@ int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
  * placement path ("zwalk_kernel", "commit_kernel", "lwalk_kernel", "opp_commit_kernel",
  * "opp_count_kernel", "score_kernel", "band_score_kernel", "perm_scan_kernel", "ordered_kernel",
  * "resident_kernel", "merge_kernel", "merge_small_kernel", "merge_pkg_kernel",
- * "merge_mid_kernel"), each bracketed
+ * "merge_path_kernel"), each bracketed
  * by its own HIP events on the stream it runs on. An unknown or unlaunched name gives zeros. */
 int  pvt_get_kernel_kstats(pvt_ctx* ctx, const char* kernel, pvt_kstats* out);
 /* Tuning knob: tasks per window (0 = the policy's default; capped at 1024). */

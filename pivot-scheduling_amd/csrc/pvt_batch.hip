@@ -82,9 +82,8 @@ struct ResLds {
     ci = cd + 32 * RES_CHUNK;                          //       anchor, group i32[2][CHUNK] (+pad)
     mt = ci + 12 * RES_CHUNK;                          //       MT copies u32[WAVES][628]
     slot = mt + 4 * RES_MAXW * RES_MT_STRIDE;          //       posts u64[2][WAVES][2], then
-    // fast posts i32[2][WAVES], vbp best-fit s2 posts {u64, i32, i32}[2][WAVES], pair posts
-    // i32[2][WAVES][4]
-    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW + 32 * RES_MAXW;
+    // fast posts i32[2][WAVES], then vbp best-fit s2 posts {u64, i32, i32}[2][WAVES]
+    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     total = walk_end > sort_end ? walk_end : sort_end;
   }
@@ -140,39 +139,9 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
   __syncthreads();
 }
 
-// Fit mask of a lane's slots (bit j: slot j fits x, `>` when S else `>=`). When x2 and x3 pass
-// the block-uniform lower bounds lb2 / lb3 of every host's third and fourth capacities (see the
-// kernel), those two comparisons hold for every host and only the first two dimensions are
-// compared: a uniform branch.
-template <bool S, int HPL>
-__device__ __forceinline__ uint32_t fit_mask(const double* a0, const double* a1, const double* a2,
-                                             const double* a3, double x0, double x1, double x2,
-                                             double x3, double lb2, double lb3) {
-  const bool two = __builtin_amdgcn_readfirstlane(S ? (x2 < lb2 && x3 < lb3 ? 1 : 0)
-                                                    : (x2 <= lb2 && x3 <= lb3 ? 1 : 0)) != 0;
-  uint32_t m = 0;
-  if (two) {
-#pragma unroll
-    for (int j = 0; j < HPL; j++)
-      m |= ((S ? (a0[j] > x0) & (a1[j] > x1) : (a0[j] >= x0) & (a1[j] >= x1)) ? 1u : 0u) << j;
-  } else {
-#pragma unroll
-    for (int j = 0; j < HPL; j++) m |= (fits<S>(a0[j], a1[j], a2[j], a3[j], x0, x1, x2, x3) ? 1u : 0u) << j;
-  }
-  return m;
-}
-
-// |d| <= 2^498 in every dimension (not NaN): the cost_aware best-fit screen's demand range
-__device__ __forceinline__ bool sane_d(double d0, double d1, double d2, double d3) {
-  return __builtin_fabs(d0) <= 0x1p+498 && __builtin_fabs(d1) <= 0x1p+498 &&
-         __builtin_fabs(d2) <= 0x1p+498 && __builtin_fabs(d3) <= 0x1p+498;
-}
-
 template <int MODE, int WAVES, int HPL>
 __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) {
   constexpr int NT = WAVES * WAVE;
-  // two tasks per exchange for the first-candidate modes (see the pair step in the task loop)
-  constexpr bool PAIRS = (MODE == VBP_FF || MODE == CA_FF || MODE == CA_BF) && WAVES > 1;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool CA = (MODE == CA_FF || MODE == CA_BF);
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
@@ -207,9 +176,6 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   // zmask bit j = a fitting host of slot j scores exactly 0 (c == 0 and bw > 0; keyed: key bits
   // 0), rmask bit j = its score may underflow to 0 or is not a number (needs the full path)
   uint32_t zmask = 0, rmask = 0;
-  // cost_aware best-fit: smask bit j = slot j's capacities are all <= 2^498 (not NaN), kept
-  // current by the commits; with a demand of magnitude <= 2^498 every residual is <= 2^499
-  uint32_t smask = 0;
   int32_t zz[HPL];
   uint32_t tb[HPL];
 #pragma unroll
@@ -225,39 +191,7 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
     key[j] = 0.0;                         // first-fit by index unless keyed
     cc[j] = 0.0;
     bb[j] = 1.0;
-    smask |= (a0[j] <= 0x1p+498 && a1[j] <= 0x1p+498 && a2[j] <= 0x1p+498 && a3[j] <= 0x1p+498 ? 1u : 0u) << j;
   }
-  // lb2 / lb3: block-uniform lower bounds of every host's capacity in dimensions 2 and 3 (-inf
-  // when a host holds NaN there). A commit of x only lowers one host by x (x >= 0), so the
-  // bounds follow as lb - x (rounding is monotone: fl(lb - x) <= fl(a - x) for lb <= a); x < 0
-  // keeps them, a NaN x voids them. fit_mask skips those two comparisons while they hold.
-  double lb2 = DINF, lb3 = DINF;
-  {
-    bool nan23 = false;
-#pragma unroll
-    for (int j = 0; j < HPL; j++)
-      if (h0 + j < H) {
-        lb2 = fmin(lb2, a2[j]);
-        lb3 = fmin(lb3, a3[j]);
-        nan23 |= !(a2[j] == a2[j]) || !(a3[j] == a3[j]);
-      }
-    for (int o = 1; o < WAVE; o <<= 1) {
-      lb2 = fmin(lb2, __shfl_xor(lb2, o));
-      lb3 = fmin(lb3, __shfl_xor(lb3, o));
-    }
-    if (__ballot(nan23)) lb2 = lb3 = -DINF;
-    double* wl = reinterpret_cast<double*>(smem + ResLds(A.Zb, A.Tpad).slot);   // (posts: unused yet)
-    if (lane == 0) { wl[2 * wave] = lb2; wl[2 * wave + 1] = lb3; }
-    __syncthreads();
-    lb2 = wl[0]; lb3 = wl[1];
-#pragma unroll
-    for (int w = 1; w < WAVES; w++) { lb2 = fmin(lb2, wl[2 * w]); lb3 = fmin(lb3, wl[2 * w + 1]); }
-    // (a -inf from a NaN wave wins every fmin)
-  }
-  auto lb_commit = [&](double x2, double x3) {
-    lb2 = x2 >= 0.0 ? lb2 - x2 : (x2 < 0.0 ? lb2 : -DINF);
-    lb3 = x3 >= 0.0 ? lb3 - x3 : (x3 < 0.0 ? lb3 : -DINF);
-  };
 
   // a2: processing order (opportunistic keeps the caller's order)
   uint64_t* ka = reinterpret_cast<uint64_t*>(smem + Lo.u);
@@ -278,7 +212,6 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   int32_t* cposts = reinterpret_cast<int32_t*>(posts);              // opp: [2][WAVES]
   int32_t* fposts = reinterpret_cast<int32_t*>(smem + Lo.slot + 32 * RES_MAXW);   // [2][WAVES]
   uint64_t* vposts = reinterpret_cast<uint64_t*>(smem + Lo.slot + 40 * RES_MAXW);  // [2][WAVES][2]
-  int32_t* pposts = reinterpret_cast<int32_t*>(smem + Lo.slot + 72 * RES_MAXW);   // [2][WAVES][4]
   MtWave mw;
   mw.buf = 0; mw.used = 0; mw.limit = 0;
   if (MODE == OPP) {
@@ -289,13 +222,12 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
 
 #ifdef PVT_STAMPS
   // phases: 0 anchor rows, 1 slot scan, 2 wave reduction, 3 exchange (post, barrier, merge),
-  // 4 full path, 5 commit; counts: 6 steps, 7 full paths, 8 pair steps
+  // 4 full path, 5 commit; counts: 6 tasks, 7 full paths
   const bool stw = blockIdx.x == 0 && wave == 0 && A.stamps != nullptr;
-  uint64_t ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t tl = stw ? rstamp() : 0;
 #endif
   int cur_anc = -1, cur_grp = -1, cur_bgrp = -1;
-  int xs = 0;                             // exchange buffer parity (toggles every step)
   const bool rt = (MODE == CA_FF || MODE == CA_BF) && R.rt_bw != nullptr;
   for (int p0 = 0; p0 < T; p0 += RES_CHUNK) {
     const int n = min(RES_CHUNK, T - p0);
@@ -333,36 +265,16 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
       }
     }
     __syncthreads();
-    // Staged rows in registers: task q (d), q + 1 (e), and the loads of q + 2 (f) and q + 3 (g),
-    // issued while task q is scored (LDS latency off the chain) and rotated in at the next
-    // iteration's top by the step just taken (1, or 2 after a pair).
-    const int nl = n - 1;
-    double d0 = cd[0], d1 = cd[1], d2 = cd[2], d3 = cd[3];
-    int anc_q = c_anc[0], grp_q = c_grp[0];
-    double e0 = cd[min(1, nl) * 4 + 0], e1 = cd[min(1, nl) * 4 + 1], e2 = cd[min(1, nl) * 4 + 2],
-           e3 = cd[min(1, nl) * 4 + 3];
-    int anc_e = c_anc[min(1, nl)], grp_e = c_grp[min(1, nl)];
-    double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, g0 = 0.0, g1 = 0.0, g2 = 0.0, g3 = 0.0;
-    int anc_f = 0, grp_f = 0, anc_g = 0, grp_g = 0;
-    int step = 0;
-    for (int q = 0; q < n; q += step) {
-      if (step == 1) {
-        d0 = e0; d1 = e1; d2 = e2; d3 = e3; anc_q = anc_e; grp_q = grp_e;
-        e0 = f0; e1 = f1; e2 = f2; e3 = f3; anc_e = anc_f; grp_e = grp_f;
-      } else if (step == 2) {
-        d0 = f0; d1 = f1; d2 = f2; d3 = f3; anc_q = anc_f; grp_q = grp_f;
-        e0 = g0; e1 = g1; e2 = g2; e3 = g3; anc_e = anc_g; grp_e = grp_g;
-      }
-      step = 1;
+    // the next task's staged row is read while this task is scored (LDS latency off the chain)
+    double n0 = cd[0], n1 = cd[1], n2 = cd[2], n3 = cd[3];
+    int n_anc = c_anc[0], n_grp = c_grp[0];
+    for (int q = 0; q < n; q++) {
       const int p = p0 + q;
-      {
-        const int qf = min(q + 2, nl), qg = min(q + 3, nl);
-        f0 = cd[qf * 4 + 0]; f1 = cd[qf * 4 + 1]; f2 = cd[qf * 4 + 2]; f3 = cd[qf * 4 + 3];
-        anc_f = c_anc[qf]; grp_f = c_grp[qf];
-        if (PAIRS && A.pairs) {
-          g0 = cd[qg * 4 + 0]; g1 = cd[qg * 4 + 1]; g2 = cd[qg * 4 + 2]; g3 = cd[qg * 4 + 3];
-          anc_g = c_anc[qg]; grp_g = c_grp[qg];
-        }
+      const double d0 = n0, d1 = n1, d2 = n2, d3 = n3;
+      const int anc_q = n_anc, grp_q = n_grp;
+      if (q + 1 < n) {
+        n0 = cd[(q + 1) * 4 + 0]; n1 = cd[(q + 1) * 4 + 1]; n2 = cd[(q + 1) * 4 + 2]; n3 = cd[(q + 1) * 4 + 3];
+        n_anc = c_anc[q + 1]; n_grp = c_grp[q + 1];
       }
       if (CA) {
         const int anc = anc_q;
@@ -407,148 +319,17 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
       }
       RSTAMP(0);
       RCOUNT(6);
-      const int par = xs;
-      xs ^= 1;
-      if (PAIRS && A.pairs && q + 1 < n && anc_e == anc_q && ((!rt && !keyed) || grp_e == grp_q) &&
-          d0 >= 0.0 && d1 >= 0.0 && d2 >= 0.0 && d3 >= 0.0 &&
-          (MODE != CA_BF || (sane_d(d0, d1, d2, d3) && sane_d(e0, e1, e2, e3)))) {
-        // ---- a pair: tasks q and q + 1 from ONE exchange. Task q's demand is >= 0, so its
-        // commit only shrinks its host hw: every other host keeps its status for q + 1, and a
-        // host that was no candidate for q + 1 stays none (cost_aware best-fit: unless an exact
-        // fit appears, which the owner's post-commit test below sees). Each wave posts its first
-        // candidate for q, its first and second for q + 1 (pre-commit) and the post-commit status
-        // of its q candidate for q + 1; hw's wave's entries then give q + 1's winner.
-        uint32_t zs = 0, cm = 0;
-        if (MODE == CA_BF) { zs = zmask & smask & ~rmask; cm = zmask | rmask; }
-        int c = 0x7fffffff, c1 = 0x7fffffff, c2 = 0x7fffffff;
-        bool chk = false;
-        constexpr bool SP = MODE == CA_BF ? false : STRICT;
-        const uint32_t fmd = fit_mask<SP, HPL>(a0, a1, a2, a3, d0, d1, d2, d3, lb2, lb3);
-        const uint32_t fme = fit_mask<SP, HPL>(a0, a1, a2, a3, e0, e1, e2, e3, lb2, lb3);
-#pragma unroll
-        for (int j = HPL - 1; j >= 0; j--) {      // (descending: the lowest candidate slot wins)
-          bool k0, k1;
-          if (MODE == CA_BF) {
-            const bool f = (fmd >> j) & 1u;
-            const bool fe = (fme >> j) & 1u;
-            const bool zj = (zs >> j) & 1u, cj = (cm >> j) & 1u;
-            k0 = f && zj;
-            k1 = fe && zj;
-            chk |= f && !zj && (cj || !(fmax(a0[j] - d0, a1[j] - d1) >= 0x1p-300));
-            chk |= fe && !zj && (cj || !(fmax(a0[j] - e0, a1[j] - e1) >= 0x1p-300));
-          } else {
-            const bool zk = !keyed || ((zmask >> j) & 1u);
-            k0 = zk && ((fmd >> j) & 1u);
-            k1 = zk && ((fme >> j) & 1u);
-          }
-          c = k0 ? h0 + j : c;
-          c2 = k1 ? c1 : c2;
-          c1 = k1 ? h0 + j : c1;
-        }
-        const uint64_t any0 = __ballot(c != 0x7fffffff), any1 = __ballot(c1 != 0x7fffffff);
-        const int wc = any0 ? __builtin_amdgcn_readlane(c, __builtin_ctzll(any0)) : 0x7fffffff;
-        int wc1 = 0x7fffffff, wc2 = 0x7fffffff;
-        if (any1) {
-          const int l1 = __builtin_ctzll(any1);
-          const uint64_t rest = any1 & (any1 - 1ull);
-          wc1 = __builtin_amdgcn_readlane(c1, l1);
-          wc2 = __builtin_amdgcn_readlane(c2, l1);
-          if (wc2 == 0x7fffffff && rest) wc2 = __builtin_amdgcn_readlane(c1, __builtin_ctzll(rest));
-        }
-        // post-commit status of wc for q + 1, by its owner lane: bit 1 a candidate, bit 2 the
-        // full path would be needed (cost_aware best-fit: risky)
-        int fl = __ballot(chk) ? 1 : 0;
-        if (wc != 0x7fffffff) {
-          const int jw = wc & (HPL - 1);
-          double b0 = 0.0, b1 = 0.0, b2 = 0.0, b3 = 0.0;
-#pragma unroll
-          for (int j = 0; j < HPL; j++)
-            if (j == jw) { b0 = a0[j] - d0; b1 = a1[j] - d1; b2 = a2[j] - d2; b3 = a3[j] - d3; }
-          int st = 0;
-          if (MODE == CA_BF) {
-            const bool f = fits<false>(b0, b1, b2, b3, e0, e1, e2, e3);
-            const double mx = fmax(fmax(b0 - e0, b1 - e1), fmax(b2 - e2, b3 - e3));
-            const bool safe = !((rmask >> jw) & 1u), zc = (zmask >> jw) & 1u;
-            const bool z = safe && ((zc && mx <= 0x1p+500) || mx == 0.0);
-            st = (f && z ? 2 : 0) | (f && !z && (!safe || !(mx >= 0x1p-300) || zc) ? 4 : 0);
-          } else {
-            const bool zk = !keyed || ((zmask >> jw) & 1u);
-            st = zk && fits<STRICT>(b0, b1, b2, b3, e0, e1, e2, e3) ? 2 : 0;
-          }
-          fl |= __builtin_amdgcn_readlane(st, (wc / HPL) & (WAVE - 1));
-        }
-        RSTAMP(1);
-        if (lane == 0) {
-          int32_t* pp = pposts + (par * RES_MAXW + wave) * 4;
-          pp[0] = wc; pp[1] = wc1; pp[2] = wc2; pp[3] = fl;
-        }
-        __syncthreads();
-        int vx[WAVES], vy[WAVES], vz[WAVES], vf[WAVES];
-#pragma unroll
-        for (int w = 0; w < WAVES; w++) {
-          const int32_t* pp = pposts + (par * RES_MAXW + w) * 4;
-          vx[w] = pp[0]; vy[w] = pp[1]; vz[w] = pp[2]; vf[w] = pp[3];
-        }
-        int hw = vx[0], ab = vf[0];
-#pragma unroll
-        for (int w = 1; w < WAVES; w++) { hw = min(hw, vx[w]); ab |= vf[w]; }
-        hw = __builtin_amdgcn_readfirstlane(hw);
-        ab = __builtin_amdgcn_readfirstlane(ab) & 1;
-        RSTAMP(3);
-        // task q resolved here unless a wave met a slot the screen cannot decide, or (best-fit,
-        // keyed first-fit) no candidate anywhere sends it to the full path
-        const bool q_ok = !ab && (hw != 0x7fffffff || !(MODE == CA_BF || keyed));
-        if (q_ok) {
-          const int ws = hw != 0x7fffffff ? hw / (HPL * WAVE) : -1;
-          int h1 = 0x7fffffff;
-          bool ok1 = true;
-#pragma unroll
-          for (int w = 0; w < WAVES; w++) {
-            int cw = vy[w];
-            if (w == ws) {
-              const int alt = vy[w] == hw ? vz[w] : vy[w];
-              cw = (vf[w] & 2) ? min(hw, alt) : alt;
-              ok1 = ok1 && !(vf[w] & 4);
-            }
-            h1 = min(h1, cw);
-          }
-          h1 = __builtin_amdgcn_readfirstlane(h1);
-          ok1 = __builtin_amdgcn_readfirstlane(ok1 ? 1 : 0) != 0;
-          if (h1 == 0x7fffffff && (MODE == CA_BF || keyed)) ok1 = false;
-          RCOUNT(8);
-          if (ok1) step = 2;
-          // commits: q at hw, then q + 1 at h1 (possibly the same host)
-#pragma unroll
-          for (int k = 0; k < 2; k++) {
-            const int hk = k == 0 ? hw : h1;
-            if (k == 1 && !ok1) break;
-            if (hk == 0x7fffffff) continue;
-            const double x0 = k == 0 ? d0 : e0, x1 = k == 0 ? d1 : e1;
-            const double x2 = k == 0 ? d2 : e2, x3 = k == 0 ? d3 : e3;
-            lb_commit(x2, x3);
-            const int jw = hk & (HPL - 1);
-            if (hk / HPL == tid) {
-#pragma unroll
-              for (int j = 0; j < HPL; j++)
-                if (j == jw) {
-                  a0[j] -= x0; a1[j] -= x1; a2[j] -= x2; a3[j] -= x3;
-                  if (MODE == CA_BF) {
-                    const bool sn = a0[j] <= 0x1p+498 && a1[j] <= 0x1p+498 && a2[j] <= 0x1p+498 && a3[j] <= 0x1p+498;
-                    smask = (smask & ~(1u << j)) | ((sn ? 1u : 0u) << j);
-                  }
-                }
-              pl[p + k] = hk;
-            }
-          }
-          RSTAMP(5);
-          continue;
-        }
-        // (a fallback: task q goes through the single-task path below)
-      }
+      const int par = p & 1;
       if (MODE == OPP) {
         // feasible hosts of this lane (np.all(r >= d), opportunistic.py:15)
-        const uint32_t fm = fit_mask<false, HPL>(a0, a1, a2, a3, d0, d1, d2, d3, lb2, lb3);
-        const int cnt = __popc(fm);
+        uint32_t fm = 0;
+        int cnt = 0;
+#pragma unroll
+        for (int j = 0; j < HPL; j++) {
+          const bool f = fits<false>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+          fm |= (f ? 1u : 0u) << j;
+          cnt += f ? 1 : 0;
+        }
         const int inc = wave_incl_scan_dpp(cnt);
         const int wt = __builtin_amdgcn_readlane(inc, 63);
         int ntot = wt, off = 0;
@@ -566,7 +347,6 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
           }
         }
         if (ntot == 0) continue;
-        lb_commit(d2, d3);                 // (a commit follows: the k-th feasible host takes d)
         const int k = (int)mt_randint(mk, mw, (uint32_t)ntot) - off;   // randomizer.choice (:16)
         if (k >= 0 && k < wt && inc > k && inc - cnt <= k) {
           int rr = k - (inc - cnt);
@@ -593,50 +373,29 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
         int c = 0x7fffffff;
         bool risky = false;
         if (MODE == CA_BF) {
-          // Screen: with a demand of magnitude <= 2^498 (uniform), a fitting slot that is zero-
-          // cost, safe and sane (zs: all capacities <= 2^498, so every residual is <= 2^499)
-          // scores exactly 0; a fitting safe slot of cost > 0 with a residual >= 2^-300 in one of
-          // the first two dimensions (two: cpu counts fit exactly often) has mx >= 2^-300, so it
-          // neither scores 0 nor is risky. Every other fitting slot (unsafe, insane, or an exact
-          // or near-exact fit in both dimensions)
-          // sends the wave to the exact test below, as does an out-of-range demand.
-          const bool dsane = sane_d(d0, d1, d2, d3);
-          bool chk = !dsane;
-          if (dsane) {
-            const uint32_t zs = zmask & smask & ~rmask, cm = zmask | rmask;
-            const uint32_t fm = fit_mask<false, HPL>(a0, a1, a2, a3, d0, d1, d2, d3, lb2, lb3);
+          // from the largest residual mx = max(a - d) of a fitting host (all residuals >= +0):
+          // mx == 0 is an exact fit (s2 == 0, score 0); mx >= 2^-300 gives s2 >= 2^-600 (the FMA
+          // chain only adds non-negative terms), so with a safe slot and c > 0 the score is
+          // >= 2^-900; with c == 0 the score is 0 while s2 is finite (mx <= 2^500). Anything
+          // else is risky and goes to the full path.
 #pragma unroll
-            for (int j = HPL - 1; j >= 0; j--) {   // (descending: the lowest candidate slot wins)
-              const bool f = (fm >> j) & 1u;
-              const bool zj = (zs >> j) & 1u;
-              c = (f && zj) ? h0 + j : c;
-              chk |= f && !zj && (((cm >> j) & 1u) || !(fmax(a0[j] - d0, a1[j] - d1) >= 0x1p-300));
-            }
+          for (int j = HPL - 1; j >= 0; j--) {     // (descending: the lowest candidate slot wins)
+            const bool f = fits<false>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+            const double mx = fmax(fmax(a0[j] - d0, a1[j] - d1), fmax(a2[j] - d2, a3[j] - d3));
+            const bool safe = !((rmask >> j) & 1u), zc = (zmask >> j) & 1u;
+            const bool z = safe && ((zc && mx <= 0x1p+500) || mx == 0.0);
+            c = (f && z) ? h0 + j : c;
+            risky |= f && !z && (!safe || !(mx >= 0x1p-300) || zc);
           }
-          if (__ballot(chk)) {
-            // exact test, from the largest residual mx = max(a - d) of a fitting host (all
-            // residuals >= +0): mx == 0 is an exact fit (s2 == 0, score 0); mx >= 2^-300 gives
-            // s2 >= 2^-600 (the FMA chain only adds non-negative terms), so with a safe slot and
-            // c > 0 the score is >= 2^-900; with c == 0 the score is 0 while s2 is finite
-            // (mx <= 2^500). Anything else is risky and goes to the full path.
-            c = 0x7fffffff;
-#pragma unroll
-            for (int j = HPL - 1; j >= 0; j--) {
-              const bool f = fits<false>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
-              const double mx = fmax(fmax(a0[j] - d0, a1[j] - d1), fmax(a2[j] - d2, a3[j] - d3));
-              const bool safe = !((rmask >> j) & 1u), zc = (zmask >> j) & 1u;
-              const bool z = safe && ((zc && mx <= 0x1p+500) || mx == 0.0);
-              c = (f && z) ? h0 + j : c;
-              risky |= f && !z && (!safe || !(mx >= 0x1p-300) || zc);
-            }
-            // (a non-finite demand can leave a NaN residual that fmax drops: full path)
-            risky |= !(__builtin_fabs(d0) < DINF && __builtin_fabs(d1) < DINF &&
-                       __builtin_fabs(d2) < DINF && __builtin_fabs(d3) < DINF);
-          }
+          // (a non-finite demand can leave a NaN residual that fmax drops: full path)
+          risky |= !(__builtin_fabs(d0) < DINF && __builtin_fabs(d1) < DINF &&
+                     __builtin_fabs(d2) < DINF && __builtin_fabs(d3) < DINF);
         } else {
-          const uint32_t fm = fit_mask<STRICT, HPL>(a0, a1, a2, a3, d0, d1, d2, d3, lb2, lb3) &
-                              (keyed ? zmask : ~0u);
-          c = fm ? h0 + __builtin_ctz(fm) : 0x7fffffff;
+#pragma unroll
+          for (int j = HPL - 1; j >= 0; j--) {
+            const bool f = fits<STRICT>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+            c = (f && (!keyed || ((zmask >> j) & 1u))) ? h0 + j : c;
+          }
         }
         RSTAMP(1);
         const uint64_t any = __ballot(c != 0x7fffffff);
@@ -676,10 +435,9 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
         uint64_t sb[HPL];
         uint64_t ls = NONE;
         int lh = 0x7fffffff;
-        const uint32_t fm = fit_mask<true, HPL>(a0, a1, a2, a3, d0, d1, d2, d3, lb2, lb3);
 #pragma unroll
         for (int j = 0; j < HPL; j++) {
-          const bool f = (fm >> j) & 1u;
+          const bool f = fits<true>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
           sb[j] = f ? dbits(norm2_seq(a0[j] - d0, a1[j] - d1, a2[j] - d2, a3[j] - d3)) : NONE;
           if (sb[j] < ls) { ls = sb[j]; lh = h0 + j; }
         }
@@ -785,18 +543,11 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
         RSTAMP(4);
       }
       if (hw == 0x7fffffff) continue;    // no host fits: the task stays waiting
-      lb_commit(d2, d3);
       const int jw = hw & (HPL - 1);     // uniform: the owning lane's register slot
       if (hw / HPL == tid) {
 #pragma unroll
         for (int j = 0; j < HPL; j++)
-          if (j == jw) {
-            a0[j] -= d0; a1[j] -= d1; a2[j] -= d2; a3[j] -= d3;   // resc[h] -= d
-            if (MODE == CA_BF) {
-              const bool sn = a0[j] <= 0x1p+498 && a1[j] <= 0x1p+498 && a2[j] <= 0x1p+498 && a3[j] <= 0x1p+498;
-              smask = (smask & ~(1u << j)) | ((sn ? 1u : 0u) << j);
-            }
-          }
+          if (j == jw) { a0[j] -= d0; a1[j] -= d1; a2[j] -= d2; a3[j] -= d3; }   // resc[h] -= d
         pl[p] = hw;
       }
       RSTAMP(5);
@@ -804,7 +555,7 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   }
 #ifdef PVT_STAMPS
   if (stw && lane == 0)
-    for (int k = 0; k < 9; k++) A.stamps[k] += ph[k];
+    for (int k = 0; k < 8; k++) A.stamps[k] += ph[k];
 #endif
 
   __syncthreads();

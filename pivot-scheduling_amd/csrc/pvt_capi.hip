@@ -181,7 +181,6 @@ struct pvt_ctx {
   int t_epoch_plan = 1;           // PVT_EPOCH_PLAN: 0 = epoch chains by distinct zone only
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
-  int res_pairs = 0;              // PVT_RES_PAIRS: resident first-candidate rounds two tasks per exchange
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
@@ -356,7 +355,6 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_OF_HOSTS")) ctx->t_of_hosts = std::max(ZW_M, atoi(e));   // tuning
   if (const char* e = getenv("PVT_EPOCH_PLAN")) ctx->t_epoch_plan = atoi(e);           // A/B
   if (const char* e = getenv("PVT_MERGE_SMALL")) ctx->t_merge_bitonic = atoi(e) == 0;  // A/B
-  if (const char* e = getenv("PVT_RES_PAIRS")) ctx->res_pairs = atoi(e) != 0;          // A/B
   if (const char* e = getenv("PVT_RES_WAVES")) ctx->res_waves = atoi(e) == 8 ? 8 : atoi(e) == 2 ? 2 : atoi(e) == 1 ? 1 : 4;  // A/B
   *out = ctx;
   return PVT_OK;
@@ -1813,7 +1811,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     bytes += c * bytes_per_candidate(mode);
   }
   if (desc_dev) {
-    ResidentArgs ra{desc_dev, mt_dev, maxZ, tpad, ctx->stamps, ctx->res_pairs};
+    ResidentArgs ra{desc_dev, mt_dev, maxZ, tpad, ctx->stamps};
     {
       Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
       launch_resident(mode, waves, hpl, n, ra, st);
@@ -1843,7 +1841,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     HIPCHK(hipMemcpyAsync(mt, ctx->rmt_host, sizeof(uint32_t) * 625 * n, hipMemcpyHostToDevice, st));
   }
   HIPCHK(hipMemcpyAsync(ctx->rdesc.p, ctx->rstage, sizeof(pvt_round) * n, hipMemcpyHostToDevice, st));
-  ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad, ctx->stamps, ctx->res_pairs};
+  ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad, ctx->stamps};
   {
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mode, waves, hpl, n, ra, st);

@@ -397,7 +397,6 @@ struct ResidentArgs {
   int Zb;                 // zone-table stride in LDS: max n_zones of the batch
   int Tpad;               // power of two >= max n_tasks of the batch (sort network size)
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): block 0 wave 0 phase cycles
-  int pairs;              // first-candidate modes: two tasks per exchange (pvt_batch.hip)
 };
 size_t resident_lds_bytes(int Zb, int Tpad);
 void resident_shape(int maxH, int* waves, int* hpl);

@@ -591,24 +591,32 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   }
 }
 
-// Merge of up to LMAX / KL score-segment lists (vbp best-fit band lists: 16 segments) with the
-// same rank-by-counting, one block per task: each entry's merged position is its index in its own
-// list plus its lower bound in every other list (binary searches in LDS), so no sorting network
-// and no barrier between the load and the store (the bitonic merge_kernel runs 55 barrier stages
-// over 1024 keys).
-__global__ __launch_bounds__(256) void merge_mid_kernel(MergeArgs A) {
-  __shared__ Key lk[LMAX];
-  __shared__ Key out[LMAX];
+// Merge of up to LMAX / KL score-segment lists (vbp best-fit band lists: 16 segments), each
+// already sorted, by merge path, one block per task: the segments (padded with invalid keys to a
+// power of two) are merged pairwise in log2(segments) rounds; in a round every thread takes four
+// consecutive outputs of its pair, finds how many of them come from the first list by a binary
+// search of the merge path (co-rank), then merges those four. 4 rounds of ~10 dependent LDS
+// probes instead of rank-by-counting's 15 binary searches per entry (1.9 ms per config-5 round,
+// slower than the 55-stage bitonic network that ignores the segments' order, 1.6 ms).
+__global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
+  __shared__ Key ka[LMAX];
+  __shared__ Key kb[LMAX];
   __shared__ int cnt_sh;
   const int task = blockIdx.x, tid = threadIdx.x;
   if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
-  const int S = A.S, n = S * KL;
+  const int S = A.S;
+  int P = 1;
+  while (P < S) P <<= 1;
+  const int n = P * KL;                          // <= LMAX (merge_variant)
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
   if (tid == 0) cnt_sh = 0;
   for (int j = tid; j < n; j += 256) {
-    const SegEntry se = A.seg[(size_t)task * S * KL + j];
-    lk[j] = {se.s, se.tb, se.id};
-    out[j] = inv;
+    Key k = inv;
+    if (j < S * KL) {
+      const SegEntry se = A.seg[(size_t)task * S * KL + j];
+      k = {se.s, se.tb, se.id};
+    }
+    ka[j] = k;
   }
   // bound: the smallest last entry of a segment with more than KL feasible hosts (every thread
   // derives it: S loads, no barrier on its path)
@@ -624,28 +632,47 @@ __global__ __launch_bounds__(256) void merge_mid_kernel(MergeArgs A) {
     }
   }
   __syncthreads();
-  int c = 0;
-  for (int j = tid; j < n; j += 256) {
-    const Key x = lk[j];
-    if (x.id == 0x7fffffff || !kless(x, bound)) continue;   // invalid, or at/after the bound
-    const int g = j / KL;
-    int pos = j - g * KL;
-    for (int h = 0; h < S; h++)
-      if (h != g) pos += lower_bound_key(lk + h * KL, KL, x);
-    out[pos] = x;
-    c++;
+  Key* src = ka;
+  Key* dst = kb;
+  for (int len = KL; len < n; len <<= 1) {
+    for (int o = tid * 4; o < n; o += 1024) {
+      const int base = o & ~(2 * len - 1), i = o - base;
+      const Key* a = src + base;
+      const Key* b = a + len;
+      // co-rank: x outputs of the first i come from a (ties: a first; keys are distinct anyway
+      // except the invalid padding, which sorts last either way)
+      int lo = max(0, i - len), hi = min(i, len);
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (!kless(b[i - mid - 1], a[mid])) lo = mid + 1;
+        else hi = mid;
+      }
+      int x = lo, y = i - lo;
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const bool ta = x < len && (y >= len || !kless(b[y], a[x]));
+        dst[o + k] = ta ? a[x] : b[y];
+        x += ta ? 1 : 0;
+        y += ta ? 0 : 1;
+      }
+    }
+    __syncthreads();
+    Key* t = src; src = dst; dst = t;
   }
+  // kept entries: valid and below the bound, the first cnt of the merged list
+  int c = 0;
+  for (int j = tid; j < n; j += 256) c += (src[j].id != 0x7fffffff) && kless(src[j], bound);
   if (c) atomicAdd(&cnt_sh, c);
   __syncthreads();
   const int cnt = cnt_sh;
   const bool complete = (bound.id == 0x7fffffff) && tot <= LMAX;
   Key bnd = bound;
-  if (cnt == LMAX && kless(out[LMAX - 1], bnd)) bnd = out[LMAX - 1];
+  if (cnt == LMAX && kless(src[LMAX - 1], bnd)) bnd = src[LMAX - 1];
   const int nw = max(cnt, KL);
   for (int j = tid; j < nw; j += 256) {
     ListEntry e;
     const bool ok = j < cnt;
-    const Key k = ok ? out[j] : inv;
+    const Key k = ok ? src[j] : inv;
     const int h = ok ? k.id : 0;
     e.s = k.s; e.tb = k.tb; e.id = k.id; e.pad = 0; e.pad2 = 0.0;
     e.zone = ok ? A.zone[h] : 0;
@@ -679,14 +706,14 @@ static int merge_variant(const MergeArgs& a) {
 }
 const char* merge_kernel_name(const MergeArgs& a) {
   static const char* names[4] = {"merge_kernel", "merge_small_kernel", "merge_pkg_kernel",
-                                 "merge_mid_kernel"};
+                                 "merge_path_kernel"};
   return names[merge_variant(a)];
 }
 void launch_merge(const MergeArgs& a, hipStream_t st) {
   switch (merge_variant(a)) {
     case 1: hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a); break;
     case 2: hipLaunchKernelGGL(merge_pkg_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(merge_mid_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(merge_path_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
     default: hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
   }
 }

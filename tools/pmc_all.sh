@@ -11,7 +11,7 @@ shift
 sets=${*:-c5 c5l c3 c4}
 set -e
 WALKS=zwalk_kernel,commit_kernel,lwalk_kernel,opp_commit_kernel
-PARS=score_kernel,band_score_kernel,opp_count_kernel,perm_scan_kernel,ordered_kernel,merge_kernel,merge_small_kernel,merge_mid_kernel
+PARS=score_kernel,band_score_kernel,opp_count_kernel,perm_scan_kernel,ordered_kernel,merge_kernel,merge_small_kernel,merge_path_kernel
 idx=()
 prof() {   # prof NAME MODE HOSTS TASKS KEYSUFFIX KERNELS PROBE-ARGS...
   local name=$1 mode=$2 h=$3 t=$4 suf=$5 kern=$6

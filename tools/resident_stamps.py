@@ -33,9 +33,8 @@ assert f(eng.ctx, buf, 16) == 0
 names = ["anchor rows", "slot scan", "wave reduction", "exchange", "full path", "commit"]
 tot = sum(buf[k] for k in range(6))
 n = max(buf[6], 1)
-print("%s B=%d H=%d T=%d steps=%d full-path tasks=%d (PVT_RES_WAVES=%s)"
+print("%s B=%d H=%d T=%d tasks=%d full-path tasks=%d (PVT_RES_WAVES=%s)"
       % (mode, B, H, T, buf[6], buf[7], os.environ.get("PVT_RES_WAVES", "default")))
 for k, nm in enumerate(names):
-    print("  %-16s %6.1f%%  %8.0f cycles/step" % (nm, 100.0 * buf[k] / max(tot, 1), buf[k] / n))
-print("  %-16s %6.1f%%  %8.0f cycles/step" % ("total", 100.0, tot / n))
-print("  steps %d, of them pair steps %d (2 tasks each unless the second fell back)" % (buf[6], buf[8]))
+    print("  %-16s %6.1f%%  %8.0f cycles/task" % (nm, 100.0 * buf[k] / max(tot, 1), buf[k] / n))
+print("  %-16s %6.1f%%  %8.0f cycles/task" % ("total", 100.0, tot / n))
