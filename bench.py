@@ -193,14 +193,16 @@ def time_round(eng, r, steps, warmup, batch=None):
     a resident batch -- the placed result(s) and the kernel-class times of the timed steps."""
     import torch
     from pivot_place.engine import DeviceBatch, DeviceRound
-    dr = DeviceBatch(batch, eng.device) if batch else DeviceRound(r, eng.device)
+    # (a single round's input availability is double-buffered: each step's reset restores the
+    # buffer the previous step used on a side stream, beside the next step -- DeviceRound)
+    dr = DeviceBatch(batch, eng.device) if batch else DeviceRound(r, eng.device, overlap_reset=True)
     run = eng.run_batch if batch else eng.run
     for _ in range(warmup):
         dr.reset()
         run(dr)
     torch.cuda.synchronize()
     eng.reset_kstats()
-    eng.set_profiling(True)
+    eng.set_profiling(2)
     t0 = time.perf_counter()
     for _ in range(steps):
         dr.reset()
@@ -731,7 +733,7 @@ def main():
         run = eng.run_batch
     else:
         r = synthetic.make_round(mode, H, T, seed=args.seed + (0 if hosts_sharded else rank))
-        dr = DeviceRound(r, eng.device)
+        dr = DeviceRound(r, eng.device, overlap_reset=True)   # (reset beside the previous step)
         run = eng.run
     if hosts_sharded:
         from pivot_place.sharded import HostShardedPlacer, torch_exchange
@@ -750,7 +752,7 @@ def main():
         % (rank, placed, T, stats["windows"], stats["refills"]))
 
     eng.reset_kstats()
-    eng.set_profiling(True)
+    eng.set_profiling(2)     # (events around the named kernels only: every launch costs ~30 us/round)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

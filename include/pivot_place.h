@@ -130,7 +130,9 @@ int  pvt_ctx_destroy(pvt_ctx* ctx);
  * what torch's default stream is. Until the first call the context uses a stream of its own. */
 int  pvt_ctx_set_stream(pvt_ctx* ctx, void* stream);
 int  pvt_place(pvt_ctx* ctx, const pvt_round* r);
-/* Profiling: record HIP events around every kernel launch (adds a little host overhead). */
+/* Profiling: on = 1 records HIP events around every kernel launch (adds a little host overhead:
+ * ~30 us per config-5 round of ~15 launches); on = 2 only around the named kernels of
+ * pvt_get_kernel_kstats (the kernel-class times of the other launches stay zero). */
 int  pvt_set_profiling(pvt_ctx* ctx, int on);
 int  pvt_reset_kstats(pvt_ctx* ctx);
 int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);

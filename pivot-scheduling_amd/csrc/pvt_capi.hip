@@ -129,6 +129,7 @@ struct RoundState {
   int of_n = 0, of_hs = 0;        //   the scored attempt's tasks and host span
   bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
   bool ffe = false;               // keyed rounds: first-fit zero-key epochs (ff_epoch)
+  bool hmin_pre = false;          // the first epoch's host minima were queued by round_begin
   int ffe_skip = -1;              //   the group they could not start (the keyed path takes it)
   // vbp best-fit band lists (pvt_band.hip): the sorted snapshot of hosts [lo, hi) is built; a
   // walk whose committed hosts are not yet flagged as touched (its own-ids buffer)
@@ -151,7 +152,7 @@ struct pvt_ctx {
   std::string err;
   int window = 0;                 // 0: per-policy default
   int64_t windows = 0, refills = 0;
-  bool profiling = false;
+  int profiling = 0;               // 0 off, 1 every launch, 2 the named kernels only
   pvt_kstats ks[PVT_K_COUNT];
   std::vector<hipEvent_t> evpool;
   std::vector<TimedLaunch> pending;
@@ -260,10 +261,11 @@ struct Scope {
         const char* kname = nullptr)
       : ctx(c), st(s ? s : c->stream) {
     t.kclass = kclass; t.kname = kname; t.candidates = cand; t.bytes = bytes; t.a = t.b = nullptr;
-    if (ctx->profiling) { t.a = take_event(ctx); (void)hipEventRecord(t.a, st); }
+    if (on()) { t.a = take_event(ctx); (void)hipEventRecord(t.a, st); }
   }
+  bool on() const { return ctx->profiling == 1 || (ctx->profiling == 2 && t.kname); }
   ~Scope() {
-    if (ctx->profiling) {
+    if (on()) {
       t.b = take_event(ctx);
       (void)hipEventRecord(t.b, st);
       ctx->pending.push_back(t);
@@ -400,7 +402,7 @@ extern "C" int pvt_ctx_set_stream(pvt_ctx* ctx, void* stream) {
 
 extern "C" int pvt_set_profiling(pvt_ctx* ctx, int on) {
   if (!ctx) return PVT_EINVAL;
-  ctx->profiling = on != 0;
+  ctx->profiling = on == 2 ? 2 : (on != 0 ? 1 : 0);
   return PVT_OK;
 }
 extern "C" int pvt_reset_kstats(pvt_ctx* ctx) {
@@ -855,6 +857,16 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
     ENSURE(ctx->csum, sizeof(double) * Z * Z);
     ENSURE(ctx->bsum, sizeof(double) * Z * Z);
     launch_zone_tables(r->cost, r->bw, Z, P<double>(ctx->csum), P<double>(ctx->bsum), st);
+  }
+  // a cost_aware best-fit round of epochs (epoch_groups) starts with the frontier walk's host
+  // minima: queued now, they run while the host waits for the grouped order's counts
+  R.hmin_pre = false;
+  if (ctx->epochs && ctx->zwalk && r->mode == PVT_CA_BF && r->task_group && r->n_groups >= 2 &&
+      T >= 2 && !r->rt_bw && Z <= ZMAX && world == 1) {
+    ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+    Scope sc(ctx, PVT_K_OTHER, 0, 0);
+    launch_host_min(r->avail, H, 0, H, P<double>(ctx->hmin), st);
+    R.hmin_pre = true;
   }
   if (pending) {   // the one synchronisation of the grouped order: counts, anchors, cost table
     HIPCHK(hipStreamSynchronize(st));
@@ -1629,11 +1641,12 @@ static int place_epochs(pvt_ctx* ctx) {
   while (t0 < R.T) {
     // the frontier walk's host minima (certificate 2) depend only on the epoch's start state:
     // reduced while the host plans the epoch
-    if (zw_possible && !force_lists) {
+    if (zw_possible && !force_lists && !(R.hmin_pre && t0 == 0)) {
       ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
       Scope sc(ctx, PVT_K_OTHER, 0, 0);
       launch_host_min(r->avail, R.H, 0, R.H, P<double>(ctx->hmin), st);
     }
+    R.hmin_pre = false;
     epoch_plan(R, t0, E);
     const int nseg = (int)E.chain.size(), nch = (int)E.segs.size(), nt = E.off.back();
     ctx->n_epochs++;

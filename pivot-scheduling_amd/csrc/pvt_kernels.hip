@@ -1046,10 +1046,11 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
   __shared__ int32_t v[GSORT_MAX];
   const int a = off[blockIdx.x], n = off[blockIdx.x + 1] - a, tid = threadIdx.x;
   if (n <= 0 || n > GSORT_MAX) return;   // (larger groups: the host sorts with radix passes)
-  if (n <= 1024) {
+  if (n <= 128) {
     // rank by counting: the keys (sort key, task index) are distinct, so an element's place is
     // the number of elements below it -- every thread scans the group's keys in LDS (broadcast
-    // reads), one barrier in all (the bitonic network below needs 55 for 1024 keys)
+    // reads), one barrier in all. (Quadratic: measured 57 us for a group of ~1000 at config 5,
+    // where the bitonic network below, 55 barrier stages, takes a few microseconds.)
     for (int i = tid; i < n; i += blockDim.x) { k[i] = skey[a + i]; v[i] = sidx[a + i]; }
     __syncthreads();
     if (tid < n) {
