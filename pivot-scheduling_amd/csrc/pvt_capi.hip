@@ -130,6 +130,7 @@ struct RoundState {
   bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
   bool ffe = false;               // keyed rounds: first-fit zero-key epochs (ff_epoch)
   bool hmin_pre = false;          // the first epoch's host minima were queued by round_begin
+  bool prep_fused = false;        // build_order's order_prep_kernel filled placement / zone tables
   int ffe_skip = -1;              //   the group they could not start (the keyed path takes it)
   // vbp best-fit band lists (pvt_band.hip): the sorted snapshot of hosts [lo, hi) is built; a
   // walk whose committed hosts are not yet flagged as touched (its own-ids buffer)
@@ -563,9 +564,12 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
   if (grouped && r->n_groups <= (1 << 20)) {
     // one synchronisation: group counts, group anchors and the cost table to the host
     const int G = r->n_groups;
-    ENSURE(ctx->gcnt, sizeof(int32_t) * (G + 1));
-    HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, sizeof(int32_t) * (G + 1), st));
-    launch_group_hist(r->task_group, T, G, P<int32_t>(ctx->gcnt), st);
+    const bool fused = T <= PREP_T_MAX && G <= GAGG_MAX;   // (order_prep_kernel: one launch)
+    if (!fused) {
+      ENSURE(ctx->gcnt, sizeof(int32_t) * (G + 1));
+      HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, sizeof(int32_t) * (G + 1), st));
+      launch_group_hist(r->task_group, T, G, P<int32_t>(ctx->gcnt), st);
+    }
     // staged in pinned memory: pageable destinations made each copy a ~20 us synchronous
     // staging step (profiles/r02q kernel trace)
     const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
@@ -585,21 +589,35 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
     HIPCHK(hipHostGetDevicePointer(&dstage, ctx->gstage, 0));
     double* dcst = reinterpret_cast<double*>(dstage);
     int32_t* dcnt = reinterpret_cast<int32_t*>(dcst + nz2);
-    launch_group_stage(P<int32_t>(ctx->gcnt), G, r->group_anchor, r->cost, (int)nz2,
-                       P<int32_t>(ctx->goff), dcnt, dcnt + G + 1, dcst, st);
-    HIPCHK(hipGetLastError());
     // the per-group sorts, optimistically (a group over GSORT_MAX tasks is left unsorted by the
     // kernel; build_order_check then redoes the order with radix passes)
     ENSURE(ctx->gskey, sizeof(uint64_t) * T);
     ENSURE(ctx->gsidx, sizeof(int32_t) * T);
-    const uint64_t* keys = nullptr;
-    if (r->sort_tasks) {
-      ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
-      launch_norm_keys(r->dem, T, nullptr, P<uint64_t>(ctx->keys64a), st);
-      keys = P<uint64_t>(ctx->keys64a);
+    if (fused) {
+      // placement fill and (cost_aware) zone tables too: round_begin skips its own
+      if (ca) {
+        ENSURE(ctx->csum, sizeof(double) * r->n_zones * r->n_zones);
+        ENSURE(ctx->bsum, sizeof(double) * r->n_zones * r->n_zones);
+      }
+      PrepArgs pa{r->task_group, T, G, r->group_anchor, r->cost, r->bw, r->n_zones, (int)nz2,
+                  r->dem, r->sort_tasks ? 1 : 0, r->placement, P<int32_t>(ctx->goff), dcnt,
+                  dcnt + G + 1, dcst, ca ? P<double>(ctx->csum) : nullptr,
+                  ca ? P<double>(ctx->bsum) : nullptr, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx)};
+      launch_order_prep(pa, st);
+      R.prep_fused = true;
+    } else {
+      launch_group_stage(P<int32_t>(ctx->gcnt), G, r->group_anchor, r->cost, (int)nz2,
+                         P<int32_t>(ctx->goff), dcnt, dcnt + G + 1, dcst, st);
+      HIPCHK(hipGetLastError());
+      const uint64_t* keys = nullptr;
+      if (r->sort_tasks) {
+        ENSURE(ctx->keys64a, sizeof(uint64_t) * T);
+        launch_norm_keys(r->dem, T, nullptr, P<uint64_t>(ctx->keys64a), st);
+        keys = P<uint64_t>(ctx->keys64a);
+      }
+      launch_group_scatter(r->task_group, keys, T, G, P<int32_t>(ctx->goff) + G + 1,
+                           P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx), st);
     }
-    launch_group_scatter(r->task_group, keys, T, G, P<int32_t>(ctx->goff) + G + 1,
-                         P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx), st);
     launch_group_sort(P<int32_t>(ctx->goff), G, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx),
                       cur, st);
     R.ginfo = ca;
@@ -838,17 +856,17 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   R.gid.clear();
   if (T == 0) { R.ngroups = 0; R.active = true; return PVT_OK; }
   hipStream_t st = ctx->stream;
-  HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
 
   bool pending = false;
+  R.prep_fused = false;
   if ((rc = build_order(ctx, r, &R.ord, &pending))) return rc;
+  if (!R.prep_fused) HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   ENSURE(ctx->grp_ord, sizeof(int32_t) * T);
-  auto order_out = [&]() -> int {
-    HIPCHK(hipMemcpyAsync(r->order, R.ord, sizeof(int32_t) * T, hipMemcpyDeviceToDevice, st));
+  auto order_out = [&]() -> int {   // (the gather also writes the caller's order)
     launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
-                        P<int32_t>(ctx->anc_ord), P<int32_t>(ctx->grp_ord), st, r->n_groups);
+                        P<int32_t>(ctx->anc_ord), P<int32_t>(ctx->grp_ord), st, r->n_groups, r->order);
     return PVT_OK;
   };
   if ((rc = order_out())) return rc;
@@ -856,7 +874,8 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   if (ca) {
     ENSURE(ctx->csum, sizeof(double) * Z * Z);
     ENSURE(ctx->bsum, sizeof(double) * Z * Z);
-    launch_zone_tables(r->cost, r->bw, Z, P<double>(ctx->csum), P<double>(ctx->bsum), st);
+    if (!R.prep_fused)
+      launch_zone_tables(r->cost, r->bw, Z, P<double>(ctx->csum), P<double>(ctx->bsum), st);
   }
   // a cost_aware best-fit round of epochs (epoch_groups) starts with the frontier walk's host
   // minima: queued now, they run while the host waits for the grouped order's counts
@@ -979,9 +998,11 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   // Windows adapt to how far commit walks get before a list is exhausted: a walk that stops
   // early means the next window only needs about that many tasks (the score pass costs the
   // same per task either way, so short windows waste less on tasks that get re-scored).
-  // default window: vbp best-fit walks search deeper lists as a window's touched hosts pile up
-  // at the top of every task's ranking, so its windows are shorter (bench sweep)
-  const int wdef = (r->mode == PVT_VBP_BF) ? 512 : MAX_WINDOW;
+  // default window: MAX_WINDOW for every policy. (vbp best-fit had 512: its walks search deeper
+  // lists as a window's touched hosts pile up at the top of every task's ranking; with the
+  // merge-path merge the longer windows win -- config 5: 3.33 ms at 512, 3.26 at 768, 3.07 at
+  // 1024, round 4 sweep.)
+  const int wdef = MAX_WINDOW;
   R.Wmax = std::max(1, std::min(ctx->window > 0 ? ctx->window : wdef, MAX_WINDOW));
   R.W = R.Wmax;
   ENSURE(ctx->seg, sizeof(SegEntry) * (size_t)SEG_ENTRIES_MAX);

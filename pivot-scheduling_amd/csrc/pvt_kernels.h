@@ -408,6 +408,30 @@ hipError_t init_kernel_attrs();
 // LDS bitonic sort of (key, task index) per group of at most GSORT_MAX tasks
 constexpr int GSORT_MAX = 4096;
 void launch_group_hist(const int32_t* tg, int T, int G, int32_t* cnt, hipStream_t st);
+// the grouped order's preparation in one block (T <= PREP_T_MAX, G <= GAGG_MAX): placement fill,
+// group counts, pinned staging, offsets, zone tables, sort keys and the (key, task) scatter
+constexpr int PREP_T_MAX = 65536;
+constexpr int GAGG_MAX = 4096;
+struct PrepArgs {
+  const int32_t* tg;
+  int T, G;
+  const int32_t* ganc;
+  const double* cost;
+  const double* bw;
+  int Z, nz2;                 // nz2: entries of the cost table staged (0: none)
+  const double* dem;
+  int sort_tasks;
+  int32_t* placement;         // filled with -1, or NULL
+  int32_t* off;               // [G + 1] group offsets in processing order
+  int32_t* hcnt;              // pinned (device-mapped): counts [G + 1], anchors [G], cost [nz2]
+  int32_t* hgan;
+  double* hcst;
+  double* csum;               // zone tables [Z * Z], or NULL
+  double* bsum;
+  uint64_t* skey;
+  int32_t* sidx;
+};
+void launch_order_prep(const PrepArgs& a, hipStream_t st);
 void launch_group_stage(const int32_t* cnt, int G, const int32_t* ganc, const double* cost, int nz2,
                         int32_t* off, int32_t* hcnt, int32_t* hgan, double* hcst, hipStream_t st);
 void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,
@@ -418,6 +442,7 @@ void launch_iota(int32_t* out, int n, hipStream_t st);
 // gather tasks into processing order: dem_ord[p][r] = dem[r*T + ord[p]], anc_ord[p]
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
                          const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
-                         int32_t* grp_ord, hipStream_t st, int G = 0x7fffffff);
+                         int32_t* grp_ord, hipStream_t st, int G = 0x7fffffff,
+                         int32_t* order_out = nullptr);
 
 }  // namespace pvt

@@ -939,7 +939,6 @@ void launch_group_keys(const int32_t* task_group, const int32_t* idx, int T, uin
 // Blocks of 1024 tasks count (and place) in LDS first when G <= GAGG_MAX groups, so a
 // group's global counter sees one atomic per block, not one per task (20 groups of 500 tasks
 // serialised 26 us of same-address atomics).
-constexpr int GAGG_MAX = 4096;
 __global__ __launch_bounds__(1024) void group_hist_kernel(const int32_t* tg, int T, int G, int32_t* cnt) {
   __shared__ int32_t loc[GAGG_MAX + 1];
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1040,6 +1039,76 @@ void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G,
   hipLaunchKernelGGL(group_scatter_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, keys, T,
                      G, cursor, skey, sidx);
 }
+// The grouped order's preparation in ONE block (rounds of at most PREP_T_MAX tasks and
+// GAGG_MAX groups; the config-5 round's seven launches -- placement fill, counter clear, group
+// histogram, stage, sort keys, scatter, zone tables -- were each a few microseconds of launch
+// latency on the host's critical path): counts in LDS, the pinned staging of counts / anchors /
+// cost table, the groups' offsets, then the (key, task) pairs scattered by LDS cursors (their
+// order inside a group is irrelevant: group_sort orders by (key, index)).
+__global__ __launch_bounds__(1024) void order_prep_kernel(PrepArgs A) {
+  __shared__ int32_t cnt[GAGG_MAX + 1];
+  __shared__ int32_t cur[GAGG_MAX];
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int T = A.T, G = A.G;
+  for (int q = t; q <= G; q += 1024) cnt[q] = 0;
+  if (t == 0) carry = 0;
+  if (A.placement)
+    for (int i = t; i < T; i += 1024) A.placement[i] = -1;
+  if (A.csum)
+    for (int i = t; i < A.Z * A.Z; i += 1024) {
+      const int a = i / A.Z, z = i - a * A.Z;
+      A.csum[i] = A.cost[a * A.Z + z] + A.cost[z * A.Z + a];   // cost_aware.py:82,113
+      A.bsum[i] = A.bw[a * A.Z + z] + A.bw[z * A.Z + a];       // (:79,111)
+    }
+  __syncthreads();
+  for (int i = t; i < T; i += 1024) {
+    const int g = A.tg[i];
+    atomicAdd(&cnt[(g >= 0 && g < G) ? g : G], 1);   // G: out of range
+  }
+  __syncthreads();
+  for (int i = t; i <= G; i += 1024) A.hcnt[i] = cnt[i];
+  for (int i = t; i < G; i += 1024) A.hgan[i] = A.ganc[i];
+  for (int i = t; i < A.nz2; i += 1024) A.hcst[i] = A.cost[i];
+  for (int g0 = 0; g0 < G; g0 += 1024) {            // exclusive scan -> offsets and cursors
+    const int g = g0 + t;
+    const int v = g < G ? cnt[g] : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int pre = carry;
+    for (int w = 0; w < wave; w++) pre += wsum[w];
+    if (g < G) { A.off[g] = pre + x - v; cur[g] = pre + x - v; }
+    __syncthreads();
+    if (t == 1023) carry = pre + x;
+    __syncthreads();
+  }
+  if (t == 0) A.off[G] = carry;
+  for (int i = t; i < T; i += 1024) {
+    const int g = A.tg[i];
+    if (g < 0 || g >= G) continue;        // (the host rejects the round after its sync)
+    uint64_t key = 0;
+    if (A.sort_tasks) {
+      const double n = __builtin_sqrt(norm2_seq(A.dem[i], A.dem[(size_t)T + i],
+                                                A.dem[2 * (size_t)T + i], A.dem[3 * (size_t)T + i]));
+      key = ~(uint64_t)__double_as_longlong(n);         // descending norm (as norm_keys_kernel)
+    }
+    const int pos = atomicAdd(&cur[g], 1);
+    A.skey[pos] = key;
+    A.sidx[pos] = i;
+  }
+  __threadfence_system();
+}
+void launch_order_prep(const PrepArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(order_prep_kernel, dim3(1), dim3(1024), 0, st, a);
+}
+
 __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, const uint64_t* skey,
                                                           const int32_t* sidx, int32_t* ord) {
   __shared__ uint64_t k[GSORT_MAX];
@@ -1102,10 +1171,11 @@ void launch_iota(int32_t* out, int n, hipStream_t st) {
 
 __global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const int32_t* tg,
                                     const int32_t* ga, int T, double* dem_ord, int32_t* anc_ord,
-                                    int32_t* grp_ord, int G) {
+                                    int32_t* grp_ord, int G, int32_t* order_out) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= T) return;
   const int t = ord[p];
+  if (order_out) order_out[p] = t;        // (the caller's order: no separate D2D copy)
   double* o = dem_ord + (size_t)p * 4;
   o[0] = dem[t]; o[1] = dem[(size_t)T + t]; o[2] = dem[2 * (size_t)T + t]; o[3] = dem[3 * (size_t)T + t];
   // (a group id out of range reads no anchor: the host rejects such a round after its sync)
@@ -1114,9 +1184,9 @@ __global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const
 }
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
                          const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
-                         int32_t* grp_ord, hipStream_t st, int G) {
+                         int32_t* grp_ord, hipStream_t st, int G, int32_t* order_out) {
   hipLaunchKernelGGL(gather_tasks_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, ord,
-                     task_group, group_anchor, T, dem_ord, anc_ord, grp_ord, G);
+                     task_group, group_anchor, T, dem_ord, anc_ord, grp_ord, G, order_out);
 }
 
 }  // namespace pvt
