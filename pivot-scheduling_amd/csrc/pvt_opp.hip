@@ -162,8 +162,6 @@ struct OppLDS {
   uint32_t kdraw[OPP_R];
   int32_t cnt[OPP_R];           // MT19937 outputs the draw consumed
   int32_t ccount[OPP_R];
-  double pz[OPP_R][8];          // pass 4: each task's chosen host's capacity now / after it
-  int32_t pw[OPP_R];            // pass 4: each task's chosen host
   int32_t dl[OPP_R];            // pass 2: the range's draw tasks (n >= 2), in order
   uint32_t mt[625];
   uint32_t mtb[625];            // state at the range start
@@ -649,10 +647,12 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
     // (nnew). Task i's draw holds while dok (same mask, k <= n - 1 for n - nnew), and its host is
     // then the mm-th candidate that still fits (the k-th feasible host, shifted by the lost hosts
     // below c_0) -- unless fewer candidates fit, when the range stops there. Every lane keeps that
-    // choice (host, capacity now, capacity after) in an LDS row, recomputed in parallel when a
-    // commit takes a host from it or changes a candidate's capacity, so the walk itself is one
-    // LDS broadcast, the fit tests of the later tasks and two ballots per task. Nothing is
-    // written to the touched table until the range ends.
+    // choice (host, capacity now, capacity after) in registers, recomputed in parallel when a
+    // commit takes a host from it (below its candidates) or changes a candidate's capacity, so
+    // the walk itself is nine v_readlane of the committing lane's row, the fit tests of the
+    // later tasks and two ballots per task (the LDS row it replaced cost ~740 cycles a commit:
+    // its load latency sat on the chain). Nothing is written to the touched table until the
+    // range ends.
     if (wave == 0) {
       const int R = e - s;
       const bool mine = lane < R;
@@ -672,16 +672,20 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       int nnew = 0, mm = 0;
       bool dok = true;
       uint32_t lm = 0;
-      // the lane's choice: the mm-th candidate still fitting, into its LDS row; false if none
+      // the lane's choice: the mm-th candidate still fitting, into its registers; false if none
+      // the lane's choice (host, capacity now, capacity after it) in registers: the walk reads a
+      // task's row by v_readlane (no LDS round trip, no fence after a re-choice)
+      int qw = 0;
+      double q0 = 0.0, q1 = 0.0, q2 = 0.0, q3 = 0.0, r0 = 0.0, r1 = 0.0, r2 = 0.0, r3 = 0.0;
       auto choose = [&]() -> bool {
         const uint32_t valid = ((1u << ccv) - 1u) & ~lm;
         if (!mine || !dok || __popc(valid) <= mm) return false;
         const int xs = select_bit(valid, mm);
         const double z0 = S.cav[lane][0][xs], z1 = S.cav[lane][1][xs];
         const double z2 = S.cav[lane][2][xs], z3 = S.cav[lane][3][xs];
-        S.pw[lane] = S.cand[lane][xs];
-        S.pz[lane][0] = z0; S.pz[lane][1] = z1; S.pz[lane][2] = z2; S.pz[lane][3] = z3;
-        S.pz[lane][4] = z0 - e0; S.pz[lane][5] = z1 - e1; S.pz[lane][6] = z2 - e2; S.pz[lane][7] = z3 - e3;
+        qw = S.cand[lane][xs];
+        q0 = z0; q1 = z1; q2 = z2; q3 = z3;
+        r0 = z0 - e0; r1 = z1 - e1; r2 = z2 - e2; r3 = z3 - e3;
         return true;
       };
       // Uniform masks over the range's lanes:
@@ -690,36 +694,29 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       const uint64_t minem = __ballot(mine);
       const uint64_t posm = __ballot(mine && nsv > 0);
       uint64_t okm = __ballot(choose());
-      wave_lds_fence();
       uint64_t cmt = 0;
       int stop = e;
       OSTAMP(9);
-      // Software-pipelined: the row of the next task with a feasible host is read while this
-      // task's commit is tested (and read again if that commit rewrote it).
       int L = posm ? __builtin_ctzll(posm) : R;
-      int w = 0;
-      double w0 = 0.0, w1 = 0.0, w2 = 0.0, w3 = 0.0, n0 = 0.0, n1 = 0.0, n2 = 0.0, n3 = 0.0;
-      auto row = [&](int l) {
-        w = S.pw[l];
-        w0 = S.pz[l][0]; w1 = S.pz[l][1]; w2 = S.pz[l][2]; w3 = S.pz[l][3];
-        n0 = S.pz[l][4]; n1 = S.pz[l][5]; n2 = S.pz[l][6]; n3 = S.pz[l][7];
-      };
-      if (L < R) row(L);
       while (L < R) {   // (tasks without a feasible host at s place nothing and change nothing)
         if (!((okm >> L) & 1ull)) {   // the draw changed, or the answer lies beyond the
           stop = s + L;               // candidates: the range stops here
           break;
         }
-        const int cw = w;
-        const double c0 = w0, c1 = w1, c2 = w2, c3 = w3, m0 = n0, m1 = n1, m2 = n2, m3 = n3;
+        // task L's row from lane L's registers (uniform values in SGPRs)
+        const int cw = __builtin_amdgcn_readlane(qw, L);
+        const double c0 = readlane_d(q0, L), c1 = readlane_d(q1, L), c2 = readlane_d(q2, L),
+                     c3 = readlane_d(q3, L);
+        const double m0 = readlane_d(r0, L), m1 = readlane_d(r1, L), m2 = readlane_d(r2, L),
+                     m3 = readlane_d(r3, L);
         const uint64_t nx = posm & ~((2ull << L) - 1ull);
         const int Ln = nx ? __builtin_ctzll(nx) : R;
-        if (Ln < R) row(Ln);
         cmt |= 1ull << L;
         // the later tasks of the range: does this commit take cw away from them (lostm: fitted
         // before, not after -- fits<false> per lane is the AND of the per-dimension ballots),
         // or is cw inside their candidates' id range (rngm; rare: a commit's host is random
-        // among ~1M)?
+        // among ~1M)? (Two commits per iteration, the second's effect computed beside the
+        // first's, measured slower: 817 against 692 cycles per commit.)
         const uint64_t am = minem & ~((2ull << L) - 1ull);
         const uint64_t fw = __ballot(c0 >= e0) & __ballot(c1 >= e1) & __ballot(c2 >= e2) & __ballot(c3 >= e3);
         const uint64_t fn = __ballot(m0 >= e0) & __ballot(m1 >= e1) & __ballot(m2 >= e2) & __ballot(m3 >= e3);
@@ -750,19 +747,11 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
           }
           // The choice moves only for a lane whose candidates changed (rngm) or whose lost host
           // lay below its candidates (mm grew); a lost host above them leaves it in place, and a
-          // draw that no longer holds only clears the lane's ok bit. Rows are rewritten (and the
-          // next row read again) only when some lane's choice moved.
+          // draw that no longer holds only clears the lane's ok bit.
           const bool redo = (((rngm >> lane) & 1ull) != 0) | (lost & (cw < c0l));
           bool ok = ((okm >> lane) & 1ull) & dok;
-          if (__ballot(redo)) {
-            wave_lds_fence();
-            if (redo) ok = choose();
-            okm = __ballot(ok);
-            wave_lds_fence();
-            if (Ln < R) row(Ln);
-          } else {
-            okm = __ballot(ok);
-          }
+          if (redo) ok = choose();
+          okm = __ballot(ok);
         }
         L = Ln;
       }
@@ -772,9 +761,9 @@ __global__ __launch_bounds__(OPP_NW * WAVE) void opp_commit_kernel(OppCommitArgs
       int rch = -1;
       double ra0 = 0.0, ra1 = 0.0, ra2 = 0.0, ra3 = 0.0, rb0 = 0.0, rb1 = 0.0, rb2 = 0.0, rb3 = 0.0;
       if ((cmt >> lane) & 1ull) {
-        rch = S.pw[lane];
-        rb0 = S.pz[lane][0]; rb1 = S.pz[lane][1]; rb2 = S.pz[lane][2]; rb3 = S.pz[lane][3];
-        ra0 = S.pz[lane][4]; ra1 = S.pz[lane][5]; ra2 = S.pz[lane][6]; ra3 = S.pz[lane][7];
+        rch = qw;
+        rb0 = q0; rb1 = q1; rb2 = q2; rb3 = q3;
+        ra0 = r0; ra1 = r1; ra2 = r2; ra3 = r3;
       }
       // A range whose first task fails cannot happen when the counts are consistent (its state
       // is exact). If it does (inconsistent counts or bitmaps), report it -- the host returns
