@@ -39,8 +39,6 @@ if mode == 2:
                                                       buf[k] / max(buf[7], 1)))
     print("  pass-4 commits %d: lost to a later task %d, among a later task's candidates' id "
           "range %d" % (buf[13], buf[11], buf[12]))
-    print("  pass-4 rare branch (a commit that takes a host from later tasks): %.0f cycles per "
-          "occurrence, %.0f per task" % (buf[10] / max(buf[11] + buf[12], 1), buf[10] / max(buf[7], 1)))
     sys.exit(0)
 if mode == 3 or os.environ.get("ZWALK"):
     # frontier walk (pvt_zwalk.hip; vbp first-fit: ordered frontier attempts): prologue
