@@ -51,8 +51,8 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=5)
-    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--mode", default="ca_bf", choices=sorted(MODES))
     p.add_argument("--hosts", type=int, default=DEFAULT_H)
     p.add_argument("--tasks", type=int, default=DEFAULT_T)
