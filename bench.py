@@ -193,9 +193,7 @@ def time_round(eng, r, steps, warmup, batch=None):
     a resident batch -- the placed result(s) and the kernel-class times of the timed steps."""
     import torch
     from pivot_place.engine import DeviceBatch, DeviceRound
-    # (a single round's input availability is double-buffered: each step's reset restores the
-    # buffer the previous step used on a side stream, beside the next step -- DeviceRound)
-    dr = DeviceBatch(batch, eng.device) if batch else DeviceRound(r, eng.device, overlap_reset=True)
+    dr = DeviceBatch(batch, eng.device) if batch else DeviceRound(r, eng.device)
     run = eng.run_batch if batch else eng.run
     for _ in range(warmup):
         dr.reset()
@@ -733,7 +731,7 @@ def main():
         run = eng.run_batch
     else:
         r = synthetic.make_round(mode, H, T, seed=args.seed + (0 if hosts_sharded else rank))
-        dr = DeviceRound(r, eng.device, overlap_reset=True)   # (reset beside the previous step)
+        dr = DeviceRound(r, eng.device)
         run = eng.run
     if hosts_sharded:
         from pivot_place.sharded import HostShardedPlacer, torch_exchange

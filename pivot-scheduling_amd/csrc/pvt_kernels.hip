@@ -1063,9 +1063,18 @@ __global__ __launch_bounds__(1024) void order_prep_kernel(PrepArgs A) {
       A.bsum[i] = A.bw[a * A.Z + z] + A.bw[z * A.Z + a];       // (:79,111)
     }
   __syncthreads();
-  for (int i = t; i < T; i += 1024) {
-    const int g = A.tg[i];
-    atomicAdd(&cnt[(g >= 0 && g < G) ? g : G], 1);   // G: out of range
+  // (loads batched PB per thread so their latencies overlap: the block is alone on its CU)
+  constexpr int PB = 16;
+  for (int i0 = 0; i0 < T; i0 += 1024 * PB) {
+    int gv[PB];
+#pragma unroll
+    for (int u = 0; u < PB; u++) {
+      const int i = i0 + u * 1024 + t;
+      gv[u] = i < T ? A.tg[i] : -2;
+    }
+#pragma unroll
+    for (int u = 0; u < PB; u++)
+      if (gv[u] != -2) atomicAdd(&cnt[(gv[u] >= 0 && gv[u] < G) ? gv[u] : G], 1);   // G: out of range
   }
   __syncthreads();
   for (int i = t; i <= G; i += 1024) A.hcnt[i] = cnt[i];
@@ -1090,18 +1099,33 @@ __global__ __launch_bounds__(1024) void order_prep_kernel(PrepArgs A) {
     __syncthreads();
   }
   if (t == 0) A.off[G] = carry;
-  for (int i = t; i < T; i += 1024) {
-    const int g = A.tg[i];
-    if (g < 0 || g >= G) continue;        // (the host rejects the round after its sync)
-    uint64_t key = 0;
-    if (A.sort_tasks) {
-      const double n = __builtin_sqrt(norm2_seq(A.dem[i], A.dem[(size_t)T + i],
-                                                A.dem[2 * (size_t)T + i], A.dem[3 * (size_t)T + i]));
-      key = ~(uint64_t)__double_as_longlong(n);         // descending norm (as norm_keys_kernel)
+  constexpr int PS = 8;
+  for (int i0 = 0; i0 < T; i0 += 1024 * PS) {
+    int gv[PS];
+    double dv[PS][4];
+#pragma unroll
+    for (int u = 0; u < PS; u++) {
+      const int i = i0 + u * 1024 + t;
+      gv[u] = i < T ? A.tg[i] : -1;
+      if (A.sort_tasks && i < T) {
+        dv[u][0] = A.dem[i]; dv[u][1] = A.dem[(size_t)T + i];
+        dv[u][2] = A.dem[2 * (size_t)T + i]; dv[u][3] = A.dem[3 * (size_t)T + i];
+      }
     }
-    const int pos = atomicAdd(&cur[g], 1);
-    A.skey[pos] = key;
-    A.sidx[pos] = i;
+#pragma unroll
+    for (int u = 0; u < PS; u++) {
+      const int i = i0 + u * 1024 + t;
+      const int g = gv[u];
+      if (i >= T || g < 0 || g >= G) continue;   // (the host rejects the round after its sync)
+      uint64_t key = 0;
+      if (A.sort_tasks) {
+        const double n = __builtin_sqrt(norm2_seq(dv[u][0], dv[u][1], dv[u][2], dv[u][3]));
+        key = ~(uint64_t)__double_as_longlong(n);       // descending norm (as norm_keys_kernel)
+      }
+      const int pos = atomicAdd(&cur[g], 1);
+      A.skey[pos] = key;
+      A.sidx[pos] = i;
+    }
   }
   __threadfence_system();
 }
@@ -1158,7 +1182,9 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
 }
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
                        int32_t* ord, hipStream_t st) {
-  hipLaunchKernelGGL(group_sort_kernel, dim3(G), dim3(1024), 0, st, off, skey, sidx, ord);
+  // (256 threads: a group of ~500 tasks keeps 256 compare-exchanges per stage busy, and each of
+  // the network's barriers waits for 4 waves instead of 16)
+  hipLaunchKernelGGL(group_sort_kernel, dim3(G), dim3(256), 0, st, off, skey, sidx, ord);
 }
 
 __global__ void iota_kernel(int32_t* out, int n) {

@@ -87,12 +87,9 @@ class DeviceRound:
     """A round resident in HBM: torch tensors plus the pvt_round struct that points at them.
 
     ``reset()`` restores the pristine availability (one D2D copy), so the same round can be
-    placed repeatedly (one bench step = reset + place). With ``overlap_reset`` the availability is
-    double-buffered: reset() switches to the other buffer (restored beside the previous place,
-    on a side stream ordered by events) and queues the restore of the one just used, so repeated
-    places do not wait for the copy (bench.py's timed steps)."""
+    placed repeatedly (one bench step = reset + place)."""
 
-    def __init__(self, r: RoundArrays, device, overlap_reset=False):
+    def __init__(self, r: RoundArrays, device):
         torch = _torch()
         self.arrays = r
         dev = torch.device(device)
@@ -123,37 +120,11 @@ class DeviceRound:
         s.rt_bw = dp(self.rt_bw)
         s.mt_state = None if self.mt is None else self.mt.ctypes.data
         self.struct = s
-        self._bufs = None
-        if overlap_reset:
-            self._bufs = [self.avail, self.avail0.clone()]
-            self._cur = 0
-            self._ready = [None, None]           # side-stream events: buffer restored
-            self._side = torch.cuda.Stream(device=dev)
 
     def reset(self):
+        self.avail.copy_(self.avail0)
         if self.mt is not None:
             self.mt[:] = self.mt0
-        if self._bufs is None:
-            self.avail.copy_(self.avail0)
-            return
-        torch = _torch()
-        main = torch.cuda.current_stream(self.avail.device)
-        used, nxt = self._cur, 1 - self._cur
-        ev_used = torch.cuda.Event()
-        ev_used.record(main)                     # (the work queued so far used bufs[used])
-        if self._ready[nxt] is None:
-            self._bufs[nxt].copy_(self.avail0)
-        else:
-            main.wait_event(self._ready[nxt])
-        self._side.wait_event(ev_used)
-        with torch.cuda.stream(self._side):
-            self._bufs[used].copy_(self.avail0)
-            ev = torch.cuda.Event()
-            ev.record(self._side)
-        self._ready[used] = ev
-        self._cur = nxt
-        self.avail = self._bufs[nxt]
-        self.struct.avail = self.avail.data_ptr()
 
     def result(self) -> RoundResult:
         T = self.arrays.n_tasks
