@@ -42,10 +42,11 @@ __global__ void band_keys_kernel(const double* avail, int H, int lo, int n, uint
 }
 
 __global__ void band_gather_kernel(const double* avail, const uint32_t* tb, int H, int n,
-                                   const int32_t* sid, double* sa, uint32_t* stb) {
+                                   const int32_t* sid, double* sa, uint32_t* stb, int32_t* pos) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const int h = sid[p];
+  pos[h] = p;                              // (host -> sorted position, for the touched flags)
 #pragma unroll
   for (int r = 0; r < 4; r++) sa[(size_t)r * n + p] = avail[(size_t)r * H + h];
   stb[p] = tb[h];
@@ -55,7 +56,8 @@ __global__ void band_gather_kernel(const double* avail, const uint32_t* tb, int 
 // are flagged and appended to the touched list, in own_ids order (one block, ballot compaction).
 __global__ __launch_bounds__(1024) void touch_update_kernel(const int32_t* own, const int32_t* status,
                                                             uint8_t* flags, int32_t* tlist,
-                                                            int32_t* tcount) {
+                                                            int32_t* tcount, const int32_t* hpos,
+                                                            int lo, int hi, uint8_t* ptouch) {
   __shared__ int32_t wcnt[16];
   __shared__ int32_t base;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -74,6 +76,7 @@ __global__ __launch_bounds__(1024) void touch_update_kernel(const int32_t* own, 
     for (int w = 0; w < wave; w++) pos += wcnt[w];
     if (add) {
       flags[h] = 1;
+      if (h >= lo && h < hi) ptouch[hpos[h]] = 1;   // (the sorted copy covers [lo, hi))
       tlist[pos] = h;
     }
     __syncthreads();
@@ -159,23 +162,26 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
   double n0 = 0, n1 = 0, n2 = 0, n3 = 0;
   uint32_t ntb = 0;
   int32_t nid = 0;
+  uint8_t npt = 0;
   auto fetch = [&](int cc) {
     const int p = min(cc * WAVE + lane, n - 1);
     n0 = A.sa[p]; n1 = A.sa[(size_t)n + p]; n2 = A.sa[2 * (size_t)n + p]; n3 = A.sa[3 * (size_t)n + p];
     ntb = A.stb[p];
     nid = A.sid[p];
+    npt = A.ptouched[p];
   };
   if (c < nch) fetch(c);
   for (; c < nch; c += A.S) {
     const double a0 = n0, a1 = n1, a2 = n2, a3 = n3;
     const uint32_t tbh = ntb;
     const int32_t h = nid;
+    const uint8_t ntc = npt;
     if (c + A.S < nch) fetch(c + A.S);
     const int p = c * WAVE + lane;
     // the chunk's smallest memory is lane 0's (or its first position at or after lb): once it
     // is beyond the radius, so is every later chunk's -- the segment's list is final
     if (readlane_d(a1, 0) - d1 > rd) break;
-    const bool ok = p < n && p >= lb && A.touched[h] == 0;   // (h: clamped past n, read anyway)
+    const bool ok = p < n && p >= lb && ntc == 0;   // (position flag: no dependent load of h's)
     consider(ok, a0, a1, a2, a3, tbh, h);
   }
   // touched hosts: live capacities
@@ -233,12 +239,14 @@ void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, 
   if (n > 0) hipLaunchKernelGGL(band_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, H, lo, n, key, idx);
 }
 void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, const int32_t* sid,
-                        double* sa, uint32_t* stb, hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(band_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, tb, H, n, sid, sa, stb);
+                        double* sa, uint32_t* stb, int32_t* pos, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(band_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, tb, H, n, sid, sa, stb, pos);
 }
 void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* flags, int32_t* tlist,
-                         int32_t* tcount, hipStream_t st) {
-  hipLaunchKernelGGL(touch_update_kernel, dim3(1), dim3(1024), 0, st, own, status, flags, tlist, tcount);
+                         int32_t* tcount, const int32_t* pos, int lo, int hi, uint8_t* ptouch,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(touch_update_kernel, dim3(1), dim3(1024), 0, st, own, status, flags, tlist,
+                     tcount, pos, lo, hi, ptouch);
 }
 void launch_band_score(const BandArgs& a, hipStream_t st) {
   const int waves = a.nt * a.S;

@@ -184,6 +184,7 @@ struct pvt_ctx {
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
+  Buf bpos, bptouch;              // band lists: host -> sorted position, touched by position
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
@@ -377,7 +378,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->cmax, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
                  &ctx->btcnt, &ctx->bsorttmp, &ctx->brow[0], &ctx->brow[1], &ctx->brdem[0],
-                 &ctx->brdem[1], &ctx->bnrep[0], &ctx->bnrep[1]};
+                 &ctx->brdem[1], &ctx->bnrep[0], &ctx->bnrep[1], &ctx->bpos, &ctx->bptouch};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -815,8 +816,12 @@ static int band_snapshot(pvt_ctx* ctx) {
   Scope sc(ctx, PVT_K_OTHER, 0, 0);
   launch_band_keys(r->avail, R.H, R.lo, n, k0, i0, st);
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->bsorttmp.p, tmp, k0, k0 + n, i0, i0 + n, n, 0, 64, st));
-  launch_band_gather(r->avail, r->tiebreak, R.H, n, i0 + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb), st);
+  ENSURE(ctx->bpos, sizeof(int32_t) * (size_t)R.H);
+  ENSURE(ctx->bptouch, (size_t)n);
+  launch_band_gather(r->avail, r->tiebreak, R.H, n, i0 + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb),
+                     P<int32_t>(ctx->bpos), st);
   HIPCHK(hipMemsetAsync(ctx->btouch.p, 0, (size_t)R.H, st));
+  HIPCHK(hipMemsetAsync(ctx->bptouch.p, 0, (size_t)n, st));
   HIPCHK(hipMemsetAsync(ctx->btcnt.p, 0, 16, st));
   HIPCHK(hipGetLastError());
   return PVT_OK;
@@ -829,7 +834,7 @@ static void flush_touched(pvt_ctx* ctx) {
   if (!R.band || R.touch_lb < 0) return;
   launch_touch_update(P<int32_t>(ctx->owned[R.touch_lb]), P<int32_t>(ctx->next),
                       P<uint8_t>(ctx->btouch), P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt),
-                      ctx->stream);
+                      P<int32_t>(ctx->bpos), R.lo, R.hi, P<uint8_t>(ctx->bptouch), ctx->stream);
   R.touch_lb = -1;
 }
 
@@ -1196,7 +1201,8 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
     BandArgs ba{P<uint64_t>(ctx->bkey) + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb),
                 P<int32_t>(ctx->bidx) + n, n, R.lo, R.hi, P<uint8_t>(ctx->btouch),
                 P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt), r->avail, r->tiebreak, R.H, dem_l,
-                nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), nt_dev};
+                nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), nt_dev,
+                P<uint8_t>(ctx->bptouch)};
     {
       Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st, "band_score_kernel");
       launch_band_score(ba, st);

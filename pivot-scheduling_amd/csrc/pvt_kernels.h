@@ -354,13 +354,15 @@ struct BandArgs {
   SegEntry* seg;          // [nt][S][KL]
   int32_t* seg_feas;      // [nt][S]
   const int32_t* nt_dev;  // or NULL: only tasks [0, *nt_dev) (representative lists)
+  const uint8_t* ptouched;  // [n] touched by sorted position (= touched[sid[p]], read with the chunk)
 };
 void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,
                       hipStream_t st);
 void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, const int32_t* sid,
-                        double* sa, uint32_t* stb, hipStream_t st);
+                        double* sa, uint32_t* stb, int32_t* pos, hipStream_t st);
 void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* flags, int32_t* tlist,
-                         int32_t* tcount, hipStream_t st);
+                         int32_t* tcount, const int32_t* pos, int lo, int hi, uint8_t* ptouch,
+                         hipStream_t st);
 void launch_band_score(const BandArgs& a, hipStream_t st);
 // Window tasks -> list rows: each run of equal demand vectors (bit for bit) shares one list row;
 // rdem = the rows' demands, *nrep = rows (nt <= MAX_WINDOW)

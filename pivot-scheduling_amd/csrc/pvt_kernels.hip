@@ -669,19 +669,34 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   Key bnd = bound;
   if (cnt == LMAX && kless(src[LMAX - 1], bnd)) bnd = src[LMAX - 1];
   const int nw = max(cnt, KL);
-  for (int j = tid; j < nw; j += 256) {
-    ListEntry e;
+  // the kept hosts' zone and snapshot availability: every gather of the thread's (up to) four
+  // entries issued before the first is used (one HBM latency, not four)
+  constexpr int PO = LMAX / 256;
+  Key kk[PO];
+  int32_t zz[PO];
+  double aa[PO][4];
+#pragma unroll
+  for (int u = 0; u < PO; u++) {
+    const int j = tid + u * 256;
     const bool ok = j < cnt;
-    const Key k = ok ? src[j] : inv;
-    const int h = ok ? k.id : 0;
-    e.s = k.s; e.tb = k.tb; e.id = k.id; e.pad = 0; e.pad2 = 0.0;
-    e.zone = ok ? A.zone[h] : 0;
-    e.a[0] = ok ? A.avail[h] : 0.0;
-    e.a[1] = ok ? A.avail[(size_t)A.H + h] : 0.0;
-    e.a[2] = ok ? A.avail[2 * (size_t)A.H + h] : 0.0;
-    e.a[3] = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
+    kk[u] = ok ? src[j] : inv;
+    const int h = ok ? kk[u].id : 0;
+    zz[u] = ok ? A.zone[h] : 0;
+    aa[u][0] = ok ? A.avail[h] : 0.0;
+    aa[u][1] = ok ? A.avail[(size_t)A.H + h] : 0.0;
+    aa[u][2] = ok ? A.avail[2 * (size_t)A.H + h] : 0.0;
+    aa[u][3] = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < PO; u++) {
+    const int j = tid + u * 256;
+    if (j >= nw) continue;
+    ListEntry e;
+    e.s = kk[u].s; e.tb = kk[u].tb; e.id = kk[u].id; e.pad = 0; e.pad2 = 0.0;
+    e.zone = zz[u];
+    e.a[0] = aa[u][0]; e.a[1] = aa[u][1]; e.a[2] = aa[u][2]; e.a[3] = aa[u][3];
     A.L.e[(size_t)task * LMAX + j] = e;
-    A.L.ids[(size_t)task * LMAX + j] = ok ? k.id : 0x7fffffff;
+    A.L.ids[(size_t)task * LMAX + j] = j < cnt ? kk[u].id : 0x7fffffff;
   }
   if (tid < 4) {
     double* tr = reinterpret_cast<double*>(&A.L.t[task]);
