@@ -718,10 +718,10 @@ static void lists_from(pvt_ctx* ctx, Lists& L, int b = 0) {
 static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
   const int T = r->n_tasks, H = r->n_hosts;
   hipStream_t st = ctx->stream;
-  // Window: the walk's per-range passes rescan the window's touched hosts, so windows stay
-  // short; longer windows cut the per-window launches and hand-offs. (bench sweep at 1M hosts x
-  // 10k tasks with the speculative-range walk, profiles/r02h: pipelined 64 -> 20.1 ms,
-  // 128 -> 18.5, 256 -> 19.4)
+  // Window: longer windows cut the per-window launches and hand-offs; the walk's touched-host
+  // tables bound them (OPP_MAXW, LDS). (bench sweeps at 1M hosts x 10k tasks: round 2 with the
+  // speculative-range walk, profiles/r02h: pipelined 64 -> 20.1 ms, 128 -> 18.5, 256 -> 19.4;
+  // round 4 with the register-row walk: 128 -> 10.0, 256 -> 9.6)
   const int wdef = ctx->pipeline ? OPP_WINDOW_PIPE : OPP_WINDOW_DEFAULT;
   const int W = std::max(1, std::min(ctx->window > 0 ? ctx->window : wdef, OPP_MAXW));
   const int nq = (H + OPP_CH - 1) / OPP_CH, nsq = (nq + OPP_SUP - 1) / OPP_SUP;

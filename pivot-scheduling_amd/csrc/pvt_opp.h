@@ -19,7 +19,9 @@ constexpr int OPP_SUP = 64;     // chunks per super-chunk (16384 hosts)
 constexpr int OPP_TW = 8;       // tasks per wave in the count kernel
 constexpr int OPP_MAXW = 256;   // tasks per window (commit-walk LDS holds 2 x OPP_MAXW touched hosts)
 constexpr int OPP_WINDOW_DEFAULT = 256;   // sequential count / walk
-constexpr int OPP_WINDOW_PIPE = 128;      // pipelined windows
+constexpr int OPP_WINDOW_PIPE = 256;      // pipelined windows (round-4 sweep at config 5 with
+                                          // the register-row walk: 96 11.3, 128 10.0, 192 9.7,
+                                          // 256 9.6 ms; config 3: 128 1.22, 256 1.15 ms)
 
 struct OppCountArgs {
   const double* avail;
