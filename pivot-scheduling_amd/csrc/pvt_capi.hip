@@ -48,7 +48,9 @@ static constexpr int EP_SEG_OFF = 0, EP_SEG_CHAIN = EP_SEG_OFF + EPOCH_SEGS + 1,
 static constexpr int EP_WORDS = EP_SAFE + EPOCH_SEGS;
 static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a frontier-walk launch
 static constexpr int ORDERED_FRONTIER_MIN = 32;  // tasks a frontier attempt must place to go on
-static constexpr int ORDERED_FRONTIER_TASKS = 1024;   // tasks per frontier attempt (default)
+static constexpr int ORDERED_FRONTIER_TASKS = 4096;   // tasks per frontier attempt (default;
+                                                       // config-5 vbp_ff sweep: 512 1.75, 1024
+                                                       // 1.09, 2048 0.94, 4096 0.90, 8192 0.98 ms)
 static constexpr int ORDERED_FRONTIER_HOSTS = 65536;   // first span of hosts the window is taken from
 // vbp best-fit: candidate lists by a memory band over hosts sorted once per round (pvt_band.hip)
 // from this many hosts (per shard) on, with this many list segments per task
