@@ -132,7 +132,7 @@ struct RoundState {
   bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
   bool ffe = false;               // keyed rounds: first-fit zero-key epochs (ff_epoch)
   bool hmin_pre = false;          // the first epoch's host minima were queued by round_begin
-  bool prep_fused = false;        // build_order's order_prep_kernel filled placement / zone tables
+  bool prep_fused = false;        // build_order's order_scatter_kernel filled placement / zone tables
   int ffe_skip = -1;              //   the group they could not start (the keyed path takes it)
   // vbp best-fit band lists (pvt_band.hip): the sorted snapshot of hosts [lo, hi) is built; a
   // walk whose committed hosts are not yet flagged as touched (its own-ids buffer)
@@ -151,6 +151,7 @@ struct pvt_ctx {
   hipStream_t side = nullptr;     // scores the next window while the current one is walked
   hipEvent_t ev_lists = nullptr;   // side stream: the next window's lists are ready
   hipEvent_t ev_walk = nullptr;    // caller stream: everything before the current walk is done
+  hipEvent_t ev_stage = nullptr;   // the grouped order's counts are in the pinned stage
   int walk_cus = 0;                // CUs the side stream leaves to the walks
   std::string err;
   int window = 0;                 // 0: per-policy default
@@ -192,6 +193,7 @@ struct pvt_ctx {
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
   Buf cmax;                       // frontier-walked epochs: chains' largest demands
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
+  int32_t* ep_hdev = nullptr;     // ep_host's device address (the accept kernel's readback)
   pvt_round* rstage = nullptr;    // pvt_place_batch: descriptors staged for the device (pinned)
   size_t rstage_cap = 0;
   uint32_t* rmt_host = nullptr;   //   and the rounds' MT19937 states (pinned)
@@ -344,10 +346,12 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
       create_streams(ctx, prop.multiProcessorCount) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_lists, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_walk, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_stage, hipEventDisableTiming) != hipSuccess ||
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
       resident_init_attrs() != hipSuccess || lwalk_init_attrs() != hipSuccess ||
       hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess ||
-      hipHostMalloc((void**)&ctx->ep_host, sizeof(int32_t) * EP_WORDS) != hipSuccess) {
+      hipHostMalloc((void**)&ctx->ep_host, sizeof(int32_t) * EP_WORDS) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&ctx->ep_hdev, ctx->ep_host, 0) != hipSuccess) {
     delete ctx;
     return PVT_EHIP;
   }
@@ -392,6 +396,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   if (ctx->rmt_host) (void)hipHostFree(ctx->rmt_host);
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
   if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
+  if (ctx->ev_stage) (void)hipEventDestroy(ctx->ev_stage);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
@@ -567,7 +572,7 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
   if (grouped && r->n_groups <= (1 << 20)) {
     // one synchronisation: group counts, group anchors and the cost table to the host
     const int G = r->n_groups;
-    const bool fused = T <= PREP_T_MAX && G <= GAGG_MAX;   // (order_prep_kernel: one launch)
+    const bool fused = T <= PREP_T_MAX && G <= GAGG_MAX;   // (launch_order_prep: two launches)
     if (!fused) {
       ENSURE(ctx->gcnt, sizeof(int32_t) * (G + 1));
       HIPCHK(hipMemsetAsync(ctx->gcnt.p, 0, sizeof(int32_t) * (G + 1), st));
@@ -606,7 +611,7 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
                   r->dem, r->sort_tasks ? 1 : 0, r->placement, P<int32_t>(ctx->goff), dcnt,
                   dcnt + G + 1, dcst, ca ? P<double>(ctx->csum) : nullptr,
                   ca ? P<double>(ctx->bsum) : nullptr, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx)};
-      launch_order_prep(pa, st);
+      launch_order_prep(pa, st, ctx->ev_stage);
       R.prep_fused = true;
     } else {
       launch_group_stage(P<int32_t>(ctx->gcnt), G, r->group_anchor, r->cost, (int)nz2,
@@ -620,7 +625,10 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
       }
       launch_group_scatter(r->task_group, keys, T, G, P<int32_t>(ctx->goff) + G + 1,
                            P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx), st);
+      HIPCHK(hipEventRecord(ctx->ev_stage, st));
     }
+    // the host waits for the staged counts only (ev_stage), not for the scatter, sorts and
+    // gathers queued after them: it plans the round while they run
     launch_group_sort(P<int32_t>(ctx->goff), G, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx),
                       cur, st);
     R.ginfo = ca;
@@ -895,7 +903,7 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
     R.hmin_pre = true;
   }
   if (pending) {   // the one synchronisation of the grouped order: counts, anchors, cost table
-    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipEventSynchronize(ctx->ev_stage));
     bool redo = false;
     if ((rc = build_order_check(ctx, r, &redo))) return rc;
     if (redo) {
@@ -1607,11 +1615,10 @@ static int ff_epoch(pvt_ctx* ctx, int* adv_out) {
   {
     Scope sc(ctx, PVT_K_OTHER, 0, 0);
     launch_epoch_final(ea, st);
-    launch_epoch_accept_apply(ea, dev + EP_RES, nch, st);
+    launch_epoch_accept_apply(ea, dev + EP_RES, nch, st, ctx->ep_hdev + EP_STATUS,
+                              EP_WORDS - EP_STATUS);   // (readback: mapped)
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
-                        hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   ctx->n_epochs++;
   ctx->n_segs += nseg;
@@ -1740,11 +1747,10 @@ static int place_epochs(pvt_ctx* ctx) {
       {
         Scope sc(ctx, PVT_K_OTHER, 0, 0);
         launch_epoch_validate(ea, st);
-        launch_epoch_accept_apply(ea, dev + EP_RES, nch, st);
+        launch_epoch_accept_apply(ea, dev + EP_RES, nch, st, ctx->ep_hdev + EP_STATUS,
+                                  EP_WORDS - EP_STATUS);   // (readback: mapped)
       }
       HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
-                            hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       int adv = 0;
       if ((rc = epoch_frontier_verdict(ctx, E, t0, &need, &adv))) return rc;
@@ -2502,7 +2508,6 @@ static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
     const EpochPlan& E = R.E;
     const int nseg = (int)E.chain.size(), nch = nslots;
     int32_t* dev = P<int32_t>(ctx->ep_dev);
-    int32_t* host = ctx->ep_host;
     ENSURE(ctx->cmax, sizeof(double) * 4 * EPOCH_SEGS);
     ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
                  P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
@@ -2522,11 +2527,10 @@ static int shard_frontier_commit(pvt_ctx* ctx, const void* packages) {
     {
       Scope sc(ctx, PVT_K_OTHER, 0, 0);
       launch_epoch_validate(ea, st);
-      launch_epoch_accept_apply(ea, dev + EP_RES, nch, st);
+      launch_epoch_accept_apply(ea, dev + EP_RES, nch, st, ctx->ep_hdev + EP_STATUS,
+                                EP_WORDS - EP_STATUS);   // (readback: mapped)
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(host + EP_STATUS, dev + EP_STATUS, sizeof(int32_t) * (EP_WORDS - EP_STATUS),
-                          hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     int need = 0, adv = 0;
     if ((rc = epoch_frontier_verdict(ctx, E, t0, &need, &adv))) return rc;

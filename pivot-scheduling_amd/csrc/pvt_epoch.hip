@@ -73,17 +73,18 @@ __device__ __forceinline__ bool beats(int32_t h, double f0, double f1, double f2
 constexpr int VAL_HASH = 512;
 
 // Every chain walked to its end and every final entry safe (EpochArgs.cmax): nothing to check.
+// The block's threads split the chains and segments (at most EPOCH_SEGS each): one load latency
+// instead of a serial walk over both tables in every thread of every block.
 __device__ __forceinline__ bool epoch_fast(const EpochArgs& A) {
   if (!A.cmax) return false;
-  for (int c = 0; c < A.nch; c++)
-    if (A.status[2 * c] != A.coff[c + 1] - A.coff[c]) return false;
-  for (int s = 0; s < A.nseg; s++)
-    if (!A.safe[s]) return false;
-  return true;
+  bool slow = false;
+  for (int c = threadIdx.x; c < A.nch; c += blockDim.x)
+    slow |= A.status[2 * c] != A.coff[c + 1] - A.coff[c];
+  for (int s = threadIdx.x; s < A.nseg; s += blockDim.x) slow |= !A.safe[s];
+  return !__syncthreads_or(slow);
 }
 
 __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
-  if (epoch_fast(A)) return;
   __shared__ int32_t e_id[256];
   __shared__ double e_a[4][256];
   __shared__ double e_c[256], e_b[256];
@@ -93,13 +94,14 @@ __global__ __launch_bounds__(256) void epoch_validate_kernel(EpochArgs A) {
   __shared__ int32_t wfull[4];
   __shared__ int32_t stop;
   const int j = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (j == 0 || j >= A.nseg) return;
+  if (j == 0 || j >= A.nseg) return;          // (block-uniform exits, cheapest first)
   const int s0 = A.seg_off[j], adv = seg_adv(A, j);
   if ((int)blockIdx.x * 256 >= adv) return;
   const int L = s0;                           // earlier window tasks: [0, s0)
   const int lo = (int)((long long)L * blockIdx.z / VAL_SPLIT);
   const int hi = (int)((long long)L * (blockIdx.z + 1) / VAL_SPLIT);
   if (lo >= hi) return;
+  if (epoch_fast(A)) return;
   const int t = s0 + blockIdx.x * 256 + tid;
   const bool mine = t < s0 + adv;
   const int cj = A.seg_chain[j];
@@ -284,45 +286,124 @@ __global__ __launch_bounds__(256) void epoch_apply_kernel(EpochArgs A, int n_acc
 // Every block derives it; block 0 reports it (res: accepted segments, next task relative to the
 // epoch, refill, rejected segments, a chain walk timed out); block c then writes chain c's
 // accepted segments' final entries, as epoch_apply_kernel. A timed-out walk applies nothing.
-__global__ __launch_bounds__(256) void epoch_accept_apply_kernel(EpochArgs A, int32_t* res) {
-  __shared__ int32_t acc_s, tout_s;
-  const int c = blockIdx.x;
-  if (threadIdx.x == 0) {
-    int acc = 0, next = 0, refill = 0, rej = 0, tout = 0;
-    for (int j = 0; j < A.nseg; j++) tout |= A.status[2 * A.seg_chain[j]] == -1;
-    if (!tout) {
-      for (int j = 0; j < A.nseg; j++) {
-        const int len = A.seg_off[j + 1] - A.seg_off[j];
-        const int adv = seg_adv(A, j);
-        if (j > 0 && A.bad[j]) { rej = A.nseg - j; break; }
-        if (A.whole && adv < len) { next = A.seg_off[j]; refill = 1; rej = A.nseg - j; break; }
-        acc = j + 1;
-        next = A.seg_off[j] + adv;
-        if (adv < len) { refill = 1; rej = A.nseg - j - 1; break; }
-      }
-    }
-    acc_s = acc;
-    tout_s = tout;
-    if (c == 0) { res[0] = acc; res[1] = next; res[2] = refill; res[3] = rej; res[4] = tout; }
+// The first stopping segment is found by all threads at once (LDS minimum), and each wave picks
+// chain c's segments 64 at a time by ballot: no serial walk over the segment table. Block 0 also
+// writes the readback words (nwords from A.status: statuses, verdicts, res, safe flags) straight
+// into the caller's mapped pinned buffer hout: no copy launch after the kernel.
+__global__ __launch_bounds__(1024) void epoch_accept_apply_kernel(EpochArgs A, int32_t* res,
+                                                                  int32_t* hout, int nwords) {
+  __shared__ int32_t first_s;
+  const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int nseg = A.nseg;
+  if (tid == 0) first_s = nseg;
+  bool tout = false;
+  for (int j = tid; j < nseg; j += blockDim.x) tout |= A.status[2 * A.seg_chain[j]] == -1;
+  const int roff = (int)(res - A.status);    // res inside the readback words
+  auto put = [&](int i, int32_t v) {
+    res[i] = v;
+    if (hout) hout[roff + i] = v;
+  };
+  if (c == 0 && hout)
+    for (int k = tid; k < nwords; k += blockDim.x)
+      if (k < roff || k >= roff + 5) hout[k] = A.status[k];
+  if (__syncthreads_or(tout)) {               // (also publishes first_s)
+    if (c == 0 && tid == 0) { put(0, 0); put(1, 0); put(2, 0); put(3, 0); put(4, 1); }
+    return;
+  }
+  for (int j = tid; j < nseg; j += blockDim.x) {
+    const int len = A.seg_off[j + 1] - A.seg_off[j];
+    if ((j > 0 && A.bad[j]) || seg_adv(A, j) < len) atomicMin(&first_s, j);
   }
   __syncthreads();
-  if (tout_s) return;
-  const int n_accept = acc_s;
-  for (int s = 0; s < n_accept; s++) {
-    if (A.seg_chain[s] != c) continue;
-    const int e0 = A.seg_off[s], ne = seg_adv(A, s);
-    for (int k = threadIdx.x; k < ne; k += blockDim.x) {
-      const WinRec& e = A.wlog[e0 + k];
-      if (e.id < 0 || e.sup) continue;
-#pragma unroll
-      for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + e.id] = e.a[r];
+  const int f = first_s;
+  int acc = nseg;
+  if (f < nseg) {
+    const int adv = seg_adv(A, f);
+    const bool whole_stop = (f > 0 && A.bad[f]) || A.whole;   // (adv < len when not rejected)
+    acc = whole_stop ? f : f + 1;
+    if (c == 0 && tid == 0) {
+      const bool rejected = f > 0 && A.bad[f];
+      put(0, acc);
+      put(1, whole_stop ? A.seg_off[f] : A.seg_off[f] + adv);
+      put(2, rejected ? 0 : 1);
+      put(3, whole_stop ? nseg - f : nseg - f - 1);
+      put(4, 0);
     }
-    __syncthreads();
+  } else if (c == 0 && tid == 0) {
+    put(0, nseg); put(1, nseg > 0 ? A.seg_off[nseg] : 0); put(2, 0); put(3, 0); put(4, 0);
+  }
+  if (acc > 64) {                              // (not from the planners: EPOCH_SEGS = 64)
+    for (int base = 0; base < acc; base += 64) {
+      const int sl = base + lane;
+      uint64_t own = __ballot(sl < acc && A.seg_chain[sl] == c);
+      while (own) {
+        const int s = base + __builtin_ctzll(own);
+        own &= own - 1;
+        const int e0 = A.seg_off[s], ne = seg_adv(A, s);
+        for (int k = tid; k < ne; k += blockDim.x) {
+          const WinRec& e = A.wlog[e0 + k];
+          if (e.id < 0 || e.sup) continue;
+#pragma unroll
+          for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + e.id] = e.a[r];
+        }
+        __syncthreads();
+      }
+    }
+    return;
+  }
+  // Chain c's accepted segments cover chain-local positions [0, P) (every one but the last is
+  // complete). An entry is written iff it is its host's last in that prefix (LDS hash: host ->
+  // largest position), so every entry is loaded once and all writes go out together.
+  __shared__ int32_t hk[FIN_SLOTS], hv[FIN_SLOTS];
+  __shared__ int32_t o_cs[64], o_off[64], n_own, plen;
+  if (tid < 64) {
+    const bool mine = tid < acc && A.seg_chain[tid] == c;
+    const uint64_t own = __ballot(mine);
+    const int i = __popcll(own & ((1ull << tid) - 1ull));
+    if (mine) {
+      o_cs[i] = A.seg_cstart[tid];
+      o_off[i] = A.seg_off[tid];
+      if (!(own >> tid >> 1)) { n_own = i + 1; plen = A.seg_cstart[tid] + seg_adv(A, tid); }
+    }
+    if (tid == 0 && !own) { n_own = 0; plen = 0; }
+  }
+  for (int q = tid; q < FIN_SLOTS; q += blockDim.x) { hk[q] = -1; hv[q] = -1; }
+  __syncthreads();
+  const int n = n_own, P = plen;
+  constexpr int PER = CHAIN_MAX / 1024;
+  WinRec e[PER];
+  int slot[PER];
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int k = tid + i * 1024;
+    slot[i] = -1;
+    if (k >= P) continue;
+    int q = 0;
+    while (q + 1 < n && o_cs[q + 1] <= k) q++;
+    e[i] = A.wlog[o_off[q] + (k - o_cs[q])];
+    const int32_t h = e[i].id;
+    if (h < 0) continue;
+    uint32_t p = ((uint32_t)h * 2654435761u) & (FIN_SLOTS - 1);
+    for (;;) {
+      const int32_t o = atomicCAS(&hk[p], -1, h);
+      if (o == -1 || o == h) break;
+      p = (p + 1) & (FIN_SLOTS - 1);
+    }
+    atomicMax(&hv[p], k);
+    slot[i] = (int)p;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    if (slot[i] < 0 || hv[slot[i]] != tid + i * 1024) continue;
+#pragma unroll
+    for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + e[i].id] = e[i].a[r];
   }
 }
 
-void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st) {
-  hipLaunchKernelGGL(epoch_accept_apply_kernel, dim3(nchains), dim3(256), 0, st, a, res);
+void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st,
+                               int32_t* hout, int nwords) {
+  hipLaunchKernelGGL(epoch_accept_apply_kernel, dim3(nchains), dim3(1024), 0, st, a, res, hout, nwords);
 }
 
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {

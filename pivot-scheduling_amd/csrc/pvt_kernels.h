@@ -205,8 +205,10 @@ void launch_epoch_validate(const EpochArgs& a, hipStream_t st);
 void launch_epoch_final(const EpochArgs& a, hipStream_t st);
 // apply: the accepted segments [0, n_accept) of each chain, chain by chain in segment order
 void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st);
-// validate's verdict to the accepted prefix and its apply, on the device; res[5] reported
-void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st);
+// validate's verdict to the accepted prefix and its apply, on the device; res[5] reported, and
+// (hout: mapped pinned memory) the nwords readback words from a.status copied there
+void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st,
+                               int32_t* hout = nullptr, int nwords = 0);
 void launch_commit_chains(const CommitArgs& a, int nchains, hipStream_t st);
 // vbp best-fit windows: the one-wave list walk with list cursors (pvt_lwalk.hip); CommitArgs as
 // for launch_commit (no epochs, no stamps). status[0] < nt: refill there (0: the list walk decides)
@@ -433,7 +435,8 @@ struct PrepArgs {
   uint64_t* skey;
   int32_t* sidx;
 };
-void launch_order_prep(const PrepArgs& a, hipStream_t st);
+// counted (optional): recorded once the counts are staged, before the scatter launch
+void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted = nullptr);
 void launch_group_stage(const int32_t* cnt, int G, const int32_t* ganc, const double* cost, int nz2,
                         int32_t* off, int32_t* hcnt, int32_t* hgan, double* hcst, hipStream_t st);
 void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,

@@ -1054,29 +1054,19 @@ void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G,
   hipLaunchKernelGGL(group_scatter_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, keys, T,
                      G, cursor, skey, sidx);
 }
-// The grouped order's preparation in ONE block (rounds of at most PREP_T_MAX tasks and
-// GAGG_MAX groups; the config-5 round's seven launches -- placement fill, counter clear, group
-// histogram, stage, sort keys, scatter, zone tables -- were each a few microseconds of launch
-// latency on the host's critical path): counts in LDS, the pinned staging of counts / anchors /
-// cost table, the groups' offsets, then the (key, task) pairs scattered by LDS cursors (their
-// order inside a group is irrelevant: group_sort orders by (key, index)).
-__global__ __launch_bounds__(1024) void order_prep_kernel(PrepArgs A) {
+// The grouped order's preparation in two one-block launches (rounds of at most PREP_T_MAX
+// tasks and GAGG_MAX groups; the config-5 round's seven launches -- placement fill, counter
+// clear, group histogram, stage, sort keys, scatter, zone tables -- were each a few microseconds
+// of launch latency on the host's critical path). order_count_kernel: the group counts in LDS
+// and the pinned staging of counts / anchors / cost table -- all the host waits for before it
+// plans the round. order_scatter_kernel, while the host plans: placement fill, zone tables, the
+// groups' offsets, then the (key, task) pairs scattered by LDS cursors (their order inside a
+// group is irrelevant: group_sort orders by (key, index)).
+__global__ __launch_bounds__(1024) void order_count_kernel(PrepArgs A) {
   __shared__ int32_t cnt[GAGG_MAX + 1];
-  __shared__ int32_t cur[GAGG_MAX];
-  __shared__ int32_t wsum[16];
-  __shared__ int32_t carry;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int t = threadIdx.x;
   const int T = A.T, G = A.G;
   for (int q = t; q <= G; q += 1024) cnt[q] = 0;
-  if (t == 0) carry = 0;
-  if (A.placement)
-    for (int i = t; i < T; i += 1024) A.placement[i] = -1;
-  if (A.csum)
-    for (int i = t; i < A.Z * A.Z; i += 1024) {
-      const int a = i / A.Z, z = i - a * A.Z;
-      A.csum[i] = A.cost[a * A.Z + z] + A.cost[z * A.Z + a];   // cost_aware.py:82,113
-      A.bsum[i] = A.bw[a * A.Z + z] + A.bw[z * A.Z + a];       // (:79,111)
-    }
   __syncthreads();
   // (loads batched PB per thread so their latencies overlap: the block is alone on its CU)
   constexpr int PB = 16;
@@ -1092,12 +1082,32 @@ __global__ __launch_bounds__(1024) void order_prep_kernel(PrepArgs A) {
       if (gv[u] != -2) atomicAdd(&cnt[(gv[u] >= 0 && gv[u] < G) ? gv[u] : G], 1);   // G: out of range
   }
   __syncthreads();
-  for (int i = t; i <= G; i += 1024) A.hcnt[i] = cnt[i];
+  // counts to the host's stage and to off (the scatter kernel scans them there)
+  for (int i = t; i <= G; i += 1024) { A.hcnt[i] = cnt[i]; A.off[i] = cnt[i]; }
   for (int i = t; i < G; i += 1024) A.hgan[i] = A.ganc[i];
   for (int i = t; i < A.nz2; i += 1024) A.hcst[i] = A.cost[i];
-  for (int g0 = 0; g0 < G; g0 += 1024) {            // exclusive scan -> offsets and cursors
+  __threadfence_system();
+}
+
+__global__ __launch_bounds__(1024) void order_scatter_kernel(PrepArgs A) {
+  __shared__ int32_t cur[GAGG_MAX];
+  __shared__ int32_t wsum[16];
+  __shared__ int32_t carry;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int T = A.T, G = A.G;
+  if (t == 0) carry = 0;
+  if (A.placement)
+    for (int i = t; i < T; i += 1024) A.placement[i] = -1;
+  if (A.csum)
+    for (int i = t; i < A.Z * A.Z; i += 1024) {
+      const int a = i / A.Z, z = i - a * A.Z;
+      A.csum[i] = A.cost[a * A.Z + z] + A.cost[z * A.Z + a];   // cost_aware.py:82,113
+      A.bsum[i] = A.bw[a * A.Z + z] + A.bw[z * A.Z + a];       // (:79,111)
+    }
+  __syncthreads();
+  for (int g0 = 0; g0 < G; g0 += 1024) {            // exclusive scan of the counts in off
     const int g = g0 + t;
-    const int v = g < G ? cnt[g] : 0;
+    const int v = g < G ? A.off[g] : 0;
     int x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1142,10 +1152,11 @@ __global__ __launch_bounds__(1024) void order_prep_kernel(PrepArgs A) {
       A.sidx[pos] = i;
     }
   }
-  __threadfence_system();
 }
-void launch_order_prep(const PrepArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(order_prep_kernel, dim3(1), dim3(1024), 0, st, a);
+void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted) {
+  hipLaunchKernelGGL(order_count_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (counted) (void)hipEventRecord(counted, st);
+  hipLaunchKernelGGL(order_scatter_kernel, dim3(1), dim3(1024), 0, st, a);
 }
 
 __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, const uint64_t* skey,
@@ -1173,31 +1184,70 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
     }
     return;
   }
+  // Bitonic network over P = 2^ceil(log2 n) elements, element i = m * 1024 + tid in registers:
+  // the compare-exchange stages of stride < 64 pair lanes of one wave (shuffles, no barrier);
+  // only the stages of stride >= 64 (10 of the 55 at P = 1024) go through LDS with a barrier
+  // each. (The all-LDS network: 20.6 us per config-5 round.)
   int P = 2;
   while (P < n) P <<= 1;
-  for (int i = tid; i < P; i += blockDim.x) {
-    k[i] = i < n ? skey[a + i] : ~0ull;
-    v[i] = i < n ? sidx[a + i] : 0x7fffffff;
+  constexpr int EMAX = GSORT_MAX / 1024;
+  const int E = (P + 1023) >> 10;
+  uint64_t rk[EMAX];
+  int32_t rv[EMAX];
+#pragma unroll
+  for (int m = 0; m < EMAX; m++) {
+    const int i = m * 1024 + tid;
+    rk[m] = (m < E && i < n) ? skey[a + i] : ~0ull;
+    rv[m] = (m < E && i < n) ? sidx[a + i] : 0x7fffffff;
   }
-  __syncthreads();
   for (int size = 2; size <= P; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int j = tid; j < (P >> 1); j += blockDim.x) {
-        const int lo = 2 * stride * (j / stride) + (j % stride), hi = lo + stride;
-        const bool up = (lo & size) == 0;
-        const uint64_t kl = k[lo], kh = k[hi];
-        const int32_t vl = v[lo], vh = v[hi];
-        const bool gt = kl > kh || (kl == kh && vl > vh);
-        if (gt == up) { k[lo] = kh; k[hi] = kl; v[lo] = vh; v[hi] = vl; }
-      }
+    int stride = size >> 1;
+    if (stride >= 64) {
+#pragma unroll
+      for (int m = 0; m < EMAX; m++)
+        if (m < E) { k[m * 1024 + tid] = rk[m]; v[m * 1024 + tid] = rv[m]; }
       __syncthreads();
+      for (; stride >= 64; stride >>= 1) {
+        for (int j = tid; j < (P >> 1); j += blockDim.x) {
+          const int lo = 2 * stride * (j / stride) + (j % stride), hi = lo + stride;
+          const bool up = (lo & size) == 0;
+          const uint64_t kl = k[lo], kh = k[hi];
+          const int32_t vl = v[lo], vh = v[hi];
+          const bool gt = kl > kh || (kl == kh && vl > vh);
+          if (gt == up) { k[lo] = kh; k[hi] = kl; v[lo] = vh; v[hi] = vl; }
+        }
+        __syncthreads();
+      }
+#pragma unroll
+      for (int m = 0; m < EMAX; m++)
+        if (m < E) { rk[m] = k[m * 1024 + tid]; rv[m] = v[m * 1024 + tid]; }
+    }
+    for (; stride > 0; stride >>= 1) {
+#pragma unroll
+      for (int m = 0; m < EMAX; m++) {
+        if (m >= E) continue;
+        const int i = m * 1024 + tid;
+        const uint32_t klo = (uint32_t)rk[m], khi = (uint32_t)(rk[m] >> 32);
+        const uint64_t pk = ((uint64_t)(uint32_t)__shfl_xor((int)khi, stride) << 32) |
+                            (uint32_t)__shfl_xor((int)klo, stride);
+        const int32_t pv = __shfl_xor(rv[m], stride);
+        const bool up = (i & size) == 0, low = (i & stride) == 0;
+        const uint64_t kl = low ? rk[m] : pk, kh = low ? pk : rk[m];
+        const int32_t vl = low ? rv[m] : pv, vh = low ? pv : rv[m];
+        const bool gt = kl > kh || (kl == kh && vl > vh);
+        if (gt == up) { rk[m] = pk; rv[m] = pv; }
+      }
     }
   }
-  for (int i = tid; i < n; i += blockDim.x) ord[a + i] = v[i];
+#pragma unroll
+  for (int m = 0; m < EMAX; m++) {
+    const int i = m * 1024 + tid;
+    if (m < E && i < n) ord[a + i] = rv[m];
+  }
 }
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
                        int32_t* ord, hipStream_t st) {
-  // (1024 threads: measured 20.6 us per config-5 round against 29.0 with 256)
+  // (1024 threads, the block's element layout above assumes it)
   hipLaunchKernelGGL(group_sort_kernel, dim3(G), dim3(1024), 0, st, off, skey, sidx, ord);
 }
 
