@@ -132,6 +132,7 @@ struct RoundState {
   bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
   bool ffe = false;               // keyed rounds: first-fit zero-key epochs (ff_epoch)
   bool hmin_pre = false;          // the first epoch's host minima were queued by round_begin
+  bool gathered = false;          // ... and group_sort_gather_kernel wrote the gathered order
   bool prep_fused = false;        // build_order's order_scatter_kernel filled placement / zone tables
   int ffe_skip = -1;              //   the group they could not start (the keyed path takes it)
   // vbp best-fit band lists (pvt_band.hip): the sorted snapshot of hosts [lo, hi) is built; a
@@ -196,6 +197,8 @@ struct pvt_ctx {
   int32_t* ep_hdev = nullptr;     // ep_host's device address (the accept kernel's readback)
   pvt_round* rstage = nullptr;    // pvt_place_batch: descriptors staged for the device (pinned)
   size_t rstage_cap = 0;
+  hipEvent_t ev_rstage = nullptr;  //   recorded after their upload (and the MT states')
+  bool rstage_busy = false;
   uint32_t* rmt_host = nullptr;   //   and the rounds' MT19937 states (pinned)
   size_t rmt_cap = 0;
   RoundState rs;
@@ -347,6 +350,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_lists, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_walk, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_stage, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_rstage, hipEventDisableTiming) != hipSuccess ||
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
       resident_init_attrs() != hipSuccess || lwalk_init_attrs() != hipSuccess ||
       hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess ||
@@ -397,6 +401,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
   if (ctx->ev_lists) (void)hipEventDestroy(ctx->ev_lists);
   if (ctx->ev_walk) (void)hipEventDestroy(ctx->ev_walk);
   if (ctx->ev_stage) (void)hipEventDestroy(ctx->ev_stage);
+  if (ctx->ev_rstage) (void)hipEventDestroy(ctx->ev_rstage);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->own) (void)hipStreamDestroy(ctx->own);
   delete ctx;
@@ -409,9 +414,23 @@ extern "C" int pvt_ctx_set_stream(pvt_ctx* ctx, void* stream) {
   return PVT_OK;
 }
 
+// Events of the timed scopes come from a pool that harvest() refills; the pool is filled and
+// every event recorded once when profiling is switched on, so a timed round neither creates an
+// event nor pays a first record (measured ~11 us on the default line's critical path).
+static constexpr size_t EVPOOL_WARM = 1024;
 extern "C" int pvt_set_profiling(pvt_ctx* ctx, int on) {
   if (!ctx) return PVT_EINVAL;
   ctx->profiling = on == 2 ? 2 : (on != 0 ? 1 : 0);
+  if (ctx->profiling && ctx->evpool.size() + 2 * ctx->pending.size() < EVPOOL_WARM) {
+    (void)hipSetDevice(ctx->device);
+    while (ctx->evpool.size() + 2 * ctx->pending.size() < EVPOOL_WARM) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) break;
+      (void)hipEventRecord(e, ctx->stream);
+      ctx->evpool.push_back(e);
+    }
+    (void)hipStreamSynchronize(ctx->stream);
+  }
   return PVT_OK;
 }
 extern "C" int pvt_reset_kstats(pvt_ctx* ctx) {
@@ -611,8 +630,18 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
                   r->dem, r->sort_tasks ? 1 : 0, r->placement, P<int32_t>(ctx->goff), dcnt,
                   dcnt + G + 1, dcst, ca ? P<double>(ctx->csum) : nullptr,
                   ca ? P<double>(ctx->bsum) : nullptr, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx)};
-      launch_order_prep(pa, st, ctx->ev_stage);
       R.prep_fused = true;
+      if (G <= GCOMPACT_MAX) {   // counts, then one launch for the sorted, gathered order
+        launch_order_prep(pa, st, ctx->ev_stage, false);
+        launch_group_sort_gather(pa, GatherOut{cur, P<double>(ctx->dem_ord), P<int32_t>(ctx->anc_ord),
+                                               P<int32_t>(ctx->grp_ord), r->order}, st);
+        R.gathered = true;
+        R.ginfo = ca;
+        *pending = true;
+        *ord_out = cur;
+        return PVT_OK;
+      }
+      launch_order_prep(pa, st, ctx->ev_stage);
     } else {
       launch_group_stage(P<int32_t>(ctx->gcnt), G, r->group_anchor, r->cost, (int)nz2,
                          P<int32_t>(ctx->goff), dcnt, dcnt + G + 1, dcst, st);
@@ -874,17 +903,18 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
 
   bool pending = false;
   R.prep_fused = false;
-  if ((rc = build_order(ctx, r, &R.ord, &pending))) return rc;
-  if (!R.prep_fused) HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
+  R.gathered = false;
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   ENSURE(ctx->grp_ord, sizeof(int32_t) * T);
+  if ((rc = build_order(ctx, r, &R.ord, &pending))) return rc;
+  if (!R.prep_fused) HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
   auto order_out = [&]() -> int {   // (the gather also writes the caller's order)
     launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
                         P<int32_t>(ctx->anc_ord), P<int32_t>(ctx->grp_ord), st, r->n_groups, r->order);
     return PVT_OK;
   };
-  if ((rc = order_out())) return rc;
+  if (!R.gathered && (rc = order_out())) return rc;
   const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
   if (ca) {
     ENSURE(ctx->csum, sizeof(double) * Z * Z);
@@ -1564,8 +1594,8 @@ static int upload_chain_tables(pvt_ctx* ctx, const EpochPlan& E) {
   }
   host[EP_COFF + nch] = nm;
   host[EP_CSOFF + nch] = ns;
-  HIPCHK(hipMemcpyAsync(ctx->ep_dev.p, host, sizeof(int32_t) * (EP_CMAP + nm), hipMemcpyHostToDevice,
-                        ctx->stream));
+  launch_upload(ctx->ep_hdev, ctx->ep_dev.p, sizeof(int32_t) * (EP_CMAP + nm), ctx->stream);
+  HIPCHK(hipGetLastError());
   return PVT_OK;
 }
 
@@ -1870,25 +1900,38 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     return PVT_OK;
   }
   int rc;
+  // the staged descriptors (and MT states) reach the device by an upload kernel reading their
+  // mapped pages when it runs: a new batch waits until the previous batch's upload has run
+  if (ctx->rstage_busy) HIPCHK(hipEventSynchronize(ctx->ev_rstage));
+  ctx->rstage_busy = false;
   if ((rc = ensure_pinned_array(ctx, ctx->rstage, ctx->rstage_cap, (size_t)n))) return rc;
   std::memcpy(ctx->rstage, rounds, sizeof(pvt_round) * n);
-  ENSURE(ctx->rdesc, sizeof(pvt_round) * (size_t)n);
+  ENSURE(ctx->rdesc, sizeof(pvt_round) * (size_t)n + 16);   // (+16: the upload's rounding)
   uint32_t* mt = nullptr;
   const bool host_mt = mode == PVT_OPP && !mt_dev;
   if (mode == PVT_OPP && mt_dev) {
     mt = mt_dev;
     for (int i = 0; i < n; i++) ctx->rstage[i].mt_state = mt + (size_t)i * 625;
   } else if (host_mt) {
-    ENSURE(ctx->rmt, sizeof(uint32_t) * 625 * (size_t)n);
+    ENSURE(ctx->rmt, sizeof(uint32_t) * 625 * (size_t)n + 16);
     mt = P<uint32_t>(ctx->rmt);
     if ((rc = ensure_pinned_array(ctx, ctx->rmt_host, ctx->rmt_cap, (size_t)n * 625))) return rc;
     for (int i = 0; i < n; i++) {
       std::memcpy(ctx->rmt_host + (size_t)i * 625, rounds[i].mt_state, sizeof(uint32_t) * 625);
       ctx->rstage[i].mt_state = mt + (size_t)i * 625;   // device copy (the kernel never reads the field)
     }
-    HIPCHK(hipMemcpyAsync(mt, ctx->rmt_host, sizeof(uint32_t) * 625 * n, hipMemcpyHostToDevice, st));
+    void* dmt = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dmt, ctx->rmt_host, 0));
+    launch_upload(dmt, mt, sizeof(uint32_t) * 625 * n, st);
   }
-  HIPCHK(hipMemcpyAsync(ctx->rdesc.p, ctx->rstage, sizeof(pvt_round) * n, hipMemcpyHostToDevice, st));
+  {
+    void* dst = nullptr;
+    HIPCHK(hipHostGetDevicePointer(&dst, ctx->rstage, 0));
+    launch_upload(dst, ctx->rdesc.p, sizeof(pvt_round) * n, st);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ctx->ev_rstage, st));
+  ctx->rstage_busy = true;
   ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad, ctx->stamps};
   {
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");

@@ -435,8 +435,23 @@ struct PrepArgs {
   uint64_t* skey;
   int32_t* sidx;
 };
-// counted (optional): recorded once the counts are staged, before the scatter launch
-void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted = nullptr);
+// counted (optional): recorded once the counts are staged, before the scatter launch (scatter
+// = false: counts only, for launch_group_sort_gather)
+void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted = nullptr,
+                       bool scatter = true);
+// Few groups (G <= GCOMPACT_MAX): after the counts, one launch collects, sorts and gathers every
+// group (order, caller order, demand rows, anchors, groups), fills placement and zone tables.
+constexpr int GCOMPACT_MAX = 64;
+struct GatherOut {
+  int32_t* ord;
+  double* dem_ord;
+  int32_t* anc_ord;
+  int32_t* grp_ord;
+  int32_t* order_out;         // the caller's order, or NULL
+};
+void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st);
+// bytes (rounded up to 16; both buffers 16-B aligned and that long) from mapped pinned memory
+void launch_upload(const void* src_mapped, void* dst, size_t bytes, hipStream_t st);
 void launch_group_stage(const int32_t* cnt, int G, const int32_t* ganc, const double* cost, int nz2,
                         int32_t* off, int32_t* hcnt, int32_t* hgan, double* hcst, hipStream_t st);
 void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,

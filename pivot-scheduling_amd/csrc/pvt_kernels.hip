@@ -10,6 +10,7 @@
 // numpy's la.norm -> OpenBLAS ddot computes for n = 4; sqrt and division are IEEE
 // correctly rounded (llvm.sqrt.f64 / fdiv lowering without afn/arcp).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -1153,35 +1154,33 @@ __global__ __launch_bounds__(1024) void order_scatter_kernel(PrepArgs A) {
     }
   }
 }
-void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted) {
+void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted, bool scatter) {
   hipLaunchKernelGGL(order_count_kernel, dim3(1), dim3(1024), 0, st, a);
   if (counted) (void)hipEventRecord(counted, st);
-  hipLaunchKernelGGL(order_scatter_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (scatter) hipLaunchKernelGGL(order_scatter_kernel, dim3(1), dim3(1024), 0, st, a);
 }
 
-__global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, const uint64_t* skey,
-                                                          const int32_t* sidx, int32_t* ord) {
-  __shared__ uint64_t k[GSORT_MAX];
-  __shared__ int32_t v[GSORT_MAX];
-  const int a = off[blockIdx.x], n = off[blockIdx.x + 1] - a, tid = threadIdx.x;
-  if (n <= 0 || n > GSORT_MAX) return;   // (larger groups: the host sorts with radix passes)
+// Sorts the n <= GSORT_MAX (key, task) pairs in LDS k / v by (key, task) ascending; on return
+// (after a barrier) v[0, n) holds the tasks in order. Block of 1024 threads, every one calling.
+__device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
+  const int tid = threadIdx.x;
   if (n <= 128) {
     // rank by counting: the keys (sort key, task index) are distinct, so an element's place is
     // the number of elements below it -- every thread scans the group's keys in LDS (broadcast
-    // reads), one barrier in all. (Quadratic: measured 57 us for a group of ~1000 at config 5,
-    // where the bitonic network below, 55 barrier stages, takes a few microseconds.)
-    for (int i = tid; i < n; i += blockDim.x) { k[i] = skey[a + i]; v[i] = sidx[a + i]; }
-    __syncthreads();
+    // reads). (Quadratic: measured 57 us for a group of ~1000 at config 5.)
+    int r = 0;
+    int32_t vi = 0;
     if (tid < n) {
       const uint64_t ki = k[tid];
-      const int32_t vi = v[tid];
-      int r = 0;
+      vi = v[tid];
       for (int j = 0; j < n; j++) {
         const uint64_t kj = k[j];
         r += (kj < ki || (kj == ki && v[j] < vi)) ? 1 : 0;
       }
-      ord[a + r] = vi;
     }
+    __syncthreads();
+    if (tid < n) v[r] = vi;
+    __syncthreads();
     return;
   }
   // Bitonic network over P = 2^ceil(log2 n) elements, element i = m * 1024 + tid in registers:
@@ -1197,9 +1196,10 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
 #pragma unroll
   for (int m = 0; m < EMAX; m++) {
     const int i = m * 1024 + tid;
-    rk[m] = (m < E && i < n) ? skey[a + i] : ~0ull;
-    rv[m] = (m < E && i < n) ? sidx[a + i] : 0x7fffffff;
+    rk[m] = (m < E && i < n) ? k[i] : ~0ull;
+    rv[m] = (m < E && i < n) ? v[i] : 0x7fffffff;
   }
+  __syncthreads();
   for (int size = 2; size <= P; size <<= 1) {
     int stride = size >> 1;
     if (stride >= 64) {
@@ -1221,6 +1221,7 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
 #pragma unroll
       for (int m = 0; m < EMAX; m++)
         if (m < E) { rk[m] = k[m * 1024 + tid]; rv[m] = v[m * 1024 + tid]; }
+      __syncthreads();
     }
     for (; stride > 0; stride >>= 1) {
 #pragma unroll
@@ -1242,13 +1243,125 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
 #pragma unroll
   for (int m = 0; m < EMAX; m++) {
     const int i = m * 1024 + tid;
-    if (m < E && i < n) ord[a + i] = rv[m];
+    if (m < E && i < n) v[i] = rv[m];
   }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, const uint64_t* skey,
+                                                          const int32_t* sidx, int32_t* ord) {
+  __shared__ uint64_t k[GSORT_MAX];
+  __shared__ int32_t v[GSORT_MAX];
+  const int a = off[blockIdx.x], n = off[blockIdx.x + 1] - a, tid = threadIdx.x;
+  if (n <= 0 || n > GSORT_MAX) return;   // (larger groups: the host sorts with radix passes)
+  for (int i = tid; i < n; i += blockDim.x) { k[i] = skey[a + i]; v[i] = sidx[a + i]; }
+  __syncthreads();
+  lds_sort_pairs(k, v, n);
+  for (int i = tid; i < n; i += blockDim.x) ord[a + i] = v[i];
+}
+
+// The grouped order of a round with few groups (G <= GCOMPACT_MAX, after order_count_kernel):
+// block g scans every task's group (T reads from L2, G of them in all), collects its own
+// (sort key, task) pairs in LDS by wave-aggregated cursors, fills their placement with -1,
+// sorts them (lds_sort_pairs) and writes the gathered rows at its group's offset (the counts
+// of the groups before it): processing order, caller order, demand rows, anchors, groups.
+// Replaces order_scatter + group_sort + gather_tasks (three launches, ~35 us per config-5
+// round). Block 0 also writes the zone tables. A group over GSORT_MAX tasks only fills its
+// placement: the host redoes the order with radix passes.
+__global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, GatherOut O) {
+  __shared__ uint64_t k[GSORT_MAX];
+  __shared__ int32_t v[GSORT_MAX];
+  __shared__ int32_t fill, base_s;
+  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const int T = A.T;
+  if (g == 0 && A.csum)
+    for (int i = tid; i < A.Z * A.Z; i += 1024) {
+      const int a = i / A.Z, z = i - a * A.Z;
+      A.csum[i] = A.cost[a * A.Z + z] + A.cost[z * A.Z + a];   // cost_aware.py:82,113
+      A.bsum[i] = A.bw[a * A.Z + z] + A.bw[z * A.Z + a];       // (:79,111)
+    }
+  if (tid < 64) {                             // the group's offset: counts of groups before it
+    int c = 0;
+    for (int q = lane; q < g; q += 64) c += A.off[q];
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+    if (lane == 0) { base_s = c; fill = 0; }
+  }
+  const int n = A.off[g];
+  const bool sortable = n <= GSORT_MAX;
+  __syncthreads();
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  constexpr int PB = 8;
+  for (int i0 = 0; i0 < T; i0 += 1024 * PB) {
+    int gv[PB];
+#pragma unroll
+    for (int u = 0; u < PB; u++) {
+      const int i = i0 + u * 1024 + tid;
+      gv[u] = i < T ? A.tg[i] : -1;
+    }
+    uint64_t key[PB];
+#pragma unroll
+    for (int u = 0; u < PB; u++) {
+      const int i = i0 + u * 1024 + tid;
+      key[u] = 0;
+      if (gv[u] == g && A.sort_tasks) {
+        const double nn = __builtin_sqrt(norm2_seq(A.dem[i], A.dem[(size_t)T + i],
+                                                   A.dem[2 * (size_t)T + i], A.dem[3 * (size_t)T + i]));
+        key[u] = ~(uint64_t)__double_as_longlong(nn);   // descending norm (as norm_keys_kernel)
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PB; u++) {
+      const int i = i0 + u * 1024 + tid;
+      const bool mine = gv[u] == g;
+      if (mine && A.placement) A.placement[i] = -1;
+      if (!sortable) continue;
+      const uint64_t bal = __ballot(mine);
+      int b = 0;
+      if (lane == 0 && bal) b = atomicAdd(&fill, __popcll(bal));
+      b = __shfl(b, 0);
+      if (mine) {
+        const int pos = b + __popcll(bal & below);
+        k[pos] = key[u];
+        v[pos] = i;
+      }
+    }
+  }
+  if (!sortable || n <= 0) return;
+  __syncthreads();
+  lds_sort_pairs(k, v, n);
+  const int a = base_s;
+  const int32_t anc = A.ganc[g];
+  for (int i = tid; i < n; i += 1024) {
+    const int p = a + i, t = v[i];
+    O.ord[p] = t;
+    if (O.order_out) O.order_out[p] = t;
+    double* o = O.dem_ord + (size_t)p * 4;
+    o[0] = A.dem[t]; o[1] = A.dem[(size_t)T + t]; o[2] = A.dem[2 * (size_t)T + t]; o[3] = A.dem[3 * (size_t)T + t];
+    O.anc_ord[p] = anc;
+    O.grp_ord[p] = g;
+  }
+}
+void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st) {
+  hipLaunchKernelGGL(group_sort_gather_kernel, dim3(a.G), dim3(1024), 0, st, a, o);
 }
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
                        int32_t* ord, hipStream_t st) {
   // (1024 threads, the block's element layout above assumes it)
   hipLaunchKernelGGL(group_sort_kernel, dim3(G), dim3(1024), 0, st, off, skey, sidx, ord);
+}
+
+// Small host tables to the device through their mapped pinned pages, as a kernel on the stream:
+// a hipMemcpyAsync from pinned memory goes through the copy engine, and the next kernel on the
+// stream then started ~20 us after the copy was queued (an idle GPU in between, default line).
+__global__ __launch_bounds__(256) void upload_kernel(const int4* src, int4* dst, int n16) {
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256) dst[i] = src[i];
+}
+void launch_upload(const void* src_mapped, void* dst, size_t bytes, hipStream_t st) {
+  const int n16 = (int)((bytes + 15) / 16);
+  if (n16 <= 0) return;
+  const int blocks = std::min(64, (n16 + 255) / 256);
+  hipLaunchKernelGGL(upload_kernel, dim3(blocks), dim3(256), 0, st,
+                     reinterpret_cast<const int4*>(src_mapped), reinterpret_cast<int4*>(dst), n16);
 }
 
 __global__ void iota_kernel(int32_t* out, int n) {

@@ -1,7 +1,9 @@
-"""GPU: the grouped processing order (order_prep_kernel + group_sort_kernel, pvt_kernels.hip)
-against the CPU restatement's, for group sizes on both sides of every sort path's threshold:
-rank by counting (<= 128 tasks), the bitonic network with 1-4 elements per thread in registers
-(129..4096) and the radix-pass fallback (> 4096 tasks in a group). Demands take few distinct
+"""GPU: the grouped processing order (launch_order_prep, group_sort_gather_kernel /
+group_sort_kernel, pvt_kernels.hip) against the CPU restatement's, for group sizes on both sides
+of every sort path's threshold: rank by counting (<= 128 tasks), the bitonic network with 1-4
+elements per thread in registers (129..4096) and the radix-pass fallback (> 4096 tasks in a
+group), on both grouped-order paths: the compacting sort-and-gather launch (at most GCOMPACT_MAX
+= 64 groups) and the scatter + sort + gather launches (more groups). Demands take few distinct
 values, so most sort keys tie and the task-index tie-break (the reference's stable sorts,
 scheduler/cost_aware.py:37-42) decides the order."""
 import numpy as np
@@ -15,8 +17,11 @@ pytestmark = pytest.mark.gpu
 EDGES = [1, 2, 63, 64, 65, 127, 128, 129, 255, 256, 257, 1000, 1023, 1024, 1025, 2047, 2048,
          2049, 3000, 4095, 4096]
 
+MANY = [int(x) for x in np.random.RandomState(5).randint(1, 300, size=100)]   # > GCOMPACT_MAX groups
 
-@pytest.mark.parametrize("sizes", [EDGES, [4097, 5, 300], [1500] * 7], ids=["edges", "radix", "even"])
+
+@pytest.mark.parametrize("sizes", [EDGES, [4097, 5, 300], [1500] * 7, MANY],
+                         ids=["edges", "radix", "even", "many"])
 @pytest.mark.parametrize("sort_tasks", [True, False])
 @pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_CA_FF])
 def test_grouped_order_matches_oracle(engine, mode, sort_tasks, sizes):
