@@ -132,6 +132,7 @@ struct RoundState {
   bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
   bool ffe = false;               // keyed rounds: first-fit zero-key epochs (ff_epoch)
   bool hmin_pre = false;          // the first epoch's host minima were queued by round_begin
+  bool stage_flag = false;        // the grouped order's counts are signalled by ctx->flag_host
   bool gathered = false;          // ... and group_sort_gather_kernel wrote the gathered order
   bool prep_fused = false;        // build_order's order_scatter_kernel filled placement / zone tables
   int ffe_skip = -1;              //   the group they could not start (the keyed path takes it)
@@ -203,6 +204,9 @@ struct pvt_ctx {
   size_t rmt_cap = 0;
   RoundState rs;
   int32_t* next_host = nullptr;   // pinned
+  int32_t* flag_host = nullptr;   // pinned word the grouped order's count kernel stores to
+  int32_t* flag_hdev = nullptr;   //   (its device address)
+  int32_t flag_seq = 0;
   void* gstage = nullptr;         // grouped order: counts, anchors, cost table (pinned)
   size_t gstage_cap = 0;
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
@@ -354,6 +358,8 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
       resident_init_attrs() != hipSuccess || lwalk_init_attrs() != hipSuccess ||
       hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->flag_host, sizeof(int32_t) * 16) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&ctx->flag_hdev, ctx->flag_host, 0) != hipSuccess ||
       hipHostMalloc((void**)&ctx->ep_host, sizeof(int32_t) * EP_WORDS) != hipSuccess ||
       hipHostGetDevicePointer((void**)&ctx->ep_hdev, ctx->ep_host, 0) != hipSuccess) {
     delete ctx;
@@ -393,6 +399,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->next_host) (void)hipHostFree(ctx->next_host);
+  if (ctx->flag_host) (void)hipHostFree(ctx->flag_host);
   if (ctx->ep_host) (void)hipHostFree(ctx->ep_host);
   if (ctx->gstage) (void)hipHostFree(ctx->gstage);
   if (ctx->hst) (void)hipHostFree(ctx->hst);
@@ -577,9 +584,31 @@ static double bytes_per_candidate(int mode) {
 // Processing order (a2). Grouped rounds take the optimistic path: group counts, offsets and the
 // pinned copies of counts / anchors / cost table, then the per-group sorts, all launched with no
 // synchronisation (*pending = true); the caller syncs once, later, and calls build_order_check.
+// Spin on the count kernel's flag (the staged counts are visible once it holds flag_seq). Every
+// 4096 polls the stream is queried: an idle stream with no flag is an error, never a hang.
+static int wait_stage_flag(pvt_ctx* ctx) {
+  volatile int32_t* f = ctx->flag_host;
+  for (uint32_t n = 1;; n++) {
+    if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == ctx->flag_seq) return PVT_OK;
+    if ((n & 4095) == 0) {
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == ctx->flag_seq) return PVT_OK;
+        return fail(ctx, PVT_EHIP, "grouped order: count kernel finished without its flag");
+      }
+      if (e != hipErrorNotReady) return fail(ctx, PVT_EHIP, "grouped order: %s", hipGetErrorString(e));
+    }
+  }
+}
+
 static int build_order_radix(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out);
-static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool* pending) {
+// hmin (or NULL): the frontier walk's host minima, written by the order's launch when it can
+// (*hmin_done); stage_flag: the host then waits on ctx->flag_host instead of ev_stage.
+static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool* pending,
+                       double* hmin = nullptr, bool* hmin_done = nullptr) {
   *pending = false;
+  if (hmin_done) *hmin_done = false;
+  ctx->rs.stage_flag = false;
   const int T = r->n_tasks;
   hipStream_t st = ctx->stream;
   ENSURE(ctx->ord, sizeof(int32_t) * T);
@@ -629,12 +658,20 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
       PrepArgs pa{r->task_group, T, G, r->group_anchor, r->cost, r->bw, r->n_zones, (int)nz2,
                   r->dem, r->sort_tasks ? 1 : 0, r->placement, P<int32_t>(ctx->goff), dcnt,
                   dcnt + G + 1, dcst, ca ? P<double>(ctx->csum) : nullptr,
-                  ca ? P<double>(ctx->bsum) : nullptr, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx)};
+                  ca ? P<double>(ctx->bsum) : nullptr, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx),
+                  nullptr, 0};
       R.prep_fused = true;
       if (G <= GCOMPACT_MAX) {   // counts, then one launch for the sorted, gathered order
-        launch_order_prep(pa, st, ctx->ev_stage, false);
+        // the host polls a flag the count kernel stores (no event: a marker on the stream cost
+        // ~5 us of idle GPU between the two launches)
+        pa.hflag = ctx->flag_hdev;
+        pa.seq = ++ctx->flag_seq;
+        R.stage_flag = true;
+        launch_order_prep(pa, st, nullptr, false);
         launch_group_sort_gather(pa, GatherOut{cur, P<double>(ctx->dem_ord), P<int32_t>(ctx->anc_ord),
-                                               P<int32_t>(ctx->grp_ord), r->order}, st);
+                                               P<int32_t>(ctx->grp_ord), r->order, r->avail,
+                                               r->n_hosts, hmin}, st);
+        if (hmin_done) *hmin_done = hmin != nullptr;
         R.gathered = true;
         R.ginfo = ca;
         *pending = true;
@@ -907,7 +944,16 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   ENSURE(ctx->dem_ord, sizeof(double) * 4 * T);
   ENSURE(ctx->anc_ord, sizeof(int32_t) * T);
   ENSURE(ctx->grp_ord, sizeof(int32_t) * T);
-  if ((rc = build_order(ctx, r, &R.ord, &pending))) return rc;
+  // a cost_aware best-fit round of epochs (epoch_groups) starts with the frontier walk's host
+  // minima: written by the grouped order's launch, or queued below, they are ready while the
+  // host waits for the grouped order's counts
+  const bool want_hmin = ctx->epochs && ctx->zwalk && r->mode == PVT_CA_BF && r->task_group &&
+                         r->n_groups >= 2 && T >= 2 && !r->rt_bw && Z <= ZMAX && world == 1;
+  if (want_hmin) ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+  bool hmin_done = false;
+  if ((rc = build_order(ctx, r, &R.ord, &pending, want_hmin ? P<double>(ctx->hmin) : nullptr,
+                        &hmin_done)))
+    return rc;
   if (!R.prep_fused) HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
   auto order_out = [&]() -> int {   // (the gather also writes the caller's order)
     launch_gather_tasks(r->dem, R.ord, r->task_group, r->group_anchor, T, P<double>(ctx->dem_ord),
@@ -922,18 +968,20 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
     if (!R.prep_fused)
       launch_zone_tables(r->cost, r->bw, Z, P<double>(ctx->csum), P<double>(ctx->bsum), st);
   }
-  // a cost_aware best-fit round of epochs (epoch_groups) starts with the frontier walk's host
-  // minima: queued now, they run while the host waits for the grouped order's counts
   R.hmin_pre = false;
-  if (ctx->epochs && ctx->zwalk && r->mode == PVT_CA_BF && r->task_group && r->n_groups >= 2 &&
-      T >= 2 && !r->rt_bw && Z <= ZMAX && world == 1) {
-    ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
-    Scope sc(ctx, PVT_K_OTHER, 0, 0);
-    launch_host_min(r->avail, H, 0, H, P<double>(ctx->hmin), st);
+  if (want_hmin) {
+    if (!hmin_done) {
+      Scope sc(ctx, PVT_K_OTHER, 0, 0);
+      launch_host_min(r->avail, H, 0, H, P<double>(ctx->hmin), st);
+    }
     R.hmin_pre = true;
   }
   if (pending) {   // the one synchronisation of the grouped order: counts, anchors, cost table
-    HIPCHK(hipEventSynchronize(ctx->ev_stage));
+    if (R.stage_flag) {
+      if ((rc = wait_stage_flag(ctx))) return rc;
+    } else {
+      HIPCHK(hipEventSynchronize(ctx->ev_stage));
+    }
     bool redo = false;
     if ((rc = build_order_check(ctx, r, &redo))) return rc;
     if (redo) {

@@ -434,6 +434,8 @@ struct PrepArgs {
   double* bsum;
   uint64_t* skey;
   int32_t* sidx;
+  int32_t* hflag;             // mapped pinned word, or NULL: order_count_kernel stores seq there
+  int32_t seq;                //   once the staged counts are visible to the host
 };
 // counted (optional): recorded once the counts are staged, before the scatter launch (scatter
 // = false: counts only, for launch_group_sort_gather)
@@ -448,6 +450,9 @@ struct GatherOut {
   int32_t* anc_ord;
   int32_t* grp_ord;
   int32_t* order_out;         // the caller's order, or NULL
+  const double* avail;        // hmin != NULL: the same launch also writes the host minima over
+  int H;                      //   [0, H) (host_min_kernel's ZW_MIN_PARTS partials, four per
+  double* hmin;               //   extra block of 1024 threads)
 };
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st);
 // bytes (rounded up to 16; both buffers 16-B aligned and that long) from mapped pinned memory

@@ -1088,6 +1088,12 @@ __global__ __launch_bounds__(1024) void order_count_kernel(PrepArgs A) {
   for (int i = t; i < G; i += 1024) A.hgan[i] = A.ganc[i];
   for (int i = t; i < A.nz2; i += 1024) A.hcst[i] = A.cost[i];
   __threadfence_system();
+  if (A.hflag) {                              // every thread's staged words, then the flag
+    __syncthreads();
+    if (t == 0) {
+      __hip_atomic_store(A.hflag, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 __global__ __launch_bounds__(1024) void order_scatter_kernel(PrepArgs A) {
@@ -1274,6 +1280,29 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   __shared__ int32_t fill, base_s;
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int T = A.T;
+  if (g >= A.G) {
+    // blocks past the groups: the frontier walk's host minima (host_min_kernel, pvt_zwalk.hip),
+    // four of its 256-thread blocks per block -- one launch less on the round's critical path
+    __shared__ double red[16][4];
+    const int vb = (g - A.G) * 4 + (tid >> 8), wave = tid >> 6;
+    double m[4] = {DINF, DINF, DINF, DINF};
+    for (int h = vb * 256 + (tid & 255); h < O.H; h += ZW_MIN_PARTS * 256)
+#pragma unroll
+      for (int r = 0; r < 4; r++) m[r] = fmin(m[r], O.avail[(size_t)r * O.H + h]);
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      for (int off = 32; off > 0; off >>= 1) m[r] = fmin(m[r], __shfl_xor(m[r], off));
+      if (lane == 0) red[wave][r] = m[r];
+    }
+    __syncthreads();
+    if ((tid & 255) < 4) {
+      const int r = tid & 255, w0 = (tid >> 8) * 4;
+      double x = red[w0][r];
+      for (int w = 1; w < 4; w++) x = fmin(x, red[w0 + w][r]);
+      O.hmin[vb * 4 + r] = x;
+    }
+    return;
+  }
   if (g == 0 && A.csum)
     for (int i = tid; i < A.Z * A.Z; i += 1024) {
       const int a = i / A.Z, z = i - a * A.Z;
@@ -1342,7 +1371,8 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   }
 }
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st) {
-  hipLaunchKernelGGL(group_sort_gather_kernel, dim3(a.G), dim3(1024), 0, st, a, o);
+  const int extra = o.hmin ? ZW_MIN_PARTS / 4 : 0;
+  hipLaunchKernelGGL(group_sort_gather_kernel, dim3(a.G + extra), dim3(1024), 0, st, a, o);
 }
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
                        int32_t* ord, hipStream_t st) {
