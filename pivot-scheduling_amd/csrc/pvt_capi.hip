@@ -256,6 +256,10 @@ template <class T>
 static T* P(Buf& b) { return reinterpret_cast<T*>(b.p); }
 
 // ---------------------------------------------------------------- profiling
+// Timing-only events: no system-scope fence when they complete (no cache writeback and
+// invalidate between the timed kernel and its neighbours; the marker of a default event cost
+// ~5 us of idle GPU per record on the default line).
+static constexpr unsigned PROFILE_EVENT_FLAGS = hipEventDisableSystemFence;
 static hipEvent_t take_event(pvt_ctx* ctx) {
   if (!ctx->evpool.empty()) {
     hipEvent_t e = ctx->evpool.back();
@@ -263,7 +267,7 @@ static hipEvent_t take_event(pvt_ctx* ctx) {
     return e;
   }
   hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
+  (void)hipEventCreateWithFlags(&e, PROFILE_EVENT_FLAGS);
   return e;
 }
 struct Scope {
@@ -432,7 +436,7 @@ extern "C" int pvt_set_profiling(pvt_ctx* ctx, int on) {
     (void)hipSetDevice(ctx->device);
     while (ctx->evpool.size() + 2 * ctx->pending.size() < EVPOOL_WARM) {
       hipEvent_t e = nullptr;
-      if (hipEventCreate(&e) != hipSuccess) break;
+      if (hipEventCreateWithFlags(&e, PROFILE_EVENT_FLAGS) != hipSuccess) break;
       (void)hipEventRecord(e, ctx->stream);
       ctx->evpool.push_back(e);
     }
@@ -520,12 +524,12 @@ extern "C" int pvt_debug_commit_stamps(pvt_ctx* ctx, uint64_t* out, int n) {
   if (!ctx || !out || n < 8) return PVT_EINVAL;
 #ifdef PVT_STAMPS
   if (!ctx->stamps) {
-    if (hipMalloc((void**)&ctx->stamps, 128) != hipSuccess) return PVT_ENOMEM;
-    (void)hipMemset(ctx->stamps, 0, 128);
-    std::memset(out, 0, sizeof(uint64_t) * std::min(n, 16));
+    if (hipMalloc((void**)&ctx->stamps, 256) != hipSuccess) return PVT_ENOMEM;
+    (void)hipMemset(ctx->stamps, 0, 256);
+    std::memset(out, 0, sizeof(uint64_t) * std::min(n, 32));
     return PVT_OK;
   }
-  if (hipMemcpy(out, ctx->stamps, sizeof(uint64_t) * std::min(n, 16), hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(out, ctx->stamps, sizeof(uint64_t) * std::min(n, 32), hipMemcpyDeviceToHost) != hipSuccess)
     return PVT_EHIP;
   return PVT_OK;
 #else
@@ -670,7 +674,7 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
         launch_order_prep(pa, st, nullptr, false);
         launch_group_sort_gather(pa, GatherOut{cur, P<double>(ctx->dem_ord), P<int32_t>(ctx->anc_ord),
                                                P<int32_t>(ctx->grp_ord), r->order, r->avail,
-                                               r->n_hosts, hmin}, st);
+                                               r->n_hosts, hmin, ctx->stamps}, st);
         if (hmin_done) *hmin_done = hmin != nullptr;
         R.gathered = true;
         R.ginfo = ca;

@@ -451,8 +451,9 @@ struct GatherOut {
   int32_t* grp_ord;
   int32_t* order_out;         // the caller's order, or NULL
   const double* avail;        // hmin != NULL: the same launch also writes the host minima over
-  int H;                      //   [0, H) (host_min_kernel's ZW_MIN_PARTS partials, four per
-  double* hmin;               //   extra block of 1024 threads)
+  int H;                      //   [0, H) (ZW_MIN_PARTS partials as host_min_kernel's, one per
+  double* hmin;               //   extra block)
+  uint64_t* stamps;           // diagnostic builds only (PVT_STAMPS): block 0's phases, [16, 20)
 };
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st);
 // bytes (rounded up to 16; both buffers 16-B aligned and that long) from mapped pinned memory

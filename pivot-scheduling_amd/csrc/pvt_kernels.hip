@@ -1229,7 +1229,8 @@ __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
         if (m < E) { rk[m] = k[m * 1024 + tid]; rv[m] = v[m * 1024 + tid]; }
       __syncthreads();
     }
-    for (; stride > 0; stride >>= 1) {
+    // (waves whose elements are all padding, i >= P, only ever pair with padding: they skip)
+    for (; stride > 0 && (tid & ~63) < P; stride >>= 1) {
 #pragma unroll
       for (int m = 0; m < EMAX; m++) {
         if (m >= E) continue;
@@ -1266,6 +1267,19 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
   for (int i = tid; i < n; i += blockDim.x) ord[a + i] = v[i];
 }
 
+#ifdef PVT_STAMPS
+__device__ __forceinline__ uint64_t gstamp() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define GSTAMP(k) do { if (g == 0 && tid == 0 && O.stamps) { const uint64_t t_ = gstamp(); gph[k] = t_ - gtl; gtl = t_; } } while (0)
+#else
+#define GSTAMP(k) do {} while (0)
+#endif
+
 // The grouped order of a round with few groups (G <= GCOMPACT_MAX, after order_count_kernel):
 // block g scans every task's group (T reads from L2, G of them in all), collects its own
 // (sort key, task) pairs in LDS by wave-aggregated cursors, fills their placement with -1,
@@ -1280,26 +1294,41 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   __shared__ int32_t fill, base_s;
   const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const int T = A.T;
+#ifdef PVT_STAMPS
+  uint64_t gph[4] = {0, 0, 0, 0}, gtl = 0;
+  if (g == 0 && tid == 0) gtl = gstamp();
+#endif
   if (g >= A.G) {
-    // blocks past the groups: the frontier walk's host minima (host_min_kernel, pvt_zwalk.hip),
-    // four of its 256-thread blocks per block -- one launch less on the round's critical path
+    // blocks past the groups: the frontier walk's host minima, one of the ZW_MIN_PARTS partials
+    // per block (the walk reduces them all, so the partition is free: four hosts per thread per
+    // pass for loads in flight; a quarter as many blocks measured ~26 us against 8.8)
     __shared__ double red[16][4];
-    const int vb = (g - A.G) * 4 + (tid >> 8), wave = tid >> 6;
+    const int pb = g - A.G, wave = tid >> 6;
     double m[4] = {DINF, DINF, DINF, DINF};
-    for (int h = vb * 256 + (tid & 255); h < O.H; h += ZW_MIN_PARTS * 256)
+    constexpr int STEP = ZW_MIN_PARTS * 1024;
+    for (int h0 = pb * 1024 + tid; h0 < O.H; h0 += 4 * STEP) {
+      double x[4][4];
 #pragma unroll
-      for (int r = 0; r < 4; r++) m[r] = fmin(m[r], O.avail[(size_t)r * O.H + h]);
+      for (int j = 0; j < 4; j++) {
+        const int h = h0 + j * STEP;
+#pragma unroll
+        for (int r = 0; r < 4; r++) x[j][r] = h < O.H ? O.avail[(size_t)r * O.H + h] : DINF;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) m[r] = fmin(m[r], x[j][r]);
+    }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       for (int off = 32; off > 0; off >>= 1) m[r] = fmin(m[r], __shfl_xor(m[r], off));
       if (lane == 0) red[wave][r] = m[r];
     }
     __syncthreads();
-    if ((tid & 255) < 4) {
-      const int r = tid & 255, w0 = (tid >> 8) * 4;
-      double x = red[w0][r];
-      for (int w = 1; w < 4; w++) x = fmin(x, red[w0 + w][r]);
-      O.hmin[vb * 4 + r] = x;
+    if (tid < 4) {
+      double x = red[0][tid];
+      for (int w = 1; w < 16; w++) x = fmin(x, red[w][tid]);
+      O.hmin[pb * 4 + tid] = x;
     }
     return;
   }
@@ -1318,46 +1347,63 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   const int n = A.off[g];
   const bool sortable = n <= GSORT_MAX;
   __syncthreads();
+  GSTAMP(0);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr int PB = 8;
   for (int i0 = 0; i0 < T; i0 += 1024 * PB) {
+    // every task's group and (sort_tasks) demand loaded at once, before any is used: one load
+    // latency per batch instead of two (the demands of other groups' tasks are L2 reads)
     int gv[PB];
+    double dv[PB][4];
 #pragma unroll
     for (int u = 0; u < PB; u++) {
       const int i = i0 + u * 1024 + tid;
       gv[u] = i < T ? A.tg[i] : -1;
+      if (A.sort_tasks && i < T) {
+        dv[u][0] = A.dem[i]; dv[u][1] = A.dem[(size_t)T + i];
+        dv[u][2] = A.dem[2 * (size_t)T + i]; dv[u][3] = A.dem[3 * (size_t)T + i];
+      }
     }
     uint64_t key[PB];
 #pragma unroll
     for (int u = 0; u < PB; u++) {
-      const int i = i0 + u * 1024 + tid;
       key[u] = 0;
       if (gv[u] == g && A.sort_tasks) {
-        const double nn = __builtin_sqrt(norm2_seq(A.dem[i], A.dem[(size_t)T + i],
-                                                   A.dem[2 * (size_t)T + i], A.dem[3 * (size_t)T + i]));
+        const double nn = __builtin_sqrt(norm2_seq(dv[u][0], dv[u][1], dv[u][2], dv[u][3]));
         key[u] = ~(uint64_t)__double_as_longlong(nn);   // descending norm (as norm_keys_kernel)
       }
     }
+    // the wave's matches of the whole batch take ONE cursor add (an LDS atomic and its return
+    // per 1024 tasks serialised the 16 waves: 24k cycles for the scan at config 5)
+    uint64_t bal[PB];
+    int tot = 0;
 #pragma unroll
     for (int u = 0; u < PB; u++) {
       const int i = i0 + u * 1024 + tid;
       const bool mine = gv[u] == g;
       if (mine && A.placement) A.placement[i] = -1;
-      if (!sortable) continue;
-      const uint64_t bal = __ballot(mine);
-      int b = 0;
-      if (lane == 0 && bal) b = atomicAdd(&fill, __popcll(bal));
-      b = __shfl(b, 0);
-      if (mine) {
-        const int pos = b + __popcll(bal & below);
+      bal[u] = __ballot(mine);
+      tot += __popcll(bal[u]);
+    }
+    if (!sortable || tot == 0) continue;
+    int b = 0;
+    if (lane == 0) b = atomicAdd(&fill, tot);
+    b = __shfl(b, 0);
+#pragma unroll
+    for (int u = 0; u < PB; u++) {
+      if (gv[u] == g) {
+        const int pos = b + __popcll(bal[u] & below);
         k[pos] = key[u];
-        v[pos] = i;
+        v[pos] = i0 + u * 1024 + tid;
       }
+      b += __popcll(bal[u]);
     }
   }
   if (!sortable || n <= 0) return;
   __syncthreads();
+  GSTAMP(1);
   lds_sort_pairs(k, v, n);
+  GSTAMP(2);
   const int a = base_s;
   const int32_t anc = A.ganc[g];
   for (int i = tid; i < n; i += 1024) {
@@ -1369,9 +1415,15 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
     O.anc_ord[p] = anc;
     O.grp_ord[p] = g;
   }
+#ifdef PVT_STAMPS
+  __syncthreads();
+  GSTAMP(3);
+  if (g == 0 && tid == 0 && O.stamps)
+    for (int q = 0; q < 4; q++) atomicAdd((unsigned long long*)&O.stamps[16 + q], (unsigned long long)gph[q]);
+#endif
 }
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st) {
-  const int extra = o.hmin ? ZW_MIN_PARTS / 4 : 0;
+  const int extra = o.hmin ? ZW_MIN_PARTS : 0;
   hipLaunchKernelGGL(group_sort_gather_kernel, dim3(a.G + extra), dim3(1024), 0, st, a, o);
 }
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,

@@ -290,7 +290,7 @@ class _Stager:
         st.placement, st.order = base + o_pl, base + o_or
         mt = None if r.mt_state is None else np.array(r.mt_state, dtype=np.uint32)
         st.mt_state = None if mt is None else mt.ctypes.data
-        eng._check(eng.lib.pvt_ctx_set_stream(eng.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        eng._set_stream(stream.cuda_stream)
         eng._check(eng.lib.pvt_place(eng.ctx, ctypes.addressof(st)))
         self.hbuf[:n_out].copy_(self.dbuf[:n_out], non_blocking=True)
         stream.synchronize()
@@ -336,11 +336,29 @@ class PlacementEngine:
             msg = self.lib.pvt_last_error(self.ctx)
             _abi.check_rc(rc, msg.decode() if msg else "")
 
+    def _bind_stream(self):
+        """Bind the context to torch's current stream on this device (the C call only when it
+        changed: torch's raw-stream query and one cached pointer, a few microseconds less per
+        resident call than a Stream object each time)."""
+        torch = _torch()
+        raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+        if raw is not None:
+            idx = self.device.index if isinstance(self.device, torch.device) else torch.device(self.device).index
+            ptr = raw(0 if idx is None else idx)
+        else:
+            ptr = torch.cuda.current_stream(self.device).cuda_stream
+        if ptr != getattr(self, "_bound_stream", None):
+            self._set_stream(ptr)
+
+    def _set_stream(self, ptr):
+        """pvt_ctx_set_stream, remembering the pointer for _bind_stream (every binding of this
+        context goes through here)."""
+        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(ptr)))
+        self._bound_stream = ptr
+
     def run(self, dr: DeviceRound):
         """Place a resident round (its avail / placement / order / mt are updated in place)."""
-        torch = _torch()
-        stream = torch.cuda.current_stream(self.device)
-        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._bind_stream()
         self._check(self.lib.pvt_place(self.ctx, ctypes.addressof(dr.struct)))
 
     def place(self, r: RoundArrays) -> RoundResult:
@@ -411,9 +429,7 @@ class PlacementEngine:
     # -- resident rounds and scenario batches (include/pivot_place.h, pvt_place_batch)
     def run_batch(self, batch: "DeviceBatch"):
         """Place every round of a resident batch in ONE launch (one workgroup per round)."""
-        torch = _torch()
-        stream = torch.cuda.current_stream(self.device)
-        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._bind_stream()
         if batch.mt_dev is not None:
             self._check(self.lib.pvt_place_batch_mt(self.ctx, ctypes.addressof(batch.structs),
                                                     len(batch), ctypes.c_void_p(batch.mt_dev.data_ptr())))
@@ -439,7 +455,7 @@ class PlacementEngine:
         device int32 row numbers (item c uses row item[c] of ``off``)."""
         torch = _torch()
         stream = torch.cuda.current_stream(self.device)
-        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._set_stream(stream.cuda_stream)
         a = _abi.pvt_anchor_args()
         a.n_items = off.numel() - 1 if item is None else item.numel()
         a.n_rows = 0 if item is None else off.numel() - 1
@@ -512,7 +528,7 @@ class PlacementEngine:
         for name, t in keep.items():
             setattr(m, name, t.data_ptr() if t.numel() else None)
         stream = torch.cuda.current_stream(dev)
-        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._set_stream(stream.cuda_stream)
         self._check(self.lib.pvt_meter(self.ctx, ctypes.addressof(m)))
         return {k: v[:S].cpu().numpy() for k, v in out.items()}
 
@@ -522,7 +538,7 @@ class PlacementEngine:
         per-rank package in bytes."""
         torch = _torch()
         stream = torch.cuda.current_stream(self.device)
-        self._check(self.lib.pvt_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)))
+        self._set_stream(stream.cuda_stream)
         mx = ctypes.c_int64()
         self._check(self.lib.pvt_shard_begin(self.ctx, ctypes.addressof(dr.struct), int(host_lo),
                                              int(host_hi), int(world), ctypes.byref(mx)))

@@ -58,7 +58,7 @@ def main():
     for k, t in d.items():
         setattr(m, k, t.data_ptr())
     stream = torch.cuda.current_stream(dev)
-    eng._check(eng.lib.pvt_ctx_set_stream(eng.ctx, ctypes.c_void_p(stream.cuda_stream)))
+    eng._set_stream(stream.cuda_stream)
     for _ in range(3):
         eng._check(eng.lib.pvt_meter(eng.ctx, ctypes.addressof(m)))
     torch.cuda.synchronize()
