@@ -1351,27 +1351,14 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   constexpr int PB = 8;
   for (int i0 = 0; i0 < T; i0 += 1024 * PB) {
-    // every task's group and (sort_tasks) demand loaded at once, before any is used: one load
-    // latency per batch instead of two (the demands of other groups' tasks are L2 reads)
+    // the groups of the batch's tasks (keys come after the collection: only the group's own
+    // tasks' demands are read and only they take the norm -- computed in the scan, every wave
+    // ran the fp64 norm for every batch whenever one lane matched: 21k of the kernel's 54k cycles)
     int gv[PB];
-    double dv[PB][4];
 #pragma unroll
     for (int u = 0; u < PB; u++) {
       const int i = i0 + u * 1024 + tid;
       gv[u] = i < T ? A.tg[i] : -1;
-      if (A.sort_tasks && i < T) {
-        dv[u][0] = A.dem[i]; dv[u][1] = A.dem[(size_t)T + i];
-        dv[u][2] = A.dem[2 * (size_t)T + i]; dv[u][3] = A.dem[3 * (size_t)T + i];
-      }
-    }
-    uint64_t key[PB];
-#pragma unroll
-    for (int u = 0; u < PB; u++) {
-      key[u] = 0;
-      if (gv[u] == g && A.sort_tasks) {
-        const double nn = __builtin_sqrt(norm2_seq(dv[u][0], dv[u][1], dv[u][2], dv[u][3]));
-        key[u] = ~(uint64_t)__double_as_longlong(nn);   // descending norm (as norm_keys_kernel)
-      }
     }
     // the wave's matches of the whole batch take ONE cursor add (an LDS atomic and its return
     // per 1024 tasks serialised the 16 waves: 24k cycles for the scan at config 5)
@@ -1391,15 +1378,22 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
     b = __shfl(b, 0);
 #pragma unroll
     for (int u = 0; u < PB; u++) {
-      if (gv[u] == g) {
-        const int pos = b + __popcll(bal[u] & below);
-        k[pos] = key[u];
-        v[pos] = i0 + u * 1024 + tid;
-      }
+      if (gv[u] == g) v[b + __popcll(bal[u] & below)] = i0 + u * 1024 + tid;
       b += __popcll(bal[u]);
     }
   }
   if (!sortable || n <= 0) return;
+  __syncthreads();
+  for (int q = tid; q < n; q += 1024) {       // the collected tasks' sort keys
+    uint64_t key = 0;
+    if (A.sort_tasks) {
+      const int i = v[q];
+      const double nn = __builtin_sqrt(norm2_seq(A.dem[i], A.dem[(size_t)T + i],
+                                                 A.dem[2 * (size_t)T + i], A.dem[3 * (size_t)T + i]));
+      key = ~(uint64_t)__double_as_longlong(nn);   // descending norm (as norm_keys_kernel)
+    }
+    k[q] = key;
+  }
   __syncthreads();
   GSTAMP(1);
   lds_sort_pairs(k, v, n);
