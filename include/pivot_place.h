@@ -132,7 +132,9 @@ int  pvt_ctx_set_stream(pvt_ctx* ctx, void* stream);
 int  pvt_place(pvt_ctx* ctx, const pvt_round* r);
 /* Profiling: on = 1 records HIP events around every kernel launch (adds a little host overhead:
  * ~30 us per config-5 round of ~15 launches); on = 2 only around the named kernels of
- * pvt_get_kernel_kstats (the kernel-class times of the other launches stay zero). */
+ * pvt_get_kernel_kstats (the kernel-class times of the other launches stay zero). The events are
+ * timing-only (hipEventDisableSystemFence) and come from a pool this call fills and records once
+ * (synchronising the context's stream), so a timed round creates none. */
 int  pvt_set_profiling(pvt_ctx* ctx, int on);
 int  pvt_reset_kstats(pvt_ctx* ctx);
 int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
