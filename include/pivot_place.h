@@ -93,7 +93,9 @@ typedef struct pvt_round {
   const uint32_t* tiebreak; /* [H] rank of the host-id string (PVT_VBP_BF), else NULL     */
   const int32_t* decay;  /* [H] max(len(h.tasks),1) (PVT_CA_FF host_decay), else NULL     */
   const double* cost;    /* [Z*Z] egress cost, cost[src*Z + dst] (ResourceMetadata.cost)  */
-  const double* bw;      /* [Z*Z] jittered bandwidth, bw[src*Z + dst]                     */
+  const double* bw;      /* [Z*Z] jittered bandwidth, bw[src*Z + dst]; every bw[a][z] +
+                            bw[z][a] > 0 (resources/network.py bandwidths are positive: the
+                            engine orders cost_aware scores >= +0 by their bits)           */
   const double* dem;     /* [4*T] task demand (cpus, mem, disk, gpus)                     */
   const int32_t* task_group;   /* [T] or NULL                                             */
   const int32_t* group_anchor; /* [G] anchor zone per group, or NULL                      */

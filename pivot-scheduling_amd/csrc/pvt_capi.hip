@@ -362,13 +362,14 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
       resident_init_attrs() != hipSuccess || lwalk_init_attrs() != hipSuccess ||
       hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess ||
-      hipHostMalloc((void**)&ctx->flag_host, sizeof(int32_t) * 16) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->flag_host, sizeof(int32_t) * 16, hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&ctx->flag_hdev, ctx->flag_host, 0) != hipSuccess ||
       hipHostMalloc((void**)&ctx->ep_host, sizeof(int32_t) * EP_WORDS) != hipSuccess ||
       hipHostGetDevicePointer((void**)&ctx->ep_hdev, ctx->ep_host, 0) != hipSuccess) {
     delete ctx;
     return PVT_EHIP;
   }
+  std::memset(ctx->flag_host, 0, sizeof(int32_t) * 16);   // (flag_seq starts at 0: no stale 1)
   ctx->stream = ctx->own;
   if (const char* e = getenv("PVT_OF_TASKS")) ctx->of_tasks = std::max(32, atoi(e));   // tuning
   if (const char* e = getenv("PVT_BAND")) ctx->band_min = std::max(0, atoi(e));       // A/B
@@ -594,6 +595,14 @@ static int wait_stage_flag(pvt_ctx* ctx) {
   volatile int32_t* f = ctx->flag_host;
   for (uint32_t n = 1;; n++) {
     if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == ctx->flag_seq) return PVT_OK;
+    __builtin_ia32_pause();                   // (yield the core's pipeline to its sibling thread)
+    if (n >= (1u << 18)) {
+      // a long wait (the GPU is shared or the round is large): stop spinning and block on the
+      // stream -- everything queued behind the count kernel runs without the host
+      HIPCHK(hipStreamSynchronize(ctx->stream));
+      if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == ctx->flag_seq) return PVT_OK;
+      return fail(ctx, PVT_EHIP, "grouped order: count kernel finished without its flag");
+    }
     if ((n & 4095) == 0) {
       const hipError_t e = hipStreamQuery(ctx->stream);
       if (e == hipSuccess) {

@@ -81,6 +81,15 @@ __device__ __forceinline__ double wave_max_d(double v) {
   for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
   return v;
 }
+// NaN-propagating maximum (fmax drops a NaN operand): the FF certificate (2') must fail on a NaN
+// capacity, whose frozen key would break the reference's sorted() order (cost_aware.py:116).
+__device__ __forceinline__ double nan_max(double a, double b) {
+  return (a != a || b <= a) ? a : b;
+}
+__device__ __forceinline__ double wave_nmax_d(double v) {
+  for (int off = 32; off > 0; off >>= 1) v = nan_max(v, __shfl_xor(v, off));
+  return v;
+}
 __device__ __forceinline__ double wave_min_d(double v) {
   for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
   return v;
@@ -281,12 +290,12 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   if (!KEYED)
     for (int k = tid; k < ZW_MINB; k += ZW_THREADS)
 #pragma unroll
-      for (int r = 0; r < 4; r++) ha[r] = FF ? fmax(ha[r], A.hmin[k * 4 + r]) : fmin(ha[r], A.hmin[k * 4 + r]);
+      for (int r = 0; r < 4; r++) ha[r] = FF ? nan_max(ha[r], A.hmin[k * 4 + r]) : fmin(ha[r], A.hmin[k * 4 + r]);
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     mx[r] = wave_max_d(mx[r]);
     mn[r] = wave_min_d(mn[r]);
-    ha[r] = FF ? wave_max_d(ha[r]) : wave_min_d(ha[r]);
+    ha[r] = FF ? wave_nmax_d(ha[r]) : wave_min_d(ha[r]);
   }
   if (lane == 0) {
 #pragma unroll
@@ -300,11 +309,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     for (int w = 1; w < ZW_WAVES; w++) {
       mx[r] = fmax(mx[r], S.red[w][r]);
       mn[r] = fmin(mn[r], S.red[w][4 + r]);
-      ha[r] = FF ? fmax(ha[r], S.red[w][8 + r]) : fmin(ha[r], S.red[w][8 + r]);
+      ha[r] = FF ? nan_max(ha[r], S.red[w][8 + r]) : fmin(ha[r], S.red[w][8 + r]);
     }
     mx[r] = fmax(mx[r], S.red[0][r]);
     mn[r] = fmin(mn[r], S.red[0][4 + r]);
-    ha[r] = FF ? fmax(ha[r], S.red[0][8 + r]) : fmin(ha[r], S.red[0][8 + r]);
+    ha[r] = FF ? nan_max(ha[r], S.red[0][8 + r]) : fmin(ha[r], S.red[0][8 + r]);
   }
   if (!KEYED && A.cmax && tid < 4) A.cmax[b * 4 + tid] = mx[tid];   // (the validation's fast path)
   bool sep = KEYED;
@@ -742,7 +751,8 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         if (!KEYED && lane < Z) {
           const double c = S.csum[a * Z + lane], bw = S.bsum[a * Z + lane];
           if (c == 0.0) ok = bw > 0.0;
-          else if (FF || !((U >> lane) & 1u)) ok = (c >= 0x1p-300) && (bw <= 0x1p300);
+          // (bw > 0: a negative bandwidth would give a negative key, ahead of every zero key)
+          else if (FF || !((U >> lane) & 1u)) ok = (c >= 0x1p-300) && (bw > 0.0) && (bw <= 0x1p300);
         }
         if (__ballot(!ok)) { failed = true; break; }
         const uint32_t am = KEYED ? ~0u : S.amask[a];   // keyed: every prefix host is zero-key

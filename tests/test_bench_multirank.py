@@ -28,6 +28,7 @@ def test_bench_two_ranks_gloo(shard, mode):
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
+    assert len(lines[0]) <= 8192
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["parity"] is True, res
     assert res["scaling"] == ("strong" if shard == "hosts" else "weak")
@@ -50,7 +51,28 @@ def test_bench_two_ranks_scenario_batch(mode):
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
+    assert len(lines[0]) <= 8192
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["parity"] is True and res["scaling"] == "weak", res
     assert res["config"]["scenarios_per_gpu"] == 64
     assert abs(res["value"] * res["ms_per_step"] * 1e-3 - 2 * 64 * 1e6) < 1e-3 * 2 * 64 * 1e6
+
+
+@pytest.mark.timeout(300)
+def test_bench_two_ranks_config4_line_fits():
+    """The N > 1 line as the driver's scaling runs print it: the default workload plus the
+    config-4 scenario line at its full per-GPU batch (--c4-batch 512, 1024 scenarios over two
+    ranks): one JSON line of at most 8 KB that parses, with the c4 extra's roofline and parity."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+           "--hosts", "20000", "--tasks", "300", "--steps", "2", "--warmup", "1",
+           "--cpu-baseline-seconds", "0", "--extra", "0", "--c4-batch", "512"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and len(lines[0]) <= 8192, out.stdout[-2000:]
+    res = json.loads(lines[0])
+    c4 = res["extra"]["c4_scenarios_ca_bf_x2"]
+    assert c4["parity"] is True and c4["n_gpus"] == 2 and c4["scenarios"] == 1024, c4
+    assert c4["value"] > 0 and "frac" in c4["roofline"], c4

@@ -85,3 +85,115 @@ def test_pmc_index_variant_keys(tmp_path, monkeypatch):
     import pmc_profile
     assert pmc_profile.base_name("void pvt::opp_commit_kernel(pvt::OppCommitArgs)") == "opp_commit_kernel"
     assert pmc_profile.base_name("void pvt::zwalk_kernel<true, false>(pvt::ZwalkArgs)") == "zwalk_kernel"
+
+
+def _full_out(world=1):
+    """A full-size bench.py result as main() builds it at N = world: every extra line with its
+    kernel times, long roofline / CPU-baseline dicts and notes (the sizes of BENCH_r04's)."""
+    long_note = "x" * 330
+    roof = {"kernel": "zwalk_kernel", "bound": "issue", "unit": "instructions/s (one workgroup)",
+            "traffic": 4168352.0, "walk_ms_per_step": 0.18233333333333, "critical_path_tasks": 1525,
+            "peak_basis": long_note, "achieved": 3.4123456789e8, "peak": 2.4e9,
+            "frac": 0.14212345678, "frac_one_wave": 0.56812345, "cycles_per_task": 291.2345678,
+            "latency_floor": {"peak_tasks_per_s": 4.8e7, "achieved_tasks_per_s": 8.37e6,
+                              "frac": 0.174}, "instructions_per_task": 40.712345678,
+            "pmc_source": "profiles/r05a/pmc_r05a_c5_ca_bf_loaded_zwalk_kernel.json",
+            "pmc_lib_sha256": "b" * 64, "issue_active_frac_pmc": 0.43712345,
+            "wait_frac_pmc": 0.515123, "waves_per_launch": 32.0,
+            "dominant_share_of_timed_kernels": 0.912345678}
+    cpu = {"value": 1.75123456789e9, "unit": "candidates/s", "cores": 16, "kind": "port",
+           "value_1thread": 1.6123456789e8, "sample": long_note}
+    kern = {"zwalk_kernel": 0.18212345, "epoch_validate_kernel": 0.0061234, "score_kernel": 0.1,
+            "merge_path_kernel": 0.2, "lwalk_kernel": 0.3}
+    extra = {}
+    tags = [] if world > 1 else (["c5_%s" % m for m in ("ca_ff", "opp", "vbp_ff", "vbp_bf")] + ["c5_ca_bf_loaded"]
+            + ["c3_%s" % m for m in bench.MODES] + ["c4_%s" % m for m in bench.MODES])
+    for t in tags:
+        extra[t] = {"value": 3.5123456789e13, "ms_per_step": 0.2912345678, "hosts": 1000000,
+                    "tasks": 10000, "steps": 5, "parity": True,
+                    "kernels_ms_per_step": {"score": 0.1, "merge": 0.2, "commit": 0.3, "other": 0.4},
+                    "kernel_ms_per_step": dict(kern),
+                    "roofline": dict(roof, pmc_source="profiles/r05a/pmc_r05a_%s_zwalk_kernel.json"
+                                     % t), "cpu_baseline": dict(cpu),
+                    "hbm_GBs_measured": 15.123456789, "hbm_frac_measured": 0.0019,
+                    "hbm_bytes_per_step": 4.1e6, "hbm_pmc_source": "profiles/r05a/x.json"}
+    for t in tags:
+        if t.startswith("c4"):
+            extra[t]["scenarios"] = 512
+    for t in ("c1_replay_cost_aware", "c2_replay_cost_aware", "c2_replay_opportunistic",
+              "c2_replay_vbp_ff", "c2_lockstep") if world == 1 else ():
+        extra[t] = {"workload": long_note, "rounds": 2145, "candidates": 84820000.0,
+                    "value": 42338040.15905987, "unit": "candidates/s", "seconds": 2.0033992995,
+                    "ms_per_round": 0.9339856874471256, "parity": True, "engine_seconds": 2.2397,
+                    "max_rounds_per_launch": 6, "cpu_1thread": {"seconds": 1.9, "value": 4.3e7},
+                    "cpu_baseline": dict(cpu), "note": long_note,
+                    "roofline": {"kernel": None, "bound": "round trip", "unit": "rounds/s",
+                                 "achieved": 1070.68, "peak": 33794.15, "frac": 0.0316824,
+                                 "traffic": None, "peak_basis": long_note}}
+    if world > 1:
+        extra["c4_scenarios_ca_bf_x%d" % world] = {
+            "workload": long_note, "value": 5.2e11 * world, "unit": "candidates/s",
+            "ms_per_step": 0.97123, "n_gpus": world, "scenarios": 512 * world,
+            "scenarios_per_gpu": 512, "hosts": 1000, "tasks": 1000, "steps": 5, "scaling": "weak",
+            "timing": long_note, "parity": True, "parity_scope": long_note,
+            "kernels_ms_per_step": {"score": 0.1}, "kernel_ms_per_step": dict(kern),
+            "roofline": dict(roof, kernel="resident_kernel", bound="valu",
+                             pmc_source="profiles/r05a/pmc_r05a_c4_ca_bf_resident_kernel.json")}
+    return {"metric": bench.METRIC, "value": 3.6617021276595e13, "unit": "candidates/s",
+            "n_gpus": world, "steps": 20, "warmup": 5, "ms_per_step": 0.2731234567,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8(d): trace demand rows, 20 locality.yml zones, seeded)",
+            "config": {"workload": "synthetic 1000000 hosts x 10000 ready tasks per round, 20 zones,"
+                                   " cost_aware best-fit, one independent scenario per GPU",
+                       "scenarios_per_gpu": 1, "hosts": 1000000, "tasks_per_round": 10000,
+                       "zones": 20, "policy": "ca_bf",
+                       "parallelism": "scenario-sharded x%d (no data-path collective)" % world,
+                       "dist_backend": "nccl" if world > 1 else None},
+            "roofline": dict(roof), "cpu_baseline": dict(cpu),
+            "kernels_ms_per_step": {"score": 0.0, "merge": 0.0, "commit": 0.18, "other": 0.05},
+            "kernel_ms_per_step": dict(kern), "walk_us_per_task": 0.0182,
+            "windows_per_step": 0, "refills_per_step": 0, "epochs_per_step": 1,
+            "segments_per_step": 20, "rejected_segments_per_step": 0,
+            "frontier_chains_per_step": 8, "list_chains_per_step": 0, "parity": True,
+            "hbm_GBs_measured": 15.26, "hbm_frac_measured": 0.0019, "hbm_bytes_per_step": 4.17e6,
+            "hbm_pmc_source": "profiles/r05a/pmc_r05a_c5_ca_bf_step.json", "extra": extra}
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_bench_line_fits_the_driver(world):
+    """The printed line stays under 8 KB with every extra (a 33 KB line went
+    unparsed) and keeps, per extra, value / time / parity / roofline / CPU baseline -- at the
+    full level, PMC source included."""
+    out = _full_out(world)
+    line = bench.compact_line(out, "gpurun_out/bench_full.json")
+    assert len(line) <= 8192 and "\n" not in line
+    res = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline", "parity", "hbm_GBs_measured"):
+        assert k in res, k
+    assert res["value"] == out["value"] and res["ms_per_step"] == out["ms_per_step"]
+    assert res["full_results"] == "gpurun_out/bench_full.json"
+    for k in ("kernel", "bound", "achieved", "peak", "frac", "traffic", "pmc_source"):
+        assert k in res["roofline"], k
+    assert set(res["extra"]) == set(out["extra"])
+    for tag, e in res["extra"].items():
+        assert e["parity"] is True and e["value"] > 0, tag
+        assert "frac" in e["roofline"], tag
+        if out["extra"][tag].get("roofline", {}).get("pmc_source"):
+            assert e["roofline"]["pmc_source"].startswith("r05a"), tag
+        if "cpu_baseline" in out["extra"][tag]:
+            assert e["cpu_baseline"]["value"] > 0 and e["cpu_baseline"]["cores"] == 16, tag
+    if world > 1:
+        c4 = res["extra"]["c4_scenarios_ca_bf_x%d" % world]
+        assert c4["n_gpus"] == world and c4["scenarios"] == 512 * world
+
+
+def test_bench_line_degrades_instead_of_growing():
+    """More extras than the line can hold: the cut gets coarser, the line stays parseable."""
+    out = _full_out(1)
+    for i in range(60):
+        out["extra"]["more_%d" % i] = dict(out["extra"]["c5_opp"])
+    line = bench.compact_line(out)
+    assert len(line) <= bench.LINE_MAX or len(json.loads(line)["extra"]) == len(out["extra"])
+    assert json.loads(line)["extra"]["more_59"]["parity"] is True

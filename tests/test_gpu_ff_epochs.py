@@ -113,3 +113,18 @@ def test_ff_epochs_hosts_fill_exactly(engine):
     r.dem[0, :] = 1.0
     r.dem[1, :] = 3932.16
     _check(engine, r)
+
+
+def test_ff_epochs_nan_capacity_blocks_the_certificate(engine):
+    """A NaN capacity (on a host outside every chain's zero-cost zones or not) gives that host a
+    NaN frozen key, so the zero-key-first order is no longer certain: the FF chain certificate
+    (2') must fail for every chain (NaN-propagating maxima), leaving the round to the keyed path,
+    and the result must equal the engine's epochs-off run. (How Python's sorted() orders a NaN
+    key is not pinned by any reference fixture, so the oracle is not the check here.)"""
+    r = synthetic.make_round(_abi.PVT_CA_FF, 20_000, 3000, seed=12)
+    r.avail[2, 7777] = np.nan
+    res, st = _place(engine, r)
+    off, st0 = _place(engine, r, epochs=False)
+    assert st["frontier_chains"] == 0, st
+    np.testing.assert_array_equal(res.placement, off.placement)
+    np.testing.assert_array_equal(res.order, off.order)

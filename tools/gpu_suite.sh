@@ -37,6 +37,7 @@ for s in "$@"; do
     st_opp)     run st_opp 150 python tools/commit_stamps.py 2 1000000 10000 ;;
     profbench)  mkdir -p gpurun_out/prof; run profbench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 $NB ;;
     pmc)        run pmc 1100 tools/pmc_all.sh "${PMC_TAG:-r04z}" ;;
+    pstep)      run pstep 400 python tools/pmc_step.py --tag "${PMC_TAG:-r05z}_c5_ca_bf" -- --mode ca_bf --hosts 1000000 --tasks 10000 ;;
     pmc_c4)     run pmc_c4 400 tools/pmc_all.sh "${PMC_TAG:-r04z}" c4 ;;
     *)          echo "unknown step $s"; exit 2 ;;
   esac

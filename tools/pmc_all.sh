@@ -4,7 +4,8 @@
 # only for the binary they were collected on). Run on the GPU box:  tools/pmc_all.sh TAG [SET..]
 # Sets: c5 (config 5, 1M x 10k, five policies), c5l (loaded config 5), c3 (100k x 1k), c4 (512
 # scenarios of 1000 x 1000, resident kernel); default all. Each tools/pmc_profile.py pass is its
-# own `rocprofv3 --pmc` child under a hard time limit (two passes per config).
+# own `rocprofv3 --pmc` child under a hard time limit (two passes per config for the kernels, two
+# for the whole step's FETCH_SIZE / WRITE_SIZE: tools/pmc_step.py).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 tag=${1:-r04}
 shift
@@ -19,6 +20,9 @@ prof() {   # prof NAME MODE HOSTS TASKS KEYSUFFIX KERNELS PROBE-ARGS...
   python tools/pmc_profile.py --tag "${tag}_${name}" --kernel "$kern" --secs 150 -- \
     tools/walk_probe.py --mode "$mode" --hosts "$h" --tasks "$t" --reps 2 "$@" \
     > "gpurun_out/pmc_${tag}_${name}.log" 2>&1
+  # the whole step's HBM bytes (every dispatch of a round; bench.py hbm_GBs_measured)
+  python tools/pmc_step.py --tag "${tag}_${name}" --secs 150 -- \
+    --mode "$mode" --hosts "$h" --tasks "$t" "$@" > "gpurun_out/pmcstep_${tag}_${name}.log" 2>&1
   for f in gpurun_out/pmc_${tag}_${name}_*.json; do
     [ -e "$f" ] && idx+=("$mode:$h:$t$suf:$f")
   done

@@ -9,6 +9,7 @@ stalls shows where). Exits non-zero if the engine reports an error (e.g. a hand-
 
 --batch B: the config-4 shape, B scenarios (seeds seed + s) in one pvt_place_batch per rep.
 --loaded 1: bench.py's loaded config-5 round (every host capped at 1 free cpu).
+--marker 1: a marker kernel before every rep (tools/pmc_step.py: HBM bytes of a whole step).
 The shapes are exactly those of bench.py's lines, so a PMC profile of the probe prices the
 launches bench.py times.
 """
@@ -34,6 +35,9 @@ def main():
     p.add_argument("--reps", type=int, default=2)
     p.add_argument("--batch", type=int, default=0)
     p.add_argument("--loaded", type=int, default=0)
+    p.add_argument("--marker", type=int, default=0,
+                   help="1: a one-element bitwise_not_ kernel before every rep (tools/pmc_step.py "
+                        "splits the dispatch list at these markers)")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -55,7 +59,10 @@ def main():
         dr, run = DeviceRound(r, eng.device), eng.run
     eng.reset_kstats()
     eng.set_profiling(True)
+    mark = torch.zeros(1, dtype=torch.int64, device=eng.device) if a.marker else None
     for rep in range(a.reps):
+        if mark is not None:
+            mark.bitwise_not_()
         t = time.perf_counter()
         dr.reset()
         run(dr)
