@@ -317,6 +317,20 @@ typedef struct pvt_ca_items {
   int32_t* status;             /* [2] out: groups formed, error kind                         */
 } pvt_ca_items;
 int  pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* items);
+/*
+ * Several independent drop-in rounds from HOST memory in one round trip: the lock-step driver's
+ * tick, where simulations running different policies each wait on one schedule() round
+ * (scheduler/__init__.py:100-103 once per simulation). rounds[i] is as for pvt_place_host, with
+ * items[i] its optional fused cost_aware grouping (items itself may be NULL); the policies may
+ * differ between rounds. Every round with tasks must fit the resident limits (n_hosts <=
+ * min(pvt_set_resident limit, PVT_RESIDENT_MAX_HOSTS), n_tasks <= PVT_RESIDENT_MAX_TASKS) --
+ * else PVT_EUNSUPPORTED before any work. One staging copy up, one launch for all rounds (one
+ * workgroup each), one copy back, one synchronisation. rcs[i] receives each round's own result
+ * (PVT_OK, or PVT_EINVAL with items[i]->status[1] set for a grouping error, its outputs then
+ * untouched); the call returns PVT_OK when the batch ran.
+ */
+int  pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_items* const* items,
+                          int32_t n_rounds, int32_t* rcs);
 
 /*
  * Meter aggregates of a batch of S scenarios (replaces the properties

@@ -139,14 +139,16 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
   __syncthreads();
 }
 
+// One round on this workgroup (R: its descriptor, in SGPRs). The MT19937 state of an
+// opportunistic round is read and written through R.mt_state (a device pointer in every
+// resident path: pvt_place_batch's upload, pvt_place_batch_mt's rows, pvt_place_host's stage).
 template <int MODE, int WAVES, int HPL>
-__global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) {
+__device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_round& R) {
   constexpr int NT = WAVES * WAVE;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool CA = (MODE == CA_FF || MODE == CA_BF);
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
   const ResLds Lo(A.Zb, A.Tpad);
-  const pvt_round R = reinterpret_cast<const pvt_round*>(A.rounds)[blockIdx.x];   // SGPRs
   const int H = R.n_hosts, T = R.n_tasks, Z = R.n_zones;
   const int tid = threadIdx.x, lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   MtWave mw;
   mw.buf = 0; mw.used = 0; mw.limit = 0;
   if (MODE == OPP) {
-    const uint32_t* src = A.mt + (size_t)blockIdx.x * 625;
+    const uint32_t* src = R.mt_state;
     for (int i = lane; i < 625; i += WAVE) mk[i] = src[i];
     __builtin_amdgcn_s_waitcnt(0xc07f);
   }
@@ -572,8 +574,30 @@ __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) 
   }
   if (MODE == OPP && wave == 0) {
     mt_unbuffer(mk, mw);
-    uint32_t* dst = A.mt + (size_t)blockIdx.x * 625;
+    uint32_t* dst = R.mt_state;
     for (int i = lane; i < 625; i += WAVE) dst[i] = mk[i];
+  }
+}
+
+template <int MODE, int WAVES, int HPL>
+__global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) {
+  const pvt_round R = reinterpret_cast<const pvt_round*>(A.rounds)[blockIdx.x];   // SGPRs
+  resident_round<MODE, WAVES, HPL>(A, R);
+}
+
+// A batch of rounds of different policies in one launch (pvt_place_host_batch: the lock-step
+// driver's tick of simulations running different schedulers): each workgroup branches on its
+// round's mode, a uniform (scalar) branch.
+template <int WAVES, int HPL>
+__global__ __launch_bounds__(WAVES * WAVE) void resident_mixed_kernel(ResidentArgs A) {
+  const pvt_round R = reinterpret_cast<const pvt_round*>(A.rounds)[blockIdx.x];   // SGPRs
+  switch (R.mode) {
+    case CA_FF: resident_round<CA_FF, WAVES, HPL>(A, R); break;
+    case CA_BF: resident_round<CA_BF, WAVES, HPL>(A, R); break;
+    case OPP: resident_round<OPP, WAVES, HPL>(A, R); break;
+    case VBP_FF: resident_round<VBP_FF, WAVES, HPL>(A, R); break;
+    case VBP_BF: resident_round<VBP_BF, WAVES, HPL>(A, R); break;
+    default: break;
   }
 }
 
@@ -626,6 +650,17 @@ void resident_shape(int maxH, int* waves, int* hpl) {
 
 void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a, hipStream_t st) {
   const size_t lds = resident_lds_bytes(a.Zb, a.Tpad);
+  if (mode == RES_MIXED) {             // (four waves; resident_shape with waves = 4)
+    const dim3 grid(n), block(4 * WAVE);
+    switch (hpl) {
+      case 1: hipLaunchKernelGGL((resident_mixed_kernel<4, 1>), grid, block, lds, st, a); break;
+      case 2: hipLaunchKernelGGL((resident_mixed_kernel<4, 2>), grid, block, lds, st, a); break;
+      case 4: hipLaunchKernelGGL((resident_mixed_kernel<4, 4>), grid, block, lds, st, a); break;
+      case 8: hipLaunchKernelGGL((resident_mixed_kernel<4, 8>), grid, block, lds, st, a); break;
+      default: hipLaunchKernelGGL((resident_mixed_kernel<4, 16>), grid, block, lds, st, a); break;
+    }
+    return;
+  }
   switch (mode) {
     case CA_FF: launch_mode<CA_FF>(waves, hpl, n, lds, a, st); break;
     case CA_BF: launch_mode<CA_BF>(waves, hpl, n, lds, a, st); break;
@@ -658,6 +693,12 @@ hipError_t resident_init_attrs() {
   if ((r = attrs_mode<OPP>(lds)) != hipSuccess) e = r;
   if ((r = attrs_mode<VBP_FF>(lds)) != hipSuccess) e = r;
   if ((r = attrs_mode<VBP_BF>(lds)) != hipSuccess) e = r;
+#define PVT_MIX_ATTR(HPL)                                                                        \
+  r = hipFuncSetAttribute((const void*)resident_mixed_kernel<4, HPL>,                            \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);                      \
+  if (r != hipSuccess) e = r;
+  PVT_MIX_ATTR(1) PVT_MIX_ATTR(2) PVT_MIX_ATTR(4) PVT_MIX_ATTR(8) PVT_MIX_ATTR(16)
+#undef PVT_MIX_ATTR
   return e;
 }
 

@@ -211,6 +211,7 @@ struct pvt_ctx {
   size_t gstage_cap = 0;
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
   void* hst = nullptr;            // pvt_place_host: pinned staging of a host-memory round
+  void* hst_map = nullptr;        //   (its device address: the copy kernels' side)
   size_t hst_cap = 0;
   Buf hdev;                       //   and its device copy
 };
@@ -2140,19 +2141,39 @@ static int ensure_pinned(pvt_ctx* ctx, size_t bytes) {
   const size_t want = std::max({bytes, ctx->hst_cap * 3 / 2, (size_t)1 << 16});
   if (ctx->hst) (void)hipHostFree(ctx->hst);
   ctx->hst = nullptr;
+  ctx->hst_map = nullptr;
   ctx->hst_cap = 0;
   if (hipHostMalloc(&ctx->hst, want) != hipSuccess) {
     ctx->hst = nullptr;
     return fail(ctx, PVT_ENOMEM, "hipHostMalloc(%zu) failed", want);
   }
+  if (hipHostGetDevicePointer(&ctx->hst_map, ctx->hst, 0) != hipSuccess) {
+    (void)hipHostFree(ctx->hst);
+    ctx->hst = ctx->hst_map = nullptr;
+    return fail(ctx, PVT_EHIP, "hipHostGetDevicePointer of the staging buffer failed");
+  }
   ctx->hst_cap = want;
   return PVT_OK;
 }
 
-extern "C" int pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* it) {
-  if (!ctx || !r) return PVT_EINVAL;
+// One host-memory round's place in the staging buffer (pvt_place_host, pvt_place_host_batch):
+// the out region (copied back: avail, placement, order, MT states, grouping status) of every
+// round of a call comes first, so the results return with ONE copy.
+struct HostSlot {
+  size_t av = 0, pl = 0, orr = 0, mt = 0, cmt = 0, st = 0;
+  size_t zone = 0, tb = 0, dc = 0, cost = 0, bw = 0, dem = 0, tg = 0, ga = 0, rt = 0;
+  size_t ti = 0, off = 0, ph = 0, ia = 0, sz = 0, zs = 0, mh = 0, az = 0, ab = 0, desc = 0;
+  int C = 0, S = 0, G = 0, GR = 0;
+  int64_t NP = 0;
+  bool resident = false, dev_mt = false;
+  pvt_round hr{};                     // the round as checked (grouped fields stand in with items)
+  pvt_round d{};                      // the device round (arrays in the staging buffer)
+};
+
+// Validation of a host round and its optional fused-grouping items (pvt_place_host's contract).
+static int check_host_round(pvt_ctx* ctx, const pvt_round* r, pvt_ca_items* it, HostSlot& s) {
   const bool ca = r->mode == PVT_CA_FF || r->mode == PVT_CA_BF;
-  const int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
+  const int T = r->n_tasks, Z = r->n_zones;
   if (it) {
     if (!ca) return fail(ctx, PVT_EINVAL, "pvt_ca_items need a cost_aware round");
     if (it->reserved != 0 || it->n_items < 0 || it->n_apps < 0 || it->n_pred < 0 || it->n_storage < 0)
@@ -2169,7 +2190,7 @@ extern "C" int pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* it) {
       return fail(ctx, PVT_EUNSUPPORTED, "fused grouping limits: T=%d (max %d), %d storages + %d "
                   "applications (max %d, at least one storage)", T, GRP_MAX_TASKS, it->n_storage,
                   it->n_apps, GRP_MAX_KEYS);
-    if (Z < 1 || Z > ZMAX) return fail(ctx, PVT_EINVAL, "bad sizes H=%d T=%d Z=%d", H, T, Z);
+    if (Z < 1 || Z > ZMAX) return fail(ctx, PVT_EINVAL, "bad sizes H=%d T=%d Z=%d", r->n_hosts, T, Z);
     for (int k = 0; k < it->n_storage; k++)
       if (it->storage_zone[k] < 0 || it->storage_zone[k] >= Z)
         return fail(ctx, PVT_EINVAL, "storage %d: zone %d outside [0, %d)", k, it->storage_zone[k], Z);
@@ -2180,134 +2201,283 @@ extern "C" int pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* it) {
       if (it->pred_off[c] < 0 || it->pred_off[c] > it->n_pred || (c && it->pred_off[c] < it->pred_off[c - 1]))
         return fail(ctx, PVT_EINVAL, "pred_off[%d] = %lld out of order or range", c, (long long)it->pred_off[c]);
   }
-  pvt_round hr = *r;                  // (the grouped fields stand in for the device's groups)
+  s.hr = *r;
   static const int32_t one = 0;
-  if (it) { hr.task_group = &one; hr.group_anchor = &one; hr.n_groups = 1; }
-  int rc = check_round(ctx, &hr);
+  if (it) { s.hr.task_group = &one; s.hr.group_anchor = &one; s.hr.n_groups = 1; }
+  int rc = check_round(ctx, &s.hr);
+  if (rc) return rc;
+  s.resident = T > 0 && resident_fits(&s.hr, ctx->resident_max);
+  s.C = it ? it->n_items : 0;
+  s.S = it ? it->n_storage : 0;
+  s.NP = it ? it->n_pred : 0;
+  s.G = it ? T : (r->task_group ? r->n_groups : 0);
+  s.GR = r->rt_bw ? std::max(r->task_group ? r->n_groups : 1, 1) : 0;
+  s.dev_mt = r->mt_state && s.resident;
+  return PVT_OK;
+}
+
+struct StageLayout {
+  size_t o = 0;
+  size_t take(size_t bytes) { const size_t at = o; o = (o + bytes + 255) / 256 * 256; return at; }
+};
+
+static void plan_out(StageLayout& L, HostSlot& s, const pvt_round* r, const pvt_ca_items* it) {
+  const int H = r->n_hosts, T = r->n_tasks;
+  s.av = L.take(32 * (size_t)H);
+  s.pl = L.take(4 * (size_t)T);
+  s.orr = L.take(4 * (size_t)T);
+  s.mt = r->mt_state ? L.take(4 * 625) : 0;
+  s.cmt = it ? L.take(4 * 625) : 0;
+  s.st = it ? L.take(16) : 0;
+}
+
+static void plan_in(StageLayout& L, HostSlot& s, const pvt_round* r, const pvt_ca_items* it) {
+  const int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
+  s.zone = L.take(4 * (size_t)H);
+  s.tb = r->tiebreak ? L.take(4 * (size_t)H) : 0;
+  s.dc = r->decay ? L.take(4 * (size_t)H) : 0;
+  s.cost = L.take(8 * (size_t)Z * Z);
+  s.bw = L.take(8 * (size_t)Z * Z);
+  s.dem = L.take(32 * (size_t)T);
+  s.tg = (it || r->task_group) ? L.take(4 * (size_t)T) : 0;
+  s.ga = (it || r->task_group) ? L.take(4 * (size_t)std::max(s.G, 1)) : 0;
+  s.rt = s.GR ? L.take(8 * (size_t)s.GR * H) : 0;
+  if (it) {
+    s.ti = L.take(4 * (size_t)T);
+    s.off = L.take(8 * (size_t)(s.C + 1));
+    s.ph = L.take(4 * (size_t)std::max<int64_t>(s.NP, 1));
+    s.ia = L.take(4 * (size_t)std::max(s.C, 1));
+    s.sz = L.take(4 * (size_t)s.S);
+    s.zs = L.take(4 * (size_t)Z);
+    s.mh = L.take(4 * (size_t)std::max(s.C, 1));
+    s.az = L.take(4 * (size_t)std::max(s.C, 1));
+    s.ab = L.take(16 + 4 * (size_t)std::max(s.C, 1));
+  }
+}
+
+// The round's inputs into the pinned buffer and its device descriptor (arrays in the device
+// copy of the buffer; a windowed opportunistic round's MT state stays a host pointer: opp_round
+// moves it itself).
+static void stage_round(char* hb, char* db, HostSlot& s, const pvt_round* r, const pvt_ca_items* it) {
+  const int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
+  auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) std::memcpy(hb + at, src, bytes); };
+  put(s.av, r->avail, 32 * (size_t)H);
+  if (r->mt_state) put(s.mt, r->mt_state, 4 * 625);
+  if (it) { put(s.cmt, it->mt_state, 4 * 625); std::memset(hb + s.st, 0, 16); }
+  put(s.zone, r->zone, 4 * (size_t)H);
+  if (r->tiebreak) put(s.tb, r->tiebreak, 4 * (size_t)H);
+  if (r->decay) put(s.dc, r->decay, 4 * (size_t)H);
+  put(s.cost, r->cost, r->cost ? 8 * (size_t)Z * Z : 0);
+  put(s.bw, r->bw, r->bw ? 8 * (size_t)Z * Z : 0);
+  put(s.dem, r->dem, 32 * (size_t)T);
+  if (r->task_group) { put(s.tg, r->task_group, 4 * (size_t)T); put(s.ga, r->group_anchor, 4 * (size_t)s.G); }
+  if (s.GR) put(s.rt, r->rt_bw, 8 * (size_t)s.GR * H);
+  if (it) {
+    put(s.ti, it->task_item, 4 * (size_t)T);
+    put(s.off, it->pred_off, 8 * (size_t)(s.C + 1));
+    put(s.ph, it->pred_host, 4 * (size_t)s.NP);
+    put(s.ia, it->item_app, 4 * (size_t)s.C);
+    put(s.sz, it->storage_zone, 4 * (size_t)s.S);
+    put(s.zs, it->zone_storage, 4 * (size_t)Z);
+    std::memset(hb + s.ab, 0, 16);
+  }
+  pvt_round& d = s.d;
+  d = s.hr;
+  d.avail = reinterpret_cast<double*>(db + s.av);
+  d.zone = reinterpret_cast<const int32_t*>(db + s.zone);
+  d.tiebreak = r->tiebreak ? reinterpret_cast<const uint32_t*>(db + s.tb) : nullptr;
+  d.decay = r->decay ? reinterpret_cast<const int32_t*>(db + s.dc) : nullptr;
+  d.cost = r->cost ? reinterpret_cast<const double*>(db + s.cost) : nullptr;
+  d.bw = r->bw ? reinterpret_cast<const double*>(db + s.bw) : nullptr;
+  d.dem = reinterpret_cast<const double*>(db + s.dem);
+  d.task_group = s.tg ? reinterpret_cast<const int32_t*>(db + s.tg) : nullptr;
+  d.group_anchor = s.ga ? reinterpret_cast<const int32_t*>(db + s.ga) : nullptr;
+  d.rt_bw = s.GR ? reinterpret_cast<const double*>(db + s.rt) : nullptr;
+  d.placement = reinterpret_cast<int32_t*>(db + s.pl);
+  d.order = reinterpret_cast<int32_t*>(db + s.orr);
+  d.mt_state = s.dev_mt ? reinterpret_cast<uint32_t*>(db + s.mt) : r->mt_state;
+  std::memcpy(hb + s.desc, &d, sizeof(pvt_round));
+}
+
+// The fused cost_aware grouping of an items round on the device (anchors, groups, draws); a
+// resident round's descriptor receives its group count.
+static int launch_items(pvt_ctx* ctx, char* db, const HostSlot& s, const pvt_ca_items* it, hipStream_t st) {
+  const int T = s.hr.n_tasks, H = s.hr.n_hosts, Z = s.hr.n_zones;
+  int32_t* ab = reinterpret_cast<int32_t*>(db + s.ab);
+  AnchorArgs k{s.C, H, s.NP, 0, 0, reinterpret_cast<const int64_t*>(db + s.off), nullptr,
+               reinterpret_cast<const int32_t*>(db + s.ph), nullptr, s.d.zone,
+               reinterpret_cast<int32_t*>(db + s.mh), reinterpret_cast<int32_t*>(db + s.az), ab,
+               ab + 4, ab + 1};
+  CaGroupArgs g{T, s.C, Z, s.S, it->n_apps, reinterpret_cast<const int32_t*>(db + s.ti),
+                reinterpret_cast<const int32_t*>(db + s.az), reinterpret_cast<const int32_t*>(db + s.ia),
+                reinterpret_cast<const int32_t*>(db + s.sz), reinterpret_cast<const int32_t*>(db + s.zs),
+                reinterpret_cast<uint32_t*>(db + s.cmt), reinterpret_cast<int32_t*>(db + s.tg),
+                reinterpret_cast<int32_t*>(db + s.ga), reinterpret_cast<int32_t*>(db + s.st),
+                s.resident ? &reinterpret_cast<pvt_round*>(db + s.desc)->n_groups : nullptr};
+  {
+    Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * (double)s.NP);
+    if (s.C > 0) launch_anchor(k, st);
+    launch_ca_groups(g, st);
+  }
+  HIPCHK(hipGetLastError());
+  return PVT_OK;
+}
+
+static int group_error(pvt_ctx* ctx, const char* hb, const HostSlot& s, pvt_ca_items* it) {
+  const int32_t* hs = reinterpret_cast<const int32_t*>(hb + s.st);
+  const int e = hs[1];
+  it->status[0] = hs[0];
+  it->status[1] = e;
+  if (!e) return PVT_OK;
+  return fail(ctx, PVT_EINVAL, "%s", e == 1 ? "a mode predecessor placement is not a host of the cluster" :
+              e == 2 ? "an anchor zone has no storage (get_storage_by_locality -> None)" :
+              "malformed anchor item lists");
+}
+
+static void return_round(const char* hb, const HostSlot& s, pvt_round* r, pvt_ca_items* it) {
+  const int H = r->n_hosts, T = r->n_tasks;
+  std::memcpy(r->avail, hb + s.av, 32 * (size_t)H);
+  std::memcpy(r->placement, hb + s.pl, 4 * (size_t)T);
+  std::memcpy(r->order, hb + s.orr, 4 * (size_t)T);
+  if (s.dev_mt) std::memcpy(r->mt_state, hb + s.mt, 4 * 625);
+  if (it) std::memcpy(it->mt_state, hb + s.cmt, 4 * 625);
+}
+
+// The staging buffer to the device and the results back as copy kernels over its mapped pages:
+// a hipMemcpyAsync from or to pinned memory goes through the copy engine, and the next kernel
+// on the stream started ~20 us after the copy was queued (launch_upload).
+static void stage_up(pvt_ctx* ctx, size_t bytes, hipStream_t st) {
+  launch_upload(ctx->hst_map, ctx->hdev.p, bytes, st);
+}
+static void stage_down(pvt_ctx* ctx, size_t bytes, hipStream_t st) {
+  launch_upload(ctx->hdev.p, ctx->hst_map, bytes, st);   // (the same copy kernel, device -> mapped)
+}
+
+extern "C" int pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* it) {
+  if (!ctx || !r) return PVT_EINVAL;
+  HostSlot s;
+  int rc = check_host_round(ctx, r, it, s);
   if (rc) return rc;
   ctx->rs.active = false;
-  if (T == 0) return PVT_OK;
+  if (r->n_tasks == 0) return PVT_OK;
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
-  const bool resident = resident_fits(&hr, ctx->resident_max);
-  const int C = it ? it->n_items : 0, S = it ? it->n_storage : 0;
-  const int64_t NP = it ? it->n_pred : 0;
-  const int G = it ? T : (r->task_group ? r->n_groups : 0);
-  const int GR = r->rt_bw ? std::max(r->task_group ? r->n_groups : 1, 1) : 0;
-  size_t o = 0;
-  auto take = [&](size_t bytes) { const size_t at = o; o = (o + bytes + 255) / 256 * 256; return at; };
-  // out region (copied back): avail, placement, order, MT states, grouping status
-  const size_t o_av = take(32 * (size_t)H), o_pl = take(4 * (size_t)T), o_or = take(4 * (size_t)T);
-  const size_t o_mt = r->mt_state ? take(4 * 625) : 0, o_cmt = it ? take(4 * 625) : 0;
-  const size_t o_st = it ? take(16) : 0;
-  const size_t n_out = o;
-  const size_t o_zone = take(4 * (size_t)H);
-  const size_t o_tb = r->tiebreak ? take(4 * (size_t)H) : 0, o_dc = r->decay ? take(4 * (size_t)H) : 0;
-  const size_t o_cost = take(8 * (size_t)Z * Z), o_bw = take(8 * (size_t)Z * Z);
-  const size_t o_dem = take(32 * (size_t)T);
-  const size_t o_tg = (it || r->task_group) ? take(4 * (size_t)T) : 0;
-  const size_t o_ga = (it || r->task_group) ? take(4 * (size_t)std::max(G, 1)) : 0;
-  const size_t o_rt = GR ? take(8 * (size_t)GR * H) : 0;
-  const size_t o_ti = it ? take(4 * (size_t)T) : 0, o_off = it ? take(8 * (size_t)(C + 1)) : 0;
-  const size_t o_ph = it ? take(4 * (size_t)std::max<int64_t>(NP, 1)) : 0;
-  const size_t o_ia = it ? take(4 * (size_t)std::max(C, 1)) : 0, o_sz = it ? take(4 * (size_t)S) : 0;
-  const size_t o_zs = it ? take(4 * (size_t)Z) : 0, o_mh = it ? take(4 * (size_t)std::max(C, 1)) : 0;
-  const size_t o_az = it ? take(4 * (size_t)std::max(C, 1)) : 0;
-  const size_t o_ab = it ? take(16 + 4 * (size_t)std::max(C, 1)) : 0;
-  const size_t o_desc = take(sizeof(pvt_round));
-  if ((rc = ensure_pinned(ctx, o))) return rc;
-  ENSURE(ctx->hdev, o);
+  StageLayout L;
+  plan_out(L, s, r, it);
+  const size_t n_out = L.o;
+  plan_in(L, s, r, it);
+  s.desc = L.take(sizeof(pvt_round));
+  if ((rc = ensure_pinned(ctx, L.o))) return rc;
+  ENSURE(ctx->hdev, L.o);
   char* hb = static_cast<char*>(ctx->hst);
   char* db = static_cast<char*>(ctx->hdev.p);
-  auto put = [&](size_t at, const void* src, size_t bytes) { if (bytes) std::memcpy(hb + at, src, bytes); };
-  put(o_av, r->avail, 32 * (size_t)H);
-  if (r->mt_state) put(o_mt, r->mt_state, 4 * 625);
-  if (it) { put(o_cmt, it->mt_state, 4 * 625); std::memset(hb + o_st, 0, 16); }
-  put(o_zone, r->zone, 4 * (size_t)H);
-  if (r->tiebreak) put(o_tb, r->tiebreak, 4 * (size_t)H);
-  if (r->decay) put(o_dc, r->decay, 4 * (size_t)H);
-  put(o_cost, r->cost ? r->cost : nullptr, r->cost ? 8 * (size_t)Z * Z : 0);
-  put(o_bw, r->bw ? r->bw : nullptr, r->bw ? 8 * (size_t)Z * Z : 0);
-  put(o_dem, r->dem, 32 * (size_t)T);
-  if (r->task_group) { put(o_tg, r->task_group, 4 * (size_t)T); put(o_ga, r->group_anchor, 4 * (size_t)G); }
-  if (GR) put(o_rt, r->rt_bw, 8 * (size_t)GR * H);
-  if (it) {
-    put(o_ti, it->task_item, 4 * (size_t)T);
-    put(o_off, it->pred_off, 8 * (size_t)(C + 1));
-    put(o_ph, it->pred_host, 4 * (size_t)NP);
-    put(o_ia, it->item_app, 4 * (size_t)C);
-    put(o_sz, it->storage_zone, 4 * (size_t)S);
-    put(o_zs, it->zone_storage, 4 * (size_t)Z);
-    std::memset(hb + o_ab, 0, 16);
-  }
-  // the device round: arrays in the staging buffer (the MT state of a windowed opportunistic
-  // round stays a host pointer: opp_round moves it itself)
-  pvt_round d = hr;
-  d.avail = reinterpret_cast<double*>(db + o_av);
-  d.zone = reinterpret_cast<const int32_t*>(db + o_zone);
-  d.tiebreak = r->tiebreak ? reinterpret_cast<const uint32_t*>(db + o_tb) : nullptr;
-  d.decay = r->decay ? reinterpret_cast<const int32_t*>(db + o_dc) : nullptr;
-  d.cost = r->cost ? reinterpret_cast<const double*>(db + o_cost) : nullptr;
-  d.bw = r->bw ? reinterpret_cast<const double*>(db + o_bw) : nullptr;
-  d.dem = reinterpret_cast<const double*>(db + o_dem);
-  d.task_group = o_tg ? reinterpret_cast<const int32_t*>(db + o_tg) : nullptr;
-  d.group_anchor = o_ga ? reinterpret_cast<const int32_t*>(db + o_ga) : nullptr;
-  d.rt_bw = GR ? reinterpret_cast<const double*>(db + o_rt) : nullptr;
-  d.placement = reinterpret_cast<int32_t*>(db + o_pl);
-  d.order = reinterpret_cast<int32_t*>(db + o_or);
-  const bool dev_mt = r->mt_state && resident;
-  d.mt_state = dev_mt ? reinterpret_cast<uint32_t*>(db + o_mt) : r->mt_state;
-  std::memcpy(hb + o_desc, &d, sizeof(pvt_round));
-  HIPCHK(hipMemcpyAsync(db, hb, o, hipMemcpyHostToDevice, st));
-  if (it) {
-    int32_t* ab = reinterpret_cast<int32_t*>(db + o_ab);
-    AnchorArgs k{C, H, NP, 0, 0, reinterpret_cast<const int64_t*>(db + o_off), nullptr,
-                 reinterpret_cast<const int32_t*>(db + o_ph), nullptr, d.zone,
-                 reinterpret_cast<int32_t*>(db + o_mh), reinterpret_cast<int32_t*>(db + o_az), ab,
-                 ab + 4, ab + 1};
-    CaGroupArgs g{T, C, Z, S, it->n_apps, reinterpret_cast<const int32_t*>(db + o_ti),
-                  reinterpret_cast<const int32_t*>(db + o_az), reinterpret_cast<const int32_t*>(db + o_ia),
-                  reinterpret_cast<const int32_t*>(db + o_sz), reinterpret_cast<const int32_t*>(db + o_zs),
-                  reinterpret_cast<uint32_t*>(db + o_cmt), reinterpret_cast<int32_t*>(db + o_tg),
-                  reinterpret_cast<int32_t*>(db + o_ga), reinterpret_cast<int32_t*>(db + o_st),
-                  resident ? &reinterpret_cast<pvt_round*>(db + o_desc)->n_groups : nullptr};
-    {
-      Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * (double)NP);
-      if (C > 0) launch_anchor(k, st);
-      launch_ca_groups(g, st);
-    }
-    HIPCHK(hipGetLastError());
-  }
-  int32_t* hst_status = reinterpret_cast<int32_t*>(hb + o_st);
-  auto group_error = [&]() -> int {
-    const int e = hst_status[1];
-    it->status[0] = hst_status[0];
-    it->status[1] = e;
-    if (!e) return PVT_OK;
-    return fail(ctx, PVT_EINVAL, "%s", e == 1 ? "a mode predecessor placement is not a host of the cluster" :
-                e == 2 ? "an anchor zone has no storage (get_storage_by_locality -> None)" :
-                "malformed anchor item lists");
-  };
-  if (resident) {
-    if ((rc = place_resident(ctx, &d, 1, db + o_desc, dev_mt ? reinterpret_cast<uint32_t*>(db + o_mt) : nullptr)))
+  stage_round(hb, db, s, r, it);
+  stage_up(ctx, L.o, st);
+  HIPCHK(hipGetLastError());
+  if (it && (rc = launch_items(ctx, db, s, it, st))) return rc;
+  if (s.resident) {
+    if ((rc = place_resident(ctx, &s.d, 1, db + s.desc, s.dev_mt ? reinterpret_cast<uint32_t*>(db + s.mt) : nullptr)))
       return rc;
   } else {
     if (it) {                         // the windowed engine plans groups on the host
-      HIPCHK(hipMemcpyAsync(hb + o_st, db + o_st, 16, hipMemcpyDeviceToHost, st));
+      launch_upload(db + s.st, static_cast<char*>(ctx->hst_map) + s.st, 16, st);
       HIPCHK(hipStreamSynchronize(st));
-      if ((rc = group_error())) return rc;
-      d.n_groups = std::max(hst_status[0], 1);
+      if ((rc = group_error(ctx, hb, s, it))) return rc;
+      s.d.n_groups = std::max(reinterpret_cast<const int32_t*>(hb + s.st)[0], 1);
     }
-    if ((rc = place_windowed(ctx, &d))) return rc;
+    if ((rc = place_windowed(ctx, &s.d))) return rc;
   }
-  HIPCHK(hipMemcpyAsync(hb, db, n_out, hipMemcpyDeviceToHost, st));
+  stage_down(ctx, n_out, st);
+  HIPCHK(hipGetLastError());
   HIPCHK(hipStreamSynchronize(st));
-  if (it && (rc = group_error())) return rc;
-  std::memcpy(r->avail, hb + o_av, 32 * (size_t)H);
-  std::memcpy(r->placement, hb + o_pl, 4 * (size_t)T);
-  std::memcpy(r->order, hb + o_or, 4 * (size_t)T);
-  if (dev_mt) std::memcpy(r->mt_state, hb + o_mt, 4 * 625);
-  if (it) std::memcpy(it->mt_state, hb + o_cmt, 4 * 625);
+  if (it && (rc = group_error(ctx, hb, s, it))) return rc;
+  return_round(hb, s, r, it);
+  return PVT_OK;
+}
+
+extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_items* const* items,
+                                    int32_t n_rounds, int32_t* rcs) {
+  if (!ctx) return PVT_EINVAL;
+  if (n_rounds < 0 || (n_rounds > 0 && (!rounds || !rcs)))
+    return fail(ctx, PVT_EINVAL, "bad host batch (%d rounds)", n_rounds);
+  ctx->rs.active = false;
+  if (n_rounds == 0) return PVT_OK;
+  std::vector<HostSlot> s(n_rounds);
+  int rc;
+  int maxH = 1, maxT = 1, maxZ = 1, mode0 = rounds[0].mode;
+  bool mixed = false;
+  for (int i = 0; i < n_rounds; i++) {
+    pvt_ca_items* it = items ? items[i] : nullptr;
+    rcs[i] = PVT_OK;
+    if ((rc = check_host_round(ctx, &rounds[i], it, s[i]))) {
+      char msg[64];
+      std::snprintf(msg, sizeof(msg), "host batch round %d: ", i);
+      ctx->err = msg + ctx->err;
+      return rc;
+    }
+    if (rounds[i].n_tasks > 0 && !s[i].resident)
+      return fail(ctx, PVT_EUNSUPPORTED, "host batch round %d: H=%d T=%d exceeds the resident limits "
+                  "(%d, %d): place it with pvt_place_host", i, rounds[i].n_hosts, rounds[i].n_tasks,
+                  std::min(ctx->resident_max, (int)PVT_RESIDENT_MAX_HOSTS), PVT_RESIDENT_MAX_TASKS);
+    if (rounds[i].n_tasks == 0) continue;
+    maxH = std::max(maxH, rounds[i].n_hosts);
+    maxT = std::max(maxT, rounds[i].n_tasks);
+    maxZ = std::max(maxZ, rounds[i].n_zones);
+    mixed |= rounds[i].mode != mode0;
+  }
+  HIPCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  // out regions of every round, then the inputs, then the descriptors of the rounds with tasks
+  // (contiguous: one resident launch takes them all)
+  StageLayout L;
+  for (int i = 0; i < n_rounds; i++)
+    if (rounds[i].n_tasks > 0) plan_out(L, s[i], &rounds[i], items ? items[i] : nullptr);
+  const size_t n_out = L.o;
+  for (int i = 0; i < n_rounds; i++)
+    if (rounds[i].n_tasks > 0) plan_in(L, s[i], &rounds[i], items ? items[i] : nullptr);
+  std::vector<int> live;
+  for (int i = 0; i < n_rounds; i++)
+    if (rounds[i].n_tasks > 0) live.push_back(i);
+  if (live.empty()) return PVT_OK;
+  const size_t o_desc = L.take(sizeof(pvt_round) * live.size());
+  for (size_t k = 0; k < live.size(); k++) s[live[k]].desc = o_desc + sizeof(pvt_round) * k;
+  if ((rc = ensure_pinned(ctx, L.o))) return rc;
+  ENSURE(ctx->hdev, L.o);
+  char* hb = static_cast<char*>(ctx->hst);
+  char* db = static_cast<char*>(ctx->hdev.p);
+  for (int i : live) stage_round(hb, db, s[i], &rounds[i], items ? items[i] : nullptr);
+  stage_up(ctx, L.o, st);
+  HIPCHK(hipGetLastError());
+  for (int i : live)
+    if (items && items[i] && (rc = launch_items(ctx, db, s[i], items[i], st))) return rc;
+  // one resident launch for every round (one workgroup each; mixed policies branch per
+  // workgroup), the MT states read and written through each descriptor's mt_state
+  {
+    int waves = mixed ? 4 : ctx->res_waves, hpl = 1;
+    resident_shape(maxH, &waves, &hpl);
+    int tpad = 64;
+    while (tpad < maxT) tpad <<= 1;
+    double cand = 0.0, bytes = 0.0;
+    for (int i : live) {
+      const double c = (double)rounds[i].n_tasks * rounds[i].n_hosts;
+      cand += c;
+      bytes += c * bytes_per_candidate(rounds[i].mode);
+    }
+    ResidentArgs ra{db + o_desc, nullptr, maxZ, tpad, ctx->stamps};
+    Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
+    launch_resident(mixed ? RES_MIXED : mode0, waves, hpl, (int)live.size(), ra, st);
+  }
+  HIPCHK(hipGetLastError());
+  ctx->windows = (int64_t)live.size();
+  ctx->refills = 0;
+  stage_down(ctx, n_out, st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(st));
+  for (int i : live) {
+    pvt_ca_items* it = items ? items[i] : nullptr;
+    if (it && (rcs[i] = group_error(ctx, hb, s[i], it))) continue;
+    return_round(hb, s[i], &rounds[i], it);
+  }
   return PVT_OK;
 }
 

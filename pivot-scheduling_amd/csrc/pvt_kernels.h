@@ -395,9 +395,10 @@ constexpr int RES_THREADS = 256;
 constexpr int RES_MAX_HPL = 16;
 constexpr int RES_MAX_HOSTS = RES_THREADS * RES_MAX_HPL;   // 4096
 constexpr int RES_MAX_TASKS = 4096;
+constexpr int RES_MIXED = -1;   // launch_resident: rounds of different policies (4 waves)
 struct ResidentArgs {
   const void* rounds;     // device copy of pvt_round[n] (device array pointers)
-  uint32_t* mt;           // [n][625] MT19937 states (PVT_OPP), else unused
+  uint32_t* mt;           // [n][625] MT19937 states (PVT_OPP; the kernel uses R.mt_state)
   int Zb;                 // zone-table stride in LDS: max n_zones of the batch
   int Tpad;               // power of two >= max n_tasks of the batch (sort network size)
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): block 0 wave 0 phase cycles

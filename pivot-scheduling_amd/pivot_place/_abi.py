@@ -108,6 +108,8 @@ class pvt_ca_items(ctypes.Structure):
 
 # pvt_place_host grouping error kinds (pvt_ca_items.status[1])
 GROUP_OK, GROUP_UNPLACED, GROUP_NO_STORAGE, GROUP_INVALID = 0, 1, 2, 3
+# fused grouping limits (csrc/pvt_groups.h): tasks of a round, storages + applications
+GRP_MAX_TASKS, GRP_MAX_KEYS = 16384, 8192
 
 # pvt_anchor anchor_zone codes (include/pivot_place.h)
 ANCHOR_NO_PREDS, ANCHOR_UNPLACED, ANCHOR_INVALID = -1, -2, -3

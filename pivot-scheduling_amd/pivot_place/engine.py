@@ -44,6 +44,9 @@ def load_library(path=None):
         "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_get_kernel_kstats": ([c_void_p, ctypes.c_char_p, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_place_host": ([c_void_p, ctypes.POINTER(_abi.pvt_round), ctypes.POINTER(_abi.pvt_ca_items)], c_int),
+        "pvt_place_host_batch": ([c_void_p, ctypes.POINTER(_abi.pvt_round),
+                                  ctypes.POINTER(ctypes.POINTER(_abi.pvt_ca_items)), ctypes.c_int32,
+                                  ctypes.POINTER(ctypes.c_int32)], c_int),
         "pvt_place_batch_mt": ([c_void_p, c_void_p, ctypes.c_int32, c_void_p], c_int),
         "pvt_set_window": ([c_void_p, c_int], c_int),
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
@@ -375,7 +378,9 @@ class PlacementEngine:
             st = self._stager = _Stager(self.device)
         return st.place(self, r)
 
-    def _place_host(self, r: RoundArrays, items):
+    @staticmethod
+    def _host_struct(r: RoundArrays):
+        """(pvt_round over r's host arrays, its RoundResult whose arrays the call fills)."""
         T = r.n_tasks
         s = _abi.fill_struct(r)
         avail = np.array(r.avail, dtype=np.float64, order="C")
@@ -389,9 +394,45 @@ class PlacementEngine:
             setattr(s, name, None if a is None else a.ctypes.data)
         s.placement, s.order = placement.ctypes.data, order.ctypes.data
         s.mt_state = None if mt is None else mt.ctypes.data
+        return s, RoundResult(placement=placement, order=order, avail=avail, mt_state=mt)
+
+    def _place_host(self, r: RoundArrays, items):
+        s, res = self._host_struct(r)
         rc = self.lib.pvt_place_host(self.ctx, ctypes.byref(s),
                                      None if items is None else ctypes.byref(items))
-        return (RoundResult(placement=placement, order=order, avail=avail, mt_state=mt), rc)
+        return res, rc
+
+    @staticmethod
+    def _ca_items(task_item, pred_off, pred_host, item_app, n_apps, storage_zone, zone_storage,
+                  mt_state):
+        """(pvt_ca_items, the arrays it points at -- kept alive by the caller -- , its MT19937
+        state array, its status array)."""
+        keep = (np.ascontiguousarray(task_item, dtype=np.int32),
+                np.ascontiguousarray(pred_off, dtype=np.int64),
+                np.ascontiguousarray(pred_host, dtype=np.int32),
+                np.ascontiguousarray(item_app, dtype=np.int32),
+                np.ascontiguousarray(storage_zone, dtype=np.int32),
+                np.ascontiguousarray(zone_storage, dtype=np.int32))
+        ti, off, ph, ia, sz, zs = keep
+        mt = np.array(mt_state, dtype=np.uint32)
+        status = np.zeros(2, dtype=np.int32)
+        it = _abi.pvt_ca_items()
+        it.n_items, it.n_apps, it.n_pred = ia.size, int(n_apps), ph.size
+        it.task_item, it.pred_off, it.pred_host = ti.ctypes.data, off.ctypes.data, ph.ctypes.data
+        it.item_app = ia.ctypes.data
+        it.n_storage, it.reserved = sz.size, 0
+        it.storage_zone, it.zone_storage = sz.ctypes.data, zs.ctypes.data
+        it.mt_state, it.status = mt.ctypes.data, status.ctypes.data
+        return it, keep, mt, status
+
+    def _ca_result(self, res, rc, mt, status):
+        if rc == _abi.PVT_EUNSUPPORTED:
+            return None
+        if rc != _abi.PVT_OK and status[1] in (_abi.GROUP_UNPLACED, _abi.GROUP_NO_STORAGE):
+            # the reference: cluster.get_host(placement).locality / storage.locality on None
+            raise AttributeError("'NoneType' object has no attribute 'locality'")
+        self._check(rc)
+        return res, int(status[0]), mt
 
     def place_cost_aware(self, r: RoundArrays, task_item, pred_off, pred_host, item_app, n_apps,
                          storage_zone, zone_storage, mt_state):
@@ -402,29 +443,58 @@ class PlacementEngine:
         when the round is beyond the fused path's limits (use anchor() + place()). Raises
         AttributeError where the reference does (a mode placement that is no host; an anchor
         zone without storage)."""
-        ti = np.ascontiguousarray(task_item, dtype=np.int32)
-        off = np.ascontiguousarray(pred_off, dtype=np.int64)
-        ph = np.ascontiguousarray(pred_host, dtype=np.int32)
-        ia = np.ascontiguousarray(item_app, dtype=np.int32)
-        sz = np.ascontiguousarray(storage_zone, dtype=np.int32)
-        zs = np.ascontiguousarray(zone_storage, dtype=np.int32)
-        mt = np.array(mt_state, dtype=np.uint32)
-        status = np.zeros(2, dtype=np.int32)
-        it = _abi.pvt_ca_items()
-        it.n_items, it.n_apps, it.n_pred = ia.size, int(n_apps), ph.size
-        it.task_item, it.pred_off, it.pred_host = ti.ctypes.data, off.ctypes.data, ph.ctypes.data
-        it.item_app = ia.ctypes.data
-        it.n_storage, it.reserved = sz.size, 0
-        it.storage_zone, it.zone_storage = sz.ctypes.data, zs.ctypes.data
-        it.mt_state, it.status = mt.ctypes.data, status.ctypes.data
+        it, _keep, mt, status = self._ca_items(task_item, pred_off, pred_host, item_app, n_apps,
+                                               storage_zone, zone_storage, mt_state)
         res, rc = self._place_host(r, it)
-        if rc == _abi.PVT_EUNSUPPORTED:
-            return None
-        if rc != _abi.PVT_OK and status[1] in (_abi.GROUP_UNPLACED, _abi.GROUP_NO_STORAGE):
-            # the reference: cluster.get_host(placement).locality / storage.locality on None
-            raise AttributeError("'NoneType' object has no attribute 'locality'")
-        self._check(rc)
-        return res, int(status[0]), mt
+        return self._ca_result(res, rc, mt, status)
+
+    def host_batch_fits(self, r: RoundArrays, ca_args=None):
+        """Whether place_host_batch takes this round (resident limits; the fused grouping's)."""
+        if r.n_tasks == 0:
+            return True
+        ok = r.n_hosts <= _abi.PVT_RESIDENT_MAX_HOSTS and r.n_tasks <= _abi.PVT_RESIDENT_MAX_TASKS
+        if ca_args is not None:
+            n_storage = len(ca_args[5])
+            ok = ok and r.n_tasks <= _abi.GRP_MAX_TASKS and 1 <= n_storage and \
+                n_storage + int(ca_args[4]) <= _abi.GRP_MAX_KEYS
+        return ok
+
+    def place_host_batch(self, reqs):
+        """Independent drop-in rounds, possibly of different policies, in ONE round trip
+        (pvt_place_host_batch). ``reqs``: (RoundArrays, ca_args) pairs, ca_args None or the
+        arguments of place_cost_aware after the round. Returns, per request, what place() or
+        place_cost_aware() would return -- or the exception that call would raise (instances
+        of Exception, returned, not raised). Every round must satisfy host_batch_fits()."""
+        n = len(reqs)
+        if n == 0:
+            return []
+        structs = (_abi.pvt_round * n)()
+        items = (ctypes.POINTER(_abi.pvt_ca_items) * n)()
+        outs, keep = [], []
+        for i, (r, ca) in enumerate(reqs):
+            s, res = self._host_struct(r)
+            structs[i] = s
+            if ca is None:
+                items[i] = ctypes.POINTER(_abi.pvt_ca_items)()
+                outs.append((res, None))
+            else:
+                it, k, mt, status = self._ca_items(*ca)
+                keep.append((it, k))
+                items[i] = ctypes.pointer(it)
+                outs.append((res, (mt, status)))
+        rcs = (ctypes.c_int32 * n)()
+        self._check(self.lib.pvt_place_host_batch(self.ctx, structs, items, n, rcs))
+        out = []
+        for i, (res, ca) in enumerate(outs):
+            if ca is None:
+                out.append(res)
+                continue
+            mt, status = ca
+            try:
+                out.append(self._ca_result(res, rcs[i], mt, status))
+            except Exception as e:     # noqa: BLE001 -- handed to the caller of this round
+                out.append(e)
+        return out
 
     # -- resident rounds and scenario batches (include/pivot_place.h, pvt_place_batch)
     def run_batch(self, batch: "DeviceBatch"):

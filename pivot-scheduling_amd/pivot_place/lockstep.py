@@ -8,8 +8,11 @@ thread, and every engine call a drop-in policy makes -- ``place`` (the round) an
 (cost_aware's mode-host anchors) -- goes through a per-simulation proxy that blocks. Whenever
 EVERY live simulation is blocked on the engine, the driver serves all waiting calls at once:
 
-* ``place``: the rounds of each policy mode go to ONE ``pvt_place_batch`` launch (one
-  workgroup per round, resident kernel) when they fit it; larger rounds go to ``pvt_place``;
+* ``place`` / ``place_cost_aware``: every waiting round -- whatever the simulations' policies,
+  cost_aware rounds with their grouping fused -- goes to ONE ``pvt_place_host_batch`` (one
+  staging copy each way, one resident launch with a workgroup per round) when it fits the
+  resident limits; larger rounds go to ``pvt_place_host`` alone. (An engine without the host
+  batch -- the CPU restatement in tests -- gets one ``place_batch`` per policy mode.)
 * ``anchor``: all items of all simulations in ONE ``pvt_anchor`` call (each simulation's host
   indices offset into one concatenated zone table).
 
@@ -51,6 +54,11 @@ class SimEngine:
     def anchor(self, off, lst, zone, inst_host=None):
         return self._driver._call(self._sim, "anchor", (off, lst, zone, inst_host))
 
+    def place_cost_aware(self, r, *ca_args):
+        """The fused cost_aware round (PlacementEngine.place_cost_aware): None when the engine
+        has no fused path or the round is beyond it (the policy then uses anchor + place)."""
+        return self._driver._call(self._sim, "place_ca", (r,) + tuple(ca_args))
+
 
 class LockstepDriver:
     """Runs simulations side by side and batches their engine calls (module docstring).
@@ -64,7 +72,8 @@ class LockstepDriver:
         self._pending = []
         self._live = 0
         self.stats = {"batches": 0, "place_calls": 0, "place_launches": 0, "anchor_calls": 0,
-                      "anchor_launches": 0, "max_rounds_per_launch": 0, "serve_s": 0.0}
+                      "anchor_launches": 0, "max_rounds_per_launch": 0, "serve_s": 0.0,
+                      "host_batch_rounds": 0, "fused_rounds": 0}
 
     # -------------------------------------------------------------- simulation side
     def _call(self, sim, kind, args):
@@ -121,7 +130,7 @@ class LockstepDriver:
         t = time.perf_counter()
         self.stats["batches"] += 1
         anchors = [c for c in batch if c.kind == "anchor"]
-        places = [c for c in batch if c.kind == "place"]
+        places = [c for c in batch if c.kind in ("place", "place_ca")]
         if anchors:
             self._serve_anchors(anchors)
         if places:
@@ -170,11 +179,53 @@ class LockstepDriver:
             for c, _, _, _ in spans:
                 c.error, c.done = e, True
 
+    def _note_launch(self, rounds):
+        self.stats["place_launches"] += 1
+        self.stats["max_rounds_per_launch"] = max(self.stats["max_rounds_per_launch"], rounds)
+
     def _serve_places(self, calls):
+        """Every waiting round in ONE pvt_place_host_batch when the engine has it (whatever the
+        policies; cost_aware rounds with their fused grouping), the rest as before: rounds of
+        one policy mode per pvt_place_batch, larger rounds one by one."""
         self.stats["place_calls"] += len(calls)
-        by_mode = {}
+        eng = self.engine
+        batched, rest = [], []
         for c in calls:
+            ca = c.args[1:] if c.kind == "place_ca" else None
+            if hasattr(eng, "place_host_batch") and eng.host_batch_fits(c.args[0], ca):
+                batched.append(c)
+            else:
+                rest.append(c)
+        for k in range(0, len(batched), self.max_batch):
+            part = batched[k:k + self.max_batch]
+            try:
+                res = eng.place_host_batch([(c.args[0], c.args[1:] if c.kind == "place_ca" else None)
+                                            for c in part])
+                for c, x in zip(part, res):
+                    if isinstance(x, Exception):
+                        c.error = x
+                    else:
+                        c.result = x
+            except Exception as e:             # noqa: BLE001 -- every caller sees the error
+                for c in part:
+                    c.error = e
+            for c in part:
+                c.done = True
+            self._note_launch(len(part))
+            self.stats["host_batch_rounds"] += len(part)
+            self.stats["fused_rounds"] += sum(c.kind == "place_ca" for c in part)
+        by_mode = {}
+        for c in rest:
             r = c.args[0]
+            if c.kind == "place_ca":           # beyond the batch: the fused call alone, if any
+                if hasattr(eng, "place_cost_aware"):
+                    try:
+                        c.result = eng.place_cost_aware(*c.args)
+                    except Exception as e:     # noqa: BLE001
+                        c.error = e
+                    self.stats["place_launches"] += 1
+                c.done = True
+                continue
             fits = (r.n_tasks > 0 and r.n_hosts <= _abi.PVT_RESIDENT_MAX_HOSTS
                     and r.n_tasks <= _abi.PVT_RESIDENT_MAX_TASKS)
             if fits:
@@ -198,6 +249,4 @@ class LockstepDriver:
                         c.error = e
                 for c in part:
                     c.done = True
-                self.stats["place_launches"] += 1
-                self.stats["max_rounds_per_launch"] = max(self.stats["max_rounds_per_launch"],
-                                                          len(part))
+                self._note_launch(len(part))

@@ -35,7 +35,7 @@ def test_bench_two_ranks_gloo(shard, mode):
     assert res["value"] > 0 and res["config"]["dist_backend"] == "gloo"
     c4 = res["extra"]["c4_scenarios_%s_x2" % mode]
     assert c4["parity"] is True and c4["n_gpus"] == 2 and c4["scenarios"] == 32, c4
-    assert c4["value"] > 0 and c4["scaling"] == "weak"
+    assert c4["value"] > 0 and "frac" in c4["roofline"]
 
 
 @pytest.mark.parametrize("mode", ["ca_bf", "vbp_bf", "opp"])

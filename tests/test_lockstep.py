@@ -51,17 +51,23 @@ def _lockstep_replay(engine):
     st = driver.stats
     assert st["place_calls"] > st["place_launches"], st     # rounds shared launches
     assert st["max_rounds_per_launch"] >= 2, st
-    assert st["anchor_calls"] > st["anchor_launches"], st
     return st
 
 
 def test_lockstep_replay_host_logic():
-    _lockstep_replay(BatchOracle())
+    st = _lockstep_replay(BatchOracle())
+    # (no fused path on the restatement: cost_aware rounds anchor first, in shared calls)
+    assert st["anchor_calls"] > st["anchor_launches"], st
 
 
 @pytest.mark.gpu
 def test_lockstep_replay_on_engine(engine):
-    _lockstep_replay(engine)
+    """On the GPU engine every tick's rounds -- four policies, cost_aware grouping fused -- go
+    to one pvt_place_host_batch: rounds of different policies share a launch."""
+    st = _lockstep_replay(engine)
+    assert st["host_batch_rounds"] == st["place_calls"], st
+    assert st["fused_rounds"] > 0 and st["anchor_calls"] == 0, st
+    assert st["max_rounds_per_launch"] >= 6, st
 
 
 def test_driver_propagates_errors():
