@@ -71,9 +71,11 @@ __device__ __forceinline__ uint64_t rstamp() {
 #endif
 
 // Dynamic LDS layout (bytes); the host sizes the launch with the same struct.
+constexpr int RW_SB = RES_MAX_TASKS / 64; // its suffix minima of the demands, per 64 positions
+
 struct ResLds {
-  int zt, ord, pl, u, cd, ci, mt, slot, total;
-  __host__ __device__ ResLds(int Zb, int Tpad) {
+  int zt, ord, pl, u, cd, ci, mt, slot, wa, wz, wm, ws, wk, total;
+  __host__ __device__ ResLds(int Zb, int Tpad, bool walk = false) {
     zt = 0;                                            // csum[Zb*Zb], bsum[Zb*Zb] f64
     ord = (16 * Zb * Zb + 15) & ~15;                   // processing order i32[Tpad]
     pl = ord + 4 * Tpad;                               // placement by position i32[Tpad]
@@ -85,11 +87,21 @@ struct ResLds {
     // fast posts i32[2][WAVES], then vbp best-fit s2 posts {u64, i32, i32}[2][WAVES]
     const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
+    // resident walk (after the sort, before the staging above): the round's hosts in LDS,
+    // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], per-chunk zero-score masks u64[16],
+    // suffix minima of the demands f64[RW_SB][4]
+    wa = u;
+    wz = wa + 32 * RW_MAXH;
+    wm = wz + 4 * RW_MAXH;
+    ws = wm + 8 * (RW_MAXH / 64);
+    wk = ws + 32 * RW_SB;                              // keyed first-fit: frozen keys f64[RW_MAXH]
+    const int rw_end = walk ? wk + 8 * RW_MAXH : 0;
     total = walk_end > sort_end ? walk_end : sort_end;
+    total = rw_end > total ? rw_end : total;
   }
 };
 
-size_t resident_lds_bytes(int Zb, int Tpad) { return (size_t)ResLds(Zb, Tpad).total; }
+size_t resident_lds_bytes(int Zb, int Tpad, bool walk) { return (size_t)ResLds(Zb, Tpad, walk).total; }
 
 __device__ __forceinline__ uint64_t dbits(double x) { return (uint64_t)__double_as_longlong(x); }
 
@@ -139,6 +151,227 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
   __syncthreads();
 }
 
+// ---- the resident walk: one wave places the round's tasks in order over its hosts in LDS
+// First-fit-shaped policies take, per task, the LOWEST-INDEX host of a "zero" class that fits:
+//   vbp first-fit (fit >=) and unsorted cost_aware first-fit (fit >): any fitting host;
+//   cost_aware best-fit: a fitting host of score exactly 0 -- zero-cost zone pair or exact fit
+//     (the fast winner of the 4-wave path above, with its "risky" rule: a fitting host whose
+//     score might underflow to 0 below the winner, or no zero-score host at all, stops the walk);
+//   keyed cost_aware first-fit: a strictly fitting host of frozen key exactly +0 (they lead the
+//     sorted host order in index order); none anywhere stops the walk.
+// Wave 0 holds chunk p0 (64 hosts, host p0 * 64 + lane) in registers -- the first chunk any
+// remaining task can still fit (suffix minima of the demands per 64 positions; capacities only
+// fall, so a chunk that cannot fit the componentwise least remaining demand never will) -- and
+// nearly every task finds its winner there with one fit test and a ballot, no barrier and no
+// memory access on its path; otherwise the later chunks are scanned in LDS. The other waves wait
+// at the closing barrier. Returns the first position the walk did not decide (T: all); the
+// 4-wave path goes on from there on the walked capacities.
+// Keyed first-fit: the frozen keys of the group in progress stay in LDS (wk) with the group
+// (*kgrp), so a walk that stops inside a group hands the 4-wave path the keys of its start.
+template <int MODE, int NT>
+__device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, const int32_t* ord,
+                             int32_t* pl, const double* csum, const double* bsum, bool has_groups,
+                             bool keyed, int* kgrp) {
+  constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
+  __shared__ int s_stop, s_kgrp;
+  const int T = R.n_tasks, H = R.n_hosts, Z = R.n_zones;
+  const int tid = threadIdx.x, lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* wa = reinterpret_cast<double*>(smem + Lo.wa);      // [4][RW_MAXH]
+  int32_t* wz = reinterpret_cast<int32_t*>(smem + Lo.wz);
+  uint64_t* wm = reinterpret_cast<uint64_t*>(smem + Lo.wm);  // keyed: zero-key hosts per chunk
+  double* ws = reinterpret_cast<double*>(smem + Lo.ws);      // [RW_SB][4]
+  double* wk = reinterpret_cast<double*>(smem + Lo.wk);      // [RW_MAXH]
+  for (int h = tid; h < H; h += NT) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) wa[r * RW_MAXH + h] = R.avail[(size_t)r * H + h];
+    wz[h] = R.zone[h];
+  }
+  const int nsb = (T + 63) >> 6;
+  for (int blk = wave; blk < nsb; blk += NT / WAVE) {
+    double m[4] = {DINF, DINF, DINF, DINF};
+    const int i = blk * 64 + lane;
+    if (i < T) {
+      const int t = ord[i];
+#pragma unroll
+      for (int r = 0; r < 4; r++) m[r] = R.dem[(size_t)r * T + t];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      for (int off = 32; off > 0; off >>= 1) m[r] = fmin(m[r], __shfl_xor(m[r], off));
+      if (lane == 0) ws[blk * 4 + r] = m[r];
+    }
+  }
+  __syncthreads();
+  if (tid < 4)
+    for (int blk = nsb - 2; blk >= 0; blk--) ws[blk * 4 + tid] = fmin(ws[blk * 4 + tid], ws[(blk + 1) * 4 + tid]);
+  __syncthreads();
+  if (wave == 0) {
+    const int nch = (H + 63) >> 6;
+    int p0 = 0;
+    double ra0, ra1, ra2, ra3;
+    int32_t rz = 0;
+    bool rv = false;
+    auto load_chunk = [&](int c) {
+      const int q = c * 64 + lane;
+      rv = q < H;
+      const int qq = rv ? q : 0;
+      ra0 = wa[qq]; ra1 = wa[RW_MAXH + qq]; ra2 = wa[2 * RW_MAXH + qq]; ra3 = wa[3 * RW_MAXH + qq];
+      rz = wz[qq];
+    };
+    auto store_chunk = [&](int c) {
+      const int q = c * 64 + lane;
+      if (rv) { wa[q] = ra0; wa[RW_MAXH + q] = ra1; wa[2 * RW_MAXH + q] = ra2; wa[3 * RW_MAXH + q] = ra3; }
+    };
+    load_chunk(0);
+    // (cost_aware) zones of score 0 for the current anchor, and the safe zones: bw in (0, 2^300]
+    // and c == 0 or c in [2^-300, inf) -- as the 4-wave path's zmask / rmask
+    uint32_t zc_z = 0, sf_z = 0;
+    int cur_anc = -1, cur_grp = -1;
+    uint64_t rkm = 0;                          // keyed: zero-key lanes of chunk p0
+    // the task records of a 64-position batch in lanes (the next batch's loads in flight)
+    auto rec = [&](int b, double (&d)[4], int& anc, int& grp) {
+      const int i = b * 64 + lane;
+      const int t = i < T ? ord[i] : 0;
+#pragma unroll
+      for (int r = 0; r < 4; r++) d[r] = R.dem[(size_t)r * T + t];
+      grp = has_groups ? R.task_group[t] : 0;
+      anc = has_groups ? R.group_anchor[grp] : 0;
+    };
+    double nd[4];
+    int nanc, ngrp;
+    rec(0, nd, nanc, ngrp);
+    int p = 0;
+    bool stop = false;
+    for (int b = 0; b < nsb && !stop; b++) {
+      double td[4] = {nd[0], nd[1], nd[2], nd[3]};
+      const int tanc = nanc, tgrp = ngrp;
+      if (b + 1 < nsb) rec(b + 1, nd, nanc, ngrp);
+      const double mn0 = ws[b * 4 + 0], mn1 = ws[b * 4 + 1], mn2 = ws[b * 4 + 2], mn3 = ws[b * 4 + 3];
+      const int kn = min(64, T - b * 64);
+      for (int k = 0; k < kn; k++, p++) {
+        p = __builtin_amdgcn_readfirstlane(p);
+        p0 = __builtin_amdgcn_readfirstlane(p0);
+        const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
+        const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
+        if (MODE == CA_BF || MODE == CA_FF) {
+          const int a = readlane_i(tanc, k);
+          const int g = readlane_i(tgrp, k);
+          if (a != cur_anc) {
+            cur_anc = a;
+            bool zc = false, sf = false;
+            if (lane < Z) {
+              const double c = csum[a * Z + lane], bw = bsum[a * Z + lane];
+              zc = c == 0.0;
+              sf = bw > 0.0 && bw <= 0x1p+300 && (c == 0.0 || (c >= 0x1p-300 && c < DINF));
+            }
+            zc_z = (uint32_t)__ballot(zc);
+            sf_z = (uint32_t)__ballot(sf);
+            cur_grp = -1;                      // (keyed: the keys depend on the anchor too)
+          }
+          if (MODE == CA_FF && keyed && g != cur_grp) {
+            // frozen host keys of the group (cost_aware.py:104-119) on the capacities now: only
+            // whether each is exactly +0 matters here
+            cur_grp = g;
+            store_chunk(p0);
+            for (int c = 0; c < nch; c++) {
+              const int q = c * 64 + lane;
+              const bool v = q < H;
+              const int qq = v ? q : 0;
+              const double x0 = wa[qq], x1 = wa[RW_MAXH + qq], x2 = wa[2 * RW_MAXH + qq], x3 = wa[3 * RW_MAXH + qq];
+              const int z = wz[qq];
+              const double r = __builtin_sqrt(norm2_seq(x0, x1, x2, x3));
+              const double df = (R.decay && v) ? (double)R.decay[q] : 1.0;
+              const double key = (csum[a * Z + z] * df) / (r * bsum[a * Z + z]);
+              if (v) wk[q] = key;
+              const uint64_t m = __ballot(v && dbits(key) == 0);
+              if (lane == 0) wm[c] = m;
+              if (c == p0) rkm = m;
+            }
+          }
+        }
+        if (MODE == CA_BF && !(__builtin_fabs(d0) < DINF && __builtin_fabs(d1) < DINF &&
+                               __builtin_fabs(d2) < DINF && __builtin_fabs(d3) < DINF)) {
+          stop = true;                         // (a non-finite demand: the 4-wave path decides)
+          break;
+        }
+        // one chunk's candidates: zm = fitting hosts of the zero class, rk = risky fitting hosts
+        auto test = [&](double x0, double x1, double x2, double x3, int32_t z, bool v,
+                        uint64_t km, uint64_t& zm, uint64_t& rk) {
+          const bool f = v && fits<STRICT>(x0, x1, x2, x3, d0, d1, d2, d3);
+          bool zz = true, risky = false;
+          if (MODE == CA_BF) {
+            const double mx = fmax(fmax(x0 - d0, x1 - d1), fmax(x2 - d2, x3 - d3));
+            const bool sf = (sf_z >> z) & 1u, zc = (zc_z >> z) & 1u;
+            zz = sf && ((zc && mx <= 0x1p+500) || mx == 0.0);
+            risky = f && !zz && (!sf || !(mx >= 0x1p-300) || zc);
+          } else if (MODE == CA_FF && keyed) {
+            zz = (km >> lane) & 1ull;
+          }
+          zm = __ballot(f && zz);
+          rk = __ballot(risky);
+        };
+        int win = -1;                           // host index, -1 none, -2 stop
+        {
+          uint64_t zm, rk;
+          test(ra0, ra1, ra2, ra3, rz, rv, rkm, zm, rk);
+          while (zm == 0 && rk == 0 && p0 + 1 < nch &&
+                 !__ballot(rv && fits<STRICT>(ra0, ra1, ra2, ra3, mn0, mn1, mn2, mn3))) {
+            store_chunk(p0);                   // dead: move the register chunk on
+            ++p0;
+            load_chunk(p0);
+            if (MODE == CA_FF && keyed) rkm = rfl_u64(wm[p0]);
+            test(ra0, ra1, ra2, ra3, rz, rv, rkm, zm, rk);
+          }
+          if (zm != 0) {
+            const int w = __builtin_ctzll(zm);
+            if (rk & ((1ull << w) - 1)) {
+              win = -2;
+            } else {
+              if (lane == w) { ra0 -= d0; ra1 -= d1; ra2 -= d2; ra3 -= d3; }   // resc[h] -= d
+              win = p0 * 64 + w;
+            }
+          } else if (rk != 0) {
+            win = -2;
+          } else {
+            for (int c = p0 + 1; c < nch; c++) {
+              const int q = c * 64 + lane;
+              const bool v = q < H;
+              const int qq = v ? q : 0;
+              const double x0 = wa[qq], x1 = wa[RW_MAXH + qq], x2 = wa[2 * RW_MAXH + qq], x3 = wa[3 * RW_MAXH + qq];
+              const uint64_t km = (MODE == CA_FF && keyed) ? rfl_u64(wm[c]) : 0ull;
+              uint64_t zm2, rk2;
+              test(x0, x1, x2, x3, wz[qq], v, km, zm2, rk2);
+              if (zm2 != 0) {
+                const int w = __builtin_ctzll(zm2);
+                if (rk2 & ((1ull << w) - 1)) { win = -2; break; }
+                if (lane == w) {
+                  wa[q] = x0 - d0; wa[RW_MAXH + q] = x1 - d1; wa[2 * RW_MAXH + q] = x2 - d2;
+                  wa[3 * RW_MAXH + q] = x3 - d3;
+                }
+                win = c * 64 + w;
+                break;
+              }
+              if (rk2 != 0) { win = -2; break; }
+            }
+            // nothing fits: first-fit by index leaves the task waiting; the zero-class
+            // policies have a positive-score / positive-key winner only the 4-wave path finds
+            if (win == -1 && (MODE == CA_BF || (MODE == CA_FF && keyed))) win = -2;
+          }
+        }
+        win = __builtin_amdgcn_readfirstlane(win);
+        if (win == -2) { stop = true; break; }
+        if (win >= 0 && lane == 0) pl[p] = win;
+      }
+    }
+    store_chunk(p0);
+    if (lane == 0) { s_stop = p; s_kgrp = cur_grp; }
+  }
+  __syncthreads();
+  *kgrp = s_kgrp;
+  return s_stop;
+}
+
 // One round on this workgroup (R: its descriptor, in SGPRs). The MT19937 state of an
 // opportunistic round is read and written through R.mt_state (a device pointer in every
 // resident path: pvt_place_batch's upload, pvt_place_batch_mt's rows, pvt_place_host's stage).
@@ -148,7 +381,7 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool CA = (MODE == CA_FF || MODE == CA_BF);
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
-  const ResLds Lo(A.Zb, A.Tpad);
+  const ResLds Lo(A.Zb, A.Tpad, A.walk != 0);
   const int H = R.n_hosts, T = R.n_tasks, Z = R.n_zones;
   const int tid = threadIdx.x, lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -206,6 +439,24 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   }
   for (int i = tid; i < T; i += NT) R.order[i] = ord[i];
 
+  // first-fit-shaped rounds of up to RW_MAXH hosts: one wave walks them (resident_walk); this
+  // path takes over where it stops, on the walked capacities (and the keyed walk's group keys)
+  int p_start = 0, kgrp = -1;
+  constexpr bool WALKABLE = (MODE == CA_BF || MODE == CA_FF || MODE == VBP_FF);
+  if (WALKABLE && A.walk && H <= RW_MAXH && T > 0 && !(CA && R.rt_bw)) {
+    p_start = resident_walk<MODE, NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, keyed, &kgrp);
+    const double* wa = reinterpret_cast<const double*>(smem + Lo.wa);
+    const double* wk = reinterpret_cast<const double*>(smem + Lo.wk);
+#pragma unroll
+    for (int j = 0; j < HPL; j++) {
+      const int h = h0 + j;
+      if (h < H) {
+        a0[j] = wa[h]; a1[j] = wa[RW_MAXH + h]; a2[j] = wa[2 * RW_MAXH + h]; a3[j] = wa[3 * RW_MAXH + h];
+        if (MODE == CA_FF && keyed && kgrp >= 0) key[j] = wk[h];
+      }
+    }
+  }
+
   double* cd = reinterpret_cast<double*>(smem + Lo.cd);
   int32_t* c_anc = reinterpret_cast<int32_t*>(smem + Lo.ci);
   int32_t* c_grp = c_anc + RES_CHUNK;
@@ -230,8 +481,15 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   uint64_t tl = stw ? rstamp() : 0;
 #endif
   int cur_anc = -1, cur_grp = -1, cur_bgrp = -1;
+  if (MODE == CA_FF && keyed && p_start < T && kgrp >= 0) {
+    // the walk stopped inside group kgrp: its keys (frozen at the group start) are in key[]
+    cur_grp = kgrp;
+    zmask = 0;
+#pragma unroll
+    for (int j = 0; j < HPL; j++) zmask |= (dbits(key[j]) == 0 ? 1u : 0u) << j;
+  }
   const bool rt = (MODE == CA_FF || MODE == CA_BF) && R.rt_bw != nullptr;
-  for (int p0 = 0; p0 < T; p0 += RES_CHUNK) {
+  for (int p0 = p_start; p0 < T; p0 += RES_CHUNK) {
     const int n = min(RES_CHUNK, T - p0);
     __syncthreads();                      // the previous chunk (and the sort keys) are consumed
     {
@@ -649,7 +907,7 @@ void resident_shape(int maxH, int* waves, int* hpl) {
 }
 
 void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a, hipStream_t st) {
-  const size_t lds = resident_lds_bytes(a.Zb, a.Tpad);
+  const size_t lds = resident_lds_bytes(a.Zb, a.Tpad, a.walk != 0);
   if (mode == RES_MIXED) {             // (four waves; resident_shape with waves = 4)
     const dim3 grid(n), block(4 * WAVE);
     switch (hpl) {
@@ -686,7 +944,7 @@ static hipError_t attrs_mode(int lds) {
 }
 
 hipError_t resident_init_attrs() {
-  const int lds = (int)resident_lds_bytes(ZMAX, RES_MAX_TASKS);
+  const int lds = (int)resident_lds_bytes(ZMAX, RES_MAX_TASKS, true);
   hipError_t e = hipSuccess, r;
   if ((r = attrs_mode<CA_FF>(lds)) != hipSuccess) e = r;
   if ((r = attrs_mode<CA_BF>(lds)) != hipSuccess) e = r;

@@ -188,6 +188,7 @@ struct pvt_ctx {
   int t_epoch_plan = 1;           // PVT_EPOCH_PLAN: 0 = epoch chains by distinct zone only
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
+  int rwalk = 1;                  // PVT_RWALK=0: resident rounds without the one-wave walk (A/B)
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf bpos, bptouch;              // band lists: host -> sorted position, touched by position
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
@@ -375,6 +376,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_OF_TASKS")) ctx->of_tasks = std::max(32, atoi(e));   // tuning
   if (const char* e = getenv("PVT_BAND")) ctx->band_min = std::max(0, atoi(e));       // A/B
   if (const char* e = getenv("PVT_LWALK")) ctx->lwalk = atoi(e) != 0;                  // A/B
+  if (const char* e = getenv("PVT_RWALK")) ctx->rwalk = atoi(e) != 0;                  // A/B
   if (const char* e = getenv("PVT_SEGMENTS")) ctx->t_segments = std::max(1, atoi(e));  // tuning
   if (const char* e = getenv("PVT_BAND_SEGS")) ctx->t_band_segs = atoi(e);             // tuning
   if (const char* e = getenv("PVT_KEYED_SCAN")) ctx->t_keyed_scan = atoi(e) != 0;      // A/B
@@ -1944,6 +1946,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
   resident_shape(maxH, &waves, &hpl);
   int tpad = 64;
   while (tpad < maxT) tpad <<= 1;
+  const int rwalk = ctx->rwalk && maxH <= RW_MAXH ? 1 : 0;
   double cand = 0.0, bytes = 0.0;
   for (int i = 0; i < n; i++) {
     const double c = (double)rounds[i].n_tasks * rounds[i].n_hosts;
@@ -1951,7 +1954,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     bytes += c * bytes_per_candidate(mode);
   }
   if (desc_dev) {
-    ResidentArgs ra{desc_dev, mt_dev, maxZ, tpad, ctx->stamps};
+    ResidentArgs ra{desc_dev, mt_dev, maxZ, tpad, ctx->stamps, rwalk};
     {
       Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
       launch_resident(mode, waves, hpl, n, ra, st);
@@ -1994,7 +1997,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ctx->ev_rstage, st));
   ctx->rstage_busy = true;
-  ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad, ctx->stamps};
+  ResidentArgs ra{ctx->rdesc.p, mt, maxZ, tpad, ctx->stamps, rwalk};
   {
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mode, waves, hpl, n, ra, st);
@@ -2463,7 +2466,8 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
       cand += c;
       bytes += c * bytes_per_candidate(rounds[i].mode);
     }
-    ResidentArgs ra{db + o_desc, nullptr, maxZ, tpad, ctx->stamps};
+    ResidentArgs ra{db + o_desc, nullptr, maxZ, tpad, ctx->stamps,
+                    ctx->rwalk && maxH <= RW_MAXH ? 1 : 0};
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mixed ? RES_MIXED : mode0, waves, hpl, (int)live.size(), ra, st);
   }

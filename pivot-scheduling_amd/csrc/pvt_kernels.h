@@ -402,8 +402,10 @@ struct ResidentArgs {
   int Zb;                 // zone-table stride in LDS: max n_zones of the batch
   int Tpad;               // power of two >= max n_tasks of the batch (sort network size)
   uint64_t* stamps;       // diagnostic builds only (PVT_STAMPS): block 0 wave 0 phase cycles
+  int walk = 0;           // 1: rounds of <= RW_MAXH hosts start with the one-wave resident walk
 };
-size_t resident_lds_bytes(int Zb, int Tpad);
+constexpr int RW_MAXH = 1024;   // resident walk: hosts held in LDS
+size_t resident_lds_bytes(int Zb, int Tpad, bool walk);
 void resident_shape(int maxH, int* waves, int* hpl);
 void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a, hipStream_t st);
 hipError_t resident_init_attrs();

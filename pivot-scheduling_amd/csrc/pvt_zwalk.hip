@@ -182,56 +182,6 @@ __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, 
   }
 }
 
-// ---- closed-form copy counts (run_bulk pass 1)
-// A lane with capacity c takes copies of a demand d > 0 one after another while the residual
-// fits: s_0 = c, s_j = fl(s_{j-1} - d), copy j fits iff s_j >= 0 (best-fit, vbp first-fit) or
-// s_j > 0 (strict). fl is monotone, so s_j only falls and the copies a lane takes are the largest
-// j with s_j fitting. Instead of subtracting copy after copy, take j0 = floor(c / d) and decide
-// the fit of s_j for j around j0 from m = fma(-j, d, c) = the correctly rounded c - j d:
-//  * exact grid: if c and d are multiples of 2^e and c + cap d < 2^(e+53), every s_i is a
-//    multiple of 2^e below 2^(e+53), so every subtraction is exact and s_j = m exactly (the
-//    cpus of the trace: multiples of 0.5);
-//  * otherwise each of the j subtractions errs by at most 2^-53 of its result, all below
-//    |c| + j d, so |s_j - (c - j d)| <= j (|c| + j d) 2^-53 (+ j 2^-1075 for underflow), and
-//    |m - (c - j d)| is below that too: |m| > 2 E with E = j (|c| + j d) 2^-52 + j 2^-1070
-//    fixes the sign of s_j. A residual that close to 0 (about 1e-10 of the capacity) is
-//    "unknown" and the caller falls back to the sequential count.
-__device__ __forceinline__ int lsb_exp(double x) {       // exponent of the lowest set bit, x != 0
-  const uint64_t b = (uint64_t)__double_as_longlong(x);
-  const int ex = (int)((b >> 52) & 0x7ff);
-  const uint64_t man = b & 0xfffffffffffffull;
-  return ex == 0 ? -1074 + __builtin_ctzll(man) : ex - 1075 + __builtin_ctzll(man | (1ull << 52));
-}
-
-// Copies (<= cap) of d > 0 that capacity c takes, or -1 when rounding may decide it.
-template <bool STRICT>
-__device__ __forceinline__ int copies_of(double c, double d, int cap) {
-  const double lim = fma((double)cap, d, __builtin_fabs(c));   // >= |c| + cap d - rounding
-  const int e = min(c == 0.0 ? 1074 : lsb_exp(c), lsb_exp(d));
-  const bool exact = lim * (1.0 + 0x1p-50) < __builtin_ldexp(1.0, e + 53);
-  // f(j): 1 = s_j fits, 0 = it does not, -1 unknown (j >= 1)
-  auto f = [&](int j) -> int {
-    const double jd = (double)j;
-    const double m = fma(-jd, d, c);
-    if (exact) return STRICT ? (m > 0.0) : (m >= 0.0);
-    const double E = jd * fma(jd, d, __builtin_fabs(c)) * 0x1p-52 + jd * 0x1p-1070;
-    return m > 2.0 * E ? 1 : (m < -2.0 * E ? 0 : -1);
-  };
-  const double q = c / d;
-  int j0 = q >= (double)cap ? cap : (q > 0.0 ? (int)q : 0);
-  // largest fitting j in [j0 - 1, j0 + 2] (clamped to [0, cap]): s_0 = c fits by the caller's
-  // mask; the quotient is within one of the count unless rounding decides it
-  int n = max(j0 - 1, 0);
-  if (n >= 1 && f(n) != 1) return -1;
-  for (int k = 0; k < 3 && n < cap; k++) {
-    const int g = f(n + 1);
-    if (g < 0) return -1;
-    if (g == 0) return n;
-    n++;
-  }
-  return n < cap ? -1 : cap;                   // (more than j0 + 2 copies: the quotient was off)
-}
-
 #ifdef PVT_STAMPS
 __device__ __forceinline__ uint64_t zstamp() {
   uint64_t t;
@@ -535,37 +485,15 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     const bool on1 = __builtin_amdgcn_inverse_ballot_w64(m0);
     const bool two = __double_as_longlong(d2) == 0 && __double_as_longlong(d3) == 0;
     R = __builtin_amdgcn_readfirstlane(R);
-    // Pass 1, closed form: the copies of every lane of m0 (copies_of), the least over the
-    // dimensions of positive demand (a dimension of demand +-0 keeps its capacity and fits as it
-    // did for m0), capped at R.
     int cnt = 0;
-    bool unk = false;
-    if (on1) {
-      int n = R;
-      auto dim = [&](double c, double d) {
-        if (n >= 0 && d > 0.0) {
-          const int k1 = copies_of<STRICT>(c, d, R);
-          n = k1 < 0 ? -1 : min(n, k1);
-        }
-      };
-      dim(c0, d0);
-      dim(c1, d1);
-      if (!two) { dim(c2, d2); dim(c3, d3); }
-      unk = n < 0;
-      cnt = max(n, 0);
-    }
-#ifdef PVT_STAMPS
-    n_iter += 1;
-#endif
-    if (UNI(__ballot(unk) != 0)) {
-      // rounding may decide some lane's count: subtract copy after copy. Without per-lane masks:
-      // with d >= 0 a lane that fails a copy fails every later one (its residual only falls
-      // further), so every lane just keeps subtracting, recording the last copy that fit;
-      // lanes outside m0 start at -inf. ZW_UNROLL copies per check (a check past the stop only
-      // raises counts of lanes that get no task or no more tasks: asg clamps them).
+    {
+      // Pass 1: without per-lane masks: with d >= 0 a lane that fails a copy fails every later
+      // one (its residual only falls further), so every lane just keeps subtracting, recording
+      // the last copy that fit (= the copies it takes); lanes outside m0 start at -inf.
+      // ZW_UNROLL copies per check (a check past the stop only raises counts of lanes that get no
+      // task or no more tasks: asg clamps them).
       double x0 = on1 ? c0 : -DINF, x1 = on1 ? c1 : -DINF, x2 = on1 ? c2 : -DINF, x3 = on1 ? c3 : -DINF;
       int t = 0;
-      cnt = 0;
       auto pass1 = [&](auto dims) {
         constexpr int D = decltype(dims)::value;
         int u = __builtin_ctzll(m0), fb = 0;
@@ -594,6 +522,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       };
       if (two) pass1(IntC<2>{});
       else pass1(IntC<4>{});
+#ifdef PVT_STAMPS
+      n_iter += t;
+#endif
     }
     const int incl = wave_incl_scan_dpp(cnt);
     const int pre = incl - cnt;
@@ -1067,21 +998,17 @@ __global__ __launch_bounds__(256) void host_absmax_kernel(const double* avail, i
   for (int h = lo + blockIdx.x * 256 + tid; h < hi; h += gridDim.x * 256)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      const double x = __builtin_fabs(avail[(size_t)r * H + h]);
-      m[r] = (x <= m[r]) ? m[r] : x;          // (a NaN capacity propagates: no certificate)
-    }
+      m[r] = nan_max(m[r], __builtin_fabs(avail[(size_t)r * H + h]));   // (NaN propagates:
+    }                                                                     //  no certificate)
 #pragma unroll
   for (int r = 0; r < 4; r++) {
-    for (int off = 32; off > 0; off >>= 1) {
-      const double o = __shfl_xor(m[r], off);
-      m[r] = (o <= m[r]) ? m[r] : o;
-    }
+    m[r] = wave_nmax_d(m[r]);
     if (lane == 0) red[wave][r] = m[r];
   }
   __syncthreads();
   if (tid < 4) {
     double v = red[0][tid];
-    for (int w = 1; w < 4; w++) v = (red[w][tid] <= v) ? v : red[w][tid];
+    for (int w = 1; w < 4; w++) v = nan_max(v, red[w][tid]);
     part[blockIdx.x * 4 + tid] = v;
   }
 }

@@ -1,0 +1,118 @@
+"""The one-wave resident walk (pvt_batch.hip resident_walk): rounds of up to 1024 hosts of the
+first-fit-shaped policies -- cost_aware best-fit (score-0 winners), keyed and unsorted cost_aware
+first-fit, vbp first-fit -- are walked by one wave over their hosts in LDS, and the 4-wave path
+takes over where the walk stops. Every round must equal the CPU restatement, including rounds
+built to stop the walk: no score-0 host (anchor zones without capacity), subnormal egress costs
+(risky scores), zero-key hosts running out inside a keyed group (the group's frozen keys are
+handed over), unplaceable tasks; and the same batch with the walk off (PVT_RWALK=0)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from pivot_place import _abi, synthetic
+from pivot_place.engine import PlacementEngine
+
+pytestmark = pytest.mark.gpu
+
+WALKED = [_abi.PVT_CA_BF, _abi.PVT_CA_FF, _abi.PVT_VBP_FF]
+
+
+def _same(got, ref, what):
+    np.testing.assert_array_equal(got.placement, ref.placement, err_msg=what)
+    np.testing.assert_array_equal(got.order, ref.order, err_msg=what)
+    assert np.array_equal(got.avail, ref.avail), what
+
+
+@pytest.fixture(scope="module")
+def engine_nowalk():
+    old = os.environ.get("PVT_RWALK")
+    os.environ["PVT_RWALK"] = "0"
+    try:
+        eng = PlacementEngine(0)
+    finally:
+        if old is None:
+            del os.environ["PVT_RWALK"]
+        else:
+            os.environ["PVT_RWALK"] = old
+    return eng
+
+
+def _check(engine, engine_nowalk, rounds, what):
+    got = engine.place_batch(rounds)
+    off = engine_nowalk.place_batch(rounds)
+    for i, (r, g, o) in enumerate(zip(rounds, got, off)):
+        ref = oracle.place(r)
+        _same(g, ref, "%s round %d (walk)" % (what, i))
+        _same(o, ref, "%s round %d (no walk)" % (what, i))
+
+
+@pytest.mark.parametrize("mode", WALKED)
+@pytest.mark.parametrize("H,T", [(1000, 1000), (1, 7), (64, 300), (65, 65), (1024, 4096), (700, 2000)])
+def test_walked_rounds_match_oracle(engine, engine_nowalk, mode, H, T):
+    rounds = [synthetic.make_round(mode, H, T, seed=11 + s) for s in range(6)]
+    _check(engine, engine_nowalk, rounds, "mode %d H=%d T=%d" % (mode, H, T))
+
+
+@pytest.mark.parametrize("sort_hosts", [True, False])
+def test_cost_aware_first_fit_both_orders(engine, engine_nowalk, sort_hosts):
+    rounds = [synthetic.make_round(_abi.PVT_CA_FF, 900, 1500, seed=40 + s, sort_hosts=sort_hosts)
+              for s in range(4)]
+    _check(engine, engine_nowalk, rounds, "ca_ff sort_hosts=%s" % sort_hosts)
+
+
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_CA_FF])
+def test_walk_stops_without_zero_class_host(engine, engine_nowalk, mode):
+    """Zones 0-11 hold no capacity: groups anchored there find no score-0 / key-0 host, the walk
+    stops (for keyed first-fit inside the group, whose frozen keys the 4-wave path takes over)."""
+    rounds = []
+    for s in range(5):
+        r = synthetic.make_round(mode, 1000, 1200, seed=60 + s)
+        r.avail[:2, r.zone < 12] = 0.0
+        rounds.append(r)
+    _check(engine, engine_nowalk, rounds, "no zero-class hosts mode %d" % mode)
+
+
+def test_keyed_zero_hosts_run_out_inside_a_group(engine, engine_nowalk):
+    """Few zero-key hosts with little memory: they fill in the middle of a group, so the walk
+    stops there and the 4-wave path goes on with the group's keys frozen at its start."""
+    rounds = []
+    for s in range(5):
+        r = synthetic.make_round(_abi.PVT_CA_FF, 1000, 2000, seed=80 + s)
+        r.avail[1] = np.minimum(r.avail[1], 9000.0)
+        rounds.append(r)
+    _check(engine, engine_nowalk, rounds, "keyed run-out")
+
+
+def test_best_fit_risky_scores(engine, engine_nowalk):
+    """Subnormal egress costs: a fitting host may score 0 by underflow (risky): the walk stops
+    before letting a later host win."""
+    rounds = []
+    for s in range(4):
+        r = synthetic.make_round(_abi.PVT_CA_BF, 800, 800, seed=90 + s)
+        r.cost = r.cost.copy()
+        r.cost[r.cost > 0] = 1e-310
+        rounds.append(r)
+    _check(engine, engine_nowalk, rounds, "risky")
+
+
+def test_vbp_first_fit_unplaceable_tasks(engine, engine_nowalk):
+    rounds = []
+    for s in range(4):
+        r = synthetic.make_round(_abi.PVT_VBP_FF, 500, 3000, seed=100 + s)
+        r.dem[0, ::7] = 100.0                       # every 7th task fits no host
+        rounds.append(r)
+    _check(engine, engine_nowalk, rounds, "unplaceable")
+
+
+def test_mixed_host_batch_walks(engine):
+    """pvt_place_host_batch with every policy: the walked modes and the others in one launch."""
+    modes = [_abi.PVT_CA_FF, _abi.PVT_CA_BF, _abi.PVT_OPP, _abi.PVT_VBP_FF, _abi.PVT_VBP_BF]
+    rounds = [synthetic.make_round(modes[i % 5], 1000, 200 + 13 * i, seed=120 + i) for i in range(15)]
+    got = engine.place_host_batch([(r, None) for r in rounds])
+    for i, (r, g) in enumerate(zip(rounds, got)):
+        ref = oracle.place(r)
+        _same(g, ref, "mixed %d" % i)
+        if ref.mt_state is not None:
+            assert np.array_equal(g.mt_state, ref.mt_state)

@@ -33,6 +33,10 @@ for s in "$@"; do
     st_zw)      for m in ca_bf vbp_ff ca_ff; do run st_$m 120 python tools/zwalk_stamps.py 1000000 10000 libpivot_place_stamps.so $m; done ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
+    t_rw)       run t_rw 400 $T tests/test_gpu_resident_walk.py tests/test_gpu_batch.py ;;
+    b_c4w)      for m in ${C4M:-ca_bf ca_ff vbp_ff}; do run b_c4w_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
+    t_host)     run t_host 400 $T tests/test_gpu_host_batch.py tests/test_lockstep.py tests/test_gpu_fused.py ;;
+    b_lock)     run b_lock 300 python -c "import bench, json; from pivot_place.engine import PlacementEngine; e = PlacementEngine(0); bench.replay_workloads(e); print(json.dumps(bench.lockstep_workload(e)))" ;;
     st_res)     for m in ${RES_MODES:-ca_bf vbp_bf vbp_ff ca_ff}; do run st_res_$m 120 python tools/resident_stamps.py $m; done ;;
     st_opp)     run st_opp 150 python tools/commit_stamps.py 2 1000000 10000 ;;
     profbench)  mkdir -p gpurun_out/prof; run profbench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 $NB ;;
