@@ -171,7 +171,7 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
 template <int MODE, int NT>
 __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, const int32_t* ord,
                              int32_t* pl, const double* csum, const double* bsum, bool has_groups,
-                             bool keyed, int* kgrp) {
+                             bool keyed, int* kgrp, uint64_t* A_stamps) {
   constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
   __shared__ int s_stop, s_kgrp;
   const int T = R.n_tasks, H = R.n_hosts, Z = R.n_zones;
@@ -207,6 +207,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
     for (int blk = nsb - 2; blk >= 0; blk--) ws[blk * 4 + tid] = fmin(ws[blk * 4 + tid], ws[(blk + 1) * 4 + tid]);
   __syncthreads();
   if (wave == 0) {
+#ifdef PVT_STAMPS
+    uint64_t n_probe = 0, n_adv = 0, n_keys = 0;
+#endif
     const int nch = (H + 63) >> 6;
     int p0 = 0;
     double ra0, ra1, ra2, ra3;
@@ -273,6 +276,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
             // frozen host keys of the group (cost_aware.py:104-119) on the capacities now: only
             // whether each is exactly +0 matters here
             cur_grp = g;
+#ifdef PVT_STAMPS
+            n_keys++;
+#endif
             store_chunk(p0);
             for (int c = 0; c < nch; c++) {
               const int q = c * 64 + lane;
@@ -318,6 +324,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
           while (zm == 0 && rk == 0 && p0 + 1 < nch &&
                  !__ballot(rv && fits<STRICT>(ra0, ra1, ra2, ra3, mn0, mn1, mn2, mn3))) {
             store_chunk(p0);                   // dead: move the register chunk on
+#ifdef PVT_STAMPS
+            n_adv++;
+#endif
             ++p0;
             load_chunk(p0);
             if (MODE == CA_FF && keyed) rkm = rfl_u64(wm[p0]);
@@ -335,6 +344,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
             win = -2;
           } else {
             for (int c = p0 + 1; c < nch; c++) {
+#ifdef PVT_STAMPS
+              n_probe++;
+#endif
               const int q = c * 64 + lane;
               const bool v = q < H;
               const int qq = v ? q : 0;
@@ -366,6 +378,13 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
     }
     store_chunk(p0);
     if (lane == 0) { s_stop = p; s_kgrp = cur_grp; }
+#ifdef PVT_STAMPS
+    if (blockIdx.x == 0 && lane == 0 && A_stamps) {
+      A_stamps[10] += n_probe;
+      A_stamps[11] += n_adv;
+      A_stamps[12] += n_keys;
+    }
+#endif
   }
   __syncthreads();
   *kgrp = s_kgrp;
@@ -444,7 +463,17 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   int p_start = 0, kgrp = -1;
   constexpr bool WALKABLE = (MODE == CA_BF || MODE == CA_FF || MODE == VBP_FF);
   if (WALKABLE && A.walk && H <= RW_MAXH && T > 0 && !(CA && R.rt_bw)) {
-    p_start = resident_walk<MODE, NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, keyed, &kgrp);
+#ifdef PVT_STAMPS
+    const uint64_t tw0 = rstamp();
+#endif
+    p_start = resident_walk<MODE, NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, keyed, &kgrp,
+                                      A.stamps);
+#ifdef PVT_STAMPS
+    if (blockIdx.x == 0 && tid == 0 && A.stamps) {   // walked tasks, walk cycles (block 0)
+      A.stamps[8] += (uint64_t)p_start;
+      A.stamps[9] += rstamp() - tw0;
+    }
+#endif
     const double* wa = reinterpret_cast<const double*>(smem + Lo.wa);
     const double* wk = reinterpret_cast<const double*>(smem + Lo.wk);
 #pragma unroll

@@ -125,6 +125,8 @@ def test_ff_epochs_nan_capacity_blocks_the_certificate(engine):
     r.avail[2, 7777] = np.nan
     res, st = _place(engine, r)
     off, st0 = _place(engine, r, epochs=False)
-    assert st["frontier_chains"] == 0, st
+    # (the keyed path's own per-group frontier walks count as frontier chains in both runs;
+    # an FF epoch chain proven despite the NaN would replace them and change the count)
+    assert st["frontier_chains"] == st0["frontier_chains"], (st, st0)
     np.testing.assert_array_equal(res.placement, off.placement)
     np.testing.assert_array_equal(res.order, off.order)

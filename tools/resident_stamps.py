@@ -38,3 +38,8 @@ print("%s B=%d H=%d T=%d tasks=%d full-path tasks=%d (PVT_RES_WAVES=%s)"
 for k, nm in enumerate(names):
     print("  %-16s %6.1f%%  %8.0f cycles/task" % (nm, 100.0 * buf[k] / max(tot, 1), buf[k] / n))
 print("  %-16s %6.1f%%  %8.0f cycles/task" % ("total", 100.0, tot / n))
+if buf[8] or buf[9]:
+    print("  resident walk: %d of %d tasks walked, %.0f cycles (%.0f per walked task; the 4-wave "
+          "phases above time the rest)" % (buf[8], T, buf[9], buf[9] / max(buf[8], 1)))
+    print("  walk: %d LDS chunk probes, %d register-chunk advances, %d keyed key passes"
+          % (buf[10], buf[11], buf[12]))
