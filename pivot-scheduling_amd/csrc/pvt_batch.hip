@@ -114,11 +114,11 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
   const int T = R.n_tasks, tid = threadIdx.x;
   for (int i = tid; i < Tpad; i += NT) {
     if (i < T) {
-      const uint32_t g = grouped ? (uint32_t)R.task_group[i] : 0u;
+      const uint32_t g = grouped ? (uint32_t)G(R.task_group)[i] : 0u;
       ka[i] = ((uint64_t)g << 32) | (uint32_t)i;
       if (sorted) {
-        const double n = __builtin_sqrt(norm2_seq(R.dem[i], R.dem[(size_t)T + i],
-                                                  R.dem[2 * (size_t)T + i], R.dem[3 * (size_t)T + i]));
+        const double n = __builtin_sqrt(norm2_seq(G(R.dem)[i], G(R.dem)[(size_t)T + i],
+                                                  G(R.dem)[2 * (size_t)T + i], G(R.dem)[3 * (size_t)T + i]));
         kb[i] = ~dbits(n);                               // descending norm
       } else {
         kb[i] = 0;
@@ -184,8 +184,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   double* wk = reinterpret_cast<double*>(smem + Lo.wk);      // [RW_MAXH]
   for (int h = tid; h < H; h += NT) {
 #pragma unroll
-    for (int r = 0; r < 4; r++) wa[r * RW_MAXH + h] = R.avail[(size_t)r * H + h];
-    wz[h] = R.zone[h];
+    for (int r = 0; r < 4; r++) wa[r * RW_MAXH + h] = G(R.avail)[(size_t)r * H + h];
+    wz[h] = G(R.zone)[h];
   }
   const int nsb = (T + 63) >> 6;
   for (int blk = wave; blk < nsb; blk += NT / WAVE) {
@@ -194,7 +194,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
     if (i < T) {
       const int t = ord[i];
 #pragma unroll
-      for (int r = 0; r < 4; r++) m[r] = R.dem[(size_t)r * T + t];
+      for (int r = 0; r < 4; r++) m[r] = G(R.dem)[(size_t)r * T + t];
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
@@ -237,9 +237,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       const int i = b * 64 + lane;
       const int t = i < T ? ord[i] : 0;
 #pragma unroll
-      for (int r = 0; r < 4; r++) d[r] = R.dem[(size_t)r * T + t];
-      grp = has_groups ? R.task_group[t] : 0;
-      anc = has_groups ? R.group_anchor[grp] : 0;
+      for (int r = 0; r < 4; r++) d[r] = G(R.dem)[(size_t)r * T + t];
+      grp = has_groups ? G(R.task_group)[t] : 0;
+      anc = has_groups ? G(R.group_anchor)[grp] : 0;
     };
     double nd[4];
     int nanc, ngrp;
@@ -287,7 +287,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
               const double x0 = wa[qq], x1 = wa[RW_MAXH + qq], x2 = wa[2 * RW_MAXH + qq], x3 = wa[3 * RW_MAXH + qq];
               const int z = wz[qq];
               const double r = __builtin_sqrt(norm2_seq(x0, x1, x2, x3));
-              const double df = (R.decay && v) ? (double)R.decay[q] : 1.0;
+              const double df = (R.decay && v) ? (double)G(R.decay)[q] : 1.0;
               const double key = (csum[a * Z + z] * df) / (r * bsum[a * Z + z]);
               if (v) wk[q] = key;
               const uint64_t m = __ballot(v && dbits(key) == 0);
@@ -414,8 +414,8 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   if (CA)
     for (int i = tid; i < Z * Z; i += NT) {
       const int a = i / Z, z = i - a * Z;
-      csum[i] = R.cost[a * Z + z] + R.cost[z * Z + a];
-      bsum[i] = R.bw[a * Z + z] + R.bw[z * Z + a];
+      csum[i] = G(R.cost)[a * Z + z] + G(R.cost)[z * Z + a];
+      bsum[i] = G(R.bw)[a * Z + z] + G(R.bw)[z * Z + a];
     }
   // Placements are kept in LDS by position and written out when the round ends: a global
   // store inside the task loop would put its round trip (vmcnt) on every task's critical path.
@@ -436,12 +436,12 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   for (int j = 0; j < HPL; j++) {
     const int h = h0 + j;
     const bool v = h < H;
-    a0[j] = v ? R.avail[h] : __builtin_nan("");
-    a1[j] = v ? R.avail[(size_t)H + h] : __builtin_nan("");
-    a2[j] = v ? R.avail[2 * (size_t)H + h] : __builtin_nan("");
-    a3[j] = v ? R.avail[3 * (size_t)H + h] : __builtin_nan("");
-    zz[j] = (CA && v) ? R.zone[h] : 0;
-    tb[j] = (MODE == VBP_BF && v) ? R.tiebreak[h] : 0u;
+    a0[j] = v ? G(R.avail)[h] : __builtin_nan("");
+    a1[j] = v ? G(R.avail)[(size_t)H + h] : __builtin_nan("");
+    a2[j] = v ? G(R.avail)[2 * (size_t)H + h] : __builtin_nan("");
+    a3[j] = v ? G(R.avail)[3 * (size_t)H + h] : __builtin_nan("");
+    zz[j] = (CA && v) ? G(R.zone)[h] : 0;
+    tb[j] = (MODE == VBP_BF && v) ? G(R.tiebreak)[h] : 0u;
     key[j] = 0.0;                         // first-fit by index unless keyed
     cc[j] = 0.0;
     bb[j] = 1.0;
@@ -456,7 +456,7 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   } else {
     res_order<NT>(R, grouped, R.sort_tasks != 0, ka, kb, ord, A.Tpad);
   }
-  for (int i = tid; i < T; i += NT) R.order[i] = ord[i];
+  for (int i = tid; i < T; i += NT) G(R.order)[i] = ord[i];
 
   // first-fit-shaped rounds of up to RW_MAXH hosts: one wave walks them (resident_walk); this
   // path takes over where it stops, on the walked capacities (and the keyed walk's group keys)
@@ -497,7 +497,7 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   MtWave mw;
   mw.buf = 0; mw.used = 0; mw.limit = 0;
   if (MODE == OPP) {
-    const uint32_t* src = R.mt_state;
+    const gptr<uint32_t> src = G(R.mt_state);
     for (int i = lane; i < 625; i += WAVE) mk[i] = src[i];
     __builtin_amdgcn_s_waitcnt(0xc07f);
   }
@@ -534,14 +534,14 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
 #pragma unroll
       for (int k = 0; k < PER; k++) {
         const int t = tt[k];
-        dd[k][0] = R.dem[t];
-        dd[k][1] = R.dem[(size_t)T + t];
-        dd[k][2] = R.dem[2 * (size_t)T + t];
-        dd[k][3] = R.dem[3 * (size_t)T + t];
-        gg[k] = has_groups ? R.task_group[t] : 0;
+        dd[k][0] = G(R.dem)[t];
+        dd[k][1] = G(R.dem)[(size_t)T + t];
+        dd[k][2] = G(R.dem)[2 * (size_t)T + t];
+        dd[k][3] = G(R.dem)[3 * (size_t)T + t];
+        gg[k] = has_groups ? G(R.task_group)[t] : 0;
       }
 #pragma unroll
-      for (int k = 0; k < PER; k++) aa[k] = has_groups ? R.group_anchor[gg[k]] : 0;
+      for (int k = 0; k < PER; k++) aa[k] = has_groups ? G(R.group_anchor)[gg[k]] : 0;
 #pragma unroll
       for (int k = 0; k < PER; k++) {
         const int i = tid + k * NT;
@@ -575,7 +575,7 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
 #pragma unroll
           for (int j = 0; j < HPL; j++) {
             cc[j] = csum[anc * Z + zz[j]];
-            bb[j] = rt ? (h0 + j < H ? R.rt_bw[(size_t)grp_q * H + h0 + j] : 1.0) : bsum[anc * Z + zz[j]];
+            bb[j] = rt ? (h0 + j < H ? G(R.rt_bw)[(size_t)grp_q * H + h0 + j] : 1.0) : bsum[anc * Z + zz[j]];
           }
           if (MODE == CA_BF) {
             zmask = 0; rmask = 0;
@@ -600,7 +600,7 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
 #pragma unroll
           for (int j = 0; j < HPL; j++) {
             const double r = __builtin_sqrt(norm2_seq(a0[j], a1[j], a2[j], a3[j]));
-            const double df = (R.decay && h0 + j < H) ? (double)R.decay[h0 + j] : 1.0;
+            const double df = (R.decay && h0 + j < H) ? (double)G(R.decay)[h0 + j] : 1.0;
             key[j] = (cc[j] * df) / (r * bb[j]);
             zmask |= (dbits(key[j]) == 0 ? 1u : 0u) << j;
           }
@@ -848,20 +848,20 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
 #endif
 
   __syncthreads();
-  for (int i = tid; i < T; i += NT) R.placement[ord[i]] = pl[i];
+  for (int i = tid; i < T; i += NT) G(R.placement)[ord[i]] = pl[i];
 #pragma unroll
   for (int j = 0; j < HPL; j++) {
     const int h = h0 + j;
     if (h < H) {
-      R.avail[h] = a0[j];
-      R.avail[(size_t)H + h] = a1[j];
-      R.avail[2 * (size_t)H + h] = a2[j];
-      R.avail[3 * (size_t)H + h] = a3[j];
+      G(R.avail)[h] = a0[j];
+      G(R.avail)[(size_t)H + h] = a1[j];
+      G(R.avail)[2 * (size_t)H + h] = a2[j];
+      G(R.avail)[3 * (size_t)H + h] = a3[j];
     }
   }
   if (MODE == OPP && wave == 0) {
     mt_unbuffer(mk, mw);
-    uint32_t* dst = R.mt_state;
+    const gptr<uint32_t> dst = G(R.mt_state);
     for (int i = lane; i < 625; i += WAVE) dst[i] = mk[i];
   }
 }

@@ -7,6 +7,13 @@ namespace pvt {
 
 #define DINF __builtin_inf()
 
+// Global-address-space view of an array whose pointer the kernel loads from memory (a round
+// descriptor): the compiler cannot infer the address space of such a pointer and emits flat
+// accesses, which count in lgkmcnt as well as vmcnt -- every LDS wait would then also wait for
+// the outstanding global loads (a prefetch of the next task records, say).
+template <class T> using gptr = __attribute__((address_space(1))) T*;
+template <class T> __device__ __forceinline__ gptr<T> G(T* p) { return (gptr<T>)p; }
+
 __device__ __forceinline__ double norm2_seq(double x0, double x1, double x2, double x3) {
   double s = __builtin_fma(x0, x0, 0.0);
   s = __builtin_fma(x1, x1, s);

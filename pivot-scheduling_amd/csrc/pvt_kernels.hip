@@ -220,9 +220,9 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
       const size_t row = (size_t)(t0 + k) * A.S + seg;
       SegEntry e;
       e.s = ls[k]; e.tb = lt[k]; e.id = li[k];
-      A.seg[row * KL + lane] = e;
+      G(A.seg)[row * KL + lane] = e;
       const int filled = __popcll(__ballot(li[k] != 0x7fffffff));
-      if (lane == 0) A.seg_feas[row] = filled == KL ? KL + 1 : filled;
+      if (lane == 0) G(A.seg_feas)[row] = filled == KL ? KL + 1 : filled;
     }
   }
 }
@@ -318,8 +318,8 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
   // entry e of source list g
   auto src = [&](int g, int e) -> const SegEntry& {
-    return packed ? A.seg[((size_t)g * A.nt + task) * (SL + 1) + e]
-                  : A.seg[((size_t)task * A.S + g) * SL + e];
+    return packed ? G(A.seg)[((size_t)g * A.nt + task) * (SL + 1) + e]
+                  : G(A.seg)[((size_t)task * A.S + g) * SL + e];
   };
   for (int j = tid; j < LMAX; j += 256) run[j] = inv;
   if (tid == 0) { bound = inv; tot = 0; cnt_sh = 0; }
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
       }
     } else if (tid == 0) {
       for (int g = g0; g < min(A.S, g0 + batch); g++) {
-        const int f = A.seg_feas[(size_t)task * A.S + g];
+        const int f = G(A.seg_feas)[(size_t)task * A.S + g];
         tot += f;
         if (f > SL) {
           const SegEntry se = src(g, SL - 1);
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
   Key* O = out[wave];
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
   for (int j = lane; j < n; j += WAVE) {
-    const SegEntry se = A.seg[((size_t)task * S) * KL + j];
+    const SegEntry se = G(A.seg)[((size_t)task * S) * KL + j];
     L[j] = {se.s, se.tb, se.id};
     O[j] = inv;
   }
@@ -438,10 +438,10 @@ __global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
   Key bound = inv;
   long long tot = 0;
   for (int g = 0; g < S; g++) {
-    const int f = A.seg_feas[(size_t)task * S + g];
+    const int f = G(A.seg_feas)[(size_t)task * S + g];
     tot += f;
     if (f > KL) {
-      const SegEntry se = A.seg[((size_t)task * S + g) * KL + KL - 1];
+      const SegEntry se = G(A.seg)[((size_t)task * S + g) * KL + KL - 1];
       const Key k = {se.s, se.tb, se.id};
       if (kless(k, bound)) bound = k;
     }
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   int valid = 0;
   for (int j = tid; j < n; j += 256) {
     const int g = j / SL, e = j - g * SL;
-    const SegEntry se = A.seg[((size_t)g * A.nt + task) * (SL + 1) + e];
+    const SegEntry se = G(A.seg)[((size_t)g * A.nt + task) * (SL + 1) + e];
     lk[j] = {se.s, se.tb, se.id};
     out[j] = inv;
     valid += se.id != 0x7fffffff;
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   if (tid == 0) {
     Key b = inv;
     for (int g = 0; g < W; g++) {
-      const SegEntry se = A.seg[((size_t)g * A.nt + task) * (SL + 1) + SL];
+      const SegEntry se = G(A.seg)[((size_t)g * A.nt + task) * (SL + 1) + SL];
       const Key k = {se.s, se.tb, se.id};
       if (kless(k, b)) b = k;
     }
@@ -600,8 +600,10 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
 // probes instead of rank-by-counting's 15 binary searches per entry (1.9 ms per config-5 round,
 // slower than the 55-stage bitonic network that ignores the segments' order, 1.6 ms).
 __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
-  __shared__ Key ka[LMAX];
-  __shared__ Key kb[LMAX];
+  // (one array with a round-parity index, not two pointers swapped per round: a swapped pointer
+  // loses its LDS address space and every co-rank probe became a flat load)
+  __shared__ Key kbuf[2][LMAX];
+  Key* const ka = kbuf[0];
   __shared__ int cnt_sh;
   const int task = blockIdx.x, tid = threadIdx.x;
   if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
@@ -614,7 +616,7 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   for (int j = tid; j < n; j += 256) {
     Key k = inv;
     if (j < S * KL) {
-      const SegEntry se = A.seg[(size_t)task * S * KL + j];
+      const SegEntry se = G(A.seg)[(size_t)task * S * KL + j];
       k = {se.s, se.tb, se.id};
     }
     ka[j] = k;
@@ -624,42 +626,43 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   Key bound = inv;
   long long tot = 0;
   for (int g = 0; g < S; g++) {
-    const int f = A.seg_feas[(size_t)task * S + g];
+    const int f = G(A.seg_feas)[(size_t)task * S + g];
     tot += f;
     if (f > KL) {
-      const SegEntry se = A.seg[((size_t)task * S + g) * KL + KL - 1];
+      const SegEntry se = G(A.seg)[((size_t)task * S + g) * KL + KL - 1];
       const Key k = {se.s, se.tb, se.id};
       if (kless(k, bound)) bound = k;
     }
   }
   __syncthreads();
-  Key* src = ka;
-  Key* dst = kb;
+  int cur = 0;
   for (int len = KL; len < n; len <<= 1) {
     for (int o = tid * 4; o < n; o += 1024) {
       const int base = o & ~(2 * len - 1), i = o - base;
-      const Key* a = src + base;
-      const Key* b = a + len;
+      const int ia = base, ib = base + len;   // (indices into kbuf[cur]: LDS accesses)
       // co-rank: x outputs of the first i come from a (ties: a first; keys are distinct anyway
       // except the invalid padding, which sorts last either way)
       int lo = max(0, i - len), hi = min(i, len);
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (!kless(b[i - mid - 1], a[mid])) lo = mid + 1;
+        if (!kless(kbuf[cur][ib + i - mid - 1], kbuf[cur][ia + mid])) lo = mid + 1;
         else hi = mid;
       }
       int x = lo, y = i - lo;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        const bool ta = x < len && (y >= len || !kless(b[y], a[x]));
-        dst[o + k] = ta ? a[x] : b[y];
+        const Key kx = kbuf[cur][ia + min(x, len - 1)], ky = kbuf[cur][ib + min(y, len - 1)];
+        const bool ta = x < len && (y >= len || !kless(ky, kx));
+        kbuf[cur ^ 1][o + k] = ta ? kx : ky;
         x += ta ? 1 : 0;
         y += ta ? 0 : 1;
       }
     }
     __syncthreads();
-    Key* t = src; src = dst; dst = t;
+    cur ^= 1;
   }
+  const int fin = cur;
+#define src kbuf[fin]
   // kept entries: valid and below the bound, the first cnt of the merged list
   int c = 0;
   for (int j = tid; j < n; j += 256) c += (src[j].id != 0x7fffffff) && kless(src[j], bound);
@@ -680,7 +683,8 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   for (int u = 0; u < PO; u++) {
     const int j = tid + u * 256;
     const bool ok = j < cnt;
-    kk[u] = ok ? src[j] : inv;
+    kk[u] = inv;
+    if (ok) kk[u] = src[j];                  // (a select of the two addresses would be flat)
     const int h = ok ? kk[u].id : 0;
     zz[u] = ok ? A.zone[h] : 0;
     aa[u][0] = ok ? A.avail[h] : 0.0;
@@ -711,6 +715,7 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
     r.ord = A.ord[task];
     r.bs = bnd.s; r.btb = bnd.tb; r.bid = bnd.id;
   }
+#undef src
 }
 
 static int merge_variant(const MergeArgs& a) {
