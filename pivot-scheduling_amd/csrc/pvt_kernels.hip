@@ -220,9 +220,9 @@ __global__ __launch_bounds__(256) void score_kernel(ScoreArgs A) {
       const size_t row = (size_t)(t0 + k) * A.S + seg;
       SegEntry e;
       e.s = ls[k]; e.tb = lt[k]; e.id = li[k];
-      G(A.seg)[row * KL + lane] = e;
+      A.seg[row * KL + lane] = e;
       const int filled = __popcll(__ballot(li[k] != 0x7fffffff));
-      if (lane == 0) G(A.seg_feas)[row] = filled == KL ? KL + 1 : filled;
+      if (lane == 0) A.seg_feas[row] = filled == KL ? KL + 1 : filled;
     }
   }
 }
@@ -318,8 +318,8 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
   // entry e of source list g
   auto src = [&](int g, int e) -> const SegEntry& {
-    return packed ? G(A.seg)[((size_t)g * A.nt + task) * (SL + 1) + e]
-                  : G(A.seg)[((size_t)task * A.S + g) * SL + e];
+    return packed ? A.seg[((size_t)g * A.nt + task) * (SL + 1) + e]
+                  : A.seg[((size_t)task * A.S + g) * SL + e];
   };
   for (int j = tid; j < LMAX; j += 256) run[j] = inv;
   if (tid == 0) { bound = inv; tot = 0; cnt_sh = 0; }
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
       }
     } else if (tid == 0) {
       for (int g = g0; g < min(A.S, g0 + batch); g++) {
-        const int f = G(A.seg_feas)[(size_t)task * A.S + g];
+        const int f = A.seg_feas[(size_t)task * A.S + g];
         tot += f;
         if (f > SL) {
           const SegEntry se = src(g, SL - 1);
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
   Key* O = out[wave];
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
   for (int j = lane; j < n; j += WAVE) {
-    const SegEntry se = G(A.seg)[((size_t)task * S) * KL + j];
+    const SegEntry se = A.seg[((size_t)task * S) * KL + j];
     L[j] = {se.s, se.tb, se.id};
     O[j] = inv;
   }
@@ -438,10 +438,10 @@ __global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
   Key bound = inv;
   long long tot = 0;
   for (int g = 0; g < S; g++) {
-    const int f = G(A.seg_feas)[(size_t)task * S + g];
+    const int f = A.seg_feas[(size_t)task * S + g];
     tot += f;
     if (f > KL) {
-      const SegEntry se = G(A.seg)[((size_t)task * S + g) * KL + KL - 1];
+      const SegEntry se = A.seg[((size_t)task * S + g) * KL + KL - 1];
       const Key k = {se.s, se.tb, se.id};
       if (kless(k, bound)) bound = k;
     }
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   int valid = 0;
   for (int j = tid; j < n; j += 256) {
     const int g = j / SL, e = j - g * SL;
-    const SegEntry se = G(A.seg)[((size_t)g * A.nt + task) * (SL + 1) + e];
+    const SegEntry se = A.seg[((size_t)g * A.nt + task) * (SL + 1) + e];
     lk[j] = {se.s, se.tb, se.id};
     out[j] = inv;
     valid += se.id != 0x7fffffff;
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   if (tid == 0) {
     Key b = inv;
     for (int g = 0; g < W; g++) {
-      const SegEntry se = G(A.seg)[((size_t)g * A.nt + task) * (SL + 1) + SL];
+      const SegEntry se = A.seg[((size_t)g * A.nt + task) * (SL + 1) + SL];
       const Key k = {se.s, se.tb, se.id};
       if (kless(k, b)) b = k;
     }
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   for (int j = tid; j < n; j += 256) {
     Key k = inv;
     if (j < S * KL) {
-      const SegEntry se = G(A.seg)[(size_t)task * S * KL + j];
+      const SegEntry se = A.seg[(size_t)task * S * KL + j];
       k = {se.s, se.tb, se.id};
     }
     ka[j] = k;
@@ -626,10 +626,10 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   Key bound = inv;
   long long tot = 0;
   for (int g = 0; g < S; g++) {
-    const int f = G(A.seg_feas)[(size_t)task * S + g];
+    const int f = A.seg_feas[(size_t)task * S + g];
     tot += f;
     if (f > KL) {
-      const SegEntry se = G(A.seg)[((size_t)task * S + g) * KL + KL - 1];
+      const SegEntry se = A.seg[((size_t)task * S + g) * KL + KL - 1];
       const Key k = {se.s, se.tb, se.id};
       if (kless(k, bound)) bound = k;
     }
