@@ -600,10 +600,8 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
 // probes instead of rank-by-counting's 15 binary searches per entry (1.9 ms per config-5 round,
 // slower than the 55-stage bitonic network that ignores the segments' order, 1.6 ms).
 __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
-  // (one array with a round-parity index, not two pointers swapped per round: a swapped pointer
-  // loses its LDS address space and every co-rank probe became a flat load)
-  __shared__ Key kbuf[2][LMAX];
-  Key* const ka = kbuf[0];
+  __shared__ Key ka[LMAX];
+  __shared__ Key kb[LMAX];
   __shared__ int cnt_sh;
   const int task = blockIdx.x, tid = threadIdx.x;
   if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
@@ -635,34 +633,36 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
     }
   }
   __syncthreads();
-  int cur = 0;
+  // (the two halves swap by pointer; the co-rank probes are then flat accesses to LDS, which
+  // measured faster than indexing both halves by a round parity: 2.69 vs 3.04 ms per config-5
+  // vbp best-fit round -- no global load is in flight during the rounds)
+  Key* src = ka;
+  Key* dst = kb;
   for (int len = KL; len < n; len <<= 1) {
     for (int o = tid * 4; o < n; o += 1024) {
       const int base = o & ~(2 * len - 1), i = o - base;
-      const int ia = base, ib = base + len;   // (indices into kbuf[cur]: LDS accesses)
+      const Key* a = src + base;
+      const Key* b = a + len;
       // co-rank: x outputs of the first i come from a (ties: a first; keys are distinct anyway
       // except the invalid padding, which sorts last either way)
       int lo = max(0, i - len), hi = min(i, len);
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (!kless(kbuf[cur][ib + i - mid - 1], kbuf[cur][ia + mid])) lo = mid + 1;
+        if (!kless(b[i - mid - 1], a[mid])) lo = mid + 1;
         else hi = mid;
       }
       int x = lo, y = i - lo;
 #pragma unroll
       for (int k = 0; k < 4; k++) {
-        const Key kx = kbuf[cur][ia + min(x, len - 1)], ky = kbuf[cur][ib + min(y, len - 1)];
-        const bool ta = x < len && (y >= len || !kless(ky, kx));
-        kbuf[cur ^ 1][o + k] = ta ? kx : ky;
+        const bool ta = x < len && (y >= len || !kless(b[y], a[x]));
+        dst[o + k] = ta ? a[x] : b[y];
         x += ta ? 1 : 0;
         y += ta ? 0 : 1;
       }
     }
     __syncthreads();
-    cur ^= 1;
+    Key* t = src; src = dst; dst = t;
   }
-  const int fin = cur;
-#define src kbuf[fin]
   // kept entries: valid and below the bound, the first cnt of the merged list
   int c = 0;
   for (int j = tid; j < n; j += 256) c += (src[j].id != 0x7fffffff) && kless(src[j], bound);
@@ -715,7 +715,6 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
     r.ord = A.ord[task];
     r.bs = bnd.s; r.btb = bnd.tb; r.bid = bnd.id;
   }
-#undef src
 }
 
 static int merge_variant(const MergeArgs& a) {
