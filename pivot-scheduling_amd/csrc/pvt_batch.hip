@@ -208,7 +208,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   __syncthreads();
   if (wave == 0) {
 #ifdef PVT_STAMPS
-    uint64_t n_probe = 0, n_adv = 0, n_keys = 0;
+    uint64_t n_probe = 0, n_adv = 0, n_keys = 0, st_task = 0;
+    const uint64_t tw_start = rstamp();
 #endif
     const int nch = (H + 63) >> 6;
     int p0 = 0;
@@ -253,6 +254,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       const double mn0 = ws[b * 4 + 0], mn1 = ws[b * 4 + 1], mn2 = ws[b * 4 + 2], mn3 = ws[b * 4 + 3];
       const int kn = min(64, T - b * 64);
       for (int k = 0; k < kn; k++, p++) {
+#ifdef PVT_STAMPS
+        const uint64_t tk0 = rstamp();
+#endif
         p = __builtin_amdgcn_readfirstlane(p);
         p0 = __builtin_amdgcn_readfirstlane(p0);
         const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
@@ -374,6 +378,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
         win = __builtin_amdgcn_readfirstlane(win);
         if (win == -2) { stop = true; break; }
         if (win >= 0 && lane == 0) pl[p] = win;
+#ifdef PVT_STAMPS
+        st_task += rstamp() - tk0;
+#endif
       }
     }
     store_chunk(p0);
@@ -383,6 +390,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       A_stamps[10] += n_probe;
       A_stamps[11] += n_adv;
       A_stamps[12] += n_keys;
+      A_stamps[13] += st_task;                  // cycles inside the task loop bodies
+      A_stamps[14] += rstamp() - tw_start;      // wave 0's whole walk (records included)
     }
 #endif
   }

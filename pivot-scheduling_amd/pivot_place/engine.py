@@ -230,6 +230,29 @@ class DeviceBatch:
         return out
 
 
+_PTRS = {}
+
+
+def _ptr(a):
+    """Address of a contiguous numpy array's data (None for None). The cluster tables a policy
+    passes every round (zone, cost, bw, tiebreak) are the same objects round after round, so
+    their addresses are cached by identity (the cache keeps the array alive); a fresh array
+    takes the ctypes buffer path (~0.5 us, against ~2 us for .ctypes.data)."""
+    if a is None:
+        return None
+    e = _PTRS.get(id(a))
+    if e is not None and e[0] is a:
+        return e[1]
+    try:
+        p = ctypes.addressof(ctypes.c_char.from_buffer(a))
+    except (TypeError, ValueError, BufferError):      # (read-only or empty buffers)
+        p = a.__array_interface__["data"][0]
+    if len(_PTRS) >= 64:                              # (per-round arrays pass through)
+        _PTRS.clear()
+    _PTRS[id(a)] = (a, p)
+    return p
+
+
 def _align(n, a=256):
     return (n + a - 1) // a * a
 
@@ -387,13 +410,12 @@ class PlacementEngine:
         placement = np.empty(T, dtype=np.int32)
         order = np.empty(T, dtype=np.int32)
         mt = None if r.mt_state is None else np.array(r.mt_state, dtype=np.uint32)
-        s.avail = avail.ctypes.data
-        for name in ("zone", "tiebreak", "decay", "cost", "bw", "dem", "task_group", "group_anchor",
-                     "rt_bw"):
-            a = getattr(r, name)
-            setattr(s, name, None if a is None else a.ctypes.data)
-        s.placement, s.order = placement.ctypes.data, order.ctypes.data
-        s.mt_state = None if mt is None else mt.ctypes.data
+        s.avail = _ptr(avail)
+        s.zone, s.tiebreak, s.decay = _ptr(r.zone), _ptr(r.tiebreak), _ptr(r.decay)
+        s.cost, s.bw, s.dem = _ptr(r.cost), _ptr(r.bw), _ptr(r.dem)
+        s.task_group, s.group_anchor, s.rt_bw = _ptr(r.task_group), _ptr(r.group_anchor), _ptr(r.rt_bw)
+        s.placement, s.order = _ptr(placement), _ptr(order)
+        s.mt_state = _ptr(mt)
         return s, RoundResult(placement=placement, order=order, avail=avail, mt_state=mt)
 
     def _place_host(self, r: RoundArrays, items):
@@ -418,11 +440,11 @@ class PlacementEngine:
         status = np.zeros(2, dtype=np.int32)
         it = _abi.pvt_ca_items()
         it.n_items, it.n_apps, it.n_pred = ia.size, int(n_apps), ph.size
-        it.task_item, it.pred_off, it.pred_host = ti.ctypes.data, off.ctypes.data, ph.ctypes.data
-        it.item_app = ia.ctypes.data
+        it.task_item, it.pred_off, it.pred_host = _ptr(ti), _ptr(off), _ptr(ph)
+        it.item_app = _ptr(ia)
         it.n_storage, it.reserved = sz.size, 0
-        it.storage_zone, it.zone_storage = sz.ctypes.data, zs.ctypes.data
-        it.mt_state, it.status = mt.ctypes.data, status.ctypes.data
+        it.storage_zone, it.zone_storage = _ptr(sz), _ptr(zs)
+        it.mt_state, it.status = _ptr(mt), _ptr(status)
         return it, keep, mt, status
 
     def _ca_result(self, res, rc, mt, status):

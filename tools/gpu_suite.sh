@@ -35,10 +35,12 @@ for s in "$@"; do
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
     t_rw)       run t_rw 400 $T tests/test_gpu_resident_walk.py tests/test_gpu_batch.py ;;
     b_c4w)      for m in ${C4M:-ca_bf ca_ff vbp_ff}; do run b_c4w_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
+    hb_split)   TAILN=6 run hb_split 300 python tools/host_batch_split.py ;;
     t_host)     run t_host 400 $T tests/test_gpu_host_batch.py tests/test_lockstep.py tests/test_gpu_fused.py ;;
     b_lock)     run b_lock 300 python -c "import bench, json; from pivot_place.engine import PlacementEngine; e = PlacementEngine(0); bench.replay_workloads(e); print(json.dumps(bench.lockstep_workload(e)))" ;;
     st_res)     for m in ${RES_MODES:-ca_bf vbp_bf vbp_ff ca_ff}; do run st_res_$m 120 python tools/resident_stamps.py $m; done ;;
     st_rw)      for m in ca_bf vbp_ff ca_ff; do TAILN=12 run st_rw_$m 120 python tools/resident_stamps.py $m; PVT_RWALK=0 TAILN=12 run st_rw0_$m 120 python tools/resident_stamps.py $m; done ;;
+    st_rw1)     for m in ${RWM:-vbp_ff}; do TAILN=14 run st_rw_$m 120 python tools/resident_stamps.py $m; done ;;
     st_opp)     run st_opp 150 python tools/commit_stamps.py 2 1000000 10000 ;;
     profbench)  mkdir -p gpurun_out/prof; run profbench 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 20 $NB ;;
     pmc)        run pmc 1100 tools/pmc_all.sh "${PMC_TAG:-r04z}" ;;

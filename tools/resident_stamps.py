@@ -43,3 +43,6 @@ if buf[8] or buf[9]:
           "phases above time the rest)" % (buf[8], T, buf[9], buf[9] / max(buf[8], 1)))
     print("  walk: %d LDS chunk probes, %d register-chunk advances, %d keyed key passes"
           % (buf[10], buf[11], buf[12]))
+    print("  walk: %.0f cycles per task in the task bodies, %.0f per task for wave 0's whole walk "
+          "(the rest of the walk total: the prologue of all waves)"
+          % (buf[13] / max(buf[8], 1), buf[14] / max(buf[8], 1)))
