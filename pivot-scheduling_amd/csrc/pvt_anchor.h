@@ -39,5 +39,10 @@ struct AnchorArgs {
 };
 
 void launch_anchor(const AnchorArgs& a, hipStream_t st);
+// nr anchor calls (their AnchorArgs in device memory) in two launches: the wave launch has
+// nblocks = the sum of anchor_batch_blocks(C) blocks, call r starting at boff[r]
+int anchor_batch_blocks(int C);
+void launch_anchor_batch(const AnchorArgs* args_dev, const int32_t* boff_dev, int nr, int nblocks,
+                         hipStream_t st);
 
 }  // namespace pvt

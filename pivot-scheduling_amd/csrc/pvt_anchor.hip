@@ -148,14 +148,19 @@ __device__ void block_item(const AnchorArgs& a, int c, uint64_t* lds, uint64_t* 
   }
 }
 
-__global__ void __launch_bounds__(ANC_THREADS) anchor_block_kernel(AnchorArgs a) {
+// The deferred long lists q = blk, blk + nblk, ... of one anchor call, one block each.
+__device__ __forceinline__ void anchor_block_part(const AnchorArgs& a, int blk, int nblk) {
   __shared__ uint64_t lds[ANC_LDS];
   __shared__ uint64_t red[ANC_THREADS / 64];
   const int nd = *a.n_deferred;
-  for (int q = blockIdx.x; q < nd; q += gridDim.x) {
+  for (int q = blk; q < nd; q += nblk) {
     block_item(a, a.deferred[q], lds, red);
     __syncthreads();
   }
+}
+
+__global__ void __launch_bounds__(ANC_THREADS) anchor_block_kernel(AnchorArgs a) {
+  anchor_block_part(a, blockIdx.x, gridDim.x);
 }
 
 // Wave-level LDS ordering between the stages of a single wave's sort.
@@ -168,10 +173,8 @@ __device__ __forceinline__ void wave_sync() {
 // One item per wave. Lists of up to 64 entries are counted in registers (lane j holds entry
 // j; a pass over the lanes gives each its host's count and first position); up to ANC_WLDS
 // entries are sorted in the wave's LDS slice; longer lists are deferred to the block kernel.
-__global__ void __launch_bounds__(ANC_THREADS) anchor_wave_kernel(AnchorArgs a) {
-  __shared__ uint64_t lds[ANC_THREADS / 64][ANC_WLDS];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int c = blockIdx.x * (ANC_THREADS / 64) + wave;
+__device__ __forceinline__ void anchor_wave_item(const AnchorArgs& a, int c, uint64_t* buf) {
+  const int lane = threadIdx.x & 63;
   if (c >= a.C) return;
   int64_t row = c;
   if (a.item) {
@@ -213,7 +216,6 @@ __global__ void __launch_bounds__(ANC_THREADS) anchor_wave_kernel(AnchorArgs a) 
     }
     if (lane < n) best = ((uint64_t)cnt << 32) | (uint64_t)(0xffffffffu - first);
   } else {
-    uint64_t* buf = lds[wave];
     int m = 64;
     while (m < n) m <<= 1;
     for (int i = lane; i < m; i += 64) {
@@ -263,11 +265,44 @@ __global__ void __launch_bounds__(ANC_THREADS) anchor_wave_kernel(AnchorArgs a) 
   }
 }
 
+__global__ void __launch_bounds__(ANC_THREADS) anchor_wave_kernel(AnchorArgs a) {
+  __shared__ uint64_t lds[ANC_THREADS / 64][ANC_WLDS];
+  const int wave = threadIdx.x >> 6;
+  anchor_wave_item(a, blockIdx.x * (ANC_THREADS / 64) + wave, lds[wave]);
+}
+
 void launch_anchor(const AnchorArgs& a, hipStream_t st) {
   if (a.C <= 0) return;
   constexpr int IPB = ANC_THREADS / 64;
   anchor_wave_kernel<<<(a.C + IPB - 1) / IPB, ANC_THREADS, 0, st>>>(a);
   anchor_block_kernel<<<a.C < 256 ? a.C : 256, ANC_THREADS, 0, st>>>(a);
+}
+
+// Several anchor calls in one launch each (pvt_place_host_batch: the cost_aware rounds of a
+// tick): block b of the wave launch serves call r with boff[r] <= b < boff[r + 1]; the block
+// launch gives every call ANC_BATCH_BLOCKS blocks.
+constexpr int ANC_BATCH_BLOCKS = 8;
+__global__ void __launch_bounds__(ANC_THREADS) anchor_wave_batch_kernel(const AnchorArgs* A,
+                                                                         const int32_t* boff, int nr) {
+  __shared__ uint64_t lds[ANC_THREADS / 64][ANC_WLDS];
+  int r = 0;
+  while (r + 1 < nr && boff[r + 1] <= (int)blockIdx.x) r++;
+  const AnchorArgs a = A[r];
+  const int wave = threadIdx.x >> 6;
+  anchor_wave_item(a, ((int)blockIdx.x - boff[r]) * (ANC_THREADS / 64) + wave, lds[wave]);
+}
+__global__ void __launch_bounds__(ANC_THREADS) anchor_block_batch_kernel(const AnchorArgs* A) {
+  const AnchorArgs a = A[blockIdx.x / ANC_BATCH_BLOCKS];
+  anchor_block_part(a, blockIdx.x % ANC_BATCH_BLOCKS, ANC_BATCH_BLOCKS);
+}
+
+int anchor_batch_blocks(int C) { constexpr int IPB = ANC_THREADS / 64; return (C + IPB - 1) / IPB; }
+
+void launch_anchor_batch(const AnchorArgs* args_dev, const int32_t* boff_dev, int nr, int nblocks,
+                         hipStream_t st) {
+  if (nr <= 0) return;
+  if (nblocks > 0) anchor_wave_batch_kernel<<<nblocks, ANC_THREADS, 0, st>>>(args_dev, boff_dev, nr);
+  anchor_block_batch_kernel<<<nr * ANC_BATCH_BLOCKS, ANC_THREADS, 0, st>>>(args_dev);
 }
 
 }  // namespace pvt

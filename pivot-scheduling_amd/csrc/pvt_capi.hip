@@ -2304,19 +2304,26 @@ static void stage_round(char* hb, char* db, HostSlot& s, const pvt_round* r, con
 
 // The fused cost_aware grouping of an items round on the device (anchors, groups, draws); a
 // resident round's descriptor receives its group count.
-static int launch_items(pvt_ctx* ctx, char* db, const HostSlot& s, const pvt_ca_items* it, hipStream_t st) {
+static void items_args(char* db, const HostSlot& s, const pvt_ca_items* it, AnchorArgs* ka,
+                       CaGroupArgs* ga) {
   const int T = s.hr.n_tasks, H = s.hr.n_hosts, Z = s.hr.n_zones;
   int32_t* ab = reinterpret_cast<int32_t*>(db + s.ab);
-  AnchorArgs k{s.C, H, s.NP, 0, 0, reinterpret_cast<const int64_t*>(db + s.off), nullptr,
-               reinterpret_cast<const int32_t*>(db + s.ph), nullptr, s.d.zone,
-               reinterpret_cast<int32_t*>(db + s.mh), reinterpret_cast<int32_t*>(db + s.az), ab,
-               ab + 4, ab + 1};
-  CaGroupArgs g{T, s.C, Z, s.S, it->n_apps, reinterpret_cast<const int32_t*>(db + s.ti),
-                reinterpret_cast<const int32_t*>(db + s.az), reinterpret_cast<const int32_t*>(db + s.ia),
-                reinterpret_cast<const int32_t*>(db + s.sz), reinterpret_cast<const int32_t*>(db + s.zs),
-                reinterpret_cast<uint32_t*>(db + s.cmt), reinterpret_cast<int32_t*>(db + s.tg),
-                reinterpret_cast<int32_t*>(db + s.ga), reinterpret_cast<int32_t*>(db + s.st),
-                s.resident ? &reinterpret_cast<pvt_round*>(db + s.desc)->n_groups : nullptr};
+  *ka = AnchorArgs{s.C, H, s.NP, 0, 0, reinterpret_cast<const int64_t*>(db + s.off), nullptr,
+                   reinterpret_cast<const int32_t*>(db + s.ph), nullptr, s.d.zone,
+                   reinterpret_cast<int32_t*>(db + s.mh), reinterpret_cast<int32_t*>(db + s.az), ab,
+                   ab + 4, ab + 1};
+  *ga = CaGroupArgs{T, s.C, Z, s.S, it->n_apps, reinterpret_cast<const int32_t*>(db + s.ti),
+                    reinterpret_cast<const int32_t*>(db + s.az), reinterpret_cast<const int32_t*>(db + s.ia),
+                    reinterpret_cast<const int32_t*>(db + s.sz), reinterpret_cast<const int32_t*>(db + s.zs),
+                    reinterpret_cast<uint32_t*>(db + s.cmt), reinterpret_cast<int32_t*>(db + s.tg),
+                    reinterpret_cast<int32_t*>(db + s.ga), reinterpret_cast<int32_t*>(db + s.st),
+                    s.resident ? &reinterpret_cast<pvt_round*>(db + s.desc)->n_groups : nullptr};
+}
+
+static int launch_items(pvt_ctx* ctx, char* db, const HostSlot& s, const pvt_ca_items* it, hipStream_t st) {
+  AnchorArgs k;
+  CaGroupArgs g;
+  items_args(db, s, it, &k, &g);
   {
     Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * (double)s.NP);
     if (s.C > 0) launch_anchor(k, st);
@@ -2438,10 +2445,19 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
   const size_t n_out = L.o;
   for (int i = 0; i < n_rounds; i++)
     if (rounds[i].n_tasks > 0) plan_in(L, s[i], &rounds[i], items ? items[i] : nullptr);
-  std::vector<int> live;
+  std::vector<int> live, withit;
   for (int i = 0; i < n_rounds; i++)
-    if (rounds[i].n_tasks > 0) live.push_back(i);
+    if (rounds[i].n_tasks > 0) {
+      live.push_back(i);
+      if (items && items[i]) withit.push_back(i);
+    }
   if (live.empty()) return PVT_OK;
+  // the fused groupings of every cost_aware round: their kernel arguments in the stage, so the
+  // anchors and the groups of all of them take three launches
+  const int ni = (int)withit.size();
+  const size_t o_ka = ni ? L.take(sizeof(AnchorArgs) * ni) : 0;
+  const size_t o_kb = ni ? L.take(sizeof(int32_t) * (ni + 1)) : 0;
+  const size_t o_kg = ni ? L.take(sizeof(CaGroupArgs) * ni) : 0;
   const size_t o_desc = L.take(sizeof(pvt_round) * live.size());
   for (size_t k = 0; k < live.size(); k++) s[live[k]].desc = o_desc + sizeof(pvt_round) * k;
   if ((rc = ensure_pinned(ctx, L.o))) return rc;
@@ -2449,10 +2465,29 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
   char* hb = static_cast<char*>(ctx->hst);
   char* db = static_cast<char*>(ctx->hdev.p);
   for (int i : live) stage_round(hb, db, s[i], &rounds[i], items ? items[i] : nullptr);
+  int nab = 0;
+  for (int k = 0; k < ni; k++) {
+    const int i = withit[k];
+    AnchorArgs ka;
+    CaGroupArgs ga;
+    items_args(db, s[i], items[i], &ka, &ga);
+    std::memcpy(hb + o_ka + sizeof(AnchorArgs) * k, &ka, sizeof(AnchorArgs));
+    std::memcpy(hb + o_kg + sizeof(CaGroupArgs) * k, &ga, sizeof(CaGroupArgs));
+    reinterpret_cast<int32_t*>(hb + o_kb)[k] = nab;
+    nab += anchor_batch_blocks(s[i].C);
+  }
+  if (ni) reinterpret_cast<int32_t*>(hb + o_kb)[ni] = nab;
   stage_up(ctx, L.o, st);
   HIPCHK(hipGetLastError());
-  for (int i : live)
-    if (items && items[i] && (rc = launch_items(ctx, db, s[i], items[i], st))) return rc;
+  if (ni) {
+    double np = 0.0;
+    for (int i : withit) np += (double)s[i].NP;
+    Scope sc(ctx, PVT_K_OTHER, 0, 4.0 * np);
+    launch_anchor_batch(reinterpret_cast<const AnchorArgs*>(db + o_ka),
+                        reinterpret_cast<const int32_t*>(db + o_kb), ni, nab, st);
+    launch_ca_groups_batch(reinterpret_cast<const CaGroupArgs*>(db + o_kg), ni, st);
+  }
+  HIPCHK(hipGetLastError());
   // one resident launch for every round (one workgroup each; mixed policies branch per
   // workgroup), the MT states read and written through each descriptor's mt_state
   {

@@ -22,5 +22,6 @@ struct CaGroupArgs {
   int32_t* desc_n_groups;       // the device round descriptor's n_groups, or NULL
 };
 void launch_ca_groups(const CaGroupArgs& a, hipStream_t st);
+void launch_ca_groups_batch(const CaGroupArgs* args_dev, int n, hipStream_t st);
 
 }  // namespace pvt

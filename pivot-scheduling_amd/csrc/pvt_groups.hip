@@ -29,7 +29,7 @@ namespace pvt {
 constexpr int GR_THREADS = 1024;
 constexpr int GR_PER = GRP_MAX_TASKS / GR_THREADS;   // tasks per thread, keys kept in registers
 
-__global__ __launch_bounds__(GR_THREADS) void ca_groups_kernel(CaGroupArgs A) {
+__device__ __forceinline__ void ca_groups_round(const CaGroupArgs& A) {
   __shared__ int32_t first[GRP_MAX_KEYS];            // first task of each key, then its group
   __shared__ uint32_t appbit[GRP_MAX_TASKS / 32];    // group g is an application group
   __shared__ int32_t wsum[GR_THREADS / 64];
@@ -127,8 +127,19 @@ __global__ __launch_bounds__(GR_THREADS) void ca_groups_kernel(CaGroupArgs A) {
   }
 }
 
+__global__ __launch_bounds__(GR_THREADS) void ca_groups_kernel(CaGroupArgs A) { ca_groups_round(A); }
+
+// Several rounds' groupings in one launch, one workgroup each (pvt_place_host_batch).
+__global__ __launch_bounds__(GR_THREADS) void ca_groups_batch_kernel(const CaGroupArgs* A) {
+  const CaGroupArgs a = A[blockIdx.x];
+  ca_groups_round(a);
+}
+
 void launch_ca_groups(const CaGroupArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(ca_groups_kernel, dim3(1), dim3(GR_THREADS), 0, st, a);
+}
+void launch_ca_groups_batch(const CaGroupArgs* args_dev, int n, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(ca_groups_batch_kernel, dim3(n), dim3(GR_THREADS), 0, st, args_dev);
 }
 
 }  // namespace pvt
