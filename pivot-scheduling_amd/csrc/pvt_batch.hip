@@ -85,7 +85,8 @@ struct ResLds {
     mt = ci + 12 * RES_CHUNK;                          //       MT copies u32[WAVES][628]
     slot = mt + 4 * RES_MAXW * RES_MT_STRIDE;          //       posts u64[2][WAVES][2], then
     // fast posts i32[2][WAVES], then vbp best-fit s2 posts {u64, i32, i32}[2][WAVES]
-    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW;
+    // (+32: the sticky winner's capacities, f64[4])
+    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW + 32;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     // resident walk (after the sort, before the staging above): the round's hosts in LDS,
     // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], per-chunk zero-score masks u64[16],
@@ -527,6 +528,16 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
     for (int j = 0; j < HPL; j++) zmask |= (dbits(key[j]) == 0 ? 1u : 0u) << j;
   }
   const bool rt = (MODE == CA_FF || MODE == CA_BF) && R.rt_bw != nullptr;
+  // Sticky winner. A task whose demand is bit for bit the previous task's (same anchor, same
+  // group when keys or realtime bandwidths are per group), with every demand >= 0, takes the
+  // previous winner h again whenever h still fits: first-fit by index or by frozen key -- the
+  // hosts before h did not fit that demand and have not changed; best-fit (vbp, cost_aware) --
+  // h's residual only shrank (every component of a - d is >= 0 and fell), so its score did not
+  // grow, and no other host changed. Such a task needs no selection and no exchange between the
+  // waves: every wave tracks h's capacities (sc), broadcast once through LDS when a run starts.
+  double* skc = reinterpret_cast<double*>(smem + Lo.slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW);
+  int sh = -1;
+  double sc0 = 0.0, sc1 = 0.0, sc2 = 0.0, sc3 = 0.0;
   for (int p0 = p_start; p0 < T; p0 += RES_CHUNK) {
     const int n = min(RES_CHUNK, T - p0);
     __syncthreads();                      // the previous chunk (and the sort keys) are consumed
@@ -617,6 +628,28 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
       }
       RSTAMP(0);
       RCOUNT(6);
+      if (MODE != OPP && sh >= 0) {
+        // (sh >= 0 only when this task's demand, anchor and group equal the previous task's)
+        const bool ok = fits<STRICT>(sc0, sc1, sc2, sc3, d0, d1, d2, d3);
+        if (ok) {
+          sc0 -= d0; sc1 -= d1; sc2 -= d2; sc3 -= d3;
+          const int jw = sh & (HPL - 1);
+          if (sh / HPL == tid) {
+#pragma unroll
+            for (int j = 0; j < HPL; j++)
+              if (j == jw) { a0[j] -= d0; a1[j] -= d1; a2[j] -= d2; a3[j] -= d3; }   // resc[h] -= d
+            pl[p] = sh;
+          }
+          const bool same_next = q + 1 < n &&
+              dbits(n0) == dbits(d0) && dbits(n1) == dbits(d1) && dbits(n2) == dbits(d2) &&
+              dbits(n3) == dbits(d3) && (!CA || n_anc == anc_q) &&
+              (!((MODE == CA_FF && keyed) || rt) || n_grp == grp_q);
+          if (!same_next) sh = -1;
+          RSTAMP(5);
+          continue;
+        }
+        sh = -1;
+      }
       const int par = p & 1;
       if (MODE == OPP) {
         // feasible hosts of this lane (np.all(r >= d), opportunistic.py:15)
@@ -842,11 +875,28 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
       }
       if (hw == 0x7fffffff) continue;    // no host fits: the task stays waiting
       const int jw = hw & (HPL - 1);     // uniform: the owning lane's register slot
+      // a run of equal demands starts: the winner's capacities after this commit go to every
+      // wave (one LDS round trip and a barrier -- which also keeps this task's posts from being
+      // overwritten before every wave has read them, the parity scheme's guarantee, while the
+      // run's tasks go without a barrier)
+      const bool run_next = MODE != OPP && q + 1 < n &&
+          dbits(n0) == dbits(d0) && dbits(n1) == dbits(d1) && dbits(n2) == dbits(d2) &&
+          dbits(n3) == dbits(d3) && (!CA || n_anc == anc_q) &&
+          (!((MODE == CA_FF && keyed) || rt) || n_grp == grp_q) &&
+          d0 >= 0.0 && d1 >= 0.0 && d2 >= 0.0 && d3 >= 0.0;
       if (hw / HPL == tid) {
 #pragma unroll
         for (int j = 0; j < HPL; j++)
-          if (j == jw) { a0[j] -= d0; a1[j] -= d1; a2[j] -= d2; a3[j] -= d3; }   // resc[h] -= d
+          if (j == jw) {
+            a0[j] -= d0; a1[j] -= d1; a2[j] -= d2; a3[j] -= d3;   // resc[h] -= d
+            if (run_next) { skc[0] = a0[j]; skc[1] = a1[j]; skc[2] = a2[j]; skc[3] = a3[j]; }
+          }
         pl[p] = hw;
+      }
+      if (run_next) {
+        __syncthreads();
+        sc0 = skc[0]; sc1 = skc[1]; sc2 = skc[2]; sc3 = skc[3];
+        sh = hw;
       }
       RSTAMP(5);
     }

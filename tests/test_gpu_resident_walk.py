@@ -116,3 +116,24 @@ def test_mixed_host_batch_walks(engine):
         _same(g, ref, "mixed %d" % i)
         if ref.mt_state is not None:
             assert np.array_equal(g.mt_state, ref.mt_state)
+
+
+@pytest.mark.parametrize("mode", [_abi.PVT_CA_BF, _abi.PVT_CA_FF, _abi.PVT_VBP_FF, _abi.PVT_VBP_BF,
+                                  _abi.PVT_OPP])
+def test_sticky_runs_of_equal_demands(engine, engine_nowalk, mode):
+    """Long runs of bit-identical demands on hosts that take an exact number of copies (capacity
+    a multiple of the demand: the last copy leaves exactly 0, which fits a >= policy once more
+    and a strict one not): the sticky winner must hand over to the next host exactly where the
+    sequential loop does; a run with a negative demand component keeps the full selection."""
+    rounds = []
+    for s in range(4):
+        r = synthetic.make_round(mode, 600, 900, seed=140 + s)
+        rows = np.array([[0.5, 2048.0], [1.0, 4096.0], [0.25, 1024.0]])
+        pick = np.sort(np.random.RandomState(s).randint(0, 3, size=r.n_tasks))
+        r.dem[0], r.dem[1] = rows[pick, 0], rows[pick, 1]
+        r.avail[0] = 0.5 * np.random.RandomState(50 + s).randint(0, 9, size=r.n_hosts)
+        r.avail[1] = 2048.0 * np.random.RandomState(60 + s).randint(0, 9, size=r.n_hosts)
+        if s == 3:
+            r.dem[2, 100:140] = -1.0                # (a run with a negative demand component)
+        rounds.append(r)
+    _check(engine, engine_nowalk, rounds, "sticky runs mode %d" % mode)
