@@ -35,6 +35,7 @@ for s in "$@"; do
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
     t_rw)       run t_rw 400 $T tests/test_gpu_resident_walk.py tests/test_gpu_batch.py ;;
     b_c4w)      for m in ${C4M:-ca_bf ca_ff vbp_ff}; do run b_c4w_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
+    b_c4ab)     for m in ${C4M:-ca_bf ca_ff vbp_ff}; do PVT_RWALK=0 run b_c4nw_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
     hb_split)   TAILN=6 run hb_split 300 python tools/host_batch_split.py ;;
     t_host)     run t_host 400 $T tests/test_gpu_host_batch.py tests/test_lockstep.py tests/test_gpu_fused.py ;;
     b_lock)     run b_lock 300 python -c "import bench, json; from pivot_place.engine import PlacementEngine; e = PlacementEngine(0); bench.replay_workloads(e); print(json.dumps(bench.lockstep_workload(e)))" ;;
