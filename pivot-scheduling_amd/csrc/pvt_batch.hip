@@ -468,10 +468,13 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   }
   for (int i = tid; i < T; i += NT) G(R.order)[i] = ord[i];
 
-  // first-fit-shaped rounds of up to RW_MAXH hosts: one wave walks them (resident_walk); this
-  // path takes over where it stops, on the walked capacities (and the keyed walk's group keys)
+  // cost_aware best-fit rounds of up to RW_MAXH hosts: one wave walks them (resident_walk);
+  // this path takes over where it stops, on the walked capacities (and the keyed walk's group
+  // keys). The walk handles CA_FF / VBP_FF too, but there the block path's early-exit scan is
+  // cheaper (config 4, 512 rounds: ca_ff 0.753 vs 0.710 ms, vbp_ff 0.558 vs 0.524 ms walked vs
+  // not; ca_bf 0.743 vs 0.779 ms), so only CA_BF walks.
   int p_start = 0, kgrp = -1;
-  constexpr bool WALKABLE = (MODE == CA_BF || MODE == CA_FF || MODE == VBP_FF);
+  constexpr bool WALKABLE = (MODE == CA_BF);
   if (WALKABLE && A.walk && H <= RW_MAXH && T > 0 && !(CA && R.rt_bw)) {
 #ifdef PVT_STAMPS
     const uint64_t tw0 = rstamp();

@@ -86,6 +86,24 @@ def _torch():
     return torch
 
 
+_HB = []
+
+
+def _hostbatch():
+    """pivot_place._hostbatch, the C++ marshaller of place_host_batch (built next to
+    libpivot_place.so by the Makefile), or None when it is absent or PVT_HOSTBATCH=0 -- then
+    the ctypes marshalling builds the same descriptors for the same C call."""
+    if not _HB:
+        mod = None
+        if os.environ.get("PVT_HOSTBATCH", "1") != "0":
+            try:
+                from . import _hostbatch as mod
+            except ImportError:
+                mod = None
+        _HB.append(mod)
+    return _HB[0]
+
+
 class DeviceRound:
     """A round resident in HBM: torch tensors plus the pvt_round struct that points at them.
 
@@ -490,6 +508,9 @@ class PlacementEngine:
         n = len(reqs)
         if n == 0:
             return []
+        hb = _hostbatch()
+        if hb is not None:
+            return self._place_host_batch_cxx(hb, reqs)
         structs = (_abi.pvt_round * n)()
         items = (ctypes.POINTER(_abi.pvt_ca_items) * n)()
         outs, keep = [], []
@@ -514,6 +535,27 @@ class PlacementEngine:
             mt, status = ca
             try:
                 out.append(self._ca_result(res, rcs[i], mt, status))
+            except Exception as e:     # noqa: BLE001 -- handed to the caller of this round
+                out.append(e)
+        return out
+
+    def _place_host_batch_cxx(self, hb, reqs):
+        """place_host_batch with the descriptors built in C++ (csrc/pvt_hostpy.cpp): the same
+        C call, ~4x less host time per round than the ctypes structs above."""
+        fn = getattr(self, "_hb_fn", None)
+        if fn is None:
+            fn = self._hb_fn = ctypes.cast(self.lib.pvt_place_host_batch, ctypes.c_void_p).value
+        rc, results, rcs = hb.place_host_batch(fn, self.ctx.value, [r for r, _ in reqs],
+                                               [ca for _, ca in reqs])
+        self._check(rc)
+        out = []
+        for (placement, order, avail, mt, imt, status), rci in zip(results, rcs):
+            res = RoundResult(placement=placement, order=order, avail=avail, mt_state=mt)
+            if status is None:
+                out.append(res)
+                continue
+            try:
+                out.append(self._ca_result(res, rci, imt, status))
             except Exception as e:     # noqa: BLE001 -- handed to the caller of this round
                 out.append(e)
         return out

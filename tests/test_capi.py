@@ -85,3 +85,25 @@ def test_engine_refuses_to_run_without_gpu():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(OSError):
         engine.load_library(str(tmp_path / "libpivot_place.so"))
+
+
+def test_host_batch_marshaller_builds_descriptors_without_a_device():
+    """pivot_place._hostbatch (csrc/pvt_hostpy.cpp) marshals a mixed batch and makes the same
+    C call as the ctypes path; a null context is refused by pvt_place_host_batch itself."""
+    import numpy as np
+    hb = engine._hostbatch()
+    assert hb is not None, "pivot_place/_hostbatch*.so is not built (make -C pivot-scheduling_amd)"
+    lib = engine.load_library()
+    fn = ctypes.cast(lib.pvt_place_host_batch, ctypes.c_void_p).value
+    r = _abi.RoundArrays(mode=_abi.PVT_CA_BF, avail=np.ones((4, 5)), zone=np.zeros(5),
+                         dem=np.full((4, 3), 0.5), mt_state=np.arange(625))
+    ca = ([0, 0, 1], np.array([0, 1, 2]), [4, 3], [0, 0], 1, [0], [0], list(range(625)))
+    rc, results, rcs = hb.place_host_batch(fn, 0, [r, r], [None, ca])
+    assert rc == _abi.PVT_EINVAL and list(rcs) == [0, 0]
+    placement, order, avail, mt, imt, status = results[1]
+    assert placement.shape == (3,) and order.dtype == np.int32 and avail.shape == (4, 5)
+    assert (avail == 1).all() and avail is not r.avail and (mt == np.arange(625)).all()
+    assert imt.dtype == np.uint32 and list(status) == [0, 0]
+    assert results[0][4] is None and results[0][5] is None
+    with pytest.raises(ValueError):
+        hb.place_host_batch(fn, 0, [r], [ca[:7] + ([1, 2],)])

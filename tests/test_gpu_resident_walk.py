@@ -1,7 +1,8 @@
-"""The one-wave resident walk (pvt_batch.hip resident_walk): rounds of up to 1024 hosts of the
-first-fit-shaped policies -- cost_aware best-fit (score-0 winners), keyed and unsorted cost_aware
-first-fit, vbp first-fit -- are walked by one wave over their hosts in LDS, and the 4-wave path
-takes over where the walk stops. Every round must equal the CPU restatement, including rounds
+"""The one-wave resident walk (pvt_batch.hip resident_walk): cost_aware best-fit rounds of up to
+1024 hosts (score-0 winners) are walked by one wave over their hosts in LDS, and the 4-wave path
+takes over where the walk stops. (The walk also handles keyed / unsorted cost_aware first-fit and
+vbp first-fit, but those modes run the 4-wave path, measured faster; their cases stay here as
+resident-path checks of the same shapes.) Every round must equal the CPU restatement, including rounds
 built to stop the walk: no score-0 host (anchor zones without capacity), subnormal egress costs
 (risky scores), zero-key hosts running out inside a keyed group (the group's frozen keys are
 handed over), unplaceable tasks; and the same batch with the walk off (PVT_RWALK=0)."""

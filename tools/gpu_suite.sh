@@ -37,6 +37,7 @@ for s in "$@"; do
     b_c4w)      for m in ${C4M:-ca_bf ca_ff vbp_ff}; do run b_c4w_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
     b_c4ab)     for m in ${C4M:-ca_bf ca_ff vbp_ff}; do PVT_RWALK=0 run b_c4nw_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
     hb_split)   TAILN=6 run hb_split 300 python tools/host_batch_split.py ;;
+    hb_ab)      PVT_HOSTBATCH=0 TAILN=6 run hb_split0 300 python tools/host_batch_split.py && TAILN=6 run hb_split 300 python tools/host_batch_split.py ;;
     t_host)     run t_host 400 $T tests/test_gpu_host_batch.py tests/test_lockstep.py tests/test_gpu_fused.py ;;
     b_lock)     run b_lock 300 python -c "import bench, json; from pivot_place.engine import PlacementEngine; e = PlacementEngine(0); bench.replay_workloads(e); print(json.dumps(bench.lockstep_workload(e)))" ;;
     st_res)     for m in ${RES_MODES:-ca_bf vbp_bf vbp_ff ca_ff}; do run st_res_$m 120 python tools/resident_stamps.py $m; done ;;
