@@ -304,6 +304,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   if (bad) S.bail = 1;                        // benign race: every writer stores 1
   if (um) atomicOr(&S.umask, um);
   __syncthreads();
+#ifdef PVT_STAMPS
+  const uint64_t t_cert = zstamp();
+#endif
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     for (int w = 1; w < ZW_WAVES; w++) {
@@ -349,6 +352,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     compact_zone_window<WM>(A.zone, Z, U, 0, H, S.wid, S.wz, S.cnt, &S.nwin);
   }
   const int nwin = S.nwin;
+#ifdef PVT_STAMPS
+  const uint64_t t_win = zstamp();
+#endif
   bool wbad = false;
   static_assert(WM % (4 * ZW_THREADS) == 0, "window capacities: four hosts per thread per pass");
   for (int p0 = 0; p0 < WM && p0 < nwin; p0 += 4 * ZW_THREADS) {
@@ -375,6 +381,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   }
   if (wbad) S.bail = 1;
   __syncthreads();
+#ifdef PVT_STAMPS
+  const uint64_t t_cap = zstamp();
+#endif
   if (S.bail || nwin == 0) {
     if (tid == 0) { status[0] = 0; status[1] = KEYED ? 0 : 1; }
     return;
@@ -497,20 +506,35 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       auto pass1 = [&](auto dims) {
         constexpr int D = decltype(dims)::value;
         int u = __builtin_ctzll(m0), fb = 0;
+        uint64_t alive = m0;                     // lanes that took every copy so far
         for (;;) {
           t = __builtin_amdgcn_readfirstlane(t);
           u = __builtin_amdgcn_readfirstlane(u);
           fb = __builtin_amdgcn_readfirstlane(fb);
-          bool f = false;
+          // ZW_UNROLL copies, tested at the last one only: fits are monotone in the copy, so a
+          // lane that takes the last copy took all of them, and only the lanes that stop inside
+          // the step (once per lane) count their copies one by one
+          double y0[ZW_UNROLL], y1[ZW_UNROLL], y2[ZW_UNROLL], y3[ZW_UNROLL];
 #pragma unroll
-          for (int j = 1; j <= ZW_UNROLL; j++) {
+          for (int j = 0; j < ZW_UNROLL; j++) {
             x0 -= d0; x1 -= d1;
             if (D == 4) { x2 -= d2; x3 -= d3; }
-            f = fit_res<STRICT>(D == 4 ? fmin(fmin(x0, x1), fmin(x2, x3)) : fmin(x0, x1));
-            cnt = f ? t + j : cnt;
+            y0[j] = x0; y1[j] = x1; y2[j] = x2; y3[j] = x3;
           }
+          const bool f = fit_res<STRICT>(D == 4 ? fmin(fmin(x0, x1), fmin(x2, x3)) : fmin(x0, x1));
+          const uint64_t an = __ballot(f);       // lanes that took copy t + ZW_UNROLL
+          cnt = f ? t + ZW_UNROLL : cnt;
+          const uint64_t stop = alive & ~an;
+          if (UNI(stop != 0)) {
+            int c = t;
+#pragma unroll
+            for (int j = 0; j < ZW_UNROLL - 1; j++)
+              c += fit_res<STRICT>(D == 4 ? fmin(fmin(y0[j], y1[j]), fmin(y2[j], y3[j]))
+                                          : fmin(y0[j], y1[j])) ? 1 : 0;
+            cnt = ((stop >> lane) & 1ull) ? c : cnt;
+          }
+          alive = an;
           t += ZW_UNROLL;
-          const uint64_t an = __ballot(f);       // lanes that took copy t
           if (UNI(an == 0)) break;
           const int un = __builtin_ctzll(an);
           if (un != u) {                         // (u only rises: every lane below un is done)
@@ -551,24 +575,26 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       amax = max(amax, n);
     }
     if (lane < covered) S.lgid[k + lane] = who;
+    // (c - d as fma(-1, d, c), rounded once, the same bits; fma(-0, d, c) == c for the finite d
+    // and c of a proven chain: one 0/1 factor per copy for every dimension)
     if (two) {
       for (int m = 0; m < amax; m += 4) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-          const bool on = m + u < asg;
-          c0 = on ? c0 - d0 : c0;
-          c1 = on ? c1 - d1 : c1;
+          const double o = m + u < asg ? -1.0 : -0.0;
+          c0 = __builtin_fma(o, d0, c0);
+          c1 = __builtin_fma(o, d1, c1);
         }
       }
     } else {
       for (int m = 0; m < amax; m += 4) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-          const bool on = m + u < asg;
-          c0 = on ? c0 - d0 : c0;
-          c1 = on ? c1 - d1 : c1;
-          c2 = on ? c2 - d2 : c2;
-          c3 = on ? c3 - d3 : c3;
+          const double o = m + u < asg ? -1.0 : -0.0;
+          c0 = __builtin_fma(o, d0, c0);
+          c1 = __builtin_fma(o, d1, c1);
+          c2 = __builtin_fma(o, d2, c2);
+          c3 = __builtin_fma(o, d3, c3);
         }
       }
     }
@@ -970,6 +996,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     atomicAdd((unsigned long long*)&A.stamps[11], (unsigned long long)n_iter);
     atomicAdd((unsigned long long*)&A.stamps[12], (unsigned long long)st_batch);
     atomicAdd((unsigned long long*)&A.stamps[13], (unsigned long long)n_single);
+    atomicAdd((unsigned long long*)&A.stamps[16], (unsigned long long)(t_cert - t_start));
+    atomicAdd((unsigned long long*)&A.stamps[17], (unsigned long long)(t_win - t_cert));
+    atomicAdd((unsigned long long*)&A.stamps[18], (unsigned long long)(t_cap - t_win));
+    atomicAdd((unsigned long long*)&A.stamps[19], (unsigned long long)(t_walk - t_cap));
   }
 #endif
 }

@@ -19,17 +19,19 @@ mode = sys.argv[4] if len(sys.argv) > 4 else "ca_bf"
 eng = PlacementEngine(0, lib_path=os.path.join(ROOT, "pivot-scheduling_amd", "diag", lib))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-buf = (ctypes.c_uint64 * 16)()
-assert f(eng.ctx, buf, 16) == 0
+buf = (ctypes.c_uint64 * 32)()
+assert f(eng.ctx, buf, 32) == 0
 r = synthetic.make_round(MODES[mode], H, T)
 dr = DeviceRound(r, eng.device)
 eng.run(dr)
 torch.cuda.synchronize()
-assert f(eng.ctx, buf, 16) == 0
+assert f(eng.ctx, buf, 32) == 0
 st = eng.epoch_stats()
 nch = max(st["frontier_chains"] + st["list_chains"], 1)
 print("%s H=%d T=%d stats=%s" % (mode, H, T, st))
 print("  prologue   %10.0f cycles per chain" % (buf[0] / nch))
+print("    tables + demand scan %.0f, window ids %.0f, window capacities %.0f, suffix minima %.0f"
+      % tuple(buf[16 + k] / nch for k in range(4)))
 print("  walk       %10.0f cycles per chain, %.0f per task" % (buf[1] / nch, buf[1] / max(buf[3], 1)))
 print("  chunks     %10.2f per task" % (buf[2] / max(buf[3], 1)))
 print("  tasks      %10d, anchor switches %d" % (buf[3], buf[4]))
