@@ -57,7 +57,10 @@ constexpr int ZW_SCAN = 16;                // hosts per thread per window-build 
 constexpr int ZW_MINB = ZW_MIN_PARTS;      // blocks of the host-minimum pass
 constexpr double ZW_BIG = 0x1p500;
 
-constexpr int ZW_UNROLL = 4;               // run_bulk pass 1: copies per stop check
+#ifndef PVT_ZW_UNROLL
+#define PVT_ZW_UNROLL 4
+#endif
+constexpr int ZW_UNROLL = PVT_ZW_UNROLL;   // run_bulk pass 1: copies per stop check
 constexpr int ZW_SB = 64;                  // suffix-minimum batches (the last one holds the rest)
 template <int WM>
 struct ZwalkLDS {
@@ -77,9 +80,27 @@ struct ZwalkLDS {
   int32_t nwin, bail;
 };
 
+// Wave reductions of doubles, uniform results: DPP row prefix steps (lane 15 of each 16-lane row
+// then holds the row's result), then the four rows by readlane -- no LDS permutes.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = dpp_u32<CTRL>((uint32_t)b, (uint32_t)b);
+  const uint32_t hi = dpp_u32<CTRL>((uint32_t)(b >> 32), (uint32_t)(b >> 32));
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+template <class Op>
+__device__ __forceinline__ double wave_reduce_d(double v, Op op) {
+  v = op(v, dpp_d<DPP_ROW_SHR1>(v));
+  v = op(v, dpp_d<DPP_ROW_SHR2>(v));
+  v = op(v, dpp_d<DPP_ROW_SHR4>(v));
+  v = op(v, dpp_d<DPP_ROW_SHR8>(v));
+  const double r0 = readlane_d(v, 15), r1 = readlane_d(v, 31);
+  const double r2 = readlane_d(v, 47), r3 = readlane_d(v, 63);
+  return op(op(r0, r1), op(r2, r3));
+}
 __device__ __forceinline__ double wave_max_d(double v) {
-  for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off));
-  return v;
+  return wave_reduce_d(v, [](double a, double b) { return fmax(a, b); });
 }
 // NaN-propagating maximum (fmax drops a NaN operand): the FF certificate (2') must fail on a NaN
 // capacity, whose frozen key would break the reference's sorted() order (cost_aware.py:116).
@@ -87,12 +108,10 @@ __device__ __forceinline__ double nan_max(double a, double b) {
   return (a != a || b <= a) ? a : b;
 }
 __device__ __forceinline__ double wave_nmax_d(double v) {
-  for (int off = 32; off > 0; off >>= 1) v = nan_max(v, __shfl_xor(v, off));
-  return v;
+  return wave_reduce_d(v, [](double a, double b) { return nan_max(a, b); });
 }
 __device__ __forceinline__ double wave_min_d(double v) {
-  for (int off = 32; off > 0; off >>= 1) v = fmin(v, __shfl_xor(v, off));
-  return v;
+  return wave_reduce_d(v, [](double a, double b) { return fmin(a, b); });
 }
 
 // Per-dimension minimum capacity over hosts [lo, hi) (certificate 2), ZW_MINB partials.
@@ -144,16 +163,22 @@ __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, 
                                                     int h_lo, int h_hi, int32_t* wid, int32_t* wz,
                                                     int32_t (*cnt)[ZW_WAVES], int32_t* nwin) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int zz[ZW_SCAN];
+#pragma unroll
+  for (int k = 0; k < ZW_SCAN; k++) {
+    const int h = h_lo + k * ZW_THREADS + tid;
+    zz[k] = h < h_hi ? zone[h] : -1;
+  }
   for (int h0 = h_lo; h0 < h_hi; h0 += ZW_SCAN * ZW_THREADS) {
     const int have = *nwin;
     if (have >= WM) break;
-    bool hit[ZW_SCAN];
-    int zz[ZW_SCAN];
+    int zn[ZW_SCAN];                         // the next pass's zones, in flight during this one
 #pragma unroll
     for (int k = 0; k < ZW_SCAN; k++) {
-      const int h = h0 + k * ZW_THREADS + tid;
-      zz[k] = h < h_hi ? zone[h] : -1;
+      const int h = h0 + ZW_SCAN * ZW_THREADS + k * ZW_THREADS + tid;
+      zn[k] = h < h_hi ? zone[h] : -1;
     }
+    bool hit[ZW_SCAN];
 #pragma unroll
     for (int k = 0; k < ZW_SCAN; k++) {
       const int z = zz[k];
@@ -179,6 +204,8 @@ __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, 
     __syncthreads();
     if (tid == 0) *nwin = min(pre, WM);
     __syncthreads();
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) zz[k] = zn[k];
   }
 }
 
@@ -215,8 +242,40 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   int32_t* status = A.status + 2 * b;
   const int Z = A.Z, H = A.H;
 
-  if (!KEYED)   // (keyed / ordered rounds: no zone tables; vbp rounds have none)
-    for (int i = tid; i < Z * Z; i += ZW_THREADS) { S.csum[i] = A.csum[i]; S.bsum[i] = A.bsum[i]; }
+  // Every load the prologue needs that depends on nothing else is issued first (the zone
+  // tables, the host minima, the chain's first task positions, its segment range), so the
+  // prologue waits for about two HBM latencies, not one per step.
+  static_assert(ZMAX * ZMAX <= 4 * ZW_THREADS && ZW_MINB == ZW_THREADS, "prologue loads");
+  const int ZZ = KEYED ? 0 : Z * Z;
+  double cs[4], bs[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int i = tid + u * ZW_THREADS;
+    cs[u] = i < ZZ ? A.csum[i] : 0.0;
+    bs[u] = i < ZZ ? A.bsum[i] : 0.0;
+  }
+  // host minima (FF: maxima of |capacity|) from the partials
+  double ha[4] = {FF ? -DINF : DINF, FF ? -DINF : DINF, FF ? -DINF : DINF, FF ? -DINF : DINF};
+  if (!KEYED) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const double x = A.hmin[tid * 4 + r];
+      ha[r] = FF ? nan_max(ha[r], x) : fmin(ha[r], x);
+    }
+  }
+  int wv[4];
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int i = u * ZW_THREADS + tid;
+    wv[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
+  }
+  const int sg0 = (!KEYED && A.cseg) ? A.csoff[b] : 0, sg1 = (!KEYED && A.cseg) ? A.csoff[b + 1] : 0;
+
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const int i = tid + u * ZW_THREADS;
+    if (i < ZZ) { S.csum[i] = cs[u]; S.bsum[i] = bs[u]; }
+  }
   if (tid == 0) { S.umask = 0; S.nwin = 0; S.bail = 0; }
   if (tid < CHAIN_MAX / 64) S.sbits[tid] = 0;
   __syncthreads();
@@ -225,34 +284,32 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     for (int z = 0; z < Z; z++) m |= (S.csum[tid * Z + z] == 0.0) ? (1u << z) : 0u;
     S.amask[tid] = m;
   }
-  if (!KEYED && A.cseg) {                    // segment starts (chain-local positions)
-    for (int k = A.csoff[b] + tid; k < A.csoff[b + 1]; k += ZW_THREADS) {
-      const int p = A.cseg[k];
-      if (p > 0 && p < CHAIN_MAX) atomicOr(&S.sbits[p >> 6], 1ull << (p & 63));
-    }
+  for (int k = sg0 + tid; k < sg1; k += ZW_THREADS) {   // segment starts (chain-local positions)
+    const int p = A.cseg[k];
+    if (p > 0 && p < CHAIN_MAX) atomicOr(&S.sbits[p >> 6], 1ull << (p & 63));
   }
-  __syncthreads();
 
-  // the chain's zones U, demand extremes and finiteness (certificates 2, 3), and the minima of
-  // the demands per 64-task batch (for the suffix minima below: a wave's 64 lanes of one pass
-  // are one batch); four rows per thread in flight at once
-  uint32_t um = 0;
+  // the chain's anchors (-> its zones U below), demand extremes and finiteness (certificates 2,
+  // 3), and the minima of the demands per 64-task batch (for the suffix minima below: a wave's
+  // 64 lanes of one pass are one batch); four rows per thread in flight at once, the next pass's
+  // positions loaded while this one is reduced
+  uint32_t abits = 0;                        // anchors seen (Z <= 32)
   double mx[4] = {-DINF, -DINF, -DINF, -DINF}, mn[4] = {DINF, DINF, DINF, DINF};
   bool bad = false;
   for (int i0 = 0; i0 < nt; i0 += 4 * ZW_THREADS) {
-    int wv[4], av[4];
+    int av[4], wn[4];
     double dv[4][4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = i0 + u * ZW_THREADS + tid;
-      wv[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
-    }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const int w = max(wv[u], 0);
       av[u] = A.anc[w];
 #pragma unroll
       for (int r = 0; r < 4; r++) dv[u][r] = A.dem[(size_t)w * 4 + r];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = i0 + 4 * ZW_THREADS + u * ZW_THREADS + tid;
+      wn[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -265,7 +322,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         if (a < 0 || a >= Z) {
           bad = true;
         } else {
-          if (!KEYED) um |= S.amask[a];
+          abits |= 1u << a;
 #pragma unroll
           for (int r = 0; r < 4; r++) {
             bad |= !(__builtin_fabs(dv[u][r]) <= ZW_BIG);
@@ -284,13 +341,13 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         }
       }
     }
-  }
-  // host minima (FF: maxima of |capacity|) from the partials
-  double ha[4] = {FF ? -DINF : DINF, FF ? -DINF : DINF, FF ? -DINF : DINF, FF ? -DINF : DINF};
-  if (!KEYED)
-    for (int k = tid; k < ZW_MINB; k += ZW_THREADS)
 #pragma unroll
-      for (int r = 0; r < 4; r++) ha[r] = FF ? nan_max(ha[r], A.hmin[k * 4 + r]) : fmin(ha[r], A.hmin[k * 4 + r]);
+    for (int u = 0; u < 4; u++) wv[u] = wn[u];
+  }
+  __syncthreads();                           // (amask)
+  uint32_t um = 0;
+  if (!KEYED)
+    for (uint32_t m = abits; m; m &= m - 1) um |= S.amask[__builtin_ctz(m)];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     mx[r] = wave_max_d(mx[r]);
@@ -408,8 +465,13 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     }
   }
   __syncthreads();
-  if (tid < 4)
-    for (int blk = nsb - 2; blk >= 0; blk--) S.smin[blk][tid] = fmin(S.smin[blk][tid], S.smin[blk + 1][tid]);
+  static_assert(ZW_SB == 64 && ZW_WAVES == 4, "suffix minima: one wave per dimension, a lane per batch");
+  {                                          // suffix minima: wave r scans dimension r
+    double v = lane < nsb ? S.smin[lane][wave] : DINF;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v = fmin(v, __shfl_down(v, off));
+    if (lane < nsb) S.smin[lane][wave] = v;
+  }
   __syncthreads();
   if (wave != 0) return;
 #ifdef PVT_STAMPS
@@ -506,35 +568,20 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       auto pass1 = [&](auto dims) {
         constexpr int D = decltype(dims)::value;
         int u = __builtin_ctzll(m0), fb = 0;
-        uint64_t alive = m0;                     // lanes that took every copy so far
         for (;;) {
           t = __builtin_amdgcn_readfirstlane(t);
           u = __builtin_amdgcn_readfirstlane(u);
           fb = __builtin_amdgcn_readfirstlane(fb);
-          // ZW_UNROLL copies, tested at the last one only: fits are monotone in the copy, so a
-          // lane that takes the last copy took all of them, and only the lanes that stop inside
-          // the step (once per lane) count their copies one by one
-          double y0[ZW_UNROLL], y1[ZW_UNROLL], y2[ZW_UNROLL], y3[ZW_UNROLL];
+          bool f = false;
 #pragma unroll
-          for (int j = 0; j < ZW_UNROLL; j++) {
+          for (int j = 1; j <= ZW_UNROLL; j++) {
             x0 -= d0; x1 -= d1;
             if (D == 4) { x2 -= d2; x3 -= d3; }
-            y0[j] = x0; y1[j] = x1; y2[j] = x2; y3[j] = x3;
+            f = fit_res<STRICT>(D == 4 ? fmin(fmin(x0, x1), fmin(x2, x3)) : fmin(x0, x1));
+            cnt = f ? t + j : cnt;
           }
-          const bool f = fit_res<STRICT>(D == 4 ? fmin(fmin(x0, x1), fmin(x2, x3)) : fmin(x0, x1));
-          const uint64_t an = __ballot(f);       // lanes that took copy t + ZW_UNROLL
-          cnt = f ? t + ZW_UNROLL : cnt;
-          const uint64_t stop = alive & ~an;
-          if (UNI(stop != 0)) {
-            int c = t;
-#pragma unroll
-            for (int j = 0; j < ZW_UNROLL - 1; j++)
-              c += fit_res<STRICT>(D == 4 ? fmin(fmin(y0[j], y1[j]), fmin(y2[j], y3[j]))
-                                          : fmin(y0[j], y1[j])) ? 1 : 0;
-            cnt = ((stop >> lane) & 1ull) ? c : cnt;
-          }
-          alive = an;
           t += ZW_UNROLL;
+          const uint64_t an = __ballot(f);       // lanes that took copy t
           if (UNI(an == 0)) break;
           const int un = __builtin_ctzll(an);
           if (un != u) {                         // (u only rises: every lane below un is done)
