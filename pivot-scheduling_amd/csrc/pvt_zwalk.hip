@@ -1043,10 +1043,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     atomicAdd((unsigned long long*)&A.stamps[11], (unsigned long long)n_iter);
     atomicAdd((unsigned long long*)&A.stamps[12], (unsigned long long)st_batch);
     atomicAdd((unsigned long long*)&A.stamps[13], (unsigned long long)n_single);
-    atomicAdd((unsigned long long*)&A.stamps[16], (unsigned long long)(t_cert - t_start));
-    atomicAdd((unsigned long long*)&A.stamps[17], (unsigned long long)(t_win - t_cert));
-    atomicAdd((unsigned long long*)&A.stamps[18], (unsigned long long)(t_cap - t_win));
-    atomicAdd((unsigned long long*)&A.stamps[19], (unsigned long long)(t_walk - t_cap));
+    atomicAdd((unsigned long long*)&A.stamps[20], (unsigned long long)(t_cert - t_start));
+    atomicAdd((unsigned long long*)&A.stamps[21], (unsigned long long)(t_win - t_cert));
+    atomicAdd((unsigned long long*)&A.stamps[22], (unsigned long long)(t_cap - t_win));
+    atomicAdd((unsigned long long*)&A.stamps[23], (unsigned long long)(t_walk - t_cap));
   }
 #endif
 }

@@ -33,6 +33,7 @@ for s in "$@"; do
     st_zw)      for m in ca_bf vbp_ff ca_ff; do run st_$m 120 python tools/zwalk_stamps.py 1000000 10000 libpivot_place_stamps.so $m; done ;;
     st_var)     for v in ${VARS:-stamps}; do for m in ${STM:-ca_bf}; do TAILN=13 run st_${v}_$m 120 python tools/zwalk_stamps.py 1000000 10000 libpivot_place_$v.so $m; done; done ;;
     b_var)      for v in ${VARS:-u8}; do for m in ${BM:-ca_bf}; do PIVOT_PLACE_LIB=pivot-scheduling_amd/diag/libpivot_place_$v.so run b_${v}_$m 150 python bench.py --mode $m $NB --steps 20; done; done ;;
+    st_ord)     TAILN=6 run st_ord 120 python tools/order_stamps.py ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
     t_rw)       run t_rw 400 $T tests/test_gpu_resident_walk.py tests/test_gpu_batch.py ;;

@@ -31,7 +31,7 @@ nch = max(st["frontier_chains"] + st["list_chains"], 1)
 print("%s H=%d T=%d stats=%s" % (mode, H, T, st))
 print("  prologue   %10.0f cycles per chain" % (buf[0] / nch))
 print("    tables + demand scan %.0f, window ids %.0f, window capacities %.0f, suffix minima %.0f"
-      % tuple(buf[16 + k] / nch for k in range(4)))
+      % tuple(buf[20 + k] / nch for k in range(4)))
 print("  walk       %10.0f cycles per chain, %.0f per task" % (buf[1] / nch, buf[1] / max(buf[3], 1)))
 print("  chunks     %10.2f per task" % (buf[2] / max(buf[3], 1)))
 print("  tasks      %10d, anchor switches %d" % (buf[3], buf[4]))
