@@ -1082,18 +1082,17 @@ __global__ __launch_bounds__(1024) void order_count_kernel(PrepArgs A) {
       const int i = i0 + u * 1024 + t;
       gv[u] = i < T ? A.tg[i] : -2;
     }
-    // one LDS atomic per distinct group of a wave's 64 tasks (a group's tasks are contiguous
-    // in the trace: 64 same-address atomics per wave serialised the kernel)
+    // a wave whose 64 tasks share one group (the trace lists an application's tasks together)
+    // takes ONE atomic: 64 same-address LDS atomics serialise; mixed waves add lane by lane
 #pragma unroll
     for (int u = 0; u < PB; u++) {
       const int q = gv[u] == -2 ? -1 : ((gv[u] >= 0 && gv[u] < G) ? gv[u] : G);   // G: out of range
-      uint64_t pend = __ballot(q >= 0);
-      while (pend) {
-        const int leader = __builtin_ctzll(pend);
-        const int lq = __builtin_amdgcn_readlane(q, leader);
-        const uint64_t m = __ballot(q == lq) & pend;
-        if ((t & 63) == leader) atomicAdd(&cnt[lq], __popcll(m));
-        pend &= ~m;
+      const int q0 = __builtin_amdgcn_readfirstlane(q);
+      const uint64_t same = __ballot(q == q0);
+      if (same == ~0ull) {
+        if ((t & 63) == 0 && q0 >= 0) atomicAdd(&cnt[q0], 64);
+      } else if (q >= 0) {
+        atomicAdd(&cnt[q], 1);
       }
     }
   }
@@ -1181,45 +1180,6 @@ void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted, bo
   if (scatter) hipLaunchKernelGGL(order_scatter_kernel, dim3(1), dim3(1024), 0, st, a);
 }
 
-// Lane exchange x[lane ^ S] for the bitonic register stages: DPP for S <= 8 (quad permutes and
-// row mirrors: i ^ 4 = (i ^ 7) ^ 3, i ^ 8 = (i ^ 15) ^ 7), an LDS swizzle for 16, a permute for
-// 32 -- the DPP forms are VALU moves with no LDS round trip.
-template <int S>
-__device__ __forceinline__ int lane_xor(int x) {
-  constexpr int QP_X1 = 0xB1, QP_X2 = 0x4E, QP_X3 = 0x1B, ROW_MIRROR = 0x140, ROW_HALF_MIRROR = 0x141;
-  if constexpr (S == 1) return __builtin_amdgcn_update_dpp(x, x, QP_X1, 0xf, 0xf, false);
-  if constexpr (S == 2) return __builtin_amdgcn_update_dpp(x, x, QP_X2, 0xf, 0xf, false);
-  if constexpr (S == 4) {
-    const int h = __builtin_amdgcn_update_dpp(x, x, ROW_HALF_MIRROR, 0xf, 0xf, false);
-    return __builtin_amdgcn_update_dpp(h, h, QP_X3, 0xf, 0xf, false);
-  }
-  if constexpr (S == 8) {
-    const int m = __builtin_amdgcn_update_dpp(x, x, ROW_MIRROR, 0xf, 0xf, false);
-    return __builtin_amdgcn_update_dpp(m, m, ROW_HALF_MIRROR, 0xf, 0xf, false);
-  }
-  if constexpr (S == 16) return __builtin_amdgcn_ds_swizzle(x, 0x1f | (0x10 << 10));
-  return __shfl_xor(x, S);
-}
-
-// One compare-exchange stage of stride S < 64 over the thread's register elements.
-template <int S, int EMAX>
-__device__ __forceinline__ void bitonic_reg_stage(uint64_t (&rk)[EMAX], int32_t (&rv)[EMAX], int E,
-                                                  int size, int tid) {
-#pragma unroll
-  for (int m = 0; m < EMAX; m++) {
-    if (m >= E) continue;
-    const int i = m * 1024 + tid;
-    const uint32_t klo = (uint32_t)rk[m], khi = (uint32_t)(rk[m] >> 32);
-    const uint64_t pk = ((uint64_t)(uint32_t)lane_xor<S>((int)khi) << 32) | (uint32_t)lane_xor<S>((int)klo);
-    const int32_t pv = lane_xor<S>(rv[m]);
-    const bool up = (i & size) == 0, low = (i & S) == 0;
-    const uint64_t kl = low ? rk[m] : pk, kh = low ? pk : rk[m];
-    const int32_t vl = low ? rv[m] : pv, vh = low ? pv : rv[m];
-    const bool gt = kl > kh || (kl == kh && vl > vh);
-    if (gt == up) { rk[m] = pk; rv[m] = pv; }
-  }
-}
-
 // Sorts the n <= GSORT_MAX (key, task) pairs in LDS k / v by (key, task) ascending; on return
 // (after a barrier) v[0, n) holds the tasks in order. Block of 1024 threads, every one calling.
 __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
@@ -1284,15 +1244,20 @@ __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
       __syncthreads();
     }
     // (waves whose elements are all padding, i >= P, only ever pair with padding: they skip)
-    if ((tid & ~63) < P) {
-      switch (stride) {                      // (uniform: falls through the smaller strides)
-        case 32: bitonic_reg_stage<32>(rk, rv, E, size, tid); [[fallthrough]];
-        case 16: bitonic_reg_stage<16>(rk, rv, E, size, tid); [[fallthrough]];
-        case 8: bitonic_reg_stage<8>(rk, rv, E, size, tid); [[fallthrough]];
-        case 4: bitonic_reg_stage<4>(rk, rv, E, size, tid); [[fallthrough]];
-        case 2: bitonic_reg_stage<2>(rk, rv, E, size, tid); [[fallthrough]];
-        case 1: bitonic_reg_stage<1>(rk, rv, E, size, tid); [[fallthrough]];
-        default: break;
+    for (; stride > 0 && (tid & ~63) < P; stride >>= 1) {
+#pragma unroll
+      for (int m = 0; m < EMAX; m++) {
+        if (m >= E) continue;
+        const int i = m * 1024 + tid;
+        const uint32_t klo = (uint32_t)rk[m], khi = (uint32_t)(rk[m] >> 32);
+        const uint64_t pk = ((uint64_t)(uint32_t)__shfl_xor((int)khi, stride) << 32) |
+                            (uint32_t)__shfl_xor((int)klo, stride);
+        const int32_t pv = __shfl_xor(rv[m], stride);
+        const bool up = (i & size) == 0, low = (i & stride) == 0;
+        const uint64_t kl = low ? rk[m] : pk, kh = low ? pk : rk[m];
+        const int32_t vl = low ? rv[m] : pv, vh = low ? pv : rv[m];
+        const bool gt = kl > kh || (kl == kh && vl > vh);
+        if (gt == up) { rk[m] = pk; rv[m] = pv; }
       }
     }
   }
@@ -1398,7 +1363,7 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   __syncthreads();
   GSTAMP(0);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  constexpr int PB = 16;
+  constexpr int PB = 8;
   for (int i0 = 0; i0 < T; i0 += 1024 * PB) {
     // the groups of the batch's tasks (keys come after the collection: only the group's own
     // tasks' demands are read and only they take the norm -- computed in the scan, every wave

@@ -187,19 +187,32 @@ __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, 
       if (lane == 0) cnt[k][wave] = __popcll(m);
     }
     __syncthreads();
+    // every row's counts read before any window store (the stores may alias cnt for the
+    // compiler, which then re-read it after each one: a serial LDS chain per pass)
+    int before[ZW_SCAN], rowtot[ZW_SCAN];
+#pragma unroll
+    for (int k = 0; k < ZW_SCAN; k++) {
+      int bf = 0, tt = 0;
+#pragma unroll
+      for (int w = 0; w < ZW_WAVES; w++) {
+        const int c = cnt[k][w];
+        bf += (w < wave) ? c : 0;
+        tt += c;
+      }
+      before[k] = bf;
+      rowtot[k] = tt;
+    }
     int pre = have;
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int k = 0; k < ZW_SCAN; k++) {
-      int before = 0;
-      for (int w = 0; w < ZW_WAVES; w++) before += (w < wave) ? cnt[k][w] : 0;
       const uint64_t m = __ballot(hit[k]);
-      const int pos = pre + before + __popcll(m & below);
+      const int pos = pre + before[k] + __popcll(m & below);
       if (hit[k] && pos < WM) {
         wid[pos] = h0 + k * ZW_THREADS + tid;
         if (wz) wz[pos] = zz[k];
       }
-      for (int w = 0; w < ZW_WAVES; w++) pre += cnt[k][w];
+      pre += rowtot[k];
     }
     __syncthreads();
     if (tid == 0) *nwin = min(pre, WM);
