@@ -53,12 +53,13 @@ namespace pvt {
 constexpr int ZW_MBIG = 3072;              // the large window (a retry for chains that outgrow ZW_M)
 constexpr int ZW_THREADS = 256;
 constexpr int ZW_WAVES = ZW_THREADS / 64;
-constexpr int ZW_SCAN = 16;                // hosts per thread per window-build pass
+constexpr int ZW_SCAN = 8;                 // 16-byte zone loads (4 hosts) per thread per window-build pass
 constexpr int ZW_MINB = ZW_MIN_PARTS;      // blocks of the host-minimum pass
+constexpr int ZW_PR = 8;                   // chain task rows per thread per prologue pass
 constexpr double ZW_BIG = 0x1p500;
 
 #ifndef PVT_ZW_UNROLL
-#define PVT_ZW_UNROLL 4
+#define PVT_ZW_UNROLL 8
 #endif
 constexpr int ZW_UNROLL = PVT_ZW_UNROLL;   // run_bulk pass 1: copies per stop check
 constexpr int ZW_SB = 64;                  // suffix-minimum batches (the last one holds the rest)
@@ -156,35 +157,56 @@ __device__ __forceinline__ void wave_lds_sync() {
 }
 
 // The first WM hosts of [h_lo, h_hi), in index order, whose zone is in the mask U, appended
-// to wid / wz from *nwin on (passes of ZW_SCAN x 256 hosts, every zone load of a pass in flight
-// at once, a stable block compaction; the block stops at the pass that fills the window).
+// to wid / wz from *nwin on: passes of ZW_SCAN rows x 256 threads x 4 hosts (one 16-byte zone
+// load per thread and row, every load of a pass in flight at once, the next pass's issued before
+// this one is compacted), a stable block compaction (per row: a DPP scan of the threads' hit
+// counts, the waves' totals through LDS); the block stops at the pass that fills the window.
 template <int WM = ZW_M>
 __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, uint32_t U,
                                                     int h_lo, int h_hi, int32_t* wid, int32_t* wz,
                                                     int32_t (*cnt)[ZW_WAVES], int32_t* nwin) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  int zz[ZW_SCAN];
+  constexpr int SPAN = ZW_SCAN * ZW_THREADS * 4;
+  const int a_lo = h_lo & ~3;
+  // (16-byte loads need a 16-byte aligned zone array: a caller's offset pointer takes the
+  // element loads, as does the last partial quad)
+  const bool vec = ((uintptr_t)zone & 15) == 0;
+  auto load = [&](int hb) -> int4 {
+    if (vec && hb + 4 <= h_hi) return *reinterpret_cast<const int4*>(zone + hb);
+    int4 r;
+    r.x = hb < h_hi ? zone[hb] : -1;
+    r.y = hb + 1 < h_hi ? zone[hb + 1] : -1;
+    r.z = hb + 2 < h_hi ? zone[hb + 2] : -1;
+    r.w = hb + 3 < h_hi ? zone[hb + 3] : -1;
+    return r;
+  };
+  int4 zz[ZW_SCAN];
 #pragma unroll
-  for (int k = 0; k < ZW_SCAN; k++) {
-    const int h = h_lo + k * ZW_THREADS + tid;
-    zz[k] = h < h_hi ? zone[h] : -1;
-  }
-  for (int h0 = h_lo; h0 < h_hi; h0 += ZW_SCAN * ZW_THREADS) {
+  for (int k = 0; k < ZW_SCAN; k++) zz[k] = load(a_lo + (k * ZW_THREADS + tid) * 4);
+  for (int h0 = a_lo; h0 < h_hi; h0 += SPAN) {
     const int have = *nwin;
     if (have >= WM) break;
-    int zn[ZW_SCAN];                         // the next pass's zones, in flight during this one
+    int4 zn[ZW_SCAN];                        // the next pass's zones, in flight during this one
+    if (h0 + SPAN < h_hi) {
 #pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) {
-      const int h = h0 + ZW_SCAN * ZW_THREADS + k * ZW_THREADS + tid;
-      zn[k] = h < h_hi ? zone[h] : -1;
+      for (int k = 0; k < ZW_SCAN; k++) zn[k] = load(h0 + SPAN + (k * ZW_THREADS + tid) * 4);
     }
-    bool hit[ZW_SCAN];
+    uint32_t hm[ZW_SCAN];                    // per row: bit c = host hb + c is a window host
+    int ex[ZW_SCAN];                         //   its hits before this thread's, in the wave
 #pragma unroll
     for (int k = 0; k < ZW_SCAN; k++) {
-      const int z = zz[k];
-      hit[k] = z >= 0 && z < Z && ((U >> z) & 1u);
-      const uint64_t m = __ballot(hit[k]);
-      if (lane == 0) cnt[k][wave] = __popcll(m);
+      const int hb = h0 + (k * ZW_THREADS + tid) * 4;
+      const int zc[4] = {zz[k].x, zz[k].y, zz[k].z, zz[k].w};
+      uint32_t m = 0;
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        m |= (hb + c >= h_lo && zc[c] >= 0 && zc[c] < Z && ((U >> zc[c]) & 1u)) ? (1u << c) : 0u;
+      hm[k] = m;
+      const int n = __popc(m);
+      const int incl = wave_incl_scan_dpp(n);
+      ex[k] = incl - n;
+      const int tot = __builtin_amdgcn_readlane(incl, 63);
+      if (lane == 0) cnt[k][wave] = tot;
     }
     __syncthreads();
     // every row's counts read before any window store (the stores may alias cnt for the
@@ -203,22 +225,30 @@ __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, 
       rowtot[k] = tt;
     }
     int pre = have;
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
 #pragma unroll
     for (int k = 0; k < ZW_SCAN; k++) {
-      const uint64_t m = __ballot(hit[k]);
-      const int pos = pre + before[k] + __popcll(m & below);
-      if (hit[k] && pos < WM) {
-        wid[pos] = h0 + k * ZW_THREADS + tid;
-        if (wz) wz[pos] = zz[k];
+      const int hb = h0 + (k * ZW_THREADS + tid) * 4;
+      const int zc[4] = {zz[k].x, zz[k].y, zz[k].z, zz[k].w};
+      int pos = pre + before[k] + ex[k];
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        if ((hm[k] >> c) & 1u) {
+          if (pos < WM) {
+            wid[pos] = hb + c;
+            if (wz) wz[pos] = zc[c];
+          }
+          pos++;
+        }
       }
       pre += rowtot[k];
     }
     __syncthreads();
     if (tid == 0) *nwin = min(pre, WM);
     __syncthreads();
+    if (h0 + SPAN < h_hi) {
 #pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) zz[k] = zn[k];
+      for (int k = 0; k < ZW_SCAN; k++) zz[k] = zn[k];
+    }
   }
 }
 
@@ -276,9 +306,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       ha[r] = FF ? nan_max(ha[r], x) : fmin(ha[r], x);
     }
   }
-  int wv[4];
+  int wv[ZW_PR];
 #pragma unroll
-  for (int u = 0; u < 4; u++) {
+  for (int u = 0; u < ZW_PR; u++) {
     const int i = u * ZW_THREADS + tid;
     wv[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
   }
@@ -304,28 +334,28 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 
   // the chain's anchors (-> its zones U below), demand extremes and finiteness (certificates 2,
   // 3), and the minima of the demands per 64-task batch (for the suffix minima below: a wave's
-  // 64 lanes of one pass are one batch); four rows per thread in flight at once, the next pass's
+  // 64 lanes of one pass are one batch); ZW_PR rows per thread in flight at once, the next pass's
   // positions loaded while this one is reduced
   uint32_t abits = 0;                        // anchors seen (Z <= 32)
   double mx[4] = {-DINF, -DINF, -DINF, -DINF}, mn[4] = {DINF, DINF, DINF, DINF};
   bool bad = false;
-  for (int i0 = 0; i0 < nt; i0 += 4 * ZW_THREADS) {
-    int av[4], wn[4];
-    double dv[4][4];
+  for (int i0 = 0; i0 < nt; i0 += ZW_PR * ZW_THREADS) {
+    int av[ZW_PR], wn[ZW_PR];
+    double dv[ZW_PR][4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < ZW_PR; u++) {
       const int w = max(wv[u], 0);
       av[u] = A.anc[w];
 #pragma unroll
       for (int r = 0; r < 4; r++) dv[u][r] = A.dem[(size_t)w * 4 + r];
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int i = i0 + 4 * ZW_THREADS + u * ZW_THREADS + tid;
+    for (int u = 0; u < ZW_PR; u++) {
+      const int i = i0 + ZW_PR * ZW_THREADS + u * ZW_THREADS + tid;
       wn[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < ZW_PR; u++) {
       const bool ok = wv[u] >= 0;
       double bm[4];
 #pragma unroll
@@ -355,7 +385,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) wv[u] = wn[u];
+    for (int u = 0; u < ZW_PR; u++) wv[u] = wn[u];
   }
   __syncthreads();                           // (amask)
   uint32_t um = 0;

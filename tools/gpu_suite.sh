@@ -34,6 +34,7 @@ for s in "$@"; do
     st_var)     for v in ${VARS:-stamps}; do for m in ${STM:-ca_bf}; do TAILN=13 run st_${v}_$m 120 python tools/zwalk_stamps.py 1000000 10000 libpivot_place_$v.so $m; done; done ;;
     b_var)      for v in ${VARS:-u8}; do for m in ${BM:-ca_bf}; do PIVOT_PLACE_LIB=pivot-scheduling_amd/diag/libpivot_place_$v.so run b_${v}_$m 150 python bench.py --mode $m $NB --steps 20; done; done ;;
     st_ord)     TAILN=6 run st_ord 120 python tools/order_stamps.py ;;
+    tl)         mkdir -p gpurun_out/tl && run tl 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d gpurun_out/tl -o run -- python bench.py --steps 10 $NB && python tools/api_timeline.py gpurun_out/tl/run_hip_api_trace.csv gpurun_out/tl/run_kernel_trace.csv 0.7 > gpurun_out/tl_summary.txt ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
     t_rw)       run t_rw 400 $T tests/test_gpu_resident_walk.py tests/test_gpu_batch.py ;;
