@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = blockIdx.x * WPB + wave;
   const int t = g / A.S, seg = g % A.S;
+  if (gate_closed(A.gate)) return;
   if (t >= A.nt || (A.nt_dev && t >= *A.nt_dev)) return;
   const double* dp = A.dem + (size_t)t * 4;
   const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
@@ -207,8 +208,10 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
 // equal demands -- adjacent in the sorted order -- is scored and merged once): row[w] = the run's
 // row, rdem[row] = its demand, *nrep = rows. One block; a block scan of the run heads.
 __global__ __launch_bounds__(1024) void band_reps_kernel(const double* dem, int nt, int32_t* row,
-                                                         double* rdem, int32_t* nrep) {
+                                                         double* rdem, int32_t* nrep,
+                                                         const int32_t* gate) {
   __shared__ int32_t wsum[16];
+  if (gate_closed(gate)) return;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   bool head = false;
   if (t < nt) {
@@ -230,8 +233,8 @@ __global__ __launch_bounds__(1024) void band_reps_kernel(const double* dem, int 
 }
 
 void launch_band_reps(const double* dem, int nt, int32_t* row, double* rdem, int32_t* nrep,
-                      hipStream_t st) {
-  if (nt > 0) hipLaunchKernelGGL(band_reps_kernel, dim3(1), dim3(1024), 0, st, dem, nt, row, rdem, nrep);
+                      hipStream_t st, const int32_t* gate) {
+  if (nt > 0) hipLaunchKernelGGL(band_reps_kernel, dim3(1), dim3(1024), 0, st, dem, nt, row, rdem, nrep, gate);
 }
 
 void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,

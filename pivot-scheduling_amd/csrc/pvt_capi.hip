@@ -48,6 +48,7 @@ static constexpr int EP_SEG_OFF = 0, EP_SEG_CHAIN = EP_SEG_OFF + EPOCH_SEGS + 1,
 static constexpr int EP_WORDS = EP_SAFE + EPOCH_SEGS;
 static constexpr int KEYED_FRONTIER_MIN = 32;   // group tasks worth a frontier-walk launch
 static constexpr int ORDERED_FRONTIER_MIN = 32;  // tasks a frontier attempt must place to go on
+static constexpr int AHEAD_MAX = 8;             // vbp best-fit walks enqueued per host round trip
 static constexpr int ORDERED_FRONTIER_TASKS = 4096;   // tasks per frontier attempt (default;
                                                        // config-5 vbp_ff sweep: 512 1.75, 1024
                                                        // 1.09, 2048 0.94, 4096 0.90, 8192 0.98 ms)
@@ -141,6 +142,7 @@ struct RoundState {
   bool band = false;
   int band_S = BAND_SEGS;
   int touch_lb = -1;
+  const int32_t* touch_status = nullptr;   //   (its status: [1] = hosts in the own-ids buffer)
   bool reps[2] = {false, false};  //   list buffer b holds representative rows (band_reps)
   bool full_lists = false;        //   (one list per task: the list walk's fallback)
   bool lw_last = false;           // the walk in flight is the one-wave list walk (pvt_lwalk.hip)
@@ -189,6 +191,8 @@ struct pvt_ctx {
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
   int rwalk = 1;                  // PVT_RWALK=0: resident rounds without the one-wave walk (A/B)
+  int ahead = 1;                  // PVT_AHEAD=0: vbp best-fit windows one host round trip each (A/B)
+  Buf wslot;                      // enqueued-ahead walks' status slots (place_ahead)
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf bpos, bptouch;              // band lists: host -> sorted position, touched by position
   Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
@@ -363,7 +367,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
       hipEventCreateWithFlags(&ctx->ev_rstage, hipEventDisableTiming) != hipSuccess ||
       init_kernel_attrs() != hipSuccess || pvt::opp_init_attrs() != hipSuccess ||
       resident_init_attrs() != hipSuccess || lwalk_init_attrs() != hipSuccess ||
-      hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * 4) != hipSuccess ||
+      hipHostMalloc((void**)&ctx->next_host, sizeof(int32_t) * (4 + 4 * AHEAD_MAX)) != hipSuccess ||
       hipHostMalloc((void**)&ctx->flag_host, sizeof(int32_t) * 16, hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&ctx->flag_hdev, ctx->flag_host, 0) != hipSuccess ||
       hipHostMalloc((void**)&ctx->ep_host, sizeof(int32_t) * EP_WORDS) != hipSuccess ||
@@ -376,6 +380,7 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_OF_TASKS")) ctx->of_tasks = std::max(32, atoi(e));   // tuning
   if (const char* e = getenv("PVT_BAND")) ctx->band_min = std::max(0, atoi(e));       // A/B
   if (const char* e = getenv("PVT_LWALK")) ctx->lwalk = atoi(e) != 0;                  // A/B
+  if (const char* e = getenv("PVT_AHEAD")) ctx->ahead = atoi(e) != 0;                  // A/B
   if (const char* e = getenv("PVT_RWALK")) ctx->rwalk = atoi(e) != 0;                  // A/B
   if (const char* e = getenv("PVT_SEGMENTS")) ctx->t_segments = std::max(1, atoi(e));  // tuning
   if (const char* e = getenv("PVT_BAND_SEGS")) ctx->t_band_segs = atoi(e);             // tuning
@@ -924,7 +929,8 @@ static int band_snapshot(pvt_ctx* ctx) {
 static void flush_touched(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   if (!R.band || R.touch_lb < 0) return;
-  launch_touch_update(P<int32_t>(ctx->owned[R.touch_lb]), P<int32_t>(ctx->next),
+  launch_touch_update(P<int32_t>(ctx->owned[R.touch_lb]),
+                      R.touch_status ? R.touch_status : P<int32_t>(ctx->next),
                       P<uint8_t>(ctx->btouch), P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt),
                       P<int32_t>(ctx->bpos), R.lo, R.hi, P<uint8_t>(ctx->bptouch), ctx->stream);
   R.touch_lb = -1;
@@ -1259,7 +1265,8 @@ static int round_next_window(pvt_ctx* ctx, int* nt_out) {
 
 // Exact candidate lists of tasks [t0, t0 + nt) over hosts [lo, hi) into list buffer `lb`, on
 // stream `st`.
-static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
+static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st,
+                        const int32_t* gate = nullptr) {
   RoundState& R = ctx->rs;
   const pvt_round* r = &R.r;
   const int Hl = R.hi - R.lo;
@@ -1298,7 +1305,7 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
       ENSURE(ctx->bnrep[lb], sizeof(int32_t) * 4);
       Scope sc(ctx, PVT_K_OTHER, 0, 0, st);
       launch_band_reps(dem_w, nt, P<int32_t>(ctx->brow[lb]), P<double>(ctx->brdem[lb]),
-                       P<int32_t>(ctx->bnrep[lb]), st);
+                       P<int32_t>(ctx->bnrep[lb]), st, gate);
       dem_l = P<double>(ctx->brdem[lb]);
       nt_dev = P<int32_t>(ctx->bnrep[lb]);
     }
@@ -1306,13 +1313,13 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st) {
                 P<int32_t>(ctx->bidx) + n, n, R.lo, R.hi, P<uint8_t>(ctx->btouch),
                 P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt), r->avail, r->tiebreak, R.H, dem_l,
                 nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), nt_dev,
-                P<uint8_t>(ctx->bptouch)};
+                P<uint8_t>(ctx->bptouch), gate};
     {
       Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st, "band_score_kernel");
       launch_band_score(ba, st);
     }
     MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_l,
-                 anc_w, R.ord + t0, R.H, nt, S, KL, L, nt_dev, ctx->t_merge_bitonic};
+                 anc_w, R.ord + t0, R.H, nt, S, KL, L, nt_dev, ctx->t_merge_bitonic, gate};
     Scope sc(ctx, PVT_K_MERGE, 0, 0, st, merge_kernel_name(ma));
     launch_merge(ma, st);
   } else {
@@ -1365,7 +1372,8 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
   }
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
-  if (R.band) R.touch_lb = lb;    // its hosts become touched before the next band score
+  if (R.band) { R.touch_lb = lb; R.touch_status = status; }   // its hosts become touched before
+                                                              // the next band score
   return PVT_OK;
 }
 
@@ -1380,41 +1388,49 @@ static void adapt_window(pvt_ctx* ctx, int adv, int nt) {
   }
 }
 
+// The one-wave list walk could not start the window [t0, t0 + nt) (R.lw_lb, R.lw_prev): the
+// list walk walks it instead; *adv = where it stopped (after a synchronisation).
+static int lw_fallback(pvt_ctx* ctx, int t0, int nt, int* adv) {
+  // the one-wave list walk could not start this window (its first task's list ends before
+  // its bound, or too many inherited hosts): the list walk walks it, on the same lists
+  RoundState& R = ctx->rs;
+  const pvt_round* r = &R.r;
+  if (R.reps[R.lw_lb]) {
+    // representative rows: the list walk reads one list per task, so the window is scored
+    // again with one (on the current state: capacities only fall, and the inherited hosts are
+    // rescored as touched). The side stream's scoring shares the segment scratch: wait for it.
+    if (ctx->side) HIPCHK(hipStreamSynchronize(ctx->side));
+    R.full_lists = true;
+    const int rc = window_lists(ctx, t0, nt, R.lw_lb, ctx->stream);
+    R.full_lists = false;
+    if (rc) return rc;
+  }
+  Lists L;
+  lists_from(ctx, L, R.lw_lb);
+  CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
+                 P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
+                 r->placement, P<int32_t>(ctx->owned[1 - R.lw_lb]), R.lw_prev,
+                 P<int32_t>(ctx->owned[R.lw_lb]), P<int32_t>(ctx->next), nullptr,
+                 P<int32_t>(ctx->grp_ord) + t0, ctx->stamps};
+  R.lw_last = false;
+  {
+    Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "commit_kernel");
+    launch_commit(ca_, ctx->stream);
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t) * 2,
+                        hipMemcpyDeviceToHost, ctx->stream));
+  HIPCHK(hipStreamSynchronize(ctx->stream));
+  *adv = ctx->next_host[0];
+  return PVT_OK;
+}
+
 static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
   HIPCHK(hipStreamSynchronize(ctx->stream));
   *adv = ctx->next_host[0];
   if (*adv == 0 && ctx->rs.lw_last) {
-    // the one-wave list walk could not start this window (its first task's list ends before
-    // its bound, or too many inherited hosts): the list walk walks it, on the same lists
-    RoundState& R = ctx->rs;
-    const pvt_round* r = &R.r;
-    if (R.reps[R.lw_lb]) {
-      // representative rows: the list walk reads one list per task, so the window is scored
-      // again with one (on the current state: capacities only fall, and the inherited hosts are
-      // rescored as touched). The side stream's scoring shares the segment scratch: wait for it.
-      if (ctx->side) HIPCHK(hipStreamSynchronize(ctx->side));
-      R.full_lists = true;
-      const int rc = window_lists(ctx, t0, nt, R.lw_lb, ctx->stream);
-      R.full_lists = false;
-      if (rc) return rc;
-    }
-    Lists L;
-    lists_from(ctx, L, R.lw_lb);
-    CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
-                   P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
-                   r->placement, P<int32_t>(ctx->owned[1 - R.lw_lb]), R.lw_prev,
-                   P<int32_t>(ctx->owned[R.lw_lb]), P<int32_t>(ctx->next), nullptr,
-                   P<int32_t>(ctx->grp_ord) + t0, ctx->stamps};
-    R.lw_last = false;
-    {
-      Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "commit_kernel");
-      launch_commit(ca_, ctx->stream);
-    }
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(ctx->next_host, P<int32_t>(ctx->next), sizeof(int32_t) * 2,
-                          hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    *adv = ctx->next_host[0];
+    int rc = lw_fallback(ctx, t0, nt, adv);
+    if (rc) return rc;
   }
   if (*adv == -1) return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out at task %d", t0);
   if (*adv < 0 || *adv > nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", *adv, nt);
@@ -1485,6 +1501,114 @@ static int ordered_frontier(pvt_ctx* ctx) {
   return PVT_OK;
 }
 
+// vbp best-fit rounds on band lists walked by the one-wave list walk, without a host round trip
+// per window: up to AHEAD_MAX walks are enqueued at once, each window's size the one a run of
+// complete walks takes (adapt_window), the next window's lists scored on the side stream while
+// a walk runs (as place_pipelined). Walk k reads the status slot of walk k - 1 (CommitArgs::gate):
+// if that one stopped early or was skipped, walk k is skipped -- and so are the scoring kernels
+// of window k + 1, gated on walk k - 1 likewise -- so after a refill at most the one speculative
+// window already scored is wasted, as before. Then one synchronisation reads every slot: the
+// first walk that stopped early is a refill (lists from where it stopped, on the current state).
+static int place_ahead(pvt_ctx* ctx) {
+  RoundState& R = ctx->rs;
+  int rc, nt = 0;
+  if ((rc = round_next_window(ctx, &nt))) return rc;
+  if (nt == 0) return PVT_OK;
+  ENSURE(ctx->wslot, sizeof(int32_t) * 4 * AHEAD_MAX);
+  int32_t* slots = P<int32_t>(ctx->wslot);
+  const int32_t* hslots = ctx->next_host + 4;
+  int t0 = R.t0, lb = 0, n_prev = 0;
+  bool inherited = false;
+  if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
+  struct Win { int t0, nt, lb; };
+  for (;;) {
+    Win q[AHEAD_MAX];
+    int nq = 0, W = R.W;
+    Win nx{0, 0, 0};                          // the window after the last enqueued walk
+    for (;;) {
+      const int32_t* gate = nq > 0 ? slots + 4 * (nq - 1) : nullptr;
+      const int nt0 = t0 + nt;
+      if (nt == W) W = std::min(R.Wmax, 2 * W);   // (adapt_window after a complete walk)
+      const int nnt = nt0 < R.T ? std::min(W, R.T - nt0) : 0;
+      flush_touched(ctx);                     // the walk before's hosts (none if it was skipped)
+      if (nnt > 0) HIPCHK(hipEventRecord(ctx->ev_walk, ctx->stream));
+      {
+        Lists L;
+        lists_from(ctx, L, lb);
+        const pvt_round* r = &R.r;
+        int32_t* slot = slots + 4 * nq;
+        CommitArgs ca_{r->avail, P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<double>(ctx->csum),
+                       P<double>(ctx->bsum), r->zone, r->tiebreak, L, R.H, R.Z, nt, r->mode,
+                       r->placement, P<int32_t>(ctx->owned[1 - lb]), nq == 0 ? n_prev : 0,
+                       P<int32_t>(ctx->owned[lb]), slot, nullptr, P<int32_t>(ctx->grp_ord) + t0,
+                       ctx->stamps};
+        if (R.reps[lb]) { ca_.rowmap = P<int32_t>(ctx->brow[lb]); ca_.ordw = R.ord + t0; }
+        ca_.gate = gate;
+        ca_.ahead = 1;
+        {
+          Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "lwalk_kernel");
+          launch_lwalk(ca_, ctx->stream);
+        }
+        HIPCHK(hipGetLastError());
+        R.touch_lb = lb;
+        R.touch_status = slot;
+      }
+      q[nq++] = {t0, nt, lb};
+      if (nnt > 0) {
+        HIPCHK(hipStreamWaitEvent(ctx->side, ctx->ev_walk, 0));
+        if ((rc = window_lists(ctx, nt0, nnt, 1 - lb, ctx->side, gate))) return rc;
+        HIPCHK(hipEventRecord(ctx->ev_lists, ctx->side));
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_lists, 0));
+      }
+      nx = {nt0, nnt, 1 - lb};
+      if (nnt == 0 || nq == AHEAD_MAX) break;
+      t0 = nt0; nt = nnt; lb = 1 - lb;
+    }
+    HIPCHK(hipMemcpyAsync(ctx->next_host + 4, slots, sizeof(int32_t) * 4 * nq, hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    int j = 0, adv = 0;
+    for (; j < nq; j++) {
+      adv = hslots[4 * j];
+      if (hslots[4 * j + 3] != 0 || adv < 0 || adv > q[j].nt)
+        return fail(ctx, PVT_EHIP, "list walk %d of %d returned %d of %d (skipped %d)", j, nq, adv,
+                    q[j].nt, hslots[4 * j + 3]);
+      if (adv < q[j].nt) break;
+      adapt_window(ctx, adv, q[j].nt);
+    }
+    if (j == nq) {                            // every walk took its whole window
+      if (nx.nt == 0) { R.t0 = R.T; break; }
+      n_prev = hslots[4 * (nq - 1) + 1];
+      t0 = nx.t0; nt = nx.nt; lb = nx.lb;
+      inherited = true;
+      continue;
+    }
+    // walk j stopped early: the walks after it were skipped, as were the scorings after the
+    // speculative one (discarded here)
+    if (adv == 0) {
+      R.lw_lb = q[j].lb;
+      R.lw_prev = j == 0 ? n_prev : hslots[4 * (j - 1) + 1];
+      if ((rc = lw_fallback(ctx, q[j].t0, q[j].nt, &adv))) return rc;
+      R.touch_lb = q[j].lb;
+      R.touch_status = P<int32_t>(ctx->next);
+      if (adv == -1) return fail(ctx, PVT_EHIP, "commit walk: ring hand-off timed out at task %d", q[j].t0);
+      if (adv < 0 || adv > q[j].nt) return fail(ctx, PVT_EHIP, "commit walk returned %d of %d", adv, q[j].nt);
+      if (adv == 0 && !(inherited || j > 0))
+        return fail(ctx, PVT_EHIP, "commit walk made no progress at task %d", q[j].t0);
+    }
+    adapt_window(ctx, adv, q[j].nt);
+    HIPCHK(hipStreamSynchronize(ctx->side));
+    flush_touched(ctx);
+    R.t0 = q[j].t0 + adv;
+    if ((rc = round_next_window(ctx, &nt))) return rc;
+    if (nt == 0) break;
+    t0 = R.t0; lb = 0; n_prev = 0; inherited = false;
+    if ((rc = window_lists(ctx, t0, nt, lb, ctx->stream))) return rc;
+  }
+  flush_touched(ctx);
+  return PVT_OK;
+}
+
 // pvt_place for the list policies. While window k is walked on the caller's stream, the side
 // stream scores window k+1 on the capacities as they stand (the walk of k-1 is complete; the
 // walk of k is in flight): an event recorded just before walk k releases it. The side stream
@@ -1496,6 +1620,8 @@ static int ordered_frontier(pvt_ctx* ctx) {
 static int place_pipelined(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   int rc, nt = 0;
+  if (R.band && ctx->lwalk && ctx->ahead && ctx->pipeline && !R.sharded && !R.ofront && !R.keyed)
+    return place_ahead(ctx);
   if ((rc = ordered_frontier(ctx))) return rc;
   if ((rc = round_next_window(ctx, &nt))) return rc;
   if (nt == 0) return PVT_OK;

@@ -99,6 +99,7 @@ struct MergeArgs {
   Lists L;
   const int32_t* nt_dev;  // or NULL: only tasks [0, *nt_dev) (vbp best-fit representative lists)
   int bitonic;            // 1: the bitonic merge_kernel always (A/B; PVT_MERGE_SMALL=0 at ctx create)
+  const int32_t* gate;    // or NULL: enqueued-ahead window (gate_closed below)
 };
 
 // Host-dimension sharding: a rank's exact local lists -> its exchange package (see MergeArgs).
@@ -165,6 +166,12 @@ struct CommitArgs {
   // NULL: row w, TaskRec.ord
   const int32_t* rowmap;
   const int32_t* ordw;
+  // Windows enqueued ahead (pvt_capi.hip place_ahead; one-wave list walk only): gate = the walk
+  // before's status slot {stopped at, owned hosts, nt, skipped} -- closed (gate_closed) when that
+  // walk was skipped or stopped early: this walk is skipped (status {0, 0, nt, 1}); open: its
+  // owned hosts are this walk's inherited ones (n_prev). ahead: status is such a 4-word slot.
+  const int32_t* gate;
+  int ahead;
 };
 
 // Speculative epochs, cost_aware best-fit. The epoch's group segments (processing order,
@@ -357,7 +364,18 @@ struct BandArgs {
   int32_t* seg_feas;      // [nt][S]
   const int32_t* nt_dev;  // or NULL: only tasks [0, *nt_dev) (representative lists)
   const uint8_t* ptouched;  // [n] touched by sorted position (= touched[sid[p]], read with the chunk)
+  const int32_t* gate;    // or NULL: enqueued-ahead window (gate_closed)
 };
+
+// An enqueued-ahead window's gate: the status slot {stopped at, owned hosts, nt, skipped} of the
+// walk two windows back for the lists (one back for a walk): closed when that walk was skipped
+// or stopped early -- the window was speculated on a continuation that did not happen.
+__device__ __forceinline__ bool gate_closed(const int32_t* g) {
+  if (!g) return false;
+  const int s = __builtin_amdgcn_readfirstlane(g[3]), a = __builtin_amdgcn_readfirstlane(g[0]);
+  const int n = __builtin_amdgcn_readfirstlane(g[2]);
+  return s != 0 || a != n;
+}
 void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,
                       hipStream_t st);
 void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, const int32_t* sid,
@@ -369,7 +387,7 @@ void launch_band_score(const BandArgs& a, hipStream_t st);
 // Window tasks -> list rows: each run of equal demand vectors (bit for bit) shares one list row;
 // rdem = the rows' demands, *nrep = rows (nt <= MAX_WINDOW)
 void launch_band_reps(const double* dem, int nt, int32_t* row, double* rdem, int32_t* nrep,
-                      hipStream_t st);
+                      hipStream_t st, const int32_t* gate = nullptr);
 
 int score_tasks_per_wave(int mode, int hosts, int force = 0);
 int score_diag(uint64_t* out, int n, int reset);   // PVT_DIAG builds; else PVT_EUNSUPPORTED

@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs A) {
   __shared__ Key bound;
   __shared__ long long tot;
   __shared__ int cnt_sh;
+  if (gate_closed(A.gate)) return;   // (an enqueued-ahead window that will not be walked)
   const int task = blockIdx.x, tid = threadIdx.x;
   if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
   const int SL = A.SL, batch = LMAX / SL;   // source lists per sort batch
@@ -422,6 +423,7 @@ constexpr int MERGE_SMALL_S = 8;
 __global__ __launch_bounds__(256) void merge_small_kernel(MergeArgs A) {
   __shared__ Key lk[4][MERGE_SMALL_S * KL];
   __shared__ Key out[4][MERGE_SMALL_S * KL];
+  if (gate_closed(A.gate)) return;   // (an enqueued-ahead window that will not be walked)
   const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int task = blockIdx.x * 4 + wave;
   if (task >= A.nt || (A.nt_dev && task >= *A.nt_dev)) return;
@@ -520,6 +522,7 @@ __global__ __launch_bounds__(256) void merge_pkg_kernel(MergeArgs A) {
   __shared__ Key out[LMAX];
   __shared__ Key bound;
   __shared__ int cnt_sh, tot_sh;
+  if (gate_closed(A.gate)) return;   // (an enqueued-ahead window that will not be walked)
   const int task = blockIdx.x, tid = threadIdx.x;
   if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
   const int W = A.S, SL = A.SL, n = W * SL;
@@ -603,6 +606,7 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   __shared__ Key ka[LMAX];
   __shared__ Key kb[LMAX];
   __shared__ int cnt_sh;
+  if (gate_closed(A.gate)) return;   // (an enqueued-ahead window that will not be walked)
   const int task = blockIdx.x, tid = threadIdx.x;
   if (A.nt_dev && task >= *A.nt_dev) return;   // (representative lists: rows past the count)
   const int S = A.S;

@@ -108,6 +108,13 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   LwalkLDS& S = *reinterpret_cast<LwalkLDS*>(smem);
   const int lane = lane_id();
+  // an enqueued-ahead window (CommitArgs::gate): skipped when the walk before did not walk its
+  // whole window; otherwise that walk's hosts are the inherited ones
+  if (gate_closed(A.gate)) {
+    if (lane == 0) { A.status[0] = 0; A.status[1] = 0; A.status[2] = A.nt; A.status[3] = 1; }
+    return;
+  }
+  const int n_prev = A.gate ? __builtin_amdgcn_readfirstlane(A.gate[1]) : A.n_prev;
   for (int i = lane; i < LW_HSLOTS; i += WAVE) S.hkey[i] = LW_EMPTY;
   if (lane == 0) { S.nlive = 0; S.ntab = 0; S.bad = 0; }
   // componentwise smallest demand of the window: a touched host that cannot fit it is dead
@@ -124,7 +131,7 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
   lw_fence();
   // inherited touched hosts (the previous walk's, committed after these lists were scored):
   // their current capacities from HBM; ids are distinct
-  const int np = min(A.n_prev, LW_TAB);
+  const int np = min(n_prev, LW_TAB);
   for (int k = lane; k < np; k += WAVE) {
     const int32_t id = A.prev_ids[k];
     const double a0 = A.avail[id], a1 = A.avail[(size_t)A.H + id];
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
   int nlive = __builtin_amdgcn_readfirstlane(S.nlive);
   int n_own = 0;
   int status = A.nt;
-  if (A.n_prev > LW_TAB) status = 0;          // (cannot hold them: the list walk decides)
+  if (n_prev > LW_TAB) status = 0;            // (cannot hold them: the list walk decides)
 
   // the current list chunk (lane j: entry cbase + j of list cw) and its untouched flags
   int cw = -1, cbase = 0, ccnt = 0, cur = 0;
@@ -387,7 +394,10 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
 #pragma unroll
       for (int r = 0; r < 4; r++) A.avail[(size_t)r * A.H + id] = S.ta[r][t];
     }
-  if (lane == 0) { A.status[0] = status; A.status[1] = n_own; }
+  if (lane == 0) {
+    A.status[0] = status; A.status[1] = n_own;
+    if (A.ahead) { A.status[2] = A.nt; A.status[3] = 0; }
+  }
 #ifdef PVT_STAMPS
   if (lane == 0 && A.stamps) {
     for (int k = 0; k < 4; k++) atomicAdd((unsigned long long*)&A.stamps[k], (unsigned long long)ph[k]);
