@@ -333,6 +333,16 @@ int  pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_items* const* 
                           int32_t n_rounds, int32_t* rcs);
 
 /*
+ * Replay support (no reference counterpart): avail[r][h] = avail0[r][h], r = 0..3, for every
+ * h = hosts[i], i < n, with 0 <= h < n_hosts (other entries are ignored), on the context's
+ * stream; device pointers. A round placed again from the same snapshot needs only the hosts
+ * its placement names restored -- a round changes no other capacity -- so passing the round's
+ * placement array as `hosts` resets it in one small launch instead of a copy of all 4 x H.
+ */
+int  pvt_restore_hosts(pvt_ctx* ctx, double* avail, const double* avail0, int32_t n_hosts,
+                       const int32_t* hosts, int32_t n);
+
+/*
  * Meter aggregates of a batch of S scenarios (replaces the properties
  * Meter.cumulative_instance_hours, .total_network_traffic_cost and .average_congestion_delay,
  * resources/meter.py:31-53, read by alibaba/runner.py:45-51 via Meter.save).

@@ -682,13 +682,12 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
                   ca ? P<double>(ctx->bsum) : nullptr, P<uint64_t>(ctx->gskey), P<int32_t>(ctx->gsidx),
                   nullptr, 0};
       R.prep_fused = true;
-      if (G <= GCOMPACT_MAX) {   // counts, then one launch for the sorted, gathered order
-        // the host polls a flag the count kernel stores (no event: a marker on the stream cost
-        // ~5 us of idle GPU between the two launches)
+      if (G <= GCOMPACT_MAX) {   // one launch: the counts (block 0) beside the sorted, gathered order
+        // the host polls a flag the count block stores (no event: a marker on the stream cost
+        // ~5 us of idle GPU between launches)
         pa.hflag = ctx->flag_hdev;
         pa.seq = ++ctx->flag_seq;
         R.stage_flag = true;
-        launch_order_prep(pa, st, nullptr, false);
         launch_group_sort_gather(pa, GatherOut{cur, P<double>(ctx->dem_ord), P<int32_t>(ctx->anc_ord),
                                                P<int32_t>(ctx->grp_ord), r->order, r->avail,
                                                r->n_hosts, hmin, ctx->stamps}, st);
@@ -2528,6 +2527,15 @@ extern "C" int pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* it) {
   HIPCHK(hipStreamSynchronize(st));
   if (it && (rc = group_error(ctx, hb, s, it))) return rc;
   return_round(hb, s, r, it);
+  return PVT_OK;
+}
+
+extern "C" int pvt_restore_hosts(pvt_ctx* ctx, double* avail, const double* avail0, int32_t n_hosts,
+                                 const int32_t* hosts, int32_t n) {
+  if (!ctx || n < 0 || n_hosts < 0 || (n > 0 && (!avail || !avail0 || !hosts))) return PVT_EINVAL;
+  HIPCHK(hipSetDevice(ctx->device));
+  launch_restore_hosts(avail, avail0, n_hosts, hosts, n, ctx->stream);
+  HIPCHK(hipGetLastError());
   return PVT_OK;
 }
 

@@ -479,6 +479,8 @@ struct GatherOut {
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st);
 // bytes (rounded up to 16; both buffers 16-B aligned and that long) from mapped pinned memory
 void launch_upload(const void* src_mapped, void* dst, size_t bytes, hipStream_t st);
+void launch_restore_hosts(double* avail, const double* avail0, int H, const int32_t* hosts, int n,
+                          hipStream_t st);
 void launch_group_stage(const int32_t* cnt, int G, const int32_t* ganc, const double* cost, int nz2,
                         int32_t* off, int32_t* hcnt, int32_t* hgan, double* hcst, hipStream_t st);
 void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,

@@ -1071,8 +1071,7 @@ void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G,
 // plans the round. order_scatter_kernel, while the host plans: placement fill, zone tables, the
 // groups' offsets, then the (key, task) pairs scattered by LDS cursors (their order inside a
 // group is irrelevant: group_sort orders by (key, index)).
-__global__ __launch_bounds__(1024) void order_count_kernel(PrepArgs A) {
-  __shared__ int32_t cnt[GAGG_MAX + 1];
+__device__ void order_count_body(const PrepArgs& A, int32_t* cnt) {
   const int t = threadIdx.x;
   const int T = A.T, G = A.G;
   for (int q = t; q <= G; q += 1024) cnt[q] = 0;
@@ -1112,6 +1111,10 @@ __global__ __launch_bounds__(1024) void order_count_kernel(PrepArgs A) {
       __hip_atomic_store(A.hflag, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+}
+__global__ __launch_bounds__(1024) void order_count_kernel(PrepArgs A) {
+  __shared__ int32_t cnt[GAGG_MAX + 1];
+  order_count_body(A, cnt);
 }
 
 __global__ __launch_bounds__(1024) void order_scatter_kernel(PrepArgs A) {
@@ -1304,20 +1307,27 @@ __device__ __forceinline__ uint64_t gstamp() {
 // sorts them (lds_sort_pairs) and writes the gathered rows at its group's offset (the counts
 // of the groups before it): processing order, caller order, demand rows, anchors, groups.
 // Replaces order_scatter + group_sort + gather_tasks (three launches, ~35 us per config-5
-// round). Block 0 also writes the zone tables. A group over GSORT_MAX tasks only fills its
-// placement: the host redoes the order with radix passes.
+// round). Block 0 is order_count_kernel (the counts and the host's stage, while the groups'
+// blocks run: each group's block counts the tasks of the groups before it itself, in its scan);
+// group g is block g + 1, which also writes the zone tables for g = 0. A group over GSORT_MAX
+// tasks only fills its placement: the host redoes the order with radix passes.
 __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, GatherOut O) {
   __shared__ uint64_t k[GSORT_MAX];
   __shared__ int32_t v[GSORT_MAX];
-  __shared__ int32_t fill, base_s;
-  const int g = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  __shared__ int32_t fill, below_s;
+  static_assert(sizeof(k) >= sizeof(int32_t) * (GCOMPACT_MAX + 1), "count table in k");
+  if (blockIdx.x == 0) {
+    order_count_body(A, reinterpret_cast<int32_t*>(k));
+    return;
+  }
+  const int g = blockIdx.x - 1, tid = threadIdx.x, lane = tid & 63;
   const int T = A.T;
 #ifdef PVT_STAMPS
   uint64_t gph[4] = {0, 0, 0, 0}, gtl = 0;
   if (g == 0 && tid == 0) gtl = gstamp();
 #endif
   if (g >= A.G) {
-    // blocks past the groups: the frontier walk's host minima, one of the ZW_MIN_PARTS partials
+    // blocks past the groups' blocks: the frontier walk's host minima, one of the ZW_MIN_PARTS partials
     // per block (the walk reduces them all, so the partition is free: four hosts per thread per
     // pass for loads in flight; a quarter as many blocks measured ~26 us against 8.8)
     __shared__ double red[16][4];
@@ -1356,14 +1366,7 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
       A.csum[i] = A.cost[a * A.Z + z] + A.cost[z * A.Z + a];   // cost_aware.py:82,113
       A.bsum[i] = A.bw[a * A.Z + z] + A.bw[z * A.Z + a];       // (:79,111)
     }
-  if (tid < 64) {                             // the group's offset: counts of groups before it
-    int c = 0;
-    for (int q = lane; q < g; q += 64) c += A.off[q];
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-    if (lane == 0) { base_s = c; fill = 0; }
-  }
-  const int n = A.off[g];
-  const bool sortable = n <= GSORT_MAX;
+  if (tid == 0) { fill = 0; below_s = 0; }
   __syncthreads();
   GSTAMP(0);
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1381,7 +1384,7 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
     // the wave's matches of the whole batch take ONE cursor add (an LDS atomic and its return
     // per 1024 tasks serialised the 16 waves: 24k cycles for the scan at config 5)
     uint64_t bal[PB];
-    int tot = 0;
+    int tot = 0, lt = 0;                      // (lt: tasks of the groups before g -- its offset)
 #pragma unroll
     for (int u = 0; u < PB; u++) {
       const int i = i0 + u * 1024 + tid;
@@ -1389,19 +1392,23 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
       if (mine && A.placement) A.placement[i] = -1;
       bal[u] = __ballot(mine);
       tot += __popcll(bal[u]);
+      lt += __popcll(__ballot(gv[u] >= 0 && gv[u] < g));
     }
-    if (!sortable || tot == 0) continue;
+    if (lane == 0 && lt) atomicAdd(&below_s, lt);
+    if (tot == 0) continue;
     int b = 0;
     if (lane == 0) b = atomicAdd(&fill, tot);
     b = __shfl(b, 0);
+    if (b + tot > GSORT_MAX) continue;        // (too large to sort here: only counted)
 #pragma unroll
     for (int u = 0; u < PB; u++) {
       if (gv[u] == g) v[b + __popcll(bal[u] & below)] = i0 + u * 1024 + tid;
       b += __popcll(bal[u]);
     }
   }
-  if (!sortable || n <= 0) return;
   __syncthreads();
+  const int n = fill;
+  if (n > GSORT_MAX || n <= 0) return;
   for (int q = tid; q < n; q += 1024) {       // the collected tasks' sort keys
     uint64_t key = 0;
     if (A.sort_tasks) {
@@ -1416,7 +1423,7 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   GSTAMP(1);
   lds_sort_pairs(k, v, n);
   GSTAMP(2);
-  const int a = base_s;
+  const int a = below_s;
   const int32_t anc = A.ganc[g];
   for (int i = tid; i < n; i += 1024) {
     const int p = a + i, t = v[i];
@@ -1436,12 +1443,27 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
 }
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st) {
   const int extra = o.hmin ? ZW_MIN_PARTS : 0;
-  hipLaunchKernelGGL(group_sort_gather_kernel, dim3(a.G + extra), dim3(1024), 0, st, a, o);
+  hipLaunchKernelGGL(group_sort_gather_kernel, dim3(1 + a.G + extra), dim3(1024), 0, st, a, o);
 }
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
                        int32_t* ord, hipStream_t st) {
   // (1024 threads, the block's element layout above assumes it)
   hipLaunchKernelGGL(group_sort_kernel, dim3(G), dim3(1024), 0, st, off, skey, sidx, ord);
+}
+
+// pvt_restore_hosts: the listed hosts' four capacities from the pristine snapshot.
+__global__ __launch_bounds__(256) void restore_hosts_kernel(double* avail, const double* avail0, int H,
+                                                            const int32_t* hosts, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int h = hosts[i];
+  if (h < 0 || h >= H) return;
+#pragma unroll
+  for (int r = 0; r < 4; r++) avail[(size_t)r * H + h] = avail0[(size_t)r * H + h];
+}
+void launch_restore_hosts(double* avail, const double* avail0, int H, const int32_t* hosts, int n,
+                          hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(restore_hosts_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, avail0, H, hosts, n);
 }
 
 // Small host tables to the device through their mapped pinned pages, as a kernel on the stream:

@@ -48,6 +48,7 @@ def load_library(path=None):
                                   ctypes.POINTER(ctypes.POINTER(_abi.pvt_ca_items)), ctypes.c_int32,
                                   ctypes.POINTER(ctypes.c_int32)], c_int),
         "pvt_place_batch_mt": ([c_void_p, c_void_p, ctypes.c_int32, c_void_p], c_int),
+        "pvt_restore_hosts": ([c_void_p, c_void_p, c_void_p, ctypes.c_int32, c_void_p, ctypes.c_int32], c_int),
         "pvt_set_window": ([c_void_p, c_int], c_int),
         "pvt_set_pipeline": ([c_void_p, c_int], c_int),
         "pvt_set_score_tw": ([c_void_p, c_int], c_int),
@@ -126,7 +127,7 @@ class DeviceRound:
         self.rt_bw = up(r.rt_bw)
         T = r.n_tasks
         self.order = torch.empty(max(T, 1), dtype=torch.int32, device=dev)
-        self.placement = torch.empty(max(T, 1), dtype=torch.int32, device=dev)
+        self.placement = torch.full((max(T, 1),), -1, dtype=torch.int32, device=dev)
         self.mt0 = None if r.mt_state is None else r.mt_state.copy()
         self.mt = None if r.mt_state is None else r.mt_state.copy()
         s = _abi.fill_struct(r)
@@ -404,6 +405,17 @@ class PlacementEngine:
         """Place a resident round (its avail / placement / order / mt are updated in place)."""
         self._bind_stream()
         self._check(self.lib.pvt_place(self.ctx, ctypes.addressof(dr.struct)))
+
+    def restore(self, dr: DeviceRound):
+        """dr.reset() after a placement of dr, restoring only the hosts its placement names (the
+        only capacities a round changes; pvt_restore_hosts): one small launch on the current
+        stream instead of a copy of the whole snapshot."""
+        self._bind_stream()
+        T = dr.arrays.n_tasks
+        self._check(self.lib.pvt_restore_hosts(self.ctx, dr.avail.data_ptr(), dr.avail0.data_ptr(),
+                                               dr.arrays.n_hosts, dr.placement.data_ptr(), T))
+        if dr.mt is not None:
+            dr.mt[:] = dr.mt0
 
     def place(self, r: RoundArrays) -> RoundResult:
         """Place a host-array round in one round trip (pvt_place_host: the context stages the

@@ -37,6 +37,7 @@ for s in "$@"; do
     st_ord)     TAILN=6 run st_ord 120 python tools/order_stamps.py ;;
     tl)         mkdir -p gpurun_out/tl && run tl 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d gpurun_out/tl -o run -- python bench.py --steps 10 $NB && python tools/api_timeline.py gpurun_out/tl/run_hip_api_trace.csv gpurun_out/tl/run_kernel_trace.csv 0.7 > gpurun_out/tl_summary.txt ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
+    t_new)      run t_new 600 $T tests/test_gpu_restore.py tests/test_gpu_fused.py tests/test_gpu_epochs.py tests/test_gpu_headline.py ;;
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
     t_rw)       run t_rw 400 $T tests/test_gpu_resident_walk.py tests/test_gpu_batch.py ;;
     b_c4w)      for m in ${C4M:-ca_bf ca_ff vbp_ff}; do run b_c4w_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
