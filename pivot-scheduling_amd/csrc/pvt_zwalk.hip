@@ -73,8 +73,8 @@ struct ZwalkLDS {
   int32_t cnt[ZW_SCAN][ZW_WAVES];          // window build: hits per (pass row, wave)
   double red[ZW_WAVES][12];                // block reductions: max d, min d, min avail
   double smin[ZW_SB][4];                   // suffix minima of the demands, per 64-task batch
-  double lg[64][4];                        // the batch's log: capacities after each commit
-  int32_t lgid[64];                        //   and the host
+  double lg[128][4];                       // the batch's log: capacities after each commit
+  int32_t lgid[128];                       //   and the host (64.. : a run carried into the next batch)
   uint64_t sbits[CHAIN_MAX / 64];          // chain mode: bit i = a group segment starts at task i
   uint32_t amask[ZMAX];                    // anchor -> its zero-cost zones
   uint32_t umask;
@@ -708,6 +708,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   double nd2 = A.dem[(size_t)nw * 4 + 2], nd3 = A.dem[(size_t)nw * 4 + 3];
   int nanc = A.anc[nw], ncal = A.ord[nw];
   int nw1 = task_at(64 + lane);
+  int carry = 0;                             // tasks of this batch a run of the last one placed
   for (int i0 = 0; UNI(i0 < nt && !failed); i0 += 64) {
 #ifdef PVT_STAMPS
     uint64_t tb0 = zstamp();
@@ -742,7 +743,36 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       // at its last copy of the run only, and the segment before must hold its own last copy)
       if (!KEYED && A.cseg) E &= ~rfl_u64(S.sbits[i0 >> 6]);
     }
-    auto run_len = [&](int k) { return k < 63 ? min(kn - k, 1 + __builtin_ctzll(~(E >> (k + 1)))) : 1; };
+    // A run that reaches the end of a full batch goes on into the next one while those tasks
+    // have the same demand vector and anchor and no segment starts (their records are already in
+    // registers, nd*): at most 64 tasks per run, the ones past the batch logged at 64.. and
+    // carried (a third of the runs were cut at batch ends).
+    int extc = -1;
+    auto ext_len = [&]() -> int {
+      if (extc < 0) {
+        extc = 0;
+        if (kn == 64 && i0 + 64 < nt && uni) {
+          const int kn2 = min(64, nt - i0 - 64);
+          const double l0 = readlane_d(td[0], 63), l1 = readlane_d(td[1], 63);
+          const double l2 = readlane_d(td[2], 63), l3 = readlane_d(td[3], 63);
+          bool eq = lane < kn2 && readlane_i(tanc, 63) == nanc &&
+                    __double_as_longlong(nd0) == __double_as_longlong(l0) &&
+                    __double_as_longlong(nd1) == __double_as_longlong(l1) &&
+                    __double_as_longlong(nd2) == __double_as_longlong(l2) &&
+                    __double_as_longlong(nd3) == __double_as_longlong(l3);
+          if (!KEYED && A.cseg) eq = eq && !((rfl_u64(S.sbits[(i0 >> 6) + 1]) >> lane) & 1ull);
+          const uint64_t m = __ballot(eq);
+          extc = m == ~0ull ? 64 : __builtin_ctzll(~m);
+        }
+        extc = __builtin_amdgcn_readfirstlane(extc);
+      }
+      return extc;
+    };
+    auto run_len = [&](int k) {
+      int r = k < 63 ? min(kn - k, 1 + __builtin_ctzll(~(E >> (k + 1)))) : 1;
+      if (k + r == 64) r = min(64, r + ext_len());
+      return r;
+    };
     // The run step, for a task k of a uniform batch that the register chunk p0 cannot take: its
     // run (R tasks with its demand, R >= 1) is placed by run_bulk on the first chunk that can
     // take a copy of it -- chunk p0 (moved on past chunks no task ahead can use), chunk pb, then
@@ -818,7 +848,16 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #ifdef PVT_STAMPS
     st_batch += zstamp() - tb0;
 #endif
-    int k = 0;
+    int k = carry;
+    if (carry) {                             // the carried run's log entries to their positions
+      wave_lds_sync();
+      if (lane < carry) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) S.lg[lane][r] = S.lg[64 + lane][r];
+        S.lgid[lane] = S.lgid[64 + lane];
+      }
+      wave_lds_sync();
+    }
     while (UNI(k < kn)) {
       // (wave-uniform state the compiler cannot prove uniform: keeps the loops below scalar)
       k = __builtin_amdgcn_readfirstlane(k);
@@ -1052,6 +1091,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       e.a[0] = S.lg[lane][0]; e.a[1] = S.lg[lane][1]; e.a[2] = S.lg[lane][2]; e.a[3] = S.lg[lane][3];
       A.placement[tcal] = id;
     }
+    carry = __builtin_amdgcn_readfirstlane(k > kn ? k - kn : 0);
 #ifdef PVT_STAMPS
     st_batch += zstamp() - tb0;
 #endif
