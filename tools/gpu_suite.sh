@@ -36,6 +36,7 @@ for s in "$@"; do
     b_var)      for v in ${VARS:-u8}; do for m in ${BM:-ca_bf}; do PIVOT_PLACE_LIB=pivot-scheduling_amd/diag/libpivot_place_$v.so run b_${v}_$m 150 python bench.py --mode $m $NB --steps 20; done; done ;;
     st_ord)     TAILN=6 run st_ord 120 python tools/order_stamps.py ;;
     tl)         mkdir -p gpurun_out/tl && run tl 300 rocprofv3 --hip-trace --kernel-trace --output-format csv -d gpurun_out/tl -o run -- python bench.py --steps 10 $NB && python tools/api_timeline.py gpurun_out/tl/run_hip_api_trace.csv gpurun_out/tl/run_kernel_trace.csv 0.7 > gpurun_out/tl_summary.txt ;;
+    kt_vbf)     mkdir -p gpurun_out/ktv && run kt_vbf 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ktv -o a -- python tools/walk_probe.py --mode vbp_bf --hosts 1000000 --tasks 10000 --reps 3 && PVT_AHEAD=0 run kt_vbf0 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ktv -o b -- python tools/walk_probe.py --mode vbp_bf --hosts 1000000 --tasks 10000 --reps 3 && python tools/trace_gaps.py gpurun_out/ktv/a_kernel_trace.csv 8 20 > gpurun_out/ktv_a.txt && python tools/trace_gaps.py gpurun_out/ktv/b_kernel_trace.csv 8 20 > gpurun_out/ktv_b.txt ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
     t_new)      run t_new 600 $T tests/test_gpu_restore.py tests/test_gpu_fused.py tests/test_gpu_epochs.py tests/test_gpu_headline.py ;;
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
