@@ -191,7 +191,8 @@ struct pvt_ctx {
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
   int rwalk = 1;                  // PVT_RWALK=0: resident rounds without the one-wave walk (A/B)
-  int ahead = 1;                  // PVT_AHEAD=0: vbp best-fit windows one host round trip each (A/B)
+  int ahead = 0;                  // PVT_AHEAD=1: vbp best-fit walks enqueued ahead (place_ahead;
+                                  // measured slower, kept for A/B)
   Buf wslot;                      // enqueued-ahead walks' status slots (place_ahead)
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf bpos, bptouch;              // band lists: host -> sorted position, touched by position
@@ -1508,6 +1509,10 @@ static int ordered_frontier(pvt_ctx* ctx) {
 // of window k + 1, gated on walk k - 1 likewise -- so after a refill at most the one speculative
 // window already scored is wasted, as before. Then one synchronisation reads every slot: the
 // first walk that stopped early is a refill (lists from where it stopped, on the current state).
+// Off by default (PVT_AHEAD=1 turns it on): measured at config 5 (rocprofv3 kernel traces of
+// tools/walk_probe.py) 6.9-7.9 ms per round against 3.9-4.2 ms with a host round trip per
+// window -- a third of the windows refill, and every skipped window still costs its five
+// dependent launches' ~15 us gaps (two of them across streams), more than the round trips saved.
 static int place_ahead(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   int rc, nt = 0;
