@@ -905,7 +905,9 @@ def main():
         % (rank, placed, T, stats["windows"], stats["refills"]))
 
     eng.reset_kstats()
-    eng.set_profiling(2)     # (events around the named kernels only: every launch costs ~30 us/round)
+    # (events around the named kernels only: every launch costs ~30 us/round; BENCH_PROF=0: no
+    # events at all, for A/B of their cost -- the roofline then has no kernel time)
+    eng.set_profiling(int(os.environ.get("BENCH_PROF", "2")))
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
