@@ -204,37 +204,45 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
   if (lane == 0) A.seg_feas[row] = filled == KL ? KL + 1 : filled;
 }
 
-// Window tasks -> list rows (vbp best-fit lists depend on the demand vector only, so each run of
-// equal demands -- adjacent in the sorted order -- is scored and merged once): row[w] = the run's
-// row, rdem[row] = its demand, *nrep = rows. One block; a block scan of the run heads.
-__global__ __launch_bounds__(1024) void band_reps_kernel(const double* dem, int nt, int32_t* row,
-                                                         double* rdem, int32_t* nrep,
-                                                         const int32_t* gate) {
+// The round's runs of equal demands (vbp best-fit lists depend on the demand vector only, and the
+// sorted order puts equal demands next to each other): run[t] = the run of processing-order task
+// t, rdem[run] = its demand. A window's list rows are then the runs it spans -- row of task t0 + w
+// = run[t0 + w] - run[t0], the rows' demands rdem + run[t0] -- with no per-window launch. One
+// block: a block scan of the run heads per 1024 tasks, carried across them.
+__global__ __launch_bounds__(1024) void band_runs_kernel(const double* dem, int T, int32_t* run,
+                                                         double* rdem) {
   __shared__ int32_t wsum[16];
-  if (gate_closed(gate)) return;
-  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  bool head = false;
-  if (t < nt) {
-    head = t == 0;
-    for (int r = 0; r < 4 && !head; r++)
-      head = __double_as_longlong(dem[(size_t)t * 4 + r]) != __double_as_longlong(dem[(size_t)(t - 1) * 4 + r]);
-  }
-  const uint64_t m = __ballot(head);
-  int incl = __popcll(lane == 63 ? m : (m & ((2ull << lane) - 1ull)));
-  if (lane == 63) wsum[wave] = incl;
+  __shared__ int32_t carry;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) carry = 0;
   __syncthreads();
-  for (int w = 0; w < wave; w++) incl += wsum[w];
-  if (t < nt) {
-    row[t] = incl - 1;
-    if (head)
-      for (int r = 0; r < 4; r++) rdem[(size_t)(incl - 1) * 4 + r] = dem[(size_t)t * 4 + r];
-    if (t == nt - 1) *nrep = incl;
+  for (int t0 = 0; t0 < T; t0 += 1024) {
+    const int t = t0 + tid;
+    bool head = false;
+    if (t < T) {
+      head = t == 0;
+      for (int r = 0; r < 4 && !head; r++)
+        head = __double_as_longlong(dem[(size_t)t * 4 + r]) != __double_as_longlong(dem[(size_t)(t - 1) * 4 + r]);
+    }
+    const uint64_t m = __ballot(head);
+    int incl = __popcll(lane == 63 ? m : (m & ((2ull << lane) - 1ull)));
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    for (int w = 0; w < wave; w++) incl += wsum[w];
+    incl += carry;
+    if (t < T) {
+      run[t] = incl - 1;
+      if (head)
+        for (int r = 0; r < 4; r++) rdem[(size_t)(incl - 1) * 4 + r] = dem[(size_t)t * 4 + r];
+    }
+    __syncthreads();
+    if (tid == 1023) carry = incl;
+    __syncthreads();
   }
 }
 
-void launch_band_reps(const double* dem, int nt, int32_t* row, double* rdem, int32_t* nrep,
-                      hipStream_t st, const int32_t* gate) {
-  if (nt > 0) hipLaunchKernelGGL(band_reps_kernel, dim3(1), dim3(1024), 0, st, dem, nt, row, rdem, nrep, gate);
+void launch_band_runs(const double* dem, int T, int32_t* run, double* rdem, hipStream_t st) {
+  if (T > 0) hipLaunchKernelGGL(band_runs_kernel, dim3(1), dim3(1024), 0, st, dem, T, run, rdem);
 }
 
 void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,

@@ -143,7 +143,9 @@ struct RoundState {
   int band_S = BAND_SEGS;
   int touch_lb = -1;
   const int32_t* touch_status = nullptr;   //   (its status: [1] = hosts in the own-ids buffer)
-  bool reps[2] = {false, false};  //   list buffer b holds representative rows (band_reps)
+  bool reps[2] = {false, false};  //   list buffer b holds representative rows (the round's runs)
+  int rbase[2] = {0, 0};          //     the run of its window's first task
+  std::vector<int32_t> runs;      //   the round's run ids (band_runs_kernel), on the host
   bool full_lists = false;        //   (one list per task: the list walk's fallback)
   bool lw_last = false;           // the walk in flight is the one-wave list walk (pvt_lwalk.hip)
   int lw_lb = 0, lw_prev = 0;     //   its list buffer and inherited hosts (for the fallback)
@@ -196,7 +198,7 @@ struct pvt_ctx {
   Buf wslot;                      // enqueued-ahead walks' status slots (place_ahead)
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
   Buf bpos, bptouch;              // band lists: host -> sorted position, touched by position
-  Buf brow[2], brdem[2], bnrep[2];        // band lists: representative rows per list buffer
+  Buf brun, brdem;                // band lists: the round's runs of equal demands (ids, demands)
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
   Buf cmax;                       // frontier-walked epochs: chains' largest demands
@@ -407,8 +409,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->oppfault, &ctx->hdev, &ctx->kskey, &ctx->kperm, &ctx->kiota,
                  &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->cmax, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
-                 &ctx->btcnt, &ctx->bsorttmp, &ctx->brow[0], &ctx->brow[1], &ctx->brdem[0],
-                 &ctx->brdem[1], &ctx->bnrep[0], &ctx->bnrep[1], &ctx->bpos, &ctx->bptouch};
+                 &ctx->btcnt, &ctx->bsorttmp, &ctx->brun, &ctx->brdem, &ctx->bpos, &ctx->bptouch};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -1109,6 +1110,19 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   R.touch_lb = -1;
   R.band = r->mode == PVT_VBP_BF && ctx->band_min > 0 && hi - lo >= ctx->band_min;
   if (R.band && (rc = band_snapshot(ctx))) return rc;
+  R.runs.clear();
+  if (R.band && ctx->lwalk && !R.sharded) {
+    // representative list rows: the round's runs of equal demands, once (their ids on the host
+    // size each window's rows; one synchronisation per round instead of a launch per window)
+    ENSURE(ctx->brun, sizeof(int32_t) * (size_t)T);
+    ENSURE(ctx->brdem, sizeof(double) * 4 * (size_t)T);
+    launch_band_runs(P<double>(ctx->dem_ord), T, P<int32_t>(ctx->brun), P<double>(ctx->brdem), st);
+    HIPCHK(hipGetLastError());
+    R.runs.resize(T);
+    HIPCHK(hipMemcpyAsync(R.runs.data(), ctx->brun.p, sizeof(int32_t) * (size_t)T,
+                          hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
 
   // Windows adapt to how far commit walks get before a list is exhausted: a walk that stops
   // early means the next window only needs about that many tasks (the score pass costs the
@@ -1295,31 +1309,28 @@ static int window_lists(pvt_ctx* ctx, int t0, int nt, int lb, hipStream_t st,
     const int n = R.hi - R.lo;
     // Representative rows (unsharded rounds, walked by the one-wave list walk, which maps each
     // task to its row): one list per run of equal demands instead of one per task.
-    const bool reps = ctx->lwalk && !R.sharded && !R.full_lists;
+    const bool reps = !R.runs.empty() && !R.full_lists;
     R.reps[lb] = reps;
     const double* dem_l = dem_w;
     const int32_t* nt_dev = nullptr;
-    if (reps) {
-      ENSURE(ctx->brow[lb], sizeof(int32_t) * MAX_WINDOW);
-      ENSURE(ctx->brdem[lb], sizeof(double) * 4 * MAX_WINDOW);
-      ENSURE(ctx->bnrep[lb], sizeof(int32_t) * 4);
-      Scope sc(ctx, PVT_K_OTHER, 0, 0, st);
-      launch_band_reps(dem_w, nt, P<int32_t>(ctx->brow[lb]), P<double>(ctx->brdem[lb]),
-                       P<int32_t>(ctx->bnrep[lb]), st, gate);
-      dem_l = P<double>(ctx->brdem[lb]);
-      nt_dev = P<int32_t>(ctx->bnrep[lb]);
+    int nt_l = nt;
+    if (reps) {                   // the rows: the runs the window spans
+      const int b0 = R.runs[t0];
+      R.rbase[lb] = b0;
+      nt_l = R.runs[t0 + nt - 1] - b0 + 1;
+      dem_l = P<double>(ctx->brdem) + (size_t)b0 * 4;
     }
     BandArgs ba{P<uint64_t>(ctx->bkey) + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb),
                 P<int32_t>(ctx->bidx) + n, n, R.lo, R.hi, P<uint8_t>(ctx->btouch),
                 P<int32_t>(ctx->btlist), P<int32_t>(ctx->btcnt), r->avail, r->tiebreak, R.H, dem_l,
-                nt, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), nt_dev,
+                nt_l, S, P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), nt_dev,
                 P<uint8_t>(ctx->bptouch), gate};
     {
       Scope sc(ctx, PVT_K_SCORE, (double)nt * Hl, (double)nt * Hl * bpc, st, "band_score_kernel");
       launch_band_score(ba, st);
     }
     MergeArgs ma{P<SegEntry>(ctx->seg), P<int32_t>(ctx->seg_feas), r->avail, r->zone, dem_l,
-                 anc_w, R.ord + t0, R.H, nt, S, KL, L, nt_dev, ctx->t_merge_bitonic, gate};
+                 anc_w, R.ord + t0, R.H, nt_l, S, KL, L, nt_dev, ctx->t_merge_bitonic, gate};
     Scope sc(ctx, PVT_K_MERGE, 0, 0, st, merge_kernel_name(ma));
     launch_merge(ma, st);
   } else {
@@ -1362,7 +1373,8 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
   R.lw_prev = n_prev;
   if (R.band && R.reps[lb]) {
     if (!R.lw_last) return fail(ctx, PVT_EHIP, "representative lists need the one-wave list walk");
-    ca_.rowmap = P<int32_t>(ctx->brow[lb]);
+    ca_.rowmap = P<int32_t>(ctx->brun) + t0;
+    ca_.rowbase = R.rbase[lb];
     ca_.ordw = R.ord + t0;
   }
   {
@@ -1546,7 +1558,11 @@ static int place_ahead(pvt_ctx* ctx) {
                        r->placement, P<int32_t>(ctx->owned[1 - lb]), nq == 0 ? n_prev : 0,
                        P<int32_t>(ctx->owned[lb]), slot, nullptr, P<int32_t>(ctx->grp_ord) + t0,
                        ctx->stamps};
-        if (R.reps[lb]) { ca_.rowmap = P<int32_t>(ctx->brow[lb]); ca_.ordw = R.ord + t0; }
+        if (R.reps[lb]) {
+          ca_.rowmap = P<int32_t>(ctx->brun) + t0;
+          ca_.rowbase = R.rbase[lb];
+          ca_.ordw = R.ord + t0;
+        }
         ca_.gate = gate;
         ca_.ahead = 1;
         {

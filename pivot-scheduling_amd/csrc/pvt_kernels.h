@@ -161,10 +161,10 @@ struct CommitArgs {
   const int32_t* cseg;
   WinRec* wlog;
   int skip_done;          // chain mode: a chain whose status already says "all walked" is skipped
-  // vbp best-fit representative lists (pvt_band.hip band_reps): window task w's list is row
+  // vbp best-fit representative lists (pvt_band.hip band_runs_kernel): window task w's list is row
   // rowmap[w], its caller index ordw[w] (the list rows' TaskRec.ord belong to other tasks);
   // NULL: row w, TaskRec.ord
-  const int32_t* rowmap;
+  const int32_t* rowmap;  //   (row = rowmap[w] - rowbase: the round's run ids, band_runs_kernel)
   const int32_t* ordw;
   // Windows enqueued ahead (pvt_capi.hip place_ahead; one-wave list walk only): gate = the walk
   // before's status slot {stopped at, owned hosts, nt, skipped} -- closed (gate_closed) when that
@@ -172,6 +172,7 @@ struct CommitArgs {
   // owned hosts are this walk's inherited ones (n_prev). ahead: status is such a 4-word slot.
   const int32_t* gate;
   int ahead;
+  int rowbase;
 };
 
 // Speculative epochs, cost_aware best-fit. The epoch's group segments (processing order,
@@ -386,8 +387,7 @@ void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* fla
 void launch_band_score(const BandArgs& a, hipStream_t st);
 // Window tasks -> list rows: each run of equal demand vectors (bit for bit) shares one list row;
 // rdem = the rows' demands, *nrep = rows (nt <= MAX_WINDOW)
-void launch_band_reps(const double* dem, int nt, int32_t* row, double* rdem, int32_t* nrep,
-                      hipStream_t st, const int32_t* gate = nullptr);
+void launch_band_runs(const double* dem, int T, int32_t* run, double* rdem, hipStream_t st);
 
 int score_tasks_per_wave(int mode, int hosts, int force = 0);
 int score_diag(uint64_t* out, int n, int reset);   // PVT_DIAG builds; else PVT_EUNSUPPORTED

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
   auto rec_load = [&](int b0, double& r0, double& r1, double& r2, double& r3, int4& ri) {
     const int w = min(b0 + lane, max(A.nt - 1, 0));
     if (A.rowmap) {
-      const int row = A.rowmap[w];
+      const int row = A.rowmap[w] - A.rowbase;
       const double2 x = *reinterpret_cast<const double2*>(A.dem + (size_t)w * 4);
       const double2 y = *reinterpret_cast<const double2*>(A.dem + (size_t)w * 4 + 2);
       const int2 cc = *reinterpret_cast<const int2*>(&A.L.t[row].cnt);

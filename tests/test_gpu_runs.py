@@ -1,5 +1,5 @@
 """GPU parity of the frontier walk's bulk runs (pvt_zwalk.hip run_bulk / run step) and of the vbp
-best-fit representative lists (pvt_band.hip band_reps + pvt_lwalk.hip), on rounds built so that
+best-fit representative lists (pvt_band.hip band_runs_kernel + pvt_lwalk.hip), on rounds built so that
 long runs of equal demands fill hosts in index order across chunk boundaries.
 
 Reference order: each task takes the lowest-index fitting host (vbp first-fit, scheduler/vbp.py
