@@ -148,6 +148,7 @@ struct RoundState {
   std::vector<int32_t> runs;      //   the round's run ids (band_runs_kernel), on the host
   bool full_lists = false;        //   (one list per task: the list walk's fallback)
   bool lw_last = false;           // the walk in flight is the one-wave list walk (pvt_lwalk.hip)
+  bool lw_flag = false;           //   reporting through ctx->flag_host[4..6] (no copy, no sync)
   int lw_lb = 0, lw_prev = 0;     //   its list buffer and inherited hosts (for the fallback)
 };
 
@@ -215,6 +216,7 @@ struct pvt_ctx {
   int32_t* flag_host = nullptr;   // pinned word the grouped order's count kernel stores to
   int32_t* flag_hdev = nullptr;   //   (its device address)
   int32_t flag_seq = 0;
+  int32_t walk_seq = 0;           // the one-wave list walk's report in flag_host[4..6]
   void* gstage = nullptr;         // grouped order: counts, anchors, cost table (pinned)
   size_t gstage_cap = 0;
   uint64_t* stamps = nullptr;     // PVT_STAMPS builds: device per-phase cycle sums
@@ -601,27 +603,29 @@ static double bytes_per_candidate(int mode) {
 // synchronisation (*pending = true); the caller syncs once, later, and calls build_order_check.
 // Spin on the count kernel's flag (the staged counts are visible once it holds flag_seq). Every
 // 4096 polls the stream is queried: an idle stream with no flag is an error, never a hang.
-static int wait_stage_flag(pvt_ctx* ctx) {
-  volatile int32_t* f = ctx->flag_host;
+static int wait_host_flag(pvt_ctx* ctx, volatile int32_t* f, int32_t seq, const char* what) {
   for (uint32_t n = 1;; n++) {
-    if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == ctx->flag_seq) return PVT_OK;
+    if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == seq) return PVT_OK;
     __builtin_ia32_pause();                   // (yield the core's pipeline to its sibling thread)
     if (n >= (1u << 18)) {
       // a long wait (the GPU is shared or the round is large): stop spinning and block on the
-      // stream -- everything queued behind the count kernel runs without the host
+      // stream -- everything queued behind the kernel runs without the host
       HIPCHK(hipStreamSynchronize(ctx->stream));
-      if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == ctx->flag_seq) return PVT_OK;
-      return fail(ctx, PVT_EHIP, "grouped order: count kernel finished without its flag");
+      if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == seq) return PVT_OK;
+      return fail(ctx, PVT_EHIP, "%s: kernel finished without its flag", what);
     }
     if ((n & 4095) == 0) {
       const hipError_t e = hipStreamQuery(ctx->stream);
       if (e == hipSuccess) {
-        if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == ctx->flag_seq) return PVT_OK;
-        return fail(ctx, PVT_EHIP, "grouped order: count kernel finished without its flag");
+        if (__atomic_load_n(f, __ATOMIC_ACQUIRE) == seq) return PVT_OK;
+        return fail(ctx, PVT_EHIP, "%s: kernel finished without its flag", what);
       }
-      if (e != hipErrorNotReady) return fail(ctx, PVT_EHIP, "grouped order: %s", hipGetErrorString(e));
+      if (e != hipErrorNotReady) return fail(ctx, PVT_EHIP, "%s: %s", what, hipGetErrorString(e));
     }
   }
+}
+static int wait_stage_flag(pvt_ctx* ctx) {
+  return wait_host_flag(ctx, ctx->flag_host, ctx->flag_seq, "grouped order");
 }
 
 static int build_order_radix(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out);
@@ -1377,13 +1381,19 @@ static int walk_launch(pvt_ctx* ctx, int t0, int nt, int lb, int n_prev) {
     ca_.rowbase = R.rbase[lb];
     ca_.ordw = R.ord + t0;
   }
+  R.lw_flag = R.lw_last;
+  if (R.lw_flag) {               // the walk reports to mapped pinned words: the host polls them
+    ca_.hflag = ctx->flag_hdev + 4;
+    ca_.hseq = ++ctx->walk_seq;
+  }
   {
     Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, R.lw_last ? "lwalk_kernel" : "commit_kernel");
     if (R.lw_last) launch_lwalk(ca_, st);
     else launch_commit(ca_, st);
   }
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
+  if (!R.lw_flag)
+    HIPCHK(hipMemcpyAsync(ctx->next_host, status, sizeof(int32_t) * 2, hipMemcpyDeviceToHost, st));
   if (R.band) { R.touch_lb = lb; R.touch_status = status; }   // its hosts become touched before
                                                               // the next band score
   return PVT_OK;
@@ -1438,7 +1448,15 @@ static int lw_fallback(pvt_ctx* ctx, int t0, int nt, int* adv) {
 }
 
 static int walk_status(pvt_ctx* ctx, int t0, int nt, bool inherited, int* adv) {
-  HIPCHK(hipStreamSynchronize(ctx->stream));
+  if (ctx->rs.lw_flag) {
+    ctx->rs.lw_flag = false;
+    int rc = wait_host_flag(ctx, ctx->flag_host + 4, ctx->walk_seq, "list walk");
+    if (rc) return rc;
+    ctx->next_host[0] = __atomic_load_n(ctx->flag_host + 5, __ATOMIC_ACQUIRE);
+    ctx->next_host[1] = __atomic_load_n(ctx->flag_host + 6, __ATOMIC_ACQUIRE);
+  } else {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  }
   *adv = ctx->next_host[0];
   if (*adv == 0 && ctx->rs.lw_last) {
     int rc = lw_fallback(ctx, t0, nt, adv);

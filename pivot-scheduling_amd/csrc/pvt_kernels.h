@@ -173,6 +173,10 @@ struct CommitArgs {
   const int32_t* gate;
   int ahead;
   int rowbase;
+  // or NULL: mapped pinned words the walk also reports to -- [1] = status[0], [2] = status[1],
+  // then [0] = hseq (system-scope release): the host polls them instead of a copy + sync
+  int32_t* hflag;
+  int32_t hseq;
 };
 
 // Speculative epochs, cost_aware best-fit. The epoch's group segments (processing order,

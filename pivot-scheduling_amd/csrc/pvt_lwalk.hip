@@ -397,6 +397,12 @@ __global__ __launch_bounds__(WAVE) void lwalk_kernel(CommitArgs A) {
   if (lane == 0) {
     A.status[0] = status; A.status[1] = n_own;
     if (A.ahead) { A.status[2] = A.nt; A.status[3] = 0; }
+    if (A.hflag) {
+      A.hflag[1] = status;
+      A.hflag[2] = n_own;
+      __threadfence_system();
+      __hip_atomic_store(A.hflag, A.hseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 #ifdef PVT_STAMPS
   if (lane == 0 && A.stamps) {
