@@ -40,6 +40,7 @@ for s in "$@"; do
     kt_vbf)     mkdir -p gpurun_out/ktv && run kt_vbf 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ktv -o a -- python tools/walk_probe.py --mode vbp_bf --hosts 1000000 --tasks 10000 --reps 3 && PVT_AHEAD=0 run kt_vbf0 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ktv -o b -- python tools/walk_probe.py --mode vbp_bf --hosts 1000000 --tasks 10000 --reps 3 && python tools/trace_gaps.py gpurun_out/ktv/a_kernel_trace.csv 8 20 > gpurun_out/ktv_a.txt && python tools/trace_gaps.py gpurun_out/ktv/b_kernel_trace.csv 8 20 > gpurun_out/ktv_b.txt ;;
     st_lw)      run st_lw 150 python tools/lwalk_stamps.py 1000000 10000 ;;
     t_new)      run t_new 600 $T tests/test_gpu_restore.py tests/test_gpu_fused.py tests/test_gpu_epochs.py tests/test_gpu_headline.py ;;
+    t_sh)       run t_sh 600 $T tests/test_gpu_sharded.py tests/test_gpu_runs.py tests/test_gpu_band.py ;;
     t_batch)    run t_batch 300 $T tests/test_gpu_batch.py ;;
     t_rw)       run t_rw 400 $T tests/test_gpu_resident_walk.py tests/test_gpu_batch.py ;;
     b_c4w)      for m in ${C4M:-ca_bf ca_ff vbp_ff}; do run b_c4w_$m 150 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done ;;
