@@ -277,6 +277,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   const uint64_t t_start = zstamp();
   uint64_t n_chunks = 0, n_switch = 0, n_bulk = 0, n_runs = 0;
   uint64_t st_search = 0, st_p1 = 0, st_p2 = 0, n_probe = 0, n_iter = 0, st_batch = 0, n_single = 0;
+  uint64_t st_setup = 0, st_loop = 0, st_who = 0, st_rep = 0;   // run_bulk's parts
 #endif
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int base = KEYED ? 0 : A.coff[b];
@@ -600,6 +601,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     const bool two = __double_as_longlong(d2) == 0 && __double_as_longlong(d3) == 0;
     R = __builtin_amdgcn_readfirstlane(R);
     int cnt = 0;
+#ifdef PVT_STAMPS
+    const uint64_t tA1 = zstamp();
+    st_setup += tA1 - tA;
+#endif
     {
       // Pass 1: without per-lane masks: with d >= 0 a lane that fails a copy fails every later
       // one (its residual only falls further), so every lane just keeps subtracting, recording
@@ -638,6 +643,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       else pass1(IntC<4>{});
 #ifdef PVT_STAMPS
       n_iter += t;
+      st_loop += zstamp() - tA1;
 #endif
     }
     const int incl = wave_incl_scan_dpp(cnt);
@@ -665,6 +671,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       amax = max(amax, n);
     }
     if (lane < covered) S.lgid[k + lane] = who;
+#ifdef PVT_STAMPS
+    const uint64_t tC = zstamp();
+    st_who += tC - tB;
+#endif
     // (c - d as fma(-1, d, c), rounded once, the same bits; fma(-0, d, c) == c for the finite d
     // and c of a proven chain: one 0/1 factor per copy for every dimension)
     if (two) {
@@ -688,6 +698,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         }
       }
     }
+#ifdef PVT_STAMPS
+    st_rep += zstamp() - tC;
+#endif
     if (asg > 0) {
       const int q = k + pre + asg - 1;
       S.lg[q][0] = c0; S.lg[q][1] = c1; S.lg[q][2] = c2; S.lg[q][3] = c3;
@@ -1130,6 +1143,10 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     atomicAdd((unsigned long long*)&A.stamps[21], (unsigned long long)(t_win - t_cert));
     atomicAdd((unsigned long long*)&A.stamps[22], (unsigned long long)(t_cap - t_win));
     atomicAdd((unsigned long long*)&A.stamps[23], (unsigned long long)(t_walk - t_cap));
+    atomicAdd((unsigned long long*)&A.stamps[24], (unsigned long long)st_setup);
+    atomicAdd((unsigned long long*)&A.stamps[25], (unsigned long long)st_loop);
+    atomicAdd((unsigned long long*)&A.stamps[26], (unsigned long long)st_who);
+    atomicAdd((unsigned long long*)&A.stamps[27], (unsigned long long)st_rep);
   }
 #endif
 }
