@@ -166,6 +166,7 @@ def check_parity(got, r, ref=None):
 
 # ---------------------------------------------------------------------------- extra workloads
 KCLASSES = (("score", 0), ("merge", 1), ("commit", 2), ("other", 3))
+KCLASS_NAMES = tuple(n for n, _ in KCLASSES)
 
 
 # the kernels of the path that can dominate a step, timed one by one (pvt_get_kernel_kstats)
@@ -200,8 +201,9 @@ def time_round(eng, r, steps, warmup, batch=None):
         reset()
         run(dr)
     torch.cuda.synchronize()
+    dom, share, kms = dominant_kernel(eng, lambda: (reset(), run(dr)))
     eng.reset_kstats()
-    eng.set_profiling(2)
+    eng.set_profiling(2, kernel=dom)
     t0 = time.perf_counter()
     for _ in range(steps):
         reset()
@@ -211,6 +213,8 @@ def time_round(eng, r, steps, warmup, batch=None):
     eng.set_profiling(False)
     ks = kstats_all(eng)
     ks["kernels"] = kernel_times(eng)
+    ks["dominant_share"] = share
+    ks["kernels_untimed_ms_per_step"] = kms
     return ms, (dr.results() if batch else dr.result()), ks
 
 
@@ -257,7 +261,7 @@ def extra_workloads(eng, args, skip_mode):
             ok = check_parity(got, r, ref) if args.parity else None
         e = {"value": cand / (ms * 1e-3), "ms_per_step": ms, "hosts": H, "tasks": T, "steps": steps,
              "parity": ok, "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items()
-                                                   if k != "kernels"},
+                                                   if k in KCLASS_NAMES},
              "kernel_ms_per_step": {k: v["ms"] / steps for k, v in ks["kernels"].items()}}
         if B:
             e["scenarios"] = B
@@ -355,7 +359,7 @@ def scenario_batch_line(eng, args, rank, world, gloo, B, H=1000, T=1000):
             "tasks": T, "steps": steps, "scaling": "weak", "timing": "max over ranks of each "
             "rank's timed steps, between barriers", "parity": (ok if args.parity else None),
             "parity_scope": "every rank's scenarios vs the oracle (MIN-reduced)",
-            "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items() if k != "kernels"},
+            "kernels_ms_per_step": {k: v["ms"] / steps for k, v in ks.items() if k in KCLASS_NAMES},
             "kernel_ms_per_step": {k: v["ms"] / steps for k, v in ks["kernels"].items()},
             "roofline": dominant_roofline(mode, H, T, ks, eng.epoch_stats(), steps,
                                           variant="_b%d" % B, rounds_per_step=B, warm=warm)}
@@ -501,6 +505,27 @@ def walk_roofline(mode, H, T, c, ep, steps, kernel="zwalk_kernel", variant="", r
     return out
 
 
+def dominant_kernel(eng, step, n=2):
+    """(name, share of the timed kernels' device time, {name: ms per step}) of the kernel that
+    takes the most device time over n untimed steps with every named kernel timed. The timed
+    steps then record events around that kernel only (each event pair idles the stream a few
+    microseconds: timing every named kernel cost 0.33 ms of a 2.74 ms vbp best-fit step)."""
+    eng.reset_kstats()
+    eng.set_profiling(2)
+    for _ in range(n):
+        step()
+    import torch
+    torch.cuda.synchronize()
+    eng.set_profiling(False)
+    kt = kernel_times(eng)
+    eng.reset_kstats()
+    if not kt:
+        return None, None, {}
+    name = max(kt, key=lambda k: kt[k]["ms"])
+    share = kt[name]["ms"] / max(sum(v["ms"] for v in kt.values()), 1e-12)
+    return name, share, {k: v["ms"] / n for k, v in kt.items()}
+
+
 def dominant_roofline(mode, H, T, ks, ep, steps, variant="", rounds_per_step=1, warm=0):
     """The roofline of the kernel that takes the most device time in the timed steps (HIP events
     per kernel), with the PMC profile of that kernel on this config and this binary."""
@@ -510,6 +535,8 @@ def dominant_roofline(mode, H, T, ks, ep, steps, variant="", rounds_per_step=1, 
                 "traffic": None, "note": "no kernel of the path was timed"}
     kernel = max(kt, key=lambda n: kt[n]["ms"])
     share = kt[kernel]["ms"] / max(sum(v["ms"] for v in kt.values()), 1e-12)
+    if ks.get("dominant_share") is not None:      # (the timed steps timed this kernel only)
+        share = ks["dominant_share"]
     if kernel in WALK_KERNELS:
         out = walk_roofline(mode, H, T, kt[kernel], ep, steps, kernel, variant, rounds_per_step, warm)
     else:
@@ -904,10 +931,13 @@ def main():
     log("[rank %d] warmup done: %d/%d placed, windows=%d refills=%d"
         % (rank, placed, T, stats["windows"], stats["refills"]))
 
+    # events around the dominant kernel only (dominant_kernel: found over two untimed steps with
+    # every named kernel timed); BENCH_PROF=0: no events at all, for A/B of their cost (the
+    # roofline then has no kernel time), BENCH_PROF=1: every launch
+    prof = int(os.environ.get("BENCH_PROF", "2"))
+    dom, dom_share, dom_kms = dominant_kernel(eng, lambda: (reset(), run(dr))) if prof == 2 else (None, None, {})
     eng.reset_kstats()
-    # (events around the named kernels only: every launch costs ~30 us/round; BENCH_PROF=0: no
-    # events at all, for A/B of their cost -- the roofline then has no kernel time)
-    eng.set_profiling(int(os.environ.get("BENCH_PROF", "2")))
+    eng.set_profiling(prof, kernel=dom)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -929,6 +959,7 @@ def main():
     value = cand_per_step / (elapsed / args.steps)
     ks = kstats_all(eng)
     ks["kernels"] = kernel_times(eng)
+    ks["dominant_share"] = dom_share
 
     if rank == 0:
         out = {
@@ -961,10 +992,10 @@ def main():
             "roofline": dominant_roofline(mode, H, T, ks, ep, args.steps,
                                           variant=("_b%d" % B) if B else "",
                                           rounds_per_step=B or 1, warm=args.warmup),
-            "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items() if k != "kernels"},
+            "kernels_ms_per_step": {k: v["ms"] / args.steps for k, v in ks.items() if k in KCLASS_NAMES},
             "kernel_ms_per_step": {k: v["ms"] / args.steps for k, v in ks["kernels"].items()},
             "walk_us_per_task": (ks["commit"]["ms"] * 1e3 / args.steps / max(T * (B or 1), 1)
-                                 if not B else None),
+                                 if not B and ks["commit"]["ms"] > 0 else None),
             "windows_per_step": stats["windows"], "refills_per_step": stats["refills"],
             "epochs_per_step": ep["epochs"], "segments_per_step": ep["segments"],
             "rejected_segments_per_step": ep["rejected"],

@@ -147,6 +147,11 @@ int  pvt_get_kstats(pvt_ctx* ctx, int kclass, pvt_kstats* out);
  * "merge_path_kernel"), each bracketed
  * by its own HIP events on the stream it runs on. An unknown or unlaunched name gives zeros. */
 int  pvt_get_kernel_kstats(pvt_ctx* ctx, const char* kernel, pvt_kstats* out);
+/* With profiling on = 2, record events around the launches of this one named kernel only
+ * (NULL or "": every named kernel). Each event pair costs the stream a few microseconds of idle
+ * GPU (config 5: 0.33 ms of a 2.74 ms vbp best-fit round with every named kernel timed), so a
+ * benchmark times only the kernel its roofline is about. */
+int  pvt_set_profiling_kernel(pvt_ctx* ctx, const char* kernel);
 /* Tuning knob: tasks per window (0 = the policy's default; capped at 1024). */
 int  pvt_set_window(pvt_ctx* ctx, int tasks);
 /* Tuning knob: tasks per wave of the best-fit score kernel, 0 (the policy's default: 2 for vbp

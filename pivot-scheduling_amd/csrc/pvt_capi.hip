@@ -164,6 +164,7 @@ struct pvt_ctx {
   int window = 0;                 // 0: per-policy default
   int64_t windows = 0, refills = 0;
   int profiling = 0;               // 0 off, 1 every launch, 2 the named kernels only
+  std::string prof_only;           //   (2: this one named kernel, when set)
   pvt_kstats ks[PVT_K_COUNT];
   std::vector<hipEvent_t> evpool;
   std::vector<TimedLaunch> pending;
@@ -291,7 +292,10 @@ struct Scope {
     t.kclass = kclass; t.kname = kname; t.candidates = cand; t.bytes = bytes; t.a = t.b = nullptr;
     if (on()) { t.a = take_event(ctx); (void)hipEventRecord(t.a, st); }
   }
-  bool on() const { return ctx->profiling == 1 || (ctx->profiling == 2 && t.kname); }
+  bool on() const {
+    return ctx->profiling == 1 ||
+           (ctx->profiling == 2 && t.kname && (ctx->prof_only.empty() || ctx->prof_only == t.kname));
+  }
   ~Scope() {
     if (on()) {
       t.b = take_event(ctx);
@@ -442,6 +446,12 @@ extern "C" int pvt_ctx_set_stream(pvt_ctx* ctx, void* stream) {
 // every event recorded once when profiling is switched on, so a timed round neither creates an
 // event nor pays a first record (measured ~11 us on the default line's critical path).
 static constexpr size_t EVPOOL_WARM = 1024;
+extern "C" int pvt_set_profiling_kernel(pvt_ctx* ctx, const char* kernel) {
+  if (!ctx) return PVT_EINVAL;
+  ctx->prof_only = kernel ? kernel : "";
+  return PVT_OK;
+}
+
 extern "C" int pvt_set_profiling(pvt_ctx* ctx, int on) {
   if (!ctx) return PVT_EINVAL;
   ctx->profiling = on == 2 ? 2 : (on != 0 ? 1 : 0);

@@ -40,6 +40,7 @@ def load_library(path=None):
         "pvt_ctx_set_stream": ([c_void_p, c_void_p], c_int),
         "pvt_place": ([c_void_p, c_void_p], c_int),
         "pvt_set_profiling": ([c_void_p, c_int], c_int),
+        "pvt_set_profiling_kernel": ([c_void_p, ctypes.c_char_p], c_int),
         "pvt_reset_kstats": ([c_void_p], c_int),
         "pvt_get_kstats": ([c_void_p, c_int, ctypes.POINTER(_abi.pvt_kstats)], c_int),
         "pvt_get_kernel_kstats": ([c_void_p, ctypes.c_char_p, ctypes.POINTER(_abi.pvt_kstats)], c_int),
@@ -741,8 +742,10 @@ class PlacementEngine:
         return {"epochs": e.value, "segments": s.value, "rejected": r.value,
                 "frontier_chains": zf.value, "list_chains": zl.value, "longest_chain_tasks": zc.value}
 
-    def set_profiling(self, on=True):
-        """True / 1: HIP events around every launch; 2: around the named kernels only."""
+    def set_profiling(self, on=True, kernel=None):
+        """True / 1: HIP events around every launch; 2: around the named kernels only -- or, with
+        ``kernel``, around that one named kernel only."""
+        self._check(self.lib.pvt_set_profiling_kernel(self.ctx, kernel.encode() if kernel else None))
         self._check(self.lib.pvt_set_profiling(self.ctx, 2 if on == 2 else int(bool(on))))
 
     def reset_kstats(self):
