@@ -61,6 +61,9 @@ constexpr double ZW_BIG = 0x1p500;
 #ifndef PVT_ZW_UNROLL
 #define PVT_ZW_UNROLL 8
 #endif
+#ifndef PVT_ZW_CF
+#define PVT_ZW_CF 1                        // run_bulk pass 1 in certified closed form (copies_cf)
+#endif
 constexpr int ZW_UNROLL = PVT_ZW_UNROLL;   // run_bulk pass 1: copies per stop check
 constexpr int ZW_SB = 64;                  // suffix-minimum batches (the last one holds the rest)
 template <int WM>
@@ -75,6 +78,7 @@ struct ZwalkLDS {
   double smin[ZW_SB][4];                   // suffix minima of the demands, per 64-task batch
   double lg[128][4];                       // the batch's log: capacities after each commit
   int32_t lgid[128];                       //   and the host (64.. : a run carried into the next batch)
+  int32_t rwho[64], rstart[64];            // run_bulk: host / start flag per run position
   uint64_t sbits[CHAIN_MAX / 64];          // chain mode: bit i = a group segment starts at task i
   uint32_t amask[ZMAX];                    // anchor -> its zero-cost zones
   uint32_t umask;
@@ -140,6 +144,45 @@ __global__ __launch_bounds__(256) void host_min_kernel(const double* avail, int 
 // Fit from the minimum residual min(a - d): a >= d (best-fit) or a > d (first-fit, strict) in
 // every dimension; exact in sign for finite values (certificate 3).
 template <int N> struct IntC { static constexpr int value = N; };
+
+// ---- closed-form copy counts (run_bulk pass 1) ----------------------------------------------
+// Copies of a demand d > 0 a capacity x takes, subtracting sequentially: c = the largest j with
+// fit(x_j), x_j = fl(x_{j-1} - d) (fit: x_j >= 0, or > 0 STRICT). In exact arithmetic that is
+// floor(x / d) (STRICT: ceil(x / d) - 1). The estimate k from an approximate quotient is certified
+// against the sequential values without computing them: e_j = x - j d exactly, and
+//  * "nice" pairs -- x and d multiples of a power of two Q with every x - j d (j <= k + 1) below
+//    2^53 Q in magnitude (cpu counts, whole MiB) -- subtract exactly: x_j == e_j, so fit(e_k) and
+//    !fit(e_{k+1}) decide;
+//  * otherwise |x_j - e_j| <= j 2^-53 (|x| + j d) (one rounding per subtraction, intermediates
+//    below |x| + j d): e_k and e_{k+1} must clear twice that bound on their side of 0.
+// Anything else is "unsure" and the caller subtracts copy by copy. (x >= d > 0 here: the lane
+// fits one copy; counts are capped at ZW_CAP, more than any run takes.)
+constexpr int ZW_CAP = 128;
+__device__ __forceinline__ int lowbit_exp(double v) {   // exponent of v's lowest set bit (0: big)
+  const uint64_t b = (uint64_t)__double_as_longlong(v);
+  const uint64_t m = b & ((1ull << 52) - 1);
+  const int e = (int)((b >> 52) & 0x7ff);
+  if (e == 0) return m ? -1074 + __builtin_ctzll(m) : 4096;
+  return (e - 1075) + __builtin_ctzll(m | (1ull << 52));
+}
+__device__ __forceinline__ int high_exp(double v) {     // floor(log2 |v|) for normal v > 0
+  return (int)(((uint64_t)__double_as_longlong(v) >> 52) & 0x7ff) - 1023;
+}
+template <bool STRICT>
+__device__ __forceinline__ int copies_cf(double x, double d, bool& sure) {
+  if (__double_as_longlong(d) == 0) return ZW_CAP;      // (+0: the dimension never binds)
+  const double q = x * __builtin_amdgcn_rcp(d);
+  double kf = STRICT ? __builtin_ceil(q) - 1.0 : __builtin_floor(q);
+  kf = __builtin_fmin(kf, (double)ZW_CAP);
+  const double e0 = __builtin_fma(-kf, d, x), e1 = __builtin_fma(-(kf + 1.0), d, x);
+  const double big = __builtin_fabs(x) + (kf + 1.0) * d;
+  const bool nice = high_exp(big) + 2 <= min(lowbit_exp(x), lowbit_exp(d)) + 53;
+  const double err = nice ? 0.0 : (kf + 2.0) * 0x1p-52 * (big + d);
+  const bool fit0 = STRICT ? (e0 > err) : (e0 >= err && (nice || e0 > err));
+  const bool out1 = kf >= (double)ZW_CAP || (STRICT ? (e1 <= -err && (nice || e1 < -err)) : (e1 < -err));
+  sure = sure && kf >= 1.0 && fit0 && out1 && (q == q);
+  return (int)kf;
+}
 
 // A branch condition the wave holds uniformly: through readfirstlane, so that the compiler's
 // divergence analysis (which loses track across this walk's nested loops) keeps the branch scalar
@@ -278,6 +321,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   uint64_t n_chunks = 0, n_switch = 0, n_bulk = 0, n_runs = 0;
   uint64_t st_search = 0, st_p1 = 0, st_p2 = 0, n_probe = 0, n_iter = 0, st_batch = 0, n_single = 0;
   uint64_t st_setup = 0, st_loop = 0, st_who = 0, st_rep = 0;   // run_bulk's parts
+  uint64_t n_cf = 0;                                              // runs counted in closed form
 #endif
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int base = KEYED ? 0 : A.coff[b];
@@ -605,7 +649,32 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     const uint64_t tA1 = zstamp();
     st_setup += tA1 - tA;
 #endif
-    {
+    bool cf = false;                         // the closed-form counts are certified
+#if PVT_ZW_CF
+    if (R >= 2) {
+      // Pass 1 in closed form (copies_cf): every lane of m0 counts its copies from a quotient,
+      // certified per dimension; uncertain lanes only matter if the lanes before them do not
+      // cover the run (then the copy-by-copy pass below decides)
+      bool sure = true;
+      int k = ZW_CAP;
+      if (on1) {
+        k = min(copies_cf<STRICT>(c0, d0, sure), copies_cf<STRICT>(c1, d1, sure));
+        if (!two) k = min(k, min(copies_cf<STRICT>(c2, d2, sure), copies_cf<STRICT>(c3, d3, sure)));
+      }
+      const bool bad = on1 && !sure;
+      const uint64_t ub = __ballot(bad);
+      const int kc = on1 && sure ? k : 0;
+      const int inc = wave_incl_scan_dpp(kc);
+      const int first_bad = ub ? __builtin_ctzll(ub) : 64;
+      const int before_bad = first_bad == 0 ? 0 : __builtin_amdgcn_readlane(inc, first_bad - 1);
+      cf = ub == 0 || before_bad >= R;
+      if (cf) cnt = (lane < first_bad) ? kc : 0;
+#ifdef PVT_STAMPS
+      n_cf += cf;
+#endif
+    }
+#endif
+    if (!cf) {
       // Pass 1: without per-lane masks: with d >= 0 a lane that fails a copy fails every later
       // one (its residual only falls further), so every lane just keeps subtracting, recording
       // the last copy that fit (= the copies it takes); lanes outside m0 start at -inf.
@@ -643,9 +712,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       else pass1(IntC<4>{});
 #ifdef PVT_STAMPS
       n_iter += t;
-      st_loop += zstamp() - tA1;
 #endif
     }
+#ifdef PVT_STAMPS
+    st_loop += zstamp() - tA1;
+#endif
     const int incl = wave_incl_scan_dpp(cnt);
     const int pre = incl - cnt;
     const int asg = max(0, min(cnt, R - pre));
@@ -661,15 +732,15 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     // every copy and the capacities after a lane's last one only: a host's earlier entries in a
     // segment are never final (epoch_final_kernel marks them; validation and apply read the
     // capacities of final entries only, and the keyed / ordered walks read no log).
-    int32_t who = 0;
-    int amax = 0;
-    for (uint64_t mm = __ballot(asg > 0); mm; mm &= mm - 1) {
-      const int L = __builtin_ctzll(mm);
-      const int p = __builtin_amdgcn_readlane(pre, L), n = __builtin_amdgcn_readlane(asg, L);
-      const int32_t id = __builtin_amdgcn_readlane(cid, L);
-      who = (lane >= p && lane < p + n) ? id : who;
-      amax = max(amax, n);
-    }
+    // (each taking lane marks its first run position; a position's host is that of the last
+    // mark at or before it: two LDS round trips, no loop over the taking lanes)
+    S.rstart[lane] = 0;
+    if (asg > 0) { S.rstart[pre] = 1; S.rwho[pre] = cid; }
+    wave_lds_sync();
+    const uint64_t starts = __ballot(S.rstart[lane] != 0);
+    const uint64_t upto = starts & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+    const int32_t who = upto ? S.rwho[63 - __builtin_clzll(upto)] : 0;
+    const int amax = wave_max_i32(asg);
     if (lane < covered) S.lgid[k + lane] = who;
 #ifdef PVT_STAMPS
     const uint64_t tC = zstamp();
@@ -1147,6 +1218,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     atomicAdd((unsigned long long*)&A.stamps[25], (unsigned long long)st_loop);
     atomicAdd((unsigned long long*)&A.stamps[26], (unsigned long long)st_who);
     atomicAdd((unsigned long long*)&A.stamps[27], (unsigned long long)st_rep);
+    atomicAdd((unsigned long long*)&A.stamps[28], (unsigned long long)n_cf);
   }
 #endif
 }
