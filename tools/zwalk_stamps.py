@@ -41,5 +41,6 @@ print("  pass 1     %10.0f cycles per bulk call, %.1f iterations" % (buf[8] / ma
 print("  pass 2     %10.0f cycles per bulk call" % (buf[9] / max(buf[6], 1)))
 print("    per run: setup %.0f, pass-1 loop %.0f, who loop + host ids %.0f, replay %.0f"
       % tuple(buf[24 + k] / max(buf[6], 1) for k in range(4)))
+print("    runs counted in closed form: %d of %d" % (buf[28], buf[6]))
 print("  batches    %10.0f cycles per task (records, run masks, log flush)" % (buf[12] / max(buf[3], 1)))
 print("  single     %10d tasks on the one-task hot path" % buf[13])
