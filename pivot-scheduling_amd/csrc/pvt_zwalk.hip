@@ -632,7 +632,9 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   // subtractions on the chunk's registers, logging the capacities after each commit at the
   // task's batch position. Returns the tasks placed (>= 1; fewer than R when the chunk runs
   // out). Bit-exact: the same sequential subtractions as one task after the other.
-  auto run_bulk = [&](double& c0, double& c1, double& c2, double& c3, int32_t cid, double d0,
+  // (CFT: IntC<1> where the closed-form counts are compiled in -- the hot loop's call only: a
+  // copy at each of the four call sites ran the walk out of scalar registers)
+  auto run_bulk = [&](auto cft, double& c0, double& c1, double& c2, double& c3, int32_t cid, double d0,
                       double d1, double d2, double d3, uint64_t m0, int R, int k) -> int {
 #ifdef PVT_STAMPS
     const uint64_t tA = zstamp();
@@ -651,7 +653,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #endif
     bool cf = false;                         // the closed-form counts are certified
 #if PVT_ZW_CF
-    if (R >= 2) {
+    if (decltype(cft)::value && R >= 2) {
       // Pass 1 in closed form (copies_cf): every lane of m0 counts its copies from a quotient,
       // certified per dimension; uncertain lanes only matter if the lanes before them do not
       // cover the run (then the copy-by-copy pass below decides)
@@ -882,7 +884,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         if (UNI(fm != 0)) {
           dirty = true;
           ZW_SEARCH_DONE();
-          return run_bulk(ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, fm, R, k);
+          return run_bulk(IntC<0>{}, ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, fm, R, k);
         }
         if (__ballot(((rvalid >> lane) & 1ull) && fits<STRICT>(ra0, ra1, ra2, ra3, mn[0], mn[1], mn[2], mn[3])))
           break;                               // chunk p0 can still take a task ahead
@@ -902,7 +904,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         if (UNI(fb != 0)) {
           bdirty = true;
           ZW_SEARCH_DONE();
-          return run_bulk(rb0, rb1, rb2, rb3, bid, d0, d1, d2, d3, fb, R, k);
+          return run_bulk(IntC<0>{}, rb0, rb1, rb2, rb3, bid, d0, d1, d2, d3, fb, R, k);
         }
       }
       for (int c = (pb >= 0 ? pb : p0) + 1; c < nch; c++) {
@@ -920,7 +922,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
         if (!FF && UNI((fm & ~xzm) != 0)) return 0;
         if (UNI(fm != 0)) {
           ZW_SEARCH_DONE();
-          const int got = run_bulk(x0, x1, x2, x3, xid, d0, d1, d2, d3, fm, R, k);
+          const int got = run_bulk(IntC<0>{}, x0, x1, x2, x3, xid, d0, d1, d2, d3, fm, R, k);
           if (p < nwin) { S.wa[0][p] = x0; S.wa[1][p] = x1; S.wa[2][p] = x2; S.wa[3][p] = x3; }
           return got;
         }
@@ -968,7 +970,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
           // a run of tasks with this demand: placed in one pass over the chunk (run_bulk)
           const int R = run_len(k);
           if (UNI(R >= 2)) {
-            const int c = run_bulk(ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, m0, R, k);
+            const int c = run_bulk(IntC<1>{}, ra0, ra1, ra2, ra3, rid, d0, d1, d2, d3, m0, R, k);
             k += c;
             done += c;
             dirty = true;
