@@ -62,7 +62,11 @@ constexpr double ZW_BIG = 0x1p500;
 #define PVT_ZW_UNROLL 8
 #endif
 #ifndef PVT_ZW_CF
-#define PVT_ZW_CF 1                        // run_bulk pass 1 in certified closed form (copies_cf)
+// run_bulk pass 1 in certified closed form (copies_cf): correct (t_zw green with it on) but not
+// faster -- config 5 ca_bf 0.218 vs 0.210-0.215 ms, 243 of 360 runs certified; the quotient,
+// the exponent tests and the certification cost about what the copy-by-copy pass does for the
+// two iterations a run takes. Off by default, kept for A/B (-DPVT_ZW_CF=1).
+#define PVT_ZW_CF 0
 #endif
 constexpr int ZW_UNROLL = PVT_ZW_UNROLL;   // run_bulk pass 1: copies per stop check
 constexpr int ZW_SB = 64;                  // suffix-minimum batches (the last one holds the rest)
