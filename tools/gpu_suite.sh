@@ -27,6 +27,7 @@ for s in "$@"; do
     b_vbpbf1)   PVT_AHEAD=1 run b_vbpbf1 200 python bench.py --mode vbp_bf $NB ;;
     b_prof)     for m in ${BM:-vbp_bf ca_bf}; do BENCH_PROF=0 run b_p0_$m 200 python bench.py --mode $m $NB && run b_p2_$m 200 python bench.py --mode $m $NB; done ;;
     b_c3)       for m in ${C3M:-ca_bf ca_ff opp vbp_ff vbp_bf}; do run b_c3_$m 150 python bench.py --mode $m --hosts 100000 --tasks 1000 $NB --steps 20; done ;;
+    b_segs)     for sg in ${SEGS:-8 32}; do PVT_BAND_SEGS=$sg run b_vbpbf_s$sg 200 python bench.py --mode vbp_bf $NB; done ;;
     b_opp)      run b_opp 200 python bench.py --mode opp $NB ;;
     b_c4)       for w in ${C4W:-4 2}; do for m in ca_bf ca_ff opp vbp_ff vbp_bf; do PVT_RES_WAVES=$w run b_c4_${m}_w$w 120 python bench.py --batch 512 --hosts 1000 --tasks 1000 --mode $m --steps 10 $NB; done; done ;;
     t_res)      run t_res 600 $T tests/test_gpu_batch.py tests/test_gpu_parity.py tests/test_policies.py tests/test_sim_replay.py tests/test_lockstep.py tests/test_gpu_fused.py tests/test_anchor.py ;;
