@@ -456,8 +456,10 @@ def walk_roofline(mode, H, T, c, ep, steps, kernel="zwalk_kernel", variant="", r
     ms = c["ms"] / max(steps, 1)
     # epoch chains (cost_aware best-fit) run side by side: the longest chain per epoch is the
     # critical path (engine counter of the last round, summed over its epochs)
+    # (cost_aware first-fit's zero-key epochs walk their chains side by side as well)
     longest = (ep.get("longest_chain_tasks", 0)
-               if kernel in ("zwalk_kernel", "commit_kernel") and mode == MODES["ca_bf"] else 0)
+               if kernel in ("zwalk_kernel", "commit_kernel") and mode in (MODES["ca_bf"], MODES["ca_ff"])
+               else 0)
     if longest <= 0:
         longest = T                      # every task of the round on one walk after another
     issue_waves = min(4, WALK_WAVES.get(kernel, 1))
