@@ -802,8 +802,9 @@ def lockstep_workload(eng):
     cand = sum(o[1] for o in out)
     ok = all(o[3] for o in out)
     return {"workload": "config 2 sweep: %d recorded reference simulations (1000 hosts; %s) run "
-                        "side by side through the lock-step driver, drop-in policy classes, one "
-                        "pvt_place_batch per policy mode and one pvt_anchor per tick"
+                        "side by side through the lock-step driver, drop-in policy classes, every "
+                        "waiting round of every policy in one pvt_place_host_batch per tick "
+                        "(cost_aware groupings and anchor draws included)"
                         % (len(LOCKSTEP), ", ".join(n[4:] for n in LOCKSTEP)),
             "simulations": len(LOCKSTEP), "rounds": rounds, "candidates": cand,
             "value": cand / secs, "unit": "candidates/s", "seconds": secs,

@@ -1,8 +1,8 @@
 """Lock-step batched-scenario driver (pivot_place.lockstep).
 
 Several simulations run side by side; every engine call their drop-in policies make is served
-in batches (one pvt_place_batch per policy mode, one pvt_anchor for all), whenever every live
-simulation waits on the engine.
+in batches -- every waiting round that fits the resident kernel, of every policy, in one
+pvt_place_host_batch (the rest one by one) -- whenever every live simulation waits on the engine.
 
 * replay (CPU restatement / GPU engine): recorded reference simulations (tests/golden/sim_*)
   replayed concurrently through the driver, every round compared with the reference's;
