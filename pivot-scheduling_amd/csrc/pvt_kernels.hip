@@ -1210,10 +1210,12 @@ __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
     __syncthreads();
     return;
   }
-  // Bitonic network over P = 2^ceil(log2 n) elements, element i = m * 1024 + tid in registers:
-  // the compare-exchange stages of stride < 64 pair lanes of one wave (shuffles, no barrier);
-  // only the stages of stride >= 64 (10 of the 55 at P = 1024) go through LDS with a barrier
-  // each. (The all-LDS network: 20.6 us per config-5 round.)
+  // Runs of 64 sorted in registers by a bitonic network (element i = m * 1024 + tid; the stages
+  // pair lanes of one wave: shuffles, no barrier), every run ascending; then the runs merged
+  // pairwise in LDS, each element to (its rank in its own run) + (the number of the other run's
+  // elements below it: a binary search) -- log2(P / 64) rounds of one barrier each, where the
+  // bitonic network's stages of size > 64 took 24 stages at P = 512 (6 of them through LDS).
+  // (Padding pairs are (~0, 2^30 + i): distinct, after every real pair.)
   int P = 2;
   while (P < n) P <<= 1;
   constexpr int EMAX = GSORT_MAX / 1024;
@@ -1224,34 +1226,13 @@ __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
   for (int m = 0; m < EMAX; m++) {
     const int i = m * 1024 + tid;
     rk[m] = (m < E && i < n) ? k[i] : ~0ull;
-    rv[m] = (m < E && i < n) ? v[i] : 0x7fffffff;
+    rv[m] = (m < E && i < n) ? v[i] : (0x40000000 + i);
   }
   __syncthreads();
-  for (int size = 2; size <= P; size <<= 1) {
-    int stride = size >> 1;
-    if (stride >= 64) {
-#pragma unroll
-      for (int m = 0; m < EMAX; m++)
-        if (m < E) { k[m * 1024 + tid] = rk[m]; v[m * 1024 + tid] = rv[m]; }
-      __syncthreads();
-      for (; stride >= 64; stride >>= 1) {
-        for (int j = tid; j < (P >> 1); j += blockDim.x) {
-          const int lo = 2 * stride * (j / stride) + (j % stride), hi = lo + stride;
-          const bool up = (lo & size) == 0;
-          const uint64_t kl = k[lo], kh = k[hi];
-          const int32_t vl = v[lo], vh = v[hi];
-          const bool gt = kl > kh || (kl == kh && vl > vh);
-          if (gt == up) { k[lo] = kh; k[hi] = kl; v[lo] = vh; v[hi] = vl; }
-        }
-        __syncthreads();
-      }
-#pragma unroll
-      for (int m = 0; m < EMAX; m++)
-        if (m < E) { rk[m] = k[m * 1024 + tid]; rv[m] = v[m * 1024 + tid]; }
-      __syncthreads();
-    }
+  const int P64 = min(P, 64);
+  for (int size = 2; size <= P64; size <<= 1) {
     // (waves whose elements are all padding, i >= P, only ever pair with padding: they skip)
-    for (; stride > 0 && (tid & ~63) < P; stride >>= 1) {
+    for (int stride = size >> 1; stride > 0 && (tid & ~63) < P; stride >>= 1) {
 #pragma unroll
       for (int m = 0; m < EMAX; m++) {
         if (m >= E) continue;
@@ -1260,7 +1241,7 @@ __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
         const uint64_t pk = ((uint64_t)(uint32_t)__shfl_xor((int)khi, stride) << 32) |
                             (uint32_t)__shfl_xor((int)klo, stride);
         const int32_t pv = __shfl_xor(rv[m], stride);
-        const bool up = (i & size) == 0, low = (i & stride) == 0;
+        const bool up = size == P64 || (i & size) == 0, low = (i & stride) == 0;
         const uint64_t kl = low ? rk[m] : pk, kh = low ? pk : rk[m];
         const int32_t vl = low ? rv[m] : pv, vh = low ? pv : rv[m];
         const bool gt = kl > kh || (kl == kh && vl > vh);
@@ -1268,12 +1249,57 @@ __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
       }
     }
   }
+  if (P <= 64) {
+#pragma unroll
+    for (int m = 0; m < EMAX; m++) {
+      const int i = m * 1024 + tid;
+      if (m < E && i < n) v[i] = rv[m];
+    }
+    __syncthreads();
+    return;
+  }
+  __shared__ uint64_t k2[GSORT_MAX];
+  __shared__ int32_t v2[GSORT_MAX];
 #pragma unroll
   for (int m = 0; m < EMAX; m++) {
     const int i = m * 1024 + tid;
-    if (m < E && i < n) v[i] = rv[m];
+    if (m < E && i < P) { k[i] = rk[m]; v[i] = rv[m]; }
   }
   __syncthreads();
+  uint64_t* ka = k;
+  int32_t* va = v;
+  uint64_t* kb = k2;
+  int32_t* vb = v2;
+  for (int w = 64; w < P; w <<= 1) {
+#pragma unroll
+    for (int m = 0; m < EMAX; m++) {
+      const int i = m * 1024 + tid;
+      if (m >= E || i >= P) continue;
+      const uint64_t key = ka[i];
+      const int32_t val = va[i];
+      const int base = i & ~(2 * w - 1), off = i - base;
+      const bool left = off < w;
+      const int ob = left ? base + w : base;          // the other run
+      int lo = 0, len = w;                            // its elements below (key, val)
+      while (len > 0) {
+        const int half = len >> 1, mid = lo + half;
+        const uint64_t km = ka[ob + mid];
+        const bool below = km < key || (km == key && va[ob + mid] < val);
+        lo = below ? mid + 1 : lo;
+        len = below ? len - half - 1 : half;
+      }
+      const int dest = base + (left ? off : off - w) + lo;
+      kb[dest] = key;
+      vb[dest] = val;
+    }
+    __syncthreads();
+    uint64_t* tk = ka; ka = kb; kb = tk;
+    int32_t* tv = va; va = vb; vb = tv;
+  }
+  if (va != v) {
+    for (int i = tid; i < n; i += 1024) v[i] = va[i];
+    __syncthreads();
+  }
 }
 
 __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, const uint64_t* skey,
