@@ -1210,44 +1210,66 @@ __device__ void lds_sort_pairs(uint64_t* k, int32_t* v, int n) {
     __syncthreads();
     return;
   }
-  // Runs of 64 sorted by rank (each element counts the run's elements below it: 64 LDS
-  // broadcast reads -- a 21-stage bitonic network of lane shuffles cost three times as much),
-  // then the runs merged pairwise in LDS, each element to (its rank in its own run) + (the
-  // number of the other run's elements below it: a binary search) -- log2(P / 64) rounds of one
-  // barrier each. (Padding pairs are (~0, 2^30 + i): distinct, after every real pair.)
-  int P = 64;
+  // Runs of 64 sorted in registers by a bitonic network (element i = m * 1024 + tid; the stages
+  // pair lanes of one wave: shuffles, no barrier), every run ascending; then the runs merged
+  // pairwise in LDS, each element to (its rank in its own run) + (the number of the other run's
+  // elements below it: a binary search) -- log2(P / 64) rounds of one barrier each, where the
+  // bitonic network's stages of size > 64 took 24 stages at P = 512 (6 of them through LDS).
+  // (Padding pairs are (~0, 2^30 + i): distinct, after every real pair.)
+  int P = 2;
   while (P < n) P <<= 1;
   constexpr int EMAX = GSORT_MAX / 1024;
   const int E = (P + 1023) >> 10;
-  __shared__ uint64_t k2[GSORT_MAX];
-  __shared__ int32_t v2[GSORT_MAX];
-  for (int i = n + tid; i < P; i += 1024) { k[i] = ~0ull; v[i] = 0x40000000 + i; }
-  __syncthreads();
+  uint64_t rk[EMAX];
+  int32_t rv[EMAX];
 #pragma unroll
   for (int m = 0; m < EMAX; m++) {
     const int i = m * 1024 + tid;
-    if (m >= E || (i & ~63) >= P) continue;   // (wave-uniform)
-    const uint64_t key = k[i];
-    const int32_t val = v[i];
-    const int rb = i & ~63;
-    int r = 0;
-    for (int j = 0; j < 64; j++) {
-      const uint64_t kj = k[rb + j];
-      r += (kj < key || (kj == key && v[rb + j] < val)) ? 1 : 0;
-    }
-    k2[rb + r] = key;
-    v2[rb + r] = val;
+    rk[m] = (m < E && i < n) ? k[i] : ~0ull;
+    rv[m] = (m < E && i < n) ? v[i] : (0x40000000 + i);
   }
   __syncthreads();
-  if (P == 64) {
-    for (int i = tid; i < n; i += 1024) v[i] = v2[i];
+  const int P64 = min(P, 64);
+  for (int size = 2; size <= P64; size <<= 1) {
+    // (waves whose elements are all padding, i >= P, only ever pair with padding: they skip)
+    for (int stride = size >> 1; stride > 0 && (tid & ~63) < P; stride >>= 1) {
+#pragma unroll
+      for (int m = 0; m < EMAX; m++) {
+        if (m >= E) continue;
+        const int i = m * 1024 + tid;
+        const uint32_t klo = (uint32_t)rk[m], khi = (uint32_t)(rk[m] >> 32);
+        const uint64_t pk = ((uint64_t)(uint32_t)__shfl_xor((int)khi, stride) << 32) |
+                            (uint32_t)__shfl_xor((int)klo, stride);
+        const int32_t pv = __shfl_xor(rv[m], stride);
+        const bool up = size == P64 || (i & size) == 0, low = (i & stride) == 0;
+        const uint64_t kl = low ? rk[m] : pk, kh = low ? pk : rk[m];
+        const int32_t vl = low ? rv[m] : pv, vh = low ? pv : rv[m];
+        const bool gt = kl > kh || (kl == kh && vl > vh);
+        if (gt == up) { rk[m] = pk; rv[m] = pv; }
+      }
+    }
+  }
+  if (P <= 64) {
+#pragma unroll
+    for (int m = 0; m < EMAX; m++) {
+      const int i = m * 1024 + tid;
+      if (m < E && i < n) v[i] = rv[m];
+    }
     __syncthreads();
     return;
   }
-  uint64_t* ka = k2;
-  int32_t* va = v2;
-  uint64_t* kb = k;
-  int32_t* vb = v;
+  __shared__ uint64_t k2[GSORT_MAX];
+  __shared__ int32_t v2[GSORT_MAX];
+#pragma unroll
+  for (int m = 0; m < EMAX; m++) {
+    const int i = m * 1024 + tid;
+    if (m < E && i < P) { k[i] = rk[m]; v[i] = rv[m]; }
+  }
+  __syncthreads();
+  uint64_t* ka = k;
+  int32_t* va = v;
+  uint64_t* kb = k2;
+  int32_t* vb = v2;
   for (int w = 64; w < P; w <<= 1) {
 #pragma unroll
     for (int m = 0; m < EMAX; m++) {
