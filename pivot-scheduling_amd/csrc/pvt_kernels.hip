@@ -614,32 +614,29 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   while (P < S) P <<= 1;
   const int n = P * KL;                          // <= LMAX (merge_variant)
   const Key inv = {DINF, 0xffffffffu, 0x7fffffff};
-  __shared__ int s_feas[LMAX / KL];
   if (tid == 0) cnt_sh = 0;
-  // the segments and their feasible counts: unconditional (clamped) loads, all in flight before
-  // the first is stored
-  const int fv = A.seg_feas[(size_t)task * S + min(tid, S - 1)];
-  constexpr int PL = LMAX / 256;
-  Key kl[PL];
-#pragma unroll
-  for (int u = 0; u < PL; u++) {
-    const SegEntry se = A.seg[(size_t)task * S * KL + min(tid + u * 256, S * KL - 1)];
-    kl[u] = {se.s, se.tb, se.id};
+  for (int j = tid; j < n; j += 256) {
+    Key k = inv;
+    if (j < S * KL) {
+      const SegEntry se = A.seg[(size_t)task * S * KL + j];
+      k = {se.s, se.tb, se.id};
+    }
+    ka[j] = k;
   }
-#pragma unroll
-  for (int u = 0; u < PL; u++)
-    if (tid + u * 256 < n) ka[tid + u * 256] = tid + u * 256 < S * KL ? kl[u] : inv;
-  if (tid < S) s_feas[tid] = fv;
-  __syncthreads();
-  // bound: the smallest last entry (ka[g * KL + KL - 1]) of a segment with more than KL feasible
-  // hosts, from LDS (S dependent global load pairs per thread before)
+  // bound: the smallest last entry of a segment with more than KL feasible hosts (every thread
+  // derives it: S loads, no barrier on its path)
   Key bound = inv;
   long long tot = 0;
   for (int g = 0; g < S; g++) {
-    const int f = s_feas[g];
+    const int f = A.seg_feas[(size_t)task * S + g];
     tot += f;
-    if (f > KL && kless(ka[g * KL + KL - 1], bound)) bound = ka[g * KL + KL - 1];
+    if (f > KL) {
+      const SegEntry se = A.seg[((size_t)task * S + g) * KL + KL - 1];
+      const Key k = {se.s, se.tb, se.id};
+      if (kless(k, bound)) bound = k;
+    }
   }
+  __syncthreads();
   // (the two halves swap by pointer; the co-rank probes are then flat accesses to LDS, which
   // measured faster than indexing both halves by a round parity: 2.69 vs 3.04 ms per config-5
   // vbp best-fit round -- no global load is in flight during the rounds)
@@ -680,27 +677,24 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
   Key bnd = bound;
   if (cnt == LMAX && kless(src[LMAX - 1], bnd)) bnd = src[LMAX - 1];
   const int nw = max(cnt, KL);
-  // the kept hosts' zone and snapshot availability: branch-free gathers (host 0 stands in for
-  // an unused slot), so all 5 x PO of the thread's loads are in flight at once -- with a branch per
-  // entry the compiler waited after each group (~20k cycles per block, now one HBM latency)
+  // the kept hosts' zone and snapshot availability: every gather of the thread's (up to) four
+  // entries issued before the first is used (one HBM latency, not four)
   constexpr int PO = LMAX / 256;
   Key kk[PO];
   int32_t zz[PO];
   double aa[PO][4];
 #pragma unroll
-  for (int u = 0; u < PO; u++) {   // (the merged keys first: src is a flat pointer, and a flat
-    const int j = tid + u * 256;   //  load's wait would also wait for every gather issued before)
-    kk[u] = src[min(j, LMAX - 1)];
-    if (j >= cnt) kk[u] = inv;
-  }
-#pragma unroll
   for (int u = 0; u < PO; u++) {
-    const int h = tid + u * 256 < cnt ? kk[u].id : 0;
-    zz[u] = A.zone[h];
-    aa[u][0] = A.avail[h];
-    aa[u][1] = A.avail[(size_t)A.H + h];
-    aa[u][2] = A.avail[2 * (size_t)A.H + h];
-    aa[u][3] = A.avail[3 * (size_t)A.H + h];
+    const int j = tid + u * 256;
+    const bool ok = j < cnt;
+    kk[u] = inv;
+    if (ok) kk[u] = src[j];                  // (a select of the two addresses would be flat)
+    const int h = ok ? kk[u].id : 0;
+    zz[u] = ok ? A.zone[h] : 0;
+    aa[u][0] = ok ? A.avail[h] : 0.0;
+    aa[u][1] = ok ? A.avail[(size_t)A.H + h] : 0.0;
+    aa[u][2] = ok ? A.avail[2 * (size_t)A.H + h] : 0.0;
+    aa[u][3] = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
   }
 #pragma unroll
   for (int u = 0; u < PO; u++) {
@@ -708,10 +702,8 @@ __global__ __launch_bounds__(256) void merge_path_kernel(MergeArgs A) {
     if (j >= nw) continue;
     ListEntry e;
     e.s = kk[u].s; e.tb = kk[u].tb; e.id = kk[u].id; e.pad = 0; e.pad2 = 0.0;
-    const bool ok = j < cnt;
-    e.zone = ok ? zz[u] : 0;
-    e.a[0] = ok ? aa[u][0] : 0.0; e.a[1] = ok ? aa[u][1] : 0.0;
-    e.a[2] = ok ? aa[u][2] : 0.0; e.a[3] = ok ? aa[u][3] : 0.0;
+    e.zone = zz[u];
+    e.a[0] = aa[u][0]; e.a[1] = aa[u][1]; e.a[2] = aa[u][2]; e.a[3] = aa[u][3];
     A.L.e[(size_t)task * LMAX + j] = e;
     A.L.ids[(size_t)task * LMAX + j] = j < cnt ? kk[u].id : 0x7fffffff;
   }
