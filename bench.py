@@ -132,20 +132,52 @@ def _time_oracle(r, budget_s, threads):
         n = int(min(r.n_tasks, max(n + 1, n * 1.2 * budget_s / dt)))
 
 
+def _paired_oracle(r, budget_s, threads):
+    """The C restatement on ONE task prefix at two thread counts: the first n tasks, n sized so
+    one thread takes about budget_s / 3 seconds, then the same n tasks on ``threads`` threads
+    (repeated to at least a second). A prefix is not a uniform sample of a round (first-fit
+    tasks early in a round exit on the first hosts), so both rates must come from the same one.
+    Returns (rate all threads, rate 1 thread, n, seconds all, seconds 1, full-round result or
+    None)."""
+    from oracle import oracle
+    from pivot_place.synthetic import subset_tasks
+    v_one, n, dt_one, res = _time_oracle(r, budget_s / 3.0, 0)
+    sub = r if n >= r.n_tasks else subset_tasks(r, n)
+    reps, t = 0, time.perf_counter()
+    while True:
+        res = oracle.place(sub, threads=threads)
+        reps += 1
+        dt_all = max(time.perf_counter() - t, 1e-6)
+        if dt_all >= 1.0 or dt_all * (reps + 1) / reps > budget_s:
+            break
+    v_all = float(reps) * n * r.n_hosts / dt_all
+    return v_all, v_one, n, dt_all / reps, dt_one, (res if n >= r.n_tasks else None)
+
+
 def cpu_baseline(r, budget_s):
     """The CPU restatement (oracle/) timed on this host beside the GPU: all the cores this job
     may use (OMP_NUM_THREADS, else min(16, os.cpu_count()); OpenMP host scans) as the reported
-    value, 1 thread alongside. Returns (baseline dict, full-round oracle result or None)."""
+    value, 1 thread alongside, both on the same first tasks of the round. Returns (baseline
+    dict, full-round oracle result or None)."""
     threads = oracle_threads()
-    v_all, n_all, dt_all, res_all = _time_oracle(r, budget_s, threads)
-    v_one, n_one, dt_one, _ = _time_oracle(r, budget_s / 3.0, 0)
+    v_all, v_one, n, dt_all, dt_one, res = _paired_oracle(r, budget_s, threads)
     out = {"value": v_all, "unit": "candidates/s", "cores": threads, "kind": "port",
-           "value_1thread": v_one,
+           "value_1thread": v_one, "tasks": n,
            "sample": "oracle/pivot_oracle.c (naive T x H scan, not the engine's algorithm; "
-                     "OpenMP host scans, %d threads): first %d tasks x %d hosts of the same round "
-                     "(%.1f s); 1 thread: first %d tasks (%.1f s)"
-                     % (threads, n_all, r.n_hosts, dt_all, n_one, dt_one)}
-    return out, (res_all if n_all >= r.n_tasks else None)
+                     "OpenMP host scans): the first %d tasks x %d hosts of the same round on "
+                     "%d threads (%.2f s) and on 1 thread (%.1f s)"
+                     % (n, r.n_hosts, threads, dt_all, dt_one)}
+    return out, res
+
+
+# ---------------------------------------------------------------------------- the step
+def step_reset(eng, dr, full):
+    """The reset of one timed step (every place that prices a step -- main, time_round,
+    tools/walk_probe.py for PMC profiles -- takes it from here). A single round restores only
+    the hosts the previous step placed on (pvt_restore_hosts: a round changes no other
+    capacity); a scenario batch or a host-sharded round copies the whole snapshot back
+    (``full``)."""
+    return dr.reset if full else (lambda: eng.restore(dr))
 
 
 # ---------------------------------------------------------------------------- parity
@@ -196,7 +228,7 @@ def time_round(eng, r, steps, warmup, batch=None):
     from pivot_place.engine import DeviceBatch, DeviceRound
     dr = DeviceBatch(batch, eng.device) if batch else DeviceRound(r, eng.device)
     run = eng.run_batch if batch else eng.run
-    reset = dr.reset if batch else (lambda: eng.restore(dr))   # (as main's steps)
+    reset = step_reset(eng, dr, bool(batch))
     for _ in range(warmup):
         reset()
         run(dr)
@@ -281,18 +313,17 @@ def extra_workloads(eng, args, skip_mode):
 
 
 def round_cpu_baseline(r, threads, budget_s):
-    """CPU baseline of one extra round: the C restatement on all the job's cores over the WHOLE
-    round when that fits the budget (the same run is the parity reference), else over a
-    bounded sample of its first tasks; 1 thread on a sample beside it."""
-    v_all, n_all, dt_all, res_all = _time_oracle(r, budget_s, threads)
-    v_one, n_one, dt_one, _ = _time_oracle(r, budget_s / 3.0, 0)
+    """CPU baseline of one extra round: the C restatement on all the job's cores and on 1
+    thread, both on the same first tasks of the round (the whole round when one thread takes it
+    within the budget -- that run is then the parity reference)."""
+    v_all, v_one, n, dt_all, dt_one, res = _paired_oracle(r, budget_s, threads)
     out = {"value": v_all, "unit": "candidates/s", "cores": threads, "kind": "port",
-           "value_1thread": v_one,
-           "sample": "oracle/pivot_oracle.c (naive T x H scan, OpenMP host scans over %d threads) "
-                     "on %s x %d hosts (%.2f s); 1 thread: first %d tasks (%.2f s)"
-                     % (threads, "all %d tasks" % n_all if n_all >= r.n_tasks else
-                        "the first %d tasks" % n_all, r.n_hosts, dt_all, n_one, dt_one)}
-    return out, (res_all if n_all >= r.n_tasks else None)
+           "value_1thread": v_one, "tasks": n,
+           "sample": "oracle/pivot_oracle.c (naive T x H scan, OpenMP host scans) on %s x %d "
+                     "hosts: %d threads %.3f s, 1 thread %.2f s"
+                     % ("all %d tasks" % n if n >= r.n_tasks else "the first %d tasks" % n,
+                        r.n_hosts, threads, dt_all, dt_one)}
+    return out, res
 
 
 def batch_cpu_baseline(rounds, threads):
@@ -573,7 +604,7 @@ ROOF_TOP = ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic", "p
 ROOF_EXTRA = ("kernel", "bound", "achieved", "peak", "frac", "traffic", "pmc_source")
 EXTRA_KEYS = ("value", "ms_per_step", "ms_per_round", "parity", "n_gpus", "scenarios",
               "engine_seconds", "max_rounds_per_launch", "hbm_GBs_measured", "error")
-CPU_KEYS = ("value", "value_1thread", "cores", "engine_seconds")
+CPU_KEYS = ("value", "value_1thread", "tasks", "cores", "engine_seconds")
 TOP_DROP = ("extra", "kernels_ms_per_step", "kernel_ms_per_step")
 
 
@@ -922,7 +953,7 @@ def main():
     # each step places the same snapshot: a single round's reset restores the hosts the last
     # step placed on (pvt_restore_hosts, the only capacities a round changes; the parity check
     # below is on the last timed step, so an incomplete reset would show there)
-    reset = dr.reset if (B or hosts_sharded) else (lambda: eng.restore(dr))
+    reset = step_reset(eng, dr, bool(B or hosts_sharded))
 
     for i in range(args.warmup):
         reset()

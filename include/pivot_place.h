@@ -92,7 +92,11 @@ typedef struct pvt_round {
   const int32_t* zone;   /* [H] zone index of each host (Host.locality)                   */
   const uint32_t* tiebreak; /* [H] rank of the host-id string (PVT_VBP_BF), else NULL     */
   const int32_t* decay;  /* [H] max(len(h.tasks),1) (PVT_CA_FF host_decay), else NULL     */
-  const double* cost;    /* [Z*Z] egress cost, cost[src*Z + dst] (ResourceMetadata.cost)  */
+  const double* cost;    /* [Z*Z] egress cost, cost[src*Z + dst] (ResourceMetadata.cost);
+                            every cost[a][z] + cost[z][a] >= +0 (egress prices: a score
+                            c*r/bw then never grows as a residual r shrinks, and 0 is the
+                            least score). Host-array calls (pvt_place_host*) check both
+                            contracts (PVT_EINVAL), device rounds must meet them          */
   const double* bw;      /* [Z*Z] jittered bandwidth, bw[src*Z + dst]; every bw[a][z] +
                             bw[z][a] > 0 (resources/network.py bandwidths are positive: the
                             engine orders cost_aware scores >= +0 by their bits)           */

@@ -112,27 +112,78 @@ __device__ __forceinline__ int band_lower_bound(const uint64_t* key, int n, uint
   return m ? lo + __builtin_ctzll(m) : hi;
 }
 
-// One wave per (task, segment): segment s takes the sorted copy's 64-host chunks c with
-// c % S == s from the task's lower bound upward, then the touched list's chunks likewise.
-__global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
-  __shared__ uint64_t s_m1[WPB][KL], s_m2[WPB][KL];
-  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int g = blockIdx.x * WPB + wave;
-  const int t = g / A.S, seg = g % A.S;
-  if (gate_closed(A.gate)) return;
-  if (t >= A.nt || (A.nt_dev && t >= *A.nt_dev)) return;
-  const double* dp = A.dem + (size_t)t * 4;
-  const double d0 = dp[0], d1 = dp[1], d2 = dp[2], d3 = dp[3];
+// Diagnostic invariant checks (PVT_BAND_CHECK builds only; never the shipped library). A
+// finished segment list must be a prefix of filled entries, strictly ascending in
+// (score, tiebreak:id), with distinct ids; every entry of an untouched host (scored on the sorted
+// snapshot) a strict fit whose score is its exact residual norm; and complete: the untouched
+// strictly fitting hosts of the segment's chunks with a key at or below the list's last (all of
+// them, if the list is not full) are exactly its untouched entries. (Touched hosts are scored on
+// live capacities that a concurrent walk may still be committing to -- the next walk inherits
+// and rescores them -- so they are not re-checked here.)
+#ifdef PVT_BAND_CHECK
+__device__ void band_check(const BandArgs& A, int t, int seg, double ls, uint32_t lt, int32_t li,
+                           double d0, double d1, double d2, double d3) {
+  const int lane = lane_id();
+  const bool f = li != 0x7fffffff;
+  const uint64_t fm = __ballot(f);
+  const int filled = __popcll(fm);
+  const bool prefix = fm == (filled == 64 ? ~0ull : ((1ull << filled) - 1ull));
+  const uint64_t k1 = (uint64_t)__double_as_longlong(ls), k2 = ((uint64_t)lt << 32) | (uint32_t)li;
+  const uint64_t p1 = (uint64_t)__shfl_up((long long)k1, 1), p2 = (uint64_t)__shfl_up((long long)k2, 1);
+  const bool asc = !f || lane == 0 || p1 < k1 || (p1 == k1 && p2 < k2);
+  int dup = 0;
+  for (int L = 0; L < filled; L++) dup += (f && L != lane && readlane_i(li, L) == li) ? 1 : 0;
+  // the entry's sorted position (untouched hosts come from the sorted copy), -1: touched
+  int pos = -1;
+  if (f && li >= A.lo && li < A.hi && !A.touched[li])
+    for (int p = 0; p < A.n; p++)
+      if (A.sid[p] == li) { pos = p; break; }
+  bool exact = true;
+  if (pos >= 0) {
+    const double a0 = A.sa[pos], a1 = A.sa[(size_t)A.n + pos];
+    const double a2 = A.sa[2 * (size_t)A.n + pos], a3 = A.sa[3 * (size_t)A.n + pos];
+    const bool fit = fits<true>(a0, a1, a2, a3, d0, d1, d2, d3);
+    const double sc = __builtin_sqrt(norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3));
+    exact = fit && __double_as_longlong(sc) == __double_as_longlong(ls) && A.stb[pos] == lt;
+  }
+  const int n_untouched = __popcll(__ballot(pos >= 0));
+  // completeness over the segment's chunks (c % S == seg) of the sorted snapshot
+  const uint64_t lk1 = readlane_u64(k1, KL - 1), lk2 = readlane_u64(k2, KL - 1);
+  int below = 0;
+  for (int c = seg; c * WAVE < A.n; c += A.S) {
+    const int p = c * WAVE + lane;
+    if (p >= A.n || A.ptouched[p]) continue;
+    const double a0 = A.sa[p], a1 = A.sa[(size_t)A.n + p];
+    const double a2 = A.sa[2 * (size_t)A.n + p], a3 = A.sa[3 * (size_t)A.n + p];
+    if (!fits<true>(a0, a1, a2, a3, d0, d1, d2, d3)) continue;
+    const uint64_t c1 = (uint64_t)__double_as_longlong(__builtin_sqrt(norm2_seq(a0 - d0, a1 - d1, a2 - d2, a3 - d3)));
+    const uint64_t c2 = ((uint64_t)A.stb[p] << 32) | (uint32_t)A.sid[p];
+    below += (filled < KL || c1 < lk1 || (c1 == lk1 && c2 <= lk2)) ? 1 : 0;
+  }
+  for (int off = 32; off > 0; off >>= 1) below += __shfl_xor(below, off);
+  const bool complete = below == n_untouched;
+  const uint64_t bad_asc = __ballot(!asc), bad_dup = __ballot(dup != 0), bad_ex = __ballot(!exact);
+  if (lane == 0 && (!prefix || bad_asc || bad_dup || bad_ex || !complete))
+    printf("band_check t=%d seg=%d filled=%d prefix=%d asc=%llx dup=%llx exact=%llx untouched=%d "
+           "in_segment=%d\n", t, seg, filled, (int)prefix, (unsigned long long)bad_asc,
+           (unsigned long long)bad_dup, (unsigned long long)bad_ex, n_untouched, below);
+}
+#endif
+
+// One 64-host block of candidates (lane = host) for a band list: prefilter, strict fit, exact
+// score, merge into the wave-held list (ls, lt, li) and refresh its bound (ts, tt, ti, lim, rd).
+struct BandList {
   double ls = DINF;
   uint32_t lt = 0xffffffffu;
   int32_t li = 0x7fffffff;
   double ts = DINF, lim = DINF, rd = DINF;
   uint32_t tt = 0xffffffffu;
   int32_t ti = 0x7fffffff;
-  const int n = A.n;
+  double d0, d1, d2, d3;
+  uint64_t *m1, *m2;
 
-  // one 64-host block of candidates (lane = host): prefilter, strict fit, exact score, merge
-  auto consider = [&](bool ok, double a0, double a1, double a2, double a3, uint32_t tbh, int32_t h) {
+  __device__ __forceinline__ void consider(bool ok, double a0, double a1, double a2, double a3,
+                                           uint32_t tbh, int32_t h) {
     const bool pre = ok && (__builtin_fabs(a1 - d1) <= rd);
     if (__ballot(pre) == 0) return;
     const bool fit = pre && fits<true>(a0, a1, a2, a3, d0, d1, d2, d3);
@@ -146,17 +197,28 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
     const uint64_t ck2 = ((uint64_t)tbh << 32) | (uint32_t)h;
     const uint64_t pm = __ballot(pass && (ck1 < tk1 || (ck1 == tk1 && ck2 < tk2)));
     if (pm) {
-      list_merge(ls, lt, li, sc, tbh, h, pm, s_m1[wave], s_m2[wave]);
+      list_merge(ls, lt, li, sc, tbh, h, pm, m1, m2);
       ts = readlane_d(ls, KL - 1);
       tt = readlane_u(lt, KL - 1);
       ti = readlane_i(li, KL - 1);
       lim = vbp_lim(ts);
       rd = vbp_rad(ts);
     }
-  };
+  }
+};
 
-  // sorted snapshot: untouched hosts
-  const int lb = band_lower_bound(A.key, n, order_bits(d1));
+// The sorted snapshot (untouched hosts): segment `seg`'s chunks from the lower bound upward,
+// the next chunk's loads in flight while one is considered, until the chunk's smallest memory
+// leaves the radius.
+#ifdef PVT_BAND_HELPER
+__device__ __noinline__
+#else
+__device__ __forceinline__
+#endif
+void band_scan_sorted(const BandArgs& A, int seg, BandList& B) {
+  const int lane = lane_id();
+  const int n = A.n;
+  const int lb = band_lower_bound(A.key, n, order_bits(B.d1));
   const int c0 = lb >> 6;
   int c = c0 + ((seg - c0 % A.S) + A.S) % A.S;
   const int nch = (n + WAVE - 1) / WAVE;
@@ -181,26 +243,78 @@ __global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
     const int p = c * WAVE + lane;
     // the chunk's smallest memory is lane 0's (or its first position at or after lb): once it
     // is beyond the radius, so is every later chunk's -- the segment's list is final
-    if (readlane_d(a1, 0) - d1 > rd) break;
+    if (readlane_d(a1, 0) - B.d1 > B.rd) break;
     const bool ok = p < n && p >= lb && ntc == 0;   // (position flag: no dependent load of h's)
-    consider(ok, a0, a1, a2, a3, tbh, h);
+    B.consider(ok, a0, a1, a2, a3, tbh, h);
   }
-  // touched hosts: live capacities
+}
+
+// The touched hosts, with their live capacities (host-sharded: this rank's hosts only).
+__device__ __forceinline__ void band_scan_touched(const BandArgs& A, int seg, BandList& B) {
+  const int lane = lane_id();
   const int nt_ = *A.tcount;
+#ifdef PVT_BAND_PIPE2
+  // software-pipelined two deep: chunk cc + S's loads in flight while chunk cc is considered
+  auto load = [&](int cc, bool& ok, int32_t& h, double& a0, double& a1, double& a2, double& a3,
+                  uint32_t& tbh) {
+    const int j = cc * WAVE + lane;
+    const int32_t hj = (cc * WAVE < nt_ && j < nt_) ? A.tlist[j] : -1;
+    ok = hj >= A.lo && hj < A.hi;
+    h = ok ? hj : 0;
+    a0 = ok ? A.avail[h] : 0.0; a1 = ok ? A.avail[(size_t)A.H + h] : 0.0;
+    a2 = ok ? A.avail[2 * (size_t)A.H + h] : 0.0; a3 = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
+    tbh = ok ? A.tb[h] : 0u;
+  };
+  bool ok;
+  int32_t h;
+  double a0, a1, a2, a3;
+  uint32_t tbh;
+  load(seg, ok, h, a0, a1, a2, a3, tbh);
+  for (int cc = seg; cc * WAVE < nt_; cc += A.S) {
+    const bool cok = ok;
+    const int32_t ch = h;
+    const double c0 = a0, c1 = a1, c2 = a2, c3 = a3;
+    const uint32_t ctb = tbh;
+    load(cc + A.S, ok, h, a0, a1, a2, a3, tbh);
+    B.consider(cok, c0, c1, c2, c3, ctb, ch);
+  }
+#else
   for (int cc = seg; cc * WAVE < nt_; cc += A.S) {
     const int j = cc * WAVE + lane;
     const int32_t hj = j < nt_ ? A.tlist[j] : -1;
-    const bool ok = hj >= A.lo && hj < A.hi;   // (host-sharded: this rank's hosts only)
+    const bool ok = hj >= A.lo && hj < A.hi;
     const int32_t h = ok ? hj : 0;
     const double a0 = ok ? A.avail[h] : 0.0, a1 = ok ? A.avail[(size_t)A.H + h] : 0.0;
     const double a2 = ok ? A.avail[2 * (size_t)A.H + h] : 0.0, a3 = ok ? A.avail[3 * (size_t)A.H + h] : 0.0;
-    consider(ok, a0, a1, a2, a3, ok ? A.tb[h] : 0u, h);
+    B.consider(ok, a0, a1, a2, a3, ok ? A.tb[h] : 0u, h);
   }
+#endif
+}
+
+// One wave per (task, segment): segment s takes the sorted copy's 64-host chunks c with
+// c % S == s from the task's lower bound upward, then the touched list's chunks likewise.
+__global__ __launch_bounds__(256) void band_score_kernel(BandArgs A) {
+  __shared__ uint64_t s_m1[WPB][KL], s_m2[WPB][KL];
+  const int lane = lane_id(), wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = blockIdx.x * WPB + wave;
+  const int t = g / A.S, seg = g % A.S;
+  if (gate_closed(A.gate)) return;
+  if (t >= A.nt || (A.nt_dev && t >= *A.nt_dev)) return;
+  const double* dp = A.dem + (size_t)t * 4;
+  BandList B;
+  B.d0 = dp[0]; B.d1 = dp[1]; B.d2 = dp[2]; B.d3 = dp[3];
+  B.m1 = s_m1[wave];
+  B.m2 = s_m2[wave];
+  band_scan_sorted(A, seg, B);
+  band_scan_touched(A, seg, B);
+#ifdef PVT_BAND_CHECK
+  band_check(A, t, seg, B.ls, B.lt, B.li, B.d0, B.d1, B.d2, B.d3);
+#endif
   const size_t row = (size_t)t * A.S + seg;
   SegEntry e;
-  e.s = ls; e.tb = lt; e.id = li;
+  e.s = B.ls; e.tb = B.lt; e.id = B.li;
   A.seg[row * KL + lane] = e;
-  const int filled = __popcll(__ballot(li != 0x7fffffff));
+  const int filled = __popcll(__ballot(B.li != 0x7fffffff));
   if (lane == 0) A.seg_feas[row] = filled == KL ? KL + 1 : filled;
 }
 

@@ -74,7 +74,7 @@ __device__ __forceinline__ uint64_t rstamp() {
 constexpr int RW_SB = RES_MAX_TASKS / 64; // its suffix minima of the demands, per 64 positions
 
 struct ResLds {
-  int zt, ord, pl, u, cd, ci, mt, slot, wa, wz, wm, ws, wk, total;
+  int zt, ord, pl, u, cd, ci, mt, slot, wa, wz, ws, total;
   __host__ __device__ ResLds(int Zb, int Tpad, bool walk = false) {
     zt = 0;                                            // csum[Zb*Zb], bsum[Zb*Zb] f64
     ord = (16 * Zb * Zb + 15) & ~15;                   // processing order i32[Tpad]
@@ -89,14 +89,11 @@ struct ResLds {
     const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW + 32;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     // resident walk (after the sort, before the staging above): the round's hosts in LDS,
-    // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], per-chunk zero-score masks u64[16],
-    // suffix minima of the demands f64[RW_SB][4]
+    // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], suffix minima of the demands f64[RW_SB][4]
     wa = u;
     wz = wa + 32 * RW_MAXH;
-    wm = wz + 4 * RW_MAXH;
-    ws = wm + 8 * (RW_MAXH / 64);
-    wk = ws + 32 * RW_SB;                              // keyed first-fit: frozen keys f64[RW_MAXH]
-    const int rw_end = walk ? wk + 8 * RW_MAXH : 0;
+    ws = wz + 4 * RW_MAXH;
+    const int rw_end = walk ? ws + 32 * RW_SB : 0;
     total = walk_end > sort_end ? walk_end : sort_end;
     total = rw_end > total ? rw_end : total;
   }
@@ -153,13 +150,12 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
 }
 
 // ---- the resident walk: one wave places the round's tasks in order over its hosts in LDS
-// First-fit-shaped policies take, per task, the LOWEST-INDEX host of a "zero" class that fits:
-//   vbp first-fit (fit >=) and unsorted cost_aware first-fit (fit >): any fitting host;
-//   cost_aware best-fit: a fitting host of score exactly 0 -- zero-cost zone pair or exact fit
-//     (the fast winner of the 4-wave path above, with its "risky" rule: a fitting host whose
-//     score might underflow to 0 below the winner, or no zero-score host at all, stops the walk);
-//   keyed cost_aware first-fit: a strictly fitting host of frozen key exactly +0 (they lead the
-//     sorted host order in index order); none anywhere stops the walk.
+// cost_aware best-fit takes, per task, the LOWEST-INDEX fitting host of score exactly 0 --
+// zero-cost zone pair or exact fit (the fast winner of the 4-wave path below, with its "risky"
+// rule: a fitting host whose score might underflow to 0 below the winner, or no zero-score host
+// at all, stops the walk). (The first-fit policies measured faster on the 4-wave path, whose
+// block scan exits early: config 4, 512 rounds, ca_ff 0.753 vs 0.710 ms, vbp_ff 0.558 vs
+// 0.524 ms walked vs not; so only cost_aware best-fit is walked.)
 // Wave 0 holds chunk p0 (64 hosts, host p0 * 64 + lane) in registers -- the first chunk any
 // remaining task can still fit (suffix minima of the demands per 64 positions; capacities only
 // fall, so a chunk that cannot fit the componentwise least remaining demand never will) -- and
@@ -167,22 +163,17 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
 // memory access on its path; otherwise the later chunks are scanned in LDS. The other waves wait
 // at the closing barrier. Returns the first position the walk did not decide (T: all); the
 // 4-wave path goes on from there on the walked capacities.
-// Keyed first-fit: the frozen keys of the group in progress stay in LDS (wk) with the group
-// (*kgrp), so a walk that stops inside a group hands the 4-wave path the keys of its start.
-template <int MODE, int NT>
+template <int NT>
 __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, const int32_t* ord,
                              int32_t* pl, const double* csum, const double* bsum, bool has_groups,
-                             bool keyed, int* kgrp, uint64_t* A_stamps) {
-  constexpr bool STRICT = (MODE == CA_FF || MODE == VBP_BF);
-  __shared__ int s_stop, s_kgrp;
+                             uint64_t* A_stamps) {
+  __shared__ int s_stop;
   const int T = R.n_tasks, H = R.n_hosts, Z = R.n_zones;
   const int tid = threadIdx.x, lane = lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   double* wa = reinterpret_cast<double*>(smem + Lo.wa);      // [4][RW_MAXH]
   int32_t* wz = reinterpret_cast<int32_t*>(smem + Lo.wz);
-  uint64_t* wm = reinterpret_cast<uint64_t*>(smem + Lo.wm);  // keyed: zero-key hosts per chunk
   double* ws = reinterpret_cast<double*>(smem + Lo.ws);      // [RW_SB][4]
-  double* wk = reinterpret_cast<double*>(smem + Lo.wk);      // [RW_MAXH]
   for (int h = tid; h < H; h += NT) {
 #pragma unroll
     for (int r = 0; r < 4; r++) wa[r * RW_MAXH + h] = G(R.avail)[(size_t)r * H + h];
@@ -209,7 +200,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   __syncthreads();
   if (wave == 0) {
 #ifdef PVT_STAMPS
-    uint64_t n_probe = 0, n_adv = 0, n_keys = 0, st_task = 0;
+    uint64_t n_probe = 0, n_adv = 0, st_task = 0;
     const uint64_t tw_start = rstamp();
 #endif
     const int nch = (H + 63) >> 6;
@@ -229,29 +220,27 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       if (rv) { wa[q] = ra0; wa[RW_MAXH + q] = ra1; wa[2 * RW_MAXH + q] = ra2; wa[3 * RW_MAXH + q] = ra3; }
     };
     load_chunk(0);
-    // (cost_aware) zones of score 0 for the current anchor, and the safe zones: bw in (0, 2^300]
-    // and c == 0 or c in [2^-300, inf) -- as the 4-wave path's zmask / rmask
+    // zones of score 0 for the current anchor, and the safe zones: bw in (0, 2^300] and c == 0
+    // or c in [2^-300, inf) -- as the 4-wave path's zmask / rmask
     uint32_t zc_z = 0, sf_z = 0;
-    int cur_anc = -1, cur_grp = -1;
-    uint64_t rkm = 0;                          // keyed: zero-key lanes of chunk p0
+    int cur_anc = -1;
     // the task records of a 64-position batch in lanes (the next batch's loads in flight)
-    auto rec = [&](int b, double (&d)[4], int& anc, int& grp) {
+    auto rec = [&](int b, double (&d)[4], int& anc) {
       const int i = b * 64 + lane;
       const int t = i < T ? ord[i] : 0;
 #pragma unroll
       for (int r = 0; r < 4; r++) d[r] = G(R.dem)[(size_t)r * T + t];
-      grp = has_groups ? G(R.task_group)[t] : 0;
-      anc = has_groups ? G(R.group_anchor)[grp] : 0;
+      anc = has_groups ? G(R.group_anchor)[G(R.task_group)[t]] : 0;
     };
     double nd[4];
-    int nanc, ngrp;
-    rec(0, nd, nanc, ngrp);
+    int nanc;
+    rec(0, nd, nanc);
     int p = 0;
     bool stop = false;
     for (int b = 0; b < nsb && !stop; b++) {
       double td[4] = {nd[0], nd[1], nd[2], nd[3]};
-      const int tanc = nanc, tgrp = ngrp;
-      if (b + 1 < nsb) rec(b + 1, nd, nanc, ngrp);
+      const int tanc = nanc;
+      if (b + 1 < nsb) rec(b + 1, nd, nanc);
       const double mn0 = ws[b * 4 + 0], mn1 = ws[b * 4 + 1], mn2 = ws[b * 4 + 2], mn3 = ws[b * 4 + 3];
       const int kn = min(64, T - b * 64);
       for (int k = 0; k < kn; k++, p++) {
@@ -262,9 +251,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
         p0 = __builtin_amdgcn_readfirstlane(p0);
         const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
         const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
-        if (MODE == CA_BF || MODE == CA_FF) {
+        {
           const int a = readlane_i(tanc, k);
-          const int g = readlane_i(tgrp, k);
           if (a != cur_anc) {
             cur_anc = a;
             bool zc = false, sf = false;
@@ -275,67 +263,37 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
             }
             zc_z = (uint32_t)__ballot(zc);
             sf_z = (uint32_t)__ballot(sf);
-            cur_grp = -1;                      // (keyed: the keys depend on the anchor too)
-          }
-          if (MODE == CA_FF && keyed && g != cur_grp) {
-            // frozen host keys of the group (cost_aware.py:104-119) on the capacities now: only
-            // whether each is exactly +0 matters here
-            cur_grp = g;
-#ifdef PVT_STAMPS
-            n_keys++;
-#endif
-            store_chunk(p0);
-            for (int c = 0; c < nch; c++) {
-              const int q = c * 64 + lane;
-              const bool v = q < H;
-              const int qq = v ? q : 0;
-              const double x0 = wa[qq], x1 = wa[RW_MAXH + qq], x2 = wa[2 * RW_MAXH + qq], x3 = wa[3 * RW_MAXH + qq];
-              const int z = wz[qq];
-              const double r = __builtin_sqrt(norm2_seq(x0, x1, x2, x3));
-              const double df = (R.decay && v) ? (double)G(R.decay)[q] : 1.0;
-              const double key = (csum[a * Z + z] * df) / (r * bsum[a * Z + z]);
-              if (v) wk[q] = key;
-              const uint64_t m = __ballot(v && dbits(key) == 0);
-              if (lane == 0) wm[c] = m;
-              if (c == p0) rkm = m;
-            }
           }
         }
-        if (MODE == CA_BF && !(__builtin_fabs(d0) < DINF && __builtin_fabs(d1) < DINF &&
+        if (!(__builtin_fabs(d0) < DINF && __builtin_fabs(d1) < DINF &&
                                __builtin_fabs(d2) < DINF && __builtin_fabs(d3) < DINF)) {
           stop = true;                         // (a non-finite demand: the 4-wave path decides)
           break;
         }
         // one chunk's candidates: zm = fitting hosts of the zero class, rk = risky fitting hosts
         auto test = [&](double x0, double x1, double x2, double x3, int32_t z, bool v,
-                        uint64_t km, uint64_t& zm, uint64_t& rk) {
-          const bool f = v && fits<STRICT>(x0, x1, x2, x3, d0, d1, d2, d3);
-          bool zz = true, risky = false;
-          if (MODE == CA_BF) {
-            const double mx = fmax(fmax(x0 - d0, x1 - d1), fmax(x2 - d2, x3 - d3));
-            const bool sf = (sf_z >> z) & 1u, zc = (zc_z >> z) & 1u;
-            zz = sf && ((zc && mx <= 0x1p+500) || mx == 0.0);
-            risky = f && !zz && (!sf || !(mx >= 0x1p-300) || zc);
-          } else if (MODE == CA_FF && keyed) {
-            zz = (km >> lane) & 1ull;
-          }
+                        uint64_t& zm, uint64_t& rk) {
+          const bool f = v && fits<false>(x0, x1, x2, x3, d0, d1, d2, d3);   // (>=, cost_aware.py:91)
+          const double mx = fmax(fmax(x0 - d0, x1 - d1), fmax(x2 - d2, x3 - d3));
+          const bool sf = (sf_z >> z) & 1u, zc = (zc_z >> z) & 1u;
+          const bool zz = sf && ((zc && mx <= 0x1p+500) || mx == 0.0);
+          const bool risky = f && !zz && (!sf || !(mx >= 0x1p-300) || zc);
           zm = __ballot(f && zz);
           rk = __ballot(risky);
         };
         int win = -1;                           // host index, -1 none, -2 stop
         {
           uint64_t zm, rk;
-          test(ra0, ra1, ra2, ra3, rz, rv, rkm, zm, rk);
+          test(ra0, ra1, ra2, ra3, rz, rv, zm, rk);
           while (zm == 0 && rk == 0 && p0 + 1 < nch &&
-                 !__ballot(rv && fits<STRICT>(ra0, ra1, ra2, ra3, mn0, mn1, mn2, mn3))) {
+                 !__ballot(rv && fits<false>(ra0, ra1, ra2, ra3, mn0, mn1, mn2, mn3))) {
             store_chunk(p0);                   // dead: move the register chunk on
 #ifdef PVT_STAMPS
             n_adv++;
 #endif
             ++p0;
             load_chunk(p0);
-            if (MODE == CA_FF && keyed) rkm = rfl_u64(wm[p0]);
-            test(ra0, ra1, ra2, ra3, rz, rv, rkm, zm, rk);
+            test(ra0, ra1, ra2, ra3, rz, rv, zm, rk);
           }
           if (zm != 0) {
             const int w = __builtin_ctzll(zm);
@@ -356,9 +314,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
               const bool v = q < H;
               const int qq = v ? q : 0;
               const double x0 = wa[qq], x1 = wa[RW_MAXH + qq], x2 = wa[2 * RW_MAXH + qq], x3 = wa[3 * RW_MAXH + qq];
-              const uint64_t km = (MODE == CA_FF && keyed) ? rfl_u64(wm[c]) : 0ull;
               uint64_t zm2, rk2;
-              test(x0, x1, x2, x3, wz[qq], v, km, zm2, rk2);
+              test(x0, x1, x2, x3, wz[qq], v, zm2, rk2);
               if (zm2 != 0) {
                 const int w = __builtin_ctzll(zm2);
                 if (rk2 & ((1ull << w) - 1)) { win = -2; break; }
@@ -371,9 +328,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
               }
               if (rk2 != 0) { win = -2; break; }
             }
-            // nothing fits: first-fit by index leaves the task waiting; the zero-class
-            // policies have a positive-score / positive-key winner only the 4-wave path finds
-            if (win == -1 && (MODE == CA_BF || (MODE == CA_FF && keyed))) win = -2;
+            // no score-0 host fits: a positive-score winner only the 4-wave path finds
+            if (win == -1) win = -2;
           }
         }
         win = __builtin_amdgcn_readfirstlane(win);
@@ -385,19 +341,17 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       }
     }
     store_chunk(p0);
-    if (lane == 0) { s_stop = p; s_kgrp = cur_grp; }
+    if (lane == 0) s_stop = p;
 #ifdef PVT_STAMPS
     if (blockIdx.x == 0 && lane == 0 && A_stamps) {
       A_stamps[10] += n_probe;
       A_stamps[11] += n_adv;
-      A_stamps[12] += n_keys;
       A_stamps[13] += st_task;                  // cycles inside the task loop bodies
       A_stamps[14] += rstamp() - tw_start;      // wave 0's whole walk (records included)
     }
 #endif
   }
   __syncthreads();
-  *kgrp = s_kgrp;
   return s_stop;
 }
 
@@ -468,19 +422,15 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   }
   for (int i = tid; i < T; i += NT) G(R.order)[i] = ord[i];
 
-  // cost_aware best-fit rounds of up to RW_MAXH hosts: one wave walks them (resident_walk);
-  // this path takes over where it stops, on the walked capacities (and the keyed walk's group
-  // keys). The walk handles CA_FF / VBP_FF too, but there the block path's early-exit scan is
-  // cheaper (config 4, 512 rounds: ca_ff 0.753 vs 0.710 ms, vbp_ff 0.558 vs 0.524 ms walked vs
-  // not; ca_bf 0.743 vs 0.779 ms), so only CA_BF walks.
-  int p_start = 0, kgrp = -1;
-  constexpr bool WALKABLE = (MODE == CA_BF);
-  if (WALKABLE && A.walk && H <= RW_MAXH && T > 0 && !(CA && R.rt_bw)) {
+  // cost_aware best-fit rounds of up to RW_MAXH hosts: one wave walks them (resident_walk;
+  // ca_bf 0.743 vs 0.779 ms at config 4); this path takes over where it stops, on the walked
+  // capacities.
+  int p_start = 0;
+  if (MODE == CA_BF && A.walk && H <= RW_MAXH && T > 0 && !R.rt_bw) {
 #ifdef PVT_STAMPS
     const uint64_t tw0 = rstamp();
 #endif
-    p_start = resident_walk<MODE, NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, keyed, &kgrp,
-                                      A.stamps);
+    p_start = resident_walk<NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, A.stamps);
 #ifdef PVT_STAMPS
     if (blockIdx.x == 0 && tid == 0 && A.stamps) {   // walked tasks, walk cycles (block 0)
       A.stamps[8] += (uint64_t)p_start;
@@ -488,13 +438,11 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
     }
 #endif
     const double* wa = reinterpret_cast<const double*>(smem + Lo.wa);
-    const double* wk = reinterpret_cast<const double*>(smem + Lo.wk);
 #pragma unroll
     for (int j = 0; j < HPL; j++) {
       const int h = h0 + j;
       if (h < H) {
         a0[j] = wa[h]; a1[j] = wa[RW_MAXH + h]; a2[j] = wa[2 * RW_MAXH + h]; a3[j] = wa[3 * RW_MAXH + h];
-        if (MODE == CA_FF && keyed && kgrp >= 0) key[j] = wk[h];
       }
     }
   }
@@ -523,13 +471,6 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   uint64_t tl = stw ? rstamp() : 0;
 #endif
   int cur_anc = -1, cur_grp = -1, cur_bgrp = -1;
-  if (MODE == CA_FF && keyed && p_start < T && kgrp >= 0) {
-    // the walk stopped inside group kgrp: its keys (frozen at the group start) are in key[]
-    cur_grp = kgrp;
-    zmask = 0;
-#pragma unroll
-    for (int j = 0; j < HPL; j++) zmask |= (dbits(key[j]) == 0 ? 1u : 0u) << j;
-  }
   const bool rt = (MODE == CA_FF || MODE == CA_BF) && R.rt_bw != nullptr;
   // Sticky winner. A task whose demand is bit for bit the previous task's (same anchor, same
   // group when keys or realtime bandwidths are per group), with every demand >= 0, takes the

@@ -2157,7 +2157,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
     if ((rc = ensure_pinned_array(ctx, ctx->rmt_host, ctx->rmt_cap, (size_t)n * 625))) return rc;
     for (int i = 0; i < n; i++) {
       std::memcpy(ctx->rmt_host + (size_t)i * 625, rounds[i].mt_state, sizeof(uint32_t) * 625);
-      ctx->rstage[i].mt_state = mt + (size_t)i * 625;   // device copy (the kernel never reads the field)
+      ctx->rstage[i].mt_state = mt + (size_t)i * 625;   // the device copy the kernel draws from
     }
     void* dmt = nullptr;
     HIPCHK(hipHostGetDevicePointer(&dmt, ctx->rmt_host, 0));
@@ -2383,6 +2383,14 @@ static int check_host_round(pvt_ctx* ctx, const pvt_round* r, pvt_ca_items* it, 
   if (it) { s.hr.task_group = &one; s.hr.group_anchor = &one; s.hr.n_groups = 1; }
   int rc = check_round(ctx, &s.hr);
   if (rc) return rc;
+  if (ca && T > 0)   // host arrays: the zone-table contract of include/pivot_place.h (cost, bw)
+    for (int a = 0; a < Z; a++)
+      for (int z = 0; z < Z; z++) {
+        const double c = r->cost[a * Z + z] + r->cost[z * Z + a], b = r->bw[a * Z + z] + r->bw[z * Z + a];
+        if (!(c >= 0.0) || !(b > 0.0))
+          return fail(ctx, PVT_EINVAL, "zones (%d, %d): cost sum %g, bw sum %g (the engine needs "
+                      "cost sums >= 0 and bw sums > 0)", a, z, c, b);
+      }
   s.resident = T > 0 && resident_fits(&s.hr, ctx->resident_max);
   s.C = it ? it->n_items : 0;
   s.S = it ? it->n_storage : 0;
@@ -2597,7 +2605,8 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
   if (n_rounds == 0) return PVT_OK;
   std::vector<HostSlot> s(n_rounds);
   int rc;
-  int maxH = 1, maxT = 1, maxZ = 1, mode0 = rounds[0].mode;
+  // mode0: the first round with tasks (an empty round launches nothing and mixes no modes)
+  int maxH = 1, maxT = 1, maxZ = 1, mode0 = -1;
   bool mixed = false;
   for (int i = 0; i < n_rounds; i++) {
     pvt_ca_items* it = items ? items[i] : nullptr;
@@ -2616,6 +2625,7 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
     maxH = std::max(maxH, rounds[i].n_hosts);
     maxT = std::max(maxT, rounds[i].n_tasks);
     maxZ = std::max(maxZ, rounds[i].n_zones);
+    if (mode0 < 0) mode0 = rounds[i].mode;
     mixed |= rounds[i].mode != mode0;
   }
   HIPCHK(hipSetDevice(ctx->device));

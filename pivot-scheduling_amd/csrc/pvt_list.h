@@ -33,11 +33,24 @@ __device__ __forceinline__ void list_merge(double& s, uint32_t& t, int32_t& i, d
     mypos = (lane == L) ? pos : mypos;
   }
   const int np = lane + below;
+#ifdef PVT_BAND_CHECK
+  // diagnostic: every slot must be written before it is read (no real entry has id 0xdeadbeef)
+  m1[lane] = 0xdeadbeefdeadbeefull; m2[lane] = 0xdeadbeefdeadbeefull;
+  wave_sync();
+#endif
   if (np < KL) { m1[np] = e1; m2[np] = e2; }
   if (mypos < KL) { m1[mypos] = c1; m2[mypos] = c2; }
   wave_sync();
   const uint64_t r1 = m1[lane], r2 = m2[lane];
   wave_sync();   // read before the next merge writes
+#ifdef PVT_BAND_CHECK
+  {
+    const uint64_t un = __ballot((uint32_t)r2 == 0xdeadbeefu);
+    if (un && lane == 0)
+      printf("list_merge: unwritten slots %llx (candidates %llx)\n", (unsigned long long)un,
+             (unsigned long long)pm);
+  }
+#endif
   s = __longlong_as_double((long long)r1);
   t = (uint32_t)(r2 >> 32);
   i = (int32_t)(uint32_t)r2;

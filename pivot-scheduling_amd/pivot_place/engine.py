@@ -534,7 +534,9 @@ class PlacementEngine:
         """Whether place_host_batch takes this round (resident limits; the fused grouping's)."""
         if r.n_tasks == 0:
             return True
-        ok = r.n_hosts <= _abi.PVT_RESIDENT_MAX_HOSTS and r.n_tasks <= _abi.PVT_RESIDENT_MAX_TASKS
+        max_hosts = min(getattr(self, "_resident_max", _abi.PVT_RESIDENT_MAX_HOSTS),
+                        _abi.PVT_RESIDENT_MAX_HOSTS)   # the C side's resident_fits limit
+        ok = r.n_hosts <= max_hosts and r.n_tasks <= _abi.PVT_RESIDENT_MAX_TASKS
         if ca_args is not None:
             n_storage = len(ca_args[5])
             ok = ok and r.n_tasks <= _abi.GRP_MAX_TASKS and 1 <= n_storage and \
@@ -622,6 +624,7 @@ class PlacementEngine:
     def set_resident(self, max_hosts=_abi.PVT_RESIDENT_MAX_HOSTS):
         """pvt_place runs rounds up to ``max_hosts`` hosts on the resident kernel (0: never)."""
         self._check(self.lib.pvt_set_resident(self.ctx, int(max_hosts)))
+        self._resident_max = int(max_hosts)   # host_batch_fits mirrors the context's limit
 
     # -- anchor resolution (include/pivot_place.h, pvt_anchor; reference cost_aware.py:45-58)
     def anchor_device(self, off, lst, zone, mode_host, anchor_zone, inst_host=None, item=None):

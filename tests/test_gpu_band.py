@@ -114,3 +114,30 @@ def test_one_wave_list_walk_equals_list_walk(H, T, seed):
         e.set_band(1)
     _same(one.place(r), ref)
     _same(scout.place(r), ref)
+
+
+@pytest.mark.parametrize("H,T,seed,one_fit", [(70_000, 2600, 11, False), (300_000, 5000, 12, False),
+                                              (20_000, 4000, 13, True)])
+def test_walks_enqueued_ahead(H, T, seed, one_fit):
+    """place_ahead (PVT_AHEAD=1, off by default: measured slower): up to 8 vbp best-fit walks
+    enqueued at once, each gated on the previous walk's device status slot (skipped after an
+    early stop, its owned hosts otherwise inherited). Same round as the oracle, including hosts
+    that fit one task each (refills, skipped windows, the inherited-host fallback)."""
+    import os
+    from pivot_place.engine import PlacementEngine
+    r = synthetic.make_round(_abi.PVT_VBP_BF, H, T, seed=seed)
+    if one_fit:
+        r.avail[0, :] = 1.5
+    ref = oracle.place(r, threads=8)
+    old = os.environ.get("PVT_AHEAD")
+    try:
+        os.environ["PVT_AHEAD"] = "1"
+        ahead = PlacementEngine(0)
+    finally:
+        if old is None:
+            os.environ.pop("PVT_AHEAD", None)
+        else:
+            os.environ["PVT_AHEAD"] = old
+    ahead.set_resident(0)
+    ahead.set_band(1)
+    _same(ahead.place(r), ref)

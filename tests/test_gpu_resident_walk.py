@@ -138,3 +138,20 @@ def test_sticky_runs_of_equal_demands(engine, engine_nowalk, mode):
             r.dem[2, 100:140] = -1.0                # (a run with a negative demand component)
         rounds.append(r)
     _check(engine, engine_nowalk, rounds, "sticky runs mode %d" % mode)
+
+
+def test_negative_egress_cost_is_refused(engine):
+    """Egress costs are prices: include/pivot_place.h requires cost[a][z] + cost[z][a] >= +0
+    (and bw sums > 0) -- the engine orders cost_aware scores >= +0 by their bits and keeps a
+    best-fit winner while its residual shrinks. Host-array calls check the contract and refuse a
+    round that breaks it (PVT_EINVAL) instead of placing it differently from the reference."""
+    for mode in (_abi.PVT_CA_BF, _abi.PVT_CA_FF):
+        for H in (600, 20_000):                   # the resident kernel and the windowed engine
+            r = synthetic.make_round(mode, H, 300, seed=160)
+            r.cost = np.where(r.cost > 0, -r.cost, 0.0)
+            with pytest.raises(Exception, match="cost sum"):
+                engine.place(r)
+            r.cost = np.where(r.cost < 0, 0.0, r.cost)
+            r.bw = np.zeros_like(r.bw)
+            with pytest.raises(Exception, match="bw sum"):
+                engine.place(r)

@@ -70,6 +70,22 @@ def test_lockstep_replay_on_engine(engine):
     assert st["max_rounds_per_launch"] >= 6, st
 
 
+@pytest.mark.gpu
+def test_lockstep_replay_resident_off(engine):
+    """With the resident kernel switched off (set_resident(0)) host_batch_fits must refuse every
+    round pvt_place_host_batch would reject, so the driver serves them one by one (fused
+    cost_aware calls and windowed rounds) -- every round still bit-exact, no error."""
+    from pivot_place import _abi
+    engine.set_resident(0)
+    try:
+        driver = LockstepDriver(engine)
+        traces = driver.run([lambda eng, n=n: _replay(n, eng) for n in REPLAY])
+        assert [t["name"] for t in traces] == REPLAY
+        assert driver.stats["host_batch_rounds"] == 0, driver.stats
+    finally:
+        engine.set_resident(_abi.PVT_RESIDENT_MAX_HOSTS)
+
+
 def test_driver_propagates_errors():
     class Boom(BatchOracle):
         def place_batch(self, rounds):

@@ -37,4 +37,4 @@ for s in $sets; do
     *)   echo "unknown set $s"; exit 2 ;;
   esac
 done
-python tools/pmc_index.py gpurun_out/pmc_index.json "${idx[@]}"
+python tools/pmc_index.py --dest "profiles/$tag" gpurun_out/pmc_index.json "${idx[@]}"

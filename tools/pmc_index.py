@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Collect tools/pmc_profile.py outputs into the index bench.py reads (profiles/pmc_index.json):
 
-    python tools/pmc_index.py profiles/pmc_index.json ca_bf:1000000:10000:gpurun_out/pmc_r03_zwalk.json ...
+    python tools/pmc_index.py [--dest profiles/r06a] profiles/pmc_index.json ca_bf:1000000:10000:gpurun_out/pmc_r03_zwalk.json ...
+
+--dest DIR: the tracked directory the profiles are copied to (gpurun_out/ is scratch); each
+entry's "source" then names DIR/<file> instead of the scratch path it was read from.
 
 Each argument after the output is mode:hosts:tasks:pmc_json. The entry key is
 "<mode>_<hosts>_<tasks>:<kernel>" (kernel = the short __global__ name the profile matched); the
@@ -24,13 +27,17 @@ def short(name):
 
 
 def main():
-    out_path = sys.argv[1]
+    argv = sys.argv[1:]
+    dest = None
+    if argv[:1] == ["--dest"]:
+        dest, argv = argv[1], argv[2:]
+    out_path = argv[0]
     idx = {"entries": {}}
     if os.path.exists(out_path):
         with open(out_path) as f:
             idx = json.load(f)
         idx.setdefault("entries", {})
-    for spec in sys.argv[2:]:
+    for spec in argv[1:]:
         mode, hosts, tasks, path = spec.split(":", 3)
         with open(path) as f:
             p = json.load(f)
@@ -38,7 +45,8 @@ def main():
         reps = int(probe[probe.index("--reps") + 1]) if "--reps" in probe else 1
         disp = p["counters_per_launch"].get("dispatches_sq", reps)
         p["launches_per_round"] = disp / float(max(reps, 1))
-        p["source"] = os.path.relpath(path)
+        p["source"] = (os.path.join(dest, os.path.basename(path)) if dest
+                       else os.path.relpath(path))
         key = "%s_%s_%s:%s" % (mode, hosts, tasks, short(p["kernel"]))
         idx["entries"][key] = p
         print(key, "launches/round %.1f" % p["launches_per_round"], p.get("lib_sha256", "?")[:12])

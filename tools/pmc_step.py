@@ -2,8 +2,9 @@
 """HBM bytes of one whole bench step, from rocprofv3 counters (run on the GPU box; every pass is
 a child `rocprofv3 --pmc ... -- python tools/walk_probe.py --marker 1 ...` under a hard limit).
 
-The step's traffic is the sum over EVERY kernel dispatch of one round (snapshot-reset copy,
-ordering, epochs, walks, validation, apply), not just the dominant kernel's:
+The step's traffic is the sum over EVERY kernel dispatch of one round (bench.py's reset --
+pvt_restore_hosts of the hosts the previous rep placed on for a single round, the snapshot copy
+for a batch --, ordering, epochs, walks, validation, apply), not just the dominant kernel's:
     hbm_bytes_per_step = sum over the step's dispatches of (2 x FETCH_SIZE + WRITE_SIZE) KiB
 (FETCH_SIZE doubled, WRITE_SIZE as read: MI355X_MICROARCH.md §HBM; FETCH_SIZE and WRITE_SIZE
 need 3 + 2 TCC slots, so they are two passes.) walk_probe.py --marker 1 launches a one-element

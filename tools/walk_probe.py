@@ -10,8 +10,10 @@ stalls shows where). Exits non-zero if the engine reports an error (e.g. a hand-
 --batch B: the config-4 shape, B scenarios (seeds seed + s) in one pvt_place_batch per rep.
 --loaded 1: bench.py's loaded config-5 round (every host capped at 1 free cpu).
 --marker 1: a marker kernel before every rep (tools/pmc_step.py: HBM bytes of a whole step).
-The shapes are exactly those of bench.py's lines, so a PMC profile of the probe prices the
-launches bench.py times.
+The shapes and the per-step reset are exactly those of bench.py's lines (bench.step_reset: a
+single round restores the hosts the previous rep placed on, a batch copies its snapshot back),
+so a PMC profile of the probe prices the launches bench.py times
+(tests/test_gpu_restore.py::test_walk_probe_step_is_bench_step).
 """
 import argparse
 import os
@@ -22,6 +24,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "pivot-scheduling_amd"), ROOT]
 
 MODES = {"ca_ff": 0, "ca_bf": 1, "opp": 2, "vbp_ff": 3, "vbp_bf": 4}
+
+
+def probe_step(eng, dr, run, batched):
+    """One rep: bench.py's step (its reset, then the placement)."""
+    from bench import step_reset
+    reset = step_reset(eng, dr, batched)
+
+    def step():
+        reset()
+        run(dr)
+    return step
 
 
 def main():
@@ -60,12 +73,12 @@ def main():
     eng.reset_kstats()
     eng.set_profiling(True)
     mark = torch.zeros(1, dtype=torch.int64, device=eng.device) if a.marker else None
+    step = probe_step(eng, dr, run, bool(a.batch))
     for rep in range(a.reps):
         if mark is not None:
             mark.bitwise_not_()
         t = time.perf_counter()
-        dr.reset()
-        run(dr)
+        step()
         torch.cuda.synchronize()
         st = eng.last_stats()
         print("walk probe rep %d: mode %s H=%d T=%d batch=%d loaded=%d pipeline=%d  %.2f ms  "
