@@ -37,6 +37,8 @@
 
 #include "pivot_place.h"
 #include "pvt_device.h"
+#include "pvt_anchor_dev.h"
+#include "pvt_groups_dev.h"
 #include "pvt_kernels.h"
 #include "pvt_mt.h"
 
@@ -166,7 +168,7 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
 template <int NT>
 __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, const int32_t* ord,
                              int32_t* pl, const double* csum, const double* bsum, bool has_groups,
-                             uint64_t* A_stamps) {
+                             int walker, uint64_t* A_stamps) {
   __shared__ int s_stop;
   const int T = R.n_tasks, H = R.n_hosts, Z = R.n_zones;
   const int tid = threadIdx.x, lane = lane_id();
@@ -198,7 +200,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   if (tid < 4)
     for (int blk = nsb - 2; blk >= 0; blk--) ws[blk * 4 + tid] = fmin(ws[blk * 4 + tid], ws[(blk + 1) * 4 + tid]);
   __syncthreads();
-  if (wave == 0) {
+  if (wave == walker) {
 #ifdef PVT_STAMPS
     uint64_t n_probe = 0, n_adv = 0, st_task = 0;
     const uint64_t tw_start = rstamp();
@@ -224,6 +226,15 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
     // or c in [2^-300, inf) -- as the 4-wave path's zmask / rmask
     uint32_t zc_z = 0, sf_z = 0;
     int cur_anc = -1;
+    // the same as lane masks of the register chunk (recomputed when the anchor or the chunk
+    // changes): valid hosts, safe zones, safe zero-cost zones
+    uint64_t m_v = 0, m_sf = 0, m_zs = 0;
+    auto chunk_masks = [&]() {
+      const bool sf = rv && ((sf_z >> rz) & 1u), zc = (zc_z >> rz) & 1u;
+      m_v = __ballot(rv);
+      m_sf = __ballot(sf);
+      m_zs = __ballot(sf && zc);
+    };
     // the task records of a 64-position batch in lanes (the next batch's loads in flight)
     auto rec = [&](int b, double (&d)[4], int& anc) {
       const int i = b * 64 + lane;
@@ -240,6 +251,9 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
     for (int b = 0; b < nsb && !stop; b++) {
       double td[4] = {nd[0], nd[1], nd[2], nd[3]};
       const int tanc = nanc;
+      // tasks of the batch with a non-finite demand component (the 4-wave path decides them)
+      const uint64_t nonfin = __ballot(!(__builtin_fabs(td[0]) < DINF && __builtin_fabs(td[1]) < DINF &&
+                                         __builtin_fabs(td[2]) < DINF && __builtin_fabs(td[3]) < DINF));
       if (b + 1 < nsb) rec(b + 1, nd, nanc);
       const double mn0 = ws[b * 4 + 0], mn1 = ws[b * 4 + 1], mn2 = ws[b * 4 + 2], mn3 = ws[b * 4 + 3];
       const int kn = min(64, T - b * 64);
@@ -263,12 +277,38 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
             }
             zc_z = (uint32_t)__ballot(zc);
             sf_z = (uint32_t)__ballot(sf);
+            chunk_masks();
           }
         }
-        if (!(__builtin_fabs(d0) < DINF && __builtin_fabs(d1) < DINF &&
-                               __builtin_fabs(d2) < DINF && __builtin_fabs(d3) < DINF)) {
+        if ((nonfin >> k) & 1ull) {
           stop = true;                         // (a non-finite demand: the 4-wave path decides)
           break;
+        }
+        // Fast path, in lane masks (SALU), on the register chunk: C = fitting hosts of safe
+        // zero-cost zones; its first, w, wins -- exactly the test below -- unless (a) a fitting
+        // host before w is in an unsafe zone (risky), (b) one of a safe zone has every residual
+        // below 2^-300 (an exact fit, which would win, or a risky one), or (c) w has a residual
+        // above 2^500 (its score need not be 0). Any of those, or no C: the full test.
+        int win = -1;                           // host index, -1 none, -2 stop
+        bool done = false;
+        {
+          const uint64_t F = m_v & __ballot(ra0 >= d0) & __ballot(ra1 >= d1) &
+                             __ballot(ra2 >= d2) & __ballot(ra3 >= d3);
+          const uint64_t C = F & m_zs;
+          if (C) {
+            const int w = __builtin_ctzll(C);
+            const uint64_t Lx = F & ~m_zs & ((1ull << w) - 1ull);
+            const double x0 = ra0 - d0, x1 = ra1 - d1, x2 = ra2 - d2, x3 = ra3 - d3;
+            const uint64_t tight = __ballot(x0 < 0x1p-300) & __ballot(x1 < 0x1p-300) &
+                                   __ballot(x2 < 0x1p-300) & __ballot(x3 < 0x1p-300);
+            const uint64_t huge = __ballot(x0 > 0x1p+500) | __ballot(x1 > 0x1p+500) |
+                                  __ballot(x2 > 0x1p+500) | __ballot(x3 > 0x1p+500);
+            if (!(Lx & (~m_sf | tight)) && !((huge >> w) & 1ull)) {
+              if (lane == w) { ra0 = x0; ra1 = x1; ra2 = x2; ra3 = x3; }   // resc[h] -= d
+              win = p0 * 64 + w;
+              done = true;
+            }
+          }
         }
         // one chunk's candidates: zm = fitting hosts of the zero class, rk = risky fitting hosts
         auto test = [&](double x0, double x1, double x2, double x3, int32_t z, bool v,
@@ -281,8 +321,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
           zm = __ballot(f && zz);
           rk = __ballot(risky);
         };
-        int win = -1;                           // host index, -1 none, -2 stop
-        {
+        if (!done) {
           uint64_t zm, rk;
           test(ra0, ra1, ra2, ra3, rz, rv, zm, rk);
           while (zm == 0 && rk == 0 && p0 + 1 < nch &&
@@ -331,6 +370,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
             // no score-0 host fits: a positive-score winner only the 4-wave path finds
             if (win == -1) win = -2;
           }
+          chunk_masks();                        // (the register chunk may have moved on)
         }
         win = __builtin_amdgcn_readfirstlane(win);
         if (win == -2) { stop = true; break; }
@@ -430,7 +470,10 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
 #ifdef PVT_STAMPS
     const uint64_t tw0 = rstamp();
 #endif
-    p_start = resident_walk<NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, A.stamps);
+    // the walking wave: 0, or (A.walk == 2, A/B) one that moves with the workgroup index, so
+    // two workgroups sharing a CU need not walk on the same SIMD
+    const int walker = A.walk == 2 ? (int)(blockIdx.x % (unsigned)WAVES) : 0;
+    p_start = resident_walk<NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, walker, A.stamps);
 #ifdef PVT_STAMPS
     if (blockIdx.x == 0 && tid == 0 && A.stamps) {   // walked tasks, walk cycles (block 0)
       A.stamps[8] += (uint64_t)p_start;
@@ -961,6 +1004,129 @@ void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a,
   }
 }
 
+// ---- fused host batch (pvt_place_host_batch): ONE launch per call ----------------------------
+// The staged path took six dependent launches per call (stage upload, anchor wave and block
+// kernels, grouping, resident placement, result download: ~5 us of launch gap each on MI355X,
+// the grouping alone ~20 us as a 1024-thread launch). Here one workgroup of four waves per round
+// copies its round's byte ranges of the pinned stage (mapped host memory) to the device copy,
+// resolves its anchors (a wave per item, deferred long lists by the block) and its groups and
+// draws (cost_aware rounds with items), places the round (resident_round), and copies its
+// output range back to the mapped stage; the host synchronises once.
+// Two byte ranges [a, a + na) and [b, b + nb) copied src -> dst by the block (whole 16-byte
+// units: the stage layout aligns every range to 256 bytes), FL loads in flight per thread before
+// the first store: the source is host memory across PCIe (~2 us a round trip), so a load-store
+// loop would pay one round trip per iteration.
+template <int FL>
+__device__ __forceinline__ void block_copy2(char* dst, const char* src, int64_t a, int64_t na,
+                                            int64_t b, int64_t nb) {
+  const int64_t n1 = na >> 4, n = n1 + (nb >> 4);
+  const int nt = blockDim.x;
+  for (int64_t i0 = 0; i0 < n; i0 += (int64_t)FL * nt) {
+    int4 v[FL];
+#pragma unroll
+    for (int k = 0; k < FL; k++) {
+      const int64_t i = i0 + (int64_t)k * nt + threadIdx.x;
+      if (i < n) v[k] = *reinterpret_cast<const int4*>(src + (i < n1 ? a + 16 * i : b + 16 * (i - n1)));
+    }
+#pragma unroll
+    for (int k = 0; k < FL; k++) {
+      const int64_t i = i0 + (int64_t)k * nt + threadIdx.x;
+      if (i < n) *reinterpret_cast<int4*>(dst + (i < n1 ? a + 16 * i : b + 16 * (i - n1))) = v[k];
+    }
+  }
+}
+
+template <int MODE, int HPL>
+__device__ __forceinline__ void fused_place(const FusedArgs& F, const pvt_round& R) {
+  if (MODE == RES_MIXED) {
+    switch (R.mode) {
+      case CA_FF: resident_round<CA_FF, 4, HPL>(F.ra, R); break;
+      case CA_BF: resident_round<CA_BF, 4, HPL>(F.ra, R); break;
+      case OPP: resident_round<OPP, 4, HPL>(F.ra, R); break;
+      case VBP_FF: resident_round<VBP_FF, 4, HPL>(F.ra, R); break;
+      case VBP_BF: resident_round<VBP_BF, 4, HPL>(F.ra, R); break;
+      default: break;
+    }
+  } else {
+    resident_round<MODE, 4, HPL>(F.ra, R);
+  }
+}
+
+template <int MODE, int HPL>
+__global__ __launch_bounds__(4 * WAVE) void resident_fused_kernel(FusedArgs F) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const FusedRound fr = reinterpret_cast<const FusedRound*>(F.hmap + F.o_rounds)[blockIdx.x];
+  constexpr bool ITEMS = MODE == RES_MIXED || MODE == CA_FF || MODE == CA_BF;
+  // (the grouping's arguments are read from the mapped stage beside the copy: one round trip)
+  AnchorArgs a{};
+  CaGroupArgs g{};
+  if (ITEMS && fr.items >= 0) {
+    a = reinterpret_cast<const AnchorArgs*>(F.hmap + F.o_ka)[fr.items];
+    g = reinterpret_cast<const CaGroupArgs*>(F.hmap + F.o_kg)[fr.items];
+  }
+  if (threadIdx.x < (int)(sizeof(pvt_round) / 8))
+    reinterpret_cast<uint64_t*>(F.dev + fr.desc)[threadIdx.x] =
+        reinterpret_cast<const uint64_t*>(F.hmap + fr.desc)[threadIdx.x];
+  block_copy2<16>(F.dev, F.hmap, fr.out_lo, fr.out_hi - fr.out_lo, fr.in_lo, fr.in_hi - fr.in_lo);
+  __syncthreads();
+  if (ITEMS && fr.items >= 0) {
+    const int wave = threadIdx.x >> 6;
+    uint64_t* lds = reinterpret_cast<uint64_t*>(smem);
+    for (int c = wave; c < a.C; c += 4) anchor_wave_item(a, c, lds + wave * ANC_WLDS);
+    __syncthreads();
+    const int nd = *a.n_deferred;
+    for (int q = 0; q < nd; q++) {
+      block_item(a, a.deferred[q], lds, lds + ANC_LDS);
+      __syncthreads();
+    }
+    ca_groups_round<4 * WAVE, RES_MAX_TASKS>(g, *reinterpret_cast<GroupLds*>(smem));
+    __syncthreads();
+  }
+  const pvt_round R = *reinterpret_cast<const pvt_round*>(F.dev + fr.desc);   // (n_groups set)
+  fused_place<MODE, HPL>(F, R);
+  __syncthreads();
+  block_copy2<16>(const_cast<char*>(F.hmap), F.dev, fr.out_lo, fr.out_hi - fr.out_lo, 0, 0);
+}
+
+size_t fused_pre_lds_bytes() {
+  size_t b = 4 * ANC_WLDS * sizeof(uint64_t);
+  b = std::max(b, (ANC_LDS + ANC_THREADS / 64) * sizeof(uint64_t));
+  return std::max(b, sizeof(GroupLds));
+}
+
+void launch_fused(int mode, int hpl, int n, size_t lds, const FusedArgs& F, hipStream_t st) {
+  const dim3 grid(n), block(4 * WAVE);
+#define PVT_FUSED_HPL(M)                                                                         \
+  switch (hpl) {                                                                                 \
+    case 1: hipLaunchKernelGGL((resident_fused_kernel<M, 1>), grid, block, lds, st, F); break;   \
+    case 2: hipLaunchKernelGGL((resident_fused_kernel<M, 2>), grid, block, lds, st, F); break;   \
+    case 4: hipLaunchKernelGGL((resident_fused_kernel<M, 4>), grid, block, lds, st, F); break;   \
+    case 8: hipLaunchKernelGGL((resident_fused_kernel<M, 8>), grid, block, lds, st, F); break;   \
+    default: hipLaunchKernelGGL((resident_fused_kernel<M, 16>), grid, block, lds, st, F); break; \
+  }
+  switch (mode) {
+    case CA_FF: PVT_FUSED_HPL(CA_FF) break;
+    case CA_BF: PVT_FUSED_HPL(CA_BF) break;
+    case OPP: PVT_FUSED_HPL(OPP) break;
+    case VBP_FF: PVT_FUSED_HPL(VBP_FF) break;
+    case VBP_BF: PVT_FUSED_HPL(VBP_BF) break;
+    default: PVT_FUSED_HPL(RES_MIXED) break;
+  }
+#undef PVT_FUSED_HPL
+}
+
+template <int MODE>
+static hipError_t attrs_fused(int lds) {
+  hipError_t e = hipSuccess, r;
+#define PVT_FUSED_ATTR(HPL)                                                                      \
+  r = hipFuncSetAttribute((const void*)resident_fused_kernel<MODE, HPL>,                         \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, lds);                      \
+  if (r != hipSuccess) e = r;
+  PVT_FUSED_ATTR(1) PVT_FUSED_ATTR(2) PVT_FUSED_ATTR(4) PVT_FUSED_ATTR(8) PVT_FUSED_ATTR(16)
+#undef PVT_FUSED_ATTR
+  return e;
+}
+
 template <int MODE>
 static hipError_t attrs_mode(int lds) {
   hipError_t e = hipSuccess, r;
@@ -989,6 +1155,13 @@ hipError_t resident_init_attrs() {
   if (r != hipSuccess) e = r;
   PVT_MIX_ATTR(1) PVT_MIX_ATTR(2) PVT_MIX_ATTR(4) PVT_MIX_ATTR(8) PVT_MIX_ATTR(16)
 #undef PVT_MIX_ATTR
+  const int flds = (int)std::max((size_t)lds, fused_pre_lds_bytes());
+  if ((r = attrs_fused<CA_FF>(flds)) != hipSuccess) e = r;
+  if ((r = attrs_fused<CA_BF>(flds)) != hipSuccess) e = r;
+  if ((r = attrs_fused<OPP>(flds)) != hipSuccess) e = r;
+  if ((r = attrs_fused<VBP_FF>(flds)) != hipSuccess) e = r;
+  if ((r = attrs_fused<VBP_BF>(flds)) != hipSuccess) e = r;
+  if ((r = attrs_fused<RES_MIXED>(flds)) != hipSuccess) e = r;
   return e;
 }
 

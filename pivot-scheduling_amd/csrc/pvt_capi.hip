@@ -195,6 +195,7 @@ struct pvt_ctx {
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
   int rwalk = 1;                  // PVT_RWALK=0: resident rounds without the one-wave walk (A/B)
+  int fused = 1;                  // PVT_FUSED=0: host batches staged in six launches (A/B)
   int ahead = 0;                  // PVT_AHEAD=1: vbp best-fit walks enqueued ahead (place_ahead;
                                   // measured slower, kept for A/B)
   Buf wslot;                      // enqueued-ahead walks' status slots (place_ahead)
@@ -390,7 +391,8 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_BAND")) ctx->band_min = std::max(0, atoi(e));       // A/B
   if (const char* e = getenv("PVT_LWALK")) ctx->lwalk = atoi(e) != 0;                  // A/B
   if (const char* e = getenv("PVT_AHEAD")) ctx->ahead = atoi(e) != 0;                  // A/B
-  if (const char* e = getenv("PVT_RWALK")) ctx->rwalk = atoi(e) != 0;                  // A/B
+  if (const char* e = getenv("PVT_RWALK")) ctx->rwalk = atoi(e);                       // A/B
+  if (const char* e = getenv("PVT_FUSED")) ctx->fused = atoi(e) != 0;                  // A/B
   if (const char* e = getenv("PVT_SEGMENTS")) ctx->t_segments = std::max(1, atoi(e));  // tuning
   if (const char* e = getenv("PVT_BAND_SEGS")) ctx->t_band_segs = atoi(e);             // tuning
   if (const char* e = getenv("PVT_KEYED_SCAN")) ctx->t_keyed_scan = atoi(e) != 0;      // A/B
@@ -2120,7 +2122,7 @@ static int place_resident(pvt_ctx* ctx, const pvt_round* rounds, int n,
   resident_shape(maxH, &waves, &hpl);
   int tpad = 64;
   while (tpad < maxT) tpad <<= 1;
-  const int rwalk = ctx->rwalk && maxH <= RW_MAXH ? 1 : 0;
+  const int rwalk = ctx->rwalk && maxH <= RW_MAXH ? ctx->rwalk : 0;
   double cand = 0.0, bytes = 0.0;
   for (int i = 0; i < n; i++) {
     const double c = (double)rounds[i].n_tasks * rounds[i].n_hosts;
@@ -2340,6 +2342,7 @@ struct HostSlot {
   size_t av = 0, pl = 0, orr = 0, mt = 0, cmt = 0, st = 0;
   size_t zone = 0, tb = 0, dc = 0, cost = 0, bw = 0, dem = 0, tg = 0, ga = 0, rt = 0;
   size_t ti = 0, off = 0, ph = 0, ia = 0, sz = 0, zs = 0, mh = 0, az = 0, ab = 0, desc = 0;
+  size_t out_lo = 0, out_hi = 0, in_lo = 0, in_hi = 0;   // its byte ranges (fused host batch)
   int C = 0, S = 0, G = 0, GR = 0;
   int64_t NP = 0;
   bool resident = false, dev_mt = false;
@@ -2408,16 +2411,19 @@ struct StageLayout {
 
 static void plan_out(StageLayout& L, HostSlot& s, const pvt_round* r, const pvt_ca_items* it) {
   const int H = r->n_hosts, T = r->n_tasks;
+  s.out_lo = L.o;
   s.av = L.take(32 * (size_t)H);
   s.pl = L.take(4 * (size_t)T);
   s.orr = L.take(4 * (size_t)T);
   s.mt = r->mt_state ? L.take(4 * 625) : 0;
   s.cmt = it ? L.take(4 * 625) : 0;
   s.st = it ? L.take(16) : 0;
+  s.out_hi = L.o;
 }
 
 static void plan_in(StageLayout& L, HostSlot& s, const pvt_round* r, const pvt_ca_items* it) {
   const int H = r->n_hosts, T = r->n_tasks, Z = r->n_zones;
+  s.in_lo = L.o;
   s.zone = L.take(4 * (size_t)H);
   s.tb = r->tiebreak ? L.take(4 * (size_t)H) : 0;
   s.dc = r->decay ? L.take(4 * (size_t)H) : 0;
@@ -2438,6 +2444,7 @@ static void plan_in(StageLayout& L, HostSlot& s, const pvt_round* r, const pvt_c
     s.az = L.take(4 * (size_t)std::max(s.C, 1));
     s.ab = L.take(16 + 4 * (size_t)std::max(s.C, 1));
   }
+  s.in_hi = L.o;
 }
 
 // The round's inputs into the pinned buffer and its device descriptor (arrays in the device
@@ -2596,6 +2603,59 @@ extern "C" int pvt_restore_hosts(pvt_ctx* ctx, double* avail, const double* avai
   return PVT_OK;
 }
 
+// The staged host batch in ONE launch (resident_fused_kernel, pvt_batch.hip): every round's
+// workgroup copies its ranges of the mapped stage to the device copy, runs its grouping (items)
+// and its placement, and copies its results back; one synchronisation. PVT_FUSED=0: the staged
+// upload / anchor / grouping / placement / download launches instead (A/B).
+static int place_host_fused(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_items* const* items,
+                            int32_t n_rounds, int32_t* rcs, std::vector<HostSlot>& s,
+                            const std::vector<int>& live, const std::vector<int>& withit,
+                            size_t o_fr, size_t o_ka, size_t o_kg, bool mixed, int mode0, int maxH,
+                            int maxT, int maxZ) {
+  hipStream_t st = ctx->stream;
+  char* hb = static_cast<char*>(ctx->hst);
+  char* db = static_cast<char*>(ctx->hdev.p);
+  FusedRound* fr = reinterpret_cast<FusedRound*>(hb + o_fr);
+  for (size_t k = 0; k < live.size(); k++) {
+    const HostSlot& h = s[live[k]];
+    fr[k] = FusedRound{(int64_t)h.out_lo, (int64_t)h.out_hi, (int64_t)h.in_lo, (int64_t)h.in_hi,
+                       (int64_t)h.desc, -1, 0};
+  }
+  for (size_t k = 0; k < withit.size(); k++)
+    for (size_t j = 0; j < live.size(); j++)
+      if (live[j] == withit[k]) fr[j].items = (int32_t)k;
+  int waves = 4, hpl = 1;
+  resident_shape(maxH, &waves, &hpl);
+  int tpad = 64;
+  while (tpad < maxT) tpad <<= 1;
+  double cand = 0.0, bytes = 0.0;
+  for (int i : live) {
+    const double c = (double)rounds[i].n_tasks * rounds[i].n_hosts;
+    cand += c;
+    bytes += c * bytes_per_candidate(rounds[i].mode);
+  }
+  const int rwalk = ctx->rwalk && maxH <= RW_MAXH ? ctx->rwalk : 0;
+  FusedArgs F{static_cast<const char*>(ctx->hst_map), db, (int64_t)o_fr, (int64_t)o_ka,
+              (int64_t)o_kg, ResidentArgs{nullptr, nullptr, maxZ, tpad, ctx->stamps, rwalk}};
+  size_t lds = resident_lds_bytes(maxZ, tpad, rwalk != 0);
+  if (!withit.empty()) lds = std::max(lds, fused_pre_lds_bytes());
+  {
+    Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_fused_kernel");
+    launch_fused(mixed ? RES_MIXED : mode0, hpl, (int)live.size(), lds, F, st);
+  }
+  HIPCHK(hipGetLastError());
+  ctx->windows = (int64_t)live.size();
+  ctx->refills = 0;
+  HIPCHK(hipStreamSynchronize(st));
+  for (int i : live) {
+    pvt_ca_items* it = items ? items[i] : nullptr;
+    if (it && (rcs[i] = group_error(ctx, hb, s[i], it))) continue;
+    return_round(hb, s[i], &rounds[i], it);
+  }
+  (void)n_rounds;
+  return PVT_OK;
+}
+
 extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_items* const* items,
                                     int32_t n_rounds, int32_t* rcs) {
   if (!ctx) return PVT_EINVAL;
@@ -2653,6 +2713,8 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
   const size_t o_kg = ni ? L.take(sizeof(CaGroupArgs) * ni) : 0;
   const size_t o_desc = L.take(sizeof(pvt_round) * live.size());
   for (size_t k = 0; k < live.size(); k++) s[live[k]].desc = o_desc + sizeof(pvt_round) * k;
+  const bool fused = ctx->fused != 0;
+  const size_t o_fr = fused ? L.take(sizeof(FusedRound) * live.size()) : 0;
   if ((rc = ensure_pinned(ctx, L.o))) return rc;
   ENSURE(ctx->hdev, L.o);
   char* hb = static_cast<char*>(ctx->hst);
@@ -2670,6 +2732,8 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
     nab += anchor_batch_blocks(s[i].C);
   }
   if (ni) reinterpret_cast<int32_t*>(hb + o_kb)[ni] = nab;
+  if (fused) return place_host_fused(ctx, rounds, items, n_rounds, rcs, s, live, withit, o_fr,
+                                     o_ka, o_kg, mixed, mode0, maxH, maxT, maxZ);
   stage_up(ctx, L.o, st);
   HIPCHK(hipGetLastError());
   if (ni) {
@@ -2695,7 +2759,7 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
       bytes += c * bytes_per_candidate(rounds[i].mode);
     }
     ResidentArgs ra{db + o_desc, nullptr, maxZ, tpad, ctx->stamps,
-                    ctx->rwalk && maxH <= RW_MAXH ? 1 : 0};
+                    ctx->rwalk && maxH <= RW_MAXH ? ctx->rwalk : 0};
     Scope sc(ctx, PVT_K_SCORE, cand, bytes, nullptr, "resident_kernel");
     launch_resident(mixed ? RES_MIXED : mode0, waves, hpl, (int)live.size(), ra, st);
   }

@@ -431,6 +431,24 @@ size_t resident_lds_bytes(int Zb, int Tpad, bool walk);
 void resident_shape(int maxH, int* waves, int* hpl);
 void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a, hipStream_t st);
 hipError_t resident_init_attrs();
+
+// The fused host batch (pvt_place_host_batch): per round (one workgroup of four waves), its byte
+// ranges of the pinned stage -- the same offsets in the mapped host copy and the device copy --
+// and its index in the stage's AnchorArgs / CaGroupArgs arrays (-1: no fused grouping).
+struct FusedRound {
+  int64_t out_lo, out_hi, in_lo, in_hi;
+  int64_t desc;           // byte offset of its pvt_round (device array pointers)
+  int32_t items, pad;
+};
+struct FusedArgs {
+  const char* hmap;       // the mapped pinned stage (the device reads its inputs, writes results)
+  char* dev;              // the device copy of the stage
+  int64_t o_rounds;       // FusedRound[n] (read from hmap)
+  int64_t o_ka, o_kg;     // AnchorArgs[ni], CaGroupArgs[ni] (read from hmap)
+  ResidentArgs ra;        // Zb, Tpad, walk, stamps (rounds unused: each workgroup has its own)
+};
+size_t fused_pre_lds_bytes();   // LDS of the anchor and grouping phases
+void launch_fused(int mode, int hpl, int n, size_t lds, const FusedArgs& F, hipStream_t st);
 size_t commit_lds_bytes();
 hipError_t init_kernel_attrs();
 // grouped processing order: group counts (cnt[G] = out-of-range ids), scatter by group, one

@@ -89,6 +89,11 @@ def main():
     k = eng.kstats(_abi.PVT_K_COMMIT)
     print("commit launches=%d avg %.3f ms" % (k["launches"], k["ms"] / max(k["launches"], 1)),
           flush=True)
+    for name in ("resident_kernel", "zwalk_kernel", "lwalk_kernel", "opp_commit_kernel"):
+        k = eng.kernel_kstats(name)
+        if k["launches"]:
+            print("%s launches=%d avg %.4f ms" % (name, k["launches"], k["ms"] / k["launches"]),
+                  flush=True)
 
 
 if __name__ == "__main__":
