@@ -76,7 +76,7 @@ __device__ __forceinline__ uint64_t rstamp() {
 constexpr int RW_SB = RES_MAX_TASKS / 64; // its suffix minima of the demands, per 64 positions
 
 struct ResLds {
-  int zt, ord, pl, u, cd, ci, mt, slot, wa, wz, ws, total;
+  int zt, ord, pl, u, cd, ci, mt, slot, wa, wz, ws, wx, wd, total;
   __host__ __device__ ResLds(int Zb, int Tpad, bool walk = false) {
     zt = 0;                                            // csum[Zb*Zb], bsum[Zb*Zb] f64
     ord = (16 * Zb * Zb + 15) & ~15;                   // processing order i32[Tpad]
@@ -91,11 +91,14 @@ struct ResLds {
     const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW + 32;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     // resident walk (after the sort, before the staging above): the round's hosts in LDS,
-    // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], suffix minima of the demands f64[RW_SB][4]
+    // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], suffix minima and maxima of the demands
+    // f64[RW_SB][4] each, the zero-cost window of the current anchor (host ids) i32[RW_MAXH]
     wa = u;
     wz = wa + 32 * RW_MAXH;
     ws = wz + 4 * RW_MAXH;
-    const int rw_end = walk ? ws + 32 * RW_SB : 0;
+    wx = ws + 32 * RW_SB;
+    wd = wx + 32 * RW_SB;
+    const int rw_end = walk ? wd + 4 * RW_MAXH : 0;
     total = walk_end > sort_end ? walk_end : sort_end;
     total = rw_end > total ? rw_end : total;
   }
@@ -176,6 +179,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   double* wa = reinterpret_cast<double*>(smem + Lo.wa);      // [4][RW_MAXH]
   int32_t* wz = reinterpret_cast<int32_t*>(smem + Lo.wz);
   double* ws = reinterpret_cast<double*>(smem + Lo.ws);      // [RW_SB][4]
+  double* wx = reinterpret_cast<double*>(smem + Lo.wx);      // [RW_SB][4]
+  int32_t* wd = reinterpret_cast<int32_t*>(smem + Lo.wd);    // [RW_MAXH]
   for (int h = tid; h < H; h += NT) {
 #pragma unroll
     for (int r = 0; r < 4; r++) wa[r * RW_MAXH + h] = G(R.avail)[(size_t)r * H + h];
@@ -183,22 +188,28 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   }
   const int nsb = (T + 63) >> 6;
   for (int blk = wave; blk < nsb; blk += NT / WAVE) {
-    double m[4] = {DINF, DINF, DINF, DINF};
+    double m[4] = {DINF, DINF, DINF, DINF}, x[4] = {-DINF, -DINF, -DINF, -DINF};
     const int i = blk * 64 + lane;
     if (i < T) {
       const int t = ord[i];
 #pragma unroll
-      for (int r = 0; r < 4; r++) m[r] = G(R.dem)[(size_t)r * T + t];
+      for (int r = 0; r < 4; r++) m[r] = x[r] = G(R.dem)[(size_t)r * T + t];
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      for (int off = 32; off > 0; off >>= 1) m[r] = fmin(m[r], __shfl_xor(m[r], off));
-      if (lane == 0) ws[blk * 4 + r] = m[r];
+      for (int off = 32; off > 0; off >>= 1) {
+        m[r] = fmin(m[r], __shfl_xor(m[r], off));
+        x[r] = fmax(x[r], __shfl_xor(x[r], off));
+      }
+      if (lane == 0) { ws[blk * 4 + r] = m[r]; wx[blk * 4 + r] = x[r]; }
     }
   }
   __syncthreads();
   if (tid < 4)
     for (int blk = nsb - 2; blk >= 0; blk--) ws[blk * 4 + tid] = fmin(ws[blk * 4 + tid], ws[(blk + 1) * 4 + tid]);
+  else if (tid >= 64 && tid < 68)
+    for (int blk = nsb - 2; blk >= 0; blk--)
+      wx[blk * 4 + tid - 64] = fmax(wx[blk * 4 + tid - 64], wx[(blk + 1) * 4 + tid - 64]);
   __syncthreads();
   if (wave == walker) {
 #ifdef PVT_STAMPS
@@ -235,6 +246,70 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       m_sf = __ballot(sf);
       m_zs = __ballot(sf && zc);
     };
+    // Zero-cost window of the current anchor (the resident form of the frontier walk's window,
+    // pvt_zwalk.hip): the anchor's zero-cost hosts in index order (wd, nd of them), walked 64 at
+    // a time in registers (dense chunk dp0: host wd[dp0 * 64 + lane], capacities gathered from
+    // and written back to wa), so every chunk holds only hosts that can score 0. Exact when
+    //   (i) every zone is safe for the anchor (sf_z full): a fitting zero-cost host scores
+    //       exactly 0 unless a residual exceeds 2^500 (checked on the winner: stop), and
+    //  (ii) some dimension r separates every other host from every remaining demand by 2^-288:
+    //       min over them of a_r - max over the tasks of d_r >= 2^-288, so none fits exactly
+    //       (score 0) or with every residual below 2^-300 (risky); their capacities do not
+    //       change while the anchor lasts (the walk commits only zero-cost hosts).
+    // Then the winner is the first fitting host of the window, as in the full test.
+    bool dense = false;
+    int nwin = 0, dp0 = 0;
+    int32_t rid = 0;
+    auto load_dense = [&](int c) {
+      const int i = c * 64 + lane;
+      rv = i < nwin;
+      rid = rv ? wd[i] : 0;
+      ra0 = wa[rid]; ra1 = wa[RW_MAXH + rid]; ra2 = wa[2 * RW_MAXH + rid]; ra3 = wa[3 * RW_MAXH + rid];
+    };
+    auto store_dense = [&]() {
+      if (rv) { wa[rid] = ra0; wa[RW_MAXH + rid] = ra1; wa[2 * RW_MAXH + rid] = ra2; wa[3 * RW_MAXH + rid] = ra3; }
+    };
+    auto leave_dense = [&]() {
+      if (!dense) return;
+      store_dense();
+      dense = false;
+      load_chunk(p0);
+    };
+    auto enter_dense = [&](int b) {
+      const uint32_t allz = Z >= 32 ? 0xffffffffu : ((1u << Z) - 1u);
+      if (__builtin_amdgcn_readfirstlane((int)(zc_z == 0 || (sf_z & allz) != allz))) return;
+      // (ii): the other hosts' least capacities against the remaining tasks' largest demands
+      double q0 = DINF, q1 = DINF, q2 = DINF, q3 = DINF;
+      for (int c = 0; c < nch; c++) {
+        const int q = c * 64 + lane;
+        if (q < H && !((zc_z >> wz[q]) & 1u)) {
+          q0 = fmin(q0, wa[q]); q1 = fmin(q1, wa[RW_MAXH + q]);
+          q2 = fmin(q2, wa[2 * RW_MAXH + q]); q3 = fmin(q3, wa[3 * RW_MAXH + q]);
+        }
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        q0 = fmin(q0, __shfl_xor(q0, off)); q1 = fmin(q1, __shfl_xor(q1, off));
+        q2 = fmin(q2, __shfl_xor(q2, off)); q3 = fmin(q3, __shfl_xor(q3, off));
+      }
+      const bool sep = (q0 - wx[b * 4 + 0] >= 0x1p-288) || (q1 - wx[b * 4 + 1] >= 0x1p-288) ||
+                       (q2 - wx[b * 4 + 2] >= 0x1p-288) || (q3 - wx[b * 4 + 3] >= 0x1p-288);
+      if (__builtin_amdgcn_readfirstlane((int)!sep)) return;
+      store_chunk(p0);
+      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      int n = 0;
+      for (int c = 0; c < nch; c++) {
+        const int q = c * 64 + lane;
+        const bool in = q < H && ((zc_z >> wz[q]) & 1u);
+        const uint64_t m = __ballot(in);
+        if (in) wd[n + __popcll(m & below)] = q;
+        n += __popcll(m);
+      }
+      wave_sync();                             // (the window ids before this wave reads them)
+      nwin = n;
+      dense = true;
+      dp0 = 0;
+      load_dense(0);
+    };
     // the task records of a 64-position batch in lanes (the next batch's loads in flight)
     auto rec = [&](int b, double (&d)[4], int& anc) {
       const int i = b * 64 + lane;
@@ -268,6 +343,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
         {
           const int a = readlane_i(tanc, k);
           if (a != cur_anc) {
+            leave_dense();
             cur_anc = a;
             bool zc = false, sf = false;
             if (lane < Z) {
@@ -277,6 +353,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
             }
             zc_z = (uint32_t)__ballot(zc);
             sf_z = (uint32_t)__ballot(sf);
+            enter_dense(b);
             chunk_masks();
           }
         }
@@ -291,7 +368,54 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
         // above 2^500 (its score need not be 0). Any of those, or no C: the full test.
         int win = -1;                           // host index, -1 none, -2 stop
         bool done = false;
-        {
+        if (dense) {
+          // the window: the first fitting zero-cost host (chunks no remaining task can use
+          // are passed for good; later ones probed from LDS)
+          uint64_t F = __ballot(rv && ra0 >= d0 && ra1 >= d1 && ra2 >= d2 && ra3 >= d3);
+          while (F == 0 && (dp0 + 1) * 64 < nwin &&
+                 !__ballot(rv && ra0 >= mn0 && ra1 >= mn1 && ra2 >= mn2 && ra3 >= mn3)) {
+            store_dense();
+            ++dp0;
+            load_dense(dp0);
+            F = __ballot(rv && ra0 >= d0 && ra1 >= d1 && ra2 >= d2 && ra3 >= d3);
+          }
+          if (F) {
+            const int w = __builtin_ctzll(F);
+            const double x0 = ra0 - d0, x1 = ra1 - d1, x2 = ra2 - d2, x3 = ra3 - d3;
+            if (__ballot(lane == w && (x0 > 0x1p+500 || x1 > 0x1p+500 || x2 > 0x1p+500 || x3 > 0x1p+500))) {
+              win = -2;                         // (a huge residual: the score need not be 0)
+            } else {
+              if (lane == w) { ra0 = x0; ra1 = x1; ra2 = x2; ra3 = x3; }   // resc[h] -= d
+              win = __builtin_amdgcn_readlane(rid, w);
+            }
+          } else {
+            for (int c = dp0 + 1; c * 64 < nwin; c++) {
+#ifdef PVT_STAMPS
+              n_probe++;
+#endif
+              const int i = c * 64 + lane;
+              const bool v = i < nwin;
+              const int32_t h = v ? wd[i] : 0;
+              const double y0 = wa[h], y1 = wa[RW_MAXH + h], y2 = wa[2 * RW_MAXH + h], y3 = wa[3 * RW_MAXH + h];
+              const uint64_t F2 = __ballot(v && y0 >= d0 && y1 >= d1 && y2 >= d2 && y3 >= d3);
+              if (F2) {
+                const int w = __builtin_ctzll(F2);
+                const double x0 = y0 - d0, x1 = y1 - d1, x2 = y2 - d2, x3 = y3 - d3;
+                if (__ballot(lane == w && (x0 > 0x1p+500 || x1 > 0x1p+500 || x2 > 0x1p+500 || x3 > 0x1p+500))) {
+                  win = -2;
+                } else {
+                  if (lane == w) { wa[h] = x0; wa[RW_MAXH + h] = x1; wa[2 * RW_MAXH + h] = x2; wa[3 * RW_MAXH + h] = x3; }
+                  win = __builtin_amdgcn_readlane(h, w);
+                }
+                break;
+              }
+            }
+            // no zero-cost host fits: a positive-score winner only the 4-wave path finds
+            if (win == -1) win = -2;
+          }
+          done = true;
+        }
+        if (!done) {
           const uint64_t F = m_v & __ballot(ra0 >= d0) & __ballot(ra1 >= d1) &
                              __ballot(ra2 >= d2) & __ballot(ra3 >= d3);
           const uint64_t C = F & m_zs;
@@ -380,6 +504,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
 #endif
       }
     }
+    leave_dense();
     store_chunk(p0);
     if (lane == 0) s_stop = p;
 #ifdef PVT_STAMPS

@@ -155,3 +155,22 @@ def test_negative_egress_cost_is_refused(engine):
             r.bw = np.zeros_like(r.bw)
             with pytest.raises(Exception, match="bw sum"):
                 engine.place(r)
+
+
+def test_zero_cost_window_certificates(engine, engine_nowalk):
+    """The walk's zero-cost window (dense chunks of the anchor's zero-cost hosts) is used only
+    under its certificates: rounds where other hosts fit some tasks exactly (score 0 outside the
+    window: certificate (ii) fails), where they have residuals below 2^-300 (risky), and where
+    the window runs dry mid-group (the 4-wave path takes over with positive scores)."""
+    rounds = []
+    for s in range(6):
+        r = synthetic.make_round(_abi.PVT_CA_BF, 900, 1200, seed=200 + s)
+        if s % 3 == 0:                          # exact fits on hosts of every zone
+            r.avail[:, ::7] = r.dem[:, (np.arange(r.n_hosts)[::7] * 13) % r.n_tasks]
+        elif s % 3 == 1:                        # residuals below 2^-300 on some hosts
+            k = (np.arange(r.n_hosts)[::11] * 7) % r.n_tasks
+            r.avail[:, ::11] = r.dem[:, k] + 1e-310
+        else:                                   # little zero-cost capacity: windows run dry
+            r.avail[0] = np.minimum(r.avail[0], 2.0)
+        rounds.append(r)
+    _check(engine, engine_nowalk, rounds, "zero-cost window certificates")
