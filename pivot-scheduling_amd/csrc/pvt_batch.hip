@@ -1192,8 +1192,17 @@ __global__ __launch_bounds__(4 * WAVE) void resident_fused_kernel(FusedArgs F) {
   if (threadIdx.x < (int)(sizeof(pvt_round) / 8))
     reinterpret_cast<uint64_t*>(F.dev + fr.desc)[threadIdx.x] =
         reinterpret_cast<const uint64_t*>(F.hmap + fr.desc)[threadIdx.x];
+#ifdef PVT_STAMPS
+  // phases of block 0 (stamps[16..20]): stage in, anchors, grouping, placement, results out
+  const bool fst = blockIdx.x == 0 && threadIdx.x == 0 && F.ra.stamps;
+  uint64_t ft = fst ? rstamp() : 0;
+#define FSTAMP(k) do { if (fst) { const uint64_t t_ = rstamp(); F.ra.stamps[16 + (k)] += t_ - ft; ft = t_; } } while (0)
+#else
+#define FSTAMP(k) do {} while (0)
+#endif
   block_copy2<16>(F.dev, F.hmap, fr.out_lo, fr.out_hi - fr.out_lo, fr.in_lo, fr.in_hi - fr.in_lo);
   __syncthreads();
+  FSTAMP(0);
   if (ITEMS && fr.items >= 0) {
     const int wave = threadIdx.x >> 6;
     uint64_t* lds = reinterpret_cast<uint64_t*>(smem);
@@ -1204,13 +1213,19 @@ __global__ __launch_bounds__(4 * WAVE) void resident_fused_kernel(FusedArgs F) {
       block_item(a, a.deferred[q], lds, lds + ANC_LDS);
       __syncthreads();
     }
+    FSTAMP(1);
     ca_groups_round<4 * WAVE, RES_MAX_TASKS>(g, *reinterpret_cast<GroupLds*>(smem));
     __syncthreads();
+    FSTAMP(2);
   }
   const pvt_round R = *reinterpret_cast<const pvt_round*>(F.dev + fr.desc);   // (n_groups set)
   fused_place<MODE, HPL>(F, R);
   __syncthreads();
+  FSTAMP(3);
   block_copy2<16>(const_cast<char*>(F.hmap), F.dev, fr.out_lo, fr.out_hi - fr.out_lo, 0, 0);
+  __syncthreads();
+  FSTAMP(4);
+#undef FSTAMP
 }
 
 size_t fused_pre_lds_bytes() {
