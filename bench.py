@@ -154,6 +154,13 @@ def _paired_oracle(r, budget_s, threads):
     return v_all, v_one, n, dt_all / reps, dt_one, (res if n >= r.n_tasks else None)
 
 
+def best_cpu(v_all, threads, v_one):
+    """(value, cores) of a CPU baseline: the faster of the all-cores and the one-thread run of
+    the same sample. The restatement's OpenMP host scans have no early exit, so on first-fit
+    rounds (whose tasks stop at the first hosts) one thread beats all of them."""
+    return (v_one, 1) if v_one > v_all else (v_all, threads)
+
+
 def cpu_baseline(r, budget_s):
     """The CPU restatement (oracle/) timed on this host beside the GPU: all the cores this job
     may use (OMP_NUM_THREADS, else min(16, os.cpu_count()); OpenMP host scans) as the reported
@@ -161,11 +168,12 @@ def cpu_baseline(r, budget_s):
     dict, full-round oracle result or None)."""
     threads = oracle_threads()
     v_all, v_one, n, dt_all, dt_one, res = _paired_oracle(r, budget_s, threads)
-    out = {"value": v_all, "unit": "candidates/s", "cores": threads, "kind": "port",
-           "value_1thread": v_one, "tasks": n,
+    value, cores = best_cpu(v_all, threads, v_one)
+    out = {"value": value, "unit": "candidates/s", "cores": cores, "kind": "port",
+           "value_1thread": v_one, "value_all_cores": v_all, "tasks": n,
            "sample": "oracle/pivot_oracle.c (naive T x H scan, not the engine's algorithm; "
                      "OpenMP host scans): the first %d tasks x %d hosts of the same round on "
-                     "%d threads (%.2f s) and on 1 thread (%.1f s)"
+                     "%d threads (%.2f s) and on 1 thread (%.1f s); value = the faster"
                      % (n, r.n_hosts, threads, dt_all, dt_one)}
     return out, res
 
@@ -317,10 +325,11 @@ def round_cpu_baseline(r, threads, budget_s):
     thread, both on the same first tasks of the round (the whole round when one thread takes it
     within the budget -- that run is then the parity reference)."""
     v_all, v_one, n, dt_all, dt_one, res = _paired_oracle(r, budget_s, threads)
-    out = {"value": v_all, "unit": "candidates/s", "cores": threads, "kind": "port",
-           "value_1thread": v_one, "tasks": n,
+    value, cores = best_cpu(v_all, threads, v_one)
+    out = {"value": value, "unit": "candidates/s", "cores": cores, "kind": "port",
+           "value_1thread": v_one, "value_all_cores": v_all, "tasks": n,
            "sample": "oracle/pivot_oracle.c (naive T x H scan, OpenMP host scans) on %s x %d "
-                     "hosts: %d threads %.3f s, 1 thread %.2f s"
+                     "hosts: %d threads %.3f s, 1 thread %.2f s; value = the faster"
                      % ("all %d tasks" % n if n >= r.n_tasks else "the first %d tasks" % n,
                         r.n_hosts, threads, dt_all, dt_one)}
     return out, res
@@ -343,8 +352,9 @@ def batch_cpu_baseline(rounds, threads):
         oracle.place(x, threads=0)
     dt_one = max(time.perf_counter() - t, 1e-6)
     c1 = float(sum(r.n_tasks * r.n_hosts for r in rounds[:n1]))
-    out = {"value": cand / dt_all, "unit": "candidates/s", "cores": threads, "kind": "port",
-           "value_1thread": c1 / dt_one,
+    value, cores = best_cpu(cand / dt_all, threads, c1 / dt_one)
+    out = {"value": value, "unit": "candidates/s", "cores": cores, "kind": "port",
+           "value_1thread": c1 / dt_one, "value_all_cores": cand / dt_all,
            "sample": "oracle/pivot_oracle.c on all %d scenarios, one scenario per thread over %d "
                      "threads (%.2f s); 1 thread: the first %d scenarios (%.2f s)"
                      % (len(rounds), threads, dt_all, n1, dt_one)}
@@ -878,11 +888,13 @@ def replay_workloads(eng):
             "seconds": secs, "ms_per_round": secs * 1e3 / nr, "parity": bool(ok),
             "cpu_1thread": {"seconds": c1, "value": cand / c1, "parity": bool(ok1)},
             "cpu_all": {"seconds": ca, "value": cand / ca, "cores": threads, "parity": bool(oka)},
-            "cpu_baseline": {"value": cand / ca, "unit": "candidates/s", "cores": threads,
-                             "kind": "port", "value_1thread": cand / c1,
+            "cpu_baseline": {"value": max(cand / ca, cand / c1), "unit": "candidates/s",
+                             "cores": threads if ca <= c1 else 1,
+                             "kind": "port", "value_1thread": cand / c1, "value_all_cores": cand / ca,
                              "sample": "the same %d recorded rounds through the same drop-in "
                                        "policy class with the C restatement behind the engine "
-                                       "contract (%d threads; 1 thread beside it)" % (nr, threads)},
+                                       "contract (%d threads and 1 thread; value = the faster)"
+                                       % (nr, threads)},
             "roofline": {"kernel": None, "bound": "round trip", "unit": "rounds/s",
                          "achieved": nr / secs, "peak": 1e3 / floor, "frac": floor / (secs * 1e3 / nr),
                          "traffic": None, "floor_ms_per_round": floor,
