@@ -226,6 +226,11 @@ struct pvt_ctx {
   void* hst_map = nullptr;        //   (its device address: the copy kernels' side)
   size_t hst_cap = 0;
   Buf hdev;                       //   and its device copy
+  // the zone tables of the last host-array round (cost then bw, Z x Z each) kept on the device:
+  // drop-in rounds of one cluster pass the same tables every time, so they are not staged again
+  std::vector<double> zt_host;
+  Buf zt_dev;
+  int zt_Z = 0;
 };
 
 static int fail(pvt_ctx* c, int code, const char* fmt, ...) {
@@ -417,7 +422,7 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->oppfault, &ctx->hdev, &ctx->kskey, &ctx->kperm, &ctx->kiota,
                  &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->cmax, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
-                 &ctx->btcnt, &ctx->bsorttmp, &ctx->brun, &ctx->brdem, &ctx->bpos, &ctx->bptouch};
+                 &ctx->btcnt, &ctx->bsorttmp, &ctx->brun, &ctx->brdem, &ctx->bpos, &ctx->bptouch, &ctx->zt_dev};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -2343,6 +2348,7 @@ struct HostSlot {
   size_t zone = 0, tb = 0, dc = 0, cost = 0, bw = 0, dem = 0, tg = 0, ga = 0, rt = 0;
   size_t ti = 0, off = 0, ph = 0, ia = 0, sz = 0, zs = 0, mh = 0, az = 0, ab = 0, desc = 0;
   size_t out_lo = 0, out_hi = 0, in_lo = 0, in_hi = 0;   // its byte ranges (fused host batch)
+  const double* zt = nullptr;         // device zone tables (cost, then bw) when cached, else NULL
   int C = 0, S = 0, G = 0, GR = 0;
   int64_t NP = 0;
   bool resident = false, dev_mt = false;
@@ -2404,6 +2410,32 @@ static int check_host_round(pvt_ctx* ctx, const pvt_round* r, pvt_ca_items* it, 
   return PVT_OK;
 }
 
+// The device copy of a host round's zone tables, when they equal the cached ones (s.zt); the
+// cache takes the tables of the first cost_aware round of a call that misses it (one small
+// copy on the stream; every host-array call ends with a synchronisation, so no kernel of an
+// earlier call still reads the old tables).
+static int zone_cache(pvt_ctx* ctx, const pvt_round* r, HostSlot& s) {
+  s.zt = nullptr;
+  if (!r->cost || !r->bw || r->n_tasks == 0) return PVT_OK;
+  const int Z = r->n_zones;
+  const size_t zz = (size_t)Z * Z;
+  auto same = [&]() {
+    return ctx->zt_Z == Z && ctx->zt_host.size() == 2 * zz &&
+           std::memcmp(ctx->zt_host.data(), r->cost, 8 * zz) == 0 &&
+           std::memcmp(ctx->zt_host.data() + zz, r->bw, 8 * zz) == 0;
+  };
+  if (!same()) {
+    ctx->zt_host.resize(2 * zz);
+    std::memcpy(ctx->zt_host.data(), r->cost, 8 * zz);
+    std::memcpy(ctx->zt_host.data() + zz, r->bw, 8 * zz);
+    ctx->zt_Z = Z;
+    ENSURE(ctx->zt_dev, 16 * zz);
+    HIPCHK(hipMemcpyAsync(ctx->zt_dev.p, ctx->zt_host.data(), 16 * zz, hipMemcpyHostToDevice, ctx->stream));
+  }
+  s.zt = P<double>(ctx->zt_dev);
+  return PVT_OK;
+}
+
 struct StageLayout {
   size_t o = 0;
   size_t take(size_t bytes) { const size_t at = o; o = (o + bytes + 255) / 256 * 256; return at; }
@@ -2427,8 +2459,8 @@ static void plan_in(StageLayout& L, HostSlot& s, const pvt_round* r, const pvt_c
   s.zone = L.take(4 * (size_t)H);
   s.tb = r->tiebreak ? L.take(4 * (size_t)H) : 0;
   s.dc = r->decay ? L.take(4 * (size_t)H) : 0;
-  s.cost = L.take(8 * (size_t)Z * Z);
-  s.bw = L.take(8 * (size_t)Z * Z);
+  s.cost = s.zt ? 0 : L.take(8 * (size_t)Z * Z);
+  s.bw = s.zt ? 0 : L.take(8 * (size_t)Z * Z);
   s.dem = L.take(32 * (size_t)T);
   s.tg = (it || r->task_group) ? L.take(4 * (size_t)T) : 0;
   s.ga = (it || r->task_group) ? L.take(4 * (size_t)std::max(s.G, 1)) : 0;
@@ -2459,8 +2491,10 @@ static void stage_round(char* hb, char* db, HostSlot& s, const pvt_round* r, con
   put(s.zone, r->zone, 4 * (size_t)H);
   if (r->tiebreak) put(s.tb, r->tiebreak, 4 * (size_t)H);
   if (r->decay) put(s.dc, r->decay, 4 * (size_t)H);
-  put(s.cost, r->cost, r->cost ? 8 * (size_t)Z * Z : 0);
-  put(s.bw, r->bw, r->bw ? 8 * (size_t)Z * Z : 0);
+  if (!s.zt) {
+    put(s.cost, r->cost, r->cost ? 8 * (size_t)Z * Z : 0);
+    put(s.bw, r->bw, r->bw ? 8 * (size_t)Z * Z : 0);
+  }
   put(s.dem, r->dem, 32 * (size_t)T);
   if (r->task_group) { put(s.tg, r->task_group, 4 * (size_t)T); put(s.ga, r->group_anchor, 4 * (size_t)s.G); }
   if (s.GR) put(s.rt, r->rt_bw, 8 * (size_t)s.GR * H);
@@ -2479,8 +2513,8 @@ static void stage_round(char* hb, char* db, HostSlot& s, const pvt_round* r, con
   d.zone = reinterpret_cast<const int32_t*>(db + s.zone);
   d.tiebreak = r->tiebreak ? reinterpret_cast<const uint32_t*>(db + s.tb) : nullptr;
   d.decay = r->decay ? reinterpret_cast<const int32_t*>(db + s.dc) : nullptr;
-  d.cost = r->cost ? reinterpret_cast<const double*>(db + s.cost) : nullptr;
-  d.bw = r->bw ? reinterpret_cast<const double*>(db + s.bw) : nullptr;
+  d.cost = s.zt ? s.zt : r->cost ? reinterpret_cast<const double*>(db + s.cost) : nullptr;
+  d.bw = s.zt ? s.zt + (size_t)Z * Z : r->bw ? reinterpret_cast<const double*>(db + s.bw) : nullptr;
   d.dem = reinterpret_cast<const double*>(db + s.dem);
   d.task_group = s.tg ? reinterpret_cast<const int32_t*>(db + s.tg) : nullptr;
   d.group_anchor = s.ga ? reinterpret_cast<const int32_t*>(db + s.ga) : nullptr;
@@ -2561,6 +2595,7 @@ extern "C" int pvt_place_host(pvt_ctx* ctx, pvt_round* r, pvt_ca_items* it) {
   if (r->n_tasks == 0) return PVT_OK;
   HIPCHK(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
+  if ((rc = zone_cache(ctx, r, s))) return rc;
   StageLayout L;
   plan_out(L, s, r, it);
   const size_t n_out = L.o;
@@ -2696,6 +2731,21 @@ extern "C" int pvt_place_host_batch(pvt_ctx* ctx, pvt_round* rounds, pvt_ca_item
   for (int i = 0; i < n_rounds; i++)
     if (rounds[i].n_tasks > 0) plan_out(L, s[i], &rounds[i], items ? items[i] : nullptr);
   const size_t n_out = L.o;
+  {
+    bool filled = false;               // (the cache takes the first round's tables at most)
+    for (int i = 0; i < n_rounds; i++) {
+      if (rounds[i].n_tasks == 0 || !rounds[i].cost) continue;
+      const int Z = rounds[i].n_zones;
+      const size_t zz = (size_t)Z * Z;
+      const bool hit = ctx->zt_Z == Z && ctx->zt_host.size() == 2 * zz &&
+                       std::memcmp(ctx->zt_host.data(), rounds[i].cost, 8 * zz) == 0 &&
+                       std::memcmp(ctx->zt_host.data() + zz, rounds[i].bw, 8 * zz) == 0;
+      if (hit || !filled) {
+        if ((rc = zone_cache(ctx, &rounds[i], s[i]))) return rc;
+        filled = true;
+      }
+    }
+  }
   for (int i = 0; i < n_rounds; i++)
     if (rounds[i].n_tasks > 0) plan_in(L, s[i], &rounds[i], items ? items[i] : nullptr);
   std::vector<int> live, withit;

@@ -53,3 +53,23 @@ def test_batch_beyond_resident_limits_is_refused(engine):
     assert not engine.host_batch_fits(r)
     with pytest.raises(Exception):
         engine.place_host_batch([(r, None)])
+
+
+def test_zone_table_cache_follows_the_tables(engine):
+    """Host-array rounds keep their zone tables on the device between calls (the drop-in rounds
+    of one cluster pass the same tables every time); a round whose tables differ -- other costs,
+    other bandwidths, another zone count -- must be staged and refresh the cache, in single
+    calls and inside a batch whose rounds carry different tables."""
+    base = [synthetic.make_round(m, 800, 120, seed=400 + i) for i, m in
+            enumerate([_abi.PVT_CA_BF, _abi.PVT_CA_FF, _abi.PVT_CA_BF])]
+    other = synthetic.make_round(_abi.PVT_CA_BF, 800, 120, seed=410)
+    other.cost = other.cost * 2.0 + 0.5
+    bw = synthetic.make_round(_abi.PVT_CA_FF, 800, 120, seed=411)
+    bw.bw = bw.bw * 0.5
+    small = synthetic.make_round(_abi.PVT_CA_BF, 600, 100, seed=412, n_zones=7)
+    seq = [base[0], other, base[1], bw, small, base[2], base[0]]
+    for i, r in enumerate(seq):                     # one round per call
+        _same(engine.place(r), oracle.place(r), "single call %d" % i)
+    got = engine.place_host_batch([(r, None) for r in seq])   # mixed tables in one call
+    for i, (r, g) in enumerate(zip(seq, got)):
+        _same(g, oracle.place(r), "batch round %d" % i)
