@@ -33,23 +33,37 @@ __device__ __forceinline__ uint64_t order_bits(double v) {   // total order of d
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
 
-__global__ void band_keys_kernel(const double* avail, int H, int lo, int n, uint64_t* key,
-                                 int32_t* idx) {
+// The sort keys, and each host's snapshot row (4 capacities and its tiebreak rank) as one
+// 64-byte record, so the gather after the sort reads one line per host (from the SoA rows it read
+// five lines per host: 640 MB per config-5 round for 36 MB of data).
+__global__ __launch_bounds__(256) void band_keys_kernel(const double* avail, const uint32_t* tb,
+                                                        int H, int lo, int n, uint64_t* key,
+                                                        int32_t* idx, BandRec* rec) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  key[p] = order_bits(avail[(size_t)H + lo + p]);
+  const size_t h = (size_t)lo + p;
+  const double a0 = avail[h], a1 = avail[(size_t)H + h];
+  const double a2 = avail[2 * (size_t)H + h], a3 = avail[3 * (size_t)H + h];
+  key[p] = order_bits(a1);
   idx[p] = lo + p;
+  double4* r = reinterpret_cast<double4*>(&rec[p]);
+  r[0] = make_double4(a0, a1, a2, a3);
+  rec[p].tb = tb ? tb[h] : 0u;
 }
 
-__global__ void band_gather_kernel(const double* avail, const uint32_t* tb, int H, int n,
-                                   const int32_t* sid, double* sa, uint32_t* stb, int32_t* pos) {
+__global__ void band_gather_kernel(const BandRec* rec, int lo, int n, const int32_t* sid,
+                                   double* sa, uint32_t* stb, int32_t* pos) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
   const int h = sid[p];
   pos[h] = p;                              // (host -> sorted position, for the touched flags)
-#pragma unroll
-  for (int r = 0; r < 4; r++) sa[(size_t)r * n + p] = avail[(size_t)r * H + h];
-  stb[p] = tb[h];
+  const BandRec& x = rec[h - lo];
+  const double4 a = *reinterpret_cast<const double4*>(&x);
+  sa[p] = a.x;
+  sa[(size_t)n + p] = a.y;
+  sa[2 * (size_t)n + p] = a.z;
+  sa[3 * (size_t)n + p] = a.w;
+  stb[p] = x.tb;
 }
 
 // After a walk: the hosts it committed to (own_ids, count status[1]) that were not touched yet
@@ -356,26 +370,28 @@ __global__ __launch_bounds__(1024) void band_runs_kernel(const double* dem, int 
 }
 
 void launch_band_runs(const double* dem, int T, int32_t* run, double* rdem, hipStream_t st) {
-  if (T > 0) hipLaunchKernelGGL(band_runs_kernel, dim3(1), dim3(1024), 0, st, dem, T, run, rdem);
+  if (T > 0) PVT_LAUNCH(band_runs_kernel, dim3(1), dim3(1024), 0, st, dem, T, run, rdem);
 }
 
-void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,
-                      hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(band_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, H, lo, n, key, idx);
+void launch_band_keys(const double* avail, const uint32_t* tb, int H, int lo, int n, uint64_t* key,
+                      int32_t* idx, BandRec* rec, hipStream_t st) {
+  if (n > 0)
+    PVT_LAUNCH(band_keys_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, tb, H, lo, n, key,
+               idx, rec);
 }
-void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, const int32_t* sid,
-                        double* sa, uint32_t* stb, int32_t* pos, hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(band_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, tb, H, n, sid, sa, stb, pos);
+void launch_band_gather(const BandRec* rec, int lo, int n, const int32_t* sid, double* sa,
+                        uint32_t* stb, int32_t* pos, hipStream_t st) {
+  if (n > 0) PVT_LAUNCH(band_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, st, rec, lo, n, sid, sa, stb, pos);
 }
 void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* flags, int32_t* tlist,
                          int32_t* tcount, const int32_t* pos, int lo, int hi, uint8_t* ptouch,
                          hipStream_t st) {
-  hipLaunchKernelGGL(touch_update_kernel, dim3(1), dim3(1024), 0, st, own, status, flags, tlist,
+  PVT_LAUNCH(touch_update_kernel, dim3(1), dim3(1024), 0, st, own, status, flags, tlist,
                      tcount, pos, lo, hi, ptouch);
 }
 void launch_band_score(const BandArgs& a, hipStream_t st) {
   const int waves = a.nt * a.S;
-  if (waves > 0) hipLaunchKernelGGL(band_score_kernel, dim3((waves + WPB - 1) / WPB), dim3(WPB * WAVE), 0, st, a);
+  if (waves > 0) PVT_LAUNCH(band_score_kernel, dim3((waves + WPB - 1) / WPB), dim3(WPB * WAVE), 0, st, a);
 }
 
 }  // namespace pvt

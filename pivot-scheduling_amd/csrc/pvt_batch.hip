@@ -1066,24 +1066,24 @@ template <int MODE, int W>
 static void launch_waves(int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
   const dim3 grid(n), block(W * WAVE);
   switch (hpl) {
-    case 1: hipLaunchKernelGGL((resident_kernel<MODE, W, 1>), grid, block, lds, st, a); break;
-    case 2: hipLaunchKernelGGL((resident_kernel<MODE, W, 2>), grid, block, lds, st, a); break;
-    case 4: hipLaunchKernelGGL((resident_kernel<MODE, W, 4>), grid, block, lds, st, a); break;
-    case 8: hipLaunchKernelGGL((resident_kernel<MODE, W, 8>), grid, block, lds, st, a); break;
-    default: hipLaunchKernelGGL((resident_kernel<MODE, 4, 16>), grid, dim3(4 * WAVE), lds, st, a); break;
+    case 1: PVT_LAUNCH((resident_kernel<MODE, W, 1>), grid, block, lds, st, a); break;
+    case 2: PVT_LAUNCH((resident_kernel<MODE, W, 2>), grid, block, lds, st, a); break;
+    case 4: PVT_LAUNCH((resident_kernel<MODE, W, 4>), grid, block, lds, st, a); break;
+    case 8: PVT_LAUNCH((resident_kernel<MODE, W, 8>), grid, block, lds, st, a); break;
+    default: PVT_LAUNCH((resident_kernel<MODE, 4, 16>), grid, dim3(4 * WAVE), lds, st, a); break;
   }
 }
 template <int MODE>
 static void launch_two(int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
   const dim3 grid(n), block(2 * WAVE);
   switch (hpl) {
-    case 8: hipLaunchKernelGGL((resident_kernel<MODE, 2, 8>), grid, block, lds, st, a); break;
-    default: hipLaunchKernelGGL((resident_kernel<MODE, 2, 16>), grid, block, lds, st, a); break;
+    case 8: PVT_LAUNCH((resident_kernel<MODE, 2, 8>), grid, block, lds, st, a); break;
+    default: PVT_LAUNCH((resident_kernel<MODE, 2, 16>), grid, block, lds, st, a); break;
   }
 }
 template <int MODE>
 static void launch_one(int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((resident_kernel<MODE, 1, 16>), dim3(n), dim3(WAVE), lds, st, a);
+  PVT_LAUNCH((resident_kernel<MODE, 1, 16>), dim3(n), dim3(WAVE), lds, st, a);
 }
 template <int MODE>
 static void launch_mode(int waves, int hpl, int n, size_t lds, const ResidentArgs& a, hipStream_t st) {
@@ -1111,11 +1111,11 @@ void launch_resident(int mode, int waves, int hpl, int n, const ResidentArgs& a,
   if (mode == RES_MIXED) {             // (four waves; resident_shape with waves = 4)
     const dim3 grid(n), block(4 * WAVE);
     switch (hpl) {
-      case 1: hipLaunchKernelGGL((resident_mixed_kernel<4, 1>), grid, block, lds, st, a); break;
-      case 2: hipLaunchKernelGGL((resident_mixed_kernel<4, 2>), grid, block, lds, st, a); break;
-      case 4: hipLaunchKernelGGL((resident_mixed_kernel<4, 4>), grid, block, lds, st, a); break;
-      case 8: hipLaunchKernelGGL((resident_mixed_kernel<4, 8>), grid, block, lds, st, a); break;
-      default: hipLaunchKernelGGL((resident_mixed_kernel<4, 16>), grid, block, lds, st, a); break;
+      case 1: PVT_LAUNCH((resident_mixed_kernel<4, 1>), grid, block, lds, st, a); break;
+      case 2: PVT_LAUNCH((resident_mixed_kernel<4, 2>), grid, block, lds, st, a); break;
+      case 4: PVT_LAUNCH((resident_mixed_kernel<4, 4>), grid, block, lds, st, a); break;
+      case 8: PVT_LAUNCH((resident_mixed_kernel<4, 8>), grid, block, lds, st, a); break;
+      default: PVT_LAUNCH((resident_mixed_kernel<4, 16>), grid, block, lds, st, a); break;
     }
     return;
   }
@@ -1238,11 +1238,11 @@ void launch_fused(int mode, int hpl, int n, size_t lds, const FusedArgs& F, hipS
   const dim3 grid(n), block(4 * WAVE);
 #define PVT_FUSED_HPL(M)                                                                         \
   switch (hpl) {                                                                                 \
-    case 1: hipLaunchKernelGGL((resident_fused_kernel<M, 1>), grid, block, lds, st, F); break;   \
-    case 2: hipLaunchKernelGGL((resident_fused_kernel<M, 2>), grid, block, lds, st, F); break;   \
-    case 4: hipLaunchKernelGGL((resident_fused_kernel<M, 4>), grid, block, lds, st, F); break;   \
-    case 8: hipLaunchKernelGGL((resident_fused_kernel<M, 8>), grid, block, lds, st, F); break;   \
-    default: hipLaunchKernelGGL((resident_fused_kernel<M, 16>), grid, block, lds, st, F); break; \
+    case 1: PVT_LAUNCH((resident_fused_kernel<M, 1>), grid, block, lds, st, F); break;   \
+    case 2: PVT_LAUNCH((resident_fused_kernel<M, 2>), grid, block, lds, st, F); break;   \
+    case 4: PVT_LAUNCH((resident_fused_kernel<M, 4>), grid, block, lds, st, F); break;   \
+    case 8: PVT_LAUNCH((resident_fused_kernel<M, 8>), grid, block, lds, st, F); break;   \
+    default: PVT_LAUNCH((resident_fused_kernel<M, 16>), grid, block, lds, st, F); break; \
   }
   switch (mode) {
     case CA_FF: PVT_FUSED_HPL(CA_FF) break;

@@ -133,6 +133,7 @@ struct RoundState {
   bool kf_pending = false;        // keyed rounds: the group start's frontier walk comes next
   bool ffe = false;               // keyed rounds: first-fit zero-key epochs (ff_epoch)
   bool hmin_pre = false;          // the first epoch's host minima were queued by round_begin
+  bool zpre = false;              // ... and its zero-cost windows were prebuilt (ctx->zwin)
   bool stage_flag = false;        // the grouped order's counts are signalled by ctx->flag_host
   bool gathered = false;          // ... and group_sort_gather_kernel wrote the gathered order
   bool prep_fused = false;        // build_order's order_scatter_kernel filled placement / zone tables
@@ -165,6 +166,8 @@ struct pvt_ctx {
   int64_t windows = 0, refills = 0;
   int profiling = 0;               // 0 off, 1 every launch, 2 the named kernels only
   std::string prof_only;           //   (2: this one named kernel, when set)
+  int bind_events = 1;             //   (2: events bound to the kernel's dispatch; PVT_BIND_EVENTS)
+  int64_t n_unbound = 0;           //   (2: named scopes whose bound events were dropped)
   pvt_kstats ks[PVT_K_COUNT];
   std::vector<hipEvent_t> evpool;
   std::vector<TimedLaunch> pending;
@@ -192,6 +195,8 @@ struct pvt_ctx {
   int t_keyed_scan = -1;          // PVT_KEYED_SCAN: keyed first-fit scan on / off (-1: keyed_scan)
   int t_of_hosts = 0;             // PVT_OF_HOSTS: ordered frontier host span (0: default)
   int t_epoch_plan = 1;           // PVT_EPOCH_PLAN: 0 = epoch chains by distinct zone only
+  int t_zpre = 1;                 // PVT_ZPRE: 0 = every frontier walk builds its own window
+  int t_chain_tab = 1;            // PVT_CHAIN_TAB: 0 = chain tables uploaded before the walk
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
   int rwalk = 1;                  // PVT_RWALK=0: resident rounds without the one-wave walk (A/B)
@@ -200,11 +205,13 @@ struct pvt_ctx {
                                   // measured slower, kept for A/B)
   Buf wslot;                      // enqueued-ahead walks' status slots (place_ahead)
   Buf bkey, bidx, bsa, bstb, btouch, btlist, btcnt, bsorttmp;   // band lists: sorted snapshot
+  Buf brec;                       // band lists: the snapshot's host records (BandRec)
   Buf bpos, bptouch;              // band lists: host -> sorted position, touched by position
   Buf brun, brdem;                // band lists: the round's runs of equal demands (ids, demands)
   Buf ep_dev, wres;               // epoch tables / status / flags, per-task commit logs
   Buf hmin;                       // frontier walk: per-dimension host minima (partials)
   Buf cmax;                       // frontier-walked epochs: chains' largest demands
+  Buf zwin;                       // the first epoch's zero-cost windows (ZoneWindows)
   int32_t* ep_host = nullptr;     // pinned staging of ep_dev
   int32_t* ep_hdev = nullptr;     // ep_host's device address (the accept kernel's readback)
   pvt_round* rstage = nullptr;    // pvt_place_batch: descriptors staged for the device (pinned)
@@ -288,26 +295,50 @@ static hipEvent_t take_event(pvt_ctx* ctx) {
   (void)hipEventCreateWithFlags(&e, PROFILE_EVENT_FLAGS);
   return e;
 }
+namespace pvt { thread_local TimedEvents g_timed; }
+// A profiling scope. profiling 1: events recorded around the scope's launches. profiling 2 (one
+// named kernel): the events are bound to that kernel's dispatch by PVT_LAUNCH (pvt_kernels.h),
+// with no marker packets in the stream; PVT_BIND_EVENTS=0 records them around it instead.
 struct Scope {
   pvt_ctx* ctx;
   hipStream_t st;
   TimedLaunch t;
+  bool bound = false;
   Scope(pvt_ctx* c, int kclass, double cand, double bytes, hipStream_t s = nullptr,
         const char* kname = nullptr)
       : ctx(c), st(s ? s : c->stream) {
     t.kclass = kclass; t.kname = kname; t.candidates = cand; t.bytes = bytes; t.a = t.b = nullptr;
-    if (on()) { t.a = take_event(ctx); (void)hipEventRecord(t.a, st); }
+    if (!on()) return;
+    t.a = take_event(ctx);
+    if (ctx->profiling == 2 && ctx->bind_events && !g_timed.armed) {
+      t.b = take_event(ctx);
+      g_timed.a = t.a; g_timed.b = t.b; g_timed.armed = true; g_timed.used = g_timed.extra = 0;
+      bound = true;
+    } else {
+      (void)hipEventRecord(t.a, st);
+    }
   }
   bool on() const {
     return ctx->profiling == 1 ||
            (ctx->profiling == 2 && t.kname && (ctx->prof_only.empty() || ctx->prof_only == t.kname));
   }
   ~Scope() {
-    if (on()) {
-      t.b = take_event(ctx);
-      (void)hipEventRecord(t.b, st);
-      ctx->pending.push_back(t);
+    if (!on()) return;
+    if (bound) {
+      const bool ok = g_timed.used == 1 && g_timed.extra == 0;
+      g_timed = TimedEvents{};
+      if (ok) {
+        ctx->pending.push_back(t);
+      } else {                        // no launch, or more than the one the events bound to
+        ctx->evpool.push_back(t.a);
+        ctx->evpool.push_back(t.b);
+        ctx->n_unbound++;
+      }
+      return;
     }
+    t.b = take_event(ctx);
+    (void)hipEventRecord(t.b, st);
+    ctx->pending.push_back(t);
   }
 };
 static void harvest(pvt_ctx* ctx) {
@@ -398,11 +429,14 @@ extern "C" int pvt_ctx_create(int device, pvt_ctx** out) {
   if (const char* e = getenv("PVT_AHEAD")) ctx->ahead = atoi(e) != 0;                  // A/B
   if (const char* e = getenv("PVT_RWALK")) ctx->rwalk = atoi(e);                       // A/B
   if (const char* e = getenv("PVT_FUSED")) ctx->fused = atoi(e) != 0;                  // A/B
+  if (const char* e = getenv("PVT_BIND_EVENTS")) ctx->bind_events = atoi(e) != 0;      // A/B
   if (const char* e = getenv("PVT_SEGMENTS")) ctx->t_segments = std::max(1, atoi(e));  // tuning
   if (const char* e = getenv("PVT_BAND_SEGS")) ctx->t_band_segs = atoi(e);             // tuning
   if (const char* e = getenv("PVT_KEYED_SCAN")) ctx->t_keyed_scan = atoi(e) != 0;      // A/B
   if (const char* e = getenv("PVT_OF_HOSTS")) ctx->t_of_hosts = std::max(ZW_M, atoi(e));   // tuning
   if (const char* e = getenv("PVT_EPOCH_PLAN")) ctx->t_epoch_plan = atoi(e);           // A/B
+  if (const char* e = getenv("PVT_ZPRE")) ctx->t_zpre = atoi(e) != 0;                  // A/B
+  if (const char* e = getenv("PVT_CHAIN_TAB")) ctx->t_chain_tab = atoi(e) != 0;        // A/B
   if (const char* e = getenv("PVT_MERGE_SMALL")) ctx->t_merge_bitonic = atoi(e) == 0;  // A/B
   if (const char* e = getenv("PVT_RES_WAVES")) ctx->res_waves = atoi(e) == 8 ? 8 : atoi(e) == 2 ? 2 : atoi(e) == 1 ? 1 : 4;  // A/B
   *out = ctx;
@@ -422,7 +456,8 @@ extern "C" int pvt_ctx_destroy(pvt_ctx* ctx) {
                  &ctx->owned[0], &ctx->owned[1], &ctx->rdesc, &ctx->rmt, &ctx->anc_scr, &ctx->oppfault, &ctx->hdev, &ctx->kskey, &ctx->kperm, &ctx->kiota,
                  &ctx->ksorttmp, &ctx->kflag, &ctx->ep_dev, &ctx->wres, &ctx->hmin, &ctx->cmax, &ctx->fwin,
                  &ctx->bkey, &ctx->bidx, &ctx->bsa, &ctx->bstb, &ctx->btouch, &ctx->btlist,
-                 &ctx->btcnt, &ctx->bsorttmp, &ctx->brun, &ctx->brdem, &ctx->bpos, &ctx->bptouch, &ctx->zt_dev};
+                 &ctx->btcnt, &ctx->bsorttmp, &ctx->brun, &ctx->brdem, &ctx->bpos, &ctx->bptouch, &ctx->zt_dev,
+                 &ctx->zwin, &ctx->brec};
   for (Buf* b : bufs)
     if (b->p) (void)hipFree(b->p);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -649,7 +684,8 @@ static int build_order_radix(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out
 // hmin (or NULL): the frontier walk's host minima, written by the order's launch when it can
 // (*hmin_done); stage_flag: the host then waits on ctx->flag_host instead of ev_stage.
 static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool* pending,
-                       double* hmin = nullptr, bool* hmin_done = nullptr) {
+                       double* hmin = nullptr, bool* hmin_done = nullptr,
+                       ZoneWindows* zwin = nullptr) {
   *pending = false;
   if (hmin_done) *hmin_done = false;
   ctx->rs.stage_flag = false;
@@ -661,6 +697,7 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
   const bool grouped = r->task_group != nullptr && r->n_groups > 1;
   RoundState& R = ctx->rs;
   R.ginfo = false;
+  R.zpre = false;
   if (grouped && r->n_groups <= (1 << 20)) {
     // one synchronisation: group counts, group anchors and the cost table to the host
     const int G = r->n_groups;
@@ -711,10 +748,13 @@ static int build_order(pvt_ctx* ctx, const pvt_round* r, int32_t** ord_out, bool
         pa.hflag = ctx->flag_hdev;
         pa.seq = ++ctx->flag_seq;
         R.stage_flag = true;
+        const bool zw = hmin && zwin && ca && r->n_zones <= ZMAX;
         launch_group_sort_gather(pa, GatherOut{cur, P<double>(ctx->dem_ord), P<int32_t>(ctx->anc_ord),
                                                P<int32_t>(ctx->grp_ord), r->order, r->avail,
-                                               r->n_hosts, hmin, ctx->stamps}, st);
+                                               r->n_hosts, hmin, ctx->stamps, r->zone,
+                                               zw ? zwin : nullptr}, st);
         if (hmin_done) *hmin_done = hmin != nullptr;
+        R.zpre = zw;
         R.gathered = true;
         R.ginfo = ca;
         *pending = true;
@@ -913,6 +953,9 @@ static int opp_round(pvt_ctx* ctx, const pvt_round* r) {
 
 // vbp best-fit band lists: hosts [lo, hi) sorted by snapshot memory (stable radix sort of the
 // orderable bits of avail[1]) and their snapshot state gathered in that order; no host touched.
+// (rocPRIM's onesweep sort measured slower than the default dispatch's merge sort at config 5's
+// 1M hosts: 8 passes of ~25 us plus two fill launches each, against ~0.19 ms; the memory values
+// of uniform random hosts vary in ~63 key bits, so no pass can be skipped.)
 static int band_snapshot(pvt_ctx* ctx) {
   RoundState& R = ctx->rs;
   const pvt_round* r = &R.r;
@@ -925,6 +968,9 @@ static int band_snapshot(pvt_ctx* ctx) {
   ENSURE(ctx->btouch, (size_t)R.H);
   ENSURE(ctx->btlist, sizeof(int32_t) * (size_t)R.H);
   ENSURE(ctx->btcnt, 16);
+  ENSURE(ctx->bpos, sizeof(int32_t) * (size_t)R.H);
+  ENSURE(ctx->bptouch, (size_t)n);
+  ENSURE(ctx->brec, sizeof(BandRec) * (size_t)n);
   uint64_t* k0 = P<uint64_t>(ctx->bkey);
   int32_t* i0 = P<int32_t>(ctx->bidx);
   size_t tmp = 0;
@@ -933,12 +979,10 @@ static int band_snapshot(pvt_ctx* ctx) {
   const int bs = ctx->t_band_segs ? ctx->t_band_segs : BAND_SEGS;   // (PVT_BAND_SEGS: 2 ... 32)
   R.band_S = (bs == 1 || bs == 2 || bs == 4 || bs == 8 || bs == 16 || bs == 32) ? bs : BAND_SEGS;
   Scope sc(ctx, PVT_K_OTHER, 0, 0);
-  launch_band_keys(r->avail, R.H, R.lo, n, k0, i0, st);
+  launch_band_keys(r->avail, r->tiebreak, R.H, R.lo, n, k0, i0, P<BandRec>(ctx->brec), st);
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(ctx->bsorttmp.p, tmp, k0, k0 + n, i0, i0 + n, n, 0, 64, st));
-  ENSURE(ctx->bpos, sizeof(int32_t) * (size_t)R.H);
-  ENSURE(ctx->bptouch, (size_t)n);
-  launch_band_gather(r->avail, r->tiebreak, R.H, n, i0 + n, P<double>(ctx->bsa), P<uint32_t>(ctx->bstb),
-                     P<int32_t>(ctx->bpos), st);
+  launch_band_gather(P<BandRec>(ctx->brec), R.lo, n, i0 + n, P<double>(ctx->bsa),
+                     P<uint32_t>(ctx->bstb), P<int32_t>(ctx->bpos), st);
   HIPCHK(hipMemsetAsync(ctx->btouch.p, 0, (size_t)R.H, st));
   HIPCHK(hipMemsetAsync(ctx->bptouch.p, 0, (size_t)n, st));
   HIPCHK(hipMemsetAsync(ctx->btcnt.p, 0, 16, st));
@@ -993,10 +1037,13 @@ static int round_begin(pvt_ctx* ctx, const pvt_round* rin, int lo, int hi, int w
   // host waits for the grouped order's counts
   const bool want_hmin = ctx->epochs && ctx->zwalk && r->mode == PVT_CA_BF && r->task_group &&
                          r->n_groups >= 2 && T >= 2 && !r->rt_bw && Z <= ZMAX && world == 1;
-  if (want_hmin) ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+  if (want_hmin) {
+    ENSURE(ctx->hmin, sizeof(double) * 4 * ZW_MIN_PARTS);
+    if (ctx->t_zpre) ENSURE(ctx->zwin, sizeof(ZoneWindows));
+  }
   bool hmin_done = false;
   if ((rc = build_order(ctx, r, &R.ord, &pending, want_hmin ? P<double>(ctx->hmin) : nullptr,
-                        &hmin_done)))
+                        &hmin_done, want_hmin && ctx->t_zpre ? P<ZoneWindows>(ctx->zwin) : nullptr)))
     return rc;
   if (!R.prep_fused) HIPCHK(hipMemsetAsync(r->placement, 0xff, sizeof(int32_t) * T, st));
   auto order_out = [&]() -> int {   // (the gather also writes the caller's order)
@@ -1844,6 +1891,35 @@ static int upload_chain_tables(pvt_ctx* ctx, const EpochPlan& E) {
   return PVT_OK;
 }
 
+// The same tables by value for the frontier walk (ChainTab: no upload launch); false when the
+// epoch does not fit them (the caller uploads instead).
+static_assert(EPOCH_SEGS == CT_SEGS, "chain tables by value hold every epoch segment");
+static bool chain_tab(pvt_ctx* ctx, const EpochPlan& E, ChainTab& t) {
+  const int nseg = (int)E.chain.size(), nch = (int)E.segs.size();
+  if (nseg < 1 || nseg > CT_SEGS || nch < 1 || nch > CT_SEGS) return false;
+  for (int c = 0; c < nch; c++)
+    if (E.len[c] > CHAIN_MAX) return false;
+  int32_t* dev = P<int32_t>(ctx->ep_dev);
+  t.nseg = nseg;
+  t.nch = nch;
+  for (int k = 0; k <= nseg; k++) t.seg_off[k] = E.off[k];
+  for (int k = 0; k < nseg; k++) { t.seg_chain[k] = E.chain[k]; t.seg_cstart[k] = E.cstart[k]; }
+  int nm = 0, ns = 0;
+  for (int c = 0; c < nch; c++) {
+    t.coff[c] = nm;
+    t.csoff[c] = ns;
+    for (int sg : E.segs[c]) t.csegid[ns++] = sg;
+    nm += E.len[c];
+  }
+  t.coff[nch] = nm;
+  t.csoff[nch] = ns;
+  t.o_seg_off = dev + EP_SEG_OFF;
+  t.o_seg_chain = dev + EP_SEG_CHAIN;
+  t.o_seg_cstart = dev + EP_SEG_CSTART;
+  t.o_coff = dev + EP_COFF;
+  return true;
+}
+
 // cost_aware first-fit with sort_hosts (cost_aware.py:99-127): an epoch of WHOLE groups from
 // the group start R.t0, chains of zero-cost components walked side by side by the first-fit
 // zero-key chain walk (pvt_zwalk.hip, FF). Every task it proves takes the lowest-index strictly
@@ -1873,12 +1949,12 @@ static int ff_epoch(pvt_ctx* ctx, int* adv_out) {
     Scope sc(ctx, PVT_K_OTHER, 0, 0);
     launch_host_absmax(r->avail, R.H, 0, R.H, P<double>(ctx->hmin), st);
   }
-  if ((rc = upload_chain_tables(ctx, E))) return rc;
   ZwalkArgs za{r->avail, r->zone, R.H, R.Z, P<double>(ctx->dem_ord) + (size_t)t0 * 4,
                P<int32_t>(ctx->anc_ord) + t0, R.ord + t0, P<double>(ctx->csum),
                P<double>(ctx->bsum), dev + EP_COFF, dev + EP_CMAP, dev + EP_STATUS,
                P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
                nullptr, 0, 0, 0, nullptr, nullptr, nullptr, dev + EP_CSOFF, dev + EP_CSEG};
+  if (!(ctx->t_chain_tab && chain_tab(ctx, E, za.tab)) && (rc = upload_chain_tables(ctx, E))) return rc;
   {
     Scope sc(ctx, PVT_K_COMMIT, 0, 0, nullptr, "zwalk_kernel");
     launch_zwalk_ff(za, nch, st);
@@ -1977,7 +2053,10 @@ static int place_epochs(pvt_ctx* ctx) {
       t0 += adv;
       continue;
     }
-    if ((rc = upload_chain_tables(ctx, E))) return rc;
+    // (the frontier walk takes the chain tables by value: no upload)
+    ChainTab tab{};
+    const bool tabv = zw && ctx->t_chain_tab && chain_tab(ctx, E, tab);
+    if (!tabv && (rc = upload_chain_tables(ctx, E))) return rc;
     // (the rejection flags are zeroed by epoch_final_kernel, launched before every validation)
     int need = nch;                           // chains left to the list walk
     EpochArgs ea{P<double>(ctx->dem_ord) + (size_t)t0 * 4, P<int32_t>(ctx->anc_ord) + t0,
@@ -2003,6 +2082,10 @@ static int place_epochs(pvt_ctx* ctx) {
                    P<WinRec>(ctx->wres), r->placement, P<double>(ctx->hmin), ctx->stamps,
                    nullptr, 0, 0, 0, nullptr, nullptr, nullptr, dev + EP_CSOFF, dev + EP_CSEG,
                    P<double>(ctx->cmax)};
+      // (the first epoch starts from the snapshot the grouped order's launch built its windows from)
+      if (R.zpre && t0 == 0 && !big) za.zpre = P<ZoneWindows>(ctx->zwin);
+      if (tabv) za.tab = tab;
+      R.zpre = false;
       ea.cmax = P<double>(ctx->cmax);
       ea.coff = dev + EP_COFF;
       ea.nch = nch;

@@ -403,22 +403,22 @@ __global__ __launch_bounds__(1024) void epoch_accept_apply_kernel(EpochArgs A, i
 
 void launch_epoch_accept_apply(const EpochArgs& a, int32_t* res, int nchains, hipStream_t st,
                                int32_t* hout, int nwords) {
-  hipLaunchKernelGGL(epoch_accept_apply_kernel, dim3(nchains), dim3(1024), 0, st, a, res, hout, nwords);
+  PVT_LAUNCH(epoch_accept_apply_kernel, dim3(nchains), dim3(1024), 0, st, a, res, hout, nwords);
 }
 
 void launch_epoch_validate(const EpochArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
+  PVT_LAUNCH(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
   const int tiles = (CHAIN_MAX + 255) / 256;   // a segment never exceeds its chain's cap
-  hipLaunchKernelGGL(epoch_validate_kernel, dim3(tiles, a.nseg, VAL_SPLIT), dim3(256), 0, st, a);
+  PVT_LAUNCH(epoch_validate_kernel, dim3(tiles, a.nseg, VAL_SPLIT), dim3(256), 0, st, a);
 }
 
 void launch_epoch_final(const EpochArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
+  PVT_LAUNCH(epoch_final_kernel, dim3(a.nseg), dim3(1024), 0, st, a);
 }
 
 void launch_epoch_apply(const EpochArgs& a, int n_accept, int nchains, hipStream_t st) {
   if (n_accept <= 0 || nchains <= 0) return;
-  hipLaunchKernelGGL(epoch_apply_kernel, dim3(nchains), dim3(256), 0, st, a, n_accept);
+  PVT_LAUNCH(epoch_apply_kernel, dim3(nchains), dim3(256), 0, st, a, n_accept);
 }
 
 }  // namespace pvt

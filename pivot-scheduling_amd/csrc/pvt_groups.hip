@@ -41,10 +41,10 @@ __global__ __launch_bounds__(GR_THREADS) void ca_groups_batch_kernel(const CaGro
 }
 
 void launch_ca_groups(const CaGroupArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(ca_groups_kernel, dim3(1), dim3(GR_THREADS), 0, st, a);
+  PVT_LAUNCH(ca_groups_kernel, dim3(1), dim3(GR_THREADS), 0, st, a);
 }
 void launch_ca_groups_batch(const CaGroupArgs* args_dev, int n, hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(ca_groups_batch_kernel, dim3(n), dim3(GR_THREADS), 0, st, args_dev);
+  if (n > 0) PVT_LAUNCH(ca_groups_batch_kernel, dim3(n), dim3(GR_THREADS), 0, st, args_dev);
 }
 
 }  // namespace pvt

@@ -8,9 +8,37 @@
 //   lists   per window task: KL candidates, sorted by (score, tiebreak, host) ascending
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 namespace pvt {
+
+// Timed launches (pvt_set_profiling 2: HIP events around one named kernel). Every launch helper
+// starts its kernel through PVT_LAUNCH. When the profiling scope (pvt_capi.hip Scope) has armed a
+// pair of events, the first launch binds them to the kernel's own dispatch
+// (hipExtLaunchKernelGGL: the events take the dispatch's start and end timestamps), so the timed
+// kernel costs the stream no marker packets. A recorded event pair around a launch left ~5 us of
+// idle GPU on each side of it (config-5 kernel trace: 7.7 us before the frontier walk, 5.0 after).
+// `extra` counts launches past the first while armed (a scope that would time only part of its
+// work; the scope then drops the sample).
+struct TimedEvents {
+  hipEvent_t a = nullptr, b = nullptr;
+  bool armed = false;
+  int used = 0, extra = 0;
+};
+extern thread_local TimedEvents g_timed;
+#define PVT_LAUNCH(kernel, grid, block, shmem, stream, ...)                                         \
+  do {                                                                                             \
+    ::pvt::TimedEvents& te_ = ::pvt::g_timed;                                                      \
+    if (te_.armed && te_.a) {                                                                      \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, te_.a, te_.b, 0u, __VA_ARGS__);    \
+      te_.a = nullptr;                                                                             \
+      te_.used++;                                                                                  \
+    } else {                                                                                       \
+      if (te_.armed) te_.extra++;                                                                  \
+      hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                         \
+    }                                                                                              \
+  } while (0)
 
 constexpr int WAVE = 64;
 constexpr int KL = 64;           // candidate list length per task (one entry per lane)
@@ -231,6 +259,27 @@ hipError_t lwalk_init_attrs();
 // list walk's chain mode (same tables, WinRec log, status[2b] = tasks walked) while it can prove
 // every winner is the lowest-index fitting zero-cost host of its window; otherwise it writes
 // status[2b] = -2 and leaves the chain to the list walk (CommitArgs.skip_done).
+// An epoch's chain tables passed BY VALUE in the frontier walk's kernel arguments (instead of an
+// upload launch before the walk: ~4 us of kernel plus its dispatch gap on the default line).
+// Segment k (one group's tasks in the epoch, processing order): epoch tasks [seg_off[k],
+// seg_off[k + 1]), walked by chain seg_chain[k] from chain-local position seg_cstart[k]. Chain c:
+// chain-local positions [0, coff[c + 1] - coff[c]), its segments csegid[csoff[c] .. csoff[c+1]) in
+// order. The walk's block 0 writes seg_off / seg_chain / seg_cstart / coff to the out pointers for
+// the epoch kernels after it. nch = 0: the tables come from the device arrays (ZwalkArgs.coff ...).
+constexpr int CT_SEGS = 64;
+struct ChainTab {
+  int32_t nseg, nch;
+  int32_t seg_off[CT_SEGS + 1];
+  int32_t seg_chain[CT_SEGS];
+  int32_t seg_cstart[CT_SEGS];
+  int32_t coff[CT_SEGS + 1];
+  int32_t csoff[CT_SEGS + 1];
+  int32_t csegid[CT_SEGS];
+  int32_t* o_seg_off;
+  int32_t* o_seg_chain;
+  int32_t* o_seg_cstart;
+  int32_t* o_coff;
+};
 struct ZwalkArgs {
   const double* avail;    // epoch-start capacities [4][H]
   const int32_t* zone;
@@ -262,6 +311,10 @@ struct ZwalkArgs {
   const int32_t* csoff;
   const int32_t* cseg;
   double* cmax;           // chain mode: [chains][4] out, each chain's largest demand per dimension
+  // chain mode, the round's first epoch: windows the grouped order's launch built from the
+  // snapshot (a chain uses the one whose zone set covers its anchors' zero-cost zones), or NULL
+  const struct ZoneWindows* zpre;
+  ChainTab tab;           // chain mode: the epoch's chain tables by value (tab.nch > 0), or none
 };
 constexpr int ZW_MIN_PARTS = 256;
 // per-dimension minima of avail over hosts [lo, hi) into part[ZW_MIN_PARTS][4]
@@ -293,6 +346,24 @@ struct FrontierSlot {
   int32_t pad[2];
   int32_t id[ZW_M];       // global host index, ascending
   double a[4][ZW_M];      // capacities
+};
+// Zero-cost windows prebuilt by the grouped order's launch (group_sort_gather_kernel) for the
+// round's first epoch of cost_aware best-fit: for each zone j that is the lowest zone of its
+// zero-cost component (zones joined by csum = 0), U[j] = the union of the zero-cost zones of the
+// round's group anchors in that component, and w[j] the first ZW_M hosts of U[j] in index order
+// with their zones and snapshot capacities (bad: some capacity is not finite with |x| <= 2^500,
+// certificate 3). U[j] = 0: no window for j. A chain's U (its anchors' zero-cost zones) lies in
+// one component, so it is covered by that component's U[j]; a window over a superset of the
+// zones is exact for the walk (pvt_zwalk.hip certificates).
+struct ZoneWindow {
+  int32_t n, bad, pad[2];
+  int32_t id[ZW_M];
+  int32_t z[ZW_M];
+  double a[4][ZW_M];
+};
+struct ZoneWindows {
+  uint32_t U[ZMAX];
+  ZoneWindow w[ZMAX];
 };
 struct FrontierHdr {
   int32_t kind, nslots, pad[14];
@@ -381,10 +452,17 @@ __device__ __forceinline__ bool gate_closed(const int32_t* g) {
   const int n = __builtin_amdgcn_readfirstlane(g[2]);
   return s != 0 || a != n;
 }
-void launch_band_keys(const double* avail, int H, int lo, int n, uint64_t* key, int32_t* idx,
-                      hipStream_t st);
-void launch_band_gather(const double* avail, const uint32_t* tb, int H, int n, const int32_t* sid,
-                        double* sa, uint32_t* stb, int32_t* pos, hipStream_t st);
+// A host's snapshot row for the band sort's gather (one 64-byte line per host).
+struct alignas(64) BandRec {
+  double a[4];
+  uint32_t tb;
+  uint32_t pad[7];
+};
+// sort keys and host records (rec[p] for host lo + p)
+void launch_band_keys(const double* avail, const uint32_t* tb, int H, int lo, int n, uint64_t* key,
+                      int32_t* idx, BandRec* rec, hipStream_t st);
+void launch_band_gather(const BandRec* rec, int lo, int n, const int32_t* sid, double* sa,
+                        uint32_t* stb, int32_t* pos, hipStream_t st);
 void launch_touch_update(const int32_t* own, const int32_t* status, uint8_t* flags, int32_t* tlist,
                          int32_t* tcount, const int32_t* pos, int lo, int hi, uint8_t* ptouch,
                          hipStream_t st);
@@ -497,6 +575,8 @@ struct GatherOut {
   int H;                      //   [0, H) (ZW_MIN_PARTS partials as host_min_kernel's, one per
   double* hmin;               //   extra block)
   uint64_t* stamps;           // diagnostic builds only (PVT_STAMPS): block 0's phases, [16, 20)
+  const int32_t* zone;        // zwin != NULL: Z more blocks prebuild the first epoch's zero-cost
+  struct ZoneWindows* zwin;   //   windows from the snapshot (ZoneWindows), or NULL
 };
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st);
 // bytes (rounded up to 16; both buffers 16-B aligned and that long) from mapped pinned memory

@@ -16,6 +16,7 @@
 
 #include "pvt_device.h"
 #include "pvt_kernels.h"
+#include "pvt_zwin_dev.h"
 #include "pvt_list.h"
 
 namespace pvt {
@@ -259,8 +260,8 @@ int score_tasks_per_wave(int mode, int hosts, int force) {
 
 template <int MODE>
 static void launch_score_tw(int tw, dim3 grid, dim3 block, const ScoreArgs& a, hipStream_t st) {
-  if (tw == 2) hipLaunchKernelGGL((score_kernel<MODE, 2>), grid, block, 0, st, a);
-  else hipLaunchKernelGGL((score_kernel<MODE, 4>), grid, block, 0, st, a);
+  if (tw == 2) PVT_LAUNCH((score_kernel<MODE, 2>), grid, block, 0, st, a);
+  else PVT_LAUNCH((score_kernel<MODE, 4>), grid, block, 0, st, a);
 }
 
 void launch_score(int mode, const ScoreArgs& a, hipStream_t st) {
@@ -735,10 +736,10 @@ const char* merge_kernel_name(const MergeArgs& a) {
 }
 void launch_merge(const MergeArgs& a, hipStream_t st) {
   switch (merge_variant(a)) {
-    case 1: hipLaunchKernelGGL(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(merge_pkg_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(merge_path_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
-    default: hipLaunchKernelGGL(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
+    case 1: PVT_LAUNCH(merge_small_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a); break;
+    case 2: PVT_LAUNCH(merge_pkg_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
+    case 3: PVT_LAUNCH(merge_path_kernel, dim3(a.nt), dim3(256), 0, st, a); break;
+    default: PVT_LAUNCH(merge_kernel, dim3(a.nt), dim3(256), 0, st, a);
   }
 }
 
@@ -774,7 +775,7 @@ __global__ __launch_bounds__(256) void pack_kernel(PackArgs A) {
   }
 }
 void launch_pack(const PackArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(pack_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+  PVT_LAUNCH(pack_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -825,8 +826,8 @@ __global__ __launch_bounds__(256) void ordered_kernel(OrderedArgs A) {
 
 void launch_ordered(const OrderedArgs& a, hipStream_t st) {
   dim3 grid((a.nt + 3) / 4), block(256);
-  if (a.strict) hipLaunchKernelGGL(ordered_kernel<true>, grid, block, 0, st, a);
-  else hipLaunchKernelGGL(ordered_kernel<false>, grid, block, 0, st, a);
+  if (a.strict) PVT_LAUNCH(ordered_kernel<true>, grid, block, 0, st, a);
+  else PVT_LAUNCH(ordered_kernel<false>, grid, block, 0, st, a);
 }
 
 // One wave per task: walk the group's sorted host order 64 positions at a time (perm and key
@@ -889,12 +890,12 @@ __global__ void zero_key_flags_kernel(const uint64_t* key, int n, uint8_t* flags
 }
 void launch_zero_key_flags(const double* key, int n, uint8_t* flags, hipStream_t st) {
   if (n > 0)
-    hipLaunchKernelGGL(zero_key_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, st,
+    PVT_LAUNCH(zero_key_flags_kernel, dim3((n + 255) / 256), dim3(256), 0, st,
                        reinterpret_cast<const uint64_t*>(key), n, flags);
 }
 
 void launch_perm_scan(const PermArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(perm_scan_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
+  PVT_LAUNCH(perm_scan_kernel, dim3((a.nt + 3) / 4), dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -910,7 +911,7 @@ __global__ void zone_tables_kernel(const double* cost, const double* bw, int Z, 
 }
 void launch_zone_tables(const double* cost, const double* bw, int Z, double* csum, double* bsum,
                         hipStream_t st) {
-  hipLaunchKernelGGL(zone_tables_kernel, dim3((Z * Z + 255) / 256), dim3(256), 0, st, cost, bw, Z,
+  PVT_LAUNCH(zone_tables_kernel, dim3((Z * Z + 255) / 256), dim3(256), 0, st, cost, bw, Z,
                      csum, bsum);
 }
 
@@ -928,7 +929,7 @@ __global__ void key_kernel(KeyArgs A) {
   A.key[h] = (c * df) / (r * bw);
 }
 void launch_key(const KeyArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(key_kernel, dim3((a.h_hi - a.h_lo + 255) / 256), dim3(256), 0, st, a);
+  PVT_LAUNCH(key_kernel, dim3((a.h_hi - a.h_lo + 255) / 256), dim3(256), 0, st, a);
 }
 
 __global__ void norm_keys_kernel(const double* dem, int T, const int32_t* idx, uint64_t* keys) {
@@ -941,7 +942,7 @@ __global__ void norm_keys_kernel(const double* dem, int T, const int32_t* idx, u
   keys[i] = ~(uint64_t)__double_as_longlong(n);
 }
 void launch_norm_keys(const double* dem, int T, const int32_t* idx, uint64_t* keys, hipStream_t st) {
-  hipLaunchKernelGGL(norm_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, T, idx, keys);
+  PVT_LAUNCH(norm_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, T, idx, keys);
 }
 
 __global__ void group_keys_kernel(const int32_t* tg, const int32_t* idx, int T, uint32_t* keys) {
@@ -951,7 +952,7 @@ __global__ void group_keys_kernel(const int32_t* tg, const int32_t* idx, int T, 
 }
 void launch_group_keys(const int32_t* task_group, const int32_t* idx, int T, uint32_t* keys,
                        hipStream_t st) {
-  hipLaunchKernelGGL(group_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, st, task_group, idx,
+  PVT_LAUNCH(group_keys_kernel, dim3((T + 255) / 256), dim3(256), 0, st, task_group, idx,
                      T, keys);
 }
 
@@ -1024,12 +1025,12 @@ __global__ __launch_bounds__(1024) void group_stage_kernel(const int32_t* cnt, i
 }
 void launch_group_stage(const int32_t* cnt, int G, const int32_t* ganc, const double* cost, int nz2,
                         int32_t* off, int32_t* hcnt, int32_t* hgan, double* hcst, hipStream_t st) {
-  hipLaunchKernelGGL(group_stage_kernel, dim3(1), dim3(1024), 0, st, cnt, G, ganc, cost, nz2, off,
+  PVT_LAUNCH(group_stage_kernel, dim3(1), dim3(1024), 0, st, cnt, G, ganc, cost, nz2, off,
                      hcnt, hgan, hcst);
 }
 
 void launch_group_hist(const int32_t* tg, int T, int G, int32_t* cnt, hipStream_t st) {
-  hipLaunchKernelGGL(group_hist_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, T, G, cnt);
+  PVT_LAUNCH(group_hist_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, T, G, cnt);
 }
 __global__ __launch_bounds__(1024) void group_scatter_kernel(const int32_t* tg, const uint64_t* keys, int T,
                                                              int G, int32_t* cursor, uint64_t* skey,
@@ -1060,7 +1061,7 @@ __global__ __launch_bounds__(1024) void group_scatter_kernel(const int32_t* tg, 
 }
 void launch_group_scatter(const int32_t* tg, const uint64_t* keys, int T, int G, int32_t* cursor,
                           uint64_t* skey, int32_t* sidx, hipStream_t st) {
-  hipLaunchKernelGGL(group_scatter_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, keys, T,
+  PVT_LAUNCH(group_scatter_kernel, dim3((T + 1023) / 1024), dim3(1024), 0, st, tg, keys, T,
                      G, cursor, skey, sidx);
 }
 // The grouped order's preparation in two one-block launches (rounds of at most PREP_T_MAX
@@ -1182,9 +1183,9 @@ __global__ __launch_bounds__(1024) void order_scatter_kernel(PrepArgs A) {
   }
 }
 void launch_order_prep(const PrepArgs& a, hipStream_t st, hipEvent_t counted, bool scatter) {
-  hipLaunchKernelGGL(order_count_kernel, dim3(1), dim3(1024), 0, st, a);
+  PVT_LAUNCH(order_count_kernel, dim3(1), dim3(1024), 0, st, a);
   if (counted) (void)hipEventRecord(counted, st);
-  if (scatter) hipLaunchKernelGGL(order_scatter_kernel, dim3(1), dim3(1024), 0, st, a);
+  if (scatter) PVT_LAUNCH(order_scatter_kernel, dim3(1), dim3(1024), 0, st, a);
 }
 
 // Sorts the n <= GSORT_MAX (key, task) pairs in LDS k / v by (key, task) ascending; on return
@@ -1314,6 +1315,69 @@ __global__ __launch_bounds__(1024) void group_sort_kernel(const int32_t* off, co
   for (int i = tid; i < n; i += blockDim.x) ord[a + i] = v[i];
 }
 
+// A block of the grouped order's launch that prebuilds the zero-cost window of zone j for the
+// round's first cost_aware best-fit epoch (ZoneWindows, pvt_kernels.h): the zero-cost masks
+// amask[a] = {z : csum[a][z] == 0} from the cost table itself (block g = 0 of the same launch
+// writes csum), the components by closure of that relation (csum is symmetric), and, when j is
+// its component's lowest zone and some group's anchor lies in the component, the first ZW_M
+// hosts of U = the union of those anchors' amask, compacted in LDS (the sort arrays, unused by
+// this block) and written with their zones and snapshot capacities.
+__device__ void zone_window_block(const PrepArgs& A, const GatherOut& O, int j, int32_t* lds) {
+  __shared__ uint32_t am[ZMAX], reach[ZMAX], gm_s;
+  __shared__ int32_t cnt[2][16], nw_s;
+  const int tid = threadIdx.x, Z = A.Z;
+  ZoneWindows* W = O.zwin;
+  if (tid < ZMAX) am[tid] = 0;
+  if (tid == 0) { gm_s = 0; nw_s = 0; }
+  __syncthreads();
+  for (int i = tid; i < Z * Z; i += 1024) {
+    const int a = i / Z, z = i - a * Z;
+    if (A.cost[a * Z + z] + A.cost[z * Z + a] == 0.0) atomicOr(&am[a], 1u << z);   // cost_aware.py:82
+  }
+  for (int g = tid; g < A.G; g += 1024) {
+    const int a = A.ganc[g];
+    if (a >= 0 && a < Z) atomicOr(&gm_s, 1u << a);
+  }
+  __syncthreads();
+  if (tid < Z) reach[tid] = am[tid] | (1u << tid);
+  __syncthreads();
+  for (int it = 0; it < 5; it++) {            // paths of up to 2^5 >= ZMAX zones
+    uint32_t r = 0;
+    if (tid < Z) {
+      r = reach[tid];
+      for (uint32_t m = r; m; m &= m - 1) r |= reach[__builtin_ctz(m)];
+    }
+    __syncthreads();
+    if (tid < Z) reach[tid] = r;
+    __syncthreads();
+  }
+  const uint32_t comp = reach[j];
+  uint32_t U = 0;
+  if ((comp & ((1u << j) - 1u)) == 0)         // j: the component's lowest zone
+    for (uint32_t m = comp & gm_s; m; m &= m - 1) U |= am[__builtin_ctz(m)];
+  if (tid == 0) W->U[j] = U;
+  if (U == 0) return;
+  int32_t* wid = lds;
+  int32_t* wz = lds + ZW_M;
+  compact_zone_window_t<ZW_M, 1024, 2>(O.zone, Z, U, 0, O.H, wid, wz, cnt, &nw_s);
+  const int n = nw_s;
+  ZoneWindow& w = W->w[j];
+  bool bad = false;
+  for (int p = tid; p < n; p += 1024) {
+    const int h = wid[p];
+    w.id[p] = h;
+    w.z[p] = wz[p];
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const double x = O.avail[(size_t)r * O.H + h];
+      bad |= !(__builtin_fabs(x) <= 0x1p500);
+      w.a[r][p] = x;
+    }
+  }
+  bad = __syncthreads_or(bad);
+  if (tid == 0) { w.n = n; w.bad = bad ? 1 : 0; }
+}
+
 #ifdef PVT_STAMPS
 __device__ __forceinline__ uint64_t gstamp() {
   uint64_t t;
@@ -1352,6 +1416,11 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
   uint64_t gph[4] = {0, 0, 0, 0}, gtl = 0;
   if (g == 0 && tid == 0) gtl = gstamp();
 #endif
+  const int nmin = O.hmin ? ZW_MIN_PARTS : 0;
+  if (g >= A.G + nmin) {                      // the first epoch's zero-cost windows
+    zone_window_block(A, O, g - A.G - nmin, reinterpret_cast<int32_t*>(k));
+    return;
+  }
   if (g >= A.G) {
     // blocks past the groups' blocks: the frontier walk's host minima, one of the ZW_MIN_PARTS partials
     // per block (the walk reduces them all, so the partition is free: four hosts per thread per
@@ -1468,13 +1537,13 @@ __global__ __launch_bounds__(1024) void group_sort_gather_kernel(PrepArgs A, Gat
 #endif
 }
 void launch_group_sort_gather(const PrepArgs& a, const GatherOut& o, hipStream_t st) {
-  const int extra = o.hmin ? ZW_MIN_PARTS : 0;
-  hipLaunchKernelGGL(group_sort_gather_kernel, dim3(1 + a.G + extra), dim3(1024), 0, st, a, o);
+  const int extra = (o.hmin ? ZW_MIN_PARTS : 0) + (o.zwin ? a.Z : 0);
+  PVT_LAUNCH(group_sort_gather_kernel, dim3(1 + a.G + extra), dim3(1024), 0, st, a, o);
 }
 void launch_group_sort(const int32_t* off, int G, const uint64_t* skey, const int32_t* sidx,
                        int32_t* ord, hipStream_t st) {
   // (1024 threads, the block's element layout above assumes it)
-  hipLaunchKernelGGL(group_sort_kernel, dim3(G), dim3(1024), 0, st, off, skey, sidx, ord);
+  PVT_LAUNCH(group_sort_kernel, dim3(G), dim3(1024), 0, st, off, skey, sidx, ord);
 }
 
 // pvt_restore_hosts: the listed hosts' four capacities from the pristine snapshot.
@@ -1489,7 +1558,7 @@ __global__ __launch_bounds__(256) void restore_hosts_kernel(double* avail, const
 }
 void launch_restore_hosts(double* avail, const double* avail0, int H, const int32_t* hosts, int n,
                           hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(restore_hosts_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, avail0, H, hosts, n);
+  if (n > 0) PVT_LAUNCH(restore_hosts_kernel, dim3((n + 255) / 256), dim3(256), 0, st, avail, avail0, H, hosts, n);
 }
 
 // Small host tables to the device through their mapped pinned pages, as a kernel on the stream:
@@ -1502,7 +1571,7 @@ void launch_upload(const void* src_mapped, void* dst, size_t bytes, hipStream_t 
   const int n16 = (int)((bytes + 15) / 16);
   if (n16 <= 0) return;
   const int blocks = std::min(64, (n16 + 255) / 256);
-  hipLaunchKernelGGL(upload_kernel, dim3(blocks), dim3(256), 0, st,
+  PVT_LAUNCH(upload_kernel, dim3(blocks), dim3(256), 0, st,
                      reinterpret_cast<const int4*>(src_mapped), reinterpret_cast<int4*>(dst), n16);
 }
 
@@ -1511,7 +1580,7 @@ __global__ void iota_kernel(int32_t* out, int n) {
   if (i < n) out[i] = i;
 }
 void launch_iota(int32_t* out, int n, hipStream_t st) {
-  hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out, n);
+  PVT_LAUNCH(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, out, n);
 }
 
 __global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const int32_t* tg,
@@ -1530,7 +1599,7 @@ __global__ void gather_tasks_kernel(const double* dem, const int32_t* ord, const
 void launch_gather_tasks(const double* dem, const int32_t* ord, const int32_t* task_group,
                          const int32_t* group_anchor, int T, double* dem_ord, int32_t* anc_ord,
                          int32_t* grp_ord, hipStream_t st, int G, int32_t* order_out) {
-  hipLaunchKernelGGL(gather_tasks_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, ord,
+  PVT_LAUNCH(gather_tasks_kernel, dim3((T + 255) / 256), dim3(256), 0, st, dem, ord,
                      task_group, group_anchor, T, dem_ord, anc_ord, grp_ord, G, order_out);
 }
 

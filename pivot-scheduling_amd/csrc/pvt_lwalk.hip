@@ -426,7 +426,7 @@ hipError_t lwalk_init_attrs() {
 }
 
 void launch_lwalk(const CommitArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(lwalk_kernel, dim3(1), dim3(WAVE), LWALK_LDS_BYTES, st, a);
+  PVT_LAUNCH(lwalk_kernel, dim3(1), dim3(WAVE), LWALK_LDS_BYTES, st, a);
 }
 
 }  // namespace pvt

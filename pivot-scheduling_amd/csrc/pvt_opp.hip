@@ -109,7 +109,7 @@ void launch_opp_count(const OppCountArgs& a0, hipStream_t st) {
   while (a.seg_q > 1 && (long long)tiles * ((nqr + a.seg_q - 1) / a.seg_q) < 2048) a.seg_q >>= 1;
   a.S = (nqr + a.seg_q - 1) / a.seg_q;
   (void)hipMemsetAsync(a.sc, 0, sizeof(int32_t) * (size_t)a.nt * a.lds, st);
-  hipLaunchKernelGGL(opp_count_kernel, dim3(tiles * a.S), dim3(256), 0, st, a);
+  PVT_LAUNCH(opp_count_kernel, dim3(tiles * a.S), dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -863,7 +863,7 @@ hipError_t opp_init_attrs() {
 }
 
 void launch_opp_commit(const OppCommitArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(opp_commit_kernel, dim3(1), dim3(OPP_NW * WAVE), sizeof(OppLDS), st, a);
+  PVT_LAUNCH(opp_commit_kernel, dim3(1), dim3(OPP_NW * WAVE), sizeof(OppLDS), st, a);
 }
 
 // Rank packages -> full tables: package r holds, task-major, the chunk bitmaps ([nt][ldq][4]
@@ -891,7 +891,7 @@ __global__ __launch_bounds__(256) void opp_unpack_kernel(OppUnpackArgs A) {
 }
 
 void launch_opp_unpack(const OppUnpackArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(opp_unpack_kernel, dim3(256, a.world), dim3(256), 0, st, a);
+  PVT_LAUNCH(opp_unpack_kernel, dim3(256, a.world), dim3(256), 0, st, a);
 }
 
 __global__ __launch_bounds__(256) void opp_apply_kernel(const OppTouched* t, double* avail, int H) {
@@ -904,7 +904,7 @@ __global__ __launch_bounds__(256) void opp_apply_kernel(const OppTouched* t, dou
 }
 
 void launch_opp_apply(const OppTouched* t, double* avail, int H, hipStream_t st) {
-  hipLaunchKernelGGL(opp_apply_kernel, dim3(OPP_MAXW / 256), dim3(256), 0, st, t, avail, H);
+  PVT_LAUNCH(opp_apply_kernel, dim3(OPP_MAXW / 256), dim3(256), 0, st, t, avail, H);
 }
 
 }  // namespace pvt

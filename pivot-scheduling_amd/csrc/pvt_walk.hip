@@ -940,10 +940,10 @@ void launch_commit_chains(const CommitArgs& a, int nchains, hipStream_t st) {
   const size_t lds = WALK_LDS_BYTES;
   const dim3 grid(nchains), block(WALK_THREADS);
   switch (a.mode) {
-    case CA_FF: hipLaunchKernelGGL(commit_kernel<CA_FF>, grid, block, lds, st, a); break;
-    case CA_BF: hipLaunchKernelGGL(commit_kernel<CA_BF>, grid, block, lds, st, a); break;
-    case VBP_FF: hipLaunchKernelGGL(commit_kernel<VBP_FF>, grid, block, lds, st, a); break;
-    case VBP_BF: hipLaunchKernelGGL(commit_kernel<VBP_BF>, grid, block, lds, st, a); break;
+    case CA_FF: PVT_LAUNCH(commit_kernel<CA_FF>, grid, block, lds, st, a); break;
+    case CA_BF: PVT_LAUNCH(commit_kernel<CA_BF>, grid, block, lds, st, a); break;
+    case VBP_FF: PVT_LAUNCH(commit_kernel<VBP_FF>, grid, block, lds, st, a); break;
+    case VBP_BF: PVT_LAUNCH(commit_kernel<VBP_BF>, grid, block, lds, st, a); break;
     default: break;
   }
 }

@@ -47,6 +47,7 @@
 #include "pivot_place.h"
 #include "pvt_device.h"
 #include "pvt_kernels.h"
+#include "pvt_zwin_dev.h"
 
 namespace pvt {
 
@@ -203,100 +204,13 @@ __device__ __forceinline__ void wave_lds_sync() {
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
-// The first WM hosts of [h_lo, h_hi), in index order, whose zone is in the mask U, appended
-// to wid / wz from *nwin on: passes of ZW_SCAN rows x 256 threads x 4 hosts (one 16-byte zone
-// load per thread and row, every load of a pass in flight at once, the next pass's issued before
-// this one is compacted), a stable block compaction (per row: a DPP scan of the threads' hit
-// counts, the waves' totals through LDS); the block stops at the pass that fills the window.
+// The first WM hosts of [h_lo, h_hi), in index order, whose zone is in the mask U
+// (pvt_zwin_dev.h, with this walk's workgroup and ZW_SCAN rows per pass).
 template <int WM = ZW_M>
 __device__ __forceinline__ void compact_zone_window(const int32_t* zone, int Z, uint32_t U,
                                                     int h_lo, int h_hi, int32_t* wid, int32_t* wz,
                                                     int32_t (*cnt)[ZW_WAVES], int32_t* nwin) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int SPAN = ZW_SCAN * ZW_THREADS * 4;
-  const int a_lo = h_lo & ~3;
-  // (16-byte loads need a 16-byte aligned zone array: a caller's offset pointer takes the
-  // element loads, as does the last partial quad)
-  const bool vec = ((uintptr_t)zone & 15) == 0;
-  auto load = [&](int hb) -> int4 {
-    if (vec && hb + 4 <= h_hi) return *reinterpret_cast<const int4*>(zone + hb);
-    int4 r;
-    r.x = hb < h_hi ? zone[hb] : -1;
-    r.y = hb + 1 < h_hi ? zone[hb + 1] : -1;
-    r.z = hb + 2 < h_hi ? zone[hb + 2] : -1;
-    r.w = hb + 3 < h_hi ? zone[hb + 3] : -1;
-    return r;
-  };
-  int4 zz[ZW_SCAN];
-#pragma unroll
-  for (int k = 0; k < ZW_SCAN; k++) zz[k] = load(a_lo + (k * ZW_THREADS + tid) * 4);
-  for (int h0 = a_lo; h0 < h_hi; h0 += SPAN) {
-    const int have = *nwin;
-    if (have >= WM) break;
-    int4 zn[ZW_SCAN];                        // the next pass's zones, in flight during this one
-    if (h0 + SPAN < h_hi) {
-#pragma unroll
-      for (int k = 0; k < ZW_SCAN; k++) zn[k] = load(h0 + SPAN + (k * ZW_THREADS + tid) * 4);
-    }
-    uint32_t hm[ZW_SCAN];                    // per row: bit c = host hb + c is a window host
-    int ex[ZW_SCAN];                         //   its hits before this thread's, in the wave
-#pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) {
-      const int hb = h0 + (k * ZW_THREADS + tid) * 4;
-      const int zc[4] = {zz[k].x, zz[k].y, zz[k].z, zz[k].w};
-      uint32_t m = 0;
-#pragma unroll
-      for (int c = 0; c < 4; c++)
-        m |= (hb + c >= h_lo && zc[c] >= 0 && zc[c] < Z && ((U >> zc[c]) & 1u)) ? (1u << c) : 0u;
-      hm[k] = m;
-      const int n = __popc(m);
-      const int incl = wave_incl_scan_dpp(n);
-      ex[k] = incl - n;
-      const int tot = __builtin_amdgcn_readlane(incl, 63);
-      if (lane == 0) cnt[k][wave] = tot;
-    }
-    __syncthreads();
-    // every row's counts read before any window store (the stores may alias cnt for the
-    // compiler, which then re-read it after each one: a serial LDS chain per pass)
-    int before[ZW_SCAN], rowtot[ZW_SCAN];
-#pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) {
-      int bf = 0, tt = 0;
-#pragma unroll
-      for (int w = 0; w < ZW_WAVES; w++) {
-        const int c = cnt[k][w];
-        bf += (w < wave) ? c : 0;
-        tt += c;
-      }
-      before[k] = bf;
-      rowtot[k] = tt;
-    }
-    int pre = have;
-#pragma unroll
-    for (int k = 0; k < ZW_SCAN; k++) {
-      const int hb = h0 + (k * ZW_THREADS + tid) * 4;
-      const int zc[4] = {zz[k].x, zz[k].y, zz[k].z, zz[k].w};
-      int pos = pre + before[k] + ex[k];
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        if ((hm[k] >> c) & 1u) {
-          if (pos < WM) {
-            wid[pos] = hb + c;
-            if (wz) wz[pos] = zc[c];
-          }
-          pos++;
-        }
-      }
-      pre += rowtot[k];
-    }
-    __syncthreads();
-    if (tid == 0) *nwin = min(pre, WM);
-    __syncthreads();
-    if (h0 + SPAN < h_hi) {
-#pragma unroll
-      for (int k = 0; k < ZW_SCAN; k++) zz[k] = zn[k];
-    }
-  }
+  compact_zone_window_t<WM, ZW_THREADS, ZW_SCAN>(zone, Z, U, h_lo, h_hi, wid, wz, cnt, nwin);
 }
 
 #ifdef PVT_STAMPS
@@ -328,9 +242,19 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   uint64_t n_cf = 0;                                              // runs counted in closed form
 #endif
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int base = KEYED ? 0 : A.coff[b];
-  const int nt = KEYED ? A.knt : A.coff[b + 1] - base;
-  const int32_t* cmap = KEYED ? nullptr : A.cmap + base;
+  // chain tables: by value in the arguments (A.tab; the host sends them only for chains of at
+  // most CHAIN_MAX tasks, as the epoch planner builds them), or device arrays (uploaded)
+  const bool tabm = !KEYED && A.tab.nch > 0;
+  const int base = KEYED ? 0 : tabm ? A.tab.coff[b] : A.coff[b];
+  const int nt = KEYED ? A.knt : tabm ? A.tab.coff[b + 1] - A.tab.coff[b] : A.coff[b + 1] - base;
+  // chain-local position -> epoch task (A.cmap, global): with the tables by value, this block
+  // writes its chain's range of it from the segments first (read back by the same block after the
+  // barrier below). (Neither a map in LDS -- the select between an LDS and a global map became a
+  // flat load per access -- nor one computed from the segments per access: the walk ran 4-7 %
+  // slower either way.)
+  const int32_t* gcmap = KEYED ? nullptr : A.cmap + base;
+  auto cmap_at = [&](int i) -> int { return gcmap[i]; };
+  const bool segm = !KEYED && (tabm || A.cseg);   // group segment starts break runs
   int32_t* status = A.status + 2 * b;
   const int Z = A.Z, H = A.H;
 
@@ -355,13 +279,35 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       ha[r] = FF ? nan_max(ha[r], x) : fmin(ha[r], x);
     }
   }
-  int wv[ZW_PR];
-#pragma unroll
-  for (int u = 0; u < ZW_PR; u++) {
-    const int i = u * ZW_THREADS + tid;
-    wv[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
+  if (tabm) {
+    int32_t* wmap = const_cast<int32_t*>(A.cmap) + base;
+    for (int k = A.tab.csoff[b]; k < A.tab.csoff[b + 1]; k++) {
+      const int sg = A.tab.csegid[k], c0 = A.tab.seg_cstart[sg], o0 = A.tab.seg_off[sg];
+      const int len = A.tab.seg_off[sg + 1] - o0;
+      for (int i = tid; i < len; i += ZW_THREADS) wmap[c0 + i] = o0 + i;
+    }
+    // block 0 publishes the tables for the epoch kernels after the walk
+    if (b == 0) {
+      const int ns = A.tab.nseg, nc = A.tab.nch;
+      for (int i = tid; i <= ns; i += ZW_THREADS) {
+        A.tab.o_seg_off[i] = A.tab.seg_off[i];
+        if (i < ns) { A.tab.o_seg_chain[i] = A.tab.seg_chain[i]; A.tab.o_seg_cstart[i] = A.tab.seg_cstart[i]; }
+      }
+      for (int i = tid; i <= nc; i += ZW_THREADS) A.tab.o_coff[i] = A.tab.coff[i];
+    }
   }
-  const int sg0 = (!KEYED && A.cseg) ? A.csoff[b] : 0, sg1 = (!KEYED && A.cseg) ? A.csoff[b + 1] : 0;
+  int wv[ZW_PR];
+  if (!tabm) {
+#pragma unroll
+    for (int u = 0; u < ZW_PR; u++) {
+      const int i = u * ZW_THREADS + tid;
+      wv[u] = i < nt ? (KEYED ? i : gcmap[i]) : -1;
+    }
+  }
+  const int sg0 = tabm ? A.tab.csoff[b] : (!KEYED && A.cseg) ? A.csoff[b] : 0;
+  const int sg1 = tabm ? A.tab.csoff[b + 1] : (!KEYED && A.cseg) ? A.csoff[b + 1] : 0;
+  // prebuilt windows' zone sets (ZoneWindows; lane j: zone j's, 0 = none)
+  const uint32_t zpu = (!KEYED && WM == ZW_M && A.zpre && lane < Z) ? A.zpre->U[lane] : 0u;
 
 #pragma unroll
   for (int u = 0; u < 4; u++) {
@@ -376,9 +322,23 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     for (int z = 0; z < Z; z++) m |= (S.csum[tid * Z + z] == 0.0) ? (1u << z) : 0u;
     S.amask[tid] = m;
   }
-  for (int k = sg0 + tid; k < sg1; k += ZW_THREADS) {   // segment starts (chain-local positions)
-    const int p = A.cseg[k];
-    if (p > 0 && p < CHAIN_MAX) atomicOr(&S.sbits[p >> 6], 1ull << (p & 63));
+  if (tabm) {                                // (the map this block wrote before the barrier)
+#pragma unroll
+    for (int u = 0; u < ZW_PR; u++) {
+      const int i = u * ZW_THREADS + tid;
+      wv[u] = i < nt ? gcmap[i] : -1;
+    }
+  }
+  if (tabm) {                                // segment starts (chain-local positions)
+    for (int k = sg0 + tid; k < sg1; k += ZW_THREADS) {
+      const int p = A.tab.seg_cstart[A.tab.csegid[k]];
+      if (p > 0 && p < CHAIN_MAX) atomicOr(&S.sbits[p >> 6], 1ull << (p & 63));
+    }
+  } else {
+    for (int k = sg0 + tid; k < sg1; k += ZW_THREADS) {
+      const int p = A.cseg[k];
+      if (p > 0 && p < CHAIN_MAX) atomicOr(&S.sbits[p >> 6], 1ull << (p & 63));
+    }
   }
 
   // the chain's anchors (-> its zones U below), demand extremes and finiteness (certificates 2,
@@ -401,7 +361,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #pragma unroll
     for (int u = 0; u < ZW_PR; u++) {
       const int i = i0 + ZW_PR * ZW_THREADS + u * ZW_THREADS + tid;
-      wn[u] = i < nt ? (KEYED ? i : cmap[i]) : -1;
+      wn[u] = i < nt ? (KEYED ? i : cmap_at(i)) : -1;
     }
 #pragma unroll
     for (int u = 0; u < ZW_PR; u++) {
@@ -477,12 +437,24 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 #pragma unroll
     for (int r = 0; r < 4; r++) sep |= (ha[r] - mx[r] >= 0x1p-288);
   }
-  const uint32_t U = S.umask;
+  uint32_t U = S.umask;
   if (S.bail || !sep || nt <= 0 || (!KEYED && nt > CHAIN_MAX)) {
     if (tid == 0) { status[0] = 0; status[1] = (KEYED || nt <= 0) ? 0 : 1; }
     return;
   }
   const FrontierSlot* pw = A.pwin ? A.pwin + (KEYED ? 0 : b) : nullptr;
+  // the round's first epoch: the window the grouped order's launch prebuilt for the component of
+  // the chain's anchors (its zone set U' covers U; a window over U' is exact, with U' in the
+  // certificates)
+  const ZoneWindow* zw = nullptr;
+  if (!KEYED && WM == ZW_M && !pw && A.zpre && U != 0) {
+    const uint64_t cover = __ballot(zpu != 0 && (U & ~zpu) == 0);
+    if (cover) {
+      const int j = __builtin_ctzll(cover);
+      zw = &A.zpre->w[j];
+      U = (uint32_t)__builtin_amdgcn_readlane((int)zpu, j);
+    }
+  }
   if (pw) {                                  // host-sharded: the merged window, capacities too
     const int nw = min(pw->n, ZW_M);
     for (int p = tid; p < nw; p += ZW_THREADS) {
@@ -490,6 +462,11 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       S.wid[p] = h;
       S.wz[p] = KEYED ? 0 : A.zone[h];
     }
+    if (tid == 0) S.nwin = nw;
+    __syncthreads();
+  } else if (zw) {                           // prebuilt: ids and zones (capacities below)
+    const int nw = min(zw->n, ZW_M);
+    for (int p = tid; p < nw; p += ZW_THREADS) { S.wid[p] = zw->id[p]; S.wz[p] = zw->z[p]; }
     if (tid == 0) S.nwin = nw;
     __syncthreads();
   } else if (KEYED) {                        // window: the zero-key prefix's first hosts
@@ -514,7 +491,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       const int h = p < nwin ? S.wid[p] : 0;   // (host 0: a valid address, never used)
 #pragma unroll
       for (int r = 0; r < 4; r++)
-        v[u][r] = p >= nwin ? 0.0 : (pw ? pw->a[r][p] : A.avail[(size_t)r * H + h]);
+        v[u][r] = p >= nwin ? 0.0 : (pw ? pw->a[r][p] : zw ? zw->a[r][p] : A.avail[(size_t)r * H + h]);
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -545,7 +522,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     const int i1 = blk == ZW_SB - 1 ? nt : min(nt, blk * 64 + 64);
     double bm[4] = {DINF, DINF, DINF, DINF};
     for (int i = blk * 64 + lane; i < i1; i += 64) {
-      const int w = KEYED ? i : cmap[i];
+      const int w = KEYED ? i : cmap_at(i);
 #pragma unroll
       for (int r = 0; r < 4; r++) bm[r] = fmin(bm[r], A.dem[(size_t)w * 4 + r]);
     }
@@ -792,7 +769,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   // task records, software-pipelined across 64-task batches: while batch b is walked, batch
   // b + 1's records and batch b + 2's chain positions are in flight (no HBM latency at a batch
   // start)
-  auto task_at = [&](int i) { return i < nt ? (KEYED ? i : cmap[i]) : 0; };
+  auto task_at = [&](int i) { return i < nt ? (KEYED ? i : cmap_at(i)) : 0; };
   int nw = task_at(lane);
   double nd0 = A.dem[(size_t)nw * 4 + 0], nd1 = A.dem[(size_t)nw * 4 + 1];
   double nd2 = A.dem[(size_t)nw * 4 + 2], nd3 = A.dem[(size_t)nw * 4 + 3];
@@ -831,7 +808,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
       E = __ballot(same);
       // (chain mode: a run stops at a group segment start -- pass 2 logs a host's capacities
       // at its last copy of the run only, and the segment before must hold its own last copy)
-      if (!KEYED && A.cseg) E &= ~rfl_u64(S.sbits[i0 >> 6]);
+      if (segm) E &= ~rfl_u64(S.sbits[i0 >> 6]);
     }
     // A run that reaches the end of a full batch goes on into the next one while those tasks
     // have the same demand vector and anchor and no segment starts (their records are already in
@@ -850,7 +827,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
                     __double_as_longlong(nd1) == __double_as_longlong(l1) &&
                     __double_as_longlong(nd2) == __double_as_longlong(l2) &&
                     __double_as_longlong(nd3) == __double_as_longlong(l3);
-          if (!KEYED && A.cseg) eq = eq && !((rfl_u64(S.sbits[(i0 >> 6) + 1]) >> lane) & 1ull);
+          if (segm) eq = eq && !((rfl_u64(S.sbits[(i0 >> 6) + 1]) >> lane) & 1ull);
           const uint64_t m = __ballot(eq);
           extc = m == ~0ull ? 64 : __builtin_ctzll(~m);
         }
@@ -1230,17 +1207,17 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
 }
 
 void launch_host_min(const double* avail, int H, int lo, int hi, double* part, hipStream_t st) {
-  hipLaunchKernelGGL(host_min_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, lo, hi, part);
+  PVT_LAUNCH(host_min_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, lo, hi, part);
 }
 
 void launch_zwalk(const ZwalkArgs& a, int nchains, hipStream_t st) {
-  hipLaunchKernelGGL((zwalk_kernel<false, false>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+  PVT_LAUNCH((zwalk_kernel<false, false>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
 }
 void launch_zwalk_big(const ZwalkArgs& a, int nchains, hipStream_t st) {
-  hipLaunchKernelGGL((zwalk_kernel<false, false, false, ZW_MBIG>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+  PVT_LAUNCH((zwalk_kernel<false, false, false, ZW_MBIG>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
 }
 void launch_zwalk_ff(const ZwalkArgs& a, int nchains, hipStream_t st) {
-  hipLaunchKernelGGL((zwalk_kernel<false, true, true>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+  PVT_LAUNCH((zwalk_kernel<false, true, true>), dim3(nchains), dim3(ZW_THREADS), 0, st, a);
 }
 
 // Per-dimension maxima of |avail| over hosts [lo, hi) (the FF walk's certificate 2'), in
@@ -1268,11 +1245,11 @@ __global__ __launch_bounds__(256) void host_absmax_kernel(const double* avail, i
   }
 }
 void launch_host_absmax(const double* avail, int H, int lo, int hi, double* part, hipStream_t st) {
-  hipLaunchKernelGGL(host_absmax_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, lo, hi, part);
+  PVT_LAUNCH(host_absmax_kernel, dim3(ZW_MINB), dim3(256), 0, st, avail, H, lo, hi, part);
 }
 void launch_zwalk_keyed(const ZwalkArgs& a, bool strict, hipStream_t st) {
-  if (strict) hipLaunchKernelGGL((zwalk_kernel<true, true>), dim3(1), dim3(ZW_THREADS), 0, st, a);
-  else hipLaunchKernelGGL((zwalk_kernel<true, false>), dim3(1), dim3(ZW_THREADS), 0, st, a);
+  if (strict) PVT_LAUNCH((zwalk_kernel<true, true>), dim3(1), dim3(ZW_THREADS), 0, st, a);
+  else PVT_LAUNCH((zwalk_kernel<true, false>), dim3(1), dim3(ZW_THREADS), 0, st, a);
 }
 
 // Ordered frontier: the smallest demand (per dimension) of tasks [0, n), then the hosts that
@@ -1307,9 +1284,9 @@ __global__ void alive_flags_kernel(const double* avail, int H, int lo, int hs, c
 }
 void launch_alive_flags(const double* avail, int H, int lo, int hs, const double* dem, int n,
                         int strict, double* dmin, uint8_t* flags, hipStream_t st) {
-  hipLaunchKernelGGL(dem_min_kernel, dim3(1), dim3(1024), 0, st, dem, n, dmin);
+  PVT_LAUNCH(dem_min_kernel, dim3(1), dim3(1024), 0, st, dem, n, dmin);
   if (hs <= lo) return;
-  hipLaunchKernelGGL(alive_flags_kernel, dim3((hs - lo + 255) / 256), dim3(256), 0, st, avail, H,
+  PVT_LAUNCH(alive_flags_kernel, dim3((hs - lo + 255) / 256), dim3(256), 0, st, avail, H,
                      lo, hs, dmin, strict, flags);
 }
 
@@ -1401,15 +1378,15 @@ __global__ __launch_bounds__(256) void zwin_merge_kernel(const uint8_t* pkgs, in
 }
 
 void launch_zwin_build(const ZwinArgs& a, int nchains, hipStream_t st) {
-  hipLaunchKernelGGL(zwin_build_kernel, dim3(nchains), dim3(ZW_THREADS), 0, st, a);
+  PVT_LAUNCH(zwin_build_kernel, dim3(nchains), dim3(ZW_THREADS), 0, st, a);
 }
 void launch_zwin_gather(const double* avail, int H, int lo, const int32_t* perm,
                         const int32_t* count, FrontierSlot* out, hipStream_t st) {
-  hipLaunchKernelGGL(zwin_gather_kernel, dim3(1), dim3(256), 0, st, avail, H, lo, perm, count, out);
+  PVT_LAUNCH(zwin_gather_kernel, dim3(1), dim3(256), 0, st, avail, H, lo, perm, count, out);
 }
 void launch_zwin_merge(const uint8_t* pkgs, int64_t pkg_bytes, int world, int nslots,
                        FrontierSlot* out, double* hmin, hipStream_t st) {
-  hipLaunchKernelGGL(zwin_merge_kernel, dim3(nslots + 1), dim3(256), 0, st, pkgs, pkg_bytes, world,
+  PVT_LAUNCH(zwin_merge_kernel, dim3(nslots + 1), dim3(256), 0, st, pkgs, pkg_bytes, world,
                      nslots, out, hmin);
 }
 

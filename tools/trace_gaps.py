@@ -2,7 +2,9 @@
 """Diagnostic: the device timeline of a `rocprofv3 --kernel-trace --output-format csv` run --
 busy time vs span and the largest idle gaps between consecutive kernels (with the kernels on
 either side), over the last N ms of the trace (the timed steps).
-usage: trace_gaps.py KERNEL_TRACE_CSV [LAST_MS] [TOP]"""
+usage: trace_gaps.py KERNEL_TRACE_CSV [LAST_MS] [TOP] [END_KERNEL]
+END_KERNEL: the window ends at the last launch of the kernel whose name contains it (skips what
+runs after the timed steps, e.g. the parity check's copies)."""
 import csv
 import sys
 from collections import defaultdict
@@ -15,6 +17,10 @@ with open(path) as f:
     for r in csv.DictReader(f):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0]))
 rows.sort()
+end_k = sys.argv[4] if len(sys.argv) > 4 else None
+if end_k:
+    last = max((i for i, r in enumerate(rows) if end_k in r[2]), default=len(rows) - 1)
+    rows = rows[:last + 1]
 if last_ms > 0 and rows:
     t_end = max(e for _, e, _ in rows)
     rows = [r for r in rows if r[0] >= t_end - last_ms * 1e6]
