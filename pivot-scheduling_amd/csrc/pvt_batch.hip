@@ -51,6 +51,7 @@ constexpr uint64_t NONE = ~0ull;
 
 // Diagnostic phase stamps (PVT_STAMPS builds; tools/resident_stamps.py): block 0, wave 0 only.
 #ifdef PVT_STAMPS
+constexpr int RES_STAMP_BASE = 32, RES_STAMP_ROUNDS = 4096;   // per-round cycles (stamps build)
 __device__ __forceinline__ uint64_t rstamp() {
   uint64_t t;
   __builtin_amdgcn_sched_barrier(0);
@@ -171,7 +172,7 @@ __device__ void res_order(const pvt_round& R, bool grouped, bool sorted, uint64_
 template <int NT>
 __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, const int32_t* ord,
                              int32_t* pl, const double* csum, const double* bsum, bool has_groups,
-                             int walker, uint64_t* A_stamps) {
+                             int walker, bool bulk, uint64_t* A_stamps) {
   __shared__ int s_stop;
   const int T = R.n_tasks, H = R.n_hosts, Z = R.n_zones;
   const int tid = threadIdx.x, lane = lane_id();
@@ -213,7 +214,7 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   __syncthreads();
   if (wave == walker) {
 #ifdef PVT_STAMPS
-    uint64_t n_probe = 0, n_adv = 0, st_task = 0;
+    uint64_t n_probe = 0, n_adv = 0, st_task = 0, n_bulk = 0, n_bulk_tasks = 0;
     const uint64_t tw_start = rstamp();
 #endif
     const int nch = (H + 63) >> 6;
@@ -332,6 +333,19 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       if (b + 1 < nsb) rec(b + 1, nd, nanc);
       const double mn0 = ws[b * 4 + 0], mn1 = ws[b * 4 + 1], mn2 = ws[b * 4 + 2], mn3 = ws[b * 4 + 3];
       const int kn = min(64, T - b * 64);
+      // runs: bit i set iff batch task i has task i - 1's demand vector (bit for bit) and anchor
+      // (every shuffle with the whole wave active: a lane that skipped one, by short-circuit, would
+      // hand its neighbour a zero -- an anchor 0 run that is not one)
+      uint64_t E;
+      {
+        const int pa = __shfl_up(tanc, 1);
+        bool same = lane > 0 && lane < kn;
+        same &= pa == tanc;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          same &= __double_as_longlong(__shfl_up(td[r], 1)) == __double_as_longlong(td[r]);
+        E = __ballot(same);
+      }
       for (int k = 0; k < kn; k++, p++) {
 #ifdef PVT_STAMPS
         const uint64_t tk0 = rstamp();
@@ -360,6 +374,78 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
         if ((nonfin >> k) & 1ull) {
           stop = true;                         // (a non-finite demand: the 4-wave path decides)
           break;
+        }
+        // A run of R >= 2 tasks with this demand (and anchor) on the dense register chunk
+        // (run_bulk, as the frontier walk's, pvt_zwalk.hip): sequentially the run fills the
+        // chunk's fitting lanes in index order, each until it cannot take another copy (d >= 0:
+        // a lane that fails a copy fails every later one, one that does not fit now never will),
+        // so every lane counts its copies in parallel, the lanes take the run's tasks in order
+        // and replay exactly their own subtractions. Taken only when the first task's winner is
+        // in the chunk and no fitting lane holds a capacity above 2^500 (the per-task stop).
+        if (bulk && dense && k + 1 < kn && ((E >> (k + 1)) & 1ull) && d0 >= 0.0 && d1 >= 0.0 &&
+            d2 >= 0.0 && d3 >= 0.0) {
+          const uint64_t m0 = __ballot(rv && ra0 >= d0 && ra1 >= d1 && ra2 >= d2 && ra3 >= d3);
+          const uint64_t big = __ballot(rv && !(ra0 <= 0x1p+500 && ra1 <= 0x1p+500 &&
+                                                ra2 <= 0x1p+500 && ra3 <= 0x1p+500));
+          if (m0 != 0 && (m0 & big) == 0) {
+            const int R = min(kn - k, 1 + (int)__builtin_ctzll(~(E >> (k + 1))));
+            const bool on = (m0 >> lane) & 1ull;
+            double x0 = on ? ra0 : -DINF, x1 = on ? ra1 : -DINF, x2 = on ? ra2 : -DINF, x3 = on ? ra3 : -DINF;
+            int cnt = 0, t = 0, u = __builtin_ctzll(m0), fb = 0;
+            for (;;) {
+              t = __builtin_amdgcn_readfirstlane(t);
+              u = __builtin_amdgcn_readfirstlane(u);
+              fb = __builtin_amdgcn_readfirstlane(fb);
+              bool f = false;
+#pragma unroll
+              for (int j = 1; j <= 8; j++) {
+                x0 -= d0; x1 -= d1; x2 -= d2; x3 -= d3;
+                f = fmin(fmin(x0, x1), fmin(x2, x3)) >= 0.0;   // (x_{j-1} >= d iff x_j >= 0)
+                cnt = f ? t + j : cnt;
+              }
+              t += 8;
+              const uint64_t an = __ballot(f);
+              if (__builtin_amdgcn_readfirstlane((int)(an == 0))) break;
+              const int un = __builtin_ctzll(an);
+              if (un != u) {                   // (lanes below un are done)
+                u = un;
+                fb = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cnt), u - 1);
+              }
+              if (__builtin_amdgcn_readfirstlane((int)(fb + t >= R))) break;
+            }
+            const int incl = wave_incl_scan_dpp(cnt);
+            const int pre = incl - cnt;
+            const int asg = max(0, min(cnt, R - pre));
+            const int covered = min(R, __builtin_amdgcn_readlane(incl, 63));
+            // positions p .. p + covered - 1 to their hosts (a few taking lanes)
+            int who = 0;
+            for (uint64_t tk = __ballot(asg > 0); tk; tk &= tk - 1) {
+              const int L = __builtin_ctzll(tk);
+              const int s0 = __builtin_amdgcn_readlane(pre, L), s1 = s0 + __builtin_amdgcn_readlane(asg, L);
+              const int id = __builtin_amdgcn_readlane(rid, L);
+              if (lane >= s0 && lane < s1) who = id;
+            }
+            if (lane < covered) pl[p + lane] = who;
+            // replay: each taking lane's own subtractions, in order (fma(-0, d, c) == c)
+            const int amax = wave_max_i32(asg);
+            for (int m = 0; m < amax; m++) {
+              const double o = m < asg ? -1.0 : -0.0;
+              ra0 = __builtin_fma(o, d0, ra0);
+              ra1 = __builtin_fma(o, d1, ra1);
+              ra2 = __builtin_fma(o, d2, ra2);
+              ra3 = __builtin_fma(o, d3, ra3);
+            }
+#ifdef PVT_STAMPS
+            n_bulk++;
+            n_bulk_tasks += covered;
+#endif
+            k += covered - 1;                  // (the loop's increments add the last one)
+            p += covered - 1;
+#ifdef PVT_STAMPS
+            st_task += rstamp() - tk0;
+#endif
+            continue;
+          }
         }
         // Fast path, in lane masks (SALU), on the register chunk: C = fitting hosts of safe
         // zero-cost zones; its first, w, wins -- exactly the test below -- unless (a) a fitting
@@ -512,6 +598,8 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
       A_stamps[10] += n_probe;
       A_stamps[11] += n_adv;
       A_stamps[13] += st_task;                  // cycles inside the task loop bodies
+      A_stamps[24] += n_bulk;                   // bulk runs and the tasks they placed
+      A_stamps[25] += n_bulk_tasks;
       A_stamps[14] += rstamp() - tw_start;      // wave 0's whole walk (records included)
     }
 #endif
@@ -597,8 +685,10 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
 #endif
     // the walking wave: 0, or (A.walk == 2, A/B) one that moves with the workgroup index, so
     // two workgroups sharing a CU need not walk on the same SIMD
-    const int walker = A.walk == 2 ? (int)(blockIdx.x % (unsigned)WAVES) : 0;
-    p_start = resident_walk<NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, walker, A.stamps);
+    // (A.walk & 4: no bulk runs in the walk, A/B)
+    const int walker = (A.walk & 3) == 2 ? (int)(blockIdx.x % (unsigned)WAVES) : 0;
+    p_start = resident_walk<NT>(R, Lo, smem, ord, pl, csum, bsum, has_groups, walker,
+                                (A.walk & 4) == 0, A.stamps);
 #ifdef PVT_STAMPS
     if (blockIdx.x == 0 && tid == 0 && A.stamps) {   // walked tasks, walk cycles (block 0)
       A.stamps[8] += (uint64_t)p_start;
@@ -1040,7 +1130,15 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
 template <int MODE, int WAVES, int HPL>
 __global__ __launch_bounds__(WAVES * WAVE) void resident_kernel(ResidentArgs A) {
   const pvt_round R = reinterpret_cast<const pvt_round*>(A.rounds)[blockIdx.x];   // SGPRs
+#ifdef PVT_STAMPS
+  // per round (diagnostic): cycles of the whole workgroup, from its start to its end
+  const uint64_t t_round = rstamp();
+#endif
   resident_round<MODE, WAVES, HPL>(A, R);
+#ifdef PVT_STAMPS
+  if (threadIdx.x == 0 && A.stamps && blockIdx.x < RES_STAMP_ROUNDS)
+    A.stamps[RES_STAMP_BASE + blockIdx.x] = rstamp() - t_round;
+#endif
 }
 
 // A batch of rounds of different policies in one launch (pvt_place_host_batch: the lock-step

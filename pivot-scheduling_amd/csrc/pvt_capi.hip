@@ -588,13 +588,15 @@ extern "C" int pvt_last_stats(pvt_ctx* ctx, int64_t* windows, int64_t* refills) 
 extern "C" int pvt_debug_commit_stamps(pvt_ctx* ctx, uint64_t* out, int n) {
   if (!ctx || !out || n < 8) return PVT_EINVAL;
 #ifdef PVT_STAMPS
+  // 32 counters, then per-round cycles of the resident kernel (4096 rounds)
+  constexpr int NW = 32 + 4096;
   if (!ctx->stamps) {
-    if (hipMalloc((void**)&ctx->stamps, 256) != hipSuccess) return PVT_ENOMEM;
-    (void)hipMemset(ctx->stamps, 0, 256);
-    std::memset(out, 0, sizeof(uint64_t) * std::min(n, 32));
+    if (hipMalloc((void**)&ctx->stamps, sizeof(uint64_t) * NW) != hipSuccess) return PVT_ENOMEM;
+    (void)hipMemset(ctx->stamps, 0, sizeof(uint64_t) * NW);
+    std::memset(out, 0, sizeof(uint64_t) * std::min(n, NW));
     return PVT_OK;
   }
-  if (hipMemcpy(out, ctx->stamps, sizeof(uint64_t) * std::min(n, 32), hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(out, ctx->stamps, sizeof(uint64_t) * std::min(n, NW), hipMemcpyDeviceToHost) != hipSuccess)
     return PVT_EHIP;
   return PVT_OK;
 #else

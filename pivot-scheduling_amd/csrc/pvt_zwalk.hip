@@ -249,7 +249,7 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
   const int nt = KEYED ? A.knt : tabm ? A.tab.coff[b + 1] - A.tab.coff[b] : A.coff[b + 1] - base;
   // chain-local position -> epoch task (A.cmap, global): with the tables by value, this block
   // writes its chain's range of it from the segments first (read back by the same block after the
-  // barrier below). (Neither a map in LDS -- the select between an LDS and a global map became a
+  // barrier below; the prologue's first positions come from the segments directly). (Neither a map in LDS -- the select between an LDS and a global map became a
   // flat load per access -- nor one computed from the segments per access: the walk ran 4-7 %
   // slower either way.)
   const int32_t* gcmap = KEYED ? nullptr : A.cmap + base;
@@ -297,7 +297,21 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     }
   }
   int wv[ZW_PR];
-  if (!tabm) {
+  if (tabm) {
+    // the first positions straight from the segments (no dependent load of the map before the
+    // demand rows: one HBM latency less in the prologue)
+    const int k0 = A.tab.csoff[b], k1 = A.tab.csoff[b + 1];
+#pragma unroll
+    for (int u = 0; u < ZW_PR; u++) {
+      const int i = u * ZW_THREADS + tid;
+      int v = -1;
+      for (int k = k0; k < k1; k++) {
+        const int sg = A.tab.csegid[k], c0 = A.tab.seg_cstart[sg];
+        if (i >= c0) v = A.tab.seg_off[sg] + (i - c0);
+      }
+      wv[u] = i < nt ? v : -1;
+    }
+  } else {
 #pragma unroll
     for (int u = 0; u < ZW_PR; u++) {
       const int i = u * ZW_THREADS + tid;
@@ -321,13 +335,6 @@ __global__ __launch_bounds__(ZW_THREADS) void zwalk_kernel(ZwalkArgs A) {
     uint32_t m = 0;
     for (int z = 0; z < Z; z++) m |= (S.csum[tid * Z + z] == 0.0) ? (1u << z) : 0u;
     S.amask[tid] = m;
-  }
-  if (tabm) {                                // (the map this block wrote before the barrier)
-#pragma unroll
-    for (int u = 0; u < ZW_PR; u++) {
-      const int i = u * ZW_THREADS + tid;
-      wv[u] = i < nt ? gcmap[i] : -1;
-    }
   }
   if (tabm) {                                // segment starts (chain-local positions)
     for (int k = sg0 + tid; k < sg1; k += ZW_THREADS) {

@@ -174,3 +174,36 @@ def test_zero_cost_window_certificates(engine, engine_nowalk):
             r.avail[0] = np.minimum(r.avail[0], 2.0)
         rounds.append(r)
     _check(engine, engine_nowalk, rounds, "zero-cost window certificates")
+
+
+def test_bulk_runs_in_the_walk(engine, engine_nowalk):
+    """Runs of equal demands placed in one step on the walk's register chunk (every fitting lane
+    counts its copies, the lanes take the run in order and replay their subtractions): runs of up
+    to a whole batch over hosts that take an exact number of copies, demands that are not exactly
+    representable (0.1 cpus: the copy counts come from the sequential roundings), all-zero demand
+    rows (a lane takes every copy), and hosts above 2^500 (no bulk step, the per-task stop; below
+    ~1e154, where a zero-cost score would be 0 * inf)."""
+    rounds = []
+    for s in range(6):
+        r = synthetic.make_round(_abi.PVT_CA_BF, 900, 1500, seed=220 + s)
+        rs = np.random.RandomState(300 + s)
+        if s in (0, 1):
+            rows = np.array([[0.5, 2048.0], [1.0, 4096.0], [0.25, 1024.0]])
+            pick = np.sort(rs.randint(0, 3, size=r.n_tasks))
+            r.dem[0], r.dem[1] = rows[pick, 0], rows[pick, 1]
+            r.avail[0] = 0.5 * rs.randint(0, 40, size=r.n_hosts)
+            r.avail[1] = 2048.0 * rs.randint(0, 40, size=r.n_hosts)
+        elif s == 2:
+            r.dem[0] = 0.1
+            r.dem[1] = 0.3 * 1024.0
+            r.avail[0] = 0.1 * rs.randint(1, 30, size=r.n_hosts) + 0.05 * (s % 2)
+        elif s == 3:
+            r.dem[:, ::3] = 0.0                  # all-zero rows between the others
+        elif s == 4:
+            r.avail[:, ::5] = 1e151              # beyond 2^500 (squares still finite): the walk's
+                                                 # per-task stop
+        else:
+            r.dem[0] = np.round(r.dem[0] * 4) / 4   # fewer distinct rows: longer runs
+            r.dem[1] = np.round(r.dem[1] / 4096.0) * 4096.0
+        rounds.append(r)
+    _check(engine, engine_nowalk, rounds, "bulk runs")

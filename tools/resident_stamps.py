@@ -23,13 +23,14 @@ eng = PlacementEngine(0, lib_path=os.environ.get("STAMPS_LIB") or os.path.join(
     ROOT, "pivot-scheduling_amd", "diag", "libpivot_place_stamps.so"))
 f = eng.lib.pvt_debug_commit_stamps
 f.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
-buf = (ctypes.c_uint64 * 16)()
-assert f(eng.ctx, buf, 16) == 0          # allocates and zeroes the device counters
+NW = 32 + 4096
+buf = (ctypes.c_uint64 * NW)()
+assert f(eng.ctx, buf, NW) == 0          # allocates and zeroes the device counters
 rounds = [synthetic.make_round(MODES[mode], H, T, seed=1 + s) for s in range(B)]
 db = DeviceBatch(rounds, eng.device)
 eng.run_batch(db)
 torch.cuda.synchronize()
-assert f(eng.ctx, buf, 16) == 0
+assert f(eng.ctx, buf, NW) == 0
 names = ["anchor rows", "slot scan", "wave reduction", "exchange", "full path", "commit"]
 tot = sum(buf[k] for k in range(6))
 n = max(buf[6], 1)
@@ -46,3 +47,14 @@ if buf[8] or buf[9]:
     print("  walk: %.0f cycles per task in the task bodies, %.0f per task for wave 0's whole walk "
           "(the rest of the walk total: the prologue of all waves)"
           % (buf[13] / max(buf[8], 1), buf[14] / max(buf[8], 1)))
+    print("  walk: %d bulk runs placed %d tasks (%.1f per run)" % (buf[24], buf[25], buf[25] / max(buf[24], 1)))
+cyc = sorted(buf[32 + k] for k in range(min(B, 4096)))
+if cyc and cyc[-1]:
+    import statistics
+    q = lambda p: cyc[min(len(cyc) - 1, int(p * len(cyc)))]
+    print("  per round (whole workgroup, cycles): min %d  p25 %d  median %d  p75 %d  p90 %d  max %d"
+          % (cyc[0], q(0.25), q(0.5), q(0.75), q(0.9), cyc[-1]))
+    per = [(buf[32 + k], k) for k in range(min(B, 4096))]
+    per.sort(reverse=True)
+    print("  slowest rounds:", ", ".join("%d (%d)" % (k, c) for c, k in per[:8]))
+
