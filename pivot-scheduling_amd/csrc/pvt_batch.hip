@@ -608,6 +608,242 @@ __device__ int resident_walk(const pvt_round& R, const ResLds& Lo, char* smem, c
   return s_stop;
 }
 
+// ---- the first-fit resident walk (vbp first-fit, fit >=: vbp.py:13-29; cost_aware first-fit
+// without sort_hosts, strict fit: cost_aware.py:99-127 in host order). Each task takes the
+// LOWEST-INDEX host that fits, so one wave walks the hosts in index order: chunk p0 (host
+// p0 * 64 + lane) in registers, the first chunk that can still fit some remaining task (suffix
+// minima of the demands per 64 positions; a chunk that cannot fit the componentwise least
+// remaining demand never will), later chunks probed in LDS; a task no host fits stays unplaced.
+// Runs of equal demands are placed in one step on the register chunk (as resident_walk's dense
+// path). Walks every task (returns T); the 4-wave path then only writes the results.
+template <int NT, bool STRICT>
+__device__ int resident_walk_ff(const pvt_round& R, const ResLds& Lo, char* smem, const int32_t* ord,
+                                int32_t* pl, int walker, bool bulk, uint64_t* A_stamps) {
+  const int T = R.n_tasks, H = R.n_hosts;
+  const int tid = threadIdx.x, lane = lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  double* wa = reinterpret_cast<double*>(smem + Lo.wa);      // [4][RW_MAXH]
+  double* ws = reinterpret_cast<double*>(smem + Lo.ws);      // [RW_SB][4]
+  for (int h = tid; h < H; h += NT) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) wa[r * RW_MAXH + h] = G(R.avail)[(size_t)r * H + h];
+  }
+  const int nsb = (T + 63) >> 6;
+  for (int blk = wave; blk < nsb; blk += NT / WAVE) {
+    double m[4] = {DINF, DINF, DINF, DINF};
+    const int i = blk * 64 + lane;
+    if (i < T) {
+      const int t = ord[i];
+#pragma unroll
+      for (int r = 0; r < 4; r++) m[r] = G(R.dem)[(size_t)r * T + t];
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      for (int off = 32; off > 0; off >>= 1) m[r] = fmin(m[r], __shfl_xor(m[r], off));
+      if (lane == 0) ws[blk * 4 + r] = m[r];
+    }
+  }
+  __syncthreads();
+  if (tid < 4)
+    for (int blk = nsb - 2; blk >= 0; blk--) ws[blk * 4 + tid] = fmin(ws[blk * 4 + tid], ws[(blk + 1) * 4 + tid]);
+  __syncthreads();
+  if (wave == walker) {
+#ifdef PVT_STAMPS
+    uint64_t n_probe = 0, n_adv = 0, st_task = 0, n_bulk = 0, n_bulk_tasks = 0;
+    const uint64_t tw_start = rstamp();
+#endif
+    const int nch = (H + 63) >> 6;
+    int p0 = 0;
+    double ra0, ra1, ra2, ra3;
+    bool rv = false;
+    auto load_chunk = [&](int c) {
+      const int q = c * 64 + lane;
+      rv = q < H;
+      const int qq = rv ? q : 0;
+      ra0 = wa[qq]; ra1 = wa[RW_MAXH + qq]; ra2 = wa[2 * RW_MAXH + qq]; ra3 = wa[3 * RW_MAXH + qq];
+    };
+    auto store_chunk = [&](int c) {
+      const int q = c * 64 + lane;
+      if (rv) { wa[q] = ra0; wa[RW_MAXH + q] = ra1; wa[2 * RW_MAXH + q] = ra2; wa[3 * RW_MAXH + q] = ra3; }
+    };
+    load_chunk(0);
+    auto rec = [&](int b, double (&d)[4]) {
+      const int i = b * 64 + lane;
+      const int t = i < T ? ord[i] : 0;
+#pragma unroll
+      for (int r = 0; r < 4; r++) d[r] = G(R.dem)[(size_t)r * T + t];
+    };
+    double nd[4];
+    rec(0, nd);
+    int p = 0;
+    for (int b = 0; b < nsb; b++) {
+      double td[4] = {nd[0], nd[1], nd[2], nd[3]};
+      if (b + 1 < nsb) rec(b + 1, nd);
+      const double mn0 = ws[b * 4 + 0], mn1 = ws[b * 4 + 1], mn2 = ws[b * 4 + 2], mn3 = ws[b * 4 + 3];
+      const int kn = min(64, T - b * 64);
+      uint64_t E;                              // (every shuffle with the whole wave active)
+      {
+        bool same = lane > 0 && lane < kn;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          same &= __double_as_longlong(__shfl_up(td[r], 1)) == __double_as_longlong(td[r]);
+        E = __ballot(same);
+      }
+      for (int k = 0; k < kn; k++, p++) {
+#ifdef PVT_STAMPS
+        const uint64_t tk0 = rstamp();
+#endif
+        p = __builtin_amdgcn_readfirstlane(p);
+        p0 = __builtin_amdgcn_readfirstlane(p0);
+        const double d0 = readlane_d(td[0], k), d1 = readlane_d(td[1], k);
+        const double d2 = readlane_d(td[2], k), d3 = readlane_d(td[3], k);
+        // the register chunk: past chunks no remaining task can use
+        uint64_t F = __ballot(rv && fits<STRICT>(ra0, ra1, ra2, ra3, d0, d1, d2, d3));
+        while (F == 0 && p0 + 1 < nch &&
+               !__ballot(rv && fits<STRICT>(ra0, ra1, ra2, ra3, mn0, mn1, mn2, mn3))) {
+          store_chunk(p0);
+#ifdef PVT_STAMPS
+          n_adv++;
+#endif
+          ++p0;
+          load_chunk(p0);
+          F = __ballot(rv && fits<STRICT>(ra0, ra1, ra2, ra3, d0, d1, d2, d3));
+        }
+        // a run of R >= 2 tasks with this demand: placed in one step on the first chunk that
+        // fits its first task -- the register chunk, else the first LDS chunk that does (taken
+        // into registers for the step and written back). Every fitting lane counts its copies
+        // (d >= 0 and finite capacities: a - d rounded keeps the sign of a - d, so x_{j-1} fits
+        // iff x_j >= 0, or > 0 strict; a lane that fails a copy fails every later one), the lanes
+        // take the run in order and replay their subtractions.
+        if (bulk && k + 1 < kn && ((E >> (k + 1)) & 1ull) && d0 >= 0.0 && d1 >= 0.0 &&
+            d2 >= 0.0 && d3 >= 0.0 && d0 < DINF && d1 < DINF && d2 < DINF && d3 < DINF) {
+          int c = p0;
+          uint64_t m0 = F;
+          double y0 = ra0, y1 = ra1, y2 = ra2, y3 = ra3;
+          bool yv = rv;
+          if (m0 == 0) {
+            for (c = p0 + 1; c < nch; c++) {
+              const int q = c * 64 + lane;
+              yv = q < H;
+              const int qq = yv ? q : 0;
+              y0 = wa[qq]; y1 = wa[RW_MAXH + qq]; y2 = wa[2 * RW_MAXH + qq]; y3 = wa[3 * RW_MAXH + qq];
+              m0 = __ballot(yv && fits<STRICT>(y0, y1, y2, y3, d0, d1, d2, d3));
+              if (m0) break;
+            }
+          }
+          c = __builtin_amdgcn_readfirstlane(c);
+          if (m0 != 0 && !(__ballot(!(__builtin_fabs(y0) < DINF && __builtin_fabs(y1) < DINF &&
+                                       __builtin_fabs(y2) < DINF && __builtin_fabs(y3) < DINF)) & m0)) {
+            const int R = min(kn - k, 1 + (int)__builtin_ctzll(~(E >> (k + 1))));
+            const bool on = (m0 >> lane) & 1ull;
+            double x0 = on ? y0 : -DINF, x1 = on ? y1 : -DINF, x2 = on ? y2 : -DINF, x3 = on ? y3 : -DINF;
+            int cnt = 0, t = 0, u = __builtin_ctzll(m0), fb = 0;
+            for (;;) {
+              t = __builtin_amdgcn_readfirstlane(t);
+              u = __builtin_amdgcn_readfirstlane(u);
+              fb = __builtin_amdgcn_readfirstlane(fb);
+              bool f = false;
+#pragma unroll
+              for (int j = 1; j <= 8; j++) {
+                x0 -= d0; x1 -= d1; x2 -= d2; x3 -= d3;
+                const double mx = fmin(fmin(x0, x1), fmin(x2, x3));
+                f = STRICT ? (mx > 0.0) : (mx >= 0.0);
+                cnt = f ? t + j : cnt;
+              }
+              t += 8;
+              const uint64_t an = __ballot(f);
+              if (__builtin_amdgcn_readfirstlane((int)(an == 0))) break;
+              const int un = __builtin_ctzll(an);
+              if (un != u) {
+                u = un;
+                fb = __builtin_amdgcn_readlane(wave_incl_scan_dpp(cnt), u - 1);
+              }
+              if (__builtin_amdgcn_readfirstlane((int)(fb + t >= R))) break;
+            }
+            const int incl = wave_incl_scan_dpp(cnt);
+            const int pre = incl - cnt;
+            const int asg = max(0, min(cnt, R - pre));
+            const int covered = min(R, __builtin_amdgcn_readlane(incl, 63));
+            int who = 0;
+            for (uint64_t tk = __ballot(asg > 0); tk; tk &= tk - 1) {
+              const int L = __builtin_ctzll(tk);
+              const int s0 = __builtin_amdgcn_readlane(pre, L), s1 = s0 + __builtin_amdgcn_readlane(asg, L);
+              if (lane >= s0 && lane < s1) who = c * 64 + L;
+            }
+            if (lane < covered) pl[p + lane] = who;
+            const int amax = wave_max_i32(asg);
+            for (int m = 0; m < amax; m++) {
+              const double o = m < asg ? -1.0 : -0.0;
+              y0 = __builtin_fma(o, d0, y0);
+              y1 = __builtin_fma(o, d1, y1);
+              y2 = __builtin_fma(o, d2, y2);
+              y3 = __builtin_fma(o, d3, y3);
+            }
+            if (c == p0) {
+              ra0 = y0; ra1 = y1; ra2 = y2; ra3 = y3;
+            } else if (asg > 0) {              // (an LDS chunk: its taking lanes write back)
+              const int q = c * 64 + lane;
+              wa[q] = y0; wa[RW_MAXH + q] = y1; wa[2 * RW_MAXH + q] = y2; wa[3 * RW_MAXH + q] = y3;
+            }
+#ifdef PVT_STAMPS
+            n_bulk++;
+            n_bulk_tasks += covered;
+            st_task += rstamp() - tk0;
+#endif
+            k += covered - 1;
+            p += covered - 1;
+            continue;
+          }
+        }
+        int win = -1;
+        if (F) {
+          const int w = __builtin_ctzll(F);
+          if (lane == w) { ra0 -= d0; ra1 -= d1; ra2 -= d2; ra3 -= d3; }   // resc[h] -= d
+          win = p0 * 64 + w;
+        } else {
+          for (int c = p0 + 1; c < nch; c++) {
+#ifdef PVT_STAMPS
+            n_probe++;
+#endif
+            const int q = c * 64 + lane;
+            const bool v = q < H;
+            const int qq = v ? q : 0;
+            const double y0 = wa[qq], y1 = wa[RW_MAXH + qq], y2 = wa[2 * RW_MAXH + qq], y3 = wa[3 * RW_MAXH + qq];
+            const uint64_t F2 = __ballot(v && fits<STRICT>(y0, y1, y2, y3, d0, d1, d2, d3));
+            if (F2) {
+              const int w = __builtin_ctzll(F2);
+              if (lane == w) {
+                wa[q] = y0 - d0; wa[RW_MAXH + q] = y1 - d1; wa[2 * RW_MAXH + q] = y2 - d2;
+                wa[3 * RW_MAXH + q] = y3 - d3;
+              }
+              win = c * 64 + w;
+              break;
+            }
+          }
+        }
+        win = __builtin_amdgcn_readfirstlane(win);
+        if (win >= 0 && lane == 0) pl[p] = win;
+#ifdef PVT_STAMPS
+        st_task += rstamp() - tk0;
+#endif
+      }
+    }
+    store_chunk(p0);
+#ifdef PVT_STAMPS
+    if (blockIdx.x == 0 && lane == 0 && A_stamps) {
+      A_stamps[10] += n_probe;
+      A_stamps[11] += n_adv;
+      A_stamps[13] += st_task;
+      A_stamps[14] += rstamp() - tw_start;
+      A_stamps[24] += n_bulk;
+      A_stamps[25] += n_bulk_tasks;
+    }
+#endif
+  }
+  __syncthreads();
+  return T;
+}
+
 // One round on this workgroup (R: its descriptor, in SGPRs). The MT19937 state of an
 // opportunistic round is read and written through R.mt_state (a device pointer in every
 // resident path: pvt_place_batch's upload, pvt_place_batch_mt's rows, pvt_place_host's stage).
@@ -679,7 +915,7 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   // ca_bf 0.743 vs 0.779 ms at config 4); this path takes over where it stops, on the walked
   // capacities.
   int p_start = 0;
-  if (MODE == CA_BF && A.walk && H <= RW_MAXH && T > 0 && !R.rt_bw) {
+  if (MODE == CA_BF && (A.walk & 3) && H <= RW_MAXH && T > 0 && !R.rt_bw) {
 #ifdef PVT_STAMPS
     const uint64_t tw0 = rstamp();
 #endif
@@ -691,6 +927,30 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
                                 (A.walk & 4) == 0, A.stamps);
 #ifdef PVT_STAMPS
     if (blockIdx.x == 0 && tid == 0 && A.stamps) {   // walked tasks, walk cycles (block 0)
+      A.stamps[8] += (uint64_t)p_start;
+      A.stamps[9] += rstamp() - tw0;
+    }
+#endif
+    const double* wa = reinterpret_cast<const double*>(smem + Lo.wa);
+#pragma unroll
+    for (int j = 0; j < HPL; j++) {
+      const int h = h0 + j;
+      if (h < H) {
+        a0[j] = wa[h]; a1[j] = wa[RW_MAXH + h]; a2[j] = wa[2 * RW_MAXH + h]; a3[j] = wa[3 * RW_MAXH + h];
+      }
+    }
+  }
+  // first fit by index (vbp first-fit; cost_aware first-fit without sort_hosts): the whole round
+  // walked by one wave (resident_walk_ff), this path then only writes the results
+  if ((MODE == VBP_FF || (MODE == CA_FF && !keyed)) && (A.walk & 8) && H <= RW_MAXH && T > 0) {
+#ifdef PVT_STAMPS
+    const uint64_t tw0 = rstamp();
+#endif
+    const int walker = (A.walk & 3) == 2 ? (int)(blockIdx.x % (unsigned)WAVES) : 0;
+    p_start = resident_walk_ff<NT, MODE == CA_FF>(R, Lo, smem, ord, pl, walker, (A.walk & 4) == 0,
+                                                  A.stamps);
+#ifdef PVT_STAMPS
+    if (blockIdx.x == 0 && tid == 0 && A.stamps) {
       A.stamps[8] += (uint64_t)p_start;
       A.stamps[9] += rstamp() - tw0;
     }

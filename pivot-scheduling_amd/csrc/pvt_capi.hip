@@ -199,7 +199,8 @@ struct pvt_ctx {
   int t_chain_tab = 1;            // PVT_CHAIN_TAB: 0 = chain tables uploaded before the walk
   int t_merge_bitonic = 0;        // PVT_MERGE_SMALL=0: the bitonic merge always
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
-  int rwalk = 1;                  // PVT_RWALK=0: resident rounds without the one-wave walk (A/B)
+  int rwalk = 9;                  // PVT_RWALK: resident one-wave walks, bits 1 cost_aware best-fit, 8
+                                  //   first fit by index, 4 without bulk runs, 2 rotated walker; 0 none (A/B)
   int fused = 1;                  // PVT_FUSED=0: host batches staged in six launches (A/B)
   int ahead = 0;                  // PVT_AHEAD=1: vbp best-fit walks enqueued ahead (place_ahead;
                                   // measured slower, kept for A/B)

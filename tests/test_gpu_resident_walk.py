@@ -176,8 +176,12 @@ def test_zero_cost_window_certificates(engine, engine_nowalk):
     _check(engine, engine_nowalk, rounds, "zero-cost window certificates")
 
 
-def test_bulk_runs_in_the_walk(engine, engine_nowalk):
-    """Runs of equal demands placed in one step on the walk's register chunk (every fitting lane
+@pytest.mark.parametrize("mode,sort_hosts", [(_abi.PVT_CA_BF, True), (_abi.PVT_VBP_FF, True),
+                                             (_abi.PVT_CA_FF, False)])
+def test_bulk_runs_in_the_walk(engine, engine_nowalk, mode, sort_hosts):
+    """Runs of equal demands placed in one step on the walk's register chunk -- cost_aware best-fit
+    (zero-cost window) and first fit by index (vbp first-fit, unsorted cost_aware first-fit,
+    strict) -- (every fitting lane
     counts its copies, the lanes take the run in order and replay their subtractions): runs of up
     to a whole batch over hosts that take an exact number of copies, demands that are not exactly
     representable (0.1 cpus: the copy counts come from the sequential roundings), all-zero demand
@@ -185,7 +189,7 @@ def test_bulk_runs_in_the_walk(engine, engine_nowalk):
     ~1e154, where a zero-cost score would be 0 * inf)."""
     rounds = []
     for s in range(6):
-        r = synthetic.make_round(_abi.PVT_CA_BF, 900, 1500, seed=220 + s)
+        r = synthetic.make_round(mode, 900, 1500, seed=220 + s, sort_hosts=sort_hosts)
         rs = np.random.RandomState(300 + s)
         if s in (0, 1):
             rows = np.array([[0.5, 2048.0], [1.0, 4096.0], [0.25, 1024.0]])
@@ -206,4 +210,4 @@ def test_bulk_runs_in_the_walk(engine, engine_nowalk):
             r.dem[0] = np.round(r.dem[0] * 4) / 4   # fewer distinct rows: longer runs
             r.dem[1] = np.round(r.dem[1] / 4096.0) * 4096.0
         rounds.append(r)
-    _check(engine, engine_nowalk, rounds, "bulk runs")
+    _check(engine, engine_nowalk, rounds, "bulk runs mode %d" % mode)
