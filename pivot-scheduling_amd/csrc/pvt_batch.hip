@@ -74,11 +74,19 @@ __device__ __forceinline__ uint64_t rstamp() {
 #define RCOUNT(k) do {} while (0)
 #endif
 
+// A run list entry: a host's full key (score bits, tiebreak:host) and its capacities.
+struct RunEntry {
+  uint64_t k1, k2;
+  double c[4];
+};
+constexpr int RES_LK = 16;                // run list length (hosts per list)
+constexpr int RES_LIST_MIN = 24;          // run lists only for at least this many remaining tasks
+
 // Dynamic LDS layout (bytes); the host sizes the launch with the same struct.
 constexpr int RW_SB = RES_MAX_TASKS / 64; // its suffix minima of the demands, per 64 positions
 
 struct ResLds {
-  int zt, ord, pl, u, cd, ci, mt, slot, wa, wz, ws, wx, wd, total;
+  int zt, ord, pl, u, cd, ci, mt, slot, lst, wa, wz, ws, wx, wd, total;
   __host__ __device__ ResLds(int Zb, int Tpad, bool walk = false) {
     zt = 0;                                            // csum[Zb*Zb], bsum[Zb*Zb] f64
     ord = (16 * Zb * Zb + 15) & ~15;                   // processing order i32[Tpad]
@@ -90,7 +98,9 @@ struct ResLds {
     slot = mt + 4 * RES_MAXW * RES_MT_STRIDE;          //       posts u64[2][WAVES][2], then
     // fast posts i32[2][WAVES], then vbp best-fit s2 posts {u64, i32, i32}[2][WAVES]
     // (+32: the sticky winner's capacities, f64[4])
-    const int walk_end = slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW + 32;
+    // then the run lists: RunEntry[RES_MAXW + 1][RES_LK] (per wave, merged)
+    lst = (slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW + 32 + 15) & ~15;
+    const int walk_end = lst + (int)sizeof(RunEntry) * (RES_MAXW + 1) * RES_LK;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     // resident walk (after the sort, before the staging above): the round's hosts in LDS,
     // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], suffix minima and maxima of the demands
@@ -1005,6 +1015,106 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   double* skc = reinterpret_cast<double*>(smem + Lo.slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW);
   int sh = -1;
   double sc0 = 0.0, sc1 = 0.0, sc2 = 0.0, sc3 = 0.0;
+  // bulk sticky runs (A.walk & 16: off, A/B); run flags u64[RES_CHUNK / 64] in the staging pad
+  const bool bulk_sticky = (A.walk & 16) == 0;
+  uint64_t* ew = reinterpret_cast<uint64_t*>(c_anc + 2 * RES_CHUNK);
+  // run lists (A.walk & 32: off, A/B; bits 8-15: the minimum remaining run, A/B), for vbp
+  // best-fit only: the other policies' fast winners (one ballot, no score reduction) measured
+  // cheaper than a list (config 4 cost_aware first-fit 2.1 vs 0.53 ms with lists for every run)
+  const bool run_lists = MODE == VBP_BF && bulk_sticky && (A.walk & 32) == 0;
+  const int list_min = (A.walk >> 8) & 255 ? (A.walk >> 8) & 255 : RES_LIST_MIN;
+  RunEntry* rlw = reinterpret_cast<RunEntry*>(smem + Lo.lst) + wave * RES_LK;   // this wave's list
+  RunEntry* rlm = reinterpret_cast<RunEntry*>(smem + Lo.lst) + RES_MAXW * RES_LK;   // merged
+  // Places the `rem` tasks at positions pos.. (demand d, a run) down run lists; returns rem.
+  auto run_list_steps = [&](int pos, int rem, double d0, double d1, double d2, double d3) -> int {
+    int placed = 0;
+    while (placed < rem) {
+      // the full path's keys: k1 score bits (first fit: 0; keyed: the frozen key), k2
+      // tiebreak:host; a host that does not fit is NONE
+      uint64_t s1[HPL];
+#pragma unroll
+      for (int j = 0; j < HPL; j++) {
+        const bool f = fits<STRICT>(a0[j], a1[j], a2[j], a3[j], d0, d1, d2, d3);
+        uint64_t k1 = 0;
+        if (MODE == CA_BF || MODE == VBP_BF) {
+          const double sq = __builtin_sqrt(norm2_seq(a0[j] - d0, a1[j] - d1, a2[j] - d2, a3[j] - d3));
+          k1 = dbits(MODE == CA_BF ? (cc[j] * sq) / bb[j] : sq);
+        } else if (MODE == CA_FF) {
+          k1 = dbits(key[j]);
+        }
+        s1[j] = f ? k1 : NONE;
+      }
+      // this wave's RES_LK smallest (k1, k2), in order (host ids make the keys distinct)
+      for (int e = 0; e < RES_LK; e++) {
+        uint64_t b1 = NONE, b2 = NONE;
+        int bj = 0;
+#pragma unroll
+        for (int j = 0; j < HPL; j++) {
+          const uint64_t k2 = ((uint64_t)tb[j] << 32) | (uint32_t)(h0 + j);
+          if (s1[j] < b1 || (s1[j] == b1 && s1[j] != NONE && k2 < b2)) { b1 = s1[j]; b2 = k2; bj = j; }
+        }
+        const uint64_t m1 = wave_min_u64(b1);
+        if (m1 == NONE) {
+          if (lane >= e && lane < RES_LK) { rlw[lane].k1 = NONE; rlw[lane].k2 = NONE; }
+          break;
+        }
+        const uint64_t tied = __ballot(b1 == m1);
+        const uint64_t m2 = __popcll(tied) > 1 ? wave_min_u64(b1 == m1 ? b2 : NONE)
+                                               : readlane_u64(b2, __builtin_ctzll(tied));
+        if (b1 == m1 && b2 == m2) {
+#pragma unroll
+          for (int j = 0; j < HPL; j++)
+            if (j == bj) {
+              rlw[e].k1 = m1; rlw[e].k2 = m2;
+              rlw[e].c[0] = a0[j]; rlw[e].c[1] = a1[j]; rlw[e].c[2] = a2[j]; rlw[e].c[3] = a3[j];
+              s1[j] = NONE;
+            }
+        }
+      }
+      __syncthreads();
+      // merge: entry (w, e) goes to rank e + the entries of the other lists below it (NONE
+      // entries tie; ordered by wave)
+      for (int x = tid; x < WAVES * RES_LK; x += NT) {
+        const int w = x / RES_LK, e = x % RES_LK;
+        const RunEntry* L = reinterpret_cast<const RunEntry*>(smem + Lo.lst);
+        const uint64_t x1 = L[w * RES_LK + e].k1, x2 = L[w * RES_LK + e].k2;
+        int rank = e;
+#pragma unroll
+        for (int v = 0; v < WAVES; v++) {
+          uint64_t y1[RES_LK], y2[RES_LK];
+#pragma unroll
+          for (int i = 0; i < RES_LK; i++) { y1[i] = L[v * RES_LK + i].k1; y2[i] = L[v * RES_LK + i].k2; }
+#pragma unroll
+          for (int i = 0; i < RES_LK; i++)
+            rank += (v != w && (y1[i] < x1 || (y1[i] == x1 && (y2[i] < x2 || (y2[i] == x2 && v < w))))) ? 1 : 0;
+        }
+        if (rank < RES_LK) rlm[rank] = L[w * RES_LK + e];
+      }
+      __syncthreads();
+      // the run down the merged list (uniform in every wave; owners take their hosts' results)
+      int i = 0;
+      for (; i < RES_LK && placed < rem; i++) {
+        if (rlm[i].k1 == NONE) { placed = rem; break; }   // no host left that fits
+        double x0 = rlm[i].c[0], x1 = rlm[i].c[1], x2 = rlm[i].c[2], x3 = rlm[i].c[3];
+        const int h = (int)(uint32_t)rlm[i].k2;
+        int c = 0;
+        while (placed + c < rem && fits<STRICT>(x0, x1, x2, x3, d0, d1, d2, d3)) {
+          x0 -= d0; x1 -= d1; x2 -= d2; x3 -= d3;
+          c++;
+        }
+        c = __builtin_amdgcn_readfirstlane(c);
+        for (int t = tid; t < c; t += NT) pl[pos + placed + t] = h;
+        placed += c;
+        if (h / HPL == tid) {
+#pragma unroll
+          for (int j = 0; j < HPL; j++)
+            if (j == (h & (HPL - 1))) { a0[j] = x0; a1[j] = x1; a2[j] = x2; a3[j] = x3; }
+        }
+      }
+      placed = __builtin_amdgcn_readfirstlane(placed);
+    }
+    return rem;
+  };
   for (int p0 = p_start; p0 < T; p0 += RES_CHUNK) {
     const int n = min(RES_CHUNK, T - p0);
     __syncthreads();                      // the previous chunk (and the sort keys) are consumed
@@ -1041,6 +1151,23 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
       }
     }
     __syncthreads();
+    if (MODE != OPP && bulk_sticky) {
+      // run flags: bit i of ew = staged row i repeats row i - 1 (demand bits; anchor; group where
+      // keys or realtime bandwidths are per group) -- the sticky winner's run condition
+      for (int i0 = 0; i0 < RES_CHUNK; i0 += NT) {
+        const int i = i0 + tid;
+        bool e = false;
+        if (i >= 1 && i < n) {
+          e = dbits(cd[i * 4 + 0]) == dbits(cd[i * 4 - 4]) && dbits(cd[i * 4 + 1]) == dbits(cd[i * 4 - 3]) &&
+              dbits(cd[i * 4 + 2]) == dbits(cd[i * 4 - 2]) && dbits(cd[i * 4 + 3]) == dbits(cd[i * 4 - 1]) &&
+              (!CA || c_anc[i] == c_anc[i - 1]) &&
+              (!((MODE == CA_FF && keyed) || rt) || c_grp[i] == c_grp[i - 1]);
+        }
+        const uint64_t b = __ballot(e);
+        if (lane == 0 && i < RES_CHUNK) ew[i >> 6] = b;
+      }
+      __syncthreads();
+    }
     // the next task's staged row is read while this task is scored (LDS latency off the chain)
     double n0 = cd[0], n1 = cd[1], n2 = cd[2], n3 = cd[3];
     int n_anc = c_anc[0], n_grp = c_grp[0];
@@ -1364,6 +1491,50 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
         __syncthreads();
         sc0 = skc[0]; sc1 = skc[1]; sc2 = skc[2]; sc3 = skc[3];
         sh = hw;
+        if (bulk_sticky) {
+          // the whole run in one step: its length from the run flags, then the copies the winner
+          // still takes by the sticky rule (fits, subtract; in order, uniform in every wave); the
+          // task after them is a new row or does not fit the winner, so it takes the full path
+          int rl = 0;
+          for (int i = q + 1; i < n;) {
+            const uint64_t w = ~(ew[i >> 6] >> (i & 63));
+            const int z = w ? (int)__builtin_ctzll(w) : 64;
+            rl += z;
+            if (z < 64 - (i & 63)) break;
+            i += z;
+          }
+          rl = __builtin_amdgcn_readfirstlane(rl);
+          int k = 0;
+          while (k < rl && fits<STRICT>(sc0, sc1, sc2, sc3, d0, d1, d2, d3)) {
+            sc0 -= d0; sc1 -= d1; sc2 -= d2; sc3 -= d3;
+            k++;
+          }
+          k = __builtin_amdgcn_readfirstlane(k);
+          if (k > 0) {
+            for (int i = tid; i < k; i += NT) pl[p + 1 + i] = hw;
+            if (hw / HPL == tid) {
+#pragma unroll
+              for (int j = 0; j < HPL; j++)
+                if (j == jw) { a0[j] = sc0; a1[j] = sc1; a2[j] = sc2; a3[j] = sc3; }
+            }
+          }
+          if (run_lists && rl - k >= list_min) {
+            // the winner ran out mid-run: the rest of the run goes down run lists -- the
+            // RES_LK best fitting hosts for this demand by the full path's key, each taking copies
+            // by the sticky rule until it no longer fits (only list hosts change during the run,
+            // so the next list host is the next winner; a list ending in a non-fitting entry
+            // held every fitting host, so the run's remaining tasks stay waiting)
+            k += run_list_steps(p + 1 + k, rl - k, d0, d1, d2, d3);
+          }
+          if (k > 0) {
+            q += k;
+            if (q + 1 < n) {
+              n0 = cd[(q + 1) * 4 + 0]; n1 = cd[(q + 1) * 4 + 1]; n2 = cd[(q + 1) * 4 + 2]; n3 = cd[(q + 1) * 4 + 3];
+              n_anc = c_anc[q + 1]; n_grp = c_grp[q + 1];
+            }
+          }
+          sh = -1;
+        }
       }
       RSTAMP(5);
     }
