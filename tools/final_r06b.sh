@@ -3,7 +3,7 @@
 # bench.py with this library's sha256), then the full bench and the default line's kernel trace.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 R=$PWD
-tools/gpu_step.sh fin_pmc 1000 tools/pmc_all.sh r06e || exit $?
+tools/gpu_step.sh fin_pmc 1000 tools/pmc_all.sh "${1:-r06e}" || exit $?
 cp gpurun_out/pmc_index.json profiles/pmc_index.json
 tools/gpu_step.sh fin_bench 500 python bench.py || exit $?
 mkdir -p gpurun_out/fin_prof
