@@ -79,8 +79,11 @@ struct RunEntry {
   uint64_t k1, k2;
   double c[4];
 };
-constexpr int RES_LK = 16;                // run list length (hosts per list)
-constexpr int RES_LIST_MIN = 24;          // run lists only for at least this many remaining tasks
+#ifndef PVT_RES_LK
+#define PVT_RES_LK 8
+#endif
+constexpr int RES_LK = PVT_RES_LK;        // run list length (hosts per wave; -DPVT_RES_LK: A/B builds)
+constexpr int RES_LIST_MIN = 8;           // run lists only for at least this many remaining tasks
 
 // Dynamic LDS layout (bytes); the host sizes the launch with the same struct.
 constexpr int RW_SB = RES_MAX_TASKS / 64; // its suffix minima of the demands, per 64 positions
@@ -98,9 +101,9 @@ struct ResLds {
     slot = mt + 4 * RES_MAXW * RES_MT_STRIDE;          //       posts u64[2][WAVES][2], then
     // fast posts i32[2][WAVES], then vbp best-fit s2 posts {u64, i32, i32}[2][WAVES]
     // (+32: the sticky winner's capacities, f64[4])
-    // then the run lists: RunEntry[RES_MAXW + 1][RES_LK] (per wave, merged)
+    // then the run lists: RunEntry[RES_MAXW][RES_LK] (per wave)
     lst = (slot + 32 * RES_MAXW + 8 * RES_MAXW + 32 * RES_MAXW + 32 + 15) & ~15;
-    const int walk_end = lst + (int)sizeof(RunEntry) * (RES_MAXW + 1) * RES_LK;
+    const int walk_end = lst + (int)sizeof(RunEntry) * RES_MAXW * RES_LK;
     const int sort_end = u + 16 * Tpad;                // sort: u64 ka[Tpad], kb[Tpad]
     // resident walk (after the sort, before the staging above): the round's hosts in LDS,
     // capacities f64[4][RW_MAXH], zones i32[RW_MAXH], suffix minima and maxima of the demands
@@ -1021,10 +1024,10 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
   // run lists (A.walk & 32: off, A/B; bits 8-15: the minimum remaining run, A/B), for vbp
   // best-fit only: the other policies' fast winners (one ballot, no score reduction) measured
   // cheaper than a list (config 4 cost_aware first-fit 2.1 vs 0.53 ms with lists for every run)
-  const bool run_lists = MODE == VBP_BF && bulk_sticky && (A.walk & 32) == 0;
+  const bool run_lists = (MODE == VBP_BF || (MODE != OPP && (A.walk & 64))) && bulk_sticky &&
+                         (A.walk & 32) == 0;
   const int list_min = (A.walk >> 8) & 255 ? (A.walk >> 8) & 255 : RES_LIST_MIN;
   RunEntry* rlw = reinterpret_cast<RunEntry*>(smem + Lo.lst) + wave * RES_LK;   // this wave's list
-  RunEntry* rlm = reinterpret_cast<RunEntry*>(smem + Lo.lst) + RES_MAXW * RES_LK;   // merged
   // Places the `rem` tasks at positions pos.. (demand d, a run) down run lists; returns rem.
   auto run_list_steps = [&](int pos, int rem, double d0, double d1, double d2, double d3) -> int {
     int placed = 0;
@@ -1072,31 +1075,32 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
         }
       }
       __syncthreads();
-      // merge: entry (w, e) goes to rank e + the entries of the other lists below it (NONE
-      // entries tie; ordered by wave)
-      for (int x = tid; x < WAVES * RES_LK; x += NT) {
-        const int w = x / RES_LK, e = x % RES_LK;
-        const RunEntry* L = reinterpret_cast<const RunEntry*>(smem + Lo.lst);
-        const uint64_t x1 = L[w * RES_LK + e].k1, x2 = L[w * RES_LK + e].k2;
-        int rank = e;
+      // the run down the lists, merged on the fly (uniform in every wave; owners take their
+      // hosts' results): the next host is the smallest head. A list used up (RES_LK hosts
+      // taken) hides its wave's next host, so the lists are rebuilt; every head a non-fitting
+      // entry: no host fits, the run's remaining tasks stay waiting.
+      const RunEntry* L = reinterpret_cast<const RunEntry*>(smem + Lo.lst);
+      int hp[WAVES];
+      uint64_t q1[WAVES], q2[WAVES];
 #pragma unroll
-        for (int v = 0; v < WAVES; v++) {
-          uint64_t y1[RES_LK], y2[RES_LK];
+      for (int w = 0; w < WAVES; w++) { hp[w] = 0; q1[w] = L[w * RES_LK].k1; q2[w] = L[w * RES_LK].k2; }
+      bool more = false;
+      while (placed < rem) {
+        int bw = -1;
+        uint64_t b1 = NONE, b2 = NONE;
+        bool used_up = false;
 #pragma unroll
-          for (int i = 0; i < RES_LK; i++) { y1[i] = L[v * RES_LK + i].k1; y2[i] = L[v * RES_LK + i].k2; }
-#pragma unroll
-          for (int i = 0; i < RES_LK; i++)
-            rank += (v != w && (y1[i] < x1 || (y1[i] == x1 && (y2[i] < x2 || (y2[i] == x2 && v < w))))) ? 1 : 0;
+        for (int w = 0; w < WAVES; w++) {
+          used_up |= hp[w] >= RES_LK;
+          if (hp[w] < RES_LK && (q1[w] < b1 || (q1[w] == b1 && q2[w] < b2))) { b1 = q1[w]; b2 = q2[w]; bw = w; }
         }
-        if (rank < RES_LK) rlm[rank] = L[w * RES_LK + e];
-      }
-      __syncthreads();
-      // the run down the merged list (uniform in every wave; owners take their hosts' results)
-      int i = 0;
-      for (; i < RES_LK && placed < rem; i++) {
-        if (rlm[i].k1 == NONE) { placed = rem; break; }   // no host left that fits
-        double x0 = rlm[i].c[0], x1 = rlm[i].c[1], x2 = rlm[i].c[2], x3 = rlm[i].c[3];
-        const int h = (int)(uint32_t)rlm[i].k2;
+        if (used_up) { more = true; break; }
+        if (bw < 0) { placed = rem; break; }
+        int ix = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) if (w == bw) ix = w * RES_LK + hp[w];
+        double x0 = L[ix].c[0], x1 = L[ix].c[1], x2 = L[ix].c[2], x3 = L[ix].c[3];
+        const int h = (int)(uint32_t)b2;
         int c = 0;
         while (placed + c < rem && fits<STRICT>(x0, x1, x2, x3, d0, d1, d2, d3)) {
           x0 -= d0; x1 -= d1; x2 -= d2; x3 -= d3;
@@ -1110,8 +1114,14 @@ __device__ __forceinline__ void resident_round(const ResidentArgs& A, const pvt_
           for (int j = 0; j < HPL; j++)
             if (j == (h & (HPL - 1))) { a0[j] = x0; a1[j] = x1; a2[j] = x2; a3[j] = x3; }
         }
+        const int nx = ix + 1;
+        const uint64_t n1 = L[nx < WAVES * RES_LK ? nx : 0].k1, n2 = L[nx < WAVES * RES_LK ? nx : 0].k2;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++)
+          if (w == bw) { hp[w]++; q1[w] = n1; q2[w] = n2; }
       }
       placed = __builtin_amdgcn_readfirstlane(placed);
+      if (more) __syncthreads();   // (every wave is done with the lists before they are rebuilt)
     }
     return rem;
   };

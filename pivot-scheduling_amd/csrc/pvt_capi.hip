@@ -201,8 +201,8 @@ struct pvt_ctx {
   int res_waves = 4;              // PVT_RES_WAVES: waves per resident round (2, 4 or 8)
   int rwalk = 9;                  // PVT_RWALK: resident one-wave walks, bits 1 cost_aware best-fit, 8
                                   //   first fit by index, 4 without bulk runs, 2 rotated walker; 0 none;
-                                  //   4-wave path: 16 no bulk sticky runs, 32 no run lists, bits 8-15
-                                  //   the shortest remaining run given a list (A/B)
+                                  //   4-wave path: 16 no bulk sticky runs, 32 no run lists, 64 run lists
+                                  //   for every policy, bits 8-15 the shortest remaining run given a list (A/B)
   int fused = 1;                  // PVT_FUSED=0: host batches staged in six launches (A/B)
   int ahead = 0;                  // PVT_AHEAD=1: vbp best-fit walks enqueued ahead (place_ahead;
                                   // measured slower, kept for A/B)

@@ -1,12 +1,12 @@
 """Bulk sticky runs and run lists in the resident kernel's 4-wave path (pvt_batch.hip
 resident_round): when a run of equal demand rows starts, the winner's copies are counted in one
 step (fits, subtract, in order) instead of one loop iteration per task, and (vbp best-fit) when
-the winner runs out with at least RES_LIST_MIN tasks of the run left, the rest goes down lists of
-the best fitting hosts by the full path's key. Every round must equal the CPU restatement, and
+the winner runs out with at least RES_LIST_MIN tasks of the run left, the rest goes down per-wave
+lists of the best fitting hosts by the full path's key, merged on the fly. Every round must equal the CPU restatement, and
 the same batch with both off (PVT_RWALK=16, A/B) too: runs longer than the 256-row staging chunk,
 demands that are not exactly representable (the copy count comes from the sequential roundings),
-winners that run out mid-run, lists that run dry (a list ending in a host that does not fit: the
-run's other tasks stay waiting), runs split by the anchor or the group, all-zero rows, and
+winners that run out mid-run, lists used up (rebuilt) and lists that run dry (every head a host
+that does not fit: the run's other tasks stay waiting), runs split by the anchor or the group, all-zero rows, and
 realtime bandwidths (runs split by group)."""
 import os
 
